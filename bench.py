@@ -1,0 +1,151 @@
+#!/usr/bin/env python3
+"""Headline benchmark (BASELINE.json): ImageNet ResNet-50 training images/sec, amp O2 (bf16
+model weights, fp32 batchnorm + fp32 master weights) + FusedAdam, whole-node aggregate.
+
+Metric exactly as the reference's examples/imagenet/main_amp.py:386-398:
+``world_size * batch_size / batch_time``, here measured over K timed steps after W warm-up
+steps, bracketed by barrier + device synchronize, max step time over ranks.
+
+Data: synthetic 3x224x224 images + random labels resident on the GPU (no network / dataset);
+weights: random init of the torchvision-equivalent ResNet-50 architecture.
+
+Single GPU:   python bench.py [--steps K --warmup W]
+N GPUs:       python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+                  --master-port P bench.py --gpus N --steps K --warmup W
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--batch-size", type=int, default=256, help="per-GPU batch (weak scaling)")
+    ap.add_argument("--arch", default="resnet50")
+    ap.add_argument("--opt-level", default="O2")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
+    ap.add_argument("--no-channels-last", action="store_true")
+    ap.add_argument("--materialize-master-grads", action="store_true",
+                    help="reference-style unscale into fp32 master grads (slower path)")
+    ap.add_argument("--sync-bn", action="store_true")
+    ap.add_argument("--lr", type=float, default=1e-3)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend="nccl", init_method="env://")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    torch.backends.cudnn.benchmark = True
+
+    import apex
+    from apex import amp
+    from apex.models import resnet as resnet_mod
+    from apex.optimizers import FusedAdam
+
+    torch.manual_seed(1234 + rank)
+    model = getattr(resnet_mod, args.arch)()
+    if args.sync_bn and distributed:
+        model = apex.parallel.convert_syncbn_model(model, channel_last=not args.no_channels_last)
+    model = model.to(dev)
+    mf = torch.contiguous_format if args.no_channels_last else torch.channels_last
+    model = model.to(memory_format=mf)
+    optimizer = FusedAdam(model.parameters(), lr=args.lr, weight_decay=1e-4,
+                          materialize_master_grads=args.materialize_master_grads)
+    low = torch.bfloat16 if args.dtype == "bf16" else torch.float16
+    model, optimizer = amp.initialize(model, optimizer, opt_level=args.opt_level, cast_model_type=low,
+                                      keep_batchnorm_fp32=True, verbosity=0)
+    if distributed:
+        model = apex.parallel.DistributedDataParallel(model)
+    criterion = torch.nn.CrossEntropyLoss().to(dev)
+
+    B = args.batch_size
+    images = torch.randn(B, 3, 224, 224, device=dev).to(memory_format=mf)
+    target = torch.randint(0, 1000, (B,), device=dev)
+
+    def step():
+        output = model(images)
+        loss = criterion(output, target)
+        optimizer.zero_grad()
+        with amp.scale_loss(loss, optimizer) as scaled_loss:
+            scaled_loss.backward()
+        optimizer.step()
+        return loss
+
+    t0 = time.time()
+    for i in range(args.warmup):
+        step()
+        if rank == 0 and (time.time() - t0) > 30 and i % 4 == 0:
+            print(f"[bench] warmup step {i + 1}/{args.warmup}", file=sys.stderr, flush=True)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    start = time.perf_counter()
+    for i in range(args.steps):
+        loss = step()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - start
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if distributed:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    ms_per_step = elapsed * 1000.0 / args.steps
+    value = world * B * args.steps / elapsed
+    if rank == 0:
+        res = {
+            "metric": "images/sec (whole node) ResNet-50 amp O2 + FusedAdam",
+            "value": round(value, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic 3x224x224 images + random labels on GPU; random-init weights",
+            "config": {
+                "model": args.arch,
+                "global_batch": B * world,
+                "per_gpu_batch": B,
+                "seq_len": None,
+                "image_size": 224,
+                "opt_level": args.opt_level,
+                "optimizer": "FusedAdam (fused amp: bf16 model grads -> fp32 master + bf16 model in one pass)"
+                if not args.materialize_master_grads else "FusedAdam (materialized fp32 master grads)",
+                "channels_last": not args.no_channels_last,
+                "sync_bn": bool(args.sync_bn and distributed),
+                "parallelism": f"dp{world}",
+                "final_loss": round(float(loss.item()), 4),
+            },
+        }
+        print(json.dumps(res), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

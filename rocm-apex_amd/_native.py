@@ -1,0 +1,47 @@
+"""Loader for the package's HIP extension (``_C``, built by ``tools/build_native.py``).
+
+Policy: GPU tensors ALWAYS go through the native gfx950 kernels.  If the extension is missing
+and a GPU op is requested we raise (no silent eager fallback); CPU tensors use the torch
+reference implementations in :mod:`apex.ops` (that is what the CPU test tier exercises).
+Set ``APEX_AMD_ALLOW_FALLBACK=1`` to permit the torch path on GPU for debugging.
+"""
+import importlib
+import os
+
+_C = None
+import_error = None
+try:
+    _C = importlib.import_module(__package__ + "._C")
+except Exception as e:  # pragma: no cover - depends on build state
+    import_error = e
+
+ALLOW_FALLBACK = os.environ.get("APEX_AMD_ALLOW_FALLBACK", "0") == "1"
+
+
+def available() -> bool:
+    return _C is not None
+
+
+def require(what: str = "native op"):
+    """Return the extension or raise loudly."""
+    if _C is None:
+        raise RuntimeError(
+            f"apex (gfx950) native extension is not built but {what} was requested on a GPU tensor; "
+            f"run `python tools/build_native.py` (import error: {import_error!r})")
+    return _C
+
+
+def submodule(name: str):
+    if _C is None:
+        return None
+    return getattr(_C, name, None)
+
+
+def use_native(*tensors) -> bool:
+    """True when the op must run on the HIP path (any GPU tensor among the inputs)."""
+    for t in tensors:
+        if t is not None and getattr(t, "is_cuda", False):
+            if _C is None and ALLOW_FALLBACK:
+                return False
+            return True
+    return False

@@ -1,0 +1,198 @@
+"""``amp.scale_loss`` / ``amp.disable_casts`` and the legacy handle objects
+(reference apex/amp/handle.py:16-281)."""
+import contextlib
+
+import torch
+
+from ._amp_state import _amp_state, maybe_print
+from .opt import OptimWrapper
+from .scaler import LossScaler
+
+
+def _as_list(optimizers):
+    if isinstance(optimizers, (list, tuple)):
+        return list(optimizers)
+    return [optimizers]
+
+
+def _patch_skip_step(opt, loss_scaler, loss_id):
+    """On overflow (sync mode) the next ``optimizer.step()`` becomes a no-op that restores the
+    real step afterwards (reference apex/amp/handle.py:129-154)."""
+    opt_step = opt.step
+
+    def skip_step(closure=None):
+        if closure is not None:
+            raise RuntimeError("Currently, Amp does not support closure use with optimizers.")
+        maybe_print(("Gradient overflow.  Skipping step, loss scaler "
+                     "{} reducing loss scale to {}").format(loss_id, loss_scaler.loss_scale()))
+        if hasattr(opt._amp_stash, "all_fp32_from_fp16_params"):
+            for param in opt._amp_stash.all_fp32_from_fp16_params:
+                param.grad = None
+        if hasattr(opt, "most_recent_scale"):
+            opt.most_recent_scale = 1.0
+            opt.scale_set_by_backward = False
+        opt.step = opt_step
+        opt._amp_stash.already_patched = False
+
+    opt.step = skip_step
+    opt._amp_stash.already_patched = True
+
+
+@contextlib.contextmanager
+def scale_loss(loss, optimizers, loss_id=0, model=None, delay_unscale=False, delay_overflow_check=False):
+    """Yields ``loss.float() * loss_scale``; on exit (unless ``delay_unscale``) checks the grads
+    for inf/NaN, unscales them into the master grads and updates the loss scale.
+
+    ``model`` is accepted for API compatibility and unused (as in the reference)."""
+    if not hasattr(_amp_state, "opt_properties"):
+        raise RuntimeError("Invoked 'with amp.scale_loss`, but internal Amp state has not been initialized.  "
+                           "model, optimizer = amp.initialize(model, optimizer, opt_level=...) must be called "
+                           "before `with amp.scale_loss`.")
+    if not _amp_state.opt_properties.enabled:
+        yield loss
+        return
+
+    optimizers = _as_list(optimizers)
+    loss_scaler = _amp_state.loss_scalers[loss_id]
+
+    if ((not _amp_state.opt_properties.master_weights) and (not loss_scaler.dynamic)
+            and loss_scaler.loss_scale() == 1.0):
+        yield loss.float()
+        if _amp_state.opt_properties.patch_torch_functions:
+            _amp_state.handle._clear_cache()
+        return
+
+    if not delay_unscale:
+        for optimizer in optimizers:
+            if not optimizer._amp_stash.params_have_scaled_gradients:
+                optimizer._prepare_amp_backward()
+
+    if loss.is_cuda:
+        loss_scaler._ensure(loss.device)
+    yield loss_scaler.scale_loss_value(loss)
+
+    if delay_unscale:
+        for optimizer in optimizers:
+            optimizer._amp_stash.params_have_scaled_gradients = True
+    else:
+        loss_scaler.clear_overflow_state()
+        for optimizer in optimizers:
+            optimizer._post_amp_backward(loss_scaler)
+            optimizer._amp_stash.params_have_scaled_gradients = False
+        should_skip = False if delay_overflow_check else loss_scaler.update_scale()
+        if loss_scaler.sync_free:
+            for optimizer in optimizers:
+                optimizer._amp_stash.skip_flag = loss_scaler.skip_flag
+                optimizer._amp_stash.inv_scale = loss_scaler.inv_scale_used
+        elif should_skip:
+            for optimizer in optimizers:
+                if not optimizer._amp_stash.already_patched:
+                    _patch_skip_step(optimizer, loss_scaler, loss_id)
+
+    if _amp_state.opt_properties.patch_torch_functions:
+        _amp_state.handle._clear_cache()
+
+
+@contextlib.contextmanager
+def disable_casts():
+    """Temporarily disables O1/O4 casting (reference apex/amp/handle.py:163-167)."""
+    h = getattr(_amp_state, "handle", None)
+    prev = h._is_active if h is not None else None
+    if h is not None:
+        h._is_active = False
+    try:
+        yield
+    finally:
+        if h is not None:
+            h._is_active = prev
+
+
+class AmpHandle(object):
+    """Legacy handle (reference apex/amp/handle.py:170-251).  Holds the O1 cast cache."""
+
+    def __init__(self, loss_scale="dynamic", enable_caching=True, verbose=False):
+        self._enable_caching = enable_caching
+        self._verbose = verbose
+        self._cache = dict()
+        self._default_scaler = LossScaler(loss_scale)
+        self._is_active = True
+        self._all_wrappers = []
+
+    def is_active(self):
+        return self._is_active
+
+    @contextlib.contextmanager
+    def _disable_casts(self):
+        self._is_active = False
+        try:
+            yield
+        finally:
+            self._is_active = True
+
+    def wrap_optimizer(self, optimizer, num_loss=1):
+        self._default_scaler = None
+        return OptimWrapper(optimizer, self, num_loss)
+
+    @contextlib.contextmanager
+    def scale_loss(self, loss, optimizer):
+        raise RuntimeError("The old Amp API is no longer supported.  Please move to the new API: "
+                           "amp.initialize() + amp.scale_loss().")
+        yield  # pragma: no cover
+
+    def _clear_cache(self):
+        self._cache.clear()
+
+    def _save_func(self, mod, fn, func):
+        self._all_wrappers.append((mod, fn, func))
+
+    def _deactivate(self):
+        from . import amp as _amp
+
+        _amp._uninstall()
+        self._all_wrappers = []
+
+    @property
+    def has_cache(self):
+        return self._enable_caching
+
+    @property
+    def cache(self):
+        return self._cache
+
+    def remove_cache(self, param):
+        if self.has_cache and param in self.cache:
+            del self.cache[param]
+
+    @property
+    def verbose(self):
+        return self._verbose
+
+
+class NoOpHandle(object):
+    def is_active(self):
+        return False
+
+    @contextlib.contextmanager
+    def _disable_casts(self):
+        yield
+
+    def wrap_optimizer(self, optimizer, num_loss=1):
+        return OptimWrapper(optimizer, self, num_loss)
+
+    @contextlib.contextmanager
+    def scale_loss(self, loss, optimizer):
+        yield loss
+
+    @property
+    def has_cache(self):
+        return False
+
+    @property
+    def verbose(self):
+        return False
+
+    def _clear_cache(self):
+        pass
+
+    def _deactivate(self):
+        pass

@@ -1,0 +1,194 @@
+// Multi-tensor-apply (MTA) engine for gfx950.
+//
+// What it replaces: the reference packs <=110 tensor addresses and <=320 (tensor, chunk) pairs
+// into the kernel-argument struct and relaunches every 320 chunks
+// (reference csrc/multi_tensor_apply.cuh:16-147).  Here the whole work list lives in a
+// device-resident table that the host builds once per distinct tensor list and caches
+// (bindings/mta_host.cpp), so an optimizer step over ANY number of tensors is ONE launch of a
+// persistent, grid-strided kernel sized to the 256 CUs, and it is capturable in a hipGraph
+// (no per-call H2D copy once the table is cached).
+#pragma once
+#include "apex_amd/device.h"
+
+namespace apex_amd {
+
+constexpr int kMtaBlock = 256;  // 4 waves per block; up to 8 blocks/CU resident
+constexpr int kVec = 8;         // elements per lane per step
+
+struct MtaMeta {
+  const int64_t* sizes;   // [ntensors] numel
+  const uint64_t* ptrs;   // [depth][ntensors] base addresses
+  const int2* chunks;     // [nchunks] {tensor index, chunk index within tensor}
+  const int* first_chunk; // [ntensors + 1] prefix of chunk counts (chunks of a tensor are contiguous)
+  float* partials;        // [2 * nchunks] scratch for per-chunk reductions
+  unsigned* ticket;       // arrival counter for single-pass grid reductions (reset by last block)
+  int ntensors;
+  int nchunks;
+  int chunk_size;
+  int depth;
+  int aligned;            // every base pointer 32-byte aligned -> vector path legal
+};
+
+template <typename T>
+__device__ __forceinline__ T* mta_ptr(const MtaMeta& m, int d, int t, int64_t start) {
+  return reinterpret_cast<T*>(m.ptrs[(size_t)d * m.ntensors + t]) + start;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Generic elementwise driver. `Op` provides:
+//   static constexpr unsigned kRead, kWrite;   // bitmask over list depth
+//   static constexpr bool kSkipOnNoop;         // early-exit when *noop != 0 at kernel start
+//   struct TS; __device__ TS tensor_state(int tensor) const;   // per-tensor scalars
+//   template<int N> __device__ void operator()(float (&r)[D][N], const TS&, bool& bad) const;
+// Ts... are the storage types of each list (float / f16_t / bf16_t).
+// ---------------------------------------------------------------------------------------------
+template <int I, typename... Ts> struct TypeAt;
+template <typename T0, typename... Ts> struct TypeAt<0, T0, Ts...> { using type = T0; };
+template <int I, typename T0, typename... Ts> struct TypeAt<I, T0, Ts...> {
+  using type = typename TypeAt<I - 1, Ts...>::type;
+};
+
+template <typename Op, int D, int I, typename... Ts>
+struct ListIO {
+  using T = typename TypeAt<I, Ts...>::type;
+  static __device__ __forceinline__ void load_vec(float (&r)[D][kVec], void* const (&base)[D], int i) {
+    if constexpr ((Op::kRead >> I) & 1u) Vec8<T>::load(r[I], reinterpret_cast<const T*>(base[I]) + i);
+    else {
+#pragma unroll
+      for (int k = 0; k < kVec; ++k) r[I][k] = 0.f;
+    }
+    if constexpr (I + 1 < D) ListIO<Op, D, I + 1, Ts...>::load_vec(r, base, i);
+  }
+  static __device__ __forceinline__ void store_vec(const float (&r)[D][kVec], void* const (&base)[D], int i) {
+    if constexpr ((Op::kWrite >> I) & 1u) Vec8<T>::store(reinterpret_cast<T*>(base[I]) + i, r[I]);
+    if constexpr (I + 1 < D) ListIO<Op, D, I + 1, Ts...>::store_vec(r, base, i);
+  }
+  static __device__ __forceinline__ void load_one(float (&r)[D][1], void* const (&base)[D], int i) {
+    if constexpr ((Op::kRead >> I) & 1u) r[I][0] = to_f(reinterpret_cast<const T*>(base[I])[i]);
+    else r[I][0] = 0.f;
+    if constexpr (I + 1 < D) ListIO<Op, D, I + 1, Ts...>::load_one(r, base, i);
+  }
+  static __device__ __forceinline__ void store_one(const float (&r)[D][1], void* const (&base)[D], int i) {
+    if constexpr ((Op::kWrite >> I) & 1u) reinterpret_cast<T*>(base[I])[i] = from_f<T>(r[I][0]);
+    if constexpr (I + 1 < D) ListIO<Op, D, I + 1, Ts...>::store_one(r, base, i);
+  }
+  static __device__ __forceinline__ void set_base(void* (&base)[D], const MtaMeta& m, int t, int64_t start) {
+    base[I] = mta_ptr<T>(m, I, t, start);
+    if constexpr (I + 1 < D) ListIO<Op, D, I + 1, Ts...>::set_base(base, m, t, start);
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Single-pass grid reduction support: every block writes its partial(s), the last arriving
+// block (agent-scope release/acquire ticket, cdna_hip_programming.md Guideline 16) finalizes.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool mta_last_block(unsigned* ticket, int* smem_flag);
+
+// Ops with kNumAcc > 0 accumulate per-element sums (or maxima when Op::kAccMax) which are
+// reduced per chunk into meta.partials; the last block then calls op.finalize(meta, smem).
+template <typename Op, typename... Ts>
+__global__ void __launch_bounds__(kMtaBlock) mta_elementwise_kernel(MtaMeta meta, int* noop, Op op) {
+  constexpr int D = sizeof...(Ts);
+  constexpr int NA = Op::kNumAcc;
+  __shared__ float smem[kMtaBlock / 64 * 2 + 2];
+  if constexpr (Op::kSkipOnNoop) {
+    // uniform early exit; a reduction op still has to take part in the ticket protocol
+    if (*reinterpret_cast<volatile int*>(noop) != 0) {
+      if constexpr (NA == 0) return;
+      else {
+        if (mta_last_block(meta.ticket, reinterpret_cast<int*>(&smem[kMtaBlock / 64 * 2]))) {
+          op.finalize_skipped(meta);
+          if (threadIdx.x == 0) __hip_atomic_store(meta.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+      }
+    }
+  }
+  bool bad = false;
+  for (int w = blockIdx.x; w < meta.nchunks; w += gridDim.x) {
+    const int2 tc = meta.chunks[w];
+    const int64_t start = (int64_t)tc.y * meta.chunk_size;
+    const int64_t rem = meta.sizes[tc.x] - start;
+    const int len = rem < meta.chunk_size ? (int)rem : meta.chunk_size;
+    void* base[D];
+    ListIO<Op, D, 0, Ts...>::set_base(base, meta, tc.x, start);
+    const auto ts = op.tensor_state(tc.x);
+    float acc[NA > 0 ? NA : 1];
+#pragma unroll
+    for (int a = 0; a < (NA > 0 ? NA : 1); ++a) acc[a] = 0.f;
+    const int nvec = meta.aligned ? (len / kVec) : 0;
+    for (int v = threadIdx.x; v < nvec; v += kMtaBlock) {
+      float r[D][kVec];
+      ListIO<Op, D, 0, Ts...>::load_vec(r, base, v * kVec);
+      op.template apply<kVec>(r, ts, bad, acc);
+      ListIO<Op, D, 0, Ts...>::store_vec(r, base, v * kVec);
+    }
+    for (int i = nvec * kVec + threadIdx.x; i < len; i += kMtaBlock) {
+      float r[D][1];
+      ListIO<Op, D, 0, Ts...>::load_one(r, base, i);
+      op.template apply<1>(r, ts, bad, acc);
+      ListIO<Op, D, 0, Ts...>::store_one(r, base, i);
+    }
+    if constexpr (NA > 0) {
+#pragma unroll
+      for (int a = 0; a < NA; ++a) {
+        float s = op.acc_is_max() ? block_max(acc[a], smem + a * (kMtaBlock / 64))
+                                  : block_sum(acc[a], smem + a * (kMtaBlock / 64));
+        if (threadIdx.x == 0) {
+          meta.partials[(size_t)a * meta.nchunks + w] = s;
+          if (Op::kCheckPartial && !is_finite(s)) bad = true;
+        }
+      }
+    }
+  }
+  if (bad) *noop = 1;  // benign race: every writer stores the same value
+  if constexpr (NA > 0) {
+    if (mta_last_block(meta.ticket, reinterpret_cast<int*>(&smem[kMtaBlock / 64 * 2]))) {
+      op.finalize(meta);
+      if (threadIdx.x == 0) __hip_atomic_store(meta.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+inline int mta_grid(int nchunks, int max_blocks) { return nchunks < max_blocks ? (nchunks > 0 ? nchunks : 1) : max_blocks; }
+
+// Base class for ops without reductions / per-tensor state.
+struct MtaOpBase {
+  static constexpr int kNumAcc = 0;
+  static constexpr bool kAccMax = false;
+  static constexpr bool kCheckPartial = false;
+  struct TS {};
+  __device__ __forceinline__ TS tensor_state(int) const { return {}; }
+  __device__ __forceinline__ bool acc_is_max() const { return false; }
+  __device__ __forceinline__ void finalize(const MtaMeta&) const {}
+  __device__ __forceinline__ void finalize_skipped(const MtaMeta&) const {}
+};
+
+// Sum (or max) partial slot `a` over the chunks of tensor t, in chunk order (deterministic).
+__device__ __forceinline__ float mta_tensor_reduce(const MtaMeta& m, int a, int t, bool is_max) {
+  const float* p = m.partials + (size_t)a * m.nchunks;
+  float s = 0.f;
+  for (int c = m.first_chunk[t]; c < m.first_chunk[t + 1]; ++c) s = is_max ? fmaxf(s, p[c]) : s + p[c];
+  return s;
+}
+
+__device__ __forceinline__ bool mta_last_block(unsigned* ticket, int* smem_flag) {
+  // every storing wave drains its stores, then one lane publishes with an agent-scope release
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int last = (prev == gridDim.x - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *smem_flag = last;
+  }
+  __syncthreads();
+  return *smem_flag != 0;
+}
+
+}  // namespace apex_amd

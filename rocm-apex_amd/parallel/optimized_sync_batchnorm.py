@@ -1,0 +1,133 @@
+"""SyncBatchNorm (reference apex/parallel/optimized_sync_batchnorm.py:9-85 and
+optimized_sync_batchnorm_kernel.py:7-119).
+
+Forward: local Welford (mean, biased var) -> ONE all_gather of [mean | var | count] per layer ->
+Welford merge -> normalize.  Backward: local (sum_dy, sum_dy_xmu, dgamma, dbeta) -> ONE
+all_reduce of [sum_dy | sum_dy_xmu] -> dx.  Stats kernels are the gfx950 Welford kernels in
+``csrc/syncbn``; the collectives are RCCL (latency-bound, 8C bytes per layer)."""
+import torch
+import torch.distributed as dist
+from torch.autograd.function import Function
+from torch.nn import functional as F
+from torch.nn.modules.batchnorm import _BatchNorm
+
+from ..ops import batchnorm as bnops
+
+
+class SyncBatchnormFunction(Function):
+    @staticmethod
+    def forward(ctx, input, z, weight, bias, running_mean, running_variance, eps, track_running_stats=True,
+                momentum=1.0, process_group=None, channel_last=False, fuse_relu=False):
+        input = input.contiguous() if not channel_last else input
+        if channel_last and not input.is_contiguous():
+            input = input.contiguous()
+        world_size = 0
+        if track_running_stats:
+            num_channels = input.size(-1) if channel_last else input.size(1)
+            count = input.numel() // num_channels
+            mean, var_biased = bnops.welford_mean_var(input, channel_last)
+            if dist.is_available() and dist.is_initialized():
+                pg = process_group if process_group else dist.group.WORLD
+                world_size = dist.get_world_size(pg)
+                count_t = torch.full((1,), float(count), dtype=mean.dtype, device=mean.device)
+                combined = torch.cat([mean.view(-1), var_biased.view(-1), count_t], dim=0)
+                if dist.get_backend(pg) == "nccl":
+                    gathered = torch.empty(world_size * combined.numel(), dtype=combined.dtype,
+                                           device=combined.device)
+                    dist.all_gather_into_tensor(gathered, combined, group=pg)
+                    gathered = gathered.view(world_size, -1)
+                else:
+                    parts = [torch.empty_like(combined) for _ in range(world_size)]
+                    dist.all_gather(parts, combined, group=pg)
+                    gathered = torch.stack(parts, 0)
+                mean_all, var_all, count_all = torch.split(gathered, num_channels, dim=1)
+                count_all = count_all.reshape(-1)
+                mean, var, inv_std = bnops.welford_parallel(mean_all, var_all, count_all.to(torch.int32), eps)
+            else:
+                count_all = torch.tensor([count], dtype=torch.int32, device=mean.device)
+                inv_std = 1.0 / torch.sqrt(var_biased + eps)
+                var = var_biased * count / max(count - 1, 1)
+            if count == 1 and world_size < 2:
+                raise ValueError("Expected more than 1 value per channel when training, got input size{}".format(
+                    input.size()))
+            if running_mean is not None:
+                r_m = mean if running_mean.dtype != torch.float16 else mean.half()
+                r_v = var if running_variance.dtype != torch.float16 else var.half()
+                running_mean.data.mul_(1 - momentum).add_(momentum * r_m)
+                running_variance.data.mul_(1 - momentum).add_(momentum * r_v)
+        else:
+            mean = running_mean.data.float()
+            inv_std = 1.0 / torch.sqrt(running_variance.data.float() + eps)
+            count_all = torch.tensor([1], dtype=torch.int32, device=mean.device)
+        ctx.save_for_backward(input, weight, mean, inv_std, z, bias, count_all.to(torch.int32))
+        ctx.process_group = process_group
+        ctx.channel_last = channel_last
+        ctx.world_size = world_size
+        ctx.fuse_relu = fuse_relu
+        return bnops.batchnorm_forward(input, mean, inv_std, weight, bias, channel_last, z, fuse_relu)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        grad_output = grad_output.contiguous()
+        saved_input, weight, mean, inv_std, z, bias, count = ctx.saved_tensors
+        channel_last = ctx.channel_last
+        grad_input = grad_z = grad_weight = grad_bias = None
+        if ctx.fuse_relu:
+            grad_output = bnops.relu_backward(grad_output, saved_input, z, mean, inv_std, weight, bias, channel_last)
+        if isinstance(z, torch.Tensor) and ctx.needs_input_grad[1]:
+            grad_z = grad_output.clone()
+        sum_dy, sum_dy_xmu, grad_weight, grad_bias = bnops.reduce_bn(grad_output, saved_input, mean, inv_std, weight,
+                                                                     channel_last)
+        if ctx.needs_input_grad[0]:
+            if dist.is_available() and dist.is_initialized():
+                c = sum_dy.shape[0]
+                combined = torch.cat([sum_dy, sum_dy_xmu], dim=0)
+                dist.all_reduce(combined, dist.ReduceOp.SUM, ctx.process_group, async_op=False)
+                sum_dy, sum_dy_xmu = torch.split(combined, c)
+            grad_input = bnops.batchnorm_backward(grad_output, saved_input, mean, inv_std, weight, sum_dy, sum_dy_xmu,
+                                                  count, channel_last)
+        if weight is None or not ctx.needs_input_grad[2]:
+            grad_weight = None
+        if weight is None or not ctx.needs_input_grad[3]:
+            grad_bias = None
+        return grad_input, grad_z, grad_weight, grad_bias, None, None, None, None, None, None, None, None
+
+
+class SyncBatchNorm(_BatchNorm):
+    """Batch norm whose training statistics are reduced across ``process_group``.
+
+    ``channel_last=True`` takes the channel as the last dim (NHWC); ``fuse_relu`` / ``z`` fuse a
+    residual add + ReLU into the normalization (channel_last only, as in the reference)."""
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1, affine=True, track_running_stats=True,
+                 process_group=None, channel_last=False, fuse_relu=False):
+        super(SyncBatchNorm, self).__init__(num_features, eps=eps, momentum=momentum, affine=affine,
+                                            track_running_stats=track_running_stats)
+        self.process_group = process_group
+        self.channel_last = channel_last
+        self.fuse_relu = fuse_relu
+
+    def _specify_process_group(self, process_group):
+        self.process_group = process_group
+
+    def _specify_channel_last(self, channel_last):
+        self.channel_last = channel_last
+
+    def _check_input_dim(self, input):
+        if input.dim() < 2:
+            raise ValueError("expected at least 2D input (got {}D input)".format(input.dim()))
+
+    def forward(self, input, z=None):
+        self._check_input_dim(input)
+        channel_last = self.channel_last if input.dim() != 2 else True
+        if (not self.training and self.track_running_stats and not channel_last and not self.fuse_relu
+                and z is None):
+            return F.batch_norm(input, self.running_mean, self.running_var, self.weight, self.bias, False, 0.0,
+                                self.eps)
+        factor = 0.0
+        if self.training and self.track_running_stats:
+            self.num_batches_tracked += 1
+            factor = 1.0 / float(self.num_batches_tracked) if self.momentum is None else self.momentum
+        return SyncBatchnormFunction.apply(input, z, self.weight, self.bias, self.running_mean, self.running_var,
+                                           self.eps, self.training or not self.track_running_stats, factor,
+                                           self.process_group, channel_last, self.fuse_relu)

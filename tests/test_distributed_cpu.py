@@ -1,0 +1,96 @@
+"""Multi-process (gloo, world_size 2) tests of the data-parallel layer (reference
+tests/distributed/: DDP race-condition test, SyncBN two-GPU unit test, amp master params)."""
+import pytest
+import torch
+import torch.distributed as dist
+
+from tests._dist_utils import run_multiprocess
+
+
+def _ddp_worker(rank, world, message_size, delay):
+    import apex
+    from apex.parallel import DistributedDataParallel as DDP
+
+    torch.manual_seed(rank)  # different init per rank -> DDP must broadcast rank 0's
+    model = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4))
+    ddp = DDP(model, message_size=message_size, delay_allreduce=delay)
+    w0 = [p.detach().clone() for p in model.parameters()]
+    gathered = [torch.empty_like(w0[0]) for _ in range(world)]
+    dist.all_gather(gathered, w0[0])
+    assert torch.equal(gathered[0], gathered[1]), "params not broadcast"
+    for it in range(3):
+        for p in model.parameters():
+            p.grad = None
+        x = torch.full((2, 8), float(rank + 1 + it))
+        ddp(x).sum().backward()
+        # analytic check: grads equal the average of per-rank grads
+        grads = [p.grad.detach().clone() for p in model.parameters()]
+        # recompute per-rank grads without DDP
+        ref_model = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4))
+        ref_model.load_state_dict(model.state_dict())
+        per = []
+        for r in range(world):
+            ref_model.zero_grad()
+            ref_model(torch.full((2, 8), float(r + 1 + it))).sum().backward()
+            per.append([p.grad.clone() for p in ref_model.parameters()])
+        for i, g in enumerate(grads):
+            exp = sum(pr[i] for pr in per) / world
+            torch.testing.assert_close(g, exp, rtol=1e-5, atol=1e-6)
+    assert len(ddp.buckets) >= 1
+
+
+@pytest.mark.parametrize("message_size,delay", [(1, False), (10000000, False), (40, True)])
+def test_ddp_gloo(message_size, delay):
+    run_multiprocess(_ddp_worker, 2, (message_size, delay))
+
+
+def _syncbn_worker(rank, world, channel_last):
+    import apex
+    from apex.parallel import SyncBatchNorm
+
+    torch.manual_seed(0)
+    full = torch.randn(8, 6, 5, 5, dtype=torch.float64).float()
+    local = full[rank * 4:(rank + 1) * 4].clone().requires_grad_()
+    bn = SyncBatchNorm(6, channel_last=channel_last)
+    ref = torch.nn.BatchNorm2d(6)
+    with torch.no_grad():
+        bn.weight.copy_(torch.linspace(0.5, 1.5, 6))
+        bn.bias.copy_(torch.linspace(-1, 1, 6))
+        ref.weight.copy_(bn.weight)
+        ref.bias.copy_(bn.bias)
+    xin = local.permute(0, 2, 3, 1).contiguous() if channel_last else local
+    y = bn(xin)
+    y_nchw = y.permute(0, 3, 1, 2) if channel_last else y
+    gy = torch.randn(8, 6, 5, 5, generator=torch.Generator().manual_seed(1))
+    (y_nchw * gy[rank * 4:(rank + 1) * 4]).sum().backward()
+    fr = full.clone().requires_grad_()
+    yr = ref(fr)
+    (yr * gy).sum().backward()
+    torch.testing.assert_close(y_nchw, yr[rank * 4:(rank + 1) * 4], rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(local.grad, fr.grad[rank * 4:(rank + 1) * 4], rtol=1e-4, atol=1e-4)
+    # weight grads are local sums (DDP averages them); compare the all-reduced sum
+    gw = bn.weight.grad.clone()
+    dist.all_reduce(gw)
+    torch.testing.assert_close(gw, ref.weight.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(bn.running_var, ref.running_var, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("channel_last", [False, True])
+def test_syncbn_gloo(channel_last):
+    run_multiprocess(_syncbn_worker, 2, (channel_last,))
+
+
+def _convert_worker(rank, world):
+    import apex
+    from apex.models import resnet18
+
+    m = apex.parallel.convert_syncbn_model(resnet18())
+    n = sum(isinstance(x, apex.parallel.SyncBatchNorm) for x in m.modules())
+    assert n == 20
+    g = apex.parallel.create_syncbn_process_group(2)
+    assert g is not None
+
+
+def test_convert_syncbn_gloo():
+    run_multiprocess(_convert_worker, 2, ())

@@ -1,0 +1,175 @@
+#!/usr/bin/env python3
+"""Build the package's single native extension (``apex._C``) for gfx950.
+
+Why not ``torch.utils.cpp_extension.CUDAExtension``: on ROCm it runs hipify over the sources;
+ours are HIP/CDNA4-native already, so we drive ``hipcc`` directly:
+
+* ``csrc/**/*.hip``  -> device translation units, torch-free (fast to compile), ``--offload-arch=gfx950``
+* ``csrc/bindings/*.cpp`` -> pybind/torch host code
+* link -> ``rocm-apex_amd/_C.<abi>.so`` IN-TREE (it travels to the GPU box with the repo snapshot)
+
+Incremental: an object is rebuilt when its source or any header under csrc/ is newer.
+Usage: ``python tools/build_native.py [-j N] [--clean] [--verbose]``
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "rocm-apex_amd")
+CSRC = os.path.join(PKG, "csrc")
+BUILD = os.path.join(ROOT, "build", "native")
+ARCH = os.environ.get("APEX_AMD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+# optional subsystems: binding file -> macro that module.cpp keys on
+SUBSYSTEMS = {
+    "norm.cpp": "APEX_AMD_WITH_NORM",
+    "softmax.cpp": "APEX_AMD_WITH_SOFTMAX",
+    "syncbn.cpp": "APEX_AMD_WITH_SYNCBN",
+    "gemm.cpp": "APEX_AMD_WITH_GEMM",
+    "xentropy.cpp": "APEX_AMD_WITH_XENTROPY",
+    "attn.cpp": "APEX_AMD_WITH_ATTN",
+    "contrib.cpp": "APEX_AMD_WITH_CONTRIB",
+}
+
+
+def ext_suffix() -> str:
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def output_path() -> str:
+    return os.path.join(PKG, "_C" + ext_suffix())
+
+
+def torch_paths():
+    import torch  # noqa: WPS433 (build-time dependency)
+
+    tdir = os.path.dirname(torch.__file__)
+    inc = [os.path.join(tdir, "include"), os.path.join(tdir, "include", "torch", "csrc", "api", "include")]
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return tdir, inc, abi
+
+
+def sources():
+    hip, cpp = [], []
+    for d, _, files in os.walk(CSRC):
+        for f in sorted(files):
+            p = os.path.join(d, f)
+            if f.endswith(".hip"):
+                hip.append(p)
+            elif f.endswith(".cpp") and os.sep + "bindings" + os.sep in p + os.sep:
+                cpp.append(p)
+    return sorted(hip), sorted(cpp)
+
+
+def newest_header() -> float:
+    t = 0.0
+    for d, _, files in os.walk(CSRC):
+        for f in files:
+            if f.endswith((".h", ".hpp", ".cuh", ".inc")):
+                t = max(t, os.path.getmtime(os.path.join(d, f)))
+    return t
+
+
+def obj_for(src: str) -> str:
+    rel = os.path.relpath(src, CSRC).replace(os.sep, "__")
+    return os.path.join(BUILD, rel + ".o")
+
+
+def compile_cmds(verbose: bool):
+    tdir, tinc, abi = torch_paths()
+    py_inc = sysconfig.get_paths()["include"]
+    hip, cpp = sources()
+    present = {os.path.basename(p) for p in cpp}
+    macros = [f"-D{m}" for f, m in SUBSYSTEMS.items() if f in present]
+    common = ["-std=c++17", "-O3", "-fPIC", f"-I{os.path.join(CSRC, 'include')}", "-Wno-unused-result",
+              "-Wno-deprecated-declarations", "-Wno-unused-command-line-argument"]
+    dev = [HIPCC, *common, f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-ffp-contract=fast",
+           "--no-offload-compress", "-x", "hip"]
+    host = [HIPCC, *common, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_EXTENSION_NAME=_C",
+            "-DTORCH_API_INCLUDE_EXTENSION_H", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", *macros,
+            *[f"-isystem{p}" for p in tinc], f"-isystem{py_inc}", "-fvisibility=hidden"]
+    jobs = []
+    for s in hip:
+        jobs.append((s, [*dev, "-c", s, "-o", obj_for(s)]))
+    for s in cpp:
+        jobs.append((s, [*host, "-c", s, "-o", obj_for(s)]))
+    link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", output_path(),
+            *[obj_for(s) for s, _ in jobs],
+            f"-L{os.path.join(tdir, 'lib')}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+            "-ltorch_python", "-lamdhip64", f"-Wl,-rpath,{os.path.join(tdir, 'lib')}"]
+    return jobs, link
+
+
+def run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    t0 = time.time()
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    return r.returncode, r.stdout, time.time() - t0
+
+
+def build(jobs_n: int | None = None, clean: bool = False, verbose: bool = False) -> str:
+    if clean and os.path.isdir(BUILD):
+        shutil.rmtree(BUILD)
+    os.makedirs(BUILD, exist_ok=True)
+    jobs, link = compile_cmds(verbose)
+    hdr = newest_header()
+    todo = []
+    for src, cmd in jobs:
+        o = obj_for(src)
+        if not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(src), hdr):
+            todo.append((src, cmd))
+    n = jobs_n or min(len(todo) or 1, max(1, (os.cpu_count() or 4)))
+    failed = []
+    if todo:
+        print(f"[build_native] compiling {len(todo)} translation unit(s) for {ARCH} with {n} job(s)", flush=True)
+        with cf.ThreadPoolExecutor(max_workers=n) as ex:
+            futs = {ex.submit(run, cmd, verbose): src for src, cmd in todo}
+            for f in cf.as_completed(futs):
+                rc, out, dt = f.result()
+                src = os.path.relpath(futs[f], ROOT)
+                if rc != 0:
+                    failed.append(src)
+                    print(f"[build_native] FAILED {src}\n{out}", flush=True)
+                else:
+                    print(f"[build_native] {src} ({dt:.1f}s)", flush=True)
+                    if out.strip() and verbose:
+                        print(out)
+    if failed:
+        raise RuntimeError(f"native build failed: {failed}")
+    out = output_path()
+    objs_newest = max(os.path.getmtime(obj_for(s)) for s, _ in jobs)
+    if todo or not os.path.exists(out) or os.path.getmtime(out) < objs_newest:
+        rc, log, dt = run(link, verbose)
+        if rc != 0:
+            print(log)
+            raise RuntimeError("native link failed")
+        print(f"[build_native] linked {os.path.relpath(out, ROOT)} ({dt:.1f}s)", flush=True)
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-j", type=int, default=None)
+    ap.add_argument("--clean", action="store_true")
+    ap.add_argument("--verbose", "-v", action="store_true")
+    a = ap.parse_args(argv)
+    try:
+        build(a.j, a.clean, a.verbose)
+    except RuntimeError as e:
+        print(f"[build_native] {e}", file=sys.stderr)
+        return 1
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
