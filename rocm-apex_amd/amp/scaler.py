@@ -158,7 +158,11 @@ class LossScaler(object):
         if not grads:
             return
         self._ensure(grads[0].device)
-        amp_C.multi_tensor_check_finite(65536, self._overflow_buf, [grads])
+        by_dtype = {}
+        for g in grads:
+            by_dtype.setdefault(g.dtype, []).append(g)
+        for gs in by_dtype.values():
+            amp_C.multi_tensor_check_finite(65536, self._overflow_buf, [gs])
 
     def unscale_with_stashed_python(self, model_grads, stashed_master_grads, master_grads, a, b):
         for model, stashed, master in zip(model_grads, stashed_master_grads, master_grads):

@@ -28,6 +28,19 @@ def _first_tensor(args):
     return None
 
 
+def _validate_lists(name, args):
+    """Same contract as the native engine (csrc/bindings/mta_host.cpp): every list is
+    dtype-homogeneous, so CPU tests catch callers that would corrupt data on the GPU."""
+    for a in args:
+        if isinstance(a, (list, tuple)) and a and isinstance(a[0], (list, tuple)):
+            for d, lst in enumerate(a):
+                ts = [x for x in lst if isinstance(x, torch.Tensor)]
+                if ts and any(x.dtype != ts[0].dtype for x in ts):
+                    raise RuntimeError(f"{name}: list {d} mixes dtypes "
+                                       f"({sorted({str(x.dtype) for x in ts})}); split lists by dtype")
+            return
+
+
 def _make(name):
     ref = getattr(_ref, name)
 
@@ -38,6 +51,7 @@ def _make(name):
                 if hasattr(a, "is_cuda"):
                     t = a
                     break
+        _validate_lists(name, args)
         if _native.use_native(t):
             return getattr(_native.require(f"amp_C.{name}").amp_C, name)(*args, **kwargs)
         with torch.no_grad():

@@ -65,8 +65,13 @@ MtaMeta mta_meta(const std::vector<std::vector<at::Tensor>>& lists, int chunk_si
       TORCH_CHECK(x.numel() == n, "multi_tensor_apply: size mismatch at list ", d, " tensor ", t);
       TORCH_CHECK(x.is_non_overlapping_and_dense(), "multi_tensor_apply: tensor ", t, " of list ", d,
                   " is not dense");
-      if (d > 0 && !x.is_contiguous())
-        TORCH_CHECK(x.strides() == t0.strides(), "multi_tensor_apply: layout mismatch at tensor ", t);
+      TORCH_CHECK(x.scalar_type() == lists[d][0].scalar_type(), "multi_tensor_apply: list ", d,
+                  " mixes dtypes (", lists[d][0].scalar_type(), " vs ", x.scalar_type(), " at tensor ", t,
+                  "); split lists by dtype");
+      // elementwise over raw storage: every list must walk the same physical element order
+      if (d > 0 && !(x.is_contiguous() && t0.is_contiguous()))
+        TORCH_CHECK(x.strides() == t0.strides(), "multi_tensor_apply: memory layout mismatch at tensor ", t,
+                    " of list ", d);
       const uint64_t p = (uint64_t)x.data_ptr();
       aligned = aligned && (p % 32 == 0);
       key.push_back(p);

@@ -1,0 +1,284 @@
+// LayerNorm / RMSNorm backward for gfx950.
+//
+// Reference: csrc/layer_norm_cuda_kernel.cu:430 (cuComputePartGradGammaBeta), :498
+// (cuComputeGradGammaBeta), :549 (cuComputeGradInput), launcher :753-833 — three kernels, and
+// dy/x are read twice (once for dgamma/dbeta, once for dx).
+//
+// Here dx and the dgamma/dbeta partials come out of ONE persistent pass: a lane owns a fixed
+// set of columns (the same for every row it visits), so while it computes dx for a row it also
+// accumulates dy*xhat and dy for its columns in registers.  Each workgroup leaves one fp32
+// partial row per quantity; a small column-reduce kernel sums the partials in a fixed order
+// (bitwise deterministic, no float atomics).
+#include "norm_common.h"
+
+namespace apex_amd {
+namespace norm {
+
+// Persistent grid: enough resident blocks to saturate HBM, few enough that the partial slab
+// stays small relative to the activations.
+inline int bwd_grid(int64_t ngroups, int cus) {
+  const int64_t cap = (int64_t)cus * 2;
+  return (int)(ngroups < cap ? (ngroups > 0 ? ngroups : 1) : cap);
+}
+
+template <typename TI, typename TW, typename TO, int W, int VPT>
+__global__ void __launch_bounds__(block_threads<W>())
+ln_bwd_kernel(const TO* __restrict__ dy, const TI* __restrict__ x, const float* __restrict__ mean,
+              const float* __restrict__ invvar, const TW* __restrict__ gamma, TI* __restrict__ dx,
+              float* __restrict__ part_g, float* __restrict__ part_b, int64_t n1, int n2, bool rms,
+              bool want_dgamma, bool want_dbeta) {
+  constexpr int NT = block_threads<W>();
+  constexpr int RPB = NT / 64 / W;
+  __shared__ float red[2 * RPB * W];
+  const int wave = threadIdx.x >> 6;
+  const int row_in_block = wave / W;
+  const int wave_in_row = wave % W;
+  const int li = wave_in_row * 64 + (threadIdx.x & 63);
+  const int nv = n2 >> 3;
+  const int64_t ngroups = (n1 + RPB - 1) / RPB;
+  const float inv_n = 1.f / (float)n2;
+
+  float g[VPT][8];
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    const int v = j * W * 64 + li;
+    if (gamma != nullptr && v < nv) {
+      Vec8<TW>::load(g[j], gamma + v * 8);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[j][k] = 1.f;
+    }
+  }
+  float ag[VPT][8], ab[VPT][8];
+#pragma unroll
+  for (int j = 0; j < VPT; ++j)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      ag[j][k] = 0.f;
+      ab[j][k] = 0.f;
+    }
+
+  for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const int64_t row = grp * RPB + row_in_block;
+    const bool valid = row < n1;
+    const int64_t rr = valid ? row : 0;
+    const float mu = (rms || !valid) ? 0.f : mean[rr];
+    const float iv = valid ? invvar[rr] : 0.f;
+    float xh[VPT][8], d[VPT][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int v = j * W * 64 + li;
+      if (valid && v < nv) {
+        Vec8<TI>::load(xh[j], x + rr * n2 + v * 8);
+        Vec8<TO>::load(d[j], dy + rr * n2 + v * 8);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          xh[j][k] = (xh[j][k] - mu) * iv;
+          const float gd = d[j][k] * g[j][k];
+          s1 += gd;
+          s2 += gd * xh[j][k];
+          ag[j][k] += d[j][k] * xh[j][k];
+          ab[j][k] += d[j][k];
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          xh[j][k] = 0.f;
+          d[j][k] = 0.f;
+        }
+      }
+    }
+    row_sum2<W>(s1, s2, red, row_in_block, wave_in_row);
+    const float m1 = rms ? 0.f : s1 * inv_n;
+    const float m2 = s2 * inv_n;
+    if (valid) {
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        const int v = j * W * 64 + li;
+        if (v < nv) {
+          float o[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] = iv * (d[j][k] * g[j][k] - m1 - xh[j][k] * m2);
+          Vec8<TI>::store(dx + rr * n2 + v * 8, o);
+        }
+      }
+    }
+  }
+
+  if (!want_dgamma && !want_dbeta) return;
+  // Combine the RPB rows-per-block lanes that own the same columns, then write one partial row.
+  // LDS image: [RPB][n2] floats, reused for dgamma then dbeta.
+  extern __shared__ __attribute__((aligned(16))) float cmb[];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if ((q == 0 && !want_dgamma) || (q == 1 && !want_dbeta)) continue;
+    float* out = (q == 0 ? part_g : part_b) + (int64_t)blockIdx.x * n2;
+    if constexpr (RPB == 1) {
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        const int v = j * W * 64 + li;
+        if (v < nv) Vec8<float>::store(out + v * 8, q == 0 ? ag[j] : ab[j]);
+      }
+    } else {
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        const int v = j * W * 64 + li;
+        if (v < nv) Vec8<float>::store(cmb + (int64_t)row_in_block * n2 + v * 8, q == 0 ? ag[j] : ab[j]);
+      }
+      __syncthreads();
+      for (int c = threadIdx.x; c < n2; c += NT) {
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < RPB; ++i) sum += cmb[i * n2 + c];
+        out[c] = sum;
+      }
+    }
+  }
+}
+
+// dgamma[c] = sum_b part[b][c] in fixed b order.  Block = 64 columns x 4 row-groups.
+template <typename TW>
+__global__ void __launch_bounds__(256)
+ln_col_reduce_kernel(const float* __restrict__ part_g, const float* __restrict__ part_b, TW* __restrict__ dgamma,
+                     TW* __restrict__ dbeta, int nparts, int n2) {
+  __shared__ float red[4][64];
+  const float* part = blockIdx.y == 0 ? part_g : part_b;
+  TW* out = blockIdx.y == 0 ? dgamma : dbeta;
+  if (out == nullptr) return;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int grp = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < n2)
+    for (int b = grp; b < nparts; b += 4) s += part[(int64_t)b * n2 + c];
+  red[grp][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (grp == 0 && c < n2) {
+    const int l = threadIdx.x & 63;
+    out[c] = from_f<TW>(((red[0][l] + red[1][l]) + red[2][l]) + red[3][l]);
+  }
+}
+
+// Generic path: dx per row (block per row) and dgamma/dbeta partials by a column-tiled pass.
+template <typename TI, typename TW, typename TO>
+__global__ void __launch_bounds__(256)
+ln_bwd_dx_generic_kernel(const TO* __restrict__ dy, const TI* __restrict__ x, const float* __restrict__ mean,
+                         const float* __restrict__ invvar, const TW* __restrict__ gamma, TI* __restrict__ dx,
+                         int64_t n1, int n2, bool rms) {
+  __shared__ float red[8];
+  const int64_t row = blockIdx.x;
+  const float mu = rms ? 0.f : mean[row];
+  const float iv = invvar[row];
+  const TI* xr = x + row * n2;
+  const TO* dr = dy + row * n2;
+  float s1 = 0.f, s2 = 0.f;
+  for (int i = threadIdx.x; i < n2; i += 256) {
+    const float gd = to_f(dr[i]) * (gamma ? to_f(gamma[i]) : 1.f);
+    s1 += gd;
+    s2 += gd * (to_f(xr[i]) - mu) * iv;
+  }
+  s1 = block_sum(s1, red);
+  s2 = block_sum(s2, red + 4);
+  const float m1 = rms ? 0.f : s1 / (float)n2, m2 = s2 / (float)n2;
+  for (int i = threadIdx.x; i < n2; i += 256) {
+    const float gd = to_f(dr[i]) * (gamma ? to_f(gamma[i]) : 1.f);
+    const float xh = (to_f(xr[i]) - mu) * iv;
+    dx[row * n2 + i] = from_f<TI>(iv * (gd - m1 - xh * m2));
+  }
+}
+
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256)
+ln_bwd_gb_generic_kernel(const TO* __restrict__ dy, const TI* __restrict__ x, const float* __restrict__ mean,
+                         const float* __restrict__ invvar, float* __restrict__ part_g, float* __restrict__ part_b,
+                         int64_t n1, int n2, bool rms) {
+  // grid (ceil(n2/256), nparts): each thread owns one column over a strided subset of rows
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= n2) return;
+  float sg = 0.f, sb = 0.f;
+  for (int64_t r = blockIdx.y; r < n1; r += gridDim.y) {
+    const float d = to_f(dy[r * n2 + c]);
+    const float xh = (to_f(x[r * n2 + c]) - (rms ? 0.f : mean[r])) * invvar[r];
+    sg += d * xh;
+    sb += d;
+  }
+  part_g[(int64_t)blockIdx.y * n2 + c] = sg;
+  part_b[(int64_t)blockIdx.y * n2 + c] = sb;
+}
+
+template <typename TI, typename TW, typename TO, int W, int VPT>
+static int launch_bwd(const NormBwdArgs& a, int cus, hipStream_t s) {
+  constexpr int NT = block_threads<W>();
+  constexpr int RPB = NT / 64 / W;
+  const int64_t ngroups = (a.n1 + RPB - 1) / RPB;
+  const int grid = bwd_grid(ngroups, cus);
+  const bool wg = a.dgamma != nullptr, wb = a.dbeta != nullptr;
+  const size_t lds = (RPB > 1 && (wg || wb)) ? (size_t)RPB * a.n2 * sizeof(float) : 0;
+  float* pg = a.workspace;
+  float* pb = a.workspace + (int64_t)grid * a.n2;
+  hipLaunchKernelGGL((ln_bwd_kernel<TI, TW, TO, W, VPT>), dim3(grid), dim3(NT), lds, s, (const TO*)a.dy,
+                     (const TI*)a.x, a.mean, a.invvar, (const TW*)a.gamma, (TI*)a.dx, pg, pb, a.n1, a.n2, a.rms,
+                     wg, wb);
+  return grid;
+}
+
+static bool aligned16(const void* p) { return p == nullptr || ((uintptr_t)p & 15u) == 0; }
+
+static int generic_parts(int64_t n1, int n2, int cus) {
+  const int64_t col_blocks = (n2 + 255) / 256;
+  int64_t p = ((int64_t)cus * 4 + col_blocks - 1) / col_blocks;
+  if (p > n1) p = n1;
+  if (p > 1024) p = 1024;
+  return (int)(p < 1 ? 1 : p);
+}
+
+void norm_bwd_impl(const NormBwdArgs& a, int cus, hipStream_t s) {
+  if (a.n1 <= 0 || a.n2 <= 0) return;
+  const Cfg c = pick_cfg(a.n2);
+  const bool fast = c.W > 0 && (a.n2 % 8 == 0) && aligned16(a.x) && aligned16(a.dy) && aligned16(a.dx) &&
+                    aligned16(a.gamma);
+  const bool want = a.dgamma != nullptr || a.dbeta != nullptr;
+  dispatch_norm_types(a.in_t, a.w_t, a.out_t, [&](auto ti, auto tw, auto to) {
+    using TI = typename decltype(ti)::type;
+    using TW = typename decltype(tw)::type;
+    using TO = typename decltype(to)::type;
+    int nparts = 0;
+    if (fast) {
+      if (c.W == 1 && c.VPT == 1) nparts = launch_bwd<TI, TW, TO, 1, 1>(a, cus, s);
+      else if (c.W == 1 && c.VPT == 2) nparts = launch_bwd<TI, TW, TO, 1, 2>(a, cus, s);
+      else if (c.W == 1 && c.VPT == 4) nparts = launch_bwd<TI, TW, TO, 1, 4>(a, cus, s);
+      else if (c.W == 4 && c.VPT == 2) nparts = launch_bwd<TI, TW, TO, 4, 2>(a, cus, s);
+      else if (c.W == 4 && c.VPT == 4) nparts = launch_bwd<TI, TW, TO, 4, 4>(a, cus, s);
+      else nparts = launch_bwd<TI, TW, TO, 8, 4>(a, cus, s);
+    } else {
+      hipLaunchKernelGGL((ln_bwd_dx_generic_kernel<TI, TW, TO>), dim3((unsigned)a.n1), dim3(256), 0, s,
+                         (const TO*)a.dy, (const TI*)a.x, a.mean, a.invvar, (const TW*)a.gamma, (TI*)a.dx, a.n1,
+                         a.n2, a.rms);
+      if (want) {
+        nparts = generic_parts(a.n1, a.n2, cus);
+        hipLaunchKernelGGL((ln_bwd_gb_generic_kernel<TI, TO>), dim3((a.n2 + 255) / 256, nparts), dim3(256), 0, s,
+                           (const TO*)a.dy, (const TI*)a.x, a.mean, a.invvar, a.workspace,
+                           a.workspace + (int64_t)nparts * a.n2, a.n1, a.n2, a.rms);
+      }
+    }
+    if (want) {
+      hipLaunchKernelGGL((ln_col_reduce_kernel<TW>), dim3((a.n2 + 63) / 64, 2), dim3(256), 0, s, a.workspace,
+                         a.workspace + (int64_t)nparts * a.n2, (TW*)a.dgamma, (TW*)a.dbeta, nparts, a.n2);
+    }
+  });
+  check_launch("layer_norm backward");
+}
+
+}  // namespace norm
+
+int64_t norm_bwd_workspace_floats(int64_t n1, int n2, int cus) {
+  const int64_t fast_parts = (int64_t)cus * 2;
+  const int64_t gen_parts = 1024;
+  const int64_t parts = fast_parts > gen_parts ? fast_parts : gen_parts;
+  return 2 * parts * (int64_t)n2;
+}
+
+void norm_bwd(const NormBwdArgs& a, int cus, hipStream_t s) { norm::norm_bwd_impl(a, cus, s); }
+
+}  // namespace apex_amd

@@ -1,0 +1,95 @@
+// Shared pieces of the LayerNorm / RMSNorm kernels (fwd in layer_norm_fwd.hip, bwd in
+// layer_norm_bwd.hip).
+//
+// Geometry (MI355X, wave64): a row of n2 elements is owned by W waves (W = 1, 4 or 8); each
+// lane holds VPT vectors of 8 elements in registers (one 16-byte load per vector for 16-bit
+// types), so a row is read from HBM exactly once per pass and all statistics are two-pass
+// (mean, then sum of squared deviations) on register-resident data — no Welford merge chain,
+// no re-read.  Vector j of lane li covers columns [(j*W*64 + li)*8, +8).  Supported fast-path
+// widths: n2 % 8 == 0 and n2 <= 16384; anything else takes the generic block-per-row kernels.
+#pragma once
+#include "apex_amd/device.h"
+#include "apex_amd/dispatch.h"
+#include "apex_amd/norm_api.h"
+
+namespace apex_amd {
+namespace norm {
+
+struct Cfg {
+  int W;    // waves per row
+  int VPT;  // 8-element vectors per lane
+};
+
+// smallest register-resident geometry that covers n2 (0 => generic path)
+inline Cfg pick_cfg(int n2) {
+  if (n2 <= 512) return {1, 1};
+  if (n2 <= 1024) return {1, 2};
+  if (n2 <= 2048) return {1, 4};
+  if (n2 <= 4096) return {4, 2};
+  if (n2 <= 8192) return {4, 4};
+  if (n2 <= 16384) return {8, 4};
+  return {0, 0};
+}
+
+template <int W>
+constexpr int block_threads() { return W == 8 ? 512 : 256; }
+
+// Sum over the W waves of one row; `red` is LDS of [rows_per_block * W] floats.  Every thread
+// of the block must call it (it contains barriers).
+template <int W>
+__device__ __forceinline__ float row_sum(float v, float* red, int row_in_block, int wave_in_row) {
+  v = wave_sum(v);
+  if constexpr (W == 1) {
+    return v;
+  } else {
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[row_in_block * W + wave_in_row] = v;
+    __syncthreads();
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < W; ++i) s += red[row_in_block * W + i];
+    return s;
+  }
+}
+
+template <int W>
+__device__ __forceinline__ void row_sum2(float& a, float& b, float* red, int row_in_block, int wave_in_row) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  if constexpr (W > 1) {
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+      red[2 * (row_in_block * W + wave_in_row)] = a;
+      red[2 * (row_in_block * W + wave_in_row) + 1] = b;
+    }
+    __syncthreads();
+    a = 0.f;
+    b = 0.f;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+      a += red[2 * (row_in_block * W + i)];
+      b += red[2 * (row_in_block * W + i) + 1];
+    }
+  }
+}
+
+// typed dispatch over the (input, weight, output) triples the python layer can produce
+template <typename F>
+inline void dispatch_norm_types(int in_t, int w_t, int out_t, F&& f) {
+  dispatch_float(in_t, [&](auto ti) {
+    dispatch_float(w_t, [&](auto tw) {
+      using TI = typename decltype(ti)::type;
+      using TW = typename decltype(tw)::type;
+      if (out_t == in_t) {
+        f(ti, tw, Tag<TI>{});
+      } else if (out_t == w_t) {
+        f(ti, tw, Tag<TW>{});
+      } else {
+        throw std::runtime_error("norm: output dtype must equal the input or the weight dtype");
+      }
+    }, "norm weight");
+  }, "norm input");
+}
+
+}  // namespace norm
+}  // namespace apex_amd

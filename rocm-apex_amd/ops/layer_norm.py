@@ -57,10 +57,12 @@ def ln_bwd(dy, x, mean, invvar, normalized_shape, weight, bias, eps, rms=False):
         m = _norm()
         if rms:
             if weight is not None:
-                return m.rms_backward_affine(dy, invvar, x, list(normalized_shape), weight, eps)
+                dx, dgamma = m.rms_backward_affine(dy, invvar, x, list(normalized_shape), weight, eps)
+                return dx, dgamma, None
             return m.rms_backward(dy, invvar, x, list(normalized_shape), eps), None, None
         if weight is not None:
-            return m.backward_affine(dy, mean, invvar, x, list(normalized_shape), weight, bias, eps)
+            dx, dgamma, dbeta = m.backward_affine(dy, mean, invvar, x, list(normalized_shape), weight, bias, eps)
+            return dx, dgamma, (dbeta if bias is not None else None)
         return m.backward(dy, mean, invvar, x, list(normalized_shape), eps), None, None
     n1, n2 = compute_n1_n2(x, normalized_shape)
     xf = x.float().reshape(n1, n2)

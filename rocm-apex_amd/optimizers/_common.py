@@ -51,7 +51,9 @@ def device_step(group, st, device):
     """Device-resident step counter: incremented only when the step is not skipped."""
     t = group.get("_step_t")
     if t is None or t.device != device:
-        t = torch.full((1,), float(group.get("step", 0)), dtype=torch.float32, device=device)
+        # the caller has already bumped the host counter for this call; the device counter
+        # starts from the last *completed* step and is the authority from here on
+        t = torch.full((1,), float(group.get("step", 1) - 1), dtype=torch.float32, device=device)
         group["_step_t"] = t
     # step += 1 - skip  (stays on device)
     t.add_(1.0 - st.skip_flag.to(torch.float32))

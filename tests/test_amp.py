@@ -250,3 +250,22 @@ def test_sync_free_overflow_skip_gpu():
     # the device step counter did not count the skipped step
     opt.state_dict()
     assert opt.param_groups[0]["step"] == 3
+
+
+@pytest.mark.gpu
+def test_o2_bf16_convbn_mixed_dtype_grads_not_skipped_gpu():
+    """Model with bf16 convs and fp32 (keep_batchnorm_fp32) BN params: the sync-free overflow
+    probe must handle the mixed-dtype grad set (regression: a mixed list was read as one dtype
+    and flagged every step as overflow)."""
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Conv2d(3, 16, 3), torch.nn.BatchNorm2d(16), torch.nn.ReLU(),
+                                torch.nn.Flatten(), torch.nn.Linear(16 * 6 * 6, 10)).cuda()
+    model = model.to(memory_format=torch.channels_last)
+    opt = FusedAdam(model.parameters(), lr=1e-3, materialize_master_grads=False)
+    model, opt = amp.initialize(model, opt, opt_level="O2", cast_model_type=torch.bfloat16, verbosity=0)
+    x = torch.randn(8, 3, 8, 8, device="cuda").to(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device="cuda")
+    before = [p.detach().clone() for p in model.parameters()]
+    _train(model, opt, 3, x, y)
+    assert amp.state_dict()["loss_scaler0"]["unskipped"] == 3
+    assert all(not torch.equal(a, b) for a, b in zip(before, model.parameters()))

@@ -164,10 +164,12 @@ def test_l2norm_scale_gpu():
 def test_check_finite_and_cache_gpu():
     xs = _lists("cuda", torch.bfloat16, SIZES)
     noop = _noop("cuda")
-    n0 = amp_C.mta_cache_size()
     amp_C.multi_tensor_check_finite(CHUNK, noop, [xs])
+    n1 = amp_C.mta_cache_size()
     amp_C.multi_tensor_check_finite(CHUNK, noop, [xs])
-    assert amp_C.mta_cache_size() == n0 + 1  # same list -> cached work table
+    # same list -> cached work table reused (an earlier test may already own this key, when the
+    # caching allocator hands back identical addresses, so only the second call is checked)
+    assert amp_C.mta_cache_size() == n1
     assert noop.item() == 0
     xs[-1][-1] = float("-inf")
     amp_C.multi_tensor_check_finite(CHUNK, noop, [xs])
