@@ -1,8 +1,13 @@
-"""Batch-norm statistics / apply primitives used by SyncBatchNorm (reference csrc/syncbn.cpp:8-109).
+"""Batch-norm statistics / apply primitives used by SyncBatchNorm and the fused NHWC BN
+(reference csrc/syncbn.cpp:8-109).
 
-GPU tensors run the gfx950 Welford kernels (``_C.syncbn``); CPU tensors use the torch
-implementations below, which also serve as the numerics oracle in tests.
-Layouts: ``channel_last=False`` -> [N, C, *]; ``channel_last=True`` -> [..., C] (NHWC/flattened)."""
+GPU tensors run the gfx950 Welford kernels (``_C.syncbn``, csrc/syncbn/welford.hip); CPU tensors
+use the torch implementations below, which are also the numerics oracle in tests.
+Layouts: ``channel_last=False`` -> [N, C, *]; ``channel_last=True`` -> [..., C] (the channel is
+the LAST logical dim; torch channels_last activations are passed in as a permuted NHWC view).
+
+Fused ReLU: ``batchnorm_forward(..., z, fuse_relu)`` computes relu(bn(x) + z); the backward
+helpers accept the same (z, bias, fuse_relu) and mask the gradient by the recomputed output."""
 import torch
 
 from .. import _native
@@ -24,11 +29,16 @@ def _bshape(x, channel_last):
     return (1, -1) + (1,) * (x.dim() - 2)
 
 
+def _c(t):
+    return None if t is None else t.contiguous()
+
+
 def welford_mean_var(x, channel_last=False):
     """Per-channel mean and biased variance (fp32 outputs)."""
     if _native.use_native(x):
         m = _syncbn()
-        return m.welford_mean_var_c_last(x) if channel_last else m.welford_mean_var(x)
+        x = x.contiguous()
+        return tuple(m.welford_mean_var_c_last(x) if channel_last else m.welford_mean_var(x))
     xf = x.float()
     dims = _reduce_dims(xf, channel_last)
     mean = xf.mean(dim=dims)
@@ -39,7 +49,7 @@ def welford_mean_var(x, channel_last=False):
 def welford_parallel(mean_all, var_all, count_all, eps):
     """Merge per-rank (mean, biased var, count) -> (mean, unbiased var, inv_std)."""
     if _native.use_native(mean_all):
-        return _syncbn().welford_parallel(mean_all, var_all, count_all.to(torch.int32), float(eps))
+        return tuple(_syncbn().welford_parallel(mean_all, var_all, count_all.to(torch.int32), float(eps)))
     cnt = count_all.double().view(-1, 1)
     n = cnt.sum(0)
     mean = (mean_all.double() * cnt).sum(0) / n
@@ -50,12 +60,7 @@ def welford_parallel(mean_all, var_all, count_all, eps):
     return mean.float(), var_u.float(), inv_std.float()
 
 
-def batchnorm_forward(x, mean, inv_std, weight, bias, channel_last=False, z=None, fuse_relu=False):
-    if _native.use_native(x):
-        m = _syncbn()
-        if channel_last:
-            return m.batchnorm_forward_c_last(x, z, mean, inv_std, weight, bias, fuse_relu)
-        return m.batchnorm_forward(x, mean, inv_std, weight, bias)
+def _torch_bn(x, mean, inv_std, weight, bias, channel_last, z=None, fuse_relu=False):
     shp = _bshape(x, channel_last)
     y = (x.float() - mean.view(shp)) * inv_std.view(shp)
     if weight is not None:
@@ -66,23 +71,46 @@ def batchnorm_forward(x, mean, inv_std, weight, bias, channel_last=False, z=None
         y = y + z.float()
     if fuse_relu:
         y = torch.relu(y)
-    return y.to(x.dtype)
+    return y
+
+
+def batchnorm_forward(x, mean, inv_std, weight, bias, channel_last=False, z=None, fuse_relu=False):
+    if _native.use_native(x):
+        m = _syncbn()
+        x = x.contiguous()
+        if channel_last:
+            return m.batchnorm_forward_c_last(x, _c(z), mean, inv_std, weight, bias, fuse_relu)
+        if z is not None or fuse_relu:
+            y = m.batchnorm_forward(x, mean, inv_std, weight, bias)
+            if z is not None:
+                y = y + z
+            return torch.relu_(y) if fuse_relu else y
+        return m.batchnorm_forward(x, mean, inv_std, weight, bias)
+    return _torch_bn(x, mean, inv_std, weight, bias, channel_last, z, fuse_relu).to(x.dtype)
 
 
 def relu_backward(grad_out, x, z, mean, inv_std, weight, bias, channel_last=True):
-    """Mask the incoming grad by the recomputed fused-ReLU output."""
-    if _native.use_native(x):
-        return _syncbn().relu_bw_c_last(grad_out, x, z, mean, inv_std, weight, bias)
-    y = batchnorm_forward(x, mean, inv_std, weight, bias, channel_last, z, False)
+    """Mask the incoming grad by the recomputed fused-ReLU output (materialized; needed when the
+    residual input ``z`` requires a gradient)."""
+    if _native.use_native(x) and channel_last:
+        return _syncbn().relu_bw_c_last(grad_out.contiguous(), x.contiguous(), _c(z), mean, inv_std, weight, bias)
+    y = _torch_bn(x, mean, inv_std, weight, bias, channel_last, z, False)
     return torch.where(y > 0, grad_out, torch.zeros_like(grad_out))
 
 
-def reduce_bn(grad_out, x, mean, inv_std, weight, channel_last=False):
-    """Returns (sum_dy, sum_dy_xmu, grad_weight, grad_bias) over the local batch."""
+def reduce_bn(grad_out, x, mean, inv_std, weight, channel_last=False, z=None, bias=None, fuse_relu=False):
+    """Returns (sum_dy, sum_dy_xmu, grad_weight, grad_bias) over the local batch.  With
+    ``fuse_relu`` the grad is first masked by relu(bn(x)+z) > 0 (recomputed in-kernel)."""
     if _native.use_native(x):
         m = _syncbn()
-        return m.reduce_bn_c_last(grad_out, x, mean, inv_std, weight) if channel_last else \
-            m.reduce_bn(grad_out, x, mean, inv_std, weight)
+        x = x.contiguous()
+        if channel_last:
+            return tuple(m.reduce_bn_c_last(grad_out, x, mean, inv_std, weight, _c(z), bias, fuse_relu))
+        if fuse_relu:
+            grad_out = relu_backward(grad_out, x, z, mean, inv_std, weight, bias, False)
+        return tuple(m.reduce_bn(grad_out.contiguous(), x, mean, inv_std, weight))
+    if fuse_relu:
+        grad_out = relu_backward(grad_out, x, z, mean, inv_std, weight, bias, channel_last)
     shp = _bshape(x, channel_last)
     dims = _reduce_dims(x, channel_last)
     dy = grad_out.float()
@@ -97,13 +125,21 @@ def reduce_bn(grad_out, x, mean, inv_std, weight, channel_last=False):
     return sum_dy, sum_dy_xmu, gw, gb
 
 
-def batchnorm_backward(grad_out, x, mean, inv_std, weight, sum_dy, sum_dy_xmu, count, channel_last=False):
+def batchnorm_backward(grad_out, x, mean, inv_std, weight, sum_dy, sum_dy_xmu, count, channel_last=False, z=None,
+                       bias=None, fuse_relu=False):
     """dx given the (globally reduced) sums; ``count`` = per-rank element counts [world]."""
     if _native.use_native(x):
         m = _syncbn()
         c = count.to(torch.int32)
-        return m.batchnorm_backward_c_last(grad_out, x, mean, inv_std, weight, sum_dy, sum_dy_xmu, c) if \
-            channel_last else m.batchnorm_backward(grad_out, x, mean, inv_std, weight, sum_dy, sum_dy_xmu, c)
+        x = x.contiguous()
+        if channel_last:
+            return m.batchnorm_backward_c_last(grad_out, x, mean, inv_std, weight, sum_dy, sum_dy_xmu, c, _c(z), bias,
+                                               fuse_relu)
+        if fuse_relu:
+            grad_out = relu_backward(grad_out, x, z, mean, inv_std, weight, bias, False)
+        return m.batchnorm_backward(grad_out.contiguous(), x, mean, inv_std, weight, sum_dy, sum_dy_xmu, c)
+    if fuse_relu:
+        grad_out = relu_backward(grad_out, x, z, mean, inv_std, weight, bias, channel_last)
     shp = _bshape(x, channel_last)
     n = float(count.sum())
     dy = grad_out.float()

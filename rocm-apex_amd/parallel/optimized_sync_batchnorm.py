@@ -72,20 +72,26 @@ class SyncBatchnormFunction(Function):
         saved_input, weight, mean, inv_std, z, bias, count = ctx.saved_tensors
         channel_last = ctx.channel_last
         grad_input = grad_z = grad_weight = grad_bias = None
-        if ctx.fuse_relu:
-            grad_output = bnops.relu_backward(grad_output, saved_input, z, mean, inv_std, weight, bias, channel_last)
-        if isinstance(z, torch.Tensor) and ctx.needs_input_grad[1]:
+        relu = ctx.fuse_relu
+        zz = z if isinstance(z, torch.Tensor) else None
+        if relu and zz is not None and ctx.needs_input_grad[1]:
+            # the residual branch needs the masked gradient itself: materialize it once
+            grad_output = bnops.relu_backward(grad_output, saved_input, zz, mean, inv_std, weight, bias, channel_last)
+            grad_z = grad_output
+            relu = False
+        elif zz is not None and ctx.needs_input_grad[1]:
             grad_z = grad_output.clone()
+        # with `relu` still set, the kernels mask dy by the recomputed output in registers
         sum_dy, sum_dy_xmu, grad_weight, grad_bias = bnops.reduce_bn(grad_output, saved_input, mean, inv_std, weight,
-                                                                     channel_last)
+                                                                     channel_last, zz, bias, relu)
         if ctx.needs_input_grad[0]:
-            if dist.is_available() and dist.is_initialized():
+            if dist.is_available() and dist.is_initialized() and ctx.world_size > 0:
                 c = sum_dy.shape[0]
                 combined = torch.cat([sum_dy, sum_dy_xmu], dim=0)
                 dist.all_reduce(combined, dist.ReduceOp.SUM, ctx.process_group, async_op=False)
                 sum_dy, sum_dy_xmu = torch.split(combined, c)
             grad_input = bnops.batchnorm_backward(grad_output, saved_input, mean, inv_std, weight, sum_dy, sum_dy_xmu,
-                                                  count, channel_last)
+                                                  count, channel_last, zz, bias, relu)
         if weight is None or not ctx.needs_input_grad[2]:
             grad_weight = None
         if weight is None or not ctx.needs_input_grad[3]:
@@ -119,7 +125,17 @@ class SyncBatchNorm(_BatchNorm):
 
     def forward(self, input, z=None):
         self._check_input_dim(input)
+        if (not self.channel_last and input.dim() == 4 and not input.is_contiguous()
+                and input.is_contiguous(memory_format=torch.channels_last)):
+            # torch channels_last memory: run the c_last kernels on a zero-copy NHWC view and
+            # hand back an NCHW-shaped, channels_last-strided result
+            zv = z.permute(0, 2, 3, 1) if z is not None else None
+            out = self._forward_impl(input.permute(0, 2, 3, 1), zv, True)
+            return out.permute(0, 3, 1, 2)
         channel_last = self.channel_last if input.dim() != 2 else True
+        return self._forward_impl(input, z, channel_last)
+
+    def _forward_impl(self, input, z, channel_last):
         if (not self.training and self.track_running_stats and not channel_last and not self.fuse_relu
                 and z is None):
             return F.batch_norm(input, self.running_mean, self.running_var, self.weight, self.bias, False, 0.0,

@@ -15,12 +15,12 @@ import sqlite3
 import sys
 
 CATEGORIES = [
-    ("apex_amd (native gfx950)", re.compile(r"apex_amd|mta_|ln_fwd|ln_bwd|softmax_|welford|bn_|_gemm_|attn_|xent")),
-    ("MIOpen conv", re.compile(r"miopen|igemm|naive_conv|Conv|conv|batched_transpose|Sp3Asm|gridwise", re.I)),
-    ("BLAS (hipBLASLt/rocBLAS/Tensile)", re.compile(r"Cijk_|Tensile|hipblaslt|rocblas|gemm", re.I)),
-    ("batchnorm (MIOpen/torch)", re.compile(r"batchnorm|BatchNorm|bn_fwd|bn_bwd|MIOpenBatchNorm", re.I)),
+    ("apex_amd (native gfx950)", re.compile(r"apex_amd::")),
+    ("batchnorm (MIOpen)", re.compile(r"BatchNorm", re.I)),
     ("RCCL", re.compile(r"nccl|rccl", re.I)),
-    ("torch elementwise/reduce", re.compile(r"at::native|elementwise|reduce_kernel|vectorized", re.I)),
+    ("conv (MIOpen igemm / CK)", re.compile(r"igemm|naive_conv|conv|gridwise|ck::|ck16", re.I)),
+    ("BLAS (hipBLASLt/rocBLAS/Tensile)", re.compile(r"Cijk_|Tensile|hipblaslt|rocblas", re.I)),
+    ("torch elementwise/reduce", re.compile(r"at::native", re.I)),
 ]
 
 
