@@ -40,6 +40,9 @@ def parse():
     ap.add_argument("--materialize-master-grads", action="store_true",
                     help="reference-style unscale into fp32 master grads (slower path)")
     ap.add_argument("--sync-bn", action="store_true")
+    ap.add_argument("--bn", default="fused", choices=["fused", "torch"],
+                    help="fused: apex.contrib.groupbn NHWC BN with fused ReLU / add+ReLU (gfx950 kernels); "
+                         "torch: nn.BatchNorm2d + ReLU (MIOpen)")
     ap.add_argument("--lr", type=float, default=1e-3)
     ap.add_argument("--impl", default="apex", choices=["apex", "torch"],
                     help="torch = stock PyTorch-ROCm baseline (autocast bf16 + AdamW(fused) + torch DDP)")
@@ -68,7 +71,8 @@ def main():
     torch.manual_seed(1234 + rank)
     if args.impl == "torch":
         return run_torch_baseline(args, dev, world, rank, distributed, resnet_mod)
-    model = getattr(resnet_mod, args.arch)()
+    fused_bn = args.bn == "fused" and not (args.sync_bn and distributed) and not args.no_channels_last
+    model = getattr(resnet_mod, args.arch)(fused_bn=fused_bn)
     if args.sync_bn and distributed:
         model = apex.parallel.convert_syncbn_model(model, channel_last=not args.no_channels_last)
     model = model.to(dev)
@@ -181,6 +185,8 @@ def timed(args, step, dev, world, rank, distributed, B, impl):
                 if impl == "apex" else "torch.optim.AdamW(fused=True)",
                 "channels_last": not args.no_channels_last,
                 "sync_bn": bool(args.sync_bn and distributed),
+                "batchnorm": ("apex fused NHWC BN+ReLU/add+ReLU (gfx950)" if (impl == "apex" and args.bn == "fused"
+                              and not args.no_channels_last) else "torch BatchNorm2d (MIOpen)"),
                 "parallelism": f"dp{world}",
                 "final_loss": round(float(loss.item()), 4),
             },

@@ -1,0 +1,119 @@
+// pybind surface of the fused NHWC batch norm: submodule ``_C.bn_nhwc`` used by
+// apex.contrib.groupbn.BatchNorm2d_NHWC and apex.models' fused ResNet blocks.  Tensors are the
+// dense [M, C] views of NHWC activations (the python layer builds them zero-copy).
+#include "common.h"
+#include "apex_amd/bn_nhwc_api.h"
+
+namespace apex_amd {
+
+namespace {
+
+using OT = c10::optional<at::Tensor>;
+bool has(const OT& t) { return t.has_value() && t->defined(); }
+const float* fptr(const OT& t) { return has(t) ? t->data_ptr<float>() : nullptr; }
+float* fptr_mut(const OT& t) { return has(t) ? t->data_ptr<float>() : nullptr; }
+
+void check2d(const at::Tensor& x, const char* what) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.is_contiguous(), "bn_nhwc: ", what, " must be a contiguous [M, C] GPU tensor");
+  TORCH_CHECK(x.size(1) % 8 == 0, "bn_nhwc: C must be a multiple of 8");
+  TORCH_CHECK(((uintptr_t)x.data_ptr() & 15u) == 0, "bn_nhwc: ", what, " must be 16-byte aligned");
+}
+
+void check_param(const OT& t, int64_t c) {
+  if (!has(t)) return;
+  TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() == c && t->is_contiguous(),
+              "bn_nhwc: weight/bias/running stats must be contiguous fp32 [C]");
+}
+
+std::vector<at::Tensor> fwd_train(at::Tensor x, OT z, OT w, OT b, OT running_mean, OT running_var, double momentum,
+                                  double eps, bool relu) {
+  check2d(x, "input");
+  const c10::hip::HIPGuard g(x.get_device());
+  const int64_t m = x.size(0);
+  const int c = (int)x.size(1);
+  for (const OT* p : {&w, &b, &running_mean, &running_var}) check_param(*p, c);
+  if (has(z)) {
+    check2d(*z, "z");
+    TORCH_CHECK(z->sizes() == x.sizes() && z->scalar_type() == x.scalar_type(), "bn_nhwc: z must match input");
+  }
+  const int cus = device_cus(x.get_device());
+  int64_t wsf = 0;
+  const int gy = bn_nhwc_plan(m, c, cus, &wsf);
+  auto fo = x.options().dtype(at::kFloat);
+  auto ws = at::empty({wsf}, fo);
+  auto save_mean = at::empty({c}, fo), save_invstd = at::empty({c}, fo), coef = at::empty({2, c}, fo);
+  auto y = at::empty_like(x);
+  const int dt = dtype_code(x.scalar_type());
+  bn_nhwc_stats(x.data_ptr(), dt, m, c, fptr(w), fptr(b), (float)eps, (float)momentum, fptr_mut(running_mean),
+                fptr_mut(running_var), save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
+                coef.data_ptr<float>(), ws.data_ptr<float>(), gy, cus, cur_stream());
+  bn_nhwc_apply(x.data_ptr(), dt, has(z) ? z->data_ptr() : nullptr, coef.data_ptr<float>(), relu, y.data_ptr(), m, c,
+                cus, cur_stream());
+  return {y, save_mean, save_invstd, coef};
+}
+
+at::Tensor fwd_eval(at::Tensor x, OT z, OT w, OT b, at::Tensor running_mean, at::Tensor running_var, double eps,
+                    bool relu) {
+  check2d(x, "input");
+  const c10::hip::HIPGuard g(x.get_device());
+  const int64_t m = x.size(0);
+  const int c = (int)x.size(1);
+  for (const OT* p : {&w, &b}) check_param(*p, c);
+  check_param(running_mean, c);
+  check_param(running_var, c);
+  auto coef = at::empty({2, c}, x.options().dtype(at::kFloat));
+  bn_nhwc_coef_from_stats(running_mean.data_ptr<float>(), running_var.data_ptr<float>(), true, fptr(w), fptr(b),
+                          (float)eps, c, coef.data_ptr<float>(), cur_stream());
+  auto y = at::empty_like(x);
+  bn_nhwc_apply(x.data_ptr(), dtype_code(x.scalar_type()), has(z) ? z->data_ptr() : nullptr, coef.data_ptr<float>(),
+                relu, y.data_ptr(), m, c, device_cus(x.get_device()), cur_stream());
+  return y;
+}
+
+std::vector<at::Tensor> bwd(at::Tensor dy_, at::Tensor x, OT z, OT w, at::Tensor save_mean, at::Tensor save_invstd,
+                            at::Tensor coef_fwd, bool relu, bool need_dz) {
+  check2d(x, "input");
+  const c10::hip::HIPGuard g(x.get_device());
+  at::Tensor dy = dy_.contiguous();
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "bn_nhwc: grad must match input");
+  const int64_t m = x.size(0);
+  const int c = (int)x.size(1);
+  const int cus = device_cus(x.get_device());
+  int64_t wsf = 0;
+  const int gy = bn_nhwc_plan(m, c, cus, &wsf);
+  auto fo = x.options().dtype(at::kFloat);
+  auto ws = at::empty({wsf}, fo);
+  auto gw = at::empty({c}, fo), gb = at::empty({c}, fo), coef_bwd = at::empty({3, c}, fo);
+  const bool has_z = has(z);
+  // the residual branch needs the masked gradient itself (grad_z); without it the mask is
+  // recomputed in registers by both passes
+  at::Tensor dz;
+  if (relu && need_dz) dz = at::empty_like(x);
+  const int dt = dtype_code(x.scalar_type());
+  bn_nhwc_bwd_reduce(dy.data_ptr(), x.data_ptr(), dt, has_z ? z->data_ptr() : nullptr, coef_fwd.data_ptr<float>(),
+                     relu, save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(), fptr(w), gw.data_ptr<float>(),
+                     gb.data_ptr<float>(), coef_bwd.data_ptr<float>(), dz.defined() ? dz.data_ptr() : nullptr, m, c,
+                     ws.data_ptr<float>(), gy, cus, cur_stream());
+  auto dx = at::empty_like(x);
+  if (dz.defined()) {
+    bn_nhwc_bwd_apply(dz.data_ptr(), true, x.data_ptr(), dt, nullptr, coef_fwd.data_ptr<float>(), relu,
+                      coef_bwd.data_ptr<float>(), dx.data_ptr(), m, c, cus, cur_stream());
+  } else {
+    bn_nhwc_bwd_apply(dy.data_ptr(), false, x.data_ptr(), dt, has_z ? z->data_ptr() : nullptr,
+                      coef_fwd.data_ptr<float>(), relu, coef_bwd.data_ptr<float>(), dx.data_ptr(), m, c, cus,
+                      cur_stream());
+    if (need_dz) dz = dy;  // no ReLU: d(z) = dy
+  }
+  return {dx, dz, gw, gb};
+}
+
+}  // namespace
+
+void bind_bn_nhwc(pybind11::module_& root) {
+  auto m = root.def_submodule("bn_nhwc", "gfx950 fused NHWC batch norm (+add+ReLU)");
+  m.def("fwd_train", &fwd_train);
+  m.def("fwd_eval", &fwd_eval);
+  m.def("bwd", &bwd);
+}
+
+}  // namespace apex_amd

@@ -11,6 +11,7 @@ void bind_gemm(pybind11::module_& m);
 void bind_xentropy(pybind11::module_& m);
 void bind_attn(pybind11::module_& m);
 void bind_contrib(pybind11::module_& m);
+void bind_bn_nhwc(pybind11::module_& m);
 }  // namespace apex_amd
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -34,6 +35,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 #endif
 #ifdef APEX_AMD_WITH_ATTN
   apex_amd::bind_attn(m);
+#endif
+#ifdef APEX_AMD_WITH_BN_NHWC
+  apex_amd::bind_bn_nhwc(m);
 #endif
 #ifdef APEX_AMD_WITH_CONTRIB
   apex_amd::bind_contrib(m);

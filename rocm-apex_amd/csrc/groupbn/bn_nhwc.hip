@@ -1,0 +1,447 @@
+// Fused NHWC batch norm (+ residual add + ReLU) for gfx950: the engine behind
+// apex.contrib.groupbn.BatchNorm2d_NHWC and the fused ResNet blocks.
+//
+// Reference: apex/contrib/csrc/groupbn/nhwc_batch_norm_kernel.h (persistent-CTA NHWC BN with
+// an in-kernel grid sync and a bitmask for the fused ReLU), batch_norm.cu :44/:143/:226,
+// batch_norm_add_relu.cu.
+//
+// MI355X design (no grid-wide sync, no persistent CTAs, deterministic):
+//  forward   1. stats_partial : every lane owns 8 channels (one 16-byte load per row), keeps
+//               4 rows in flight, accumulates pivot-shifted sums (s, s^2) -> per-lane (mean, M2);
+//               Chan-merged across the block's row-groups in LDS -> one partial per block
+//            2. stats_finalize: merges partials in a fixed order, writes mean / inv_std, the
+//               running-stat EMA and the epilogue constants scale/shift (one launch per layer)
+//            3. apply         : y = relu(x*scale + shift + z) — one FMA per element, 16-byte I/O
+//  backward  1. bwd_partial   : sum(dy'), sum(dy'*(x-mean)) with dy' = dy masked by the ReLU
+//               output recomputed in registers (never stored unless the residual branch needs
+//               it as grad_z, then written here in the same pass)
+//            2. bwd_finalize  : grad_w, grad_b and dx = A*dy' + B*x + K constants
+//            3. bwd_apply     : dx in one FMA pair per element
+// Passes over the activation per layer: fwd 3 (x, x, y) [+z], bwd 5 (dy, x, dy, x, dx) — vs
+// 5 / 8 for MIOpen BN + separate ReLU / threshold-backward kernels.
+#include "apex_amd/bn_nhwc_api.h"
+#include "apex_amd/device.h"
+#include "apex_amd/dispatch.h"
+
+#include <type_traits>
+
+namespace apex_amd {
+namespace bnh {
+
+constexpr int kU = 4;  // rows in flight per lane
+
+struct Geo {
+  int tx, ty, gx, gy;
+};
+
+inline Geo geo(int64_t m, int c, int cus) {
+  Geo g;
+  const int cv = c / 8;
+  g.tx = cv < 64 ? cv : 64;
+  g.ty = 256 / g.tx;
+  if (g.ty > 32) g.ty = 32;
+  g.gx = (cv + g.tx - 1) / g.tx;
+  const int64_t rows_per_iter = (int64_t)g.ty * kU;
+  int64_t gy = ((int64_t)cus * 4 + g.gx - 1) / g.gx;
+  const int64_t cap = (m + rows_per_iter - 1) / rows_per_iter;
+  if (gy > cap) gy = cap;
+  if (gy > 1024) gy = 1024;
+  g.gy = (int)(gy < 1 ? 1 : gy);
+  return g;
+}
+
+__device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float mb, float m2b) {
+  if (nb == 0.f) return;
+  const float nn = n + nb;
+  const float d = mb - mean;
+  const float f = nb / nn;
+  mean += d * f;
+  m2 += m2b + d * d * n * f;
+  n = nn;
+}
+
+__device__ __forceinline__ void load8f(float (&v)[8], const float* p) { Vec8<float>::load(v, p); }
+
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) stats_partial(const T* __restrict__ x, int64_t m, int c,
+                                                     float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int TX = blockDim.x, TY = blockDim.y, tx = threadIdx.x, ty = threadIdx.y;
+  const int c0 = (blockIdx.x * TX + tx) * 8;
+  const bool active = c0 < c;
+  float piv[8], s[8], ss[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) piv[k] = s[k] = ss[k] = 0.f;
+  float n = 0.f;
+  const int64_t R = (int64_t)TY * kU;
+  for (int64_t base = (int64_t)blockIdx.y * R; base < m; base += R * gridDim.y) {
+    float v[kU][8];
+    bool ok[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t r = base + ty + (int64_t)u * TY;
+      ok[u] = active && r < m;
+      if (ok[u]) Vec8<T>::load(v[u], x + r * c + c0);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (!ok[u]) continue;
+      if (n == 0.f) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) piv[k] = v[u][k];
+      }
+      n += 1.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float d = v[u][k] - piv[k];
+        s[k] += d;
+        ss[k] += d * d;
+      }
+    }
+  }
+  const int W = TX * 8;
+  float* sm = smem;
+  float* s2 = smem + TY * W;
+  float* sn = smem + 2 * TY * W;
+  if (active) {
+    const float inv = n > 0.f ? 1.f / n : 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sm[ty * W + tx * 8 + k] = piv[k] + s[k] * inv;
+      s2[ty * W + tx * 8 + k] = fmaxf(ss[k] - s[k] * s[k] * inv, 0.f);
+    }
+  }
+  if (tx == 0) sn[ty] = n;
+  __syncthreads();
+  if (ty == 0 && active) {
+    const int gy = gridDim.y;
+    float tot = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float nn = sn[0], mm = sm[tx * 8 + k], MM = s2[tx * 8 + k];
+      for (int j = 1; j < TY; ++j) chan_merge(nn, mm, MM, sn[j], sm[j * W + tx * 8 + k], s2[j * W + tx * 8 + k]);
+      part[(int64_t)blockIdx.y * c + c0 + k] = mm;
+      part[(int64_t)gy * c + (int64_t)blockIdx.y * c + c0 + k] = MM;
+      tot = nn;
+    }
+    if (blockIdx.x == 0 && tx == 0) part[2 * (int64_t)gy * c + blockIdx.y] = tot;
+  }
+}
+
+// block (64 channels x 4 partial-groups); fixed merge order => deterministic
+__global__ void __launch_bounds__(256) stats_finalize(const float* __restrict__ part, int gy, int c,
+                                                      const float* __restrict__ w, const float* __restrict__ b,
+                                                      float eps, float momentum, float* __restrict__ rmean,
+                                                      float* __restrict__ rvar, float* __restrict__ save_mean,
+                                                      float* __restrict__ save_invstd, float* __restrict__ coef) {
+  __shared__ float sn[4][64], sm[4][64], s2[4][64];
+  const int cx = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int ch = blockIdx.x * 64 + cx;
+  float n = 0.f, mm = 0.f, MM = 0.f;
+  if (ch < c)
+    for (int j = g; j < gy; j += 4) chan_merge(n, mm, MM, part[2 * (int64_t)gy * c + j], part[(int64_t)j * c + ch],
+                                              part[(int64_t)(gy + j) * c + ch]);
+  sn[g][cx] = n;
+  sm[g][cx] = mm;
+  s2[g][cx] = MM;
+  __syncthreads();
+  if (g != 0 || ch >= c) return;
+  for (int j = 1; j < 4; ++j) chan_merge(n, mm, MM, sn[j][cx], sm[j][cx], s2[j][cx]);
+  const float var_b = n > 0.f ? MM / n : 0.f;
+  const float istd = rsqrtf(var_b + eps);
+  save_mean[ch] = mm;
+  save_invstd[ch] = istd;
+  const float sc = istd * (w ? w[ch] : 1.f);
+  coef[ch] = sc;
+  coef[c + ch] = (b ? b[ch] : 0.f) - mm * sc;
+  if (rmean) rmean[ch] = (1.f - momentum) * rmean[ch] + momentum * mm;
+  if (rvar) rvar[ch] = (1.f - momentum) * rvar[ch] + momentum * (n > 1.f ? MM / (n - 1.f) : var_b);
+}
+
+__global__ void coef_from_stats(const float* __restrict__ mean, const float* __restrict__ v, int is_var,
+                                const float* __restrict__ w, const float* __restrict__ b, float eps, int c,
+                                float* __restrict__ coef) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= c) return;
+  const float istd = is_var ? rsqrtf(v[ch] + eps) : v[ch];
+  const float sc = istd * (w ? w[ch] : 1.f);
+  coef[ch] = sc;
+  coef[c + ch] = (b ? b[ch] : 0.f) - mean[ch] * sc;
+}
+
+// ------------------------------------------------------------------------------------------
+template <typename T, bool HAS_Z, bool RELU>
+__global__ void __launch_bounds__(256) apply_kernel(const T* __restrict__ x, const T* __restrict__ z,
+                                                    const float* __restrict__ coef, T* __restrict__ y, int64_t nvec,
+                                                    int c) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    const int64_t e = i * 8;
+    const int c0 = (int)(e % c);
+    float v[8], sc[8], sh[8];
+    Vec8<T>::load(v, x + e);
+    load8f(sc, coef + c0);
+    load8f(sh, coef + c + c0);
+    float zz[8];
+    if constexpr (HAS_Z) Vec8<T>::load(zz, z + e);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float o = fmaf(v[k], sc[k], sh[k]);
+      if constexpr (HAS_Z) o += zz[k];
+      if constexpr (RELU) o = fmaxf(o, 0.f);
+      v[k] = o;
+    }
+    Vec8<T>::store(y + e, v);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+template <typename T, bool HAS_Z, bool RELU, bool WRITE_MASKED>
+__global__ void __launch_bounds__(256) bwd_partial(const T* __restrict__ dy, const T* __restrict__ x,
+                                                   const T* __restrict__ z, const float* __restrict__ coef,
+                                                   const float* __restrict__ mean, T* __restrict__ dym, int64_t m,
+                                                   int c, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int TX = blockDim.x, TY = blockDim.y, tx = threadIdx.x, ty = threadIdx.y;
+  const int c0 = (blockIdx.x * TX + tx) * 8;
+  const bool active = c0 < c;
+  float a1[8], a2[8], mu[8], sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a1[k] = a2[k] = 0.f;
+  if (active) {
+    load8f(mu, mean + c0);
+    if constexpr (RELU) {
+      load8f(sc, coef + c0);
+      load8f(sh, coef + c + c0);
+    }
+  }
+  const int64_t R = (int64_t)TY * kU;
+  for (int64_t base = (int64_t)blockIdx.y * R; base < m; base += R * gridDim.y) {
+    float g[kU][8], v[kU][8];
+    bool ok[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t r = base + ty + (int64_t)u * TY;
+      ok[u] = active && r < m;
+      if (ok[u]) {
+        Vec8<T>::load(g[u], dy + r * c + c0);
+        Vec8<T>::load(v[u], x + r * c + c0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (!ok[u]) continue;
+      const int64_t e = (base + ty + (int64_t)u * TY) * c + c0;
+      if constexpr (RELU) {
+        float zz[8];
+        if constexpr (HAS_Z) Vec8<T>::load(zz, z + e);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float o = fmaf(v[u][k], sc[k], sh[k]);
+          if constexpr (HAS_Z) o += zz[k];
+          if (!(o > 0.f)) g[u][k] = 0.f;
+        }
+        if constexpr (WRITE_MASKED) Vec8<T>::store(dym + e, g[u]);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        a1[k] += g[u][k];
+        a2[k] = fmaf(g[u][k], v[u][k] - mu[k], a2[k]);
+      }
+    }
+  }
+  const int W = TX * 8;
+  if (active) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      smem[ty * W + tx * 8 + k] = a1[k];
+      smem[TY * W + ty * W + tx * 8 + k] = a2[k];
+    }
+  }
+  __syncthreads();
+  if (ty == 0 && active) {
+    const int gy = gridDim.y;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float p = 0.f, q = 0.f;
+      for (int j = 0; j < TY; ++j) {
+        p += smem[j * W + tx * 8 + k];
+        q += smem[TY * W + j * W + tx * 8 + k];
+      }
+      part[(int64_t)blockIdx.y * c + c0 + k] = p;
+      part[(int64_t)gy * c + (int64_t)blockIdx.y * c + c0 + k] = q;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) bwd_finalize(const float* __restrict__ part, int gy, int c, float inv_n,
+                                                    const float* __restrict__ mean, const float* __restrict__ istd,
+                                                    const float* __restrict__ w, float* __restrict__ gw,
+                                                    float* __restrict__ gb, float* __restrict__ coef) {
+  __shared__ float r1[4][64], r2[4][64];
+  const int cx = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int ch = blockIdx.x * 64 + cx;
+  float a = 0.f, q = 0.f;
+  if (ch < c)
+    for (int j = g; j < gy; j += 4) {
+      a += part[(int64_t)j * c + ch];
+      q += part[(int64_t)(gy + j) * c + ch];
+    }
+  r1[g][cx] = a;
+  r2[g][cx] = q;
+  __syncthreads();
+  if (g != 0 || ch >= c) return;
+  const float sdy = ((r1[0][cx] + r1[1][cx]) + r1[2][cx]) + r1[3][cx];
+  const float sdyx = ((r2[0][cx] + r2[1][cx]) + r2[2][cx]) + r2[3][cx];
+  const float is = istd[ch];
+  if (gw) gw[ch] = sdyx * is;
+  if (gb) gb[ch] = sdy;
+  const float A = is * (w ? w[ch] : 1.f);
+  const float B = -A * is * is * (sdyx * inv_n);
+  coef[ch] = A;
+  coef[c + ch] = B;
+  coef[2 * c + ch] = -A * (sdy * inv_n) - B * mean[ch];
+}
+
+template <typename T, bool HAS_Z, bool MASK>
+__global__ void __launch_bounds__(256) bwd_apply(const T* __restrict__ dy, const T* __restrict__ x,
+                                                 const T* __restrict__ z, const float* __restrict__ cf,
+                                                 const float* __restrict__ cb, T* __restrict__ dx, int64_t nvec,
+                                                 int c) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    const int64_t e = i * 8;
+    const int c0 = (int)(e % c);
+    float g[8], v[8], A[8], B[8], K[8];
+    Vec8<T>::load(g, dy + e);
+    Vec8<T>::load(v, x + e);
+    load8f(A, cb + c0);
+    load8f(B, cb + c + c0);
+    load8f(K, cb + 2 * c + c0);
+    if constexpr (MASK) {
+      float sc[8], sh[8], zz[8];
+      load8f(sc, cf + c0);
+      load8f(sh, cf + c + c0);
+      if constexpr (HAS_Z) Vec8<T>::load(zz, z + e);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float o = fmaf(v[k], sc[k], sh[k]);
+        if constexpr (HAS_Z) o += zz[k];
+        if (!(o > 0.f)) g[k] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = fmaf(A[k], g[k], fmaf(B[k], v[k], K[k]));
+    Vec8<T>::store(dx + e, v);
+  }
+}
+
+inline unsigned ew_grid(int64_t nvec, int cus) {
+  int64_t g = (nvec + 255) / 256;
+  const int64_t cap = (int64_t)cus * 8;
+  if (g > cap) g = cap;
+  return (unsigned)(g < 1 ? 1 : g);
+}
+
+inline void check_shape(int64_t m, int c) {
+  if (c % 8 != 0 || c <= 0 || m <= 0) throw std::runtime_error("bn_nhwc: C must be a positive multiple of 8");
+}
+
+}  // namespace bnh
+
+int bn_nhwc_plan(int64_t m, int c, int cus, int64_t* ws_floats) {
+  const bnh::Geo g = bnh::geo(m, c, cus);
+  if (ws_floats) *ws_floats = 2 * (int64_t)g.gy * c + g.gy;
+  return g.gy;
+}
+
+void bn_nhwc_stats(const void* x, int x_t, int64_t m, int c, const float* w, const float* b, float eps, float momentum,
+                   float* running_mean, float* running_var, float* save_mean, float* save_invstd, float* coef_fwd,
+                   float* ws, int gy, int cus, hipStream_t s) {
+  bnh::check_shape(m, c);
+  bnh::Geo g = bnh::geo(m, c, cus);
+  g.gy = gy;
+  const size_t lds = ((size_t)2 * g.ty * g.tx * 8 + g.ty) * sizeof(float);
+  dispatch_float(x_t, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    hipLaunchKernelGGL((bnh::stats_partial<T>), dim3(g.gx, g.gy), dim3(g.tx, g.ty), lds, s, (const T*)x, m, c, ws);
+  }, "bn_nhwc stats");
+  hipLaunchKernelGGL(bnh::stats_finalize, dim3((c + 63) / 64), dim3(256), 0, s, ws, g.gy, c, w, b, eps, momentum,
+                     running_mean, running_var, save_mean, save_invstd, coef_fwd);
+  check_launch("bn_nhwc_stats");
+}
+
+void bn_nhwc_coef_from_stats(const float* mean, const float* v, bool is_var, const float* w, const float* b, float eps,
+                             int c, float* coef_fwd, hipStream_t s) {
+  hipLaunchKernelGGL(bnh::coef_from_stats, dim3((c + 255) / 256), dim3(256), 0, s, mean, v, is_var ? 1 : 0, w, b, eps,
+                     c, coef_fwd);
+  check_launch("bn_nhwc_coef_from_stats");
+}
+
+void bn_nhwc_apply(const void* x, int x_t, const void* z, const float* coef_fwd, bool relu, void* y, int64_t m, int c,
+                   int cus, hipStream_t s) {
+  bnh::check_shape(m, c);
+  const int64_t nvec = m * c / 8;
+  const unsigned grid = bnh::ew_grid(nvec, cus);
+  dispatch_float(x_t, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    auto go = [&](auto hz, auto rl) {
+      hipLaunchKernelGGL((bnh::apply_kernel<T, decltype(hz)::value, decltype(rl)::value>), dim3(grid), dim3(256), 0, s,
+                         (const T*)x, (const T*)z, coef_fwd, (T*)y, nvec, c);
+    };
+    if (z) {
+      if (relu) go(std::true_type{}, std::true_type{});
+      else go(std::true_type{}, std::false_type{});
+    } else {
+      if (relu) go(std::false_type{}, std::true_type{});
+      else go(std::false_type{}, std::false_type{});
+    }
+  }, "bn_nhwc apply");
+  check_launch("bn_nhwc_apply");
+}
+
+void bn_nhwc_bwd_reduce(const void* dy, const void* x, int x_t, const void* z, const float* coef_fwd, bool relu,
+                        const float* save_mean, const float* save_invstd, const float* w, float* grad_w, float* grad_b,
+                        float* coef_bwd, void* dy_masked_out, int64_t m, int c, float* ws, int gy, int cus,
+                        hipStream_t s) {
+  bnh::check_shape(m, c);
+  bnh::Geo g = bnh::geo(m, c, cus);
+  g.gy = gy;
+  const size_t lds = (size_t)2 * g.ty * g.tx * 8 * sizeof(float);
+  dispatch_float(x_t, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    auto go = [&](auto hz, auto rl, auto wm) {
+      hipLaunchKernelGGL((bnh::bwd_partial<T, decltype(hz)::value, decltype(rl)::value, decltype(wm)::value>),
+                         dim3(g.gx, g.gy), dim3(g.tx, g.ty), lds, s, (const T*)dy, (const T*)x, (const T*)z, coef_fwd,
+                         save_mean, (T*)dy_masked_out, m, c, ws);
+    };
+    if (!relu) go(std::false_type{}, std::false_type{}, std::false_type{});
+    else if (z && dy_masked_out) go(std::true_type{}, std::true_type{}, std::true_type{});
+    else if (z) go(std::true_type{}, std::true_type{}, std::false_type{});
+    else if (dy_masked_out) go(std::false_type{}, std::true_type{}, std::true_type{});
+    else go(std::false_type{}, std::true_type{}, std::false_type{});
+  }, "bn_nhwc bwd reduce");
+  hipLaunchKernelGGL(bnh::bwd_finalize, dim3((c + 63) / 64), dim3(256), 0, s, ws, g.gy, c, 1.f / (float)m, save_mean,
+                     save_invstd, w, grad_w, grad_b, coef_bwd);
+  check_launch("bn_nhwc_bwd_reduce");
+}
+
+void bn_nhwc_bwd_apply(const void* dy, bool dy_is_masked, const void* x, int x_t, const void* z, const float* coef_fwd,
+                       bool relu, const float* coef_bwd, void* dx, int64_t m, int c, int cus, hipStream_t s) {
+  bnh::check_shape(m, c);
+  const int64_t nvec = m * c / 8;
+  const unsigned grid = bnh::ew_grid(nvec, cus);
+  const bool mask = relu && !dy_is_masked;
+  dispatch_float(x_t, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    auto go = [&](auto hz, auto mk) {
+      hipLaunchKernelGGL((bnh::bwd_apply<T, decltype(hz)::value, decltype(mk)::value>), dim3(grid), dim3(256), 0, s,
+                         (const T*)dy, (const T*)x, (const T*)z, coef_fwd, coef_bwd, (T*)dx, nvec, c);
+    };
+    if (!mask) go(std::false_type{}, std::false_type{});
+    else if (z) go(std::true_type{}, std::true_type{});
+    else go(std::false_type{}, std::true_type{});
+  }, "bn_nhwc bwd apply");
+  check_launch("bn_nhwc_bwd_apply");
+}
+
+}  // namespace apex_amd

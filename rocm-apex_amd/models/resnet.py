@@ -3,7 +3,13 @@ headline ImageNet benchmark (reference examples/imagenet/main_amp.py uses torchv
 ``resnet50``; torchvision is not a dependency here, so the architecture is defined directly).
 
 Layout notes for MI355X: build with ``memory_format=torch.channels_last`` — MIOpen's NHWC
-convolution kernels and our NHWC batch-norm kernels are the fast path on gfx950."""
+convolution kernels and our NHWC batch-norm kernels are the fast path on gfx950.
+
+``fused_bn=True`` swaps every BatchNorm (+ReLU) (+residual add +ReLU) group for
+``apex.contrib.groupbn.BatchNorm2d_NHWC`` with the ReLU / add fused in (reference capability:
+apex/contrib/groupbn, the NHWC BN with fused add+ReLU used for ResNet-50).  Parameters, buffers
+and state_dict keys are identical to the torch.nn.BatchNorm2d model; the math is the same
+training-mode batch norm, computed by the gfx950 kernels in fewer HBM passes."""
 import torch
 import torch.nn as nn
 
@@ -19,23 +25,33 @@ def conv1x1(cin, cout, stride=1):
     return nn.Conv2d(cin, cout, kernel_size=1, stride=stride, bias=False)
 
 
+def _fused_bn(planes, relu):
+    from ..contrib.groupbn import BatchNorm2d_NHWC
+
+    return BatchNorm2d_NHWC(planes, fuse_relu=relu, torch_channels_last=True)
+
+
 class BasicBlock(nn.Module):
     expansion = 1
 
     def __init__(self, inplanes, planes, stride=1, downsample=None, groups=1, base_width=64, dilation=1,
-                 norm_layer=None):
+                 norm_layer=None, fused_bn=False):
         super().__init__()
         norm_layer = norm_layer or nn.BatchNorm2d
+        self.fused_bn = fused_bn
         self.conv1 = conv3x3(inplanes, planes, stride)
-        self.bn1 = norm_layer(planes)
+        self.bn1 = _fused_bn(planes, True) if fused_bn else norm_layer(planes)
         self.relu = nn.ReLU(inplace=True)
         self.conv2 = conv3x3(planes, planes)
-        self.bn2 = norm_layer(planes)
+        self.bn2 = _fused_bn(planes, True) if fused_bn else norm_layer(planes)
         self.downsample = downsample
         self.stride = stride
 
     def forward(self, x):
         identity = x if self.downsample is None else self.downsample(x)
+        if self.fused_bn:
+            out = self.bn1(self.conv1(x))
+            return self.bn2(self.conv2(out), identity)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.bn2(self.conv2(out))
         return self.relu(out + identity)
@@ -45,22 +61,28 @@ class Bottleneck(nn.Module):
     expansion = 4
 
     def __init__(self, inplanes, planes, stride=1, downsample=None, groups=1, base_width=64, dilation=1,
-                 norm_layer=None):
+                 norm_layer=None, fused_bn=False):
         super().__init__()
         norm_layer = norm_layer or nn.BatchNorm2d
+        self.fused_bn = fused_bn
         width = int(planes * (base_width / 64.0)) * groups
+        nl = (lambda c, relu: _fused_bn(c, relu)) if fused_bn else (lambda c, relu: norm_layer(c))  # noqa: E731
         self.conv1 = conv1x1(inplanes, width)
-        self.bn1 = norm_layer(width)
+        self.bn1 = nl(width, True)
         self.conv2 = conv3x3(width, width, stride, groups, dilation)
-        self.bn2 = norm_layer(width)
+        self.bn2 = nl(width, True)
         self.conv3 = conv1x1(width, planes * self.expansion)
-        self.bn3 = norm_layer(planes * self.expansion)
+        self.bn3 = nl(planes * self.expansion, True)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
         self.stride = stride
 
     def forward(self, x):
         identity = x if self.downsample is None else self.downsample(x)
+        if self.fused_bn:
+            out = self.bn1(self.conv1(x))
+            out = self.bn2(self.conv2(out))
+            return self.bn3(self.conv3(out), identity)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.relu(self.bn2(self.conv2(out)))
         out = self.bn3(self.conv3(out))
@@ -69,15 +91,16 @@ class Bottleneck(nn.Module):
 
 class ResNet(nn.Module):
     def __init__(self, block, layers, num_classes=1000, zero_init_residual=False, groups=1, width_per_group=64,
-                 norm_layer=None):
+                 norm_layer=None, fused_bn=False):
         super().__init__()
         self._norm_layer = norm_layer or nn.BatchNorm2d
+        self.fused_bn = fused_bn
         self.inplanes = 64
         self.dilation = 1
         self.groups = groups
         self.base_width = width_per_group
         self.conv1 = nn.Conv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
-        self.bn1 = self._norm_layer(self.inplanes)
+        self.bn1 = _fused_bn(self.inplanes, True) if fused_bn else self._norm_layer(self.inplanes)
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0])
@@ -104,18 +127,21 @@ class ResNet(nn.Module):
         norm_layer = self._norm_layer
         downsample = None
         if stride != 1 or self.inplanes != planes * block.expansion:
-            downsample = nn.Sequential(conv1x1(self.inplanes, planes * block.expansion, stride),
-                                       norm_layer(planes * block.expansion))
+            bn = _fused_bn(planes * block.expansion, False) if self.fused_bn else norm_layer(planes * block.expansion)
+            downsample = nn.Sequential(conv1x1(self.inplanes, planes * block.expansion, stride), bn)
         layers = [block(self.inplanes, planes, stride, downsample, self.groups, self.base_width, self.dilation,
-                        norm_layer)]
+                        norm_layer, fused_bn=self.fused_bn)]
         self.inplanes = planes * block.expansion
         for _ in range(1, blocks):
             layers.append(block(self.inplanes, planes, groups=self.groups, base_width=self.base_width,
-                                dilation=self.dilation, norm_layer=norm_layer))
+                                dilation=self.dilation, norm_layer=norm_layer, fused_bn=self.fused_bn))
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        if self.fused_bn:
+            x = self.maxpool(self.bn1(self.conv1(x)))
+        else:
+            x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)

@@ -26,7 +26,7 @@ class SyncBatchnormFunction(Function):
             num_channels = input.size(-1) if channel_last else input.size(1)
             count = input.numel() // num_channels
             mean, var_biased = bnops.welford_mean_var(input, channel_last)
-            if dist.is_available() and dist.is_initialized():
+            if process_group != "local" and dist.is_available() and dist.is_initialized():
                 pg = process_group if process_group else dist.group.WORLD
                 world_size = dist.get_world_size(pg)
                 count_t = torch.full((1,), float(count), dtype=mean.dtype, device=mean.device)

@@ -56,9 +56,9 @@ def _gather_along_last_dim(input_):
     if world_size == 1:
         return input_
     x = input_.contiguous()
-    buf = torch.empty((world_size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
-    torch.distributed.all_gather_into_tensor(buf, x, group=get_tensor_model_parallel_group())
-    return torch.cat(buf.unbind(0), dim=-1).contiguous()
+    buf = torch.empty(world_size * x.numel(), dtype=x.dtype, device=x.device)
+    torch.distributed.all_gather_into_tensor(buf, x.view(-1), group=get_tensor_model_parallel_group())
+    return torch.cat(buf.view((world_size,) + tuple(x.shape)).unbind(0), dim=-1).contiguous()
 
 
 def _gather_along_first_dim(input_):

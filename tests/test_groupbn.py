@@ -1,0 +1,137 @@
+"""BatchNorm2d_NHWC (fused BN / BN+ReLU / BN+add+ReLU) numerics.
+
+Model: reference apex/contrib/test/groupbn/test_groupbn.py (NHWC BN vs a torch reference, with
+and without the fused residual add + ReLU).  GPU tests compare the gfx950 pipeline against
+torch.nn.BatchNorm2d (+ add + ReLU) in fp32 math, including running statistics and the
+parameter gradients, and a fused-BN ResNet against the plain one."""
+import pytest
+import torch
+
+from apex.contrib.groupbn import BatchNorm2d_NHWC
+
+
+def _torch_ref(x, z, bn, relu):
+    y = bn(x)
+    if z is not None:
+        y = y + z
+    return torch.relu(y) if relu else y
+
+
+def test_cpu_nhwc_bn_add_relu_matches_torch():
+    torch.manual_seed(0)
+    x = torch.randn(4, 16, 6, 6).to(memory_format=torch.channels_last).requires_grad_(True)
+    z = torch.randn(4, 16, 6, 6).to(memory_format=torch.channels_last).requires_grad_(True)
+    m = BatchNorm2d_NHWC(16, fuse_relu=True, torch_channels_last=True)
+    ref = torch.nn.BatchNorm2d(16)
+    y = m(x, z)
+    xr = x.detach().clone().requires_grad_(True)
+    zr = z.detach().clone().requires_grad_(True)
+    yr = _torch_ref(xr, zr, ref, True)
+    torch.testing.assert_close(y, yr, atol=1e-5, rtol=1e-5)
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g)
+    torch.testing.assert_close(x.grad, xr.grad, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(z.grad, zr.grad, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(m.weight.grad, ref.weight.grad, atol=1e-4, rtol=1e-4)
+
+
+def test_cpu_fused_resnet_matches_plain():
+    from apex.models import resnet18
+
+    torch.manual_seed(0)
+    a = resnet18(num_classes=10)
+    b = resnet18(num_classes=10, fused_bn=True)
+    b.load_state_dict(a.state_dict())
+    x = torch.randn(4, 3, 64, 64).to(memory_format=torch.channels_last)
+    a, b = a.to(memory_format=torch.channels_last), b.to(memory_format=torch.channels_last)
+    torch.testing.assert_close(a(x), b(x), atol=2e-3, rtol=2e-3)
+
+
+SHAPES = [(8, 64, 56, 56), (16, 256, 14, 14), (4, 2048, 7, 7), (2, 24, 9, 9), (64, 128, 28, 28)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("mode", ["bn", "bn_relu", "bn_add_relu"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+def test_gpu_bn_nhwc(shape, mode, dtype):
+    import apex
+
+    assert apex._native.available()
+    torch.manual_seed(sum(shape))
+    c = shape[1]
+    relu = mode != "bn"
+    x = (torch.randn(*shape, device="cuda") * 2 + 0.5).to(dtype).to(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    z = None
+    if mode == "bn_add_relu":
+        z = torch.randn(*shape, device="cuda").to(dtype).to(memory_format=torch.channels_last).requires_grad_(True)
+    m = BatchNorm2d_NHWC(c, fuse_relu=relu, torch_channels_last=True).cuda()
+    ref = torch.nn.BatchNorm2d(c).cuda()
+    with torch.no_grad():
+        w = torch.rand(c) + 0.5
+        b = torch.randn(c) * 0.2
+        m.weight.copy_(w)
+        m.bias.copy_(b)
+        ref.weight.copy_(w)
+        ref.bias.copy_(b)
+    y = m(x, z)
+    assert y.dtype == dtype and y.shape == x.shape
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    xr = x.detach().float().requires_grad_(True)
+    zr = z.detach().float().requires_grad_(True) if z is not None else None
+    yr = _torch_ref(xr, zr, ref, relu)
+    tol = 2e-4 if dtype == torch.float32 else 4e-2
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    torch.testing.assert_close(m.running_mean, ref.running_mean, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(m.running_var, ref.running_var, atol=1e-3, rtol=1e-3)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=tol * 10, rtol=tol * 5)
+    if z is not None:
+        torch.testing.assert_close(z.grad.float(), zr.grad, atol=tol, rtol=tol)
+    gs = max(1.0, float(ref.weight.grad.abs().max()))
+    torch.testing.assert_close(m.weight.grad / gs, ref.weight.grad / gs, atol=tol * 5, rtol=tol * 5)
+    gs = max(1.0, float(ref.bias.grad.abs().max()))
+    torch.testing.assert_close(m.bias.grad / gs, ref.bias.grad / gs, atol=tol * 5, rtol=tol * 5)
+
+
+@pytest.mark.gpu
+def test_gpu_bn_nhwc_eval_and_deterministic():
+    torch.manual_seed(3)
+    x = torch.randn(32, 128, 14, 14, device="cuda").to(memory_format=torch.channels_last)
+    m = BatchNorm2d_NHWC(128, fuse_relu=True, torch_channels_last=True).cuda()
+    x.requires_grad_(True)
+    outs = []
+    for _ in range(2):
+        x.grad = None
+        m.zero_grad()
+        y = m(x)
+        y.backward(torch.ones_like(y))
+        outs.append((y.detach().clone(), x.grad.clone(), m.weight.grad.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    m.eval()
+    ref = torch.nn.BatchNorm2d(128).cuda().eval()
+    ref.load_state_dict(m.state_dict())
+    torch.testing.assert_close(m(x.detach()), torch.relu(ref(x.detach())), atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_gpu_fused_resnet50_step_matches_plain():
+    from apex.models import resnet50
+
+    torch.manual_seed(0)
+    a = resnet50(num_classes=100).cuda().to(memory_format=torch.channels_last)
+    b = resnet50(num_classes=100, fused_bn=True).cuda().to(memory_format=torch.channels_last)
+    b.load_state_dict(a.state_dict())
+    x = torch.randn(8, 3, 64, 64, device="cuda").to(memory_format=torch.channels_last)
+    ya, yb = a(x), b(x)
+    torch.testing.assert_close(yb, ya, atol=2e-3, rtol=2e-3)
+    ya.sum().backward()
+    yb.sum().backward()
+    for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
+        s = max(1.0, float(p.grad.abs().max()))
+        torch.testing.assert_close(q.grad / s, p.grad / s, atol=5e-3, rtol=5e-3, msg=n)

@@ -38,6 +38,7 @@ SUBSYSTEMS = {
     "xentropy.cpp": "APEX_AMD_WITH_XENTROPY",
     "attn.cpp": "APEX_AMD_WITH_ATTN",
     "contrib.cpp": "APEX_AMD_WITH_CONTRIB",
+    "bn_nhwc.cpp": "APEX_AMD_WITH_BN_NHWC",
 }
 
 
