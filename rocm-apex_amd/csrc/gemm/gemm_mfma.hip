@@ -1,0 +1,385 @@
+// gfx950 MFMA GEMM with fused bias / activation / activation-gradient epilogues.
+//
+// Reference: csrc/fused_dense_cuda.cu (cuBLASLt epilogues BIAS / GELU_AUX_BIAS / DGELU / BGRADB;
+// on ROCm the reference falls back to rocBLAS + a bias copy, never computes d_bias and returns
+// status 1 for the GeLU variants — :64-68, :1290, :1361-1495) and csrc/mlp_cuda.cu (rocBLAS GEMM
+// + separate bias/activation kernels, :528-1041).
+//
+// Kernel (one launch per GEMM):
+//  * 128 x 128 output tile per 256-thread workgroup (4 wave64s in 2 x 2, each 64 x 64 as 2 x 2
+//    v_mfma_f32_32x32x16 tiles -> 64 fp32 accumulators per lane), BK = 64.
+//  * global -> registers -> LDS staging, double-buffered: the next K-tile's 16-byte loads are
+//    issued before the current tile's MFMAs and written to the other LDS buffer after them
+//    (issue-early / write-late), one barrier per K-tile.
+//  * k-major operands: LDS rows padded to 144 B (row r starts at 16-B slot 9r mod 16) so the
+//    ds_read_b128 fragment reads of 16 different rows hit 16 different slots (conflict-free).
+//    m/n-major operands keep the global [k][row] image with 320-B rows (4 consecutive k-rows
+//    start 64 B apart) and are read with ds_read_b64_tr_b16 (hardware transpose), two reads per
+//    8-deep k fragment.
+//  * epilogue through LDS: fp32 accumulators are parked in a [128][132] fp32 tile, then every
+//    thread applies bias / activation / activation-gradient on 8 consecutive columns and writes
+//    16-byte vectors (and the 16-byte aux pre-activation for GeLU).
+//  * XCD-aware tile order: consecutive workgroups are dealt round-robin over the 8 XCDs, so the
+//    tile id is remapped to give every XCD a contiguous band of tiles (L2 reuse of A / B panels).
+#include "apex_amd/device.h"
+#include "apex_amd/dispatch.h"
+#include "apex_amd/gemm_api.h"
+
+namespace apex_amd {
+namespace gemm {
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int KSTR = BK + 8;    // k-major LDS row stride (elements) -> 144 B
+constexpr int MSTR = 128 + 32;  // m/n-major LDS row stride (elements) -> 320 B
+constexpr int CSTR = BN + 4;    // epilogue fp32 tile row stride (floats) -> 528 B
+
+template <bool KMAJ>
+constexpr int tile_elems() { return KMAJ ? BM * KSTR : BK * MSTR; }
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+struct Stage {
+  uint4 r[4];
+};
+
+// ---- global -> registers (16 B per load, zero fill outside the matrix) ----
+template <bool KMAJ>
+__device__ __forceinline__ void stage_load(Stage& s, const uint16_t* __restrict__ base, int64_t ld, int rows_total,
+                                           int k_total, int row0, int k0, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    bool ok;
+    const uint16_t* p;
+    if constexpr (KMAJ) {
+      const int row = (tid >> 3) + 32 * i, ch = tid & 7;
+      const int gr = row0 + row, gk = k0 + ch * 8;
+      ok = gr < rows_total && gk < k_total;
+      p = base + (int64_t)gr * ld + gk;
+    } else {
+      const int kr = (tid >> 4) + 16 * i, ch = tid & 15;
+      const int gk = k0 + kr, gc = row0 + ch * 8;
+      ok = gk < k_total && gc < rows_total;
+      p = base + (int64_t)gk * ld + gc;
+    }
+    s.r[i] = ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
+  }
+}
+
+// ---- registers -> LDS ----
+template <bool KMAJ>
+__device__ __forceinline__ void stage_store(const Stage& s, uint16_t* lds, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if constexpr (KMAJ) {
+      const int row = (tid >> 3) + 32 * i, ch = tid & 7;
+      *reinterpret_cast<uint4*>(lds + row * KSTR + ch * 8) = s.r[i];
+    } else {
+      const int kr = (tid >> 4) + 16 * i, ch = tid & 15;
+      *reinterpret_cast<uint4*>(lds + kr * MSTR + ch * 8) = s.r[i];
+    }
+  }
+}
+
+__device__ __forceinline__ s16x4 tr_read(const uint16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)((__attribute__((address_space(3))) uint16_t*)p));
+}
+
+// fragment of a 32-row subtile at k-step kk (16 deep): lane l gets rows rowbase + (l & 31),
+// k = 16 kk + 8 (l >> 5) + j, j = 0..7 (the v_mfma_f32_32x32x16 A/B operand map)
+template <bool KMAJ>
+__device__ __forceinline__ s16x8 frag(const uint16_t* lds, int rowbase, int kk, int lane) {
+  if constexpr (KMAJ) {
+    const int row = rowbase + (lane & 31);
+    const int k = kk * 16 + 8 * (lane >> 5);
+    return *reinterpret_cast<const s16x8*>(lds + row * KSTR + k);
+  } else {
+    const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+    const int rb = rowbase + 16 * (g & 1), kb = kk * 16 + 8 * (g >> 1);
+    const uint16_t* a0 = lds + (kb + q) * MSTR + rb + 4 * p;
+    const s16x4 lo = tr_read(a0);
+    const s16x4 hi = tr_read(a0 + 4 * MSTR);
+    return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ f32x16 mfma(s16x8 a, s16x8 b, f32x16 c);
+template <>
+__device__ __forceinline__ f32x16 mfma<bf16_t>(s16x8 a, s16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                 0, 0);
+}
+template <>
+__device__ __forceinline__ f32x16 mfma<f16_t>(s16x8 a, s16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                0);
+}
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+__device__ __forceinline__ float dgelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float u = k0 * (x + k1 * x * x * x);
+  const float t = tanhf(u);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
+}
+
+// XCD-aware, bijective remap of the linear workgroup id, then GROUP_M-grouped tile order
+__device__ __forceinline__ void tile_coords(int nwg, int tiles_m, int tiles_n, int& bm, int& bn) {
+  const int orig = blockIdx.x;
+  const int xcd = orig % 8, q = nwg / 8, r = nwg % 8;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  constexpr int GROUP_M = 8;
+  const int group = wgid / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gm = min(tiles_m - first_m, GROUP_M);
+  bm = first_m + (wgid % (GROUP_M * tiles_n)) % gm;
+  bn = (wgid % (GROUP_M * tiles_n)) / gm;
+}
+
+template <typename T, bool AK, bool BKM, int EPI>
+__global__ void __launch_bounds__(256, 2)
+gemm_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, T* __restrict__ C, int64_t lda,
+            int64_t ldb, int64_t ldc, int M, int N, int K, const T* __restrict__ bias, const T* __restrict__ aux_in,
+            T* __restrict__ aux_out) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  constexpr int TA = tile_elems<AK>(), TB = tile_elems<BKM>();
+  // buffer b: A tile at b*(TA+TB), B tile right after it
+  auto a_buf = [&](int b) { return lds + b * (TA + TB); };
+  auto b_buf = [&](int b) { return lds + b * (TA + TB) + TA; };
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  int bm, bn;
+  tile_coords(tiles_m * tiles_n, tiles_m, tiles_n, bm, bn);
+  const int row0 = bm * BM, col0 = bn * BN;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  Stage sa, sb;
+  stage_load<AK>(sa, A, lda, M, K, row0, 0, tid);
+  stage_load<BKM>(sb, B, ldb, N, K, col0, 0, tid);
+  stage_store<AK>(sa, a_buf(0), tid);
+  stage_store<BKM>(sb, b_buf(0), tid);
+  __syncthreads();
+
+  const int nk = (K + BK - 1) / BK;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      stage_load<AK>(sa, A, lda, M, K, row0, (kt + 1) * BK, tid);
+      stage_load<BKM>(sb, B, ldb, N, K, col0, (kt + 1) * BK, tid);
+    }
+    const uint16_t* a_t = a_buf(cur);
+    const uint16_t* b_t = b_buf(cur);
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      const s16x8 a0 = frag<AK>(a_t, wm * 64, kk, lane);
+      const s16x8 a1 = frag<AK>(a_t, wm * 64 + 32, kk, lane);
+      const s16x8 b0 = frag<BKM>(b_t, wn * 64, kk, lane);
+      const s16x8 b1 = frag<BKM>(b_t, wn * 64 + 32, kk, lane);
+      acc[0][0] = mfma<T>(a0, b0, acc[0][0]);
+      acc[0][1] = mfma<T>(a0, b1, acc[0][1]);
+      acc[1][0] = mfma<T>(a1, b0, acc[1][0]);
+      acc[1][1] = mfma<T>(a1, b1, acc[1][1]);
+    }
+    if (more) {
+      stage_store<AK>(sa, a_buf(cur ^ 1), tid);
+      stage_store<BKM>(sb, b_buf(cur ^ 1), tid);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: park fp32 accumulators in LDS, then 16-byte row-vector stores ----
+  float* cs = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rl = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int cl = wn * 64 + j * 32 + (lane & 31);
+        cs[rl * CSTR + cl] = acc[i][j][r];
+      }
+  __syncthreads();
+  const int ch = tid & 15;
+  const int gc = col0 + ch * 8;
+  if (gc >= N) return;
+  float bv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bv[e] = 0.f;
+  if (bias != nullptr) Vec8<T>::load(bv, bias + gc);
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int rl = (tid >> 4) + 16 * it;
+    const int gr = row0 + rl;
+    if (gr >= M) break;
+    float v[8];
+    const float4 lo = *reinterpret_cast<const float4*>(cs + rl * CSTR + ch * 8);
+    const float4 hi = *reinterpret_cast<const float4*>(cs + rl * CSTR + ch * 8 + 4);
+    v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+    v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+    const int64_t off = (int64_t)gr * ldc + gc;
+    if constexpr (EPI == kEpiNone) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bv[e];
+    } else if constexpr (EPI == kEpiGelu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bv[e];
+      if (aux_out != nullptr) Vec8<T>::store(aux_out + off, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
+    } else if constexpr (EPI == kEpiRelu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] + bv[e], 0.f);
+    } else if constexpr (EPI == kEpiSigmoid) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 1.f / (1.f + __expf(-(v[e] + bv[e])));
+    } else {
+      float a[8];
+      Vec8<T>::load(a, aux_in + off);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if constexpr (EPI == kEpiDGelu) v[e] *= dgelu_tanh(a[e]);
+        else if constexpr (EPI == kEpiDRelu) v[e] = a[e] > 0.f ? v[e] : 0.f;
+        else v[e] *= a[e] * (1.f - a[e]);
+      }
+    }
+    Vec8<T>::store(C + off, v);
+  }
+}
+
+// ---- column sums (bias gradients): partial [P][N] then fixed-order finalize ----
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_partial(const T* __restrict__ x, int64_t m, int n, int64_t ldx,
+                                                      float* __restrict__ part) {
+  // block = 32 column-vectors (8 columns each) x 8 row groups
+  const int cv = blockIdx.x * 32 + (threadIdx.x & 31);
+  const int rg = threadIdx.x >> 5;
+  const int c0 = cv * 8;
+  __shared__ float red[8][32 * 8];
+  float s[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s[e] = 0.f;
+  if (c0 < n) {
+    for (int64_t r = (int64_t)blockIdx.y * 8 + rg; r < m; r += (int64_t)gridDim.y * 8) {
+      float v[8];
+      Vec8<T>::load(v, x + r * ldx + c0);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += v[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rg][(threadIdx.x & 31) * 8 + e] = s[e];
+  __syncthreads();
+  if (rg == 0 && c0 < n) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float t = 0.f;
+      for (int g = 0; g < 8; ++g) t += red[g][(threadIdx.x & 31) * 8 + e];
+      part[(int64_t)blockIdx.y * n + c0 + e] = t;
+    }
+  }
+}
+
+template <typename TO>
+__global__ void colsum_finalize(const float* __restrict__ part, int p, int n, TO* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  float s = 0.f;
+  for (int j = 0; j < p; ++j) s += part[(int64_t)j * n + c];
+  out[c] = from_f<TO>(s);
+}
+
+inline int colsum_parts(int64_t m, int n, int cus) {
+  const int gx = (n / 8 + 31) / 32;
+  int64_t p = ((int64_t)cus * 4 + gx - 1) / gx;
+  const int64_t cap = (m + 7) / 8;
+  if (p > cap) p = cap;
+  if (p > 512) p = 512;
+  return (int)(p < 1 ? 1 : p);
+}
+
+template <typename T, bool AK, bool BKM>
+void launch_epi(const GemmArgs& g, hipStream_t s) {
+  const int tiles = ((g.m + BM - 1) / BM) * ((g.n + BN - 1) / BN);
+  const size_t op_bytes = (size_t)2 * (tile_elems<AK>() + tile_elems<BKM>()) * sizeof(uint16_t);
+  const size_t epi_bytes = (size_t)BM * CSTR * sizeof(float);
+  const size_t lds = op_bytes > epi_bytes ? op_bytes : epi_bytes;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(tiles), dim3(256), lds, s, (const uint16_t*)g.a, (const uint16_t*)g.b, (T*)g.c,
+                       g.lda, g.ldb, g.ldc, g.m, g.n, g.k, (const T*)g.bias, (const T*)g.aux_in, (T*)g.aux_out);
+  };
+  switch (g.epilogue) {
+    case kEpiNone: go(gemm_kernel<T, AK, BKM, kEpiNone>); break;
+    case kEpiGelu: go(gemm_kernel<T, AK, BKM, kEpiGelu>); break;
+    case kEpiRelu: go(gemm_kernel<T, AK, BKM, kEpiRelu>); break;
+    case kEpiSigmoid: go(gemm_kernel<T, AK, BKM, kEpiSigmoid>); break;
+    case kEpiDGelu: go(gemm_kernel<T, AK, BKM, kEpiDGelu>); break;
+    case kEpiDRelu: go(gemm_kernel<T, AK, BKM, kEpiDRelu>); break;
+    case kEpiDSigmoid: go(gemm_kernel<T, AK, BKM, kEpiDSigmoid>); break;
+    default: throw std::runtime_error("gemm: unknown epilogue");
+  }
+}
+
+}  // namespace gemm
+
+bool gemm_supported(const GemmArgs& g) {
+  if (g.dtype != kF16 && g.dtype != kBF16) return false;
+  if (g.m <= 0 || g.n <= 0 || g.k <= 0) return false;
+  auto al = [](const void* p) { return p == nullptr || ((uintptr_t)p & 15u) == 0; };
+  if (!al(g.a) || !al(g.b) || !al(g.c) || !al(g.bias) || !al(g.aux_in) || !al(g.aux_out)) return false;
+  if (g.k % 8 || g.n % 8 || g.ldc % 8 || g.lda % 8 || g.ldb % 8) return false;
+  if (!g.a_kmajor && g.m % 8) return false;
+  if ((g.epilogue >= kEpiDGelu) && g.aux_in == nullptr) return false;
+  return true;
+}
+
+void gemm_mfma(const GemmArgs& g, int /*cus*/, hipStream_t s) {
+  if (!gemm_supported(g)) throw std::runtime_error("gemm_mfma: unsupported shape/alignment/dtype");
+  dispatch_16(g.dtype, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    if (g.a_kmajor && g.b_kmajor) gemm::launch_epi<T, true, true>(g, s);
+    else if (g.a_kmajor && !g.b_kmajor) gemm::launch_epi<T, true, false>(g, s);
+    else if (!g.a_kmajor && g.b_kmajor) gemm::launch_epi<T, false, true>(g, s);
+    else gemm::launch_epi<T, false, false>(g, s);
+  }, "gemm_mfma");
+  check_launch("gemm_mfma");
+}
+
+int64_t column_sum_workspace_floats(int64_t m, int n, int cus) { return (int64_t)gemm::colsum_parts(m, n, cus) * n; }
+
+void column_sum(const void* x, int dtype, int64_t m, int n, int64_t ldx, void* out, int out_dtype, float* ws, int cus,
+                hipStream_t s) {
+  if (n <= 0) return;
+  if (n % 8 || ldx % 8 || ((uintptr_t)x & 15u)) throw std::runtime_error("column_sum: n, ldx must be multiples of 8");
+  const int p = gemm::colsum_parts(m, n, cus);
+  dispatch_float(dtype, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    hipLaunchKernelGGL((gemm::colsum_partial<T>), dim3((n / 8 + 31) / 32, p), dim3(256), 0, s, (const T*)x, m, n, ldx,
+                       ws);
+  }, "column_sum");
+  dispatch_float(out_dtype, [&](auto tag) {
+    using TO = typename decltype(tag)::type;
+    hipLaunchKernelGGL((gemm::colsum_finalize<TO>), dim3((n + 255) / 256), dim3(256), 0, s, ws, p, n, (TO*)out);
+  }, "column_sum out");
+  check_launch("column_sum");
+}
+
+}  // namespace apex_amd

@@ -7,9 +7,9 @@
 //
 // MI355X design (no grid-wide sync, no persistent CTAs, deterministic):
 //  forward   1. stats_partial : every lane owns 8 channels (one 16-byte load per row), keeps
-//               4 rows in flight, accumulates pivot-shifted sums (s, s^2) -> per-lane (mean, M2);
-//               Chan-merged across the block's row-groups in LDS -> one partial per block
-//            2. stats_finalize: merges partials in a fixed order, writes mean / inv_std, the
+//               4 rows in flight, accumulates sums of (x - shift), (x - shift)^2 with a common
+//               per-channel shift (row 0); summed across the block's row-groups in LDS
+//            2. stats_finalize: sums the partials in a fixed order, writes mean / inv_std, the
 //               running-stat EMA and the epilogue constants scale/shift (one launch per layer)
 //            3. apply         : y = relu(x*scale + shift + z) — one FMA per element, 16-byte I/O
 //  backward  1. bwd_partial   : sum(dy'), sum(dy'*(x-mean)) with dy' = dy masked by the ReLU
@@ -42,7 +42,7 @@ inline Geo geo(int64_t m, int c, int cus) {
   if (g.ty > 32) g.ty = 32;
   g.gx = (cv + g.tx - 1) / g.tx;
   const int64_t rows_per_iter = (int64_t)g.ty * kU;
-  int64_t gy = ((int64_t)cus * 4 + g.gx - 1) / g.gx;
+  int64_t gy = ((int64_t)cus * 2 + g.gx - 1) / g.gx;
   const int64_t cap = (m + rows_per_iter - 1) / rows_per_iter;
   if (gy > cap) gy = cap;
   if (gy > 1024) gy = 1024;
@@ -50,19 +50,13 @@ inline Geo geo(int64_t m, int c, int cus) {
   return g;
 }
 
-__device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float mb, float m2b) {
-  if (nb == 0.f) return;
-  const float nn = n + nb;
-  const float d = mb - mean;
-  const float f = nb / nn;
-  mean += d * f;
-  m2 += m2b + d * d * n * f;
-  n = nn;
-}
-
 __device__ __forceinline__ void load8f(float (&v)[8], const float* p) { Vec8<float>::load(v, p); }
 
 // ------------------------------------------------------------------------------------------
+// Statistics use a COMMON per-channel shift (the channel's value in row 0): every block
+// accumulates plain sums S1 = sum(x - shift), S2 = sum((x - shift)^2), so the cross-block merge
+// is a plain (fixed-order, deterministic) sum and mean/var follow from S1/n and S2/n - (S1/n)^2.
+// A real sample of the channel as the shift keeps the cancellation in S2 benign.
 template <typename T>
 __global__ void __launch_bounds__(256) stats_partial(const T* __restrict__ x, int64_t m, int c,
                                                      float* __restrict__ part) {
@@ -70,10 +64,10 @@ __global__ void __launch_bounds__(256) stats_partial(const T* __restrict__ x, in
   const int TX = blockDim.x, TY = blockDim.y, tx = threadIdx.x, ty = threadIdx.y;
   const int c0 = (blockIdx.x * TX + tx) * 8;
   const bool active = c0 < c;
-  float piv[8], s[8], ss[8];
+  float sh[8], s[8], ss[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) piv[k] = s[k] = ss[k] = 0.f;
-  float n = 0.f;
+  for (int k = 0; k < 8; ++k) sh[k] = s[k] = ss[k] = 0.f;
+  if (active) Vec8<T>::load(sh, x + c0);
   const int64_t R = (int64_t)TY * kU;
   for (int64_t base = (int64_t)blockIdx.y * R; base < m; base += R * gridDim.y) {
     float v[kU][8];
@@ -87,68 +81,86 @@ __global__ void __launch_bounds__(256) stats_partial(const T* __restrict__ x, in
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       if (!ok[u]) continue;
-      if (n == 0.f) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) piv[k] = v[u][k];
-      }
-      n += 1.f;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const float d = v[u][k] - piv[k];
+        const float d = v[u][k] - sh[k];
         s[k] += d;
-        ss[k] += d * d;
+        ss[k] = fmaf(d, d, ss[k]);
       }
     }
   }
   const int W = TX * 8;
-  float* sm = smem;
-  float* s2 = smem + TY * W;
-  float* sn = smem + 2 * TY * W;
   if (active) {
-    const float inv = n > 0.f ? 1.f / n : 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      sm[ty * W + tx * 8 + k] = piv[k] + s[k] * inv;
-      s2[ty * W + tx * 8 + k] = fmaxf(ss[k] - s[k] * s[k] * inv, 0.f);
+      smem[ty * W + tx * 8 + k] = s[k];
+      smem[TY * W + ty * W + tx * 8 + k] = ss[k];
     }
   }
-  if (tx == 0) sn[ty] = n;
   __syncthreads();
   if (ty == 0 && active) {
     const int gy = gridDim.y;
-    float tot = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      float nn = sn[0], mm = sm[tx * 8 + k], MM = s2[tx * 8 + k];
-      for (int j = 1; j < TY; ++j) chan_merge(nn, mm, MM, sn[j], sm[j * W + tx * 8 + k], s2[j * W + tx * 8 + k]);
-      part[(int64_t)blockIdx.y * c + c0 + k] = mm;
-      part[(int64_t)gy * c + (int64_t)blockIdx.y * c + c0 + k] = MM;
-      tot = nn;
+      float a = 0.f, b = 0.f;
+      for (int j = 0; j < TY; ++j) {
+        a += smem[j * W + tx * 8 + k];
+        b += smem[TY * W + j * W + tx * 8 + k];
+      }
+      part[(int64_t)blockIdx.y * c + c0 + k] = a;
+      part[(int64_t)gy * c + (int64_t)blockIdx.y * c + c0 + k] = b;
     }
-    if (blockIdx.x == 0 && tx == 0) part[2 * (int64_t)gy * c + blockIdx.y] = tot;
   }
 }
 
-// block (64 channels x 4 partial-groups); fixed merge order => deterministic
-__global__ void __launch_bounds__(256) stats_finalize(const float* __restrict__ part, int gy, int c,
+// Sum the gy partial rows of two [gy][C] slabs for 16 channels per block: thread (ch, g) sums rows
+// g, g+16, ... (4 independent accumulators keep loads in flight), then a fixed-order LDS reduce.
+__device__ __forceinline__ void sum_partials(const float* __restrict__ part, int gy, int c, int ch, int g,
+                                             float (&red)[2][16][17], float& a, float& b) {
+  float a4[4] = {0.f, 0.f, 0.f, 0.f}, b4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (ch < c) {
+    int j = g;
+    for (; j + 48 < gy; j += 64) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a4[u] += part[(int64_t)(j + 16 * u) * c + ch];
+        b4[u] += part[(int64_t)(gy + j + 16 * u) * c + ch];
+      }
+    }
+    for (; j < gy; j += 16) {
+      a4[0] += part[(int64_t)j * c + ch];
+      b4[0] += part[(int64_t)(gy + j) * c + ch];
+    }
+  }
+  red[0][g][threadIdx.x & 15] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+  red[1][g][threadIdx.x & 15] = (b4[0] + b4[1]) + (b4[2] + b4[3]);
+  __syncthreads();
+  a = 0.f;
+  b = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    a += red[0][i][threadIdx.x & 15];
+    b += red[1][i][threadIdx.x & 15];
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) stats_finalize(const float* __restrict__ part, int gy, int c, float n,
                                                       const float* __restrict__ w, const float* __restrict__ b,
                                                       float eps, float momentum, float* __restrict__ rmean,
                                                       float* __restrict__ rvar, float* __restrict__ save_mean,
-                                                      float* __restrict__ save_invstd, float* __restrict__ coef) {
-  __shared__ float sn[4][64], sm[4][64], s2[4][64];
-  const int cx = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int ch = blockIdx.x * 64 + cx;
-  float n = 0.f, mm = 0.f, MM = 0.f;
-  if (ch < c)
-    for (int j = g; j < gy; j += 4) chan_merge(n, mm, MM, part[2 * (int64_t)gy * c + j], part[(int64_t)j * c + ch],
-                                              part[(int64_t)(gy + j) * c + ch]);
-  sn[g][cx] = n;
-  sm[g][cx] = mm;
-  s2[g][cx] = MM;
-  __syncthreads();
+                                                      float* __restrict__ save_invstd, float* __restrict__ coef,
+                                                      const T* __restrict__ x) {
+  __shared__ float red[2][16][17];
+  const int g = threadIdx.x >> 4;
+  const int ch = blockIdx.x * 16 + (threadIdx.x & 15);
+  float s1, s2;
+  sum_partials(part, gy, c, ch, g, red, s1, s2);
   if (g != 0 || ch >= c) return;
-  for (int j = 1; j < 4; ++j) chan_merge(n, mm, MM, sn[j][cx], sm[j][cx], s2[j][cx]);
-  const float var_b = n > 0.f ? MM / n : 0.f;
+  const float shift = to_f(x[ch]);  // the stats kernel's shift: row 0
+  const float dm = s1 / n;
+  const float var_b = fmaxf(s2 / n - dm * dm, 0.f);
+  const float mm = shift + dm;
   const float istd = rsqrtf(var_b + eps);
   save_mean[ch] = mm;
   save_invstd[ch] = istd;
@@ -156,7 +168,7 @@ __global__ void __launch_bounds__(256) stats_finalize(const float* __restrict__ 
   coef[ch] = sc;
   coef[c + ch] = (b ? b[ch] : 0.f) - mm * sc;
   if (rmean) rmean[ch] = (1.f - momentum) * rmean[ch] + momentum * mm;
-  if (rvar) rvar[ch] = (1.f - momentum) * rvar[ch] + momentum * (n > 1.f ? MM / (n - 1.f) : var_b);
+  if (rvar) rvar[ch] = (1.f - momentum) * rvar[ch] + momentum * (n > 1.f ? var_b * n / (n - 1.f) : var_b);
 }
 
 __global__ void coef_from_stats(const float* __restrict__ mean, const float* __restrict__ v, int is_var,
@@ -278,21 +290,12 @@ __global__ void __launch_bounds__(256) bwd_finalize(const float* __restrict__ pa
                                                     const float* __restrict__ mean, const float* __restrict__ istd,
                                                     const float* __restrict__ w, float* __restrict__ gw,
                                                     float* __restrict__ gb, float* __restrict__ coef) {
-  __shared__ float r1[4][64], r2[4][64];
-  const int cx = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int ch = blockIdx.x * 64 + cx;
-  float a = 0.f, q = 0.f;
-  if (ch < c)
-    for (int j = g; j < gy; j += 4) {
-      a += part[(int64_t)j * c + ch];
-      q += part[(int64_t)(gy + j) * c + ch];
-    }
-  r1[g][cx] = a;
-  r2[g][cx] = q;
-  __syncthreads();
+  __shared__ float red[2][16][17];
+  const int g = threadIdx.x >> 4;
+  const int ch = blockIdx.x * 16 + (threadIdx.x & 15);
+  float sdy, sdyx;
+  sum_partials(part, gy, c, ch, g, red, sdy, sdyx);
   if (g != 0 || ch >= c) return;
-  const float sdy = ((r1[0][cx] + r1[1][cx]) + r1[2][cx]) + r1[3][cx];
-  const float sdyx = ((r2[0][cx] + r2[1][cx]) + r2[2][cx]) + r2[3][cx];
   const float is = istd[ch];
   if (gw) gw[ch] = sdyx * is;
   if (gb) gb[ch] = sdy;
@@ -350,7 +353,7 @@ inline void check_shape(int64_t m, int c) {
 
 int bn_nhwc_plan(int64_t m, int c, int cus, int64_t* ws_floats) {
   const bnh::Geo g = bnh::geo(m, c, cus);
-  if (ws_floats) *ws_floats = 2 * (int64_t)g.gy * c + g.gy;
+  if (ws_floats) *ws_floats = 2 * (int64_t)g.gy * c;
   return g.gy;
 }
 
@@ -360,13 +363,13 @@ void bn_nhwc_stats(const void* x, int x_t, int64_t m, int c, const float* w, con
   bnh::check_shape(m, c);
   bnh::Geo g = bnh::geo(m, c, cus);
   g.gy = gy;
-  const size_t lds = ((size_t)2 * g.ty * g.tx * 8 + g.ty) * sizeof(float);
+  const size_t lds = (size_t)2 * g.ty * g.tx * 8 * sizeof(float);
   dispatch_float(x_t, [&](auto tag) {
     using T = typename decltype(tag)::type;
     hipLaunchKernelGGL((bnh::stats_partial<T>), dim3(g.gx, g.gy), dim3(g.tx, g.ty), lds, s, (const T*)x, m, c, ws);
+    hipLaunchKernelGGL((bnh::stats_finalize<T>), dim3((c + 15) / 16), dim3(256), 0, s, ws, g.gy, c, (float)m, w, b,
+                       eps, momentum, running_mean, running_var, save_mean, save_invstd, coef_fwd, (const T*)x);
   }, "bn_nhwc stats");
-  hipLaunchKernelGGL(bnh::stats_finalize, dim3((c + 63) / 64), dim3(256), 0, s, ws, g.gy, c, w, b, eps, momentum,
-                     running_mean, running_var, save_mean, save_invstd, coef_fwd);
   check_launch("bn_nhwc_stats");
 }
 
@@ -420,7 +423,7 @@ void bn_nhwc_bwd_reduce(const void* dy, const void* x, int x_t, const void* z, c
     else if (dy_masked_out) go(std::false_type{}, std::true_type{}, std::true_type{});
     else go(std::false_type{}, std::true_type{}, std::false_type{});
   }, "bn_nhwc bwd reduce");
-  hipLaunchKernelGGL(bnh::bwd_finalize, dim3((c + 63) / 64), dim3(256), 0, s, ws, g.gy, c, 1.f / (float)m, save_mean,
+  hipLaunchKernelGGL(bnh::bwd_finalize, dim3((c + 15) / 16), dim3(256), 0, s, ws, g.gy, c, 1.f / (float)m, save_mean,
                      save_invstd, w, grad_w, grad_b, coef_bwd);
   check_launch("bn_nhwc_bwd_reduce");
 }

@@ -1,0 +1,3 @@
+from .fused_dense import (FusedDense, FusedDenseGeluDense, DenseNoBiasFunc, FusedDenseFunc,  # noqa: F401
+                          FusedDenseGeluDenseFunc, fused_dense_function, dense_no_bias_function,
+                          fused_dense_gelu_dense_function)

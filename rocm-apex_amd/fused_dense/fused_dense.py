@@ -1,0 +1,167 @@
+"""Fused dense layers (reference apex/fused_dense/fused_dense.py:5-85).
+
+``FusedDense``           y = x W^T + b                      (GEMM + bias epilogue)
+``FusedDenseGeluDense``  y = gelu(x W1^T + b1) W2^T + b2    (GEMM + bias + GeLU-with-aux epilogue,
+                                                             then GEMM + bias)
+Backward: dgrad GEMMs (the first one with the GeLU-derivative epilogue), wgrad GEMMs and
+column-sum bias gradients — every piece is a gfx950 kernel (``csrc/gemm/gemm_mfma.hip``); the
+reference's ROCm build leaves d_bias uninitialised and makes the GeLU variants no-ops
+(csrc/fused_dense.cpp:64-68, csrc/fused_dense_cuda.cu:1361-1495).
+
+Runs the native path for fp16/bf16 GPU tensors with K, N multiples of 8; otherwise (CPU, fp32,
+odd sizes) the same math in torch.  GeLU is the tanh approximation (the cuBLASLt GELU epilogue
+the reference targets)."""
+import torch
+from torch import nn
+
+from .. import _native
+from ..amp import half_function
+
+
+def _g():
+    return _native.require("gemm").gemm
+
+
+def _fd():
+    return _native.require("fused_dense_cuda").fused_dense_cuda
+
+
+def fused_linear_available(x, weight, bias=None):
+    if not _native.use_native(x) or _native.submodule("gemm") is None:
+        return False
+    if x.dtype not in (torch.float16, torch.bfloat16) or weight.dtype != x.dtype:
+        return False
+    if bias is not None and bias.dtype != x.dtype:
+        return False
+    k = x.shape[-1]
+    n = weight.shape[0]
+    return k % 8 == 0 and n % 8 == 0 and x.numel() > 0
+
+
+def linear_bias_forward(x, weight, bias):
+    shape = x.shape[:-1] + (weight.shape[0],)
+    return _fd().linear_bias_forward(x, weight, bias).view(shape)
+
+
+def _gelu_tanh(x):
+    return torch.nn.functional.gelu(x, approximate="tanh")
+
+
+class FusedDenseFunc(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, input, weight, bias):
+        ctx.save_for_backward(input, weight)
+        ctx.native = fused_linear_available(input, weight, bias)
+        ctx.has_bias = bias is not None
+        if ctx.native:
+            return linear_bias_forward(input, weight, bias)
+        out = torch.matmul(input, weight.t())
+        return out + bias if bias is not None else out
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        input, weight = ctx.saved_tensors
+        if ctx.native:
+            dx, dw, db = _fd().linear_bias_backward(input, weight, grad_output.contiguous())
+            return dx.view(input.shape), dw, (db if ctx.has_bias else None)
+        g2 = grad_output.reshape(-1, grad_output.shape[-1])
+        x2 = input.reshape(-1, input.shape[-1])
+        grad_input = grad_output.matmul(weight)
+        grad_weight = g2.t().matmul(x2)
+        grad_bias = g2.sum(0) if ctx.has_bias else None
+        return grad_input, grad_weight, grad_bias
+
+
+class DenseNoBiasFunc(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, input, weight):
+        return FusedDenseFunc.forward(ctx, input, weight, None)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        dx, dw, _ = FusedDenseFunc.backward(ctx, grad_output)
+        return dx, dw
+
+
+class FusedDenseGeluDenseFunc(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, input, weight1, bias1, weight2, bias2):
+        ctx.native = (fused_linear_available(input, weight1, bias1) and weight2.dtype == input.dtype
+                      and bias2.dtype == input.dtype and weight2.shape[0] % 8 == 0 and weight2.shape[1] % 8 == 0)
+        if ctx.native:
+            out1, out2, gelu_in = _fd().linear_gelu_linear_forward(input, weight1, bias1, weight2, bias2)
+            out2 = out2.view(input.shape[:-1] + (weight2.shape[0],))
+        else:
+            gelu_in = torch.matmul(input, weight1.t()) + bias1
+            out1 = _gelu_tanh(gelu_in)
+            out2 = torch.matmul(out1, weight2.t()) + bias2
+        ctx.save_for_backward(input, weight1, weight2, gelu_in, out1)
+        return out2
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        input, weight1, weight2, gelu_in, output1 = ctx.saved_tensors
+        if ctx.native:
+            dx, dw1, db1, dw2, db2 = _fd().linear_gelu_linear_backward(input, gelu_in, output1, weight1, weight2,
+                                                                        grad_output.contiguous())
+            return dx.view(input.shape), dw1, db1, dw2, db2
+        g2 = grad_output.reshape(-1, grad_output.shape[-1])
+        h = output1.reshape(-1, output1.shape[-1])
+        dw2 = g2.t().matmul(h)
+        db2 = g2.sum(0)
+        z = gelu_in.reshape(-1, gelu_in.shape[-1]).detach().requires_grad_(True)
+        with torch.enable_grad():
+            gz = torch.autograd.grad(_gelu_tanh(z), z, g2.matmul(weight2))[0]
+        x2 = input.reshape(-1, input.shape[-1])
+        dw1 = gz.t().matmul(x2)
+        db1 = gz.sum(0)
+        dx = gz.matmul(weight1).view(input.shape)
+        return dx, dw1, db1, dw2, db2
+
+
+fused_dense_function = half_function(FusedDenseFunc.apply)
+dense_no_bias_function = half_function(DenseNoBiasFunc.apply)
+fused_dense_gelu_dense_function = half_function(FusedDenseGeluDenseFunc.apply)
+
+
+class FusedDense(nn.Module):
+    def __init__(self, in_features, out_features, bias=True):
+        super().__init__()
+        self.in_features = in_features
+        self.out_features = out_features
+        self.weight = nn.Parameter(torch.empty(out_features, in_features))
+        if bias:
+            self.bias = nn.Parameter(torch.empty(out_features))
+        else:
+            self.register_parameter("bias", None)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        nn.init.kaiming_uniform_(self.weight, a=5 ** 0.5)
+        if self.bias is not None:
+            bound = 1 / (self.in_features ** 0.5)
+            nn.init.uniform_(self.bias, -bound, bound)
+
+    def forward(self, input):
+        if self.bias is not None:
+            return fused_dense_function(input, self.weight, self.bias)
+        return dense_no_bias_function(input, self.weight)
+
+
+class FusedDenseGeluDense(nn.Module):
+    def __init__(self, in_features, intermediate_features, out_features, bias=True):
+        super().__init__()
+        assert bias, "DenseGeluDense module without bias is currently not supported"
+        self.in_features = in_features
+        self.intermediate_features = intermediate_features
+        self.out_features = out_features
+        self.weight1 = nn.Parameter(torch.empty(intermediate_features, in_features))
+        self.bias1 = nn.Parameter(torch.empty(intermediate_features))
+        self.weight2 = nn.Parameter(torch.empty(out_features, intermediate_features))
+        self.bias2 = nn.Parameter(torch.empty(out_features))
+        for w, b, fan_in in ((self.weight1, self.bias1, in_features), (self.weight2, self.bias2, intermediate_features)):
+            nn.init.kaiming_uniform_(w, a=5 ** 0.5)
+            nn.init.uniform_(b, -1 / fan_in ** 0.5, 1 / fan_in ** 0.5)
+
+    def forward(self, input):
+        return fused_dense_gelu_dense_function(input, self.weight1, self.bias1, self.weight2, self.bias2)

@@ -1,0 +1,173 @@
+"""Fused dense / MLP / MFMA GEMM numerics.
+
+Model: reference apex/contrib/test/fused_dense/test_fused_dense.py (y, dx, dw, db vs matmul) and
+tests/L0/run_mlp/test_mlp.py (MLP vs nn.Sequential(Linear, ReLU, ...)).  GPU tests compare the
+gfx950 MFMA kernel (all four operand-major combinations, every epilogue, ragged shapes) against
+fp32 torch math."""
+import pytest
+import torch
+
+from apex.fused_dense import FusedDense, FusedDenseGeluDense
+from apex.mlp import MLP
+
+
+def test_cpu_fused_dense_and_mlp():
+    torch.manual_seed(0)
+    m = FusedDense(16, 24)
+    x = torch.randn(5, 16, requires_grad=True)
+    y = m(x)
+    torch.testing.assert_close(y, x @ m.weight.t() + m.bias)
+    y.sum().backward()
+    torch.testing.assert_close(m.bias.grad, torch.full((24,), 5.0))
+    g = FusedDenseGeluDense(16, 32, 8)
+    out = g(x)
+    ref = torch.nn.functional.gelu(x @ g.weight1.t() + g.bias1, approximate="tanh") @ g.weight2.t() + g.bias2
+    torch.testing.assert_close(out, ref)
+    out.sum().backward()
+    mlp = MLP([16, 32, 8])
+    mlp(x).mean().backward()
+
+
+def _ref_mm(a, a_kmajor, b, b_kmajor, m, n, k):
+    A = a.float().view(m, k) if a_kmajor else a.float().view(k, m).t()
+    B = b.float().view(n, k).t() if b_kmajor else b.float().view(k, n)
+    return A @ B
+
+
+SHAPES = [(128, 128, 64), (256, 384, 512), (200, 136, 72), (1000, 1032, 2048), (64, 4096, 1024), (3072, 1024, 8)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,n,k", SHAPES)
+@pytest.mark.parametrize("a_kmajor,b_kmajor", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_gpu_gemm_layouts(m, n, k, a_kmajor, b_kmajor, dtype):
+    import apex
+
+    g = apex._native.require("gemm").gemm
+    torch.manual_seed(m + n + k)
+    a = torch.randn(m * k, device="cuda").to(dtype)
+    b = torch.randn(k * n, device="cuda").to(dtype)
+    if not a_kmajor and m % 8:
+        pytest.skip("m-major A needs M % 8 == 0")
+    c, _ = g.matmul(a, a_kmajor, b, b_kmajor, m, n, k)
+    ref = _ref_mm(a, a_kmajor, b, b_kmajor, m, n, k)
+    scale = (k ** 0.5)
+    torch.testing.assert_close(c.float() / scale, ref / scale, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_gpu_gemm_epilogues(dtype):
+    import apex
+
+    g = apex._native.require("gemm").gemm
+    torch.manual_seed(1)
+    m, n, k = 300, 264, 320
+    x = (torch.randn(m, k, device="cuda") * 0.3).to(dtype)
+    w = (torch.randn(n, k, device="cuda") * 0.1).to(dtype)
+    b = torch.randn(n, device="cuda").to(dtype)
+    z = x.float() @ w.float().t() + b.float()
+    tol = dict(atol=3e-2, rtol=3e-2)
+    y, aux = g.linear(x, w, b, g.EPI_GELU, True)
+    torch.testing.assert_close(aux.float(), z, **tol)
+    torch.testing.assert_close(y.float(), torch.nn.functional.gelu(z, approximate="tanh"), **tol)
+    y, _ = g.linear(x, w, b, g.EPI_RELU, False)
+    torch.testing.assert_close(y.float(), torch.relu(z), **tol)
+    y, _ = g.linear(x, w, b, g.EPI_SIGMOID, False)
+    torch.testing.assert_close(y.float(), torch.sigmoid(z), **tol)
+    dy = torch.randn(m, n, device="cuda").to(dtype)
+    zz = z.to(dtype)
+    dx = g.linear_dgrad(dy, w, g.EPI_NONE, None)
+    torch.testing.assert_close(dx.float(), dy.float() @ w.float(), **tol)
+    # activation-derivative epilogues (aux has the shape of the GEMM output: [m, k])
+    auxk = torch.randn(m, k, device="cuda").to(dtype)
+    base = dy.float() @ w.float()
+    zt = auxk.float().requires_grad_(True)
+    dg = torch.autograd.grad(torch.nn.functional.gelu(zt, approximate="tanh").sum(), zt)[0]
+    torch.testing.assert_close(g.linear_dgrad(dy, w, g.EPI_DGELU, auxk).float(), base * dg, **tol)
+    torch.testing.assert_close(g.linear_dgrad(dy, w, g.EPI_DRELU, auxk).float(), base * (auxk.float() > 0), **tol)
+    s = torch.sigmoid(auxk.float()).to(dtype)
+    torch.testing.assert_close(g.linear_dgrad(dy, w, g.EPI_DSIGMOID, s).float(),
+                               base * s.float() * (1 - s.float()), **tol)
+    dw = g.linear_wgrad(dy, x)
+    torch.testing.assert_close(dw.float() / 10, (dy.float().t() @ x.float()) / 10, **tol)
+    cs = g.column_sum(dy, torch.float32)
+    torch.testing.assert_close(cs, dy.float().sum(0), atol=1e-2, rtol=1e-3)
+    del zz
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_gpu_fused_dense_reference_test(dtype):
+    """The reference's test shapes: 3 x 512 tokens, 1024 -> 3072 (dx, dw, db all checked)."""
+    torch.manual_seed(0)
+    x = torch.randn(3 * 512, 1024, device="cuda").to(dtype).requires_grad_(True)
+    dense = FusedDense(1024, 3072).cuda().to(dtype)
+    y = dense(x)
+    xr = x.detach().float().requires_grad_(True)
+    yr = xr @ dense.weight.float().t() + dense.bias.float()
+    torch.testing.assert_close(y.float() / 8, yr / 8, atol=2e-2, rtol=2e-2)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    dw_ref = dy.float().t() @ xr.detach()
+    dx_ref = dy.float() @ dense.weight.float()
+    db_ref = dy.float().sum(0)
+    torch.testing.assert_close(x.grad.float() / 8, dx_ref / 8, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(dense.weight.grad.float() / 40, dw_ref / 40, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(dense.bias.grad.float() / 40, db_ref / 40, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_gpu_fused_dense_gelu_dense(dtype):
+    torch.manual_seed(2)
+    x = (torch.randn(2, 256, 512, device="cuda") * 0.5).to(dtype).requires_grad_(True)
+    mod = FusedDenseGeluDense(512, 2048, 512).cuda().to(dtype)
+    y = mod(x)
+    xr = x.detach().float().requires_grad_(True)
+    w1, b1, w2, b2 = [p.detach().float().requires_grad_(True) for p in (mod.weight1, mod.bias1, mod.weight2, mod.bias2)]
+    yr = torch.nn.functional.gelu(xr @ w1.t() + b1, approximate="tanh") @ w2.t() + b2
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=3e-2)
+    dy = torch.randn_like(yr)
+    y.backward(dy.to(dtype))
+    yr.backward(dy)
+    for got, ref in ((x.grad, xr.grad), (mod.weight1.grad, w1.grad), (mod.bias1.grad, b1.grad),
+                     (mod.weight2.grad, w2.grad), (mod.bias2.grad, b2.grad)):
+        s = max(1.0, float(ref.abs().max()))
+        torch.testing.assert_close(got.float() / s, ref / s, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("activation", ["none", "relu", "sigmoid"])
+@pytest.mark.parametrize("bias", [True, False])
+def test_gpu_mlp_vs_sequential(activation, bias):
+    torch.manual_seed(3)
+    sizes = [480, 1024, 1024, 512, 256]
+    mlp = MLP(sizes, bias=bias, activation=activation).cuda().to(torch.bfloat16)
+    layers = []
+    for i in range(mlp.num_layers):
+        lin = torch.nn.Linear(sizes[i], sizes[i + 1], bias=bias).cuda()
+        with torch.no_grad():
+            lin.weight.copy_(mlp.weights[i].float())
+            if bias:
+                lin.bias.copy_(mlp.biases[i].float())
+        layers.append(lin)
+        if activation == "relu":
+            layers.append(torch.nn.ReLU())
+        elif activation == "sigmoid":
+            layers.append(torch.nn.Sigmoid())
+    ref = torch.nn.Sequential(*layers)
+    x = torch.rand(128, sizes[0], device="cuda") * 2 - 1
+    xt = x.to(torch.bfloat16).requires_grad_(True)
+    xr = xt.detach().float().requires_grad_(True)
+    out = mlp(xt)
+    out_ref = ref(xr)
+    torch.testing.assert_close(out.float(), out_ref, atol=3e-2, rtol=3e-2)
+    out.float().mean().mul(10.0).backward()
+    out_ref.mean().mul(10.0).backward()
+    s = max(1e-3, float(xr.grad.abs().max()))
+    torch.testing.assert_close(xt.grad.float() / s, xr.grad / s, atol=3e-2, rtol=3e-2)
+    if bias:
+        s = max(1e-3, float(ref[0].bias.grad.abs().max()))
+        torch.testing.assert_close(mlp.biases[0].grad.float() / s, ref[0].bias.grad / s, atol=3e-2, rtol=3e-2)

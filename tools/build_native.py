@@ -124,10 +124,18 @@ def build(jobs_n: int | None = None, clean: bool = False, verbose: bool = False)
     os.makedirs(BUILD, exist_ok=True)
     jobs, link = compile_cmds(verbose)
     hdr = newest_header()
+    # module.cpp's registrations depend on which subsystem bindings exist (-D macros): rebuild it
+    # whenever that set changes
+    _, cpp = sources()
+    present = sorted(os.path.basename(p) for p in cpp)
+    stamp = os.path.join(BUILD, "subsystems.stamp")
+    prev = open(stamp).read() if os.path.exists(stamp) else ""
+    subsystems_changed = prev != ",".join(present)
     todo = []
     for src, cmd in jobs:
         o = obj_for(src)
-        if not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(src), hdr):
+        stale = not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(src), hdr)
+        if stale or (subsystems_changed and src.endswith("module.cpp")):
             todo.append((src, cmd))
     n = jobs_n or min(len(todo) or 1, max(1, (os.cpu_count() or 4)))
     failed = []
@@ -147,6 +155,8 @@ def build(jobs_n: int | None = None, clean: bool = False, verbose: bool = False)
                         print(out)
     if failed:
         raise RuntimeError(f"native build failed: {failed}")
+    with open(stamp, "w") as f:
+        f.write(",".join(present))
     out = output_path()
     objs_newest = max(os.path.getmtime(obj_for(s)) for s, _ in jobs)
     if todo or not os.path.exists(out) or os.path.getmtime(out) < objs_newest:
