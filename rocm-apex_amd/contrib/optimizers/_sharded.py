@@ -1,0 +1,240 @@
+"""Flat, sharded parameter / gradient storage shared by DistributedFusedAdam and
+DistributedFusedLAMB (ZeRO-2 style).
+
+Reference: apex/contrib/optimizers/distributed_fused_adam.py:128-371 (flat fp16 grad buffer split
+[block x chunk x shard], per-param hooks copying grads in, reduce-scatter per block on
+``dwu_num_rs_pg`` streams, inter-group all-reduce, all-gather of the updated params with the
+NVIDIA-only ``no_copy=True`` kwarg).
+
+MI355X design:
+  * ONE contiguous model-dtype parameter buffer and ONE gradient buffer; every parameter's
+    ``.data`` and ``.grad`` are views into them, so autograd accumulates straight into the
+    buffer (no per-parameter copy hooks, no flatten/unflatten).  288 GB of HBM per GPU makes the
+    extra full-size gradient buffer free.
+  * the buffer is cut into ``num_blocks`` equal blocks in reverse registration order (the order
+    gradients become ready in backward); each block is ``world`` equal shards.  When the last
+    parameter of a block has its gradient (``register_post_accumulate_grad_hook``) the block is
+    reduce-scattered on a side stream, overlapping the rest of backward.  Blocks are sized so a
+    reduce-scatter moves >= a few MB per rank (RCCL over xGMI is per-link bound; small messages
+    are latency bound).
+  * each rank keeps fp32 master params and optimizer moments ONLY for its shards
+    (``[num_blocks, shard]``), updates them with one fused multi-tensor launch that also writes
+    the model-dtype copy in place, and the updated shards are all-gathered per block
+    (``all_gather_into_tensor`` — stock RCCL, no ``no_copy`` extension).
+  * optional e5m2 (fp8) all-gather compression, global grad-norm clipping, and sync-free
+    overflow handling (device skip flag + inverse scale consumed by the kernels).
+"""
+import math
+
+import torch
+import torch.distributed as dist
+
+_ALIGN = 128  # elements; keeps every param / shard 16-byte aligned for the vector kernels
+
+
+class FlatShardedBuffers:
+    def __init__(self, params, process_group=None, num_blocks=4, min_block_elems=1 << 20, grad_dtype=None,
+                 overlap_reductions=True):
+        params = [p for p in params if p.requires_grad]
+        assert params, "no trainable parameters"
+        dtypes = {p.dtype for p in params}
+        if len(dtypes) != 1:
+            raise RuntimeError("Distributed fused optimizers need parameters of one dtype; got {}".format(dtypes))
+        self.dtype = params[0].dtype
+        self.grad_dtype = grad_dtype or self.dtype
+        self.device = params[0].device
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
+        self.params = params
+        self.overlap = overlap_reductions
+        self._gloo = dist.is_initialized() and dist.get_backend(process_group) == "gloo"
+
+        # layout: reverse order (gradients arrive roughly last-layer-first)
+        order = list(reversed(range(len(params))))
+        offsets = [0] * len(params)
+        cur = 0
+        for i in order:
+            offsets[i] = cur
+            cur += int(math.ceil(params[i].numel() / _ALIGN)) * _ALIGN
+        used = cur
+        unit = self.world * _ALIGN
+        nb = max(1, min(num_blocks, int(math.ceil(used / max(min_block_elems, unit)))))
+        block = int(math.ceil(used / (nb * unit))) * unit
+        self.num_blocks = nb
+        self.block = block
+        self.shard = block // self.world
+        self.total = nb * block
+        self.offsets = offsets
+
+        self.flat_param = torch.zeros(self.total, dtype=self.dtype, device=self.device)
+        self.flat_grad = torch.zeros(self.total, dtype=self.grad_dtype, device=self.device)
+        with torch.no_grad():
+            for p, off in zip(params, offsets):
+                n = p.numel()
+                self.flat_param[off:off + n].copy_(p.detach().reshape(-1))
+                p.data = self.flat_param[off:off + n].view_as(p)
+        self.attach_grads()
+
+        # parameters per block (a param belongs to every block it overlaps)
+        self.block_params = [set() for _ in range(nb)]
+        for i, (p, off) in enumerate(zip(params, offsets)):
+            first, last = off // block, (off + max(p.numel(), 1) - 1) // block
+            for b in range(first, last + 1):
+                self.block_params[b].add(i)
+        self.param_blocks = [[b for b in range(nb) if i in self.block_params[b]] for i in range(len(params))]
+
+        # this rank's shards: [num_blocks, shard] fp32 masters + reduced-grad staging
+        self.shard_grad = torch.zeros(nb, self.shard, dtype=torch.float32 if self.grad_dtype == torch.float32
+                                      else self.grad_dtype, device=self.device)
+        self.master = torch.empty(nb, self.shard, dtype=torch.float32, device=self.device)
+        with torch.no_grad():
+            for b in range(nb):
+                self.master[b].copy_(self.param_shard(b).float())
+
+        self._pending = [len(s) for s in self.block_params]
+        self._ready = [0] * nb
+        self._handles = [None] * nb
+        self._fired = [False] * len(params)
+        self._dirty = set()
+        self._stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+        self.is_accumulation_step = False
+        self._hooks = []
+        if overlap_reductions:
+            for i, p in enumerate(params):
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+
+    # ---- views ----
+    def attach_grads(self):
+        for p, off in zip(self.params, self.offsets):
+            n = p.numel()
+            p.grad = self.flat_grad[off:off + n].view_as(p)
+
+    def _adopt_grad(self, i):
+        """Put a gradient autograd allocated outside the flat buffer (after a user
+        ``zero_grad(set_to_none=True)``) back into the buffer."""
+        p, off = self.params[i], self.offsets[i]
+        view = self.flat_grad[off:off + p.numel()]
+        g = p.grad
+        if g is not None and g.data_ptr() != view.data_ptr():
+            view.copy_(g.reshape(-1))
+            p.grad = view.view_as(p)
+
+    def block_view(self, buf, b):
+        return buf[b * self.block:(b + 1) * self.block]
+
+    def param_shard(self, b, rank=None):
+        r = self.rank if rank is None else rank
+        s = b * self.block + r * self.shard
+        return self.flat_param[s:s + self.shard]
+
+    def grad_shard_views(self):
+        return [self.shard_grad[b] for b in range(self.num_blocks)]
+
+    def fragments(self):
+        """(param index, block, start, end) of every parameter fragment inside this rank's shards,
+        as offsets into the shard row ``[0, shard)`` of block ``block``."""
+        out = []
+        for i, (p, off) in enumerate(zip(self.params, self.offsets)):
+            n = p.numel()
+            for b in self.param_blocks[i]:
+                s0 = b * self.block + self.rank * self.shard
+                lo, hi = max(off, s0), min(off + n, s0 + self.shard)
+                if lo < hi:
+                    out.append((i, b, lo - s0, hi - s0))
+        return out
+
+    # ---- reductions ----
+    def _make_hook(self, i):
+        def hook(param):
+            self._adopt_grad(i)
+            if self.is_accumulation_step:
+                return
+            if self._fired[i]:
+                # a shared parameter accumulated again after its block may have been reduced:
+                # reduce those blocks once more at the end (same decision on every rank)
+                self._dirty.update(b for b in self.param_blocks[i] if self._handles[b] is not None)
+                return
+            self._fired[i] = True
+            for b in self.param_blocks[i]:
+                self._ready[b] += 1
+                if self._ready[b] == self._pending[b]:
+                    self._reduce_block(b)
+        return hook
+
+    def _reduce_block(self, b):
+        if self._handles[b] is not None:
+            return
+        src = self.block_view(self.flat_grad, b)
+        dst = self.shard_grad[b]
+        if self.world == 1:
+            dst.copy_(src)
+            self._handles[b] = True
+            return
+        if self._stream is not None:
+            self._stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self._stream):
+                out = dst if dst.dtype == src.dtype else torch.empty_like(src[:self.shard])
+                self._handles[b] = (dist.reduce_scatter_tensor(out, src, group=self.pg, async_op=True), out, dst)
+        else:
+            out = dst if dst.dtype == src.dtype else torch.empty_like(src[:self.shard])
+            dist.reduce_scatter_tensor(out, src, group=self.pg)
+            self._handles[b] = (None, out, dst)
+
+    def complete_reductions(self):
+        """Reduce every block not reduced yet and wait for all of them."""
+        if not self.overlap:
+            for i in range(len(self.params)):
+                self._adopt_grad(i)
+        for b in range(self.num_blocks):
+            if self._handles[b] is None:
+                self._reduce_block(b)
+        for b in range(self.num_blocks):
+            h = self._handles[b]
+            if isinstance(h, tuple):
+                work, out, dst = h
+                if work is not None:
+                    work.wait()
+                if out is not dst:
+                    dst.copy_(out)
+        if self._stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._stream)
+        for b in sorted(self._dirty):
+            self._handles[b] = None
+            self._reduce_block(b)
+            work, out, dst = self._handles[b] if isinstance(self._handles[b], tuple) else (None, None, None)
+            if work is not None:
+                work.wait()
+            if out is not None and out is not dst:
+                dst.copy_(out)
+        if self._dirty and self._stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._stream)
+        self._dirty = set()
+        self._handles = [None] * self.num_blocks
+        self._ready = [0] * self.num_blocks
+        self._fired = [False] * len(self.params)
+
+    def zero_grad(self):
+        self.flat_grad.zero_()
+        self.attach_grads()
+
+    # ---- parameter all-gather ----
+    def all_gather_params(self, e5m2=False):
+        if self.world == 1:
+            return
+        for b in range(self.num_blocks):
+            full = self.block_view(self.flat_param, b)
+            mine = self.param_shard(b)
+            if e5m2:
+                q = mine.to(torch.float8_e5m2)
+                buf = torch.empty(self.block, dtype=torch.float8_e5m2, device=self.device)
+                dist.all_gather_into_tensor(buf.view(torch.uint8), q.view(torch.uint8), group=self.pg)
+                full.copy_(buf.to(self.dtype))
+            else:
+                # RCCL gathers in place when the input is this rank's slice of the output
+                src = mine.clone() if self._gloo else mine
+                dist.all_gather_into_tensor(full, src, group=self.pg)
+
+    def state_dict_shards(self):
+        return {"rank": self.rank, "world": self.world, "block": self.block, "num_blocks": self.num_blocks,
+                "master": self.master.clone()}

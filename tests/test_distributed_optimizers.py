@@ -1,0 +1,204 @@
+"""ZeRO distributed optimizers and legacy contrib optimizers.
+
+Model: reference apex/contrib/test/optimizers/test_dist_adam.py (DistributedFusedAdam on every
+rank vs torch.optim.AdamW on the full model with all-reduced gradients, params compared after
+several steps) and test_distributed_fused_lamb.py (LAMB vs reference LAMB math).  CPU tiers run
+world_size 2 over gloo (fp32 params, so the comparison is tight)."""
+import copy
+
+import pytest
+import torch
+import torch.distributed as dist
+
+from tests._dist_utils import run_multiprocess
+
+
+def _model(seed=0):
+    torch.manual_seed(seed)
+    return torch.nn.Sequential(torch.nn.Linear(13, 37), torch.nn.Tanh(), torch.nn.Linear(37, 29),
+                               torch.nn.Tanh(), torch.nn.Linear(29, 5))
+
+
+def _batches(rank, n=4):
+    g = torch.Generator().manual_seed(100 + rank)
+    return [(torch.randn(8, 13, generator=g), torch.randn(8, 5, generator=g)) for _ in range(n)]
+
+
+def _ref_lamb_step(params, grads, state, lr, b1, b2, eps, wd, step):
+    for p, g in zip(params, grads):
+        st = state.setdefault(id(p), {"m": torch.zeros_like(p), "v": torch.zeros_like(p)})
+        st["m"].mul_(b1).add_(g, alpha=1 - b1)
+        st["v"].mul_(b2).addcmul_(g, g, value=1 - b2)
+        mh = st["m"] / (1 - b1 ** step)
+        vh = st["v"] / (1 - b2 ** step)
+        u = mh / (vh.sqrt() + eps) + wd * p
+        pn, un = p.norm(), u.norm()
+        ratio = (pn / un) if (pn > 0 and un > 0) else 1.0
+        p.sub_(lr * ratio * u)
+
+
+def _worker(rank, world, kind, num_blocks, max_grad_norm):
+    from apex.contrib.optimizers import DistributedFusedAdam, DistributedFusedLAMB
+
+    model = _model()
+    ref = copy.deepcopy(model)
+    kw = dict(lr=1e-2, betas=(0.9, 0.99), eps=1e-8, weight_decay=0.01, dwu_num_blocks=num_blocks,
+              min_block_elems=256)
+    if kind == "adam":
+        opt = DistributedFusedAdam(model.parameters(), max_grad_norm=max_grad_norm, **kw)
+        ref_opt = torch.optim.AdamW(ref.parameters(), lr=1e-2, betas=(0.9, 0.99), eps=1e-8, weight_decay=0.01)
+    else:
+        opt = DistributedFusedLAMB(model.parameters(), max_grad_norm=max_grad_norm, **kw)
+        ref_state = {}
+    assert opt._flat.num_blocks >= 1
+    for step, (x, y) in enumerate(_batches(rank), start=1):
+        loss = torch.nn.functional.mse_loss(model(x), y)
+        loss.backward()
+        opt.step()
+        # reference: full model, gradient averaged over ranks
+        ref.zero_grad()
+        torch.nn.functional.mse_loss(ref(x), y).backward()
+        grads = []
+        for p in ref.parameters():
+            dist.all_reduce(p.grad)
+            p.grad.div_(world)
+            grads.append(p.grad)
+        if max_grad_norm > 0:
+            torch.nn.utils.clip_grad_norm_(list(ref.parameters()), max_grad_norm)
+        if kind == "adam":
+            ref_opt.step()
+        else:
+            with torch.no_grad():
+                _ref_lamb_step(list(ref.parameters()), [p.grad for p in ref.parameters()], ref_state, 1e-2, 0.9, 0.99,
+                               1e-8, 0.01, step)
+        for p, q in zip(model.parameters(), ref.parameters()):
+            torch.testing.assert_close(p, q, atol=2e-5, rtol=1e-4)
+        if max_grad_norm > 0:
+            assert opt.L2_grad_norm is not None
+    # model params are views into the flat buffer; grads were zeroed into the buffer
+    assert all(p.grad is not None and float(p.grad.abs().sum()) == 0 for p in model.parameters())
+
+
+@pytest.mark.parametrize("kind", ["adam", "lamb"])
+@pytest.mark.parametrize("num_blocks,max_grad_norm", [(1, 0.0), (3, 0.0), (2, 0.05)])
+def test_distributed_optimizer_matches_full_model(kind, num_blocks, max_grad_norm):
+    run_multiprocess(_worker, world=2, args=(kind, num_blocks, max_grad_norm))
+
+
+def _overflow_worker(rank, world):
+    from apex.contrib.optimizers import DistributedFusedAdam
+
+    model = _model(1)
+    opt = DistributedFusedAdam(model.parameters(), lr=1e-2, min_block_elems=128)
+    before = [p.detach().clone() for p in model.parameters()]
+    x, y = _batches(rank, 1)[0]
+    xb = x.clone()
+    if rank == 1:  # non-finite grads on one rank (reduced during backward) skip the step on every rank
+        xb[0, 0] = float("inf")
+    torch.nn.functional.mse_loss(model(xb), y).backward()
+    opt.step()
+    assert opt.has_overflow
+    for p, b in zip(model.parameters(), before):
+        assert torch.equal(p, b)
+    # next, clean step proceeds; step counter only advanced once
+    torch.nn.functional.mse_loss(model(x), y).backward()
+    opt.step()
+    assert not opt.has_overflow
+    assert float(opt._step_t) == 1.0
+    # sharded checkpoint round trip
+    sd = opt.state_dict()
+    opt2 = DistributedFusedAdam(_model(1).parameters(), lr=1e-2, min_block_elems=128)
+    opt2.load_state_dict(sd)
+    torch.testing.assert_close(opt2._m, opt._m)
+    torch.testing.assert_close(opt2._flat.flat_param, opt._flat.flat_param)
+
+
+def test_distributed_adam_overflow_skip_and_checkpoint():
+    run_multiprocess(_overflow_worker, world=2)
+
+
+def _accum_worker(rank, world):
+    from apex.contrib.optimizers import DistributedFusedAdam
+
+    model = _model(2)
+    ref = copy.deepcopy(model)
+    opt = DistributedFusedAdam(model.parameters(), lr=1e-2, weight_decay=0.0, min_block_elems=128)
+    ref_opt = torch.optim.AdamW(ref.parameters(), lr=1e-2, weight_decay=0.0)
+    b = _batches(rank, 2)
+    opt.set_is_accumulation_step(True)
+    torch.nn.functional.mse_loss(model(b[0][0]), b[0][1]).backward()
+    opt.set_is_accumulation_step(False)
+    model.zero_grad(set_to_none=False)  # drop the accumulated micro-batch (zeroes the flat buffer in place)
+    torch.nn.functional.mse_loss(model(b[0][0]), b[0][1]).backward()
+    torch.nn.functional.mse_loss(model(b[1][0]), b[1][1]).backward()  # second micro-batch, hooks re-fire
+    opt.step()
+    for x, y in b:
+        torch.nn.functional.mse_loss(ref(x), y).backward()
+    for p in ref.parameters():
+        dist.all_reduce(p.grad)
+        p.grad.div_(world)
+    ref_opt.step()
+    for p, q in zip(model.parameters(), ref.parameters()):
+        torch.testing.assert_close(p, q, atol=2e-5, rtol=1e-4)
+
+
+def test_distributed_adam_accumulation_and_refire():
+    run_multiprocess(_accum_worker, world=2)
+
+
+def test_distributed_adam_single_process_set_to_none():
+    """world=1 without init: grads re-adopted after zero_grad(set_to_none=True)."""
+    from apex.contrib.optimizers import DistributedFusedAdam
+
+    model = _model(3)
+    ref = copy.deepcopy(model)
+    opt = DistributedFusedAdam(model.parameters(), lr=1e-2, weight_decay=0.0)
+    ref_opt = torch.optim.AdamW(ref.parameters(), lr=1e-2, weight_decay=0.0)
+    for x, y in _batches(0, 3):
+        model.zero_grad(set_to_none=True)
+        torch.nn.functional.mse_loss(model(x), y).backward()
+        opt.step()
+        ref_opt.zero_grad()
+        torch.nn.functional.mse_loss(ref(x), y).backward()
+        ref_opt.step()
+    for p, q in zip(model.parameters(), ref.parameters()):
+        torch.testing.assert_close(p, q, atol=2e-5, rtol=1e-4)
+
+
+def test_contrib_legacy_optimizers_with_fp16_optimizer():
+    from apex.contrib.optimizers import FP16_Optimizer, FusedAdam, FusedLAMB, FusedSGD
+
+    torch.manual_seed(0)
+    for cls, kw, ref_cls, ref_kw in [
+        (FusedAdam, dict(lr=1e-2), torch.optim.AdamW, dict(lr=1e-2, weight_decay=0.0)),
+        (FusedSGD, dict(lr=0.1, momentum=0.9), torch.optim.SGD, dict(lr=0.1, momentum=0.9)),
+    ]:
+        model = _model(4)
+        ref = copy.deepcopy(model)
+        opt = FP16_Optimizer(cls(model.parameters(), **kw), static_loss_scale=128.0)
+        ref_opt = ref_cls(ref.parameters(), **ref_kw)
+        for x, y in _batches(0, 3):
+            opt.zero_grad()
+            opt.backward(torch.nn.functional.mse_loss(model(x), y))
+            opt.step()
+            ref_opt.zero_grad()
+            torch.nn.functional.mse_loss(ref(x), y).backward()
+            ref_opt.step()
+        for p, q in zip(model.parameters(), ref.parameters()):
+            torch.testing.assert_close(p, q, atol=1e-4, rtol=1e-3)
+    model = _model(5)
+    ref = copy.deepcopy(model)
+    opt = FusedLAMB(model.parameters(), lr=1e-2, weight_decay=0.01, max_grad_norm=1e9, betas=(0.9, 0.99), eps=1e-8)
+    st = {}
+    for step, (x, y) in enumerate(_batches(0, 3), start=1):
+        opt.zero_grad()
+        torch.nn.functional.mse_loss(model(x), y).backward()
+        opt.step()
+        for p in ref.parameters():
+            p.grad = None
+        torch.nn.functional.mse_loss(ref(x), y).backward()
+        with torch.no_grad():
+            _ref_lamb_step(list(ref.parameters()), [p.grad for p in ref.parameters()], st, 1e-2, 0.9, 0.99, 1e-8,
+                           0.01, step)
+    for p, q in zip(model.parameters(), ref.parameters()):
+        torch.testing.assert_close(p, q, atol=1e-5, rtol=1e-4)
