@@ -1,0 +1,568 @@
+// Flash-style fused attention, forward and backward, for gfx950 (wave64, v_mfma_f32_32x32x16).
+//
+// Replaces the reference's three separate attention paths with one kernel family:
+//   * contrib multihead_attn "fast" impl: QKV GEMM -> strided-batched QK^T -> masked softmax +
+//     dropout -> strided-batched PV (apex/contrib/csrc/multihead_attn/self_multihead_attn_cuda.cu,
+//     materialises the [b*h, sq, sk] score and probability tensors in HBM),
+//   * contrib fmha (sm80-only CUTLASS kernels, head dim 64, seq <= 512;
+//     apex/contrib/csrc/fmha/src/fmha_fprop_fp16_kernel.sm80.cu),
+//   * the masked softmax of apex.transformer.functional.FusedScaleMaskSoftmax when the caller
+//     wants the whole attention.
+// Nothing of size sq x sk ever reaches HBM.
+//
+// Forward (one workgroup = 4 waves = 128 query rows of one (batch, head); 64-key tiles):
+//   * "swapped" S^T = K Q^T: K tile rows are the MFMA A operand (row reads from LDS), each wave's
+//     32 query rows live in registers as the B operand.  The accumulator then holds, per lane,
+//     ONE query and 16 keys per 32-key tile, so the online-softmax row max / row sum are 31
+//     in-register ops plus one lane^32 exchange.
+//   * P stays in registers: accumulator registers 8s..8s+7 are the B operand of O^T += V^T P^T
+//     (k permuted by crow(), V^T read with ds_read_b64_tr_b16 at the matching rows).
+//   * K/V tiles double-buffered in LDS with register staging (issue next tile's loads before the
+//     MFMAs, write them after), one barrier per tile; K rows padded to D+8 (conflict-free
+//     ds_read_b128), V rows to a 64/192-B bank offset for the transposed reads.
+//   * masks: key padding (varlen lengths), causal, additive fp32 bias with broadcast strides;
+//     dropout by a counter-based hash of (seed, offset, batch*head, query, key) — regenerated
+//     bit-exactly by the backward pass.
+// Backward (FlashAttention-2 order; one workgroup = 4 waves = 128 keys of one (batch, kv head)):
+//   * per 32-query slice: S and dP with the key on the lane (K, V of the wave's 32 keys in
+//     registers), P = exp2(c S - lse2), dS = P (dP - delta); dV^T += dO^T P and dK^T += Q^T dS
+//     with P / dS fed from registers (same crow() trick), Q / dO read transposed from one LDS
+//     image each; dS crosses LDS once for dQ = dS K, which is summed over key blocks with
+//     no-return global_atomic_add_f32 into an fp32 buffer (full 128-B segments per instruction).
+//   * GQA: the workgroup sweeps every query head of its kv group, so dK / dV need no cross-
+//     workgroup sum.
+#include "apex_amd/attn_api.h"
+#include "apex_amd/device.h"
+#include "apex_amd/dispatch.h"
+#include "apex_amd/mfma.h"
+
+namespace apex_amd {
+namespace attn {
+
+using namespace mfma;
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+template <int D>
+struct Geo {
+  static constexpr int KSTR = D + 8;                 // row-read images (16-B slot shift per row)
+  static constexpr int TSTR = (D == 32) ? 96 : D + 32;  // transposed-read images (64/192-B bank offset per row)
+  static constexpr int NKK = D / 16;                 // 16-deep k steps over d
+  static constexpr int NDT = D / 32;                 // 32-wide d tiles
+};
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+// Counter-based dropout decision; mirrored in python (apex.contrib.multihead_attn / tests).
+__device__ __forceinline__ uint32_t drop_hash(uint32_t seed_mix, uint32_t bh, uint32_t q, uint32_t k) {
+  const uint32_t a = mix32(seed_mix ^ (bh * 0x9E3779B9u));
+  const uint32_t b = mix32(a ^ (q * 0x85EBCA6Bu));
+  return mix32(b ^ (k * 0xC2B2AE35u));
+}
+__host__ __device__ inline uint32_t seed_mix_of(uint64_t seed, uint64_t offset) {
+  uint32_t x = (uint32_t)seed ^ ((uint32_t)(seed >> 32) * 0x27d4eb2du) ^ ((uint32_t)offset * 0x165667b1u) ^
+               ((uint32_t)(offset >> 32) * 0xd3a2646cu);
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+struct Seq {
+  int64_t qrow0, krow0;  // token-space base row (side buffers)
+  int64_t qoff, koff;    // element offset of the sequence start for the batch stride / varlen row
+  int lq, lk;
+};
+
+__device__ __forceinline__ void seq_of(const AttnArgs& a, int b, int64_t q_sb, int64_t q_ss, int64_t k_sb,
+                                       int64_t k_ss, Seq& s) {
+  if (a.cu_q != nullptr) {
+    const int c0 = a.cu_q[b];
+    s.qrow0 = c0;
+    s.lq = a.cu_q[b + 1] - c0;
+    s.qoff = (int64_t)c0 * q_ss;
+  } else {
+    s.qrow0 = (int64_t)b * a.sq;
+    s.lq = a.sq;
+    s.qoff = (int64_t)b * q_sb;
+  }
+  if (a.cu_k != nullptr) {
+    const int c0 = a.cu_k[b];
+    s.krow0 = c0;
+    s.lk = a.cu_k[b + 1] - c0;
+    s.koff = (int64_t)c0 * k_ss;
+  } else {
+    s.krow0 = (int64_t)b * a.sk;
+    s.lk = a.sk;
+    s.koff = (int64_t)b * k_sb;
+  }
+}
+
+__device__ __forceinline__ int64_t tensor_off(const AttnTensor& t, const Seq& s, bool is_q, bool varlen, int b) {
+  // offset of the (batch, seq=0, head=0) element for tensor t sharing the q- or k-side sequence map
+  if (varlen) return (is_q ? s.qrow0 : s.krow0) * t.ss;
+  return (int64_t)b * t.sb;
+}
+
+// =============================================================================================
+// forward
+// =============================================================================================
+template <typename T, int D>
+__global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) fwd_kernel(const AttnArgs a) {
+  using G = Geo<D>;
+  constexpr int BN = 64, KSTR = G::KSTR, VSTR = G::TSTR, NKK = G::NKK, NDT = G::NDT;
+  constexpr int KT = BN * KSTR, VT = BN * VSTR;
+  constexpr int CPR = D / 8;                 // 16-B chunks per row
+  constexpr int CPT = BN * CPR / 256;        // chunks per thread per tensor (D >= 32 -> >= 1)
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  auto kbuf = [&](int i) { return lds + i * (KT + VT); };
+  auto vbuf = [&](int i) { return lds + i * (KT + VT) + KT; };
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h2 = lane >> 5, ql = lane & 31;
+  const int hq = blockIdx.y, b = blockIdx.z;
+  const int hk = hq / (a.h / a.h_k);
+  Seq sq;
+  seq_of(a, b, a.q.sb, a.q.ss, a.k.sb, a.k.ss, sq);
+  const int q_start = blockIdx.x * 128;
+  if (q_start >= sq.lq) return;  // uniform over the workgroup
+  const bool varq = a.cu_q != nullptr, vark = a.cu_k != nullptr;
+  const uint16_t* qp = (const uint16_t*)a.q.p + tensor_off(a.q, sq, true, varq, b) + (int64_t)hq * a.q.sh;
+  const uint16_t* kp = (const uint16_t*)a.k.p + tensor_off(a.k, sq, false, vark, b) + (int64_t)hk * a.k.sh;
+  const uint16_t* vp = (const uint16_t*)a.v.p + tensor_off(a.v, sq, false, vark, b) + (int64_t)hk * a.v.sh;
+  T* op = (T*)a.o.p + tensor_off(a.o, sq, true, varq, b) + (int64_t)hq * a.o.sh;
+
+  const int myq = q_start + wave * 32 + ql;
+  const bool qvalid = myq < sq.lq;
+  s16x8 qf[NKK];
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) {
+    if (qvalid) qf[kk] = *reinterpret_cast<const s16x8*>(qp + (int64_t)myq * a.q.ss + kk * 16 + 8 * h2);
+    else
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[kk][j] = 0;
+  }
+
+  int k_end = sq.lk;
+  if (a.causal) k_end = min(k_end, q_start + 128);
+  const int nkb = (k_end + BN - 1) / BN;
+  const int wave_q_last = min(q_start + wave * 32 + 31, sq.lq - 1);
+
+  uint4 rk[CPT], rv[CPT];
+  auto gload = [&](int kb0) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int ch = tid + 256 * i, row = ch / CPR, col = (ch % CPR) * 8;
+      const int key = kb0 + row;
+      const bool ok = key < sq.lk;
+      rk[i] = ok ? *reinterpret_cast<const uint4*>(kp + (int64_t)key * a.k.ss + col) : make_uint4(0, 0, 0, 0);
+      rv[i] = ok ? *reinterpret_cast<const uint4*>(vp + (int64_t)key * a.v.ss + col) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int ch = tid + 256 * i, row = ch / CPR, col = (ch % CPR) * 8;
+      *reinterpret_cast<uint4*>(kbuf(buf) + row * KSTR + col) = rk[i];
+      *reinterpret_cast<uint4*>(vbuf(buf) + row * VSTR + col) = rv[i];
+    }
+  };
+
+  f32x16 o[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i) o[i] = zero16();
+  float m_i = -INFINITY, l_i = 0.f;
+  const float c = a.scale * kLog2e;
+  const bool dropout = a.p_drop > 0.f;
+  const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
+  const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
+  const uint32_t smix = seed_mix_of(a.seed, a.offset);
+  const uint32_t bh = (uint32_t)(b * a.h + hq);
+  const float* biasp = a.bias ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh + (int64_t)myq * a.bias_sq
+                              : nullptr;
+
+  if (nkb > 0) {
+    gload(0);
+    lstore(0);
+  }
+  __syncthreads();
+  for (int it = 0; it < nkb; ++it) {
+    const int cur = it & 1, kb0 = it * BN;
+    const bool more = it + 1 < nkb;
+    if (more) gload(kb0 + BN);
+    const uint16_t* Kl = kbuf(cur);
+    const uint16_t* Vl = vbuf(cur);
+
+    f32x16 s[2] = {zero16(), zero16()};
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      const s16x8 a0 = frag_rows<KSTR>(Kl, 0, kk, lane);
+      const s16x8 a1 = frag_rows<KSTR>(Kl, 32, kk, lane);
+      s[0] = mma<T>(a0, qf[kk], s[0]);
+      s[1] = mma<T>(a1, qf[kk], s[1]);
+    }
+    float x[2][16];
+    const bool need_mask = (kb0 + BN > sq.lk) || (a.causal && kb0 + BN - 1 > q_start + wave * 32) || biasp != nullptr;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) x[t][r] = s[t][r] * c;
+    if (need_mask) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kb0 + 32 * t + crow(r, h2);
+          const bool ok = key < sq.lk && (!a.causal || key <= myq);
+          float v = x[t][r];
+          if (biasp != nullptr && ok && qvalid) v += biasp[(int64_t)key * a.bias_sk] * kLog2e;
+          x[t][r] = ok ? v : -INFINITY;
+        }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, x[t][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_i, mx);
+    const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+    const float alpha = exp2f(m_i - m_use);
+    float ls = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = exp2f(x[t][r] - m_use);
+        ls += p;
+        x[t][r] = p;
+      }
+    ls += __shfl_xor(ls, 32, 64);
+    l_i = l_i * alpha + ls;
+    m_i = m_new;
+#pragma unroll
+    for (int i = 0; i < NDT; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+    if (dropout) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const uint32_t key = (uint32_t)(kb0 + 32 * t + crow(r, h2));
+          x[t][r] *= drop_hash(smix, bh, (uint32_t)myq, key) >= thresh ? inv_keep : 0.f;
+        }
+    }
+    // O^T[d][q] += V^T[d][key] P^T[key][q]
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const s16x8 pf = pack8<T>(&x[t][8 * s2]);
+        const int klo = 32 * t + 16 * s2 + 4 * h2;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          const s16x8 vf = frag_tr<VSTR>(Vl, 32 * dt, klo, klo + 8, lane);
+          o[dt] = mma<T>(vf, pf, o[dt]);
+        }
+      }
+    if (more) lstore(cur ^ 1);
+    __syncthreads();
+  }
+  (void)wave_q_last;
+
+  if (qvalid) {
+    const float inv_l = l_i > 0.f ? 1.f / l_i : 0.f;
+    T* orow = op + (int64_t)myq * a.o.ss;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 32 * dt + 8 * g4 + 4 * h2;
+        uint32_t w0 = (uint32_t)from_f<T>(o[dt][4 * g4] * inv_l).x | ((uint32_t)from_f<T>(o[dt][4 * g4 + 1] * inv_l).x << 16);
+        uint32_t w1 = (uint32_t)from_f<T>(o[dt][4 * g4 + 2] * inv_l).x | ((uint32_t)from_f<T>(o[dt][4 * g4 + 3] * inv_l).x << 16);
+        *reinterpret_cast<uint2*>(orow + d0) = make_uint2(w0, w1);
+      }
+    if (h2 == 0 && a.lse != nullptr)
+      a.lse[(int64_t)hq * a.rows_q + sq.qrow0 + myq] = l_i > 0.f ? (m_i + log2f(l_i)) * kLn2 : INFINITY;
+  }
+}
+
+// =============================================================================================
+// backward
+// =============================================================================================
+// delta[h][row] = sum_d dO * O   (D/8 lanes per row)
+template <typename T, int D>
+__global__ void __launch_bounds__(256) bwd_delta_kernel(const AttnBwdArgs ba) {
+  const AttnArgs& a = ba.f;
+  constexpr int LPR = D / 8, RPB = 256 / LPR;
+  const int hq = blockIdx.y, b = blockIdx.z;
+  Seq sq;
+  seq_of(a, b, a.q.sb, a.q.ss, a.k.sb, a.k.ss, sq);
+  const int q = blockIdx.x * RPB + threadIdx.x / LPR, c8 = (threadIdx.x % LPR) * 8;
+  float acc = 0.f;
+  const bool varq = a.cu_q != nullptr;
+  if (q < sq.lq) {
+    const T* o = (const T*)a.o.p + tensor_off(a.o, sq, true, varq, b) + (int64_t)hq * a.o.sh + (int64_t)q * a.o.ss;
+    const T* g = (const T*)ba.dout.p + tensor_off(ba.dout, sq, true, varq, b) + (int64_t)hq * ba.dout.sh +
+                 (int64_t)q * ba.dout.ss;
+    float ov[8], gv[8];
+    Vec8<T>::load(ov, o + c8);
+    Vec8<T>::load(gv, g + c8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc += ov[e] * gv[e];
+  }
+#pragma unroll
+  for (int off = LPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if (q < sq.lq && (threadIdx.x % LPR) == 0) ba.delta[(int64_t)hq * a.rows_q + sq.qrow0 + q] = acc;
+}
+
+template <typename T, int D>
+__global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
+  const AttnArgs& a = ba.f;
+  using G = Geo<D>;
+  constexpr int BK = 128, QB = 32, NKK = G::NKK, NDT = G::NDT;
+  constexpr int KLSTR = G::TSTR;   // K image: transposed reads for dQ
+  constexpr int QSTR = G::KSTR;    // Q / dO images: row reads (S, dP) and transposed reads (dK, dV)
+  constexpr int DSSTR = BK + 8;    // dS image: row reads for dQ
+  constexpr int CPR = D / 8;
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  uint16_t* Kl = lds;
+  uint16_t* Ql = Kl + BK * KLSTR;
+  uint16_t* dOl = Ql + QB * QSTR;
+  uint16_t* dSl = dOl + QB * QSTR;
+  float* lse_l = reinterpret_cast<float*>(dSl + QB * DSSTR);
+  float* del_l = lse_l + QB;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h2 = lane >> 5, ql = lane & 31;
+  const int hk = blockIdx.y, b = blockIdx.z;
+  Seq sq;
+  seq_of(a, b, a.q.sb, a.q.ss, a.k.sb, a.k.ss, sq);
+  const int k_start = blockIdx.x * BK;
+  if (k_start >= sq.lk) return;
+  const bool varq = a.cu_q != nullptr, vark = a.cu_k != nullptr;
+  const uint16_t* kp = (const uint16_t*)a.k.p + tensor_off(a.k, sq, false, vark, b) + (int64_t)hk * a.k.sh;
+  const uint16_t* vp = (const uint16_t*)a.v.p + tensor_off(a.v, sq, false, vark, b) + (int64_t)hk * a.v.sh;
+
+  // K tile of the workgroup -> LDS (transposed reads for dQ); own 32 keys' K, V -> registers
+  for (int ch = tid; ch < BK * CPR; ch += 256) {
+    const int row = ch / CPR, col = (ch % CPR) * 8, key = k_start + row;
+    *reinterpret_cast<uint4*>(Kl + row * KLSTR + col) =
+        key < sq.lk ? *reinterpret_cast<const uint4*>(kp + (int64_t)key * a.k.ss + col) : make_uint4(0, 0, 0, 0);
+  }
+  const int mykey = k_start + wave * 32 + ql;
+  const bool kvalid = mykey < sq.lk;
+  s16x8 kf[NKK], vf[NKK];
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) {
+    if (kvalid) {
+      kf[kk] = *reinterpret_cast<const s16x8*>(kp + (int64_t)mykey * a.k.ss + kk * 16 + 8 * h2);
+      vf[kk] = *reinterpret_cast<const s16x8*>(vp + (int64_t)mykey * a.v.ss + kk * 16 + 8 * h2);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) kf[kk][j] = vf[kk][j] = 0;
+    }
+  }
+
+  f32x16 dk[NDT], dv[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i) dk[i] = dv[i] = zero16();
+  const float c = a.scale * kLog2e;
+  const bool dropout = a.p_drop > 0.f;
+  const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
+  const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
+  const uint32_t smix = seed_mix_of(a.seed, a.offset);
+  const int group = a.h / a.h_k;
+  // dQ tile ownership: d-tile dtq, key part kpart of kparts (NDT * kparts == 4 waves)
+  constexpr int KPARTS = 4 / NDT, KPL = BK / KPARTS;
+  const int dtq = wave % NDT, kpart = wave / NDT;
+
+  for (int hq = hk * group; hq < (hk + 1) * group; ++hq) {
+    const uint16_t* qp = (const uint16_t*)a.q.p + tensor_off(a.q, sq, true, varq, b) + (int64_t)hq * a.q.sh;
+    const uint16_t* gp =
+        (const uint16_t*)ba.dout.p + tensor_off(ba.dout, sq, true, varq, b) + (int64_t)hq * ba.dout.sh;
+    const float* lse_h = a.lse + (int64_t)hq * a.rows_q + sq.qrow0;
+    const float* del_h = ba.delta + (int64_t)hq * a.rows_q + sq.qrow0;
+    float* dq_h = ba.dq_acc + (sq.qrow0 * a.h + hq) * D;
+    const uint32_t bh = (uint32_t)(b * a.h + hq);
+    const float* biash = a.bias ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh : nullptr;
+    const int q_begin = a.causal ? (k_start / QB) * QB : 0;
+    for (int q0 = q_begin; q0 < sq.lq; q0 += QB) {
+      for (int ch = tid; ch < QB * CPR; ch += 256) {
+        const int row = ch / CPR, col = (ch % CPR) * 8, q = q0 + row;
+        const bool ok = q < sq.lq;
+        *reinterpret_cast<uint4*>(Ql + row * QSTR + col) =
+            ok ? *reinterpret_cast<const uint4*>(qp + (int64_t)q * a.q.ss + col) : make_uint4(0, 0, 0, 0);
+        *reinterpret_cast<uint4*>(dOl + row * QSTR + col) =
+            ok ? *reinterpret_cast<const uint4*>(gp + (int64_t)q * ba.dout.ss + col) : make_uint4(0, 0, 0, 0);
+      }
+      if (tid < QB) {
+        const int q = q0 + tid;
+        lse_l[tid] = q < sq.lq ? lse_h[q] : INFINITY;
+        del_l[tid] = q < sq.lq ? del_h[q] : 0.f;
+      }
+      __syncthreads();
+
+      // S[q][key] and dP[q][key] with the key on the lane
+      f32x16 sacc = zero16(), dpacc = zero16();
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        const s16x8 aq = frag_rows<QSTR>(Ql, 0, kk, lane);
+        sacc = mma<T>(aq, kf[kk], sacc);
+        const s16x8 ag = frag_rows<QSTR>(dOl, 0, kk, lane);
+        dpacc = mma<T>(ag, vf[kk], dpacc);
+      }
+      float p[16], ds[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qr = crow(r, h2), q = q0 + qr;
+        const bool ok = kvalid && q < sq.lq && (!a.causal || mykey <= q);
+        float xv = sacc[r] * c - lse_l[qr] * kLog2e;
+        if (biash != nullptr && ok) xv += biash[(int64_t)q * a.bias_sq + (int64_t)mykey * a.bias_sk] * kLog2e;
+        const float pv = ok ? exp2f(xv) : 0.f;
+        float dpv = dpacc[r];
+        float pd = pv;
+        if (dropout) {
+          const float mk = drop_hash(smix, bh, (uint32_t)q, (uint32_t)mykey) >= thresh ? inv_keep : 0.f;
+          pd = pv * mk;
+          dpv *= mk;
+        }
+        p[r] = pd;
+        ds[r] = pv * (dpv - del_l[qr]);
+      }
+      // dV^T += dO^T P,  dK^T += Q^T dS   (P / dS straight from registers)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const s16x8 pf = pack8<T>(&p[8 * s2]);
+        const s16x8 dsf = pack8<T>(&ds[8 * s2]);
+        const int klo = 16 * s2 + 4 * h2;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          const s16x8 gt = frag_tr<QSTR>(dOl, 32 * dt, klo, klo + 8, lane);
+          dv[dt] = mma<T>(gt, pf, dv[dt]);
+          const s16x8 qt = frag_tr<QSTR>(Ql, 32 * dt, klo, klo + 8, lane);
+          dk[dt] = mma<T>(qt, dsf, dk[dt]);
+        }
+      }
+      // dS -> LDS [q][key]
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dSl[crow(r, h2) * DSSTR + wave * 32 + ql] = from_f<T>(ds[r]).x;
+      __syncthreads();
+      // dQ[q][d] += dS[q][keys] K[keys][d] for this wave's (d tile, key part)
+      f32x16 dq = zero16();
+#pragma unroll
+      for (int kk = 0; kk < KPL / 16; ++kk) {
+        const int kb = kpart * KPL + 16 * kk;
+        const s16x8 af = frag_rows<DSSTR>(dSl, 0, kb / 16, lane);
+        const s16x8 bf = frag_tr<KLSTR>(Kl, 32 * dtq, kb + 8 * h2, kb + 8 * h2 + 4, lane);
+        dq = mma<T>(af, bf, dq);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int q = q0 + crow(r, h2);
+        if (q < sq.lq) unsafeAtomicAdd(dq_h + (int64_t)q * a.h * D + 32 * dtq + ql, dq[r] * a.scale);
+      }
+    }
+  }
+
+  if (kvalid) {
+    T* dkp = (T*)ba.dk.p + tensor_off(ba.dk, sq, false, vark, b) + (int64_t)hk * ba.dk.sh + (int64_t)mykey * ba.dk.ss;
+    T* dvp = (T*)ba.dv.p + tensor_off(ba.dv, sq, false, vark, b) + (int64_t)hk * ba.dv.sh + (int64_t)mykey * ba.dv.ss;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 32 * dt + 8 * g4 + 4 * h2;
+        const float s = a.scale;
+        uint32_t k0 = (uint32_t)from_f<T>(dk[dt][4 * g4] * s).x | ((uint32_t)from_f<T>(dk[dt][4 * g4 + 1] * s).x << 16);
+        uint32_t k1 = (uint32_t)from_f<T>(dk[dt][4 * g4 + 2] * s).x | ((uint32_t)from_f<T>(dk[dt][4 * g4 + 3] * s).x << 16);
+        *reinterpret_cast<uint2*>(dkp + d0) = make_uint2(k0, k1);
+        uint32_t v0 = (uint32_t)from_f<T>(dv[dt][4 * g4]).x | ((uint32_t)from_f<T>(dv[dt][4 * g4 + 1]).x << 16);
+        uint32_t v1 = (uint32_t)from_f<T>(dv[dt][4 * g4 + 2]).x | ((uint32_t)from_f<T>(dv[dt][4 * g4 + 3]).x << 16);
+        *reinterpret_cast<uint2*>(dvp + d0) = make_uint2(v0, v1);
+      }
+  }
+}
+
+// dQ (fp32 accumulator [rows][h][D]) -> output dtype with the caller's strides
+template <typename T, int D>
+__global__ void __launch_bounds__(256) dq_convert_kernel(const AttnBwdArgs ba) {
+  const AttnArgs& a = ba.f;
+  constexpr int LPR = D / 8, RPB = 256 / LPR;
+  const int hq = blockIdx.y, b = blockIdx.z;
+  Seq sq;
+  seq_of(a, b, a.q.sb, a.q.ss, a.k.sb, a.k.ss, sq);
+  const int q = blockIdx.x * RPB + threadIdx.x / LPR, c8 = (threadIdx.x % LPR) * 8;
+  if (q >= sq.lq) return;
+  float v[8];
+  Vec8<float>::load(v, ba.dq_acc + ((sq.qrow0 + q) * a.h + hq) * D + c8);
+  T* dst = (T*)ba.dq.p + tensor_off(ba.dq, sq, true, a.cu_q != nullptr, b) + (int64_t)hq * ba.dq.sh +
+           (int64_t)q * ba.dq.ss + c8;
+  Vec8<T>::store(dst, v);
+}
+
+template <int D>
+constexpr size_t fwd_lds() {
+  return (size_t)2 * (64 * Geo<D>::KSTR + 64 * Geo<D>::TSTR) * 2;
+}
+template <int D>
+constexpr size_t bwd_lds() {
+  return (size_t)(128 * Geo<D>::TSTR + 2 * 32 * Geo<D>::KSTR + 32 * (128 + 8)) * 2 + 2 * 32 * 4;
+}
+
+template <typename T, int D>
+void launch_fwd(const AttnArgs& a, hipStream_t s) {
+  const dim3 grid((a.sq + 127) / 128, a.h, a.b);
+  hipLaunchKernelGGL((fwd_kernel<T, D>), grid, dim3(256), fwd_lds<D>(), s, a);
+}
+
+template <typename T, int D>
+void launch_bwd(const AttnBwdArgs& ba, hipStream_t s) {
+  const AttnArgs& a = ba.f;
+  constexpr int RPB = 256 / (D / 8);
+  hipMemsetAsync(ba.dq_acc, 0, (size_t)a.rows_q * a.h * D * sizeof(float), s);
+  hipLaunchKernelGGL((bwd_delta_kernel<T, D>), dim3((a.sq + RPB - 1) / RPB, a.h, a.b), dim3(256), 0, s, ba);
+  hipLaunchKernelGGL((bwd_kernel<T, D>), dim3((a.sk + 127) / 128, a.h_k, a.b), dim3(256), bwd_lds<D>(), s, ba);
+  hipLaunchKernelGGL((dq_convert_kernel<T, D>), dim3((a.sq + RPB - 1) / RPB, a.h, a.b), dim3(256), 0, s, ba);
+}
+
+}  // namespace attn
+
+bool attn_supported(int d, int dtype) { return (d == 32 || d == 64 || d == 128) && (dtype == kF16 || dtype == kBF16); }
+
+void attn_fwd(const AttnArgs& a, hipStream_t s) {
+  if (!attn_supported(a.d, a.dtype)) throw std::runtime_error("attn_fwd: unsupported head dim / dtype");
+  if (a.h_k <= 0 || a.h % a.h_k) throw std::runtime_error("attn_fwd: h must be a multiple of h_k");
+  dispatch_16(a.dtype, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    switch (a.d) {
+      case 32: attn::launch_fwd<T, 32>(a, s); break;
+      case 64: attn::launch_fwd<T, 64>(a, s); break;
+      default: attn::launch_fwd<T, 128>(a, s); break;
+    }
+  }, "attn_fwd");
+  check_launch("attn_fwd");
+}
+
+void attn_bwd(const AttnBwdArgs& a, hipStream_t s) {
+  if (!attn_supported(a.f.d, a.f.dtype)) throw std::runtime_error("attn_bwd: unsupported head dim / dtype");
+  dispatch_16(a.f.dtype, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    switch (a.f.d) {
+      case 32: attn::launch_bwd<T, 32>(a, s); break;
+      case 64: attn::launch_bwd<T, 64>(a, s); break;
+      default: attn::launch_bwd<T, 128>(a, s); break;
+    }
+  }, "attn_bwd");
+  check_launch("attn_bwd");
+}
+
+}  // namespace apex_amd

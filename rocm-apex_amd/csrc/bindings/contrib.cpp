@@ -1,0 +1,166 @@
+// pybind surface of contrib kernels:
+//   _C.transducer_joint_cuda.forward / backward   (reference apex/contrib/csrc/transducer/transducer_joint.cpp)
+//   _C.transducer_loss_cuda.forward / backward    (reference apex/contrib/csrc/transducer/transducer_loss.cpp)
+#include "common.h"
+#include "apex_amd/transducer_api.h"
+
+namespace apex_amd {
+
+namespace {
+
+at::Tensor as_int(const at::Tensor& t) { return t.to(at::kInt).contiguous(); }
+
+struct JointHold {
+  JointArgs a{};
+  at::Tensor f, g, fl, gl, bo;
+};
+
+void joint_setup(JointHold& j, const at::Tensor& f, const at::Tensor& g, const at::Tensor& f_len,
+                 const at::Tensor& g_len, const at::Tensor& batch_offset, bool pack_output) {
+  TORCH_CHECK(f.is_cuda() && g.is_cuda() && f.dim() == 3 && g.dim() == 3, "transducer joint: f [B,T,H], g [B,U,H]");
+  TORCH_CHECK(f.scalar_type() == g.scalar_type(), "transducer joint: dtype mismatch");
+  j.f = f.contiguous();
+  j.g = g.contiguous();
+  j.fl = as_int(f_len);
+  j.gl = as_int(g_len);
+  JointArgs& a = j.a;
+  a.f = j.f.data_ptr();
+  a.g = j.g.data_ptr();
+  a.f_len = j.fl.data_ptr<int>();
+  a.g_len = j.gl.data_ptr<int>();
+  a.B = (int)f.size(0);
+  a.T = (int)f.size(1);
+  a.U = (int)g.size(1);
+  a.H = (int)f.size(2);
+  a.packed = pack_output;
+  if (pack_output) {
+    j.bo = batch_offset.to(at::kLong).contiguous();
+    a.batch_offset = j.bo.data_ptr<int64_t>();
+  }
+  a.dtype = dtype_code(f.scalar_type());
+}
+
+std::vector<at::Tensor> joint_forward(at::Tensor f, at::Tensor g, at::Tensor f_len, at::Tensor g_len,
+                                      at::Tensor batch_offset, int64_t packed_batch, int64_t opt, bool pack_output,
+                                      bool relu, bool dropout, double dropout_prob, int64_t tile_size, int64_t seed,
+                                      int64_t offset) {
+  (void)opt;
+  (void)tile_size;
+  const c10::hip::HIPGuard guard(f.get_device());
+  JointHold j;
+  joint_setup(j, f, g, f_len, g_len, batch_offset, pack_output);
+  auto shape = pack_output ? std::vector<int64_t>{packed_batch, j.a.H}
+                           : std::vector<int64_t>{j.a.B, j.a.T, j.a.U, j.a.H};
+  auto out = at::empty(shape, f.options());
+  at::Tensor mask;
+  if (relu || dropout) {
+    mask = at::empty(shape, f.options().dtype(at::kByte));
+    j.a.mask = mask.data_ptr<uint8_t>();
+  }
+  j.a.out = out.data_ptr();
+  j.a.relu = relu;
+  j.a.dropout = dropout;
+  j.a.p_drop = (float)dropout_prob;
+  j.a.seed = (uint64_t)seed;
+  j.a.offset = (uint64_t)offset;
+  transducer_joint_fwd(j.a, cur_stream());
+  return {out, mask};
+}
+
+std::vector<at::Tensor> joint_backward(std::vector<at::Tensor> inp, at::Tensor f_len, at::Tensor g_len,
+                                       at::Tensor batch_offset, int64_t max_f_len, int64_t max_g_len, bool pack_output,
+                                       double scale, at::Tensor f_like, at::Tensor g_like) {
+  const c10::hip::HIPGuard guard(inp[0].get_device());
+  JointHold j;
+  joint_setup(j, f_like, g_like, f_len, g_len, batch_offset, pack_output);
+  TORCH_CHECK(j.a.T == max_f_len && j.a.U == max_g_len, "transducer joint bwd: shape mismatch");
+  at::Tensor grad = inp[0].contiguous();
+  at::Tensor mask;
+  if (inp.size() > 1) {
+    mask = inp[1].to(at::kByte).contiguous();
+    j.a.mask = mask.data_ptr<uint8_t>();
+  }
+  auto fg = at::empty({j.a.B, j.a.T, j.a.H}, grad.options());
+  auto gg = at::empty({j.a.B, j.a.U, j.a.H}, grad.options());
+  transducer_joint_bwd(j.a, grad.data_ptr(), fg.data_ptr(), gg.data_ptr(), (float)scale, cur_stream());
+  return {fg, gg};
+}
+
+struct LossHold {
+  LossArgs a{};
+  at::Tensor x, label, fl, yl, bo;
+};
+
+void loss_setup(LossHold& h, const at::Tensor& x, const at::Tensor& label, const at::Tensor& f_len,
+                const at::Tensor& y_len, const at::Tensor& batch_offset, int64_t max_f_len, int64_t blank,
+                bool packed) {
+  h.x = x.contiguous();
+  h.label = as_int(label);
+  h.fl = as_int(f_len);
+  h.yl = as_int(y_len);
+  LossArgs& a = h.a;
+  a.x = h.x.data_ptr();
+  a.label = h.label.data_ptr<int>();
+  a.f_len = h.fl.data_ptr<int>();
+  a.y_len = h.yl.data_ptr<int>();
+  a.B = (int)f_len.size(0);
+  a.T = (int)max_f_len;
+  a.U = (int)h.label.size(1) + 1;
+  a.V = x.size(-1);
+  a.blank = (int)blank;
+  a.packed = packed;
+  if (packed) {
+    h.bo = batch_offset.to(at::kLong).contiguous();
+    a.batch_offset = h.bo.data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(x.dim() == 4 && x.size(1) == max_f_len && x.size(2) == a.U, "transducer loss: x must be [B, T, U+1, V]");
+  }
+  a.dtype = dtype_code(x.scalar_type());
+}
+
+std::vector<at::Tensor> loss_forward(at::Tensor x, at::Tensor label, at::Tensor f_len, at::Tensor y_len,
+                                     at::Tensor batch_offset, int64_t max_f_len, int64_t blank_idx, int64_t opt,
+                                     bool packed_input) {
+  (void)opt;
+  const c10::hip::HIPGuard guard(x.get_device());
+  LossHold h;
+  loss_setup(h, x, label, f_len, y_len, batch_offset, max_f_len, blank_idx, packed_input);
+  auto fo = x.options().dtype(at::kFloat);
+  auto alpha = at::empty({h.a.B, h.a.T, h.a.U}, fo);
+  auto beta = at::empty({h.a.B, h.a.T, h.a.U}, fo);
+  auto loss = at::empty({h.a.B}, fo);
+  h.a.alpha = alpha.data_ptr<float>();
+  h.a.beta = beta.data_ptr<float>();
+  h.a.loss = loss.data_ptr<float>();
+  transducer_loss_fwd(h.a, cur_stream());
+  return {alpha, beta, loss.to(x.scalar_type())};
+}
+
+at::Tensor loss_backward(at::Tensor x, at::Tensor loss_grad, at::Tensor alpha, at::Tensor beta, at::Tensor f_len,
+                         at::Tensor y_len, at::Tensor label, at::Tensor batch_offset, int64_t max_f_len,
+                         int64_t blank_idx, int64_t opt, bool fuse_softmax_backward, bool packed_input) {
+  (void)opt;
+  const c10::hip::HIPGuard guard(x.get_device());
+  LossHold h;
+  loss_setup(h, x, label, f_len, y_len, batch_offset, max_f_len, blank_idx, packed_input);
+  at::Tensor a_c = alpha.contiguous(), b_c = beta.contiguous();
+  h.a.alpha = a_c.data_ptr<float>();
+  h.a.beta = b_c.data_ptr<float>();
+  at::Tensor lg = loss_grad.to(at::kFloat).contiguous();
+  auto xg = packed_input ? at::zeros_like(h.x) : at::empty_like(h.x);
+  transducer_loss_bwd(h.a, lg.data_ptr<float>(), xg.data_ptr(), fuse_softmax_backward, cur_stream());
+  return xg;
+}
+
+}  // namespace
+
+void bind_contrib(pybind11::module_& root) {
+  auto j = root.def_submodule("transducer_joint_cuda", "RNN-T joint (gfx950)");
+  j.def("forward", &joint_forward);
+  j.def("backward", &joint_backward);
+  auto l = root.def_submodule("transducer_loss_cuda", "RNN-T loss (gfx950)");
+  l.def("forward", &loss_forward);
+  l.def("backward", &loss_backward);
+}
+
+}  // namespace apex_amd

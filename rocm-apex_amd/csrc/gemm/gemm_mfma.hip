@@ -345,7 +345,11 @@ bool gemm_supported(const GemmArgs& g) {
   if (g.m <= 0 || g.n <= 0 || g.k <= 0) return false;
   auto al = [](const void* p) { return p == nullptr || ((uintptr_t)p & 15u) == 0; };
   if (!al(g.a) || !al(g.b) || !al(g.c) || !al(g.bias) || !al(g.aux_in) || !al(g.aux_out)) return false;
-  if (g.k % 8 || g.n % 8 || g.ldc % 8 || g.lda % 8 || g.ldb % 8) return false;
+  // k-major operands are read as 16-byte k-vectors (K % 8); m/n-major operands are read as
+  // 16-byte row vectors with per-k-row bounds checks, so their K may be ragged (weight grads
+  // over an arbitrary token count).
+  if ((g.a_kmajor || g.b_kmajor) && g.k % 8) return false;
+  if (g.n % 8 || g.ldc % 8 || g.lda % 8 || g.ldb % 8) return false;
   if (!g.a_kmajor && g.m % 8) return false;
   if ((g.epilogue >= kEpiDGelu) && g.aux_in == nullptr) return false;
   return true;

@@ -1,0 +1,268 @@
+"""Fused attention: flash kernels, multihead_attn modules, FMHA.
+
+Model: reference apex/contrib/test/multihead_attn/test_self_multihead_attn.py (fast impl vs
+default impl, outputs and input grads), test_encdec_multihead_attn.py, test_mha_fused_softmax.py,
+and apex/contrib/test/fmha/test_fmha.py (packed varlen qkv vs per-sequence python attention).
+GPU tiers compare the gfx950 kernels against fp32 torch math of the same op, including the
+dropout mask (the kernels' counter-based hash is mirrored in python)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from apex.ops.attention import dropout_keep_mask, flash_attn_func
+
+
+def naive(q, k, v, scale, causal=False, bias=None, keep=None, p=0.0):
+    # q [b, sq, h, d]; k, v [b, sk, hk, d]
+    rep = q.size(2) // k.size(2)
+    qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k, v))
+    kf, vf = kf.repeat_interleave(rep, 1), vf.repeat_interleave(rep, 1)
+    s = qf @ kf.transpose(-1, -2) * scale
+    if bias is not None:
+        s = s + bias
+    if causal:
+        s = s.masked_fill(torch.ones(s.shape[-2:], dtype=torch.bool, device=s.device).triu(1), float("-inf"))
+    pr = torch.softmax(s, -1)
+    if keep is not None:
+        pr = pr * keep / (1 - p)
+    return (pr @ vf).transpose(1, 2)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_cpu_reference_matches_naive(causal):
+    torch.manual_seed(0)
+    q, k, v = (torch.randn(2, 9, 4, 16, requires_grad=True) for _ in range(3))
+    bias = torch.randn(2, 1, 1, 9)
+    out = flash_attn_func(q, k, v, causal=causal, bias=bias)
+    ref = naive(q, k, v, 0.25, causal, bias)
+    torch.testing.assert_close(out, ref, atol=1e-5, rtol=1e-5)
+    g = torch.randn_like(out)
+    gq = torch.autograd.grad(out, (q, k, v), g)
+    gr = torch.autograd.grad(ref, (q, k, v), g)
+    for a, b in zip(gq, gr):
+        torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-5)
+
+
+def test_cpu_gqa_varlen_dropout_semantics():
+    torch.manual_seed(1)
+    lens = [5, 11, 3]
+    cu = torch.tensor([0, 5, 16, 19], dtype=torch.int32)
+    q = torch.randn(19, 4, 16)
+    k = torch.randn(19, 2, 16)
+    v = torch.randn(19, 2, 16)
+    out = flash_attn_func(q, k, v, cu_seqlens_q=cu, cu_seqlens_k=cu, dropout_p=0.3, seed=7, offset=3)
+    for bi, (a, b) in enumerate(zip(cu[:-1].tolist(), cu[1:].tolist())):
+        bh = bi * 4 + torch.arange(4)
+        keep = dropout_keep_mask(7, 3, bh, lens[bi], lens[bi], 0.3).view(1, 4, lens[bi], lens[bi])
+        ref = naive(q[a:b][None], k[a:b][None], v[a:b][None], 0.25, keep=keep.float(), p=0.3)[0]
+        torch.testing.assert_close(out[a:b], ref, atol=1e-5, rtol=1e-5)
+    frac = dropout_keep_mask(1, 2, torch.arange(8), 64, 64, 0.25).float().mean().item()
+    assert abs(frac - 0.75) < 0.02
+
+
+def _mha_pair(cls, **kw):
+    from apex.contrib.multihead_attn import EncdecMultiheadAttn, SelfMultiheadAttn  # noqa: F401
+
+    torch.manual_seed(2)
+    fast = cls(64, 4, impl="fast", **kw)
+    default = cls(64, 4, impl="default", **kw)
+    default.load_state_dict(fast.state_dict(), strict=False)
+    return fast, default
+
+
+@pytest.mark.parametrize("bias,norm_add,mask", [(False, False, None), (True, False, "pad"), (True, True, "time"),
+                                                (False, True, "pad")])
+def test_cpu_self_mha_fast_vs_default(bias, norm_add, mask):
+    from apex.contrib.multihead_attn import SelfMultiheadAttn
+
+    fast = SelfMultiheadAttn(64, 4, bias=bias, include_norm_add=norm_add, impl="fast")
+    default = SelfMultiheadAttn(64, 4, bias=bias, include_norm_add=norm_add, impl="default")
+    sd = fast.state_dict()
+    if norm_add:
+        sd = {k: v for k, v in sd.items() if not k.startswith("lyr_nrm")}
+    default.load_state_dict(sd, strict=False)
+    x = torch.randn(10, 3, 64, requires_grad=True)
+    kpm = tm = None
+    if mask == "pad":
+        kpm = torch.zeros(3, 10, dtype=torch.bool)
+        kpm[1, 7:] = True
+    elif mask == "time":
+        tm = torch.ones(10, 10, dtype=torch.bool).triu(1)
+    y1, _ = fast(x, x, x, key_padding_mask=kpm, attn_mask=tm, is_training=False)
+    y2, _ = default(x, x, x, key_padding_mask=kpm, attn_mask=tm, is_training=False)
+    torch.testing.assert_close(y1, y2, atol=1e-5, rtol=1e-4)
+    g1 = torch.autograd.grad(y1.sum(), x)[0]
+    g2 = torch.autograd.grad(y2.sum(), x)[0]
+    torch.testing.assert_close(g1, g2, atol=1e-5, rtol=1e-4)
+
+
+def test_cpu_encdec_mha_and_softmax_dropout():
+    from apex.contrib.multihead_attn import EncdecMultiheadAttn, fast_mask_softmax_dropout_func
+
+    fast = EncdecMultiheadAttn(64, 8, impl="fast")
+    default = EncdecMultiheadAttn(64, 8, impl="default")
+    default.load_state_dict(fast.state_dict())
+    q = torch.randn(6, 2, 64)
+    kv = torch.randn(9, 2, 64)
+    kpm = torch.zeros(2, 9, dtype=torch.bool)
+    kpm[0, 5:] = True
+    y1, _ = fast(q, kv, kv, key_padding_mask=kpm, is_training=False)
+    y2, _ = default(q, kv, kv, key_padding_mask=kpm, is_training=False)
+    torch.testing.assert_close(y1, y2, atol=1e-5, rtol=1e-4)
+    s = torch.randn(2 * 8, 6, 9, requires_grad=True)
+    out = fast_mask_softmax_dropout_func(False, 8, s, kpm, False, 0.0)
+    ref = torch.softmax(s.view(2, 8, 6, 9).masked_fill(kpm.view(2, 1, 1, 9), float("-inf")), -1).view(16, 6, 9)
+    torch.testing.assert_close(out, ref)
+    gs = torch.autograd.grad(out.sum() + (out * out).sum(), s)[0]
+    gr = torch.autograd.grad(ref.sum() + (ref * ref).sum(), s)[0]
+    torch.testing.assert_close(gs, gr, atol=1e-6, rtol=1e-5)
+
+
+def test_cpu_fmha_module():
+    from apex.contrib.fmha import FMHA
+
+    class Cfg:
+        attention_probs_dropout_prob = 0.0
+        num_attention_heads = 2
+        hidden_size = 64
+
+    cu = torch.tensor([0, 4, 10], dtype=torch.int32)
+    qkv = torch.randn(10, 3 * 64, requires_grad=True)
+    out = FMHA(Cfg())(qkv, cu, 6, is_training=False)
+    x = qkv.view(10, 3, 2, 32)
+    for a, b in ((0, 4), (4, 10)):
+        ref = naive(x[a:b, 0][None], x[a:b, 1][None], x[a:b, 2][None], 32 ** -0.5)[0].reshape(b - a, 64)
+        torch.testing.assert_close(out[a:b], ref, atol=1e-5, rtol=1e-5)
+    out.sum().backward()
+    assert qkv.grad is not None and torch.isfinite(qkv.grad).all()
+
+
+# ------------------------------------------------------------------------------------------
+# GPU: gfx950 kernels vs fp32 math
+# ------------------------------------------------------------------------------------------
+def _close(got, ref, tol):
+    s = max(1.0, float(ref.abs().max()))
+    torch.testing.assert_close(got.float() / s, ref.float() / s, atol=tol, rtol=tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d", [32, 64, 128])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("causal", [False, True])
+def test_gpu_flash_fwd_bwd(d, dtype, causal):
+    import apex
+
+    assert apex._native.submodule("attn") is not None, "attention kernels not built"
+    torch.manual_seed(d)
+    b, sq, sk, h = 2, 200, 200 if causal else 333, 4
+    q = torch.randn(b, sq, h, d, device="cuda", dtype=dtype, requires_grad=True)
+    k = torch.randn(b, sk, h, d, device="cuda", dtype=dtype, requires_grad=True)
+    v = torch.randn(b, sk, h, d, device="cuda", dtype=dtype, requires_grad=True)
+    scale = d ** -0.5
+    out = flash_attn_func(q, k, v, causal=causal)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    ref = naive(qr, kr, vr, scale, causal)
+    tol = 2e-2
+    _close(out, ref, tol)
+    g = torch.randn_like(ref)
+    out.backward(g.to(dtype))
+    ref.backward(g)
+    _close(q.grad, qr.grad, tol)
+    _close(k.grad, kr.grad, tol)
+    _close(v.grad, vr.grad, tol)
+
+
+@pytest.mark.gpu
+def test_gpu_flash_bias_gqa_dropout_varlen():
+    torch.manual_seed(5)
+    dtype = torch.bfloat16
+    # bias + GQA + dropout, padded layout
+    b, s, h, hk, d = 2, 150, 8, 2, 64
+    q = torch.randn(b, s, h, d, device="cuda", dtype=dtype, requires_grad=True)
+    k = torch.randn(b, s, hk, d, device="cuda", dtype=dtype, requires_grad=True)
+    v = torch.randn(b, s, hk, d, device="cuda", dtype=dtype, requires_grad=True)
+    bias = torch.zeros(b, 1, 1, s, device="cuda")
+    bias[1, :, :, 100:] = float("-inf")
+    bias[0] += torch.randn(1, 1, s, device="cuda")
+    p = 0.2
+    out = flash_attn_func(q, k, v, dropout_p=p, bias=bias, seed=11, offset=5)
+    bh = torch.arange(b * h)
+    keep = dropout_keep_mask(11, 5, bh, s, s, p, "cuda").view(b, h, s, s).float()
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    ref = naive(qr, kr, vr, d ** -0.5, bias=bias, keep=keep, p=p)
+    _close(out, ref, 2e-2)
+    g = torch.randn_like(ref)
+    out.backward(g.to(dtype))
+    ref.backward(g)
+    for a, r in ((q.grad, qr.grad), (k.grad, kr.grad), (v.grad, vr.grad)):
+        _close(a, r, 3e-2)
+    # varlen packed
+    lens = [17, 130, 64, 1]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device="cuda")
+    tot = sum(lens)
+    q = torch.randn(tot, 4, 128, device="cuda", dtype=dtype, requires_grad=True)
+    k = torch.randn(tot, 4, 128, device="cuda", dtype=dtype, requires_grad=True)
+    v = torch.randn(tot, 4, 128, device="cuda", dtype=dtype, requires_grad=True)
+    out = flash_attn_func(q, k, v, cu_seqlens_q=cu, cu_seqlens_k=cu, causal=True)
+    g = torch.randn_like(out)
+    out.backward(g)
+    c = cu.tolist()
+    for i in range(len(lens)):
+        a, e = c[i], c[i + 1]
+        qr, kr, vr = (t.detach()[a:e].float()[None].requires_grad_(True) for t in (q, k, v))
+        ref = naive(qr, kr, vr, 128 ** -0.5, causal=True)
+        _close(out[a:e][None], ref, 2e-2)
+        ref.backward(g[a:e][None].float())
+        _close(q.grad[a:e][None], qr.grad, 3e-2)
+        _close(k.grad[a:e][None], kr.grad, 3e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("norm_add", [False, True])
+def test_gpu_self_mha_fast_vs_default(norm_add):
+    from apex.contrib.multihead_attn import SelfMultiheadAttn
+
+    torch.manual_seed(3)
+    fast = SelfMultiheadAttn(1024, 16, bias=True, include_norm_add=norm_add, impl="fast").cuda().half()
+    default = SelfMultiheadAttn(1024, 16, bias=True, include_norm_add=norm_add, impl="default").cuda().half()
+    sd = {k: v for k, v in fast.state_dict().items() if not k.startswith("lyr_nrm")}
+    default.load_state_dict(sd, strict=False)
+    x = torch.randn(128, 8, 1024, device="cuda", dtype=torch.half, requires_grad=True)
+    kpm = torch.zeros(8, 128, dtype=torch.bool, device="cuda")
+    kpm[3, 90:] = True
+    y1, _ = fast(x, x, x, key_padding_mask=kpm, is_training=False)
+    y2, _ = default(x, x, x, key_padding_mask=kpm, is_training=False)
+    _close(y1, y2, 2e-2)
+    g = torch.randn_like(y1)
+    g1 = torch.autograd.grad(y1, x, g)[0]
+    g2 = torch.autograd.grad(y2, x, g)[0]
+    _close(g1, g2, 3e-2)
+
+
+@pytest.mark.gpu
+def test_gpu_fmha_vs_reference():
+    from apex.contrib.fmha import FMHA
+
+    class Cfg:
+        attention_probs_dropout_prob = 0.0
+        num_attention_heads = 16
+        hidden_size = 1024
+
+    torch.manual_seed(4)
+    lens = [128, 384, 77, 512]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device="cuda")
+    qkv = torch.randn(sum(lens), 3 * 1024, device="cuda", dtype=torch.half, requires_grad=True)
+    out = FMHA(Cfg())(qkv, cu, 512, is_training=True)
+    g = torch.randn_like(out)
+    out.backward(g)
+    x = qkv.detach().view(-1, 3, 16, 64)
+    c = cu.tolist()
+    for i in range(len(lens)):
+        a, e = c[i], c[i + 1]
+        xr = x[a:e].float().requires_grad_(True)
+        ref = naive(xr[:, 0][None], xr[:, 1][None], xr[:, 2][None], 0.125)[0].reshape(e - a, 1024)
+        _close(out[a:e], ref, 2e-2)
+        ref.backward(g[a:e].float())
+        _close(qkv.grad[a:e].view(-1, 3, 16, 64), xr.grad, 3e-2)

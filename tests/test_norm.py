@@ -150,3 +150,53 @@ def test_gpu_layer_norm_deterministic():
         outs.append((x.grad.clone(), m.weight.grad.clone(), m.bias.grad.clone()))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_cpu_fast_layer_norm_module():
+    from apex.contrib.layer_norm import FastLayerNorm
+
+    torch.manual_seed(0)
+    m = FastLayerNorm(48)
+    with torch.no_grad():
+        m.weight.uniform_(0.5, 1.5)
+        m.bias.uniform_(-0.5, 0.5)
+    x = torch.randn(6, 5, 48, requires_grad=True)
+    ref = torch.nn.functional.layer_norm(x, (48,), m.weight, m.bias, 1e-5)
+    y = m(x)
+    torch.testing.assert_close(y, ref, atol=1e-5, rtol=1e-5)
+    g = torch.randn_like(y)
+    got = torch.autograd.grad(y, (x, m.weight, m.bias), g)
+    exp = torch.autograd.grad(ref, (x, m.weight, m.bias), g)
+    for a, b in zip(got, exp):
+        torch.testing.assert_close(a, b, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hidden", [768, 1024, 4096, 12288, 25600])
+@pytest.mark.parametrize("itype,wtype", [(torch.bfloat16, torch.bfloat16), (torch.float16, torch.float32),
+                                         (torch.float32, torch.float32)])
+def test_gpu_fast_layer_norm(hidden, itype, wtype):
+    """reference apex/contrib/test/layer_norm/test_fast_layer_norm.py: hidden sizes x dtype combos."""
+    from apex.contrib.layer_norm import FastLayerNorm
+
+    torch.manual_seed(hidden)
+    m = FastLayerNorm(hidden).cuda().to(wtype)
+    with torch.no_grad():
+        m.weight.uniform_(0.5, 1.5)
+        m.bias.uniform_(-0.5, 0.5)
+    x = torch.randn(64, hidden, device="cuda").to(itype).requires_grad_(True)
+    y = m(x)
+    assert y.dtype == itype
+    xr = x.detach().float().requires_grad_(True)
+    wr, br = m.weight.detach().float().requires_grad_(True), m.bias.detach().float().requires_grad_(True)
+    ref = torch.nn.functional.layer_norm(xr, (hidden,), wr, br, 1e-5)
+    tol = 2e-2 if itype != torch.float32 else 1e-4
+    torch.testing.assert_close(y.float(), ref, atol=tol, rtol=tol)
+    g = torch.randn_like(ref)
+    y.backward(g.to(itype))
+    ref.backward(g)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=tol * 2, rtol=tol * 2)
+    s = float(wr.grad.abs().max())
+    torch.testing.assert_close(m.weight.grad.float() / s, wr.grad / s, atol=tol, rtol=tol)
+    s = float(br.grad.abs().max())
+    torch.testing.assert_close(m.bias.grad.float() / s, br.grad / s, atol=tol, rtol=tol)

@@ -143,9 +143,34 @@ def bench_adam():
     emit(kernel="fused_adam_fp32", params=n, ms=t, gbps=nbytes / t / 1e6, torch_fused_ms=tr, speedup=tr / t)
 
 
+def bench_attn():
+    from apex.ops.attention import flash_attn_func
+    import torch.nn.functional as F
+
+    for (b, s, h, d, causal) in [(16, 1024, 16, 64, False), (8, 2048, 16, 128, False), (8, 2048, 16, 128, True),
+                                 (4, 4096, 32, 128, True), (32, 512, 16, 64, False)]:
+        q = torch.randn(b, s, h, d, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+        k = torch.randn_like(q, requires_grad=True)
+        v = torch.randn_like(q, requires_grad=True)
+        flops = 4.0 * b * h * s * s * d * (0.5 if causal else 1.0)
+        t = timeit(lambda: flash_attn_func(q, k, v, causal=causal))
+        qt, kt, vt = (x.detach().transpose(1, 2).contiguous().requires_grad_(True) for x in (q, k, v))
+        tr = timeit(lambda: F.scaled_dot_product_attention(qt, kt, vt, is_causal=causal))
+        emit(kernel="flash_fwd", b=b, s=s, h=h, d=d, causal=causal, ms=t, tflops=flops / t / 1e9, sdpa_ms=tr,
+             sdpa_tflops=flops / tr / 1e9, speedup=tr / t)
+        o = flash_attn_func(q, k, v, causal=causal)
+        g = torch.randn_like(o)
+        t = timeit(lambda: torch.autograd.grad(o, (q, k, v), g, retain_graph=True))
+        orr = F.scaled_dot_product_attention(qt, kt, vt, is_causal=causal)
+        gt = g.transpose(1, 2).contiguous()
+        tr = timeit(lambda: torch.autograd.grad(orr, (qt, kt, vt), gt, retain_graph=True))
+        emit(kernel="flash_bwd", b=b, s=s, h=h, d=d, causal=causal, ms=t, tflops=2.5 * flops / t / 1e9, sdpa_ms=tr,
+             sdpa_tflops=2.5 * flops / tr / 1e9, speedup=tr / t)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="gemm,ln,softmax,bn,adam")
+    ap.add_argument("--only", default="attn,gemm,ln,softmax,bn,adam")
     a = ap.parse_args()
     torch.manual_seed(0)
     for name in a.only.split(","):
