@@ -77,6 +77,9 @@ __host__ __device__ inline uint32_t seed_mix_of(uint64_t seed, uint64_t offset) 
   return x;
 }
 
+// v_exp_f32 directly (inputs here are <= 0 or -inf; no denormal range reduction needed)
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 struct Seq {
   int64_t qrow0, krow0;  // token-space base row (side buffers)
   int64_t qoff, koff;    // element offset of the sequence start for the batch stride / varlen row
@@ -235,23 +238,25 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) fwd_kernel(const Attn
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m_i, mx);
     const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-    const float alpha = exp2f(m_i - m_use);
+    const float alpha = fast_exp2(m_i - m_use);
     float ls = 0.f;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(x[t][r] - m_use);
+        const float p = fast_exp2(x[t][r] - m_use);
         ls += p;
         x[t][r] = p;
       }
     ls += __shfl_xor(ls, 32, 64);
     l_i = l_i * alpha + ls;
     m_i = m_new;
+    if (__any(alpha != 1.f)) {  // after the first tiles the running max rarely moves
 #pragma unroll
-    for (int i = 0; i < NDT; ++i)
+      for (int i = 0; i < NDT; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+        for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+    }
     if (dropout) {
 #pragma unroll
       for (int t = 0; t < 2; ++t)
@@ -395,21 +400,49 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
     const uint32_t bh = (uint32_t)(b * a.h + hq);
     const float* biash = a.bias ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh : nullptr;
     const int q_begin = a.causal ? (k_start / QB) * QB : 0;
-    for (int q0 = q_begin; q0 < sq.lq; q0 += QB) {
-      for (int ch = tid; ch < QB * CPR; ch += 256) {
-        const int row = ch / CPR, col = (ch % CPR) * 8, q = q0 + row;
-        const bool ok = q < sq.lq;
-        *reinterpret_cast<uint4*>(Ql + row * QSTR + col) =
-            ok ? *reinterpret_cast<const uint4*>(qp + (int64_t)q * a.q.ss + col) : make_uint4(0, 0, 0, 0);
-        *reinterpret_cast<uint4*>(dOl + row * QSTR + col) =
-            ok ? *reinterpret_cast<const uint4*>(gp + (int64_t)q * ba.dout.ss + col) : make_uint4(0, 0, 0, 0);
+    // next Q / dO slice is fetched into registers under the current slice's MFMAs and written
+    // to LDS after the dQ phase (issue-early / write-late), so no global latency is exposed
+    constexpr int QCH = QB * CPR, QCPT = (QCH + 255) / 256;
+    uint4 pq[QCPT], pg[QCPT];
+    float plse = INFINITY, pdel = 0.f;
+    auto fetch = [&](int q0n) {
+#pragma unroll
+      for (int i = 0; i < QCPT; ++i) {
+        const int ch = tid + 256 * i;
+        if (ch < QCH) {
+          const int row = ch / CPR, col = (ch % CPR) * 8, q = q0n + row;
+          const bool ok = q < sq.lq;
+          pq[i] = ok ? *reinterpret_cast<const uint4*>(qp + (int64_t)q * a.q.ss + col) : make_uint4(0, 0, 0, 0);
+          pg[i] = ok ? *reinterpret_cast<const uint4*>(gp + (int64_t)q * ba.dout.ss + col) : make_uint4(0, 0, 0, 0);
+        }
       }
       if (tid < QB) {
-        const int q = q0 + tid;
-        lse_l[tid] = q < sq.lq ? lse_h[q] : INFINITY;
-        del_l[tid] = q < sq.lq ? del_h[q] : 0.f;
+        const int q = q0n + tid;
+        plse = q < sq.lq ? lse_h[q] : INFINITY;
+        pdel = q < sq.lq ? del_h[q] : 0.f;
       }
-      __syncthreads();
+    };
+    auto commit = [&]() {
+#pragma unroll
+      for (int i = 0; i < QCPT; ++i) {
+        const int ch = tid + 256 * i;
+        if (ch < QCH) {
+          const int row = ch / CPR, col = (ch % CPR) * 8;
+          *reinterpret_cast<uint4*>(Ql + row * QSTR + col) = pq[i];
+          *reinterpret_cast<uint4*>(dOl + row * QSTR + col) = pg[i];
+        }
+      }
+      if (tid < QB) {
+        lse_l[tid] = plse;
+        del_l[tid] = pdel;
+      }
+    };
+    fetch(q_begin);
+    commit();
+    __syncthreads();
+    for (int q0 = q_begin; q0 < sq.lq; q0 += QB) {
+      const bool more = q0 + QB < sq.lq;
+      if (more) fetch(q0 + QB);
 
       // S[q][key] and dP[q][key] with the key on the lane
       f32x16 sacc = zero16(), dpacc = zero16();
@@ -427,7 +460,7 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
         const bool ok = kvalid && q < sq.lq && (!a.causal || mykey <= q);
         float xv = sacc[r] * c - lse_l[qr] * kLog2e;
         if (biash != nullptr && ok) xv += biash[(int64_t)q * a.bias_sq + (int64_t)mykey * a.bias_sk] * kLog2e;
-        const float pv = ok ? exp2f(xv) : 0.f;
+        const float pv = ok ? fast_exp2(xv) : 0.f;
         float dpv = dpacc[r];
         float pd = pv;
         if (dropout) {
@@ -470,6 +503,8 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
         const int q = q0 + crow(r, h2);
         if (q < sq.lq) unsafeAtomicAdd(dq_h + (int64_t)q * a.h * D + 32 * dtq + ql, dq[r] * a.scale);
       }
+      if (more) commit();
+      __syncthreads();
     }
   }
 
@@ -528,7 +563,7 @@ template <typename T, int D>
 void launch_bwd(const AttnBwdArgs& ba, hipStream_t s) {
   const AttnArgs& a = ba.f;
   constexpr int RPB = 256 / (D / 8);
-  hipMemsetAsync(ba.dq_acc, 0, (size_t)a.rows_q * a.h * D * sizeof(float), s);
+  (void)hipMemsetAsync(ba.dq_acc, 0, (size_t)a.rows_q * a.h * D * sizeof(float), s);
   hipLaunchKernelGGL((bwd_delta_kernel<T, D>), dim3((a.sq + RPB - 1) / RPB, a.h, a.b), dim3(256), 0, s, ba);
   hipLaunchKernelGGL((bwd_kernel<T, D>), dim3((a.sk + 127) / 128, a.h_k, a.b), dim3(256), bwd_lds<D>(), s, ba);
   hipLaunchKernelGGL((dq_convert_kernel<T, D>), dim3((a.sq + RPB - 1) / RPB, a.h, a.b), dim3(256), 0, s, ba);

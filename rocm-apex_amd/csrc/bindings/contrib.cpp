@@ -3,6 +3,7 @@
 //   _C.transducer_loss_cuda.forward / backward    (reference apex/contrib/csrc/transducer/transducer_loss.cpp)
 #include "common.h"
 #include "apex_amd/transducer_api.h"
+#include "apex_amd/pool_api.h"
 
 namespace apex_amd {
 
@@ -152,6 +153,50 @@ at::Tensor loss_backward(at::Tensor x, at::Tensor loss_grad, at::Tensor alpha, a
   return xg;
 }
 
+// ---- NHWC max pool: x is a channels_last NCHW tensor (memory [N, H, W, C]) ----
+PoolArgs pool_args(const at::Tensor& x, std::vector<int64_t> k, std::vector<int64_t> st, std::vector<int64_t> pad) {
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "maxpool_nhwc: channels_last 4-D input");
+  PoolArgs a{};
+  a.N = (int)x.size(0);
+  a.C = (int)x.size(1);
+  a.H = (int)x.size(2);
+  a.W = (int)x.size(3);
+  a.KH = (int)k[0];
+  a.KW = (int)k[1];
+  a.SH = (int)st[0];
+  a.SW = (int)st[1];
+  a.PH = (int)pad[0];
+  a.PW = (int)pad[1];
+  a.OH = (a.H + 2 * a.PH - a.KH) / a.SH + 1;
+  a.OW = (a.W + 2 * a.PW - a.KW) / a.SW + 1;
+  a.dtype = dtype_code(x.scalar_type());
+  return a;
+}
+
+std::vector<at::Tensor> maxpool_fwd(at::Tensor x, std::vector<int64_t> k, std::vector<int64_t> st,
+                                    std::vector<int64_t> pad) {
+  const c10::hip::HIPGuard guard(x.get_device());
+  PoolArgs a = pool_args(x, k, st, pad);
+  auto opts = x.options().memory_format(at::MemoryFormat::ChannelsLast);
+  auto y = at::empty({a.N, a.C, a.OH, a.OW}, opts);
+  auto idx = at::empty({a.N, a.C, a.OH, a.OW}, opts.dtype(at::kByte));
+  maxpool_nhwc_fwd(a, x.data_ptr(), y.data_ptr(), idx.data_ptr<uint8_t>(), device_cus(x.get_device()), cur_stream());
+  return {y, idx};
+}
+
+at::Tensor maxpool_bwd(at::Tensor dy, at::Tensor idx, at::Tensor x_like, std::vector<int64_t> k,
+                       std::vector<int64_t> st, std::vector<int64_t> pad) {
+  const c10::hip::HIPGuard guard(dy.get_device());
+  PoolArgs a = pool_args(x_like, k, st, pad);
+  at::Tensor g = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(g.size(2) == a.OH && g.size(3) == a.OW && idx.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "maxpool_nhwc bwd: shape mismatch");
+  auto dx = at::empty(x_like.sizes(), x_like.options().memory_format(at::MemoryFormat::ChannelsLast));
+  maxpool_nhwc_bwd(a, g.data_ptr(), idx.data_ptr<uint8_t>(), dx.data_ptr(), device_cus(dy.get_device()),
+                   cur_stream());
+  return dx;
+}
+
 }  // namespace
 
 void bind_contrib(pybind11::module_& root) {
@@ -161,6 +206,9 @@ void bind_contrib(pybind11::module_& root) {
   auto l = root.def_submodule("transducer_loss_cuda", "RNN-T loss (gfx950)");
   l.def("forward", &loss_forward);
   l.def("backward", &loss_backward);
+  auto p = root.def_submodule("maxpool_nhwc", "channels_last max pooling with 1-byte indices (gfx950)");
+  p.def("forward", &maxpool_fwd);
+  p.def("backward", &maxpool_bwd);
 }
 
 }  // namespace apex_amd

@@ -21,6 +21,8 @@
 //    16-byte vectors (and the 16-byte aux pre-activation for GeLU).
 //  * XCD-aware tile order: consecutive workgroups are dealt round-robin over the 8 XCDs, so the
 //    tile id is remapped to give every XCD a contiguous band of tiles (L2 reuse of A / B panels).
+#include <cstdlib>
+
 #include "apex_amd/device.h"
 #include "apex_amd/dispatch.h"
 #include "apex_amd/gemm_api.h"
@@ -338,6 +340,226 @@ void launch_epi(const GemmArgs& g, hipStream_t s) {
   }
 }
 
+
+// =============================================================================================
+// 256 x 256 x 64 tile (all four operand-major combinations), 8 waves (2 x 4), each wave
+// 128 x 64 = 4 x 2 v_mfma_f32_32x32x16 tiles (128 accumulator registers).  Operands move
+// global -> LDS by LDS-DMA (global_load_lds_dwordx4: no staging registers, no ds_write pass),
+// 2 LDS buffers x (A 32 KB + B 32 KB), the next K-tile's DMA in flight under the current tile's
+// 32 MFMAs per wave, one barrier per K-tile.  The LDS image is lane-linear per DMA instruction
+// (1 KB = 8 rows of 128 B), so the bank swizzle is applied on the SOURCE address: 16-byte chunk
+// c of row r is stored at chunk c ^ ((r >> 1) & 7), which makes the 16 rows read by each
+// 16-lane group of a ds_read_b128 fragment load hit 16 distinct 16-byte slots.
+// Epilogue: accumulators staged through LDS as fp32 in two 128-row halves, then 16-byte
+// row-vector stores with the same bias / activation / derivative epilogues as above.
+// =============================================================================================
+namespace g256 {
+
+constexpr int BM = 256, BN = 256, BK = 64, THREADS = 512;
+constexpr int TILE = BM * BK;          // elements per operand tile (32 KB)
+constexpr int CST = BN + 4;            // epilogue fp32 row stride
+constexpr size_t LDS_BYTES = (size_t)128 * CST * 4 > (size_t)4 * TILE * 2 ? (size_t)128 * CST * 4 : (size_t)4 * TILE * 2;
+
+__device__ __forceinline__ void dma16(const uint16_t* src, uint16_t* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+
+// Issue this wave's 4 DMA pieces for one operand tile.
+// k-major operand (rows = M/N, k contiguous): image [256][64], 1-KB piece = 8 rows of 128 B,
+//   chunk c of row r at c ^ ((r >> 1) & 7)  (row-fragment ds_read_b128, 16 rows -> 16 slots).
+// m-major operand (k rows, M/N contiguous): image [64][256], 1-KB piece = 2 k-rows of 512 B,
+//   chunk c of k-row r at c ^ ((r & 3) << 1) (transposed ds_read_b64_tr_b16: the 4 k-rows a
+//   16-lane group reads start 32 B apart -> conflict-free).
+template <bool KMAJ>
+__device__ __forceinline__ void issue_tile(const uint16_t* __restrict__ X, int64_t ld, int rows, int r0, int k0,
+                                           uint16_t* dst, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = i * 8 + wave;
+    if constexpr (KMAJ) {
+      const int row = 8 * j + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      int gr = r0 + row;
+      gr = gr < rows ? gr : rows - 1;  // rows past the edge are computed but never stored
+      dma16(X + (int64_t)gr * ld + k0 + 8 * c, dst + j * 512);
+    } else {
+      const int krow = 2 * j + (lane >> 5);
+      const int c = (lane & 31) ^ ((krow & 3) << 1);
+      int col = r0 + 8 * c;
+      col = col <= rows - 8 ? col : rows - 8;  // rows % 8 == 0 for m-major operands
+      dma16(X + (int64_t)(k0 + krow) * ld + col, dst + j * 512);
+    }
+  }
+}
+
+template <bool KMAJ>
+__device__ __forceinline__ s16x8 frag_sw(const uint16_t* tile, int rowbase, int kk, int lane) {
+  if constexpr (KMAJ) {
+    const int row = rowbase + (lane & 31);
+    const int c = (2 * kk + (lane >> 5)) ^ ((row >> 1) & 7);
+    return *reinterpret_cast<const s16x8*>(tile + row * BK + 8 * c);
+  } else {
+    const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+    const int kb = 16 * kk + 8 * (g >> 1);
+    const int col = rowbase + 16 * (g & 1) + 4 * p;
+    const int ck = col >> 3, off = col & 7;
+    const int r0 = kb + q, r1 = kb + 4 + q;
+    const s16x4 lo = tr_read(tile + r0 * 256 + ((ck ^ ((r0 & 3) << 1)) << 3) + off);
+    const s16x4 hi = tr_read(tile + r1 * 256 + ((ck ^ ((r1 & 3) << 1)) << 3) + off);
+    return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  }
+}
+
+template <typename T, bool AK, bool BKM, int EPI>
+__global__ void __launch_bounds__(512, 1)
+gemm256_nt(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, T* __restrict__ C, int64_t lda,
+           int64_t ldb, int64_t ldc, int M, int N, int K, const T* __restrict__ bias, const T* __restrict__ aux_in,
+           T* __restrict__ aux_out) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  auto a_buf = [&](int b) { return lds + b * 2 * TILE; };
+  auto b_buf = [&](int b) { return lds + b * 2 * TILE + TILE; };
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  int bm, bn;
+  tile_coords(tiles_m * tiles_n, tiles_m, tiles_n, bm, bn);
+  const int row0 = bm * BM, col0 = bn * BN;
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nk = K / BK;
+  issue_tile<AK>(A, lda, M, row0, 0, a_buf(0), wave, lane);
+  issue_tile<BKM>(B, ldb, N, col0, 0, b_buf(0), wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      issue_tile<AK>(A, lda, M, row0, (kt + 1) * BK, a_buf(cur ^ 1), wave, lane);
+      issue_tile<BKM>(B, ldb, N, col0, (kt + 1) * BK, b_buf(cur ^ 1), wave, lane);
+    }
+    const uint16_t* at = a_buf(cur);
+    const uint16_t* bt = b_buf(cur);
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      s16x8 af[4], bf[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag_sw<AK>(at, wm * 128 + 32 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[j] = frag_sw<BKM>(bt, wn * 64 + 32 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma<T>(af[i], bf[j], acc[i][j]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  float* cs = reinterpret_cast<float*>(lds);
+  const int ch = tid & 31, rsub = tid >> 5;
+  const int gc = col0 + ch * 8;
+  float bv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bv[e] = 0.f;
+  if (bias != nullptr && gc < N) Vec8<T>::load(bv, bias + gc);
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    if (wm == half) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rl = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            cs[rl * CST + wn * 64 + 32 * j + (lane & 31)] = acc[i][j][r];
+          }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int rl = rsub + 16 * it;
+      const int gr = row0 + half * 128 + rl;
+      if (gr < M && gc < N) {
+        float v[8];
+        const float4 lo = *reinterpret_cast<const float4*>(cs + rl * CST + ch * 8);
+        const float4 hi = *reinterpret_cast<const float4*>(cs + rl * CST + ch * 8 + 4);
+        v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+        v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+        const int64_t off = (int64_t)gr * ldc + gc;
+        if constexpr (EPI == kEpiNone) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += bv[e];
+        } else if constexpr (EPI == kEpiGelu) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += bv[e];
+          if (aux_out != nullptr) Vec8<T>::store(aux_out + off, v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
+        } else if constexpr (EPI == kEpiRelu) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] + bv[e], 0.f);
+        } else if constexpr (EPI == kEpiSigmoid) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = 1.f / (1.f + __expf(-(v[e] + bv[e])));
+        } else {
+          float a[8];
+          Vec8<T>::load(a, aux_in + off);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            if constexpr (EPI == kEpiDGelu) v[e] *= dgelu_tanh(a[e]);
+            else if constexpr (EPI == kEpiDRelu) v[e] = a[e] > 0.f ? v[e] : 0.f;
+            else v[e] *= a[e] * (1.f - a[e]);
+          }
+        }
+        Vec8<T>::store(C + off, v);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <typename T, bool AK, bool BKM>
+void launch(const GemmArgs& g, hipStream_t s) {
+  const int tiles = ((g.m + BM - 1) / BM) * ((g.n + BN - 1) / BN);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(tiles), dim3(THREADS), LDS_BYTES, s, (const uint16_t*)g.a, (const uint16_t*)g.b,
+                       (T*)g.c, g.lda, g.ldb, g.ldc, g.m, g.n, g.k, (const T*)g.bias, (const T*)g.aux_in,
+                       (T*)g.aux_out);
+  };
+  switch (g.epilogue) {
+    case kEpiNone: go(gemm256_nt<T, AK, BKM, kEpiNone>); break;
+    case kEpiGelu: go(gemm256_nt<T, AK, BKM, kEpiGelu>); break;
+    case kEpiRelu: go(gemm256_nt<T, AK, BKM, kEpiRelu>); break;
+    case kEpiSigmoid: go(gemm256_nt<T, AK, BKM, kEpiSigmoid>); break;
+    case kEpiDGelu: go(gemm256_nt<T, AK, BKM, kEpiDGelu>); break;
+    case kEpiDRelu: go(gemm256_nt<T, AK, BKM, kEpiDRelu>); break;
+    case kEpiDSigmoid: go(gemm256_nt<T, AK, BKM, kEpiDSigmoid>); break;
+    default: throw std::runtime_error("gemm256: unknown epilogue");
+  }
+}
+
+// the 256-tile kernel needs K % 64 == 0 and enough tiles to fill the chip.
+// APEX_AMD_GEMM256=force|off overrides the size heuristic (tests / A-B timing).
+inline bool usable(const GemmArgs& g, int cus) {
+  if (g.k % BK) return false;
+  const char* env = std::getenv("APEX_AMD_GEMM256");
+  if (env != nullptr && env[0] == 'o') return false;
+  if (env != nullptr && env[0] == 'f') return true;
+  const int64_t tiles = (int64_t)((g.m + BM - 1) / BM) * ((g.n + BN - 1) / BN);
+  return tiles >= cus / 2;
+}
+
+}  // namespace g256
+
 }  // namespace gemm
 
 bool gemm_supported(const GemmArgs& g) {
@@ -355,11 +577,16 @@ bool gemm_supported(const GemmArgs& g) {
   return true;
 }
 
-void gemm_mfma(const GemmArgs& g, int /*cus*/, hipStream_t s) {
+void gemm_mfma(const GemmArgs& g, int cus, hipStream_t s) {
   if (!gemm_supported(g)) throw std::runtime_error("gemm_mfma: unsupported shape/alignment/dtype");
   dispatch_16(g.dtype, [&](auto tag) {
     using T = typename decltype(tag)::type;
-    if (g.a_kmajor && g.b_kmajor) gemm::launch_epi<T, true, true>(g, s);
+    if (gemm::g256::usable(g, cus)) {
+      if (g.a_kmajor && g.b_kmajor) gemm::g256::launch<T, true, true>(g, s);
+      else if (g.a_kmajor) gemm::g256::launch<T, true, false>(g, s);
+      else if (g.b_kmajor) gemm::g256::launch<T, false, true>(g, s);
+      else gemm::g256::launch<T, false, false>(g, s);
+    } else if (g.a_kmajor && g.b_kmajor) gemm::launch_epi<T, true, true>(g, s);
     else if (g.a_kmajor && !g.b_kmajor) gemm::launch_epi<T, true, false>(g, s);
     else if (!g.a_kmajor && g.b_kmajor) gemm::launch_epi<T, false, true>(g, s);
     else gemm::launch_epi<T, false, false>(g, s);

@@ -13,6 +13,8 @@ training-mode batch norm, computed by the gfx950 kernels in fewer HBM passes."""
 import torch
 import torch.nn as nn
 
+from ..ops.pooling import MaxPool2dNHWC
+
 __all__ = ["ResNet", "BasicBlock", "Bottleneck", "resnet18", "resnet34", "resnet50", "resnet101", "resnet152"]
 
 
@@ -102,7 +104,9 @@ class ResNet(nn.Module):
         self.conv1 = nn.Conv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
         self.bn1 = _fused_bn(self.inplanes, True) if fused_bn else self._norm_layer(self.inplanes)
         self.relu = nn.ReLU(inplace=True)
-        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        # fused path (channels_last): gfx950 NHWC max pool with 1-byte indices
+        self.maxpool = MaxPool2dNHWC(kernel_size=3, stride=2, padding=1) if fused_bn else \
+            nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0])
         self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
         self.layer3 = self._make_layer(block, 256, layers[2], stride=2)

@@ -44,6 +44,17 @@ def _col(header, *cands):
     return None
 
 
+def _int(v, default=0):
+    """rocprofv3 writes some ids as text ("Agent 2"): keep the trailing integer."""
+    if v is None or v == "":
+        return default
+    try:
+        return int(v)
+    except ValueError:
+        digits = "".join(ch for ch in str(v).split()[-1] if ch.isdigit())
+        return int(digits) if digits else default
+
+
 def _read_csv(path):
     with open(path, newline="") as f:
         r = csv.reader(f)
@@ -63,22 +74,22 @@ def load_csv(path):
             "queue": ("Queue_Id", "Stream_Id"), "agent": ("Agent_Id", "Device_Id")}.items()}
         for row in rows:
             g = lambda k, d=None: row[ci[k]] if ci[k] is not None and ci[k] < len(row) else d  # noqa: E731
-            kernels.append({"name": g("name"), "start": int(g("start")), "end": int(g("end")),
-                            "corr": int(g("corr", -1) or -1), "tid": int(g("tid", -1) or -1),
-                            "grid": tuple(int(g(k, 1) or 1) for k in ("gx", "gy", "gz")),
-                            "block": tuple(int(g(k, 1) or 1) for k in ("bx", "by", "bz")),
-                            "stream": int(g("queue", 0) or 0), "device": int(g("agent", 0) or 0)})
+            kernels.append({"name": g("name"), "start": _int(g("start")), "end": _int(g("end")),
+                            "corr": _int(g("corr"), -1), "tid": _int(g("tid"), -1),
+                            "grid": tuple(_int(g(k), 1) for k in ("gx", "gy", "gz")),
+                            "block": tuple(_int(g(k), 1) for k in ("bx", "by", "bz")),
+                            "stream": _int(g("queue")), "device": _int(g("agent"))})
     for mpath in _find(path, "marker_api_trace.csv"):
         h, rows = _read_csv(mpath)
         fi, si, ei, ti = (_col(h, "Function", "Message"), _col(h, "Start_Timestamp"), _col(h, "End_Timestamp"),
                           _col(h, "Thread_Id"))
         for row in rows:
-            markers.append((int(row[ti]) if ti is not None else -1, int(row[si]), int(row[ei]), row[fi]))
+            markers.append((_int(row[ti], -1) if ti is not None else -1, _int(row[si]), _int(row[ei]), row[fi]))
     for apath in _find(path, "hip_api_trace.csv"):
         h, rows = _read_csv(apath)
         ci, si, ti = _col(h, "Correlation_Id"), _col(h, "Start_Timestamp"), _col(h, "Thread_Id")
         for row in rows:
-            api[int(row[ci])] = (int(row[ti]) if ti is not None else -1, int(row[si]))
+            api[_int(row[ci])] = (_int(row[ti], -1) if ti is not None else -1, _int(row[si]))
     return kernels, markers, api
 
 

@@ -134,8 +134,35 @@ MODULE_OPS = {"Linear": "linear", "Conv1d": "conv1d", "Conv2d": "conv2d", "Conv3
               "Softmax": "softmax", "Dropout": "dropout"}
 
 
+def _repr_ints(text):
+    out = {}
+    for part in (text or "").split(","):
+        if "=" in part:
+            k, v = part.split("=", 1)
+            try:
+                out[k.strip()] = int(v.strip())
+            except ValueError:
+                pass
+    return out
+
+
+def module_linear(rec):
+    """nn.Linear.forward marker: weight shape from extra_repr (in/out features)."""
+    ts = _tensors(rec.get("args", []))
+    rp = _repr_ints(rec.get("strRepr", ""))
+    if not ts or "in_features" not in rp:
+        return 0, 0, ""
+    x = ts[0]
+    k, n = rp["in_features"], rp["out_features"]
+    m = _n(x) // k
+    eb = _BYTES.get(x.get("dtype"), 4)
+    return 2 * m * n * k, (m * k + n * k + m * n) * eb, "M={},N={},K={}".format(m, n, k)
+
+
 def model_for(rec):
     op, mod = rec.get("op", ""), rec.get("mod", "")
+    if op == "forward" and mod == "Linear":
+        return module_linear(rec)
     if op == "forward" and mod in MODULE_OPS:
         op = MODULE_OPS[mod]
     fn = MODELS.get(op)

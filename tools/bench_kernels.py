@@ -48,9 +48,12 @@ def bench_gemm():
         w = torch.randn(n, k, device="cuda", dtype=dt)
         flops = 2.0 * m * n * k
         t_ours = timeit(lambda: g.linear(a, w, None, g.EPI_NONE, False))
+        os.environ["APEX_AMD_GEMM256"] = "off"
+        t_128 = timeit(lambda: g.linear(a, w, None, g.EPI_NONE, False))
+        os.environ.pop("APEX_AMD_GEMM256")
         t_ref = timeit(lambda: torch.matmul(a, w.t()))
-        emit(kernel="gemm_fwd_nt", m=m, n=n, k=k, ms=t_ours, tflops=flops / t_ours / 1e9, hipblaslt_ms=t_ref,
-             hipblaslt_tflops=flops / t_ref / 1e9, speedup=t_ref / t_ours)
+        emit(kernel="gemm_fwd_nt", m=m, n=n, k=k, ms=t_ours, tflops=flops / t_ours / 1e9, tile128_tflops=flops / t_128 / 1e9,
+             hipblaslt_ms=t_ref, hipblaslt_tflops=flops / t_ref / 1e9, speedup=t_ref / t_ours)
         dy = torch.randn(m, n, device="cuda", dtype=dt)
         t_ours = timeit(lambda: g.linear_dgrad(dy, w, g.EPI_NONE, None))
         t_ref = timeit(lambda: torch.matmul(dy, w))
