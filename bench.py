@@ -32,8 +32,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--batch-size", type=int, default=256, help="per-GPU batch (weak scaling)")
+    ap.add_argument("--batch-size", type=int, default=None,
+                    help="per-GPU batch (weak scaling); default 256 images / the transformer config's micro batch")
     ap.add_argument("--arch", default="resnet50")
+    ap.add_argument("--model", default="resnet", choices=["resnet", "gpt2-medium", "bert-large"],
+                    help="resnet (headline, --arch picks the depth) or a BASELINE.json transformer config")
     ap.add_argument("--opt-level", default="O2")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
     ap.add_argument("--no-channels-last", action="store_true")
@@ -46,11 +49,31 @@ def parse():
     ap.add_argument("--lr", type=float, default=1e-3)
     ap.add_argument("--impl", default="apex", choices=["apex", "torch"],
                     help="torch = stock PyTorch-ROCm baseline (autocast bf16 + AdamW(fused) + torch DDP)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    a.batch_size_set = a.batch_size is not None
+    if a.batch_size is None:
+        a.batch_size = 256
+    return a
+
+
+def _heartbeat(period=30.0):
+    """stderr progress line while the first steps run MIOpen's convolution search (minutes on a
+    fresh box with an empty find-db) so a supervising runner does not take the run for hung."""
+    import threading
+
+    t0 = time.time()
+
+    def run():
+        while True:
+            time.sleep(period)
+            print(f"[bench] running, {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=run, daemon=True).start()
 
 
 def main():
     args = parse()
+    _heartbeat()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -69,6 +92,13 @@ def main():
     from apex.optimizers import FusedAdam
 
     torch.manual_seed(1234 + rank)
+    if args.model != "resnet":
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import bench_transformer
+
+        step, B, S, params = bench_transformer.build(args, dev, distributed)
+        desc = bench_transformer.describe(args, B, S, world, params)
+        return timed(args, step, dev, world, rank, distributed, B, "apex", desc)
     if args.impl == "torch":
         return run_torch_baseline(args, dev, world, rank, distributed, resnet_mod)
     fused_bn = args.bn == "fused" and not (args.sync_bn and distributed) and not args.no_channels_last
@@ -131,7 +161,7 @@ def run_torch_baseline(args, dev, world, rank, distributed, resnet_mod):
     return timed(args, step, dev, world, rank, distributed, B, "torch")
 
 
-def timed(args, step, dev, world, rank, distributed, B, impl):
+def timed(args, step, dev, world, rank, distributed, B, impl, desc=None):
     t0 = time.time()
     for i in range(args.warmup):
         step()
@@ -158,7 +188,15 @@ def timed(args, step, dev, world, rank, distributed, B, impl):
     elapsed = float(t.item())
     ms_per_step = elapsed * 1000.0 / args.steps
     value = world * B * args.steps / elapsed
-    if rank == 0:
+    if rank == 0 and desc is not None:
+        value = world * desc["items_per_gpu_step"] * args.steps / elapsed
+        cfg = dict(desc["config"], final_loss=round(float(loss.item()), 4))
+        res = {"metric": desc["metric"], "value": round(value, 2), "unit": desc["unit"], "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+               "data": "synthetic token ids / labels on GPU; random-init weights", "config": cfg}
+        print(json.dumps(res), flush=True)
+    elif rank == 0:
         res = {
             "metric": "images/sec (whole node) ResNet-50 amp O2 + FusedAdam" if impl == "apex"
             else "images/sec (whole node) ResNet-50 stock torch autocast + AdamW(fused) [baseline]",
@@ -192,7 +230,7 @@ def timed(args, step, dev, world, rank, distributed, B, impl):
             },
         }
         print(json.dumps(res), flush=True)
-    if distributed:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -119,7 +119,7 @@ __device__ __forceinline__ int64_t tensor_off(const AttnTensor& t, const Seq& s,
 // =============================================================================================
 // forward
 // =============================================================================================
-template <typename T, int D>
+template <typename T, int D, bool LAZY>
 __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) fwd_kernel(const AttnArgs a) {
   using G = Geo<D>;
   constexpr int BN = 64, KSTR = G::KSTR, VSTR = G::TSTR, NKK = G::NKK, NDT = G::NDT;
@@ -251,7 +251,9 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) fwd_kernel(const Attn
     ls += __shfl_xor(ls, 32, 64);
     l_i = l_i * alpha + ls;
     m_i = m_new;
-    if (__any(alpha != 1.f)) {  // after the first tiles the running max rarely moves
+    // LAZY: skip the O rescale when no lane's running max moved (after the first tiles it rarely
+    // does); the wave-uniform branch costs MFMA/VALU overlap, so it is a per-head-dim choice
+    if (!LAZY || __any(alpha != 1.f)) {
 #pragma unroll
       for (int i = 0; i < NDT; ++i)
 #pragma unroll
@@ -527,6 +529,334 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Split backward (default): dK/dV and dQ in two atomic-free kernels.
+//
+// The fused kernel above sums dQ over key blocks with fp32 global atomics: (sk / 128) * sq * h * d
+// * 4 B of atomic traffic (2 GB at b8 h16 s2048 d128), and the chip retires atomics at only
+// ~1.3 TB/s of added bytes (MI355X_MICROARCH.md, atomics price list) — that, not the MFMAs, set
+// its time.  Recomputing S and dP once more in a query-major kernel costs 2 extra s^2 d GEMMs
+// (7 instead of 5) but removes every atomic, the fp32 dQ buffer, its memset and the convert pass.
+// ---------------------------------------------------------------------------------------------
+
+// dK, dV: one workgroup = 4 waves = 128 keys (K, V of the wave's 32 keys in registers); 32-query
+// slices of Q / dO (+ lse, delta) double-buffered in LDS, one barrier per slice.
+template <typename T, int D>
+__global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const AttnBwdArgs ba) {
+  const AttnArgs& a = ba.f;
+  using G = Geo<D>;
+  constexpr int BK = 128, QB = 32, NKK = G::NKK, NDT = G::NDT;
+  constexpr int QSTR = G::KSTR;  // row reads (S, dP) and transposed reads (dK, dV)
+  constexpr int CPR = D / 8;
+  constexpr int SLICE = 2 * QB * QSTR + 4 * QB;  // Q, dO images + lse, delta (fp32) in 16-bit units
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  auto Ql = [&](int i) { return lds + i * SLICE; };
+  auto dOl = [&](int i) { return lds + i * SLICE + QB * QSTR; };
+  auto lse_l = [&](int i) { return reinterpret_cast<float*>(lds + i * SLICE + 2 * QB * QSTR); };
+  auto del_l = [&](int i) { return lse_l(i) + QB; };
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h2 = lane >> 5, ql = lane & 31;
+  const int hk = blockIdx.y, b = blockIdx.z;
+  Seq sq;
+  seq_of(a, b, a.q.sb, a.q.ss, a.k.sb, a.k.ss, sq);
+  const int k_start = blockIdx.x * BK;
+  if (k_start >= sq.lk) return;
+  const bool varq = a.cu_q != nullptr, vark = a.cu_k != nullptr;
+  const uint16_t* kp = (const uint16_t*)a.k.p + tensor_off(a.k, sq, false, vark, b) + (int64_t)hk * a.k.sh;
+  const uint16_t* vp = (const uint16_t*)a.v.p + tensor_off(a.v, sq, false, vark, b) + (int64_t)hk * a.v.sh;
+  const int mykey = k_start + wave * 32 + ql;
+  const bool kvalid = mykey < sq.lk;
+  s16x8 kf[NKK], vf[NKK];
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) {
+    if (kvalid) {
+      kf[kk] = *reinterpret_cast<const s16x8*>(kp + (int64_t)mykey * a.k.ss + kk * 16 + 8 * h2);
+      vf[kk] = *reinterpret_cast<const s16x8*>(vp + (int64_t)mykey * a.v.ss + kk * 16 + 8 * h2);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) kf[kk][j] = vf[kk][j] = 0;
+    }
+  }
+  f32x16 dk[NDT], dv[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i) dk[i] = dv[i] = zero16();
+  const float c = a.scale * kLog2e;
+  const bool dropout = a.p_drop > 0.f;
+  const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
+  const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
+  const uint32_t smix = seed_mix_of(a.seed, a.offset);
+  const int group = a.h / a.h_k;
+  constexpr int QCH = QB * CPR, QCPT = (QCH + 255) / 256;
+
+  for (int hq = hk * group; hq < (hk + 1) * group; ++hq) {
+    const uint16_t* qp = (const uint16_t*)a.q.p + tensor_off(a.q, sq, true, varq, b) + (int64_t)hq * a.q.sh;
+    const uint16_t* gp =
+        (const uint16_t*)ba.dout.p + tensor_off(ba.dout, sq, true, varq, b) + (int64_t)hq * ba.dout.sh;
+    const float* lse_h = a.lse + (int64_t)hq * a.rows_q + sq.qrow0;
+    const float* del_h = ba.delta + (int64_t)hq * a.rows_q + sq.qrow0;
+    const uint32_t bh = (uint32_t)(b * a.h + hq);
+    const float* biash = a.bias ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh : nullptr;
+    const int q_begin = a.causal ? (k_start / QB) * QB : 0;
+    uint4 pq[QCPT], pg[QCPT];
+    float plse = INFINITY, pdel = 0.f;
+    auto fetch = [&](int q0n) {
+#pragma unroll
+      for (int i = 0; i < QCPT; ++i) {
+        const int ch = tid + 256 * i;
+        if (ch < QCH) {
+          const int row = ch / CPR, col = (ch % CPR) * 8, q = q0n + row;
+          const bool ok = q < sq.lq;
+          pq[i] = ok ? *reinterpret_cast<const uint4*>(qp + (int64_t)q * a.q.ss + col) : make_uint4(0, 0, 0, 0);
+          pg[i] = ok ? *reinterpret_cast<const uint4*>(gp + (int64_t)q * ba.dout.ss + col) : make_uint4(0, 0, 0, 0);
+        }
+      }
+      if (tid < QB) {
+        const int q = q0n + tid;
+        plse = q < sq.lq ? lse_h[q] : INFINITY;
+        pdel = q < sq.lq ? del_h[q] : 0.f;
+      }
+    };
+    auto commit = [&](int buf) {
+#pragma unroll
+      for (int i = 0; i < QCPT; ++i) {
+        const int ch = tid + 256 * i;
+        if (ch < QCH) {
+          const int row = ch / CPR, col = (ch % CPR) * 8;
+          *reinterpret_cast<uint4*>(Ql(buf) + row * QSTR + col) = pq[i];
+          *reinterpret_cast<uint4*>(dOl(buf) + row * QSTR + col) = pg[i];
+        }
+      }
+      if (tid < QB) {
+        lse_l(buf)[tid] = plse * kLog2e;
+        del_l(buf)[tid] = pdel;
+      }
+    };
+    // the previous head's last slice ended with a barrier: both buffers are free
+    fetch(q_begin);
+    commit(0);
+    __syncthreads();
+    int buf = 0;
+    for (int q0 = q_begin; q0 < sq.lq; q0 += QB, buf ^= 1) {
+      const bool more = q0 + QB < sq.lq;
+      if (more) fetch(q0 + QB);
+      const uint16_t* Qb = Ql(buf);
+      const uint16_t* Gb = dOl(buf);
+      const float* lb = lse_l(buf);
+      const float* db = del_l(buf);
+      f32x16 sacc = zero16(), dpacc = zero16();
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        sacc = mma<T>(frag_rows<QSTR>(Qb, 0, kk, lane), kf[kk], sacc);
+        dpacc = mma<T>(frag_rows<QSTR>(Gb, 0, kk, lane), vf[kk], dpacc);
+      }
+      float p[16], ds[16];
+      const bool edge = !kvalid || q0 + QB > sq.lq || (a.causal && q0 < k_start + wave * 32 + 32);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qr = crow(r, h2), q = q0 + qr;
+        const bool ok = !edge || (kvalid && q < sq.lq && (!a.causal || mykey <= q));
+        float xv = sacc[r] * c - lb[qr];
+        if (biash != nullptr && ok) xv += biash[(int64_t)q * a.bias_sq + (int64_t)mykey * a.bias_sk] * kLog2e;
+        const float pv = ok ? fast_exp2(xv) : 0.f;
+        float dpv = dpacc[r];
+        float pd = pv;
+        if (dropout) {
+          const float mk = drop_hash(smix, bh, (uint32_t)q, (uint32_t)mykey) >= thresh ? inv_keep : 0.f;
+          pd = pv * mk;
+          dpv *= mk;
+        }
+        p[r] = pd;
+        ds[r] = pv * (dpv - db[qr]);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const s16x8 pf = pack8<T>(&p[8 * s2]);
+        const s16x8 dsf = pack8<T>(&ds[8 * s2]);
+        const int klo = 16 * s2 + 4 * h2;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          dv[dt] = mma<T>(frag_tr<QSTR>(Gb, 32 * dt, klo, klo + 8, lane), pf, dv[dt]);
+          dk[dt] = mma<T>(frag_tr<QSTR>(Qb, 32 * dt, klo, klo + 8, lane), dsf, dk[dt]);
+        }
+      }
+      if (more) commit(buf ^ 1);
+      __syncthreads();
+    }
+  }
+
+  if (kvalid) {
+    T* dkp = (T*)ba.dk.p + tensor_off(ba.dk, sq, false, vark, b) + (int64_t)hk * ba.dk.sh + (int64_t)mykey * ba.dk.ss;
+    T* dvp = (T*)ba.dv.p + tensor_off(ba.dv, sq, false, vark, b) + (int64_t)hk * ba.dv.sh + (int64_t)mykey * ba.dv.ss;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 32 * dt + 8 * g4 + 4 * h2;
+        const float s = a.scale;
+        uint32_t k0 = (uint32_t)from_f<T>(dk[dt][4 * g4] * s).x | ((uint32_t)from_f<T>(dk[dt][4 * g4 + 1] * s).x << 16);
+        uint32_t k1 = (uint32_t)from_f<T>(dk[dt][4 * g4 + 2] * s).x | ((uint32_t)from_f<T>(dk[dt][4 * g4 + 3] * s).x << 16);
+        *reinterpret_cast<uint2*>(dkp + d0) = make_uint2(k0, k1);
+        uint32_t v0 = (uint32_t)from_f<T>(dv[dt][4 * g4]).x | ((uint32_t)from_f<T>(dv[dt][4 * g4 + 1]).x << 16);
+        uint32_t v1 = (uint32_t)from_f<T>(dv[dt][4 * g4 + 2]).x | ((uint32_t)from_f<T>(dv[dt][4 * g4 + 3]).x << 16);
+        *reinterpret_cast<uint2*>(dvp + d0) = make_uint2(v0, v1);
+      }
+  }
+}
+
+// dQ: the forward's structure (one workgroup = 4 waves = 128 queries, 64-key tiles of K / V
+// double-buffered in LDS through registers), with Q and dO of the wave's 32 queries in
+// registers.  Per tile: S^T = K Q^T and dP^T = V dO^T (query on the lane), P from the saved lse,
+// dS = P (dP - delta), then dQ^T += K^T dS^T with dS fed from registers (crow() k order).  K is
+// kept as two LDS images: row-read (S) and transposed-read (dQ) paddings differ.
+template <typename T, int D>
+__global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dq_kernel(const AttnBwdArgs ba) {
+  const AttnArgs& a = ba.f;
+  using G = Geo<D>;
+  constexpr int BN = 64, RSTR = G::KSTR, TSTR = G::TSTR, NKK = G::NKK, NDT = G::NDT;
+  constexpr int KT = BN * RSTR, KTT = BN * TSTR, VT = BN * RSTR, TILE = KT + KTT + VT;
+  constexpr int CPR = D / 8;
+  constexpr int CPT = BN * CPR / 256;
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  auto krow = [&](int i) { return lds + i * TILE; };
+  auto ktr = [&](int i) { return lds + i * TILE + KT; };
+  auto vrow = [&](int i) { return lds + i * TILE + KT + KTT; };
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h2 = lane >> 5, ql = lane & 31;
+  const int hq = blockIdx.y, b = blockIdx.z;
+  const int hk = hq / (a.h / a.h_k);
+  Seq sq;
+  seq_of(a, b, a.q.sb, a.q.ss, a.k.sb, a.k.ss, sq);
+  const int q_start = blockIdx.x * 128;
+  if (q_start >= sq.lq) return;
+  const bool varq = a.cu_q != nullptr, vark = a.cu_k != nullptr;
+  const uint16_t* qp = (const uint16_t*)a.q.p + tensor_off(a.q, sq, true, varq, b) + (int64_t)hq * a.q.sh;
+  const uint16_t* gp = (const uint16_t*)ba.dout.p + tensor_off(ba.dout, sq, true, varq, b) + (int64_t)hq * ba.dout.sh;
+  const uint16_t* kp = (const uint16_t*)a.k.p + tensor_off(a.k, sq, false, vark, b) + (int64_t)hk * a.k.sh;
+  const uint16_t* vp = (const uint16_t*)a.v.p + tensor_off(a.v, sq, false, vark, b) + (int64_t)hk * a.v.sh;
+  T* dqp = (T*)ba.dq.p + tensor_off(ba.dq, sq, true, varq, b) + (int64_t)hq * ba.dq.sh;
+
+  const int myq = q_start + wave * 32 + ql;
+  const bool qvalid = myq < sq.lq;
+  s16x8 qf[NKK], gf[NKK];
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) {
+    if (qvalid) {
+      qf[kk] = *reinterpret_cast<const s16x8*>(qp + (int64_t)myq * a.q.ss + kk * 16 + 8 * h2);
+      gf[kk] = *reinterpret_cast<const s16x8*>(gp + (int64_t)myq * ba.dout.ss + kk * 16 + 8 * h2);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[kk][j] = gf[kk][j] = 0;
+    }
+  }
+  const float lse2 = qvalid ? a.lse[(int64_t)hq * a.rows_q + sq.qrow0 + myq] * kLog2e : INFINITY;
+  const float dlt = qvalid ? ba.delta[(int64_t)hq * a.rows_q + sq.qrow0 + myq] : 0.f;
+
+  int k_end = sq.lk;
+  if (a.causal) k_end = min(k_end, q_start + 128);
+  const int nkb = (k_end + BN - 1) / BN;
+
+  uint4 rk[CPT], rv[CPT];
+  auto gload = [&](int kb0) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int ch = tid + 256 * i, row = ch / CPR, col = (ch % CPR) * 8;
+      const int key = kb0 + row;
+      const bool ok = key < sq.lk;
+      rk[i] = ok ? *reinterpret_cast<const uint4*>(kp + (int64_t)key * a.k.ss + col) : make_uint4(0, 0, 0, 0);
+      rv[i] = ok ? *reinterpret_cast<const uint4*>(vp + (int64_t)key * a.v.ss + col) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int ch = tid + 256 * i, row = ch / CPR, col = (ch % CPR) * 8;
+      *reinterpret_cast<uint4*>(krow(buf) + row * RSTR + col) = rk[i];
+      *reinterpret_cast<uint4*>(ktr(buf) + row * TSTR + col) = rk[i];
+      *reinterpret_cast<uint4*>(vrow(buf) + row * RSTR + col) = rv[i];
+    }
+  };
+
+  f32x16 dq[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i) dq[i] = zero16();
+  const float c = a.scale * kLog2e;
+  const bool dropout = a.p_drop > 0.f;
+  const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
+  const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
+  const uint32_t smix = seed_mix_of(a.seed, a.offset);
+  const uint32_t bh = (uint32_t)(b * a.h + hq);
+  const float* biasp = a.bias ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh + (int64_t)myq * a.bias_sq
+                              : nullptr;
+
+  if (nkb > 0) {
+    gload(0);
+    lstore(0);
+  }
+  __syncthreads();
+  for (int it = 0; it < nkb; ++it) {
+    const int cur = it & 1, kb0 = it * BN;
+    const bool more = it + 1 < nkb;
+    if (more) gload(kb0 + BN);
+    const uint16_t* Kr = krow(cur);
+    const uint16_t* Kt = ktr(cur);
+    const uint16_t* Vr = vrow(cur);
+
+    f32x16 s[2] = {zero16(), zero16()}, dp[2] = {zero16(), zero16()};
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      s[0] = mma<T>(frag_rows<RSTR>(Kr, 0, kk, lane), qf[kk], s[0]);
+      s[1] = mma<T>(frag_rows<RSTR>(Kr, 32, kk, lane), qf[kk], s[1]);
+      dp[0] = mma<T>(frag_rows<RSTR>(Vr, 0, kk, lane), gf[kk], dp[0]);
+      dp[1] = mma<T>(frag_rows<RSTR>(Vr, 32, kk, lane), gf[kk], dp[1]);
+    }
+    const bool need_mask = !qvalid || (kb0 + BN > sq.lk) || (a.causal && kb0 + BN - 1 > q_start + wave * 32) ||
+                           biasp != nullptr;
+    float ds[2][16];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb0 + 32 * t + crow(r, h2);
+        float xv = s[t][r] * c - lse2;
+        bool ok = true;
+        if (need_mask) {
+          ok = qvalid && key < sq.lk && (!a.causal || key <= myq);
+          if (biasp != nullptr && ok) xv += biasp[(int64_t)key * a.bias_sk] * kLog2e;
+        }
+        const float pv = ok ? fast_exp2(xv) : 0.f;
+        float dpv = dp[t][r];
+        if (dropout) dpv *= drop_hash(smix, bh, (uint32_t)myq, (uint32_t)key) >= thresh ? inv_keep : 0.f;
+        ds[t][r] = pv * (dpv - dlt);
+      }
+    // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const s16x8 dsf = pack8<T>(&ds[t][8 * s2]);
+        const int klo = 32 * t + 16 * s2 + 4 * h2;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) dq[dt] = mma<T>(frag_tr<TSTR>(Kt, 32 * dt, klo, klo + 8, lane), dsf, dq[dt]);
+      }
+    if (more) lstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  if (qvalid) {
+    T* row = dqp + (int64_t)myq * ba.dq.ss;
+    const float s = a.scale;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 32 * dt + 8 * g4 + 4 * h2;
+        uint32_t w0 = (uint32_t)from_f<T>(dq[dt][4 * g4] * s).x | ((uint32_t)from_f<T>(dq[dt][4 * g4 + 1] * s).x << 16);
+        uint32_t w1 = (uint32_t)from_f<T>(dq[dt][4 * g4 + 2] * s).x | ((uint32_t)from_f<T>(dq[dt][4 * g4 + 3] * s).x << 16);
+        *reinterpret_cast<uint2*>(row + d0) = make_uint2(w0, w1);
+      }
+  }
+}
+
 // dQ (fp32 accumulator [rows][h][D]) -> output dtype with the caller's strides
 template <typename T, int D>
 __global__ void __launch_bounds__(256) dq_convert_kernel(const AttnBwdArgs ba) {
@@ -556,13 +886,32 @@ constexpr size_t bwd_lds() {
 template <typename T, int D>
 void launch_fwd(const AttnArgs& a, hipStream_t s) {
   const dim3 grid((a.sq + 127) / 128, a.h, a.b);
-  hipLaunchKernelGGL((fwd_kernel<T, D>), grid, dim3(256), fwd_lds<D>(), s, a);
+  const char* e = std::getenv("APEX_ATTN_FWD_LAZY");  // A/B override of the per-D default
+  const bool lazy = e == nullptr ? D < 128 : std::atoi(e) > 0;
+  if (lazy) hipLaunchKernelGGL((fwd_kernel<T, D, true>), grid, dim3(256), fwd_lds<D>(), s, a);
+  else hipLaunchKernelGGL((fwd_kernel<T, D, false>), grid, dim3(256), fwd_lds<D>(), s, a);
+}
+
+template <int D>
+constexpr size_t dkdv_lds() {
+  return (size_t)2 * (2 * 32 * Geo<D>::KSTR + 4 * 32) * 2;
+}
+template <int D>
+constexpr size_t dq_lds() {
+  return (size_t)2 * 64 * (2 * Geo<D>::KSTR + Geo<D>::TSTR) * 2;
 }
 
 template <typename T, int D>
 void launch_bwd(const AttnBwdArgs& ba, hipStream_t s) {
   const AttnArgs& a = ba.f;
   constexpr int RPB = 256 / (D / 8);
+  if (ba.dq_acc == nullptr) {  // split, atomic-free path
+    hipLaunchKernelGGL((bwd_delta_kernel<T, D>), dim3((a.sq + RPB - 1) / RPB, a.h, a.b), dim3(256), 0, s, ba);
+    hipLaunchKernelGGL((bwd_dkdv_kernel<T, D>), dim3((a.sk + 127) / 128, a.h_k, a.b), dim3(256), dkdv_lds<D>(), s,
+                       ba);
+    hipLaunchKernelGGL((bwd_dq_kernel<T, D>), dim3((a.sq + 127) / 128, a.h, a.b), dim3(256), dq_lds<D>(), s, ba);
+    return;
+  }
   (void)hipMemsetAsync(ba.dq_acc, 0, (size_t)a.rows_q * a.h * D * sizeof(float), s);
   hipLaunchKernelGGL((bwd_delta_kernel<T, D>), dim3((a.sq + RPB - 1) / RPB, a.h, a.b), dim3(256), 0, s, ba);
   hipLaunchKernelGGL((bwd_kernel<T, D>), dim3((a.sk + 127) / 128, a.h_k, a.b), dim3(256), bwd_lds<D>(), s, ba);

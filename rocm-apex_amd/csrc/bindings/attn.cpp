@@ -128,9 +128,15 @@ std::vector<at::Tensor> bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Ten
   ba.dq = view_of(dq, varlen, "dq");
   ba.dk = view_of(dk, varlen, "dk");
   ba.dv = view_of(dv, varlen, "dv");
-  at::Tensor dq_acc = at::empty({(int64_t)c.a.rows_q * c.a.h * c.a.d}, q.options().dtype(at::kFloat));
+  // head dim <= 64: split atomic-free dK/dV + dQ kernels (2x the fused kernel on MI355X);
+  // head dim 128: the fused kernel summing dQ with fp32 atomics (equal non-causal, 20 % faster
+  // causal: profiles/kernels_attn_r01e.jsonl).  APEX_ATTN_BWD=atomic|split overrides (A/B timing).
+  const char* mode = std::getenv("APEX_ATTN_BWD");
+  const bool atomic = mode != nullptr ? std::string(mode) == "atomic" : c.a.d == 128;
+  at::Tensor dq_acc;
+  if (atomic) dq_acc = at::empty({(int64_t)c.a.rows_q * c.a.h * c.a.d}, q.options().dtype(at::kFloat));
   at::Tensor delta = at::empty({(int64_t)c.a.h * c.a.rows_q}, q.options().dtype(at::kFloat));
-  ba.dq_acc = dq_acc.data_ptr<float>();
+  ba.dq_acc = atomic ? dq_acc.data_ptr<float>() : nullptr;
   ba.delta = delta.data_ptr<float>();
   attn_bwd(ba, cur_stream());
   return {dq, dk, dv};

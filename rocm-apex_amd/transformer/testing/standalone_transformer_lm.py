@@ -131,7 +131,29 @@ class ParallelMLP(MegatronModule):
             skip_bias_add=True, use_cpu_initialization=args.use_cpu_initialization, params_dtype=args.params_dtype,
             sequence_parallel_enabled=args.sequence_parallel)
 
+    def _use_fused(self, x):
+        from ...fused_dense.fused_dense import fused_linear_available
+
+        w1, b1 = self.dense_h_to_4h.weight, self.dense_h_to_4h.bias
+        w2, b2 = self.dense_4h_to_h.weight, self.dense_4h_to_h.bias
+        return (self.bias_gelu_fusion and not self.dense_h_to_4h.sequence_parallel_enabled and b1 is not None
+                and b2 is not None and fused_linear_available(x, w1, b1) and w2.dtype == x.dtype
+                and b2.dtype == x.dtype and w2.shape[0] % 8 == 0 and x.is_contiguous())
+
     def forward(self, hidden_states):
+        if self._use_fused(hidden_states):
+            # one fused_dense pair on the local shard: GEMM + bias + GeLU(tanh) epilogue (aux saved for
+            # the backward), then GEMM; the row-parallel bias is added after the TP reduction
+            from ...fused_dense.fused_dense import FusedDenseGeluDenseFunc
+
+            tp = parallel_state.get_tensor_model_parallel_world_size()
+            x = tensor_parallel.copy_to_tensor_model_parallel_region(hidden_states) if tp > 1 else hidden_states
+            b2 = self.dense_4h_to_h.bias
+            out = FusedDenseGeluDenseFunc.apply(x, self.dense_h_to_4h.weight, self.dense_h_to_4h.bias,
+                                                self.dense_4h_to_h.weight, b2 if tp == 1 else torch.zeros_like(b2))
+            if tp > 1:
+                return tensor_parallel.reduce_from_tensor_model_parallel_region(out), b2
+            return out, None
         inter, bias = self.dense_h_to_4h(hidden_states)
         if self.bias_gelu_fusion:
             inter = bias_gelu(bias, inter)

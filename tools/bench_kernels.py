@@ -146,7 +146,21 @@ def bench_adam():
     emit(kernel="fused_adam_fp32", params=n, ms=t, gbps=nbytes / t / 1e6, torch_fused_ms=tr, speedup=tr / t)
 
 
+def _with_env(name, value, fn):
+    old = os.environ.get(name)
+    os.environ[name] = value
+    try:
+        return fn()
+    finally:
+        if old is None:
+            del os.environ[name]
+        else:
+            os.environ[name] = old
+
+
 def bench_attn():
+    """flash fwd / bwd vs torch SDPA; the kernel variants are timed side by side
+    (fwd: lazy O-rescale on/off; bwd: split atomic-free kernels vs the fused dQ-atomic kernel)."""
     from apex.ops.attention import flash_attn_func
     import torch.nn.functional as F
 
@@ -156,19 +170,23 @@ def bench_attn():
         k = torch.randn_like(q, requires_grad=True)
         v = torch.randn_like(q, requires_grad=True)
         flops = 4.0 * b * h * s * s * d * (0.5 if causal else 1.0)
-        t = timeit(lambda: flash_attn_func(q, k, v, causal=causal))
+        fwd = lambda: flash_attn_func(q, k, v, causal=causal)  # noqa: E731
+        t = timeit(fwd)
+        var = {f"lazy{x}_ms": _with_env("APEX_ATTN_FWD_LAZY", str(x), lambda: timeit(fwd)) for x in (0, 1)}
         qt, kt, vt = (x.detach().transpose(1, 2).contiguous().requires_grad_(True) for x in (q, k, v))
         tr = timeit(lambda: F.scaled_dot_product_attention(qt, kt, vt, is_causal=causal))
         emit(kernel="flash_fwd", b=b, s=s, h=h, d=d, causal=causal, ms=t, tflops=flops / t / 1e9, sdpa_ms=tr,
-             sdpa_tflops=flops / tr / 1e9, speedup=tr / t)
+             sdpa_tflops=flops / tr / 1e9, speedup=tr / t, **var)
         o = flash_attn_func(q, k, v, causal=causal)
         g = torch.randn_like(o)
-        t = timeit(lambda: torch.autograd.grad(o, (q, k, v), g, retain_graph=True))
+        bwd = lambda: torch.autograd.grad(o, (q, k, v), g, retain_graph=True)  # noqa: E731
+        t = timeit(bwd)
+        var = {f"{m}_ms": _with_env("APEX_ATTN_BWD", m, lambda: timeit(bwd)) for m in ("split", "atomic")}
         orr = F.scaled_dot_product_attention(qt, kt, vt, is_causal=causal)
         gt = g.transpose(1, 2).contiguous()
         tr = timeit(lambda: torch.autograd.grad(orr, (qt, kt, vt), gt, retain_graph=True))
         emit(kernel="flash_bwd", b=b, s=s, h=h, d=d, causal=causal, ms=t, tflops=2.5 * flops / t / 1e9, sdpa_ms=tr,
-             sdpa_tflops=2.5 * flops / tr / 1e9, speedup=tr / t)
+             sdpa_tflops=2.5 * flops / tr / 1e9, speedup=tr / t, **var)
 
 
 def main():
