@@ -346,7 +346,13 @@ def _process_optimizer(optimizer, properties):
                     if to_none:
                         param.grad = None
                     else:
-                        param.grad.detach_()
+                        # as torch.optim.Optimizer.zero_grad: grads may be views into a DDP
+                        # bucket (apex.parallel.DistributedDataParallel keeps them there), which
+                        # cannot be detached in place
+                        if param.grad.grad_fn is not None:
+                            param.grad.detach_()
+                        else:
+                            param.grad.requires_grad_(False)
                         param.grad.zero_()
             for param in st.all_fp32_from_fp16_params:
                 param.grad = None

@@ -43,7 +43,10 @@ class FP16_Optimizer(object):
                 if set_grads_to_None:
                     p.grad = None
                 elif p.grad is not None:
-                    p.grad.detach_()
+                    if p.grad.grad_fn is not None:
+                        p.grad.detach_()  # grads may be DDP bucket views
+                    else:
+                        p.grad.requires_grad_(False)
                     p.grad.zero_()
 
     def step(self, closure=None):

@@ -94,3 +94,75 @@ def _convert_worker(rank, world):
 
 def test_convert_syncbn_gloo():
     run_multiprocess(_convert_worker, 2, ())
+
+
+# ------------------------------------------------------------------ DDP race condition
+# (reference tests/distributed/DDP/ddp_race_condition_test.py: message_size=1 so every parameter
+# is its own bucket, allreduce trigger params, 3 allreduce streams / communicators; the gradient
+# sums are analytic, so any bucket fired before its gradient landed, or a stale buffer, shows up)
+def _ddp_race_worker(rank, world, streams, trigger):
+    from apex.parallel import DistributedDataParallel as DDP
+
+    class Model(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = torch.nn.Parameter(torch.ones(4096))
+            self.b = torch.nn.Parameter(torch.ones(4096))
+            self.c = torch.nn.Parameter(torch.ones(2048))
+
+        def forward(self, x):
+            return (self.a * x).sum() + (self.b * x).sum() * 2.0 + (self.c * x[:2048]).sum() * 3.0
+
+    model = Model()
+    kw = dict(message_size=1, num_allreduce_streams=streams)
+    if trigger:
+        kw = dict(allreduce_trigger_params=[model.a, model.c], num_allreduce_streams=streams)
+    ddp = DDP(model, **kw)
+    for it in range(6):
+        for p in model.parameters():
+            p.grad = None
+        x = torch.full((4096,), float((rank + 1) * (it + 1)))
+        ddp(x).backward()
+        mean_x = sum((r + 1) * (it + 1) for r in range(world)) / world
+        assert torch.equal(model.a.grad, torch.full((4096,), mean_x)), (it, model.a.grad[:4])
+        assert torch.equal(model.b.grad, torch.full((4096,), 2.0 * mean_x)), (it, model.b.grad[:4])
+        assert torch.equal(model.c.grad, torch.full((2048,), 3.0 * mean_x)), (it, model.c.grad[:4])
+
+
+@pytest.mark.parametrize("streams,trigger", [(3, False), (1, True), (2, True)])
+def test_ddp_race_condition_gloo(streams, trigger):
+    run_multiprocess(_ddp_race_worker, 2, (streams, trigger))
+
+
+# ------------------------------------------------------------------ amp O2 master params across ranks
+# (reference tests/distributed/amp_master_params: after DDP training with amp O2 the fp32 master
+# params are identical on every rank and the low-precision model params are their casts)
+def _amp_master_worker(rank, world):
+    from apex import amp
+    from apex.optimizers import FusedAdam
+    from apex.parallel import DistributedDataParallel as DDP
+
+    torch.manual_seed(rank)
+    model = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 4))
+    opt = FusedAdam(model.parameters(), lr=1e-2)
+    model, opt = amp.initialize(model, opt, opt_level="O2", cast_model_type=torch.bfloat16, verbosity=0)
+    ddp = DDP(model)
+    for it in range(4):
+        x = torch.randn(8, 16, generator=torch.Generator().manual_seed(100 * rank + it))
+        loss = ddp(x).float().pow(2).mean()
+        opt.zero_grad()
+        with amp.scale_loss(loss, opt) as s:
+            s.backward()
+        opt.step()
+    masters = list(amp.master_params(opt))
+    assert all(p.dtype == torch.float32 for p in masters)
+    flat = torch.cat([p.detach().reshape(-1) for p in masters])
+    gathered = [torch.empty_like(flat) for _ in range(world)]
+    dist.all_gather(gathered, flat)
+    assert torch.equal(gathered[0], gathered[1]), "master params diverged across ranks"
+    for m, p in zip(masters, model.parameters()):
+        torch.testing.assert_close(p.detach().float(), m.detach().to(torch.bfloat16).float(), rtol=0, atol=0)
+
+
+def test_amp_o2_master_params_equal_across_ranks_gloo():
+    run_multiprocess(_amp_master_worker, 2, ())
