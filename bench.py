@@ -79,8 +79,10 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
     if distributed:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group(backend="nccl", init_method="env://")
+        # APEX_BENCH_BACKEND=gloo rehearses the multi-rank path with several ranks sharing one GPU
+        # (correctness only: RCCL needs one GPU per rank)
+        torch.cuda.set_device(local_rank % torch.cuda.device_count())
+        dist.init_process_group(backend=os.environ.get("APEX_BENCH_BACKEND", "nccl"), init_method="env://")
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())

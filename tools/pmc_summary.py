@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Join rocprofv3 hardware-counter passes (tools/gpu_pmc.sh) into one per-kernel table.
+
+Each pass directory holds a ``*counter_collection.csv`` (one row per dispatch x counter) and the
+kernel-trace pass a ``*kernel_trace.csv``.  Per kernel (name truncated) we report mean duration
+and the mean of every counter, plus derived metrics:
+  MFMA util  = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE * 1024 SIMDs)
+  LDS conf   = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (extra LDS cycles per LDS-array cycle)
+  HBM GB/s   = (FETCH_SIZE + WRITE_SIZE) KiB / duration  (FETCH_SIZE under-counts wide streams on
+               gfx950 by up to 2x: cdna_hip_programming.md §7 — read as a lower bound)
+Usage: python tools/pmc_summary.py gpurun_out/pmc [--md profiles/pmc_kernels.md]"""
+import argparse
+import collections
+import csv
+import glob
+import os
+import re
+
+
+def short(name):
+    name = re.sub(r"\(.*", "", name)
+    name = name.replace("void ", "")
+    return name[:90]
+
+
+def load(d):
+    counters = collections.defaultdict(lambda: collections.defaultdict(list))
+    durations = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        per = collections.defaultdict(dict)
+        for r in csv.DictReader(open(f)):
+            key = (r.get("Dispatch_Id") or r.get("Correlation_Id"), short(r["Kernel_Name"]))
+            per[key][r["Counter_Name"]] = per[key].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        for (_, k), vals in per.items():
+            for c, v in vals.items():
+                counters[k][c].append(v)
+    for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            durations[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    return counters, durations
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--md")
+    ap.add_argument("--filter", default="apex_amd::")
+    a = ap.parse_args()
+    counters, durations = load(a.dir)
+    rows = []
+    for k in sorted(set(counters) | set(durations)):
+        if a.filter not in k:
+            continue
+        c = {n: sum(v) / len(v) for n, v in counters[k].items()}
+        dur = sorted(durations.get(k, [0.0]))[len(durations.get(k, [0.0])) // 2]
+        mfma = c.get("SQ_VALU_MFMA_BUSY_CYCLES")
+        gui = c.get("GRBM_GUI_ACTIVE")
+        util = 100.0 * mfma / (gui * 1024) if mfma is not None and gui else None
+        lds = c.get("SQ_LDS_BANK_CONFLICT"), c.get("SQ_LDS_IDX_ACTIVE")
+        conf = 100.0 * lds[0] / lds[1] if lds[0] is not None and lds[1] else None
+        fetch, write = c.get("FETCH_SIZE"), c.get("WRITE_SIZE")
+        gbs = (fetch + write) * 1024 / (dur * 1e3) if fetch is not None and write is not None and dur else None
+        rows.append((k, dur, util, conf, fetch, write, gbs, c))
+    lines = ["| kernel | us (median) | MFMA util % | LDS bank-conflict cycles % | FETCH KiB | WRITE KiB | HBM GB/s (lower bound) | MFMA insts | VALU insts | waves |",
+             "|---|---|---|---|---|---|---|---|---|---|"]
+    fmt = lambda v, f="{:.1f}": "-" if v is None else f.format(v)  # noqa: E731
+    for k, dur, util, conf, fetch, write, gbs, c in rows:
+        lines.append("| `{}` | {} | {} | {} | {} | {} | {} | {} | {} | {} |".format(
+            k, fmt(dur), fmt(util), fmt(conf), fmt(fetch, "{:.0f}"), fmt(write, "{:.0f}"), fmt(gbs, "{:.0f}"),
+            fmt(c.get("SQ_INSTS_MFMA"), "{:.0f}"), fmt(c.get("SQ_INSTS_VALU"), "{:.0f}"),
+            fmt(c.get("SQ_WAVES"), "{:.0f}")))
+    out = "\n".join(lines)
+    print(out)
+    if a.md:
+        with open(a.md, "w") as f:
+            f.write("# Hardware counters of the native gfx950 kernels (1 x MI355X, rocprofv3 --pmc)\n\n")
+            f.write("Source: `tools/gpu_pmc.sh` (one rocprofv3 pass per counter group over `tools/pmc_kernels.py`),"
+                    " joined by `tools/pmc_summary.py`. Mean over 3 calls per kernel.\n\n")
+            f.write(out + "\n")
+
+
+if __name__ == "__main__":
+    main()
