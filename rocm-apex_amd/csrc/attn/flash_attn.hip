@@ -119,7 +119,7 @@ __device__ __forceinline__ int64_t tensor_off(const AttnTensor& t, const Seq& s,
 // =============================================================================================
 // forward
 // =============================================================================================
-template <typename T, int D, bool LAZY>
+template <typename T, int D, bool PLAIN>
 __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) fwd_kernel(const AttnArgs a) {
   using G = Geo<D>;
   constexpr int BN = 64, KSTR = G::KSTR, VSTR = G::TSTR, NKK = G::NKK, NDT = G::NDT;
@@ -184,12 +184,12 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) fwd_kernel(const Attn
   for (int i = 0; i < NDT; ++i) o[i] = zero16();
   float m_i = -INFINITY, l_i = 0.f;
   const float c = a.scale * kLog2e;
-  const bool dropout = a.p_drop > 0.f;
+  const bool dropout = !PLAIN && a.p_drop > 0.f;  // PLAIN: no bias, no dropout (compiled out)
   const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
   const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
   const uint32_t smix = seed_mix_of(a.seed, a.offset);
   const uint32_t bh = (uint32_t)(b * a.h + hq);
-  const float* biasp = a.bias ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh + (int64_t)myq * a.bias_sq
+  const float* biasp = (!PLAIN && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh + (int64_t)myq * a.bias_sq
                               : nullptr;
 
   if (nkb > 0) {
@@ -251,9 +251,9 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) fwd_kernel(const Attn
     ls += __shfl_xor(ls, 32, 64);
     l_i = l_i * alpha + ls;
     m_i = m_new;
-    // LAZY: skip the O rescale when no lane's running max moved (after the first tiles it rarely
-    // does); the wave-uniform branch costs MFMA/VALU overlap, so it is a per-head-dim choice
-    if (!LAZY || __any(alpha != 1.f)) {
+    // skip the O rescale when no lane's running max moved (after the first tiles it rarely does;
+    // measured equal or faster at every head dim: profiles/kernels_attn_r01e.jsonl lazy0/lazy1)
+    if (__any(alpha != 1.f)) {
 #pragma unroll
       for (int i = 0; i < NDT; ++i)
 #pragma unroll
@@ -332,7 +332,7 @@ __global__ void __launch_bounds__(256) bwd_delta_kernel(const AttnBwdArgs ba) {
   if (q < sq.lq && (threadIdx.x % LPR) == 0) ba.delta[(int64_t)hq * a.rows_q + sq.qrow0 + q] = acc;
 }
 
-template <typename T, int D>
+template <typename T, int D, bool PLAIN>
 __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
   const AttnArgs& a = ba.f;
   using G = Geo<D>;
@@ -383,7 +383,7 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
 #pragma unroll
   for (int i = 0; i < NDT; ++i) dk[i] = dv[i] = zero16();
   const float c = a.scale * kLog2e;
-  const bool dropout = a.p_drop > 0.f;
+  const bool dropout = !PLAIN && a.p_drop > 0.f;  // PLAIN: no bias, no dropout (compiled out)
   const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
   const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
   const uint32_t smix = seed_mix_of(a.seed, a.offset);
@@ -400,7 +400,7 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
     const float* del_h = ba.delta + (int64_t)hq * a.rows_q + sq.qrow0;
     float* dq_h = ba.dq_acc + (sq.qrow0 * a.h + hq) * D;
     const uint32_t bh = (uint32_t)(b * a.h + hq);
-    const float* biash = a.bias ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh : nullptr;
+    const float* biash = (!PLAIN && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh : nullptr;
     const int q_begin = a.causal ? (k_start / QB) * QB : 0;
     // next Q / dO slice is fetched into registers under the current slice's MFMAs and written
     // to LDS after the dQ phase (issue-early / write-late), so no global latency is exposed
@@ -456,13 +456,24 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
         dpacc = mma<T>(ag, vf[kk], dpacc);
       }
       float p[16], ds[16];
+      const bool edge = !kvalid || q0 + QB > sq.lq || (a.causal && q0 < k_start + wave * 32 + 32) ||
+                        biash != nullptr;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) p[r] = sacc[r] * c - lse_l[crow(r, h2)] * kLog2e;
+      if (edge) {  // wave-uniform: interior slices run the element loop branch-free
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int q = q0 + crow(r, h2);
+          const bool ok = kvalid && q < sq.lq && (!a.causal || mykey <= q);
+          float xv = p[r];
+          if (biash != nullptr && ok) xv += biash[(int64_t)q * a.bias_sq + (int64_t)mykey * a.bias_sk] * kLog2e;
+          p[r] = ok ? xv : -INFINITY;
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qr = crow(r, h2), q = q0 + qr;
-        const bool ok = kvalid && q < sq.lq && (!a.causal || mykey <= q);
-        float xv = sacc[r] * c - lse_l[qr] * kLog2e;
-        if (biash != nullptr && ok) xv += biash[(int64_t)q * a.bias_sq + (int64_t)mykey * a.bias_sk] * kLog2e;
-        const float pv = ok ? fast_exp2(xv) : 0.f;
+        const float pv = fast_exp2(p[r]);
         float dpv = dpacc[r];
         float pd = pv;
         if (dropout) {
@@ -541,7 +552,7 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
 
 // dK, dV: one workgroup = 4 waves = 128 keys (K, V of the wave's 32 keys in registers); 32-query
 // slices of Q / dO (+ lse, delta) double-buffered in LDS, one barrier per slice.
-template <typename T, int D>
+template <typename T, int D, bool PLAIN>
 __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const AttnBwdArgs ba) {
   const AttnArgs& a = ba.f;
   using G = Geo<D>;
@@ -581,7 +592,7 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
 #pragma unroll
   for (int i = 0; i < NDT; ++i) dk[i] = dv[i] = zero16();
   const float c = a.scale * kLog2e;
-  const bool dropout = a.p_drop > 0.f;
+  const bool dropout = !PLAIN && a.p_drop > 0.f;  // PLAIN: no bias, no dropout (compiled out)
   const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
   const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
   const uint32_t smix = seed_mix_of(a.seed, a.offset);
@@ -595,7 +606,7 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
     const float* lse_h = a.lse + (int64_t)hq * a.rows_q + sq.qrow0;
     const float* del_h = ba.delta + (int64_t)hq * a.rows_q + sq.qrow0;
     const uint32_t bh = (uint32_t)(b * a.h + hq);
-    const float* biash = a.bias ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh : nullptr;
+    const float* biash = (!PLAIN && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh : nullptr;
     const int q_begin = a.causal ? (k_start / QB) * QB : 0;
     uint4 pq[QCPT], pg[QCPT];
     float plse = INFINITY, pdel = 0.f;
@@ -650,14 +661,24 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
         dpacc = mma<T>(frag_rows<QSTR>(Gb, 0, kk, lane), vf[kk], dpacc);
       }
       float p[16], ds[16];
-      const bool edge = !kvalid || q0 + QB > sq.lq || (a.causal && q0 < k_start + wave * 32 + 32);
+      const bool edge = !kvalid || q0 + QB > sq.lq || (a.causal && q0 < k_start + wave * 32 + 32) ||
+                        biash != nullptr;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) p[r] = sacc[r] * c - lb[crow(r, h2)];
+      if (edge) {  // wave-uniform: interior slices run the element loop branch-free
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int q = q0 + crow(r, h2);
+          const bool ok = kvalid && q < sq.lq && (!a.causal || mykey <= q);
+          float xv = p[r];
+          if (biash != nullptr && ok) xv += biash[(int64_t)q * a.bias_sq + (int64_t)mykey * a.bias_sk] * kLog2e;
+          p[r] = ok ? xv : -INFINITY;
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qr = crow(r, h2), q = q0 + qr;
-        const bool ok = !edge || (kvalid && q < sq.lq && (!a.causal || mykey <= q));
-        float xv = sacc[r] * c - lb[qr];
-        if (biash != nullptr && ok) xv += biash[(int64_t)q * a.bias_sq + (int64_t)mykey * a.bias_sk] * kLog2e;
-        const float pv = ok ? fast_exp2(xv) : 0.f;
+        const float pv = fast_exp2(p[r]);
         float dpv = dpacc[r];
         float pd = pv;
         if (dropout) {
@@ -708,7 +729,7 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
 // registers.  Per tile: S^T = K Q^T and dP^T = V dO^T (query on the lane), P from the saved lse,
 // dS = P (dP - delta), then dQ^T += K^T dS^T with dS fed from registers (crow() k order).  K is
 // kept as two LDS images: row-read (S) and transposed-read (dQ) paddings differ.
-template <typename T, int D>
+template <typename T, int D, bool PLAIN>
 __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dq_kernel(const AttnBwdArgs ba) {
   const AttnArgs& a = ba.f;
   using G = Geo<D>;
@@ -780,12 +801,12 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dq_kernel(const A
 #pragma unroll
   for (int i = 0; i < NDT; ++i) dq[i] = zero16();
   const float c = a.scale * kLog2e;
-  const bool dropout = a.p_drop > 0.f;
+  const bool dropout = !PLAIN && a.p_drop > 0.f;  // PLAIN: no bias, no dropout (compiled out)
   const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
   const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
   const uint32_t smix = seed_mix_of(a.seed, a.offset);
   const uint32_t bh = (uint32_t)(b * a.h + hq);
-  const float* biasp = a.bias ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh + (int64_t)myq * a.bias_sq
+  const float* biasp = (!PLAIN && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh + (int64_t)myq * a.bias_sq
                               : nullptr;
 
   if (nkb > 0) {
@@ -815,17 +836,29 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dq_kernel(const A
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kb0 + 32 * t + crow(r, h2);
-        float xv = s[t][r] * c - lse2;
-        bool ok = true;
-        if (need_mask) {
-          ok = qvalid && key < sq.lk && (!a.causal || key <= myq);
+      for (int r = 0; r < 16; ++r) ds[t][r] = s[t][r] * c - lse2;
+    if (need_mask) {  // wave-uniform: the interior tiles run the element loop branch-free
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kb0 + 32 * t + crow(r, h2);
+          const bool ok = qvalid && key < sq.lk && (!a.causal || key <= myq);
+          float xv = ds[t][r];
           if (biasp != nullptr && ok) xv += biasp[(int64_t)key * a.bias_sk] * kLog2e;
+          ds[t][r] = ok ? xv : -INFINITY;
         }
-        const float pv = ok ? fast_exp2(xv) : 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pv = fast_exp2(ds[t][r]);
         float dpv = dp[t][r];
-        if (dropout) dpv *= drop_hash(smix, bh, (uint32_t)myq, (uint32_t)key) >= thresh ? inv_keep : 0.f;
+        if (dropout) {
+          const int key = kb0 + 32 * t + crow(r, h2);
+          dpv *= drop_hash(smix, bh, (uint32_t)myq, (uint32_t)key) >= thresh ? inv_keep : 0.f;
+        }
         ds[t][r] = pv * (dpv - dlt);
       }
     // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
@@ -886,9 +919,7 @@ constexpr size_t bwd_lds() {
 template <typename T, int D>
 void launch_fwd(const AttnArgs& a, hipStream_t s) {
   const dim3 grid((a.sq + 127) / 128, a.h, a.b);
-  const char* e = std::getenv("APEX_ATTN_FWD_LAZY");  // A/B override of the per-D default
-  const bool lazy = e == nullptr ? D < 128 : std::atoi(e) > 0;
-  if (lazy) hipLaunchKernelGGL((fwd_kernel<T, D, true>), grid, dim3(256), fwd_lds<D>(), s, a);
+  if (a.bias == nullptr && !(a.p_drop > 0.f)) hipLaunchKernelGGL((fwd_kernel<T, D, true>), grid, dim3(256), fwd_lds<D>(), s, a);
   else hipLaunchKernelGGL((fwd_kernel<T, D, false>), grid, dim3(256), fwd_lds<D>(), s, a);
 }
 
@@ -901,21 +932,27 @@ constexpr size_t dq_lds() {
   return (size_t)2 * 64 * (2 * Geo<D>::KSTR + Geo<D>::TSTR) * 2;
 }
 
-template <typename T, int D>
-void launch_bwd(const AttnBwdArgs& ba, hipStream_t s) {
+template <typename T, int D, bool PLAIN>
+void launch_bwd_v(const AttnBwdArgs& ba, hipStream_t s) {
   const AttnArgs& a = ba.f;
   constexpr int RPB = 256 / (D / 8);
+  hipLaunchKernelGGL((bwd_delta_kernel<T, D>), dim3((a.sq + RPB - 1) / RPB, a.h, a.b), dim3(256), 0, s, ba);
   if (ba.dq_acc == nullptr) {  // split, atomic-free path
-    hipLaunchKernelGGL((bwd_delta_kernel<T, D>), dim3((a.sq + RPB - 1) / RPB, a.h, a.b), dim3(256), 0, s, ba);
-    hipLaunchKernelGGL((bwd_dkdv_kernel<T, D>), dim3((a.sk + 127) / 128, a.h_k, a.b), dim3(256), dkdv_lds<D>(), s,
+    hipLaunchKernelGGL((bwd_dkdv_kernel<T, D, PLAIN>), dim3((a.sk + 127) / 128, a.h_k, a.b), dim3(256),
+                       dkdv_lds<D>(), s, ba);
+    hipLaunchKernelGGL((bwd_dq_kernel<T, D, PLAIN>), dim3((a.sq + 127) / 128, a.h, a.b), dim3(256), dq_lds<D>(), s,
                        ba);
-    hipLaunchKernelGGL((bwd_dq_kernel<T, D>), dim3((a.sq + 127) / 128, a.h, a.b), dim3(256), dq_lds<D>(), s, ba);
     return;
   }
   (void)hipMemsetAsync(ba.dq_acc, 0, (size_t)a.rows_q * a.h * D * sizeof(float), s);
-  hipLaunchKernelGGL((bwd_delta_kernel<T, D>), dim3((a.sq + RPB - 1) / RPB, a.h, a.b), dim3(256), 0, s, ba);
-  hipLaunchKernelGGL((bwd_kernel<T, D>), dim3((a.sk + 127) / 128, a.h_k, a.b), dim3(256), bwd_lds<D>(), s, ba);
+  hipLaunchKernelGGL((bwd_kernel<T, D, PLAIN>), dim3((a.sk + 127) / 128, a.h_k, a.b), dim3(256), bwd_lds<D>(), s, ba);
   hipLaunchKernelGGL((dq_convert_kernel<T, D>), dim3((a.sq + RPB - 1) / RPB, a.h, a.b), dim3(256), 0, s, ba);
+}
+
+template <typename T, int D>
+void launch_bwd(const AttnBwdArgs& ba, hipStream_t s) {
+  if (ba.f.bias == nullptr && !(ba.f.p_drop > 0.f)) launch_bwd_v<T, D, true>(ba, s);
+  else launch_bwd_v<T, D, false>(ba, s);
 }
 
 }  // namespace attn

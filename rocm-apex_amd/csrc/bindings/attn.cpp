@@ -128,11 +128,11 @@ std::vector<at::Tensor> bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Ten
   ba.dq = view_of(dq, varlen, "dq");
   ba.dk = view_of(dk, varlen, "dk");
   ba.dv = view_of(dv, varlen, "dv");
-  // head dim <= 64: split atomic-free dK/dV + dQ kernels (2x the fused kernel on MI355X);
-  // head dim 128: the fused kernel summing dQ with fp32 atomics (equal non-causal, 20 % faster
-  // causal: profiles/kernels_attn_r01e.jsonl).  APEX_ATTN_BWD=atomic|split overrides (A/B timing).
+  // default: split atomic-free dK/dV + dQ kernels (1.1-3x the fused dQ-atomic kernel at every
+  // head dim once their element loops are branch-free: profiles/kernels_attn_r01e.jsonl);
+  // APEX_ATTN_BWD=atomic selects the fused kernel (kept for A/B timing)
   const char* mode = std::getenv("APEX_ATTN_BWD");
-  const bool atomic = mode != nullptr ? std::string(mode) == "atomic" : c.a.d == 128;
+  const bool atomic = mode != nullptr && std::string(mode) == "atomic";
   at::Tensor dq_acc;
   if (atomic) dq_acc = at::empty({(int64_t)c.a.rows_q * c.a.h * c.a.d}, q.options().dtype(at::kFloat));
   at::Tensor delta = at::empty({(int64_t)c.a.h * c.a.rows_q}, q.options().dtype(at::kFloat));

@@ -174,3 +174,57 @@ def flash_attn_func(q, k, v, dropout_p=0.0, softmax_scale=None, causal=False, bi
         max_seqlen_q, max_seqlen_k = q.size(1), k.size(1)
     return FlashAttnFunc.apply(q, k, v, float(scale), bool(causal), bias, float(dropout_p), seed, offset,
                                cu_seqlens_q, cu_seqlens_k, int(max_seqlen_q), int(max_seqlen_k))
+
+
+class _PackedQKVSelfAttention(torch.autograd.Function):
+    """Self-attention from a fused QKV projection in Megatron layout ``[s, b, heads, 3*d]`` to the
+    context ``[s, b, heads*d]``.  Q / K / V are strided views of the projection, the forward
+    kernel writes the context directly in ``[s, b]`` order and the backward kernel writes dQ / dK /
+    dV into one d(QKV) buffer — autograd never sees the three slices, so there is no per-slice
+    zero-filled gradient, copy and sum, and no transpose copy of the context or its gradient."""
+
+    @staticmethod
+    def forward(ctx, mixed, scale, causal, bias, p, seed, offset):
+        C = _native.require("flash attention")
+        s, b, nh, three_d = mixed.shape
+        d = three_d // 3
+        q, k, v = (mixed[..., i * d:(i + 1) * d].permute(1, 0, 2, 3) for i in range(3))
+        out = torch.empty(s, b, nh, d, device=mixed.device, dtype=mixed.dtype)
+        bias4 = None if bias is None else bias.float()
+        if bias4 is not None:
+            while bias4.dim() < 4:
+                bias4 = bias4.unsqueeze(0)
+        _, lse = C.attn.fwd(q, k, v, None, None, 0, 0, scale, causal, bias4, p, seed, offset, out.permute(1, 0, 2, 3))
+        ctx.save_for_backward(mixed, out, lse, bias4)
+        ctx.meta = (scale, causal, p, seed, offset)
+        return out.view(s, b, nh * d)
+
+    @staticmethod
+    def backward(ctx, dout):
+        C = _native.require("flash attention backward")
+        mixed, out, lse, bias4 = ctx.saved_tensors
+        scale, causal, p, seed, offset = ctx.meta
+        s, b, nh, three_d = mixed.shape
+        d = three_d // 3
+        q, k, v = (mixed[..., i * d:(i + 1) * d].permute(1, 0, 2, 3) for i in range(3))
+        dmixed = torch.empty_like(mixed)
+        dq, dk, dv = (dmixed[..., i * d:(i + 1) * d].permute(1, 0, 2, 3) for i in range(3))
+        g = dout.contiguous().view(s, b, nh, d).permute(1, 0, 2, 3)
+        C.attn.bwd(g, q, k, v, out.permute(1, 0, 2, 3), lse, None, None, 0, 0, scale, causal, bias4, p, seed, offset,
+                   dq, dk, dv)
+        return dmixed, None, None, None, None, None, None
+
+
+def packed_qkv_self_attention(mixed, scale, causal=False, bias=None, dropout_p=0.0, seed=0, offset=0):
+    """``[s, b, heads, 3*d]`` fused-QKV projection -> ``[s, b, heads*d]`` attention context
+    (Megatron self-attention layout; see :class:`_PackedQKVSelfAttention`).  Non-native inputs
+    take :func:`flash_attn_func` on the q / k / v views."""
+    s, b, nh, three_d = mixed.shape
+    d = three_d // 3
+    q, k, v = (mixed[..., i * d:(i + 1) * d].permute(1, 0, 2, 3) for i in range(3))
+    if _native_ok(q, k, v, bias) and mixed.is_contiguous():
+        return _PackedQKVSelfAttention.apply(mixed, float(scale), bool(causal), bias, float(dropout_p), int(seed),
+                                             int(offset))
+    ctx = flash_attn_func(q, k, v, dropout_p=dropout_p, softmax_scale=scale, causal=causal, bias=bias, seed=seed,
+                          offset=offset)
+    return ctx.transpose(0, 1).reshape(s, b, nh * d)

@@ -78,6 +78,49 @@ class _VocabParallelCrossEntropy(torch.autograd.Function):
         return grad_input, None, None
 
 
+class _FusedCrossEntropy(torch.autograd.Function):
+    """Unsharded vocabulary (TP world 1) on a GPU: the gfx950 softmax cross-entropy kernel of
+    apex.contrib.xentropy run straight on the bf16 / fp16 logits (fp32 math inside) — one read of
+    the [tokens, vocab] logits forward, one read + one write backward, instead of an fp32 copy, a
+    materialised fp32 softmax and five elementwise / reduction passes.  Megatron's label
+    smoothing s maps onto the kernel's as s * V / (V - 1) (same loss, same gradient)."""
+
+    @staticmethod
+    def forward(ctx, logits, target, label_smoothing):
+        from ... import _native
+
+        ext = _native.require("xentropy_cuda").xentropy_cuda
+        v = logits.size(-1)
+        x2 = logits.reshape(-1, v)
+        t1 = target.reshape(-1)
+        s = label_smoothing * v / (v - 1) if label_smoothing > 0 else 0.0
+        losses, lse = ext.forward(x2, t1, float(s), True, None)
+        ctx.save_for_backward(x2, lse, t1)
+        ctx.smoothing = s
+        ctx.shape = logits.shape
+        return losses.view(target.shape)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        from ... import _native
+
+        x2, lse, t1 = ctx.saved_tensors
+        grad = _native.require("xentropy_cuda").xentropy_cuda.backward(
+            grad_output.reshape(-1).float().contiguous(), x2, lse, t1, ctx.smoothing, None)
+        return grad.view(ctx.shape), None, None
+
+
+def _fused_ok(logits):
+    from ... import _native
+
+    return (get_tensor_model_parallel_world_size() == 1 and logits.is_cuda and _native.use_native(logits)
+            and _native.submodule("xentropy_cuda") is not None
+            and logits.dtype in (torch.float16, torch.bfloat16, torch.float32))
+
+
 def vocab_parallel_cross_entropy(vocab_parallel_logits, target, label_smoothing=0.0):
-    """Per-token loss for logits sharded along the vocabulary over the TP group."""
+    """Per-token loss for logits sharded along the vocabulary over the TP group (fp32 math;
+    low-precision logits are upcast inside, never materialised in fp32 on the fused path)."""
+    if _fused_ok(vocab_parallel_logits):
+        return _FusedCrossEntropy.apply(vocab_parallel_logits, target, label_smoothing)
     return _VocabParallelCrossEntropy.apply(vocab_parallel_logits, target, label_smoothing)

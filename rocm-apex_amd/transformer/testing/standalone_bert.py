@@ -55,7 +55,7 @@ def post_language_model_processing(lm_output, pooled_output, lm_head, binary_hea
         assert lm_logits.dtype == torch.half
         lm_loss = tensor_parallel.vocab_parallel_cross_entropy(lm_logits, lm_labels)
     else:
-        lm_loss = tensor_parallel.vocab_parallel_cross_entropy(lm_logits.float(), lm_labels)
+        lm_loss = tensor_parallel.vocab_parallel_cross_entropy(lm_logits, lm_labels)  # fp32 math inside
     return lm_loss.transpose(0, 1).contiguous(), binary_logits
 
 

@@ -20,7 +20,7 @@ def post_language_model_processing(lm_output, labels, logit_weights, parallel_ou
         assert output.dtype == torch.half
         loss = tensor_parallel.vocab_parallel_cross_entropy(output, labels)
     else:
-        loss = tensor_parallel.vocab_parallel_cross_entropy(output.float(), labels)
+        loss = tensor_parallel.vocab_parallel_cross_entropy(output, labels)  # fp32 math inside
     return loss.transpose(0, 1).contiguous()  # [b, s]
 
 

@@ -17,7 +17,7 @@ import torch
 import torch.nn.functional as F
 
 from ...normalization import FusedLayerNorm as LayerNorm
-from ...ops.attention import flash_attn_func
+from ...ops.attention import flash_attn_func, packed_qkv_self_attention
 from .. import parallel_state, tensor_parallel
 from ..enums import AttnMaskType, AttnType, LayerType, ModelType
 from ..utils import divide
@@ -198,23 +198,26 @@ class ParallelAttention(MegatronModule):
 
     def forward(self, hidden_states, attention_mask, encoder_output=None, inference_params=None):
         np_, hn = self.num_attention_heads_per_partition, self.hidden_size_per_attention_head
+        causal = self.attn_mask_type == AttnMaskType.causal
+        p = self.attention_dropout if self.training else 0.0
         if self.attention_type == AttnType.self_attn:
             mixed, _ = self.query_key_value(hidden_states)
             s, b = mixed.shape[:2]
-            mixed = mixed.view(s, b, np_, 3 * hn)
-            q, k, v = mixed[..., :hn], mixed[..., hn:2 * hn], mixed[..., 2 * hn:]
-        else:
-            kv, _ = self.key_value(encoder_output)
-            sk, b = kv.shape[:2]
-            kv = kv.view(sk, b, np_, 2 * hn)
-            k, v = kv[..., :hn], kv[..., hn:]
-            q, _ = self.query(hidden_states)
-            q = q.view(q.size(0), b, np_, hn)
+            _attn_calls[0] += 1
+            # q / k / v stay strided views of the projection; context comes back in [s, b, h]
+            ctx = packed_qkv_self_attention(mixed.view(s, b, np_, 3 * hn), self.scale, causal=causal,
+                                            bias=None if causal else attention_mask, dropout_p=p,
+                                            seed=self.seed_base, offset=_attn_calls[0])
+            return self.dense(ctx)
+        kv, _ = self.key_value(encoder_output)
+        sk, b = kv.shape[:2]
+        kv = kv.view(sk, b, np_, 2 * hn)
+        k, v = kv[..., :hn], kv[..., hn:]
+        q, _ = self.query(hidden_states)
+        q = q.view(q.size(0), b, np_, hn)
         # [s, b, np, hn] views -> [b, s, np, hn] views (no copy)
         q4, k4, v4 = (t.permute(1, 0, 2, 3) for t in (q, k, v))
-        causal = self.attn_mask_type == AttnMaskType.causal
         bias = None if causal else attention_mask
-        p = self.attention_dropout if self.training else 0.0
         _attn_calls[0] += 1
         ctx = flash_attn_func(q4, k4, v4, dropout_p=p, softmax_scale=self.scale, causal=causal, bias=bias,
                               seed=self.seed_base, offset=_attn_calls[0])

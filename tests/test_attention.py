@@ -266,3 +266,55 @@ def test_gpu_fmha_vs_reference():
         _close(out[a:e], ref, 2e-2)
         ref.backward(g[a:e].float())
         _close(qkv.grad[a:e].view(-1, 3, 16, 64), xr.grad, 3e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("causal", [False, True])
+def test_gpu_packed_qkv_self_attention_matches_views(causal):
+    """Megatron [s, b, h, 3d] packed path (strided q/k/v, in-place [s, b] context, one d(QKV)
+    buffer) against flash_attn_func on the same views."""
+    from apex.ops.attention import packed_qkv_self_attention
+
+    torch.manual_seed(7)
+    s, b, h, d = 200, 3, 4, 64
+    mixed = torch.randn(s, b, h, 3 * d, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    bias = None
+    if not causal:
+        bias = torch.zeros(b, 1, 1, s, device="cuda")
+        bias[1, ..., 150:] = -10000.0
+    out = packed_qkv_self_attention(mixed, d ** -0.5, causal=causal, bias=bias, dropout_p=0.1, seed=3, offset=9)
+    m2 = mixed.detach().clone().requires_grad_(True)
+    q, k, v = (m2[..., i * d:(i + 1) * d].permute(1, 0, 2, 3) for i in range(3))
+    ref = flash_attn_func(q, k, v, dropout_p=0.1, softmax_scale=d ** -0.5, causal=causal, bias=bias, seed=3, offset=9)
+    ref = ref.transpose(0, 1).reshape(s, b, h * d)
+    torch.testing.assert_close(out, ref, rtol=0, atol=0)
+    g = torch.randn_like(out)
+    out.backward(g)
+    ref.backward(g)
+    torch.testing.assert_close(mixed.grad, m2.grad, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("smoothing", [0.0, 0.1])
+def test_gpu_fused_vocab_cross_entropy(smoothing):
+    """TP-1 fused CE (xentropy kernel on bf16 logits) vs fp32 Megatron-semantics math."""
+    from apex.transformer.tensor_parallel.cross_entropy import _FusedCrossEntropy
+
+    torch.manual_seed(1)
+    s, b, v = 64, 4, 50304
+    logits = (torch.randn(s, b, v, device="cuda") * 3).to(torch.bfloat16).requires_grad_(True)
+    target = torch.randint(0, v, (s, b), device="cuda")
+    loss = _FusedCrossEntropy.apply(logits, target, smoothing)
+    x = logits.detach().float().requires_grad_(True)
+    logp = torch.log_softmax(x, -1)
+    nll = -logp.gather(-1, target.unsqueeze(-1)).squeeze(-1)
+    if smoothing > 0:
+        sm = smoothing * v / (v - 1)
+        ref = (1 - sm) * nll - sm * logp.mean(-1)
+    else:
+        ref = nll
+    torch.testing.assert_close(loss, ref, rtol=1e-4, atol=1e-4)
+    g = torch.rand_like(ref)
+    loss.backward(g)
+    ref.backward(g)
+    torch.testing.assert_close(logits.grad.float(), x.grad, rtol=2e-2, atol=1e-4)

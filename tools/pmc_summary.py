@@ -4,7 +4,8 @@
 Each pass directory holds a ``*counter_collection.csv`` (one row per dispatch x counter) and the
 kernel-trace pass a ``*kernel_trace.csv``.  Per kernel (name truncated) we report mean duration
 and the mean of every counter, plus derived metrics:
-  MFMA util  = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE * 1024 SIMDs)
+  MFMA % peak = SQ_INSTS_MFMA x 32768 FLOP (every MFMA here is v_mfma_f32_32x32x16 bf16/f16)
+                / duration / 2.5 PFLOP/s dense bf16 peak
   LDS conf   = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (extra LDS cycles per LDS-array cycle)
   HBM GB/s   = (FETCH_SIZE + WRITE_SIZE) KiB / duration  (FETCH_SIZE under-counts wide streams on
                gfx950 by up to 2x: cdna_hip_programming.md §7 — read as a lower bound)
@@ -53,15 +54,14 @@ def main():
             continue
         c = {n: sum(v) / len(v) for n, v in counters[k].items()}
         dur = sorted(durations.get(k, [0.0]))[len(durations.get(k, [0.0])) // 2]
-        mfma = c.get("SQ_VALU_MFMA_BUSY_CYCLES")
-        gui = c.get("GRBM_GUI_ACTIVE")
-        util = 100.0 * mfma / (gui * 1024) if mfma is not None and gui else None
+        nm = c.get("SQ_INSTS_MFMA")
+        util = 100.0 * nm * 32768 / (dur * 1e-6) / 2.5e15 if nm and dur else (0.0 if nm == 0 else None)
         lds = c.get("SQ_LDS_BANK_CONFLICT"), c.get("SQ_LDS_IDX_ACTIVE")
         conf = 100.0 * lds[0] / lds[1] if lds[0] is not None and lds[1] else None
         fetch, write = c.get("FETCH_SIZE"), c.get("WRITE_SIZE")
         gbs = (fetch + write) * 1024 / (dur * 1e3) if fetch is not None and write is not None and dur else None
         rows.append((k, dur, util, conf, fetch, write, gbs, c))
-    lines = ["| kernel | us (median) | MFMA util % | LDS bank-conflict cycles % | FETCH KiB | WRITE KiB | HBM GB/s (lower bound) | MFMA insts | VALU insts | waves |",
+    lines = ["| kernel | us (median) | MFMA % of 2.5 PF peak | LDS bank-conflict cycles % | FETCH KiB | WRITE KiB | HBM GB/s (lower bound) | MFMA insts | VALU insts | waves |",
              "|---|---|---|---|---|---|---|---|---|---|"]
     fmt = lambda v, f="{:.1f}": "-" if v is None else f.format(v)  # noqa: E731
     for k, dur, util, conf, fetch, write, gbs, c in rows:
