@@ -53,7 +53,15 @@ at::Tensor run_gemm(const at::Tensor& a, bool a_kmajor, const at::Tensor& b, boo
   }
   TORCH_CHECK(gemm_supported(g), "gemm: unsupported shape/alignment/dtype (need fp16/bf16, K, N multiples of 8, "
               "16-byte aligned operands)");
-  gemm_mfma(g, device_cus(a.get_device()), cur_stream());
+  const int cus = device_cus(a.get_device());
+  at::Tensor ws;  // split-K partials (weight gradients with few output tiles); caching allocator
+  const int64_t wsf = gemm_splitk_workspace_floats(g, cus);
+  const char* sk = std::getenv("APEX_AMD_SPLITK");  // =off disables (A/B timing)
+  if (wsf > 0 && !(sk != nullptr && sk[0] == 'o')) {
+    ws = at::empty({wsf}, a.options().dtype(at::kFloat));
+    g.splitk_ws = ws.data_ptr<float>();
+  }
+  gemm_mfma(g, cus, cur_stream());
   return c;
 }
 

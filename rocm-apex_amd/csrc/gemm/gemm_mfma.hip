@@ -23,6 +23,7 @@
 //    tile id is remapped to give every XCD a contiguous band of tiles (L2 reuse of A / B panels).
 #include <cstdlib>
 
+#include "apex_amd/colreduce.h"
 #include "apex_amd/device.h"
 #include "apex_amd/dispatch.h"
 #include "apex_amd/gemm_api.h"
@@ -301,12 +302,12 @@ __global__ void __launch_bounds__(256) colsum_partial(const T* __restrict__ x, i
 }
 
 template <typename TO>
-__global__ void colsum_finalize(const float* __restrict__ part, int p, int n, TO* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= n) return;
-  float s = 0.f;
-  for (int j = 0; j < p; ++j) s += part[(int64_t)j * n + c];
-  out[c] = from_f<TO>(s);
+__global__ void __launch_bounds__(256) colsum_finalize(const float* __restrict__ part, int p, int n,
+                                                       TO* __restrict__ out) {
+  __shared__ float red[16][17];
+  const float v = colreduce16(part, p, n, red);
+  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
+  if ((threadIdx.x >> 4) == 0 && c < n) out[c] = from_f<TO>(v);
 }
 
 inline int colsum_parts(int64_t m, int n, int cus) {
@@ -415,7 +416,7 @@ template <typename T, bool AK, bool BKM, int EPI>
 __global__ void __launch_bounds__(512, 1)
 gemm256_nt(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, T* __restrict__ C, int64_t lda,
            int64_t ldb, int64_t ldc, int M, int N, int K, const T* __restrict__ bias, const T* __restrict__ aux_in,
-           T* __restrict__ aux_out) {
+           T* __restrict__ aux_out, float* __restrict__ part, int kchunk) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   auto a_buf = [&](int b) { return lds + b * 2 * TILE; };
   auto b_buf = [&](int b) { return lds + b * 2 * TILE + TILE; };
@@ -434,16 +435,18 @@ gemm256_nt(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, T* __
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int nk = K / BK;
-  issue_tile<AK>(A, lda, M, row0, 0, a_buf(0), wave, lane);
-  issue_tile<BKM>(B, ldb, N, col0, 0, b_buf(0), wave, lane);
+  // split-K (part != null): blockIdx.y picks the K chunk, the epilogue stores an fp32 partial
+  const int kbeg = (int)blockIdx.y * kchunk;
+  const int nk = (min(K, kbeg + kchunk) - kbeg) / BK;
+  issue_tile<AK>(A, lda, M, row0, kbeg, a_buf(0), wave, lane);
+  issue_tile<BKM>(B, ldb, N, col0, kbeg, b_buf(0), wave, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) {
-      issue_tile<AK>(A, lda, M, row0, (kt + 1) * BK, a_buf(cur ^ 1), wave, lane);
-      issue_tile<BKM>(B, ldb, N, col0, (kt + 1) * BK, b_buf(cur ^ 1), wave, lane);
+      issue_tile<AK>(A, lda, M, row0, kbeg + (kt + 1) * BK, a_buf(cur ^ 1), wave, lane);
+      issue_tile<BKM>(B, ldb, N, col0, kbeg + (kt + 1) * BK, b_buf(cur ^ 1), wave, lane);
     }
     const uint16_t* at = a_buf(cur);
     const uint16_t* bt = b_buf(cur);
@@ -495,6 +498,12 @@ gemm256_nt(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, T* __
         v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
         v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
         const int64_t off = (int64_t)gr * ldc + gc;
+        if (EPI == kEpiNone && part != nullptr) {
+          float* dst = part + ((int64_t)blockIdx.y * M + gr) * N + gc;
+          *reinterpret_cast<float4*>(dst) = lo;
+          *reinterpret_cast<float4*>(dst + 4) = hi;
+          continue;
+        }
         if constexpr (EPI == kEpiNone) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += bv[e];
@@ -527,13 +536,64 @@ gemm256_nt(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, T* __
   }
 }
 
+// sum of the split-K fp32 partials [S][M][N] (+ bias) -> C, 8 consecutive columns per thread
+template <typename T>
+__global__ void __launch_bounds__(256) splitk_reduce(const float* __restrict__ part, int S, int M, int N,
+                                                     const T* __restrict__ bias, T* __restrict__ C, int64_t ldc) {
+  const int64_t nvec = (int64_t)M * N / 8;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    const int64_t e = i * 8;
+    const int r = (int)(e / N), c = (int)(e % N);
+    float v[8], t[8];
+    Vec8<float>::load(v, part + e);
+    for (int s = 1; s < S; ++s) {
+      Vec8<float>::load(t, part + (int64_t)s * M * N + e);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += t[k];
+    }
+    if (bias != nullptr) {
+      Vec8<T>::load(t, bias + c);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += t[k];
+    }
+    Vec8<T>::store(C + (int64_t)r * ldc + c, v);
+  }
+}
+
+// number of K chunks for a split-K launch of g (1 = no split); chunk length in *kchunk
+inline int splitk_parts(const GemmArgs& g, int cus, int* kchunk) {
+  *kchunk = g.k;
+  if (g.epilogue != kEpiNone || g.k % BK || g.n % 8) return 1;
+  const int64_t tiles = (int64_t)((g.m + BM - 1) / BM) * ((g.n + BN - 1) / BN);
+  if (tiles >= cus || g.k < 2048) return 1;
+  int64_t sp = (cus + tiles - 1) / tiles;
+  if (sp > g.k / 1024) sp = g.k / 1024;
+  if (sp < 2) return 1;
+  const int chunk = (int)(((g.k + sp - 1) / sp + BK - 1) / BK * BK);
+  *kchunk = chunk;
+  return (g.k + chunk - 1) / chunk;
+}
+
 template <typename T, bool AK, bool BKM>
-void launch(const GemmArgs& g, hipStream_t s) {
+void launch(const GemmArgs& g, hipStream_t s, int cus) {
   const int tiles = ((g.m + BM - 1) / BM) * ((g.n + BN - 1) / BN);
+  int kchunk = g.k;
+  const int sp = g.splitk_ws != nullptr ? splitk_parts(g, cus, &kchunk) : 1;
+  if (sp > 1) {
+    hipLaunchKernelGGL((gemm256_nt<T, AK, BKM, kEpiNone>), dim3(tiles, sp), dim3(THREADS), LDS_BYTES, s,
+                       (const uint16_t*)g.a, (const uint16_t*)g.b, (T*)g.c, g.lda, g.ldb, g.ldc, g.m, g.n, g.k,
+                       (const T*)nullptr, (const T*)nullptr, (T*)nullptr, g.splitk_ws, kchunk);
+    const int64_t nvec = (int64_t)g.m * g.n / 8;
+    int64_t grid = (nvec + 255) / 256;
+    if (grid > (int64_t)cus * 8) grid = (int64_t)cus * 8;
+    hipLaunchKernelGGL((splitk_reduce<T>), dim3((unsigned)grid), dim3(256), 0, s, (const float*)g.splitk_ws, sp, g.m,
+                       g.n, (const T*)g.bias, (T*)g.c, g.ldc);
+    return;
+  }
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(tiles), dim3(THREADS), LDS_BYTES, s, (const uint16_t*)g.a, (const uint16_t*)g.b,
                        (T*)g.c, g.lda, g.ldb, g.ldc, g.m, g.n, g.k, (const T*)g.bias, (const T*)g.aux_in,
-                       (T*)g.aux_out);
+                       (T*)g.aux_out, (float*)nullptr, g.k);
   };
   switch (g.epilogue) {
     case kEpiNone: go(gemm256_nt<T, AK, BKM, kEpiNone>); break;
@@ -555,7 +615,8 @@ inline bool usable(const GemmArgs& g, int cus) {
   if (env != nullptr && env[0] == 'o') return false;
   if (env != nullptr && env[0] == 'f') return true;
   const int64_t tiles = (int64_t)((g.m + BM - 1) / BM) * ((g.n + BN - 1) / BN);
-  return tiles >= cus / 2;
+  int kc;
+  return tiles >= cus / 2 || (g.splitk_ws != nullptr && splitk_parts(g, cus, &kc) > 1);
 }
 
 }  // namespace g256
@@ -582,16 +643,23 @@ void gemm_mfma(const GemmArgs& g, int cus, hipStream_t s) {
   dispatch_16(g.dtype, [&](auto tag) {
     using T = typename decltype(tag)::type;
     if (gemm::g256::usable(g, cus)) {
-      if (g.a_kmajor && g.b_kmajor) gemm::g256::launch<T, true, true>(g, s);
-      else if (g.a_kmajor) gemm::g256::launch<T, true, false>(g, s);
-      else if (g.b_kmajor) gemm::g256::launch<T, false, true>(g, s);
-      else gemm::g256::launch<T, false, false>(g, s);
+      if (g.a_kmajor && g.b_kmajor) gemm::g256::launch<T, true, true>(g, s, cus);
+      else if (g.a_kmajor) gemm::g256::launch<T, true, false>(g, s, cus);
+      else if (g.b_kmajor) gemm::g256::launch<T, false, true>(g, s, cus);
+      else gemm::g256::launch<T, false, false>(g, s, cus);
     } else if (g.a_kmajor && g.b_kmajor) gemm::launch_epi<T, true, true>(g, s);
     else if (g.a_kmajor && !g.b_kmajor) gemm::launch_epi<T, true, false>(g, s);
     else if (!g.a_kmajor && g.b_kmajor) gemm::launch_epi<T, false, true>(g, s);
     else gemm::launch_epi<T, false, false>(g, s);
   }, "gemm_mfma");
   check_launch("gemm_mfma");
+}
+
+int64_t gemm_splitk_workspace_floats(const GemmArgs& g, int cus) {
+  if (!gemm_supported(g)) return 0;
+  int kc;
+  const int sp = gemm::g256::splitk_parts(g, cus, &kc);
+  return sp > 1 ? (int64_t)sp * g.m * g.n : 0;
 }
 
 int64_t column_sum_workspace_floats(int64_t m, int n, int cus) { return (int64_t)gemm::colsum_parts(m, n, cus) * n; }
@@ -608,7 +676,7 @@ void column_sum(const void* x, int dtype, int64_t m, int n, int64_t ldx, void* o
   }, "column_sum");
   dispatch_float(out_dtype, [&](auto tag) {
     using TO = typename decltype(tag)::type;
-    hipLaunchKernelGGL((gemm::colsum_finalize<TO>), dim3((n + 255) / 256), dim3(256), 0, s, ws, p, n, (TO*)out);
+    hipLaunchKernelGGL((gemm::colsum_finalize<TO>), dim3((n + 15) / 16), dim3(256), 0, s, ws, p, n, (TO*)out);
   }, "column_sum out");
   check_launch("column_sum");
 }

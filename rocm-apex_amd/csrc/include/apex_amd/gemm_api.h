@@ -37,11 +37,17 @@ struct GemmArgs {
   const void* bias;     // [N] or null
   const void* aux_in;   // [M][ldc] or null
   void* aux_out;        // [M][ldc] or null
+  float* splitk_ws;     // fp32 split-K partials (gemm_splitk_workspace_floats) or null = no split
 };
 
 // true when the shape / alignment / dtype is supported by the MFMA kernel
 bool gemm_supported(const GemmArgs& g);
 void gemm_mfma(const GemmArgs& g, int cus, hipStream_t s);
+// fp32 workspace a split-K launch of g needs (0: the shape runs unsplit).  Split-K is used for
+// no-epilogue GEMMs whose output has too few 256x256 tiles to fill the chip but whose K is long
+// (weight gradients over many tokens): K is cut into chunks of >= 1024, each (tile, chunk)
+// workgroup writes an fp32 partial tile, and a reduce pass sums the chunks and adds the bias.
+int64_t gemm_splitk_workspace_floats(const GemmArgs& g, int cus);
 
 // out[n] = sum_m x[m][n]  (fp32 accumulate, deterministic; used for bias gradients)
 void column_sum(const void* x, int dtype, int64_t m, int n, int64_t ldx, void* out, int out_dtype, float* ws, int cus,

@@ -143,21 +143,13 @@ template <typename TW>
 __global__ void __launch_bounds__(256)
 ln_col_reduce_kernel(const float* __restrict__ part_g, const float* __restrict__ part_b, TW* __restrict__ dgamma,
                      TW* __restrict__ dbeta, int nparts, int n2) {
-  __shared__ float red[4][64];
+  __shared__ float red[16][17];
   const float* part = blockIdx.y == 0 ? part_g : part_b;
   TW* out = blockIdx.y == 0 ? dgamma : dbeta;
-  if (out == nullptr) return;
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int grp = threadIdx.x >> 6;
-  float s = 0.f;
-  if (c < n2)
-    for (int b = grp; b < nparts; b += 4) s += part[(int64_t)b * n2 + c];
-  red[grp][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (grp == 0 && c < n2) {
-    const int l = threadIdx.x & 63;
-    out[c] = from_f<TW>(((red[0][l] + red[1][l]) + red[2][l]) + red[3][l]);
-  }
+  if (out == nullptr) return;  // uniform over the block
+  const float v = colreduce16(part, nparts, n2, red);
+  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
+  if ((threadIdx.x >> 4) == 0 && c < n2) out[c] = from_f<TW>(v);
 }
 
 // Generic path: dx per row (block per row) and dgamma/dbeta partials by a column-tiled pass.
@@ -263,7 +255,7 @@ void norm_bwd_impl(const NormBwdArgs& a, int cus, hipStream_t s) {
       }
     }
     if (want) {
-      hipLaunchKernelGGL((ln_col_reduce_kernel<TW>), dim3((a.n2 + 63) / 64, 2), dim3(256), 0, s, a.workspace,
+      hipLaunchKernelGGL((ln_col_reduce_kernel<TW>), dim3((a.n2 + 15) / 16, 2), dim3(256), 0, s, a.workspace,
                          a.workspace + (int64_t)nparts * a.n2, (TW*)a.dgamma, (TW*)a.dbeta, nparts, a.n2);
     }
   });

@@ -8,6 +8,7 @@
 // no re-read.  Vector j of lane li covers columns [(j*W*64 + li)*8, +8).  Supported fast-path
 // widths: n2 % 8 == 0 and n2 <= 16384; anything else takes the generic block-per-row kernels.
 #pragma once
+#include "apex_amd/colreduce.h"
 #include "apex_amd/device.h"
 #include "apex_amd/dispatch.h"
 #include "apex_amd/norm_api.h"

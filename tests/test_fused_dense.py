@@ -221,3 +221,24 @@ def test_gpu_gemm256_layouts(m, n, k, a_kmajor, b_kmajor, monkeypatch):
     ref = _ref_mm(a, a_kmajor, b, b_kmajor, m, n, k)
     scale = k ** 0.5
     torch.testing.assert_close(c.float() / scale, ref / scale, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,n,k", [(512, 256, 8192), (1000, 1032, 4096), (4096, 1024, 16384)])
+@pytest.mark.parametrize("a_kmajor,b_kmajor", [(False, False), (True, True)])
+@pytest.mark.parametrize("splitk", ["on", "off"])
+def test_gpu_gemm_splitk(m, n, k, a_kmajor, b_kmajor, splitk, monkeypatch):
+    """Few output tiles x long K (weight gradients): split-K launch (fp32 partial tiles + reduce)
+    vs the unsplit kernels, both against fp32 math."""
+    import apex
+
+    if splitk == "off":
+        monkeypatch.setenv("APEX_AMD_SPLITK", "off")
+    g = apex._native.require("gemm").gemm
+    torch.manual_seed(m + n + k)
+    a = torch.randn(m * k, device="cuda").to(torch.bfloat16)
+    b = torch.randn(k * n, device="cuda").to(torch.bfloat16)
+    c, _ = g.matmul(a, a_kmajor, b, b_kmajor, m, n, k)
+    ref = _ref_mm(a, a_kmajor, b, b_kmajor, m, n, k)
+    scale = k ** 0.5
+    torch.testing.assert_close(c.float() / scale, ref / scale, atol=2e-2, rtol=2e-2)

@@ -60,9 +60,10 @@ def bench_gemm():
         emit(kernel="gemm_dgrad_nn", m=m, n=k, k=n, ms=t_ours, tflops=flops / t_ours / 1e9, hipblaslt_ms=t_ref,
              speedup=t_ref / t_ours)
         t_ours = timeit(lambda: g.linear_wgrad(dy, a))
+        t_nosplit = _with_env("APEX_AMD_SPLITK", "off", lambda: timeit(lambda: g.linear_wgrad(dy, a)))
         t_ref = timeit(lambda: torch.matmul(dy.t(), a))
         emit(kernel="gemm_wgrad_tn", m=n, n=k, k=m, ms=t_ours, tflops=flops / t_ours / 1e9, hipblaslt_ms=t_ref,
-             speedup=t_ref / t_ours)
+             speedup=t_ref / t_ours, no_splitk_ms=t_nosplit)
         b = torch.randn(n, device="cuda", dtype=dt)
         t_ours = timeit(lambda: g.linear(a, w, b, g.EPI_GELU, True))
         t_ref = timeit(lambda: torch.nn.functional.gelu(torch.addmm(b, a, w.t()), approximate="tanh"))
