@@ -7,7 +7,41 @@
 
 namespace apex_amd {
 
+void bias_dropout_add_fwd(const void* x, const void* bias, const void* res, void* out, int64_t n, int h, int dtype,
+                          float p, uint64_t seed, uint64_t offset, int cus, hipStream_t s);
+void bias_dropout_add_bwd(const void* g, void* dx, int64_t n, int dtype, float p, uint64_t seed, uint64_t offset, int cus,
+                          hipStream_t s);
+
 namespace {
+
+// out = residual + dropout(x + bias) with a regenerable counter-hash mask (csrc/transformer/bias_dropout_add.hip)
+at::Tensor bda_forward(const at::Tensor& x, const c10::optional<at::Tensor>& bias, const at::Tensor& residual, double p,
+                       int64_t seed, int64_t offset) {
+  TORCH_CHECK(x.is_cuda() && x.sizes() == residual.sizes() && x.scalar_type() == residual.scalar_type(),
+              "bias_dropout_add: x and residual must be same-shape GPU tensors");
+  const c10::hip::HIPGuard guard(x.get_device());
+  at::Tensor xc = x.contiguous(), rc = residual.contiguous();
+  at::Tensor bc;
+  const int h = (int)x.size(-1);
+  if (bias.has_value() && bias->defined()) {
+    bc = bias->contiguous().to(x.scalar_type());
+    TORCH_CHECK(bc.numel() == h, "bias_dropout_add: bias must have the hidden size");
+  }
+  at::Tensor out = at::empty_like(xc);
+  bias_dropout_add_fwd(xc.data_ptr(), bc.defined() ? bc.data_ptr() : nullptr, rc.data_ptr(), out.data_ptr(), xc.numel(),
+                       h, dtype_code(x.scalar_type()), (float)p, (uint64_t)seed, (uint64_t)offset,
+                       device_cus(x.get_device()), cur_stream());
+  return out;
+}
+
+at::Tensor bda_backward(const at::Tensor& g, double p, int64_t seed, int64_t offset) {
+  const c10::hip::HIPGuard guard(g.get_device());
+  at::Tensor gc = g.contiguous();
+  at::Tensor dx = at::empty_like(gc);
+  bias_dropout_add_bwd(gc.data_ptr(), dx.data_ptr(), gc.numel(), dtype_code(g.scalar_type()), (float)p, (uint64_t)seed,
+                       (uint64_t)offset, device_cus(g.get_device()), cur_stream());
+  return dx;
+}
 
 at::Tensor as_int(const at::Tensor& t) { return t.to(at::kInt).contiguous(); }
 
@@ -209,6 +243,11 @@ void bind_contrib(pybind11::module_& root) {
   auto p = root.def_submodule("maxpool_nhwc", "channels_last max pooling with 1-byte indices (gfx950)");
   p.def("forward", &maxpool_fwd);
   p.def("backward", &maxpool_bwd);
+  auto t = root.def_submodule("fused_transformer", "transformer block elementwise fusions (gfx950)");
+  t.def("bias_dropout_add_forward", &bda_forward, pybind11::arg("x"), pybind11::arg("bias"), pybind11::arg("residual"),
+        pybind11::arg("p"), pybind11::arg("seed"), pybind11::arg("offset"));
+  t.def("bias_dropout_add_backward", &bda_backward, pybind11::arg("grad"), pybind11::arg("p"), pybind11::arg("seed"),
+        pybind11::arg("offset"));
 }
 
 }  // namespace apex_amd

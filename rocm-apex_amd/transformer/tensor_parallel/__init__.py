@@ -10,11 +10,12 @@ from .mappings import (copy_to_tensor_model_parallel_region, gather_from_sequenc
                        reduce_scatter_to_sequence_parallel_region, scatter_to_sequence_parallel_region,
                        scatter_to_tensor_model_parallel_region)
 from .memory import MemoryBuffer, RingMemBuffer, allocate_mem_buff, get_mem_buff
-from .random import (CudaRNGStatesTracker, checkpoint, get_cuda_rng_tracker, init_checkpointed_activations_memory_buffer,
+from .random import (CounterRNGStreams, CudaRNGStatesTracker, checkpoint, get_counter_rng_streams, get_cuda_rng_tracker, init_checkpointed_activations_memory_buffer,
                      model_parallel_cuda_manual_seed, reset_checkpointed_activations_memory_buffer)
 from .utils import VocabUtility, split_tensor_along_last_dim
 
 __all__ = [
+    "CounterRNGStreams", "get_counter_rng_streams",
     "vocab_parallel_cross_entropy", "broadcast_data", "ColumnParallelLinear", "RowParallelLinear",
     "VocabParallelEmbedding", "set_tensor_model_parallel_attributes",
     "set_defaults_if_not_set_tensor_model_parallel_attributes", "copy_tensor_model_parallel_attributes",

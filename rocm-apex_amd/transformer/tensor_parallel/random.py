@@ -123,6 +123,35 @@ def get_cuda_rng_tracker():
     return _CUDA_RNG_STATE_TRACKER
 
 
+class CounterRNGStreams:
+    """Call counters of the counter-hash dropout streams (flash-attention probability dropout, the
+    fused bias-dropout-add): a dropout mask here is a pure function of (seed, stream offset,
+    element index), so the offset IS the generator state.  CheckpointFunction saves and restores
+    it with the device generator and the tracker states, so a recomputed segment draws exactly the
+    masks of its original forward."""
+
+    def __init__(self):
+        self.counts = {}
+
+    def next(self, name):
+        c = self.counts.get(name, 0) + 1
+        self.counts[name] = c
+        return c
+
+    def get_states(self):
+        return dict(self.counts)
+
+    def set_states(self, states):
+        self.counts = dict(states)
+
+
+_COUNTER_RNG_STREAMS = CounterRNGStreams()
+
+
+def get_counter_rng_streams():
+    return _COUNTER_RNG_STREAMS
+
+
 def model_parallel_cuda_manual_seed(seed):
     """Seed the default stream with ``seed`` and the tracked TP stream with
     ``seed + 2718 + tp_rank`` (call after initialize_model_parallel)."""
@@ -143,6 +172,7 @@ class CheckpointFunction(torch.autograd.Function):
         ctx.fwd_cpu_rng_state = torch.get_rng_state()
         ctx.fwd_cuda_rng_state = _get_device_rng_state()
         ctx.fwd_cuda_rng_state_tracker = get_cuda_rng_tracker().get_states()
+        ctx.fwd_counter_streams = _COUNTER_RNG_STREAMS.get_states()
         with torch.no_grad():
             outputs = run_function(*args)
         if distribute_saved_activations:
@@ -166,12 +196,15 @@ class CheckpointFunction(torch.autograd.Function):
         torch.set_rng_state(ctx.fwd_cpu_rng_state)
         _set_device_rng_state(ctx.fwd_cuda_rng_state)
         get_cuda_rng_tracker().set_states(ctx.fwd_cuda_rng_state_tracker)
+        bwd_counter_streams = _COUNTER_RNG_STREAMS.get_states()
+        _COUNTER_RNG_STREAMS.set_states(ctx.fwd_counter_streams)
         detached_inputs = detach_variable(inputs)
         with torch.enable_grad():
             outputs = ctx.run_function(*detached_inputs)
         torch.set_rng_state(bwd_cpu_rng_state)
         _set_device_rng_state(bwd_cuda_rng_state)
         get_cuda_rng_tracker().set_states(bwd_cuda_rng_state_tracker)
+        _COUNTER_RNG_STREAMS.set_states(bwd_counter_streams)
         if isinstance(outputs, torch.Tensor):
             outputs = (outputs,)
         torch.autograd.backward(outputs, args)

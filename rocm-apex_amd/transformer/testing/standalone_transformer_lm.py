@@ -18,6 +18,7 @@ import torch.nn.functional as F
 
 from ...normalization import FusedLayerNorm as LayerNorm
 from ...ops.attention import flash_attn_func, packed_qkv_self_attention
+from ..functional.fused_bias_dropout_add import fused_bias_dropout_add
 from .. import parallel_state, tensor_parallel
 from ..enums import AttnMaskType, AttnType, LayerType, ModelType
 from ..utils import divide
@@ -63,8 +64,12 @@ def bias_dropout_add(x, bias, residual, prob, training):
 
 
 def get_bias_dropout_add(training):
+    """The fused gfx950 epilogue (apex.transformer.functional.fused_bias_dropout_add): one kernel
+    per direction, mask regenerated from the "hidden_dropout" counter stream (restored by
+    activation checkpointing like the device RNG)."""
     def _f(x, bias, residual, prob):
-        return bias_dropout_add(x, bias, residual, prob, training)
+        off = tensor_parallel.get_counter_rng_streams().next("hidden_dropout")
+        return fused_bias_dropout_add(x, bias, residual, prob, training, get_args().seed, off)
 
     return _f
 
@@ -162,7 +167,6 @@ class ParallelMLP(MegatronModule):
         return self.dense_4h_to_h(inter)
 
 
-_attn_calls = [0]
 
 
 class ParallelAttention(MegatronModule):
@@ -203,11 +207,11 @@ class ParallelAttention(MegatronModule):
         if self.attention_type == AttnType.self_attn:
             mixed, _ = self.query_key_value(hidden_states)
             s, b = mixed.shape[:2]
-            _attn_calls[0] += 1
+            offset = tensor_parallel.get_counter_rng_streams().next("attention")
             # q / k / v stay strided views of the projection; context comes back in [s, b, h]
             ctx = packed_qkv_self_attention(mixed.view(s, b, np_, 3 * hn), self.scale, causal=causal,
                                             bias=None if causal else attention_mask, dropout_p=p,
-                                            seed=self.seed_base, offset=_attn_calls[0])
+                                            seed=self.seed_base, offset=offset)
             return self.dense(ctx)
         kv, _ = self.key_value(encoder_output)
         sk, b = kv.shape[:2]
@@ -218,9 +222,9 @@ class ParallelAttention(MegatronModule):
         # [s, b, np, hn] views -> [b, s, np, hn] views (no copy)
         q4, k4, v4 = (t.permute(1, 0, 2, 3) for t in (q, k, v))
         bias = None if causal else attention_mask
-        _attn_calls[0] += 1
+        offset = tensor_parallel.get_counter_rng_streams().next("attention")
         ctx = flash_attn_func(q4, k4, v4, dropout_p=p, softmax_scale=self.scale, causal=causal, bias=bias,
-                              seed=self.seed_base, offset=_attn_calls[0])
+                              seed=self.seed_base, offset=offset)
         sq, b = q.shape[0], q.shape[1]
         ctx = ctx.transpose(0, 1).reshape(sq, b, np_ * hn)
         return self.dense(ctx)

@@ -318,3 +318,27 @@ def test_gpu_fused_vocab_cross_entropy(smoothing):
     loss.backward(g)
     ref.backward(g)
     torch.testing.assert_close(logits.grad.float(), x.grad, rtol=2e-2, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_bias", [True, False])
+def test_gpu_fused_bias_dropout_add(with_bias):
+    """gfx950 bias+dropout+residual kernel vs the torch mirror of the same counter-hash mask."""
+    from apex.transformer.functional.fused_bias_dropout_add import _torch_bias_dropout_add, fused_bias_dropout_add
+
+    torch.manual_seed(2)
+    x = torch.randn(128, 4, 1024, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn_like(x, requires_grad=True)
+    b = torch.randn(1024, device="cuda", dtype=torch.bfloat16, requires_grad=True) if with_bias else None
+    y = fused_bias_dropout_add(x, b, r, 0.1, True, 77, 3)
+    x2, r2 = (t.detach().float().requires_grad_(True) for t in (x, r))
+    b2 = b.detach().float().requires_grad_(True) if with_bias else None
+    ref = _torch_bias_dropout_add(x2, b2, r2, 0.1, 77, 3)
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=2e-2)
+    g = torch.randn_like(ref)
+    y.backward(g.to(y.dtype))
+    ref.backward(g)
+    torch.testing.assert_close(x.grad.float(), x2.grad, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(r.grad.float(), r2.grad, atol=1e-2, rtol=1e-2)
+    if with_bias:
+        torch.testing.assert_close(b.grad.float(), b2.grad, atol=0.5, rtol=2e-2)

@@ -258,3 +258,25 @@ def _no_pipe_worker(rank, world):
 
 def test_no_pipelining_gloo():
     run_multiprocess(_no_pipe_worker, world=2)
+
+
+def test_bias_dropout_add_mask_statistics_and_checkpoint_restore():
+    """Counter-hash dropout: keep rate matches p, masks are a pure function of (seed, offset),
+    and activation checkpointing restores the counter streams so a recompute redraws them."""
+    from apex.transformer.functional.fused_bias_dropout_add import fused_bias_dropout_add, keep_mask
+    from apex.transformer.tensor_parallel import get_counter_rng_streams
+
+    keep = keep_mask(5, 11, 1 << 20, 0.1)
+    assert abs(keep.float().mean().item() - 0.9) < 2e-3
+    assert torch.equal(keep, keep_mask(5, 11, 1 << 20, 0.1))
+    assert not torch.equal(keep, keep_mask(5, 12, 1 << 20, 0.1))
+    x, r, b = torch.randn(64, 32), torch.randn(64, 32), torch.randn(32)
+    y = fused_bias_dropout_add(x, b, r, 0.1, True, 5, 11)
+    k = keep_mask(5, 11, x.numel(), 0.1).view(x.shape)
+    torch.testing.assert_close(y, r + torch.where(k, (x + b) / 0.9, torch.zeros_like(x)))
+    torch.testing.assert_close(fused_bias_dropout_add(x, b, r, 0.1, False, 5, 11), r + (x + b))
+    st = get_counter_rng_streams()
+    saved = st.get_states()
+    a = st.next("hidden_dropout")
+    st.set_states(saved)
+    assert st.next("hidden_dropout") == a
