@@ -135,171 +135,179 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) fwd_kernel(const Attn
   const int hk = hq / (a.h / a.h_k);
   Seq sq;
   seq_of(a, b, a.q.sb, a.q.ss, a.k.sb, a.k.ss, sq);
-  const int q_start = blockIdx.x * 128;
-  if (q_start >= sq.lq) return;  // uniform over the workgroup
-  const bool varq = a.cu_q != nullptr, vark = a.cu_k != nullptr;
-  const uint16_t* qp = (const uint16_t*)a.q.p + tensor_off(a.q, sq, true, varq, b) + (int64_t)hq * a.q.sh;
-  const uint16_t* kp = (const uint16_t*)a.k.p + tensor_off(a.k, sq, false, vark, b) + (int64_t)hk * a.k.sh;
-  const uint16_t* vp = (const uint16_t*)a.v.p + tensor_off(a.v, sq, false, vark, b) + (int64_t)hk * a.v.sh;
-  T* op = (T*)a.o.p + tensor_off(a.o, sq, true, varq, b) + (int64_t)hq * a.o.sh;
+  // causal: workgroup x also runs block n-1-x (work per block grows / shrinks linearly with x), so
+  // every workgroup does the same number of tiles
+  const int nblk = (a.sq + 127) / 128;
+  for (int pass = 0; pass < (a.causal ? 2 : 1); ++pass) {
+    const int blk = pass == 0 ? (int)blockIdx.x : nblk - 1 - (int)blockIdx.x;
+    if (pass == 1 && blk <= (int)blockIdx.x) break;
+    const int q_start = blk * 128;
+    if (q_start >= sq.lq) continue;  // uniform over the workgroup
+    const bool varq = a.cu_q != nullptr, vark = a.cu_k != nullptr;
+    const uint16_t* qp = (const uint16_t*)a.q.p + tensor_off(a.q, sq, true, varq, b) + (int64_t)hq * a.q.sh;
+    const uint16_t* kp = (const uint16_t*)a.k.p + tensor_off(a.k, sq, false, vark, b) + (int64_t)hk * a.k.sh;
+    const uint16_t* vp = (const uint16_t*)a.v.p + tensor_off(a.v, sq, false, vark, b) + (int64_t)hk * a.v.sh;
+    T* op = (T*)a.o.p + tensor_off(a.o, sq, true, varq, b) + (int64_t)hq * a.o.sh;
 
-  const int myq = q_start + wave * 32 + ql;
-  const bool qvalid = myq < sq.lq;
-  s16x8 qf[NKK];
-#pragma unroll
-  for (int kk = 0; kk < NKK; ++kk) {
-    if (qvalid) qf[kk] = *reinterpret_cast<const s16x8*>(qp + (int64_t)myq * a.q.ss + kk * 16 + 8 * h2);
-    else
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[kk][j] = 0;
-  }
-
-  int k_end = sq.lk;
-  if (a.causal) k_end = min(k_end, q_start + 128);
-  const int nkb = (k_end + BN - 1) / BN;
-  const int wave_q_last = min(q_start + wave * 32 + 31, sq.lq - 1);
-
-  uint4 rk[CPT], rv[CPT];
-  auto gload = [&](int kb0) {
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int ch = tid + 256 * i, row = ch / CPR, col = (ch % CPR) * 8;
-      const int key = kb0 + row;
-      const bool ok = key < sq.lk;
-      rk[i] = ok ? *reinterpret_cast<const uint4*>(kp + (int64_t)key * a.k.ss + col) : make_uint4(0, 0, 0, 0);
-      rv[i] = ok ? *reinterpret_cast<const uint4*>(vp + (int64_t)key * a.v.ss + col) : make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto lstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int ch = tid + 256 * i, row = ch / CPR, col = (ch % CPR) * 8;
-      *reinterpret_cast<uint4*>(kbuf(buf) + row * KSTR + col) = rk[i];
-      *reinterpret_cast<uint4*>(vbuf(buf) + row * VSTR + col) = rv[i];
-    }
-  };
-
-  f32x16 o[NDT];
-#pragma unroll
-  for (int i = 0; i < NDT; ++i) o[i] = zero16();
-  float m_i = -INFINITY, l_i = 0.f;
-  const float c = a.scale * kLog2e;
-  const bool dropout = !PLAIN && a.p_drop > 0.f;  // PLAIN: no bias, no dropout (compiled out)
-  const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
-  const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
-  const uint32_t smix = seed_mix_of(a.seed, a.offset);
-  const uint32_t bh = (uint32_t)(b * a.h + hq);
-  const float* biasp = (!PLAIN && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh + (int64_t)myq * a.bias_sq
-                              : nullptr;
-
-  if (nkb > 0) {
-    gload(0);
-    lstore(0);
-  }
-  __syncthreads();
-  for (int it = 0; it < nkb; ++it) {
-    const int cur = it & 1, kb0 = it * BN;
-    const bool more = it + 1 < nkb;
-    if (more) gload(kb0 + BN);
-    const uint16_t* Kl = kbuf(cur);
-    const uint16_t* Vl = vbuf(cur);
-
-    f32x16 s[2] = {zero16(), zero16()};
-#pragma unroll
+    const int myq = q_start + wave * 32 + ql;
+    const bool qvalid = myq < sq.lq;
+    s16x8 qf[NKK];
+    #pragma unroll
     for (int kk = 0; kk < NKK; ++kk) {
-      const s16x8 a0 = frag_rows<KSTR>(Kl, 0, kk, lane);
-      const s16x8 a1 = frag_rows<KSTR>(Kl, 32, kk, lane);
-      s[0] = mma<T>(a0, qf[kk], s[0]);
-      s[1] = mma<T>(a1, qf[kk], s[1]);
+      if (qvalid) qf[kk] = *reinterpret_cast<const s16x8*>(qp + (int64_t)myq * a.q.ss + kk * 16 + 8 * h2);
+      else
+        #pragma unroll
+        for (int j = 0; j < 8; ++j) qf[kk][j] = 0;
     }
-    float x[2][16];
-    const bool need_mask = (kb0 + BN > sq.lk) || (a.causal && kb0 + BN - 1 > q_start + wave * 32) || biasp != nullptr;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) x[t][r] = s[t][r] * c;
-    if (need_mask) {
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kb0 + 32 * t + crow(r, h2);
-          const bool ok = key < sq.lk && (!a.causal || key <= myq);
-          float v = x[t][r];
-          if (biasp != nullptr && ok && qvalid) v += biasp[(int64_t)key * a.bias_sk] * kLog2e;
-          x[t][r] = ok ? v : -INFINITY;
-        }
-    }
-    float mx = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, x[t][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_i, mx);
-    const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-    const float alpha = fast_exp2(m_i - m_use);
-    float ls = 0.f;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = fast_exp2(x[t][r] - m_use);
-        ls += p;
-        x[t][r] = p;
-      }
-    ls += __shfl_xor(ls, 32, 64);
-    l_i = l_i * alpha + ls;
-    m_i = m_new;
-    // skip the O rescale when no lane's running max moved (after the first tiles it rarely does;
-    // measured equal or faster at every head dim: profiles/kernels_attn_r01e.jsonl lazy0/lazy1)
-    if (__any(alpha != 1.f)) {
-#pragma unroll
-      for (int i = 0; i < NDT; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
-    }
-    if (dropout) {
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const uint32_t key = (uint32_t)(kb0 + 32 * t + crow(r, h2));
-          x[t][r] *= drop_hash(smix, bh, (uint32_t)myq, key) >= thresh ? inv_keep : 0.f;
-        }
-    }
-    // O^T[d][q] += V^T[d][key] P^T[key][q]
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const s16x8 pf = pack8<T>(&x[t][8 * s2]);
-        const int klo = 32 * t + 16 * s2 + 4 * h2;
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) {
-          const s16x8 vf = frag_tr<VSTR>(Vl, 32 * dt, klo, klo + 8, lane);
-          o[dt] = mma<T>(vf, pf, o[dt]);
-        }
-      }
-    if (more) lstore(cur ^ 1);
-    __syncthreads();
-  }
-  (void)wave_q_last;
 
-  if (qvalid) {
-    const float inv_l = l_i > 0.f ? 1.f / l_i : 0.f;
-    T* orow = op + (int64_t)myq * a.o.ss;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d0 = 32 * dt + 8 * g4 + 4 * h2;
-        uint32_t w0 = (uint32_t)from_f<T>(o[dt][4 * g4] * inv_l).x | ((uint32_t)from_f<T>(o[dt][4 * g4 + 1] * inv_l).x << 16);
-        uint32_t w1 = (uint32_t)from_f<T>(o[dt][4 * g4 + 2] * inv_l).x | ((uint32_t)from_f<T>(o[dt][4 * g4 + 3] * inv_l).x << 16);
-        *reinterpret_cast<uint2*>(orow + d0) = make_uint2(w0, w1);
+    int k_end = sq.lk;
+    if (a.causal) k_end = min(k_end, q_start + 128);
+    const int nkb = (k_end + BN - 1) / BN;
+    const int wave_q_last = min(q_start + wave * 32 + 31, sq.lq - 1);
+
+    uint4 rk[CPT], rv[CPT];
+    auto gload = [&](int kb0) {
+      #pragma unroll
+      for (int i = 0; i < CPT; ++i) {
+        const int ch = tid + 256 * i, row = ch / CPR, col = (ch % CPR) * 8;
+        const int key = kb0 + row;
+        const bool ok = key < sq.lk;
+        rk[i] = ok ? *reinterpret_cast<const uint4*>(kp + (int64_t)key * a.k.ss + col) : make_uint4(0, 0, 0, 0);
+        rv[i] = ok ? *reinterpret_cast<const uint4*>(vp + (int64_t)key * a.v.ss + col) : make_uint4(0, 0, 0, 0);
       }
-    if (h2 == 0 && a.lse != nullptr)
-      a.lse[(int64_t)hq * a.rows_q + sq.qrow0 + myq] = l_i > 0.f ? (m_i + log2f(l_i)) * kLn2 : INFINITY;
+    };
+    auto lstore = [&](int buf) {
+      #pragma unroll
+      for (int i = 0; i < CPT; ++i) {
+        const int ch = tid + 256 * i, row = ch / CPR, col = (ch % CPR) * 8;
+        *reinterpret_cast<uint4*>(kbuf(buf) + row * KSTR + col) = rk[i];
+        *reinterpret_cast<uint4*>(vbuf(buf) + row * VSTR + col) = rv[i];
+      }
+    };
+
+    f32x16 o[NDT];
+    #pragma unroll
+    for (int i = 0; i < NDT; ++i) o[i] = zero16();
+    float m_i = -INFINITY, l_i = 0.f;
+    const float c = a.scale * kLog2e;
+    const bool dropout = !PLAIN && a.p_drop > 0.f;  // PLAIN: no bias, no dropout (compiled out)
+    const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
+    const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
+    const uint32_t smix = seed_mix_of(a.seed, a.offset);
+    const uint32_t bh = (uint32_t)(b * a.h + hq);
+    const float* biasp = (!PLAIN && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh + (int64_t)myq * a.bias_sq
+                                : nullptr;
+
+    if (nkb > 0) {
+      gload(0);
+      lstore(0);
+    }
+    __syncthreads();
+    for (int it = 0; it < nkb; ++it) {
+      const int cur = it & 1, kb0 = it * BN;
+      const bool more = it + 1 < nkb;
+      if (more) gload(kb0 + BN);
+      const uint16_t* Kl = kbuf(cur);
+      const uint16_t* Vl = vbuf(cur);
+
+      f32x16 s[2] = {zero16(), zero16()};
+      #pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        const s16x8 a0 = frag_rows<KSTR>(Kl, 0, kk, lane);
+        const s16x8 a1 = frag_rows<KSTR>(Kl, 32, kk, lane);
+        s[0] = mma<T>(a0, qf[kk], s[0]);
+        s[1] = mma<T>(a1, qf[kk], s[1]);
+      }
+      float x[2][16];
+      const bool need_mask = (kb0 + BN > sq.lk) || (a.causal && kb0 + BN - 1 > q_start + wave * 32) || biasp != nullptr;
+      #pragma unroll
+      for (int t = 0; t < 2; ++t)
+        #pragma unroll
+        for (int r = 0; r < 16; ++r) x[t][r] = s[t][r] * c;
+      if (need_mask) {
+        #pragma unroll
+        for (int t = 0; t < 2; ++t)
+          #pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kb0 + 32 * t + crow(r, h2);
+            const bool ok = key < sq.lk && (!a.causal || key <= myq);
+            float v = x[t][r];
+            if (biasp != nullptr && ok && qvalid) v += biasp[(int64_t)key * a.bias_sk] * kLog2e;
+            x[t][r] = ok ? v : -INFINITY;
+          }
+      }
+      float mx = -INFINITY;
+      #pragma unroll
+      for (int t = 0; t < 2; ++t)
+        #pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, x[t][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_i, mx);
+      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+      const float alpha = fast_exp2(m_i - m_use);
+      float ls = 0.f;
+      #pragma unroll
+      for (int t = 0; t < 2; ++t)
+        #pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = fast_exp2(x[t][r] - m_use);
+          ls += p;
+          x[t][r] = p;
+        }
+      ls += __shfl_xor(ls, 32, 64);
+      l_i = l_i * alpha + ls;
+      m_i = m_new;
+      // skip the O rescale when no lane's running max moved (after the first tiles it rarely does;
+      // measured equal or faster at every head dim: profiles/kernels_attn_r01e.jsonl lazy0/lazy1)
+      if (__any(alpha != 1.f)) {
+        #pragma unroll
+        for (int i = 0; i < NDT; ++i)
+          #pragma unroll
+          for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+      }
+      if (dropout) {
+        #pragma unroll
+        for (int t = 0; t < 2; ++t)
+          #pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const uint32_t key = (uint32_t)(kb0 + 32 * t + crow(r, h2));
+            x[t][r] *= drop_hash(smix, bh, (uint32_t)myq, key) >= thresh ? inv_keep : 0.f;
+          }
+      }
+      // O^T[d][q] += V^T[d][key] P^T[key][q]
+      #pragma unroll
+      for (int t = 0; t < 2; ++t)
+        #pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const s16x8 pf = pack8<T>(&x[t][8 * s2]);
+          const int klo = 32 * t + 16 * s2 + 4 * h2;
+          #pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) {
+            const s16x8 vf = frag_tr<VSTR>(Vl, 32 * dt, klo, klo + 8, lane);
+            o[dt] = mma<T>(vf, pf, o[dt]);
+          }
+        }
+      if (more) lstore(cur ^ 1);
+      __syncthreads();
+    }
+    (void)wave_q_last;
+
+    if (qvalid) {
+      const float inv_l = l_i > 0.f ? 1.f / l_i : 0.f;
+      T* orow = op + (int64_t)myq * a.o.ss;
+      #pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+        #pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d0 = 32 * dt + 8 * g4 + 4 * h2;
+          uint32_t w0 = (uint32_t)from_f<T>(o[dt][4 * g4] * inv_l).x | ((uint32_t)from_f<T>(o[dt][4 * g4 + 1] * inv_l).x << 16);
+          uint32_t w1 = (uint32_t)from_f<T>(o[dt][4 * g4 + 2] * inv_l).x | ((uint32_t)from_f<T>(o[dt][4 * g4 + 3] * inv_l).x << 16);
+          *reinterpret_cast<uint2*>(orow + d0) = make_uint2(w0, w1);
+        }
+      if (h2 == 0 && a.lse != nullptr)
+        a.lse[(int64_t)hq * a.rows_q + sq.qrow0 + myq] = l_i > 0.f ? (m_i + log2f(l_i)) * kLn2 : INFINITY;
+    }
+    __syncthreads();  // LDS is reused by the paired block
   }
 }
 
@@ -324,10 +332,10 @@ __global__ void __launch_bounds__(256) bwd_delta_kernel(const AttnBwdArgs ba) {
     float ov[8], gv[8];
     Vec8<T>::load(ov, o + c8);
     Vec8<T>::load(gv, g + c8);
-#pragma unroll
+    #pragma unroll
     for (int e = 0; e < 8; ++e) acc += ov[e] * gv[e];
   }
-#pragma unroll
+  #pragma unroll
   for (int off = LPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
   if (q < sq.lq && (threadIdx.x % LPR) == 0) ba.delta[(int64_t)hq * a.rows_q + sq.qrow0 + q] = acc;
 }
@@ -368,19 +376,19 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
   const int mykey = k_start + wave * 32 + ql;
   const bool kvalid = mykey < sq.lk;
   s16x8 kf[NKK], vf[NKK];
-#pragma unroll
+  #pragma unroll
   for (int kk = 0; kk < NKK; ++kk) {
     if (kvalid) {
       kf[kk] = *reinterpret_cast<const s16x8*>(kp + (int64_t)mykey * a.k.ss + kk * 16 + 8 * h2);
       vf[kk] = *reinterpret_cast<const s16x8*>(vp + (int64_t)mykey * a.v.ss + kk * 16 + 8 * h2);
     } else {
-#pragma unroll
+      #pragma unroll
       for (int j = 0; j < 8; ++j) kf[kk][j] = vf[kk][j] = 0;
     }
   }
 
   f32x16 dk[NDT], dv[NDT];
-#pragma unroll
+  #pragma unroll
   for (int i = 0; i < NDT; ++i) dk[i] = dv[i] = zero16();
   const float c = a.scale * kLog2e;
   const bool dropout = !PLAIN && a.p_drop > 0.f;  // PLAIN: no bias, no dropout (compiled out)
@@ -408,7 +416,7 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
     uint4 pq[QCPT], pg[QCPT];
     float plse = INFINITY, pdel = 0.f;
     auto fetch = [&](int q0n) {
-#pragma unroll
+      #pragma unroll
       for (int i = 0; i < QCPT; ++i) {
         const int ch = tid + 256 * i;
         if (ch < QCH) {
@@ -425,7 +433,7 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
       }
     };
     auto commit = [&]() {
-#pragma unroll
+      #pragma unroll
       for (int i = 0; i < QCPT; ++i) {
         const int ch = tid + 256 * i;
         if (ch < QCH) {
@@ -448,7 +456,7 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
 
       // S[q][key] and dP[q][key] with the key on the lane
       f32x16 sacc = zero16(), dpacc = zero16();
-#pragma unroll
+      #pragma unroll
       for (int kk = 0; kk < NKK; ++kk) {
         const s16x8 aq = frag_rows<QSTR>(Ql, 0, kk, lane);
         sacc = mma<T>(aq, kf[kk], sacc);
@@ -458,10 +466,10 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
       float p[16], ds[16];
       const bool edge = !kvalid || q0 + QB > sq.lq || (a.causal && q0 < k_start + wave * 32 + 32) ||
                         biash != nullptr;
-#pragma unroll
+      #pragma unroll
       for (int r = 0; r < 16; ++r) p[r] = sacc[r] * c - lse_l[crow(r, h2)] * kLog2e;
       if (edge) {  // wave-uniform: interior slices run the element loop branch-free
-#pragma unroll
+        #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int q = q0 + crow(r, h2);
           const bool ok = kvalid && q < sq.lq && (!a.causal || mykey <= q);
@@ -470,7 +478,7 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
           p[r] = ok ? xv : -INFINITY;
         }
       }
-#pragma unroll
+      #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qr = crow(r, h2), q = q0 + qr;
         const float pv = fast_exp2(p[r]);
@@ -485,12 +493,12 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
         ds[r] = pv * (dpv - del_l[qr]);
       }
       // dV^T += dO^T P,  dK^T += Q^T dS   (P / dS straight from registers)
-#pragma unroll
+      #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const s16x8 pf = pack8<T>(&p[8 * s2]);
         const s16x8 dsf = pack8<T>(&ds[8 * s2]);
         const int klo = 16 * s2 + 4 * h2;
-#pragma unroll
+        #pragma unroll
         for (int dt = 0; dt < NDT; ++dt) {
           const s16x8 gt = frag_tr<QSTR>(dOl, 32 * dt, klo, klo + 8, lane);
           dv[dt] = mma<T>(gt, pf, dv[dt]);
@@ -499,19 +507,19 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
         }
       }
       // dS -> LDS [q][key]
-#pragma unroll
+      #pragma unroll
       for (int r = 0; r < 16; ++r) dSl[crow(r, h2) * DSSTR + wave * 32 + ql] = from_f<T>(ds[r]).x;
       __syncthreads();
       // dQ[q][d] += dS[q][keys] K[keys][d] for this wave's (d tile, key part)
       f32x16 dq = zero16();
-#pragma unroll
+      #pragma unroll
       for (int kk = 0; kk < KPL / 16; ++kk) {
         const int kb = kpart * KPL + 16 * kk;
         const s16x8 af = frag_rows<DSSTR>(dSl, 0, kb / 16, lane);
         const s16x8 bf = frag_tr<KLSTR>(Kl, 32 * dtq, kb + 8 * h2, kb + 8 * h2 + 4, lane);
         dq = mma<T>(af, bf, dq);
       }
-#pragma unroll
+      #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int q = q0 + crow(r, h2);
         if (q < sq.lq) unsafeAtomicAdd(dq_h + (int64_t)q * a.h * D + 32 * dtq + ql, dq[r] * a.scale);
@@ -524,9 +532,9 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
   if (kvalid) {
     T* dkp = (T*)ba.dk.p + tensor_off(ba.dk, sq, false, vark, b) + (int64_t)hk * ba.dk.sh + (int64_t)mykey * ba.dk.ss;
     T* dvp = (T*)ba.dv.p + tensor_off(ba.dv, sq, false, vark, b) + (int64_t)hk * ba.dv.sh + (int64_t)mykey * ba.dv.ss;
-#pragma unroll
+    #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
+      #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const int d0 = 32 * dt + 8 * g4 + 4 * h2;
         const float s = a.scale;
@@ -570,157 +578,165 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
   const int hk = blockIdx.y, b = blockIdx.z;
   Seq sq;
   seq_of(a, b, a.q.sb, a.q.ss, a.k.sb, a.k.ss, sq);
-  const int k_start = blockIdx.x * BK;
-  if (k_start >= sq.lk) return;
-  const bool varq = a.cu_q != nullptr, vark = a.cu_k != nullptr;
-  const uint16_t* kp = (const uint16_t*)a.k.p + tensor_off(a.k, sq, false, vark, b) + (int64_t)hk * a.k.sh;
-  const uint16_t* vp = (const uint16_t*)a.v.p + tensor_off(a.v, sq, false, vark, b) + (int64_t)hk * a.v.sh;
-  const int mykey = k_start + wave * 32 + ql;
-  const bool kvalid = mykey < sq.lk;
-  s16x8 kf[NKK], vf[NKK];
-#pragma unroll
-  for (int kk = 0; kk < NKK; ++kk) {
-    if (kvalid) {
-      kf[kk] = *reinterpret_cast<const s16x8*>(kp + (int64_t)mykey * a.k.ss + kk * 16 + 8 * h2);
-      vf[kk] = *reinterpret_cast<const s16x8*>(vp + (int64_t)mykey * a.v.ss + kk * 16 + 8 * h2);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) kf[kk][j] = vf[kk][j] = 0;
+  // causal: workgroup x also runs block n-1-x (work per block grows / shrinks linearly with x), so
+  // every workgroup does the same number of tiles
+  const int nblk = (a.sk + BK - 1) / BK;
+  for (int pass = 0; pass < (a.causal ? 2 : 1); ++pass) {
+    const int blk = pass == 0 ? (int)blockIdx.x : nblk - 1 - (int)blockIdx.x;
+    if (pass == 1 && blk <= (int)blockIdx.x) break;
+    const int k_start = blk * BK;
+    if (k_start >= sq.lk) continue;  // uniform over the workgroup
+    const bool varq = a.cu_q != nullptr, vark = a.cu_k != nullptr;
+    const uint16_t* kp = (const uint16_t*)a.k.p + tensor_off(a.k, sq, false, vark, b) + (int64_t)hk * a.k.sh;
+    const uint16_t* vp = (const uint16_t*)a.v.p + tensor_off(a.v, sq, false, vark, b) + (int64_t)hk * a.v.sh;
+    const int mykey = k_start + wave * 32 + ql;
+    const bool kvalid = mykey < sq.lk;
+    s16x8 kf[NKK], vf[NKK];
+    #pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      if (kvalid) {
+        kf[kk] = *reinterpret_cast<const s16x8*>(kp + (int64_t)mykey * a.k.ss + kk * 16 + 8 * h2);
+        vf[kk] = *reinterpret_cast<const s16x8*>(vp + (int64_t)mykey * a.v.ss + kk * 16 + 8 * h2);
+      } else {
+        #pragma unroll
+        for (int j = 0; j < 8; ++j) kf[kk][j] = vf[kk][j] = 0;
+      }
     }
-  }
-  f32x16 dk[NDT], dv[NDT];
-#pragma unroll
-  for (int i = 0; i < NDT; ++i) dk[i] = dv[i] = zero16();
-  const float c = a.scale * kLog2e;
-  const bool dropout = !PLAIN && a.p_drop > 0.f;  // PLAIN: no bias, no dropout (compiled out)
-  const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
-  const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
-  const uint32_t smix = seed_mix_of(a.seed, a.offset);
-  const int group = a.h / a.h_k;
-  constexpr int QCH = QB * CPR, QCPT = (QCH + 255) / 256;
+    f32x16 dk[NDT], dv[NDT];
+    #pragma unroll
+    for (int i = 0; i < NDT; ++i) dk[i] = dv[i] = zero16();
+    const float c = a.scale * kLog2e;
+    const bool dropout = !PLAIN && a.p_drop > 0.f;  // PLAIN: no bias, no dropout (compiled out)
+    const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
+    const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
+    const uint32_t smix = seed_mix_of(a.seed, a.offset);
+    const int group = a.h / a.h_k;
+    constexpr int QCH = QB * CPR, QCPT = (QCH + 255) / 256;
 
-  for (int hq = hk * group; hq < (hk + 1) * group; ++hq) {
-    const uint16_t* qp = (const uint16_t*)a.q.p + tensor_off(a.q, sq, true, varq, b) + (int64_t)hq * a.q.sh;
-    const uint16_t* gp =
-        (const uint16_t*)ba.dout.p + tensor_off(ba.dout, sq, true, varq, b) + (int64_t)hq * ba.dout.sh;
-    const float* lse_h = a.lse + (int64_t)hq * a.rows_q + sq.qrow0;
-    const float* del_h = ba.delta + (int64_t)hq * a.rows_q + sq.qrow0;
-    const uint32_t bh = (uint32_t)(b * a.h + hq);
-    const float* biash = (!PLAIN && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh : nullptr;
-    const int q_begin = a.causal ? (k_start / QB) * QB : 0;
-    uint4 pq[QCPT], pg[QCPT];
-    float plse = INFINITY, pdel = 0.f;
-    auto fetch = [&](int q0n) {
-#pragma unroll
-      for (int i = 0; i < QCPT; ++i) {
-        const int ch = tid + 256 * i;
-        if (ch < QCH) {
-          const int row = ch / CPR, col = (ch % CPR) * 8, q = q0n + row;
-          const bool ok = q < sq.lq;
-          pq[i] = ok ? *reinterpret_cast<const uint4*>(qp + (int64_t)q * a.q.ss + col) : make_uint4(0, 0, 0, 0);
-          pg[i] = ok ? *reinterpret_cast<const uint4*>(gp + (int64_t)q * ba.dout.ss + col) : make_uint4(0, 0, 0, 0);
+    for (int hq = hk * group; hq < (hk + 1) * group; ++hq) {
+      const uint16_t* qp = (const uint16_t*)a.q.p + tensor_off(a.q, sq, true, varq, b) + (int64_t)hq * a.q.sh;
+      const uint16_t* gp =
+          (const uint16_t*)ba.dout.p + tensor_off(ba.dout, sq, true, varq, b) + (int64_t)hq * ba.dout.sh;
+      const float* lse_h = a.lse + (int64_t)hq * a.rows_q + sq.qrow0;
+      const float* del_h = ba.delta + (int64_t)hq * a.rows_q + sq.qrow0;
+      const uint32_t bh = (uint32_t)(b * a.h + hq);
+      const float* biash = (!PLAIN && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh : nullptr;
+      const int q_begin = a.causal ? (k_start / QB) * QB : 0;
+      uint4 pq[QCPT], pg[QCPT];
+      float plse = INFINITY, pdel = 0.f;
+      auto fetch = [&](int q0n) {
+        #pragma unroll
+        for (int i = 0; i < QCPT; ++i) {
+          const int ch = tid + 256 * i;
+          if (ch < QCH) {
+            const int row = ch / CPR, col = (ch % CPR) * 8, q = q0n + row;
+            const bool ok = q < sq.lq;
+            pq[i] = ok ? *reinterpret_cast<const uint4*>(qp + (int64_t)q * a.q.ss + col) : make_uint4(0, 0, 0, 0);
+            pg[i] = ok ? *reinterpret_cast<const uint4*>(gp + (int64_t)q * ba.dout.ss + col) : make_uint4(0, 0, 0, 0);
+          }
         }
-      }
-      if (tid < QB) {
-        const int q = q0n + tid;
-        plse = q < sq.lq ? lse_h[q] : INFINITY;
-        pdel = q < sq.lq ? del_h[q] : 0.f;
-      }
-    };
-    auto commit = [&](int buf) {
-#pragma unroll
-      for (int i = 0; i < QCPT; ++i) {
-        const int ch = tid + 256 * i;
-        if (ch < QCH) {
-          const int row = ch / CPR, col = (ch % CPR) * 8;
-          *reinterpret_cast<uint4*>(Ql(buf) + row * QSTR + col) = pq[i];
-          *reinterpret_cast<uint4*>(dOl(buf) + row * QSTR + col) = pg[i];
+        if (tid < QB) {
+          const int q = q0n + tid;
+          plse = q < sq.lq ? lse_h[q] : INFINITY;
+          pdel = q < sq.lq ? del_h[q] : 0.f;
         }
-      }
-      if (tid < QB) {
-        lse_l(buf)[tid] = plse * kLog2e;
-        del_l(buf)[tid] = pdel;
-      }
-    };
-    // the previous head's last slice ended with a barrier: both buffers are free
-    fetch(q_begin);
-    commit(0);
-    __syncthreads();
-    int buf = 0;
-    for (int q0 = q_begin; q0 < sq.lq; q0 += QB, buf ^= 1) {
-      const bool more = q0 + QB < sq.lq;
-      if (more) fetch(q0 + QB);
-      const uint16_t* Qb = Ql(buf);
-      const uint16_t* Gb = dOl(buf);
-      const float* lb = lse_l(buf);
-      const float* db = del_l(buf);
-      f32x16 sacc = zero16(), dpacc = zero16();
-#pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) {
-        sacc = mma<T>(frag_rows<QSTR>(Qb, 0, kk, lane), kf[kk], sacc);
-        dpacc = mma<T>(frag_rows<QSTR>(Gb, 0, kk, lane), vf[kk], dpacc);
-      }
-      float p[16], ds[16];
-      const bool edge = !kvalid || q0 + QB > sq.lq || (a.causal && q0 < k_start + wave * 32 + 32) ||
-                        biash != nullptr;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) p[r] = sacc[r] * c - lb[crow(r, h2)];
-      if (edge) {  // wave-uniform: interior slices run the element loop branch-free
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int q = q0 + crow(r, h2);
-          const bool ok = kvalid && q < sq.lq && (!a.causal || mykey <= q);
-          float xv = p[r];
-          if (biash != nullptr && ok) xv += biash[(int64_t)q * a.bias_sq + (int64_t)mykey * a.bias_sk] * kLog2e;
-          p[r] = ok ? xv : -INFINITY;
+      };
+      auto commit = [&](int buf) {
+        #pragma unroll
+        for (int i = 0; i < QCPT; ++i) {
+          const int ch = tid + 256 * i;
+          if (ch < QCH) {
+            const int row = ch / CPR, col = (ch % CPR) * 8;
+            *reinterpret_cast<uint4*>(Ql(buf) + row * QSTR + col) = pq[i];
+            *reinterpret_cast<uint4*>(dOl(buf) + row * QSTR + col) = pg[i];
+          }
         }
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qr = crow(r, h2), q = q0 + qr;
-        const float pv = fast_exp2(p[r]);
-        float dpv = dpacc[r];
-        float pd = pv;
-        if (dropout) {
-          const float mk = drop_hash(smix, bh, (uint32_t)q, (uint32_t)mykey) >= thresh ? inv_keep : 0.f;
-          pd = pv * mk;
-          dpv *= mk;
+        if (tid < QB) {
+          lse_l(buf)[tid] = plse * kLog2e;
+          del_l(buf)[tid] = pdel;
         }
-        p[r] = pd;
-        ds[r] = pv * (dpv - db[qr]);
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const s16x8 pf = pack8<T>(&p[8 * s2]);
-        const s16x8 dsf = pack8<T>(&ds[8 * s2]);
-        const int klo = 16 * s2 + 4 * h2;
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) {
-          dv[dt] = mma<T>(frag_tr<QSTR>(Gb, 32 * dt, klo, klo + 8, lane), pf, dv[dt]);
-          dk[dt] = mma<T>(frag_tr<QSTR>(Qb, 32 * dt, klo, klo + 8, lane), dsf, dk[dt]);
-        }
-      }
-      if (more) commit(buf ^ 1);
+      };
+      // the previous head's last slice ended with a barrier: both buffers are free
+      fetch(q_begin);
+      commit(0);
       __syncthreads();
-    }
-  }
-
-  if (kvalid) {
-    T* dkp = (T*)ba.dk.p + tensor_off(ba.dk, sq, false, vark, b) + (int64_t)hk * ba.dk.sh + (int64_t)mykey * ba.dk.ss;
-    T* dvp = (T*)ba.dv.p + tensor_off(ba.dv, sq, false, vark, b) + (int64_t)hk * ba.dv.sh + (int64_t)mykey * ba.dv.ss;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d0 = 32 * dt + 8 * g4 + 4 * h2;
-        const float s = a.scale;
-        uint32_t k0 = (uint32_t)from_f<T>(dk[dt][4 * g4] * s).x | ((uint32_t)from_f<T>(dk[dt][4 * g4 + 1] * s).x << 16);
-        uint32_t k1 = (uint32_t)from_f<T>(dk[dt][4 * g4 + 2] * s).x | ((uint32_t)from_f<T>(dk[dt][4 * g4 + 3] * s).x << 16);
-        *reinterpret_cast<uint2*>(dkp + d0) = make_uint2(k0, k1);
-        uint32_t v0 = (uint32_t)from_f<T>(dv[dt][4 * g4]).x | ((uint32_t)from_f<T>(dv[dt][4 * g4 + 1]).x << 16);
-        uint32_t v1 = (uint32_t)from_f<T>(dv[dt][4 * g4 + 2]).x | ((uint32_t)from_f<T>(dv[dt][4 * g4 + 3]).x << 16);
-        *reinterpret_cast<uint2*>(dvp + d0) = make_uint2(v0, v1);
+      int buf = 0;
+      for (int q0 = q_begin; q0 < sq.lq; q0 += QB, buf ^= 1) {
+        const bool more = q0 + QB < sq.lq;
+        if (more) fetch(q0 + QB);
+        const uint16_t* Qb = Ql(buf);
+        const uint16_t* Gb = dOl(buf);
+        const float* lb = lse_l(buf);
+        const float* db = del_l(buf);
+        f32x16 sacc = zero16(), dpacc = zero16();
+        #pragma unroll
+        for (int kk = 0; kk < NKK; ++kk) {
+          sacc = mma<T>(frag_rows<QSTR>(Qb, 0, kk, lane), kf[kk], sacc);
+          dpacc = mma<T>(frag_rows<QSTR>(Gb, 0, kk, lane), vf[kk], dpacc);
+        }
+        float p[16], ds[16];
+        const bool edge = !kvalid || q0 + QB > sq.lq || (a.causal && q0 < k_start + wave * 32 + 32) ||
+                          biash != nullptr;
+        #pragma unroll
+        for (int r = 0; r < 16; ++r) p[r] = sacc[r] * c - lb[crow(r, h2)];
+        if (edge) {  // wave-uniform: interior slices run the element loop branch-free
+          #pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int q = q0 + crow(r, h2);
+            const bool ok = kvalid && q < sq.lq && (!a.causal || mykey <= q);
+            float xv = p[r];
+            if (biash != nullptr && ok) xv += biash[(int64_t)q * a.bias_sq + (int64_t)mykey * a.bias_sk] * kLog2e;
+            p[r] = ok ? xv : -INFINITY;
+          }
+        }
+        #pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qr = crow(r, h2), q = q0 + qr;
+          const float pv = fast_exp2(p[r]);
+          float dpv = dpacc[r];
+          float pd = pv;
+          if (dropout) {
+            const float mk = drop_hash(smix, bh, (uint32_t)q, (uint32_t)mykey) >= thresh ? inv_keep : 0.f;
+            pd = pv * mk;
+            dpv *= mk;
+          }
+          p[r] = pd;
+          ds[r] = pv * (dpv - db[qr]);
+        }
+        #pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const s16x8 pf = pack8<T>(&p[8 * s2]);
+          const s16x8 dsf = pack8<T>(&ds[8 * s2]);
+          const int klo = 16 * s2 + 4 * h2;
+          #pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) {
+            dv[dt] = mma<T>(frag_tr<QSTR>(Gb, 32 * dt, klo, klo + 8, lane), pf, dv[dt]);
+            dk[dt] = mma<T>(frag_tr<QSTR>(Qb, 32 * dt, klo, klo + 8, lane), dsf, dk[dt]);
+          }
+        }
+        if (more) commit(buf ^ 1);
+        __syncthreads();
       }
+    }
+
+    if (kvalid) {
+      T* dkp = (T*)ba.dk.p + tensor_off(ba.dk, sq, false, vark, b) + (int64_t)hk * ba.dk.sh + (int64_t)mykey * ba.dk.ss;
+      T* dvp = (T*)ba.dv.p + tensor_off(ba.dv, sq, false, vark, b) + (int64_t)hk * ba.dv.sh + (int64_t)mykey * ba.dv.ss;
+      #pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+        #pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d0 = 32 * dt + 8 * g4 + 4 * h2;
+          const float s = a.scale;
+          uint32_t k0 = (uint32_t)from_f<T>(dk[dt][4 * g4] * s).x | ((uint32_t)from_f<T>(dk[dt][4 * g4 + 1] * s).x << 16);
+          uint32_t k1 = (uint32_t)from_f<T>(dk[dt][4 * g4 + 2] * s).x | ((uint32_t)from_f<T>(dk[dt][4 * g4 + 3] * s).x << 16);
+          *reinterpret_cast<uint2*>(dkp + d0) = make_uint2(k0, k1);
+          uint32_t v0 = (uint32_t)from_f<T>(dv[dt][4 * g4]).x | ((uint32_t)from_f<T>(dv[dt][4 * g4 + 1]).x << 16);
+          uint32_t v1 = (uint32_t)from_f<T>(dv[dt][4 * g4 + 2]).x | ((uint32_t)from_f<T>(dv[dt][4 * g4 + 3]).x << 16);
+          *reinterpret_cast<uint2*>(dvp + d0) = make_uint2(v0, v1);
+        }
+    }
+    __syncthreads();  // LDS is reused by the paired block
   }
 }
 
@@ -747,146 +763,152 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dq_kernel(const A
   const int hk = hq / (a.h / a.h_k);
   Seq sq;
   seq_of(a, b, a.q.sb, a.q.ss, a.k.sb, a.k.ss, sq);
-  const int q_start = blockIdx.x * 128;
-  if (q_start >= sq.lq) return;
-  const bool varq = a.cu_q != nullptr, vark = a.cu_k != nullptr;
-  const uint16_t* qp = (const uint16_t*)a.q.p + tensor_off(a.q, sq, true, varq, b) + (int64_t)hq * a.q.sh;
-  const uint16_t* gp = (const uint16_t*)ba.dout.p + tensor_off(ba.dout, sq, true, varq, b) + (int64_t)hq * ba.dout.sh;
-  const uint16_t* kp = (const uint16_t*)a.k.p + tensor_off(a.k, sq, false, vark, b) + (int64_t)hk * a.k.sh;
-  const uint16_t* vp = (const uint16_t*)a.v.p + tensor_off(a.v, sq, false, vark, b) + (int64_t)hk * a.v.sh;
-  T* dqp = (T*)ba.dq.p + tensor_off(ba.dq, sq, true, varq, b) + (int64_t)hq * ba.dq.sh;
+  // causal: heaviest query blocks first (the tail then ends on light blocks); the pairing used by
+  // the other kernels would push this one past 256 VGPRs (spills) in its dropout variant
+  const int nblk = (a.sq + 127) / 128;
+  {
+    const int blk = a.causal ? nblk - 1 - (int)blockIdx.x : (int)blockIdx.x;
+    const int q_start = blk * 128;
+    if (q_start >= sq.lq) return;  // uniform over the workgroup
+    const bool varq = a.cu_q != nullptr, vark = a.cu_k != nullptr;
+    const uint16_t* qp = (const uint16_t*)a.q.p + tensor_off(a.q, sq, true, varq, b) + (int64_t)hq * a.q.sh;
+    const uint16_t* gp = (const uint16_t*)ba.dout.p + tensor_off(ba.dout, sq, true, varq, b) + (int64_t)hq * ba.dout.sh;
+    const uint16_t* kp = (const uint16_t*)a.k.p + tensor_off(a.k, sq, false, vark, b) + (int64_t)hk * a.k.sh;
+    const uint16_t* vp = (const uint16_t*)a.v.p + tensor_off(a.v, sq, false, vark, b) + (int64_t)hk * a.v.sh;
+    T* dqp = (T*)ba.dq.p + tensor_off(ba.dq, sq, true, varq, b) + (int64_t)hq * ba.dq.sh;
 
-  const int myq = q_start + wave * 32 + ql;
-  const bool qvalid = myq < sq.lq;
-  s16x8 qf[NKK], gf[NKK];
-#pragma unroll
-  for (int kk = 0; kk < NKK; ++kk) {
-    if (qvalid) {
-      qf[kk] = *reinterpret_cast<const s16x8*>(qp + (int64_t)myq * a.q.ss + kk * 16 + 8 * h2);
-      gf[kk] = *reinterpret_cast<const s16x8*>(gp + (int64_t)myq * ba.dout.ss + kk * 16 + 8 * h2);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[kk][j] = gf[kk][j] = 0;
-    }
-  }
-  const float lse2 = qvalid ? a.lse[(int64_t)hq * a.rows_q + sq.qrow0 + myq] * kLog2e : INFINITY;
-  const float dlt = qvalid ? ba.delta[(int64_t)hq * a.rows_q + sq.qrow0 + myq] : 0.f;
-
-  int k_end = sq.lk;
-  if (a.causal) k_end = min(k_end, q_start + 128);
-  const int nkb = (k_end + BN - 1) / BN;
-
-  uint4 rk[CPT], rv[CPT];
-  auto gload = [&](int kb0) {
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int ch = tid + 256 * i, row = ch / CPR, col = (ch % CPR) * 8;
-      const int key = kb0 + row;
-      const bool ok = key < sq.lk;
-      rk[i] = ok ? *reinterpret_cast<const uint4*>(kp + (int64_t)key * a.k.ss + col) : make_uint4(0, 0, 0, 0);
-      rv[i] = ok ? *reinterpret_cast<const uint4*>(vp + (int64_t)key * a.v.ss + col) : make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto lstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int ch = tid + 256 * i, row = ch / CPR, col = (ch % CPR) * 8;
-      *reinterpret_cast<uint4*>(krow(buf) + row * RSTR + col) = rk[i];
-      *reinterpret_cast<uint4*>(ktr(buf) + row * TSTR + col) = rk[i];
-      *reinterpret_cast<uint4*>(vrow(buf) + row * RSTR + col) = rv[i];
-    }
-  };
-
-  f32x16 dq[NDT];
-#pragma unroll
-  for (int i = 0; i < NDT; ++i) dq[i] = zero16();
-  const float c = a.scale * kLog2e;
-  const bool dropout = !PLAIN && a.p_drop > 0.f;  // PLAIN: no bias, no dropout (compiled out)
-  const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
-  const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
-  const uint32_t smix = seed_mix_of(a.seed, a.offset);
-  const uint32_t bh = (uint32_t)(b * a.h + hq);
-  const float* biasp = (!PLAIN && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh + (int64_t)myq * a.bias_sq
-                              : nullptr;
-
-  if (nkb > 0) {
-    gload(0);
-    lstore(0);
-  }
-  __syncthreads();
-  for (int it = 0; it < nkb; ++it) {
-    const int cur = it & 1, kb0 = it * BN;
-    const bool more = it + 1 < nkb;
-    if (more) gload(kb0 + BN);
-    const uint16_t* Kr = krow(cur);
-    const uint16_t* Kt = ktr(cur);
-    const uint16_t* Vr = vrow(cur);
-
-    f32x16 s[2] = {zero16(), zero16()}, dp[2] = {zero16(), zero16()};
-#pragma unroll
+    const int myq = q_start + wave * 32 + ql;
+    const bool qvalid = myq < sq.lq;
+    s16x8 qf[NKK], gf[NKK];
+    #pragma unroll
     for (int kk = 0; kk < NKK; ++kk) {
-      s[0] = mma<T>(frag_rows<RSTR>(Kr, 0, kk, lane), qf[kk], s[0]);
-      s[1] = mma<T>(frag_rows<RSTR>(Kr, 32, kk, lane), qf[kk], s[1]);
-      dp[0] = mma<T>(frag_rows<RSTR>(Vr, 0, kk, lane), gf[kk], dp[0]);
-      dp[1] = mma<T>(frag_rows<RSTR>(Vr, 32, kk, lane), gf[kk], dp[1]);
-    }
-    const bool need_mask = !qvalid || (kb0 + BN > sq.lk) || (a.causal && kb0 + BN - 1 > q_start + wave * 32) ||
-                           biasp != nullptr;
-    float ds[2][16];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) ds[t][r] = s[t][r] * c - lse2;
-    if (need_mask) {  // wave-uniform: the interior tiles run the element loop branch-free
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kb0 + 32 * t + crow(r, h2);
-          const bool ok = qvalid && key < sq.lk && (!a.causal || key <= myq);
-          float xv = ds[t][r];
-          if (biasp != nullptr && ok) xv += biasp[(int64_t)key * a.bias_sk] * kLog2e;
-          ds[t][r] = ok ? xv : -INFINITY;
-        }
-    }
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float pv = fast_exp2(ds[t][r]);
-        float dpv = dp[t][r];
-        if (dropout) {
-          const int key = kb0 + 32 * t + crow(r, h2);
-          dpv *= drop_hash(smix, bh, (uint32_t)myq, (uint32_t)key) >= thresh ? inv_keep : 0.f;
-        }
-        ds[t][r] = pv * (dpv - dlt);
+      if (qvalid) {
+        qf[kk] = *reinterpret_cast<const s16x8*>(qp + (int64_t)myq * a.q.ss + kk * 16 + 8 * h2);
+        gf[kk] = *reinterpret_cast<const s16x8*>(gp + (int64_t)myq * ba.dout.ss + kk * 16 + 8 * h2);
+      } else {
+        #pragma unroll
+        for (int j = 0; j < 8; ++j) qf[kk][j] = gf[kk][j] = 0;
       }
-    // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const s16x8 dsf = pack8<T>(&ds[t][8 * s2]);
-        const int klo = 32 * t + 16 * s2 + 4 * h2;
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) dq[dt] = mma<T>(frag_tr<TSTR>(Kt, 32 * dt, klo, klo + 8, lane), dsf, dq[dt]);
-      }
-    if (more) lstore(cur ^ 1);
-    __syncthreads();
-  }
+    }
+    const float lse2 = qvalid ? a.lse[(int64_t)hq * a.rows_q + sq.qrow0 + myq] * kLog2e : INFINITY;
+    const float dlt = qvalid ? ba.delta[(int64_t)hq * a.rows_q + sq.qrow0 + myq] : 0.f;
 
-  if (qvalid) {
-    T* row = dqp + (int64_t)myq * ba.dq.ss;
-    const float s = a.scale;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d0 = 32 * dt + 8 * g4 + 4 * h2;
-        uint32_t w0 = (uint32_t)from_f<T>(dq[dt][4 * g4] * s).x | ((uint32_t)from_f<T>(dq[dt][4 * g4 + 1] * s).x << 16);
-        uint32_t w1 = (uint32_t)from_f<T>(dq[dt][4 * g4 + 2] * s).x | ((uint32_t)from_f<T>(dq[dt][4 * g4 + 3] * s).x << 16);
-        *reinterpret_cast<uint2*>(row + d0) = make_uint2(w0, w1);
+    int k_end = sq.lk;
+    if (a.causal) k_end = min(k_end, q_start + 128);
+    const int nkb = (k_end + BN - 1) / BN;
+
+    uint4 rk[CPT], rv[CPT];
+    auto gload = [&](int kb0) {
+      #pragma unroll
+      for (int i = 0; i < CPT; ++i) {
+        const int ch = tid + 256 * i, row = ch / CPR, col = (ch % CPR) * 8;
+        const int key = kb0 + row;
+        const bool ok = key < sq.lk;
+        rk[i] = ok ? *reinterpret_cast<const uint4*>(kp + (int64_t)key * a.k.ss + col) : make_uint4(0, 0, 0, 0);
+        rv[i] = ok ? *reinterpret_cast<const uint4*>(vp + (int64_t)key * a.v.ss + col) : make_uint4(0, 0, 0, 0);
       }
+    };
+    auto lstore = [&](int buf) {
+      #pragma unroll
+      for (int i = 0; i < CPT; ++i) {
+        const int ch = tid + 256 * i, row = ch / CPR, col = (ch % CPR) * 8;
+        *reinterpret_cast<uint4*>(krow(buf) + row * RSTR + col) = rk[i];
+        *reinterpret_cast<uint4*>(ktr(buf) + row * TSTR + col) = rk[i];
+        *reinterpret_cast<uint4*>(vrow(buf) + row * RSTR + col) = rv[i];
+      }
+    };
+
+    f32x16 dq[NDT];
+    #pragma unroll
+    for (int i = 0; i < NDT; ++i) dq[i] = zero16();
+    const float c = a.scale * kLog2e;
+    const bool dropout = !PLAIN && a.p_drop > 0.f;  // PLAIN: no bias, no dropout (compiled out)
+    const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
+    const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
+    const uint32_t smix = seed_mix_of(a.seed, a.offset);
+    const uint32_t bh = (uint32_t)(b * a.h + hq);
+    const float* biasp = (!PLAIN && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh + (int64_t)myq * a.bias_sq
+                                : nullptr;
+
+    if (nkb > 0) {
+      gload(0);
+      lstore(0);
+    }
+    __syncthreads();
+    for (int it = 0; it < nkb; ++it) {
+      const int cur = it & 1, kb0 = it * BN;
+      const bool more = it + 1 < nkb;
+      if (more) gload(kb0 + BN);
+      const uint16_t* Kr = krow(cur);
+      const uint16_t* Kt = ktr(cur);
+      const uint16_t* Vr = vrow(cur);
+
+      f32x16 s[2] = {zero16(), zero16()}, dp[2] = {zero16(), zero16()};
+      #pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        s[0] = mma<T>(frag_rows<RSTR>(Kr, 0, kk, lane), qf[kk], s[0]);
+        s[1] = mma<T>(frag_rows<RSTR>(Kr, 32, kk, lane), qf[kk], s[1]);
+        dp[0] = mma<T>(frag_rows<RSTR>(Vr, 0, kk, lane), gf[kk], dp[0]);
+        dp[1] = mma<T>(frag_rows<RSTR>(Vr, 32, kk, lane), gf[kk], dp[1]);
+      }
+      const bool need_mask = !qvalid || (kb0 + BN > sq.lk) || (a.causal && kb0 + BN - 1 > q_start + wave * 32) ||
+                             biasp != nullptr;
+      float ds[2][16];
+      #pragma unroll
+      for (int t = 0; t < 2; ++t)
+        #pragma unroll
+        for (int r = 0; r < 16; ++r) ds[t][r] = s[t][r] * c - lse2;
+      if (need_mask) {  // wave-uniform: the interior tiles run the element loop branch-free
+        #pragma unroll
+        for (int t = 0; t < 2; ++t)
+          #pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kb0 + 32 * t + crow(r, h2);
+            const bool ok = qvalid && key < sq.lk && (!a.causal || key <= myq);
+            float xv = ds[t][r];
+            if (biasp != nullptr && ok) xv += biasp[(int64_t)key * a.bias_sk] * kLog2e;
+            ds[t][r] = ok ? xv : -INFINITY;
+          }
+      }
+      #pragma unroll
+      for (int t = 0; t < 2; ++t)
+        #pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pv = fast_exp2(ds[t][r]);
+          float dpv = dp[t][r];
+          if (dropout) {
+            const int key = kb0 + 32 * t + crow(r, h2);
+            dpv *= drop_hash(smix, bh, (uint32_t)myq, (uint32_t)key) >= thresh ? inv_keep : 0.f;
+          }
+          ds[t][r] = pv * (dpv - dlt);
+        }
+      // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
+      #pragma unroll
+      for (int t = 0; t < 2; ++t)
+        #pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const s16x8 dsf = pack8<T>(&ds[t][8 * s2]);
+          const int klo = 32 * t + 16 * s2 + 4 * h2;
+          #pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) dq[dt] = mma<T>(frag_tr<TSTR>(Kt, 32 * dt, klo, klo + 8, lane), dsf, dq[dt]);
+        }
+      if (more) lstore(cur ^ 1);
+      __syncthreads();
+    }
+
+    if (qvalid) {
+      T* row = dqp + (int64_t)myq * ba.dq.ss;
+      const float s = a.scale;
+      #pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+        #pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d0 = 32 * dt + 8 * g4 + 4 * h2;
+          uint32_t w0 = (uint32_t)from_f<T>(dq[dt][4 * g4] * s).x | ((uint32_t)from_f<T>(dq[dt][4 * g4 + 1] * s).x << 16);
+          uint32_t w1 = (uint32_t)from_f<T>(dq[dt][4 * g4 + 2] * s).x | ((uint32_t)from_f<T>(dq[dt][4 * g4 + 3] * s).x << 16);
+          *reinterpret_cast<uint2*>(row + d0) = make_uint2(w0, w1);
+        }
+    }
   }
 }
 
@@ -918,7 +940,8 @@ constexpr size_t bwd_lds() {
 
 template <typename T, int D>
 void launch_fwd(const AttnArgs& a, hipStream_t s) {
-  const dim3 grid((a.sq + 127) / 128, a.h, a.b);
+  const int nqb = (a.sq + 127) / 128;
+  const dim3 grid(a.causal ? (nqb + 1) / 2 : nqb, a.h, a.b);
   if (a.bias == nullptr && !(a.p_drop > 0.f)) hipLaunchKernelGGL((fwd_kernel<T, D, true>), grid, dim3(256), fwd_lds<D>(), s, a);
   else hipLaunchKernelGGL((fwd_kernel<T, D, false>), grid, dim3(256), fwd_lds<D>(), s, a);
 }
@@ -938,10 +961,10 @@ void launch_bwd_v(const AttnBwdArgs& ba, hipStream_t s) {
   constexpr int RPB = 256 / (D / 8);
   hipLaunchKernelGGL((bwd_delta_kernel<T, D>), dim3((a.sq + RPB - 1) / RPB, a.h, a.b), dim3(256), 0, s, ba);
   if (ba.dq_acc == nullptr) {  // split, atomic-free path
-    hipLaunchKernelGGL((bwd_dkdv_kernel<T, D, PLAIN>), dim3((a.sk + 127) / 128, a.h_k, a.b), dim3(256),
+    const int nkb = (a.sk + 127) / 128, nqb = (a.sq + 127) / 128;
+    hipLaunchKernelGGL((bwd_dkdv_kernel<T, D, PLAIN>), dim3(a.causal ? (nkb + 1) / 2 : nkb, a.h_k, a.b), dim3(256),
                        dkdv_lds<D>(), s, ba);
-    hipLaunchKernelGGL((bwd_dq_kernel<T, D, PLAIN>), dim3((a.sq + 127) / 128, a.h, a.b), dim3(256), dq_lds<D>(), s,
-                       ba);
+    hipLaunchKernelGGL((bwd_dq_kernel<T, D, PLAIN>), dim3(nqb, a.h, a.b), dim3(256), dq_lds<D>(), s, ba);
     return;
   }
   (void)hipMemsetAsync(ba.dq_acc, 0, (size_t)a.rows_q * a.h * D * sizeof(float), s);
