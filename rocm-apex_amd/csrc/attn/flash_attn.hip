@@ -116,11 +116,28 @@ __device__ __forceinline__ int64_t tensor_off(const AttnTensor& t, const Seq& s,
   return (int64_t)b * t.sb;
 }
 
+// XCD-aware workgroup order: the hardware deals consecutive workgroups round-robin over the 8
+// XCDs (private L2 each); remapping the linear id so every XCD gets a contiguous chunk keeps the
+// query blocks of one (batch, head) — which all read the same K / V (or the key blocks that all
+// read the same Q / dO) — on one L2 (bijective for any grid size).
+__device__ __forceinline__ void xcd_remap(int& bx, int& by, int& bz) {
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int n = gx * gy * gridDim.z;
+  const int lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int xcd = lin & 7, i = lin >> 3, q = n >> 3, r = n & 7;
+  const int nl = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + i;
+  bx = nl % gx;
+  by = (nl / gx) % gy;
+  bz = nl / (gx * gy);
+}
+
 // =============================================================================================
 // forward
 // =============================================================================================
 template <typename T, int D, bool PLAIN>
 __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) fwd_kernel(const AttnArgs a) {
+  int bx, by, bz;
+  xcd_remap(bx, by, bz);
   using G = Geo<D>;
   constexpr int BN = 64, KSTR = G::KSTR, VSTR = G::TSTR, NKK = G::NKK, NDT = G::NDT;
   constexpr int KT = BN * KSTR, VT = BN * VSTR;
@@ -131,7 +148,7 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) fwd_kernel(const Attn
   auto vbuf = [&](int i) { return lds + i * (KT + VT) + KT; };
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h2 = lane >> 5, ql = lane & 31;
-  const int hq = blockIdx.y, b = blockIdx.z;
+  const int hq = by, b = bz;
   const int hk = hq / (a.h / a.h_k);
   Seq sq;
   seq_of(a, b, a.q.sb, a.q.ss, a.k.sb, a.k.ss, sq);
@@ -139,8 +156,8 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) fwd_kernel(const Attn
   // every workgroup does the same number of tiles
   const int nblk = (a.sq + 127) / 128;
   for (int pass = 0; pass < (a.causal ? 2 : 1); ++pass) {
-    const int blk = pass == 0 ? (int)blockIdx.x : nblk - 1 - (int)blockIdx.x;
-    if (pass == 1 && blk <= (int)blockIdx.x) break;
+    const int blk = pass == 0 ? (int)bx : nblk - 1 - (int)bx;
+    if (pass == 1 && blk <= (int)bx) break;
     const int q_start = blk * 128;
     if (q_start >= sq.lq) continue;  // uniform over the workgroup
     const bool varq = a.cu_q != nullptr, vark = a.cu_k != nullptr;
@@ -562,6 +579,8 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
 // slices of Q / dO (+ lse, delta) double-buffered in LDS, one barrier per slice.
 template <typename T, int D, bool PLAIN>
 __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const AttnBwdArgs ba) {
+  int bx, by, bz;
+  xcd_remap(bx, by, bz);
   const AttnArgs& a = ba.f;
   using G = Geo<D>;
   constexpr int BK = 128, QB = 32, NKK = G::NKK, NDT = G::NDT;
@@ -575,15 +594,15 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
   auto del_l = [&](int i) { return lse_l(i) + QB; };
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h2 = lane >> 5, ql = lane & 31;
-  const int hk = blockIdx.y, b = blockIdx.z;
+  const int hk = by, b = bz;
   Seq sq;
   seq_of(a, b, a.q.sb, a.q.ss, a.k.sb, a.k.ss, sq);
   // causal: workgroup x also runs block n-1-x (work per block grows / shrinks linearly with x), so
   // every workgroup does the same number of tiles
   const int nblk = (a.sk + BK - 1) / BK;
   for (int pass = 0; pass < (a.causal ? 2 : 1); ++pass) {
-    const int blk = pass == 0 ? (int)blockIdx.x : nblk - 1 - (int)blockIdx.x;
-    if (pass == 1 && blk <= (int)blockIdx.x) break;
+    const int blk = pass == 0 ? (int)bx : nblk - 1 - (int)bx;
+    if (pass == 1 && blk <= (int)bx) break;
     const int k_start = blk * BK;
     if (k_start >= sq.lk) continue;  // uniform over the workgroup
     const bool varq = a.cu_q != nullptr, vark = a.cu_k != nullptr;
@@ -747,6 +766,8 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
 // kept as two LDS images: row-read (S) and transposed-read (dQ) paddings differ.
 template <typename T, int D, bool PLAIN>
 __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dq_kernel(const AttnBwdArgs ba) {
+  int bx, by, bz;
+  xcd_remap(bx, by, bz);
   const AttnArgs& a = ba.f;
   using G = Geo<D>;
   constexpr int BN = 64, RSTR = G::KSTR, TSTR = G::TSTR, NKK = G::NKK, NDT = G::NDT;
@@ -759,7 +780,7 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dq_kernel(const A
   auto vrow = [&](int i) { return lds + i * TILE + KT + KTT; };
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h2 = lane >> 5, ql = lane & 31;
-  const int hq = blockIdx.y, b = blockIdx.z;
+  const int hq = by, b = bz;
   const int hk = hq / (a.h / a.h_k);
   Seq sq;
   seq_of(a, b, a.q.sb, a.q.ss, a.k.sb, a.k.ss, sq);
@@ -767,7 +788,7 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dq_kernel(const A
   // the other kernels would push this one past 256 VGPRs (spills) in its dropout variant
   const int nblk = (a.sq + 127) / 128;
   {
-    const int blk = a.causal ? nblk - 1 - (int)blockIdx.x : (int)blockIdx.x;
+    const int blk = a.causal ? nblk - 1 - (int)bx : (int)bx;
     const int q_start = blk * 128;
     if (q_start >= sq.lq) return;  // uniform over the workgroup
     const bool varq = a.cu_q != nullptr, vark = a.cu_k != nullptr;
