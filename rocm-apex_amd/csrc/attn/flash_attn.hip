@@ -135,7 +135,7 @@ __device__ __forceinline__ void xcd_remap(int& bx, int& by, int& bz) {
 // forward
 // =============================================================================================
 template <typename T, int D, bool PLAIN>
-__global__ void __launch_bounds__(256, (D == 128 && !PLAIN) ? 1 : 2) fwd_kernel(const AttnArgs a) {
+__global__ void __launch_bounds__(256, (D == 128 && !PLAIN) ? 1 : ((D <= 64 && PLAIN) ? 3 : 2)) fwd_kernel(const AttnArgs a) {
   int bx, by, bz;
   xcd_remap(bx, by, bz);
   using G = Geo<D>;
