@@ -8,8 +8,10 @@ NCHW-shaped tensor in ``torch.channels_last`` memory (what convolutions produce)
 to the kernels as the same zero-copy ``[M, C]`` view and the output keeps the input's layout.
 
 ``bn_group > 1`` (statistics shared by groups of adjacent ranks; the reference does this through
-CUDA-IPC peer memory and compiles it out on HIP) is implemented with an RCCL sub-group all-gather
-of the per-rank (mean, var, count) — xGMI makes that a few-microsecond collective.  CPU tensors
+CUDA-IPC peer memory and compiles it out on HIP): the per-rank (mean, var, count) and the backward
+(sum_dy, sum_dy_xmu) are exchanged through hipIpc peer buffers over xGMI — one single-workgroup
+push/flag-wait kernel per layer (``apex.parallel.peer_memory``) — or, with ``peer_memory=False``,
+by an RCCL sub-group all-gather / all-reduce.  CPU tensors
 and channel counts that are not a multiple of 8 use the generic SyncBatchNorm primitives.
 """
 import torch
@@ -113,7 +115,7 @@ class BatchNorm2d_NHWC(_BatchNorm):
     from the CU count)."""
 
     def __init__(self, num_features, fuse_relu=False, bn_group=1, torch_channels_last=False, max_cta_per_sm=2,
-                 cta_launch_margin=12, multi_stream=False, eps=1e-5, momentum=0.1):
+                 cta_launch_margin=12, multi_stream=False, eps=1e-5, momentum=0.1, peer_memory=True):
         super().__init__(num_features, eps=eps, momentum=momentum)
         self.fuse_relu = fuse_relu
         self.torch_channels_last = torch_channels_last
@@ -124,6 +126,12 @@ class BatchNorm2d_NHWC(_BatchNorm):
         self.process_group = None
         if bn_group > 1:
             self.process_group = _bn_group(bn_group)
+            if peer_memory and torch.cuda.is_available():
+                # statistics exchanged through hipIpc peer buffers over xGMI (the reference's
+                # groupbn IPC design, parallel/peer_memory.py) instead of one RCCL call per layer
+                from ...parallel.peer_memory import enable_peer_memory
+
+                enable_peer_memory(self.process_group)
 
     def _check_input_dim(self, input):
         if input.dim() != 4:

@@ -12,7 +12,37 @@ void bias_dropout_add_fwd(const void* x, const void* bias, const void* res, void
 void bias_dropout_add_bwd(const void* g, void* dx, int64_t n, int dtype, float p, uint64_t seed, uint64_t offset, int cus,
                           hipStream_t s);
 
+void* peer_alloc(size_t bytes);
+void peer_free(void* p);
+std::string peer_handle(void* p);
+void* peer_open(const std::string& handle);
+void peer_close(void* p);
+int peer_max_group();
+void peer_allgather(const float* local, int n, int nmax, float* const* bufs, int me, int group, uint32_t epoch,
+                    float* out, int* err, hipStream_t s);
+
 namespace {
+
+// ---- peer memory (hipIpc over xGMI) exchange: csrc/comm/peer.hip ----
+int64_t pm_alloc(int64_t bytes) { return (int64_t)(uintptr_t)peer_alloc((size_t)bytes); }
+void pm_free(int64_t p) { peer_free((void*)(uintptr_t)p); }
+pybind11::bytes pm_handle(int64_t p) { return pybind11::bytes(peer_handle((void*)(uintptr_t)p)); }
+int64_t pm_open(const std::string& h) { return (int64_t)(uintptr_t)peer_open(h); }
+void pm_close(int64_t p) { peer_close((void*)(uintptr_t)p); }
+
+// out[group][n] = every member's `local` [n] (fp32), exchanged through the members' buffers
+void pm_allgather(const at::Tensor& local, const std::vector<int64_t>& bufs, int64_t nmax, int64_t me,
+                  int64_t epoch, at::Tensor& out, at::Tensor& err) {
+  TORCH_CHECK(local.is_cuda() && local.scalar_type() == at::kFloat && local.is_contiguous(), "peer: fp32 local");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() &&
+                  out.numel() == (int64_t)bufs.size() * local.numel(), "peer: out must be [group, n] fp32");
+  TORCH_CHECK(err.is_cuda() && err.scalar_type() == at::kInt, "peer: err must be an int32 GPU tensor");
+  const c10::hip::HIPGuard guard(local.get_device());
+  std::vector<float*> ptrs;
+  for (int64_t b : bufs) ptrs.push_back((float*)(uintptr_t)b);
+  peer_allgather(local.data_ptr<float>(), (int)local.numel(), (int)nmax, ptrs.data(), (int)me, (int)bufs.size(),
+                 (uint32_t)epoch, out.data_ptr<float>(), err.data_ptr<int>(), cur_stream());
+}
 
 // out = residual + dropout(x + bias) with a regenerable counter-hash mask (csrc/transformer/bias_dropout_add.hip)
 at::Tensor bda_forward(const at::Tensor& x, const c10::optional<at::Tensor>& bias, const at::Tensor& residual, double p,
@@ -243,6 +273,14 @@ void bind_contrib(pybind11::module_& root) {
   auto p = root.def_submodule("maxpool_nhwc", "channels_last max pooling with 1-byte indices (gfx950)");
   p.def("forward", &maxpool_fwd);
   p.def("backward", &maxpool_bwd);
+  auto pm = root.def_submodule("peer_memory", "hipIpc peer-memory exchange for latency-bound collectives");
+  pm.def("alloc", &pm_alloc);
+  pm.def("free", &pm_free);
+  pm.def("handle", &pm_handle);
+  pm.def("open", &pm_open);
+  pm.def("close", &pm_close);
+  pm.def("max_group", &peer_max_group);
+  pm.def("allgather", &pm_allgather);
   auto t = root.def_submodule("fused_transformer", "transformer block elementwise fusions (gfx950)");
   t.def("bias_dropout_add_forward", &bda_forward, pybind11::arg("x"), pybind11::arg("bias"), pybind11::arg("residual"),
         pybind11::arg("p"), pybind11::arg("seed"), pybind11::arg("offset"));

@@ -1,0 +1,123 @@
+// Peer-memory (hipIpc over xGMI) exchange for tiny, latency-bound collectives inside one node —
+// the per-layer batch-norm statistics of SyncBatchNorm / BatchNorm2d_NHWC(bn_group > 1)
+// (reference: apex/contrib/csrc/groupbn/ipc.cu + nhwc_batch_norm_kernel.h:595-730, a CUDA-IPC
+// butterfly compiled out on HIP; SURVEY §5.8: RCCL's all_gather costs a launch + protocol
+// round trip per layer for ~16 KB).
+//
+// Every rank owns one exchange buffer in device memory, exported with hipIpcGetMemHandle and
+// opened by the other members of its group.  Layout: [2 parities][group][slot], slot = 16-byte
+// header (epoch flag) + nmax fp32 payload.  One call (one 256-thread workgroup):
+//   1. push: write the local payload into slot `me` of EVERY member's buffer (remote stores go
+//      straight over xGMI), system-scope release fence, then store the epoch into each header;
+//   2. wait: spin (bounded, with s_sleep) until all `group` headers of this parity in the LOCAL
+//      buffer carry the epoch (system-scope acquire);
+//   3. read: copy the `group` payloads into the output [group][n].
+// Parity = epoch & 1 double-buffers the slots: a rank can only reach epoch e+2 after every member
+// published e+1, which each member does only after it finished reading epoch e.  A spin that runs
+// out (a member never arrived) sets *err and returns, so the kernel always terminates.
+#include "apex_amd/device.h"
+#include "apex_amd/dispatch.h"
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+namespace apex_amd {
+namespace peer {
+
+constexpr int kHeaderFloats = 4;
+constexpr int kMaxGroup = 8;
+constexpr uint32_t kSpinLimit = 1u << 22;  // x ~64-cycle s_sleep => O(100 ms) before giving up
+
+struct Ptrs {
+  float* buf[kMaxGroup];
+};
+
+__global__ void __launch_bounds__(256) allgather_kernel(const float* __restrict__ local, int n, int nmax, Ptrs bufs,
+                                                        int me, int group, uint32_t epoch, float* __restrict__ out,
+                                                        int* __restrict__ err) {
+  const int tid = threadIdx.x;
+  const int slot = nmax + kHeaderFloats;
+  const int parity = (int)(epoch & 1u);
+  // 1. push
+  for (int j = 0; j < group; ++j) {
+    float* dst = bufs.buf[j] + (int64_t)(parity * group + me) * slot + kHeaderFloats;
+    for (int i = tid; i < n; i += 256) dst[i] = local[i];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: remote payload stores performed
+  __syncthreads();
+  if (tid < group) {
+    uint32_t* flag = reinterpret_cast<uint32_t*>(bufs.buf[tid] + (int64_t)(parity * group + me) * slot);
+    __hip_atomic_store(flag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // 2. wait for every member's slot in the local buffer
+  __shared__ int timed_out;
+  if (tid == 0) timed_out = 0;
+  __syncthreads();
+  if (tid < group) {
+    uint32_t* flag = reinterpret_cast<uint32_t*>(bufs.buf[me] + (int64_t)(parity * group + tid) * slot);
+    uint32_t it = 0;
+    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+      if (++it >= kSpinLimit) {
+        timed_out = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: no stale L1 / L2 lines of the slots
+  if (timed_out) {
+    if (tid == 0) atomicExch(err, 1);
+    return;
+  }
+  // 3. read
+  for (int j = 0; j < group; ++j) {
+    const float* src = bufs.buf[me] + (int64_t)(parity * group + j) * slot + kHeaderFloats;
+    for (int i = tid; i < n; i += 256) out[(int64_t)j * n + i] = src[i];
+  }
+}
+
+}  // namespace peer
+
+void* peer_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) throw std::runtime_error("peer_alloc: hipMalloc failed");
+  if (hipMemset(p, 0, bytes) != hipSuccess) throw std::runtime_error("peer_alloc: hipMemset failed");
+  if (hipDeviceSynchronize() != hipSuccess) throw std::runtime_error("peer_alloc: sync failed");
+  return p;
+}
+
+void peer_free(void* p) { (void)hipFree(p); }
+
+std::string peer_handle(void* p) {
+  hipIpcMemHandle_t h;
+  if (hipIpcGetMemHandle(&h, p) != hipSuccess) throw std::runtime_error("peer_handle: hipIpcGetMemHandle failed");
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void* peer_open(const std::string& handle) {
+  if (handle.size() != sizeof(hipIpcMemHandle_t)) throw std::runtime_error("peer_open: bad handle size");
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle.data(), sizeof(h));
+  void* p = nullptr;
+  if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess)
+    throw std::runtime_error("peer_open: hipIpcOpenMemHandle failed");
+  return p;
+}
+
+void peer_close(void* p) { (void)hipIpcCloseMemHandle(p); }
+
+int peer_max_group() { return peer::kMaxGroup; }
+
+void peer_allgather(const float* local, int n, int nmax, float* const* bufs, int me, int group, uint32_t epoch,
+                    float* out, int* err, hipStream_t s) {
+  if (group < 1 || group > peer::kMaxGroup || me < 0 || me >= group || n > nmax)
+    throw std::runtime_error("peer_allgather: bad group / size");
+  peer::Ptrs p{};
+  for (int j = 0; j < group; ++j) p.buf[j] = bufs[j];
+  hipLaunchKernelGGL(peer::allgather_kernel, dim3(1), dim3(256), 0, s, local, n, nmax, p, me, group, epoch, out, err);
+  check_launch("peer_allgather");
+}
+
+}  // namespace apex_amd

@@ -46,3 +46,4 @@ def create_syncbn_process_group(group_size):
             group = cur
     assert group is not None
     return group
+from .peer_memory import PeerExchange, disable_peer_memory, enable_peer_memory, get_peer_exchange  # noqa: E402,F401

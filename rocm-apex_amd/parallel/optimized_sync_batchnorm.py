@@ -12,6 +12,7 @@ from torch.nn import functional as F
 from torch.nn.modules.batchnorm import _BatchNorm
 
 from ..ops import batchnorm as bnops
+from .peer_memory import get_peer_exchange
 
 
 class SyncBatchnormFunction(Function):
@@ -31,7 +32,10 @@ class SyncBatchnormFunction(Function):
                 world_size = dist.get_world_size(pg)
                 count_t = torch.full((1,), float(count), dtype=mean.dtype, device=mean.device)
                 combined = torch.cat([mean.view(-1), var_biased.view(-1), count_t], dim=0)
-                if dist.get_backend(pg) == "nccl":
+                peer = get_peer_exchange(process_group)
+                if peer is not None:  # hipIpc exchange over xGMI (parallel/peer_memory.py)
+                    gathered = peer.all_gather(combined).to(combined.dtype)
+                elif dist.get_backend(pg) == "nccl":
                     gathered = torch.empty(world_size * combined.numel(), dtype=combined.dtype,
                                            device=combined.device)
                     dist.all_gather_into_tensor(gathered, combined, group=pg)
@@ -88,7 +92,11 @@ class SyncBatchnormFunction(Function):
             if dist.is_available() and dist.is_initialized() and ctx.world_size > 0:
                 c = sum_dy.shape[0]
                 combined = torch.cat([sum_dy, sum_dy_xmu], dim=0)
-                dist.all_reduce(combined, dist.ReduceOp.SUM, ctx.process_group, async_op=False)
+                peer = get_peer_exchange(ctx.process_group)
+                if peer is not None:
+                    combined = peer.all_reduce_sum(combined)
+                else:
+                    dist.all_reduce(combined, dist.ReduceOp.SUM, ctx.process_group, async_op=False)
                 sum_dy, sum_dy_xmu = torch.split(combined, c)
             grad_input = bnops.batchnorm_backward(grad_output, saved_input, mean, inv_std, weight, sum_dy, sum_dy_xmu,
                                                   count, channel_last, zz, bias, relu)
