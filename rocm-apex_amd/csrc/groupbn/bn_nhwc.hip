@@ -28,7 +28,8 @@
 namespace apex_amd {
 namespace bnh {
 
-constexpr int kU = 4;  // rows in flight per lane
+constexpr int kU = 4;   // rows in flight per lane (backward: two tensors per row)
+constexpr int kUS = 8;  // rows in flight per lane in the one-tensor statistics pass
 
 struct Geo {
   int tx, ty, gx, gy;
@@ -68,18 +69,18 @@ __global__ void __launch_bounds__(256) stats_partial(const T* __restrict__ x, in
 #pragma unroll
   for (int k = 0; k < 8; ++k) sh[k] = s[k] = ss[k] = 0.f;
   if (active) Vec8<T>::load(sh, x + c0);
-  const int64_t R = (int64_t)TY * kU;
+  const int64_t R = (int64_t)TY * kUS;
   for (int64_t base = (int64_t)blockIdx.y * R; base < m; base += R * gridDim.y) {
-    float v[kU][8];
-    bool ok[kU];
+    float v[kUS][8];
+    bool ok[kUS];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
+    for (int u = 0; u < kUS; ++u) {
       const int64_t r = base + ty + (int64_t)u * TY;
       ok[u] = active && r < m;
       if (ok[u]) Vec8<T>::load(v[u], x + r * c + c0);
     }
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
+    for (int u = 0; u < kUS; ++u) {
       if (!ok[u]) continue;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
