@@ -48,7 +48,8 @@ def _from_2d(t2d, like, torch_channels_last):
 class _BnNHWCFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, z, weight, bias, running_mean, running_var, momentum, eps, fuse_relu, training,
-                torch_channels_last):
+                torch_channels_last, fork=False):
+        ctx.set_materialize_grads(False)
         x2 = _to_2d(x, torch_channels_last)
         z2 = _to_2d(z, torch_channels_last)
         ext = _ext()
@@ -63,24 +64,35 @@ class _BnNHWCFunction(torch.autograd.Function):
         ctx.training = training
         ctx.has_z = z is not None
         ctx.layout = (torch_channels_last, x.shape, x.dim())
-        return _from_2d(y2, x, torch_channels_last)
+        y = _from_2d(y2, x, torch_channels_last)
+        if fork:
+            # two aliases of one output for two consumers (a residual block's main and shortcut
+            # branches): autograd hands their gradients to backward separately and the reduction
+            # kernel sums them in registers — no separate gradient-add pass over the activation
+            return y, y.view_as(y)
+        return y
 
     @staticmethod
-    def backward(ctx, grad_y):
+    def backward(ctx, grad_y, grad_y2=None):
         x2, z2, weight, save_mean, save_invstd, coef = ctx.saved_tensors
         if not ctx.training:
             raise RuntimeError("BatchNorm2d_NHWC: backward through an eval-mode forward is not supported")
+        if grad_y is None:
+            grad_y, grad_y2 = grad_y2, None
+        if grad_y is None:
+            return (None,) * 12
         tcl, shape, _ = ctx.layout
         g2 = _to_2d(grad_y, tcl)
+        gg2 = _to_2d(grad_y2, tcl) if grad_y2 is not None else None
         need_dz = ctx.has_z and ctx.needs_input_grad[1]
         dx2, dz2, gw, gb = _ext().bwd(g2, x2, z2, weight, save_mean, save_invstd, coef, bool(ctx.fuse_relu),
-                                      bool(need_dz))
+                                      bool(need_dz), gg2)
         like = torch.empty(shape, device="meta")
         dx = _from_2d(dx2, like, tcl)
         dz = _from_2d(dz2, like, tcl) if need_dz else None
         gw = gw if (weight is not None and ctx.needs_input_grad[2]) else None
         gb = gb if (weight is not None and ctx.needs_input_grad[3]) else None
-        return dx, dz, gw, gb, None, None, None, None, None, None, None
+        return dx, dz, gw, gb, None, None, None, None, None, None, None, None
 
 
 def _reference_bn(x, z, weight, bias, running_mean, running_var, momentum, eps, fuse_relu, training, channels_last_dim):
@@ -92,11 +104,20 @@ def _reference_bn(x, z, weight, bias, running_mean, running_var, momentum, eps, 
 
 
 def bn_nhwc_function(x, z, weight, bias, running_mean, running_var, momentum=0.1, eps=1e-5, fuse_relu=False,
-                     training=True, torch_channels_last=True):
+                     training=True, torch_channels_last=True, fork=False):
+    """``fork=True`` returns ``(y, y_alias)``: one output for two consumers whose gradients the
+    fused backward sums itself (ResNet blocks hand the alias to the next block's shortcut)."""
     c = x.size(1) if (torch_channels_last and x.dim() == 4) else x.size(-1)
     if _native.use_native(x) and c % 8 == 0 and weight is not None and weight.dtype == torch.float32:
         return _BnNHWCFunction.apply(x, z, weight, bias, running_mean, running_var, momentum, eps, fuse_relu,
-                                     training, torch_channels_last)
+                                     training, torch_channels_last, fork)
+    y = _bn_generic(x, z, weight, bias, running_mean, running_var, momentum, eps, fuse_relu, training,
+                    torch_channels_last)
+    return (y, y) if fork else y
+
+
+def _bn_generic(x, z, weight, bias, running_mean, running_var, momentum, eps, fuse_relu, training,
+                torch_channels_last):
     if torch_channels_last and x.dim() == 4:
         xv = x.permute(0, 2, 3, 1)
         zv = z.permute(0, 2, 3, 1) if z is not None else None
@@ -137,7 +158,7 @@ class BatchNorm2d_NHWC(_BatchNorm):
         if input.dim() != 4:
             raise ValueError("expected 4D input (got {}D input)".format(input.dim()))
 
-    def forward(self, x, z=None):
+    def forward(self, x, z=None, fork=False):
         if z is not None:
             assert self.fuse_relu, "BatchNorm2d_NHWC: z (residual) requires fuse_relu=True"
         training = self.training or not self.track_running_stats
@@ -148,9 +169,10 @@ class BatchNorm2d_NHWC(_BatchNorm):
             zv = (z.permute(0, 2, 3, 1) if self.torch_channels_last else z) if z is not None else None
             y = SyncBatchnormFunction.apply(xv, zv, self.weight, self.bias, self.running_mean, self.running_var,
                                             self.eps, True, self.momentum, self.process_group, True, self.fuse_relu)
-            return y.permute(0, 3, 1, 2) if self.torch_channels_last else y
+            y = y.permute(0, 3, 1, 2) if self.torch_channels_last else y
+            return (y, y) if fork else y
         return bn_nhwc_function(x, z, self.weight, self.bias, self.running_mean, self.running_var, self.momentum,
-                                self.eps, self.fuse_relu, training, self.torch_channels_last)
+                                self.eps, self.fuse_relu, training, self.torch_channels_last, fork)
 
 
 _GROUPS = {}

@@ -71,11 +71,22 @@ at::Tensor fwd_eval(at::Tensor x, OT z, OT w, OT b, at::Tensor running_mean, at:
 }
 
 std::vector<at::Tensor> bwd(at::Tensor dy_, at::Tensor x, OT z, OT w, at::Tensor save_mean, at::Tensor save_invstd,
-                            at::Tensor coef_fwd, bool relu, bool need_dz) {
+                            at::Tensor coef_fwd, bool relu, bool need_dz, OT dy2_) {
   check2d(x, "input");
   const c10::hip::HIPGuard g(x.get_device());
   at::Tensor dy = dy_.contiguous();
   TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "bn_nhwc: grad must match input");
+  // second gradient of a forked output (both branches of a residual block consumed it): summed
+  // in the reduction pass, which then writes the masked sum for the apply pass
+  at::Tensor dy2;
+  if (has(dy2_)) {
+    dy2 = dy2_->contiguous();
+    TORCH_CHECK(dy2.sizes() == x.sizes() && dy2.scalar_type() == x.scalar_type(), "bn_nhwc: grad2 must match input");
+    if (!relu) {
+      dy = dy + dy2;
+      dy2 = at::Tensor();
+    }
+  }
   const int64_t m = x.size(0);
   const int c = (int)x.size(1);
   const int cus = device_cus(x.get_device());
@@ -88,12 +99,12 @@ std::vector<at::Tensor> bwd(at::Tensor dy_, at::Tensor x, OT z, OT w, at::Tensor
   // the residual branch needs the masked gradient itself (grad_z); without it the mask is
   // recomputed in registers by both passes
   at::Tensor dz;
-  if (relu && need_dz) dz = at::empty_like(x);
+  if (relu && (need_dz || dy2.defined())) dz = at::empty_like(x);
   const int dt = dtype_code(x.scalar_type());
   bn_nhwc_bwd_reduce(dy.data_ptr(), x.data_ptr(), dt, has_z ? z->data_ptr() : nullptr, coef_fwd.data_ptr<float>(),
                      relu, save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(), fptr(w), gw.data_ptr<float>(),
                      gb.data_ptr<float>(), coef_bwd.data_ptr<float>(), dz.defined() ? dz.data_ptr() : nullptr, m, c,
-                     ws.data_ptr<float>(), gy, cus, cur_stream());
+                     ws.data_ptr<float>(), gy, cus, cur_stream(), dy2.defined() ? dy2.data_ptr() : nullptr);
   auto dx = at::empty_like(x);
   if (dz.defined()) {
     bn_nhwc_bwd_apply(dz.data_ptr(), true, x.data_ptr(), dt, nullptr, coef_fwd.data_ptr<float>(), relu,
@@ -104,6 +115,7 @@ std::vector<at::Tensor> bwd(at::Tensor dy_, at::Tensor x, OT z, OT w, at::Tensor
                       cur_stream());
     if (need_dz) dz = dy;  // no ReLU: d(z) = dy
   }
+  if (!need_dz) dz = at::Tensor();
   return {dx, dz, gw, gb};
 }
 
@@ -113,7 +125,9 @@ void bind_bn_nhwc(pybind11::module_& root) {
   auto m = root.def_submodule("bn_nhwc", "gfx950 fused NHWC batch norm (+add+ReLU)");
   m.def("fwd_train", &fwd_train);
   m.def("fwd_eval", &fwd_eval);
-  m.def("bwd", &bwd);
+  m.def("bwd", &bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("z"), pybind11::arg("w"),
+        pybind11::arg("save_mean"), pybind11::arg("save_invstd"), pybind11::arg("coef_fwd"), pybind11::arg("relu"),
+        pybind11::arg("need_dz"), pybind11::arg("dy2") = c10::nullopt);
 }
 
 }  // namespace apex_amd

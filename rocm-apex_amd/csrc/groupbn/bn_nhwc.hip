@@ -188,9 +188,12 @@ template <typename T, bool HAS_Z, bool RELU>
 __global__ void __launch_bounds__(256) apply_kernel(const T* __restrict__ x, const T* __restrict__ z,
                                                     const float* __restrict__ coef, T* __restrict__ y, int64_t nvec,
                                                     int c) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int cstep = (int)((stride * 8) % c);
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  // the channel offset advances by a fixed step per grid stride: no 64-bit modulo in the loop
+  for (int c0 = (int)((i * 8) % c); i < nvec; i += stride, c0 = c0 + cstep >= c ? c0 + cstep - c : c0 + cstep) {
     const int64_t e = i * 8;
-    const int c0 = (int)(e % c);
     float v[8], sc[8], sh[8];
     Vec8<T>::load(v, x + e);
     load8f(sc, coef + c0);
@@ -209,8 +212,11 @@ __global__ void __launch_bounds__(256) apply_kernel(const T* __restrict__ x, con
 }
 
 // ------------------------------------------------------------------------------------------
-template <typename T, bool HAS_Z, bool RELU, bool WRITE_MASKED>
-__global__ void __launch_bounds__(256) bwd_partial(const T* __restrict__ dy, const T* __restrict__ x,
+// DY2: the output fed two consumers (a residual block's main and shortcut branches) and its
+// gradient arrives as two tensors, summed here in registers instead of by a separate add pass
+template <typename T, bool HAS_Z, bool RELU, bool WRITE_MASKED, bool DY2>
+__global__ void __launch_bounds__(256) bwd_partial(const T* __restrict__ dy, const T* __restrict__ dy2,
+                                                   const T* __restrict__ x,
                                                    const T* __restrict__ z, const float* __restrict__ coef,
                                                    const float* __restrict__ mean, T* __restrict__ dym, int64_t m,
                                                    int c, float* __restrict__ part) {
@@ -239,6 +245,12 @@ __global__ void __launch_bounds__(256) bwd_partial(const T* __restrict__ dy, con
       if (ok[u]) {
         Vec8<T>::load(g[u], dy + r * c + c0);
         Vec8<T>::load(v[u], x + r * c + c0);
+        if constexpr (DY2) {
+          float h[8];
+          Vec8<T>::load(h, dy2 + r * c + c0);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) g[u][k] += h[k];
+        }
       }
     }
 #pragma unroll
@@ -312,9 +324,11 @@ __global__ void __launch_bounds__(256) bwd_apply(const T* __restrict__ dy, const
                                                  const T* __restrict__ z, const float* __restrict__ cf,
                                                  const float* __restrict__ cb, T* __restrict__ dx, int64_t nvec,
                                                  int c) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int cstep = (int)((stride * 8) % c);
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (int c0 = (int)((i * 8) % c); i < nvec; i += stride, c0 = c0 + cstep >= c ? c0 + cstep - c : c0 + cstep) {
     const int64_t e = i * 8;
-    const int c0 = (int)(e % c);
     float g[8], v[8], A[8], B[8], K[8];
     Vec8<T>::load(g, dy + e);
     Vec8<T>::load(v, x + e);
@@ -406,23 +420,32 @@ void bn_nhwc_apply(const void* x, int x_t, const void* z, const float* coef_fwd,
 void bn_nhwc_bwd_reduce(const void* dy, const void* x, int x_t, const void* z, const float* coef_fwd, bool relu,
                         const float* save_mean, const float* save_invstd, const float* w, float* grad_w, float* grad_b,
                         float* coef_bwd, void* dy_masked_out, int64_t m, int c, float* ws, int gy, int cus,
-                        hipStream_t s) {
+                        hipStream_t s, const void* dy2) {
+  if (dy2 && !(relu && dy_masked_out))
+    throw std::runtime_error("bn_nhwc bwd: a second gradient needs the fused-ReLU masked-gradient path");
   bnh::check_shape(m, c);
   bnh::Geo g = bnh::geo(m, c, cus);
   g.gy = gy;
   const size_t lds = (size_t)2 * g.ty * g.tx * 8 * sizeof(float);
   dispatch_float(x_t, [&](auto tag) {
     using T = typename decltype(tag)::type;
-    auto go = [&](auto hz, auto rl, auto wm) {
-      hipLaunchKernelGGL((bnh::bwd_partial<T, decltype(hz)::value, decltype(rl)::value, decltype(wm)::value>),
-                         dim3(g.gx, g.gy), dim3(g.tx, g.ty), lds, s, (const T*)dy, (const T*)x, (const T*)z, coef_fwd,
-                         save_mean, (T*)dy_masked_out, m, c, ws);
+    auto go = [&](auto hz, auto rl, auto wm, auto d2) {
+      hipLaunchKernelGGL((bnh::bwd_partial<T, decltype(hz)::value, decltype(rl)::value, decltype(wm)::value,
+                                           decltype(d2)::value>),
+                         dim3(g.gx, g.gy), dim3(g.tx, g.ty), lds, s, (const T*)dy, (const T*)dy2, (const T*)x,
+                         (const T*)z, coef_fwd, save_mean, (T*)dy_masked_out, m, c, ws);
     };
-    if (!relu) go(std::false_type{}, std::false_type{}, std::false_type{});
-    else if (z && dy_masked_out) go(std::true_type{}, std::true_type{}, std::true_type{});
-    else if (z) go(std::true_type{}, std::true_type{}, std::false_type{});
-    else if (dy_masked_out) go(std::false_type{}, std::true_type{}, std::true_type{});
-    else go(std::false_type{}, std::true_type{}, std::false_type{});
+    using F = std::false_type;
+    using Tr = std::true_type;
+    if (!relu) go(F{}, F{}, F{}, F{});
+    else if (z && dy_masked_out) {
+      if (dy2) go(Tr{}, Tr{}, Tr{}, Tr{});
+      else go(Tr{}, Tr{}, Tr{}, F{});
+    } else if (z) go(Tr{}, Tr{}, F{}, F{});
+    else if (dy_masked_out) {
+      if (dy2) go(F{}, Tr{}, Tr{}, Tr{});
+      else go(F{}, Tr{}, Tr{}, F{});
+    } else go(F{}, Tr{}, F{}, F{});
   }, "bn_nhwc bwd reduce");
   hipLaunchKernelGGL(bnh::bwd_finalize, dim3((c + 15) / 16), dim3(256), 0, s, ws, g.gy, c, 1.f / (float)m, save_mean,
                      save_invstd, w, grad_w, grad_b, coef_bwd);

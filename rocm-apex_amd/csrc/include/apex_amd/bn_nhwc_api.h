@@ -36,11 +36,12 @@ void bn_nhwc_apply(const void* x, int x_t, const void* z, const float* coef_fwd,
                    int cus, hipStream_t s);
 
 // backward reduction: grad_w / grad_b (fp32) and coef_bwd; optionally writes the ReLU-masked dy
-// (needed as grad_z for the add+relu variant)
+// (needed as grad_z for the add+relu variant); dy2 (optional, relu + dy_masked_out only) is a
+// second gradient of the same output, summed into dy in registers
 void bn_nhwc_bwd_reduce(const void* dy, const void* x, int x_t, const void* z, const float* coef_fwd, bool relu,
                         const float* save_mean, const float* save_invstd, const float* w, float* grad_w,
                         float* grad_b, float* coef_bwd, void* dy_masked_out, int64_t m, int c, float* ws, int gy,
-                        int cus, hipStream_t s);
+                        int cus, hipStream_t s, const void* dy2 = nullptr);
 
 // dx = A * dy' + B * x + K   (dy' masked in registers when relu && !dy_is_masked)
 void bn_nhwc_bwd_apply(const void* dy, bool dy_is_masked, const void* x, int x_t, const void* z,

@@ -1,5 +1,6 @@
 // Host-side dtype dispatch for device TUs (no torch dependency).
 #pragma once
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include "apex_amd/device.h"
@@ -27,8 +28,21 @@ inline void dispatch_16(int dt, F&& f, const char* what) {
   }
 }
 
+// APEX_AMD_SYNC_LAUNCH=1: debug mode — every native launch is followed by a
+// device synchronize, so an asynchronous fault (out-of-bounds access, trap) is reported as an
+// exception naming the op that caused it instead of surfacing at some later sync point.  Like
+// AMD_SERIALIZE_KERNEL it serialises the process; not for use under hipGraph capture.
+inline bool sync_launch_debug() {
+  static const bool on = [] {
+    const char* v = std::getenv("APEX_AMD_SYNC_LAUNCH");
+    return v != nullptr && v[0] != '\0' && v[0] != '0';
+  }();
+  return on;
+}
+
 inline void check_launch(const char* what) {
   hipError_t e = hipGetLastError();
+  if (e == hipSuccess && sync_launch_debug()) e = hipDeviceSynchronize();
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 

@@ -6,6 +6,8 @@
 //  * backward as a GATHER: one lane per (n, ih, iw, 8 channels) visits the <= ceil(K/S)^2
 //    windows that contain the pixel and sums the gradients whose index points at it — every dx
 //    element written exactly once, no atomics and no zero-fill pass.
+// Index decomposition runs in 32-bit unsigned math whenever the lane count allows (IDX =
+// uint32_t): 64-bit div/mod expands to a long VALU sequence and was the pool kernels' bottleneck.
 #include "apex_amd/device.h"
 #include "apex_amd/dispatch.h"
 #include "apex_amd/pool_api.h"
@@ -13,18 +15,18 @@
 namespace apex_amd {
 namespace pool {
 
-template <typename T>
+template <typename T, typename IDX>
 __global__ void __launch_bounds__(256) fwd_kernel(const PoolArgs a, const T* __restrict__ x, T* __restrict__ y,
                                                   uint8_t* __restrict__ idx) {
-  const int cv = a.C / 8;
-  const int64_t total = (int64_t)a.N * a.OH * a.OW * cv;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+  const IDX cv = (IDX)(a.C / 8);
+  const IDX total = (IDX)a.N * a.OH * a.OW * cv;
+  for (IDX i = blockIdx.x * (IDX)blockDim.x + threadIdx.x; i < total; i += (IDX)gridDim.x * blockDim.x) {
     const int c8 = (int)(i % cv) * 8;
-    int64_t r = i / cv;
-    const int ow = (int)(r % a.OW);
-    r /= a.OW;
-    const int oh = (int)(r % a.OH);
-    const int n = (int)(r / a.OH);
+    IDX r = i / cv;
+    const int ow = (int)(r % (IDX)a.OW);
+    r /= (IDX)a.OW;
+    const int oh = (int)(r % (IDX)a.OH);
+    const int n = (int)(r / (IDX)a.OH);
     float best[8];
     uint8_t bi[8];
 #pragma unroll
@@ -60,18 +62,18 @@ __global__ void __launch_bounds__(256) fwd_kernel(const PoolArgs a, const T* __r
   }
 }
 
-template <typename T>
+template <typename T, typename IDX>
 __global__ void __launch_bounds__(256) bwd_kernel(const PoolArgs a, const T* __restrict__ dy,
                                                   const uint8_t* __restrict__ idx, T* __restrict__ dx) {
-  const int cv = a.C / 8;
-  const int64_t total = (int64_t)a.N * a.H * a.W * cv;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+  const IDX cv = (IDX)(a.C / 8);
+  const IDX total = (IDX)a.N * a.H * a.W * cv;
+  for (IDX i = blockIdx.x * (IDX)blockDim.x + threadIdx.x; i < total; i += (IDX)gridDim.x * blockDim.x) {
     const int c8 = (int)(i % cv) * 8;
-    int64_t r = i / cv;
-    const int iw = (int)(r % a.W);
-    r /= a.W;
-    const int ih = (int)(r % a.H);
-    const int n = (int)(r / a.H);
+    IDX r = i / cv;
+    const int iw = (int)(r % (IDX)a.W);
+    r /= (IDX)a.W;
+    const int ih = (int)(r % (IDX)a.H);
+    const int n = (int)(r / (IDX)a.H);
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     // windows oh with oh*SH - PH <= ih <= oh*SH - PH + KH - 1
     const int hh = ih + a.PH, ww = iw + a.PW;
@@ -111,6 +113,9 @@ inline int grid_for(int64_t total, int cus) {
   return (int)(g < cap ? (g < 1 ? 1 : g) : cap);
 }
 
+// the grid-stride loop's last increment must not wrap a 32-bit counter
+inline bool fits32(int64_t total, unsigned grid) { return total + (int64_t)grid * 256 < (int64_t)UINT32_MAX; }
+
 }  // namespace pool
 
 void maxpool_nhwc_fwd(const PoolArgs& a, const void* x, void* y, uint8_t* idx, int cus, hipStream_t s) {
@@ -119,8 +124,11 @@ void maxpool_nhwc_fwd(const PoolArgs& a, const void* x, void* y, uint8_t* idx, i
   dispatch_float(a.dtype, [&](auto tag) {
     using T = typename decltype(tag)::type;
     const int64_t total = (int64_t)a.N * a.OH * a.OW * (a.C / 8);
-    hipLaunchKernelGGL((pool::fwd_kernel<T>), dim3(pool::grid_for(total, cus)), dim3(256), 0, s, a, (const T*)x,
-                       (T*)y, idx);
+    const dim3 grid(pool::grid_for(total, cus));
+    if (pool::fits32(total, grid.x))
+      hipLaunchKernelGGL((pool::fwd_kernel<T, uint32_t>), grid, dim3(256), 0, s, a, (const T*)x, (T*)y, idx);
+    else
+      hipLaunchKernelGGL((pool::fwd_kernel<T, int64_t>), grid, dim3(256), 0, s, a, (const T*)x, (T*)y, idx);
   }, "maxpool_nhwc_fwd");
   check_launch("maxpool_nhwc_fwd");
 }
@@ -129,8 +137,11 @@ void maxpool_nhwc_bwd(const PoolArgs& a, const void* dy, const uint8_t* idx, voi
   dispatch_float(a.dtype, [&](auto tag) {
     using T = typename decltype(tag)::type;
     const int64_t total = (int64_t)a.N * a.H * a.W * (a.C / 8);
-    hipLaunchKernelGGL((pool::bwd_kernel<T>), dim3(pool::grid_for(total, cus)), dim3(256), 0, s, a, (const T*)dy,
-                       idx, (T*)dx);
+    const dim3 grid(pool::grid_for(total, cus));
+    if (pool::fits32(total, grid.x))
+      hipLaunchKernelGGL((pool::bwd_kernel<T, uint32_t>), grid, dim3(256), 0, s, a, (const T*)dy, idx, (T*)dx);
+    else
+      hipLaunchKernelGGL((pool::bwd_kernel<T, int64_t>), grid, dim3(256), 0, s, a, (const T*)dy, idx, (T*)dx);
   }, "maxpool_nhwc_bwd");
   check_launch("maxpool_nhwc_bwd");
 }

@@ -9,7 +9,12 @@ convolution kernels and our NHWC batch-norm kernels are the fast path on gfx950.
 ``apex.contrib.groupbn.BatchNorm2d_NHWC`` with the ReLU / add fused in (reference capability:
 apex/contrib/groupbn, the NHWC BN with fused add+ReLU used for ResNet-50).  Parameters, buffers
 and state_dict keys are identical to the torch.nn.BatchNorm2d model; the math is the same
-training-mode batch norm, computed by the gfx950 kernels in fewer HBM passes."""
+training-mode batch norm, computed by the gfx950 kernels in fewer HBM passes.
+
+In the fused model every block but the last hands its output on as a ``(main, shortcut)`` pair of
+aliases (``BatchNorm2d_NHWC(..., fork=True)``): the next block's conv1 reads one and its shortcut
+the other, so the two gradients of the block output reach the producing batch norm separately
+and are summed inside its backward reduction instead of by an autograd add over the activation."""
 import torch
 import torch.nn as nn
 
@@ -48,12 +53,15 @@ class BasicBlock(nn.Module):
         self.bn2 = _fused_bn(planes, True) if fused_bn else norm_layer(planes)
         self.downsample = downsample
         self.stride = stride
+        self.fork_out = False
 
     def forward(self, x):
-        identity = x if self.downsample is None else self.downsample(x)
         if self.fused_bn:
-            out = self.bn1(self.conv1(x))
-            return self.bn2(self.conv2(out), identity)
+            xm, xr = x if isinstance(x, tuple) else (x, x)
+            identity = xr if self.downsample is None else self.downsample(xr)
+            out = self.bn1(self.conv1(xm))
+            return self.bn2(self.conv2(out), identity, fork=self.fork_out)
+        identity = x if self.downsample is None else self.downsample(x)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.bn2(self.conv2(out))
         return self.relu(out + identity)
@@ -78,13 +86,16 @@ class Bottleneck(nn.Module):
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
         self.stride = stride
+        self.fork_out = False
 
     def forward(self, x):
-        identity = x if self.downsample is None else self.downsample(x)
         if self.fused_bn:
-            out = self.bn1(self.conv1(x))
+            xm, xr = x if isinstance(x, tuple) else (x, x)
+            identity = xr if self.downsample is None else self.downsample(xr)
+            out = self.bn1(self.conv1(xm))
             out = self.bn2(self.conv2(out))
-            return self.bn3(self.conv3(out), identity)
+            return self.bn3(self.conv3(out), identity, fork=self.fork_out)
+        identity = x if self.downsample is None else self.downsample(x)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.relu(self.bn2(self.conv2(out)))
         out = self.bn3(self.conv3(out))
@@ -120,6 +131,10 @@ class ResNet(nn.Module):
                 if getattr(m, "weight", None) is not None:
                     nn.init.constant_(m.weight, 1)
                     nn.init.constant_(m.bias, 0)
+        if fused_bn:
+            blocks = [b for layer in (self.layer1, self.layer2, self.layer3, self.layer4) for b in layer]
+            for b in blocks[:-1]:
+                b.fork_out = True
         if zero_init_residual:
             for m in self.modules():
                 if isinstance(m, Bottleneck):

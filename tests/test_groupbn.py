@@ -103,6 +103,47 @@ def test_gpu_bn_nhwc(shape, mode, dtype):
 
 
 @pytest.mark.gpu
+def test_gpu_bn_nhwc_fork_sums_two_gradients():
+    """fork=True: two aliases of the output; their gradients are summed inside the backward
+    reduction kernel (the residual-block path of the fused ResNet) — compared with torch BN on
+    the summed gradient, and a single used alias with the plain (non-fork) backward."""
+    torch.manual_seed(7)
+    shape = (16, 256, 14, 14)
+    x = torch.randn(*shape, device="cuda").to(torch.bfloat16).to(memory_format=torch.channels_last)
+    z = torch.randn(*shape, device="cuda").to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    z.requires_grad_(True)
+    m = BatchNorm2d_NHWC(256, fuse_relu=True, torch_channels_last=True).cuda()
+    ref = torch.nn.BatchNorm2d(256).cuda()
+    ya, yb = m(x, z, fork=True)
+    assert ya.data_ptr() == yb.data_ptr() and ya.is_contiguous(memory_format=torch.channels_last)
+    g1 = torch.randn(*shape, device="cuda").to(torch.bfloat16)
+    g2 = torch.randn(*shape, device="cuda").to(torch.bfloat16)
+    torch.autograd.backward([ya, yb], [g1, g2])
+    xr = x.detach().float().requires_grad_(True)
+    zr = z.detach().float().requires_grad_(True)
+    yr = _torch_ref(xr, zr, ref, True)
+    yr.backward(g1.float() + g2.float())
+    tol = 4e-2
+    torch.testing.assert_close(ya.float(), yr, atol=tol, rtol=tol)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=tol * 10, rtol=tol * 5)
+    bad = (z.grad.float() - zr.grad).abs() > tol + tol * zr.grad.abs()
+    assert int(bad.sum()) <= 2, int(bad.sum())
+    gs = max(1.0, float(ref.weight.grad.abs().max()))
+    torch.testing.assert_close(m.weight.grad / gs, ref.weight.grad / gs, atol=tol * 5, rtol=tol * 5)
+    # one alias unused: identical to the non-fork backward
+    grads = []
+    for fork in (True, False):
+        x.grad = z.grad = None
+        m.zero_grad()
+        out = m(x, z, fork=fork)
+        (out[1] if fork else out).backward(g2)
+        grads.append((x.grad.clone(), z.grad.clone(), m.weight.grad.clone()))
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
 def test_gpu_bn_nhwc_eval_and_deterministic():
     torch.manual_seed(3)
     x = torch.randn(32, 128, 14, 14, device="cuda").to(memory_format=torch.channels_last)
