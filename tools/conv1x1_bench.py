@@ -48,11 +48,26 @@ def main():
         yg = gemm_conv(x, conv.weight)
         t_g_b = timeit(lambda: torch.autograd.grad(yg, (x, conv.weight), gy, retain_graph=True))
         assert yg.is_contiguous(memory_format=torch.channels_last)
-        err = (yg.float() - y.float()).abs().max().item()
         fl = 2.0 * 256 * hw * hw * cin * cout
+        err = (yg.float() - y.float()).abs().max().item()
+        extra = {}
+        try:
+            import apex
+            G = apex._native._C.gemm
+            x2 = x.detach().permute(0, 2, 3, 1).reshape(-1, cin)
+            w2 = conv.weight.detach().view(cout, cin).contiguous()
+            gy2 = gy.permute(0, 2, 3, 1).reshape(-1, cout)
+            t_a_f = timeit(lambda: G.linear(x2, w2, None, 0, False))
+            t_a_b = timeit(lambda: (G.linear_dgrad(gy2, w2, 0, None), G.linear_wgrad(gy2, x2)))
+            ya = G.linear(x2, w2, None, 0, False)[0].view(256, hw, hw, cout).permute(0, 3, 1, 2)
+            extra = dict(apex_fwd_ms=t_a_f, apex_bwd_ms=t_a_b, apex_fwd_speedup=t_m_f / t_a_f,
+                         apex_bwd_speedup=t_m_b / t_a_b, apex_err=(ya.float() - y.float()).abs().max().item(),
+                         apex_fwd_tflops=fl / t_a_f / 1e9)
+        except Exception as e:  # noqa: BLE001
+            extra = dict(apex_error=repr(e)[:200])
         print(json.dumps(dict(cin=cin, cout=cout, hw=hw, miopen_fwd_ms=t_m_f, gemm_fwd_ms=t_g_f, miopen_bwd_ms=t_m_b,
                               gemm_bwd_ms=t_g_b, fwd_speedup=t_m_f / t_g_f, bwd_speedup=t_m_b / t_g_b,
-                              gemm_fwd_tflops=fl / t_g_f / 1e9, max_abs_err=err)), flush=True)
+                              gemm_fwd_tflops=fl / t_g_f / 1e9, max_abs_err=err, **extra)), flush=True)
 
 
 if __name__ == "__main__":
