@@ -5,7 +5,8 @@ headline ImageNet benchmark (reference examples/imagenet/main_amp.py uses torchv
 Layout notes for MI355X: build with ``memory_format=torch.channels_last`` — MIOpen's NHWC
 convolution kernels and our NHWC batch-norm kernels are the fast path on gfx950.
 
-``fused_bn=True`` swaps every BatchNorm (+ReLU) (+residual add +ReLU) group for
+``fused_bn=True`` also routes the bottleneck 1x1 convolutions through ``ops.conv.Conv1x1NHWC``
+(native MFMA GEMM where it beats MIOpen for the shape) and swaps every BatchNorm (+ReLU) (+residual add +ReLU) group for
 ``apex.contrib.groupbn.BatchNorm2d_NHWC`` with the ReLU / add fused in (reference capability:
 apex/contrib/groupbn, the NHWC BN with fused add+ReLU used for ResNet-50).  Parameters, buffers
 and state_dict keys are identical to the torch.nn.BatchNorm2d model; the math is the same
@@ -18,6 +19,7 @@ and are summed inside its backward reduction instead of by an autograd add over 
 import torch
 import torch.nn as nn
 
+from ..ops.conv import Conv1x1NHWC
 from ..ops.pooling import MaxPool2dNHWC
 
 __all__ = ["ResNet", "BasicBlock", "Bottleneck", "resnet18", "resnet34", "resnet50", "resnet101", "resnet152"]
@@ -28,7 +30,11 @@ def conv3x3(cin, cout, stride=1, groups=1, dilation=1):
                      dilation=dilation)
 
 
-def conv1x1(cin, cout, stride=1):
+def conv1x1(cin, cout, stride=1, native=False):
+    # native: per-shape routing of the NHWC GEMM to the gfx950 MFMA kernels (ops/conv.py); same
+    # parameters / state_dict as nn.Conv2d
+    if native:
+        return Conv1x1NHWC(cin, cout, stride)
     return nn.Conv2d(cin, cout, kernel_size=1, stride=stride, bias=False)
 
 
@@ -77,11 +83,11 @@ class Bottleneck(nn.Module):
         self.fused_bn = fused_bn
         width = int(planes * (base_width / 64.0)) * groups
         nl = (lambda c, relu: _fused_bn(c, relu)) if fused_bn else (lambda c, relu: norm_layer(c))  # noqa: E731
-        self.conv1 = conv1x1(inplanes, width)
+        self.conv1 = conv1x1(inplanes, width, native=fused_bn)
         self.bn1 = nl(width, True)
         self.conv2 = conv3x3(width, width, stride, groups, dilation)
         self.bn2 = nl(width, True)
-        self.conv3 = conv1x1(width, planes * self.expansion)
+        self.conv3 = conv1x1(width, planes * self.expansion, native=fused_bn)
         self.bn3 = nl(planes * self.expansion, True)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample

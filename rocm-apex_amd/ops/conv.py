@@ -1,0 +1,94 @@
+"""1x1 stride-1 convolution on the gfx950 MFMA GEMM where it beats MIOpen.
+
+On a channels_last activation a 1x1 stride-1 convolution IS a GEMM over the dense NHWC view:
+``y[M, Cout] = x[M, Cin] W[Cout, Cin]^T`` with M = N*H*W, and its backward is the dgrad
+``dx = dy W`` and the weight gradient ``dW = dy^T x`` (K = M, split-K in the native kernel).
+``Conv1x1NHWC`` is a drop-in ``nn.Conv2d(cin, cout, 1, bias=False)`` (same parameter and
+state_dict) that routes each of forward / backward to the native GEMM (``csrc/gemm/gemm_mfma.hip``)
+or to MIOpen per shape, from the measurements in ``profiles/conv1x1_miopen_vs_gemm_r01f.jsonl``
+(1 x MI355X, ResNet-50 bs 256 shapes):
+
+* backward: native 1.14-1.24x MIOpen at 14x14 / 7x7 (M <= 50k) and for Cin >= 512 at 28x28;
+  MIOpen ahead at 56x56 where Cout = 64 leaves the 256-wide MFMA tiles half empty;
+* forward: native ahead only for the Cin = 1024 reductions at 14x14.
+
+Everything else (CPU, autocast, other layouts / dtypes, odd channel counts) is plain
+``nn.Conv2d``.  ``APEX_AMD_CONV1X1=0`` disables the native routing (A/B switch).
+
+Reference capability: the fused 1x1 convolutions of apex/contrib/bottleneck (cudnn-frontend
+graphs, ``apex/contrib/csrc/bottleneck/bottleneck.cpp``) — here the GEMM is our own MFMA kernel.
+"""
+import os
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import _native
+
+_ENABLED = os.environ.get("APEX_AMD_CONV1X1", "1") != "0"
+
+
+def route(m, cin, cout):
+    """(forward_native, backward_native) for a 1x1 stride-1 conv with M = N*H*W rows."""
+    bwd = m <= 65536 or (cin >= 512 and cout >= 256 and m <= 262144)
+    fwd = cin >= 1024 and 32768 <= m <= 65536
+    return fwd, bwd
+
+
+class _Conv1x1Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, fwd_native, bwd_native):
+        n, c, h, wd = x.shape
+        cout = w.size(0)
+        x2 = x.permute(0, 2, 3, 1).reshape(-1, c)  # zero-copy: x is channels_last contiguous
+        w2 = w.view(cout, c)
+        if fwd_native:
+            g = _native.require("conv1x1").gemm
+            y = g.linear(x2, w2, None, g.EPI_NONE, False)[0].view(n, h, wd, cout).permute(0, 3, 1, 2)
+        else:
+            y = F.conv2d(x, w)
+        ctx.save_for_backward(x, w)
+        ctx.bwd_native = bwd_native
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        if not ctx.bwd_native:
+            dx, dw, _ = torch.ops.aten.convolution_backward(gy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                                                            [need_x, need_w, False])
+            return dx, dw, None, None
+        g = _native.require("conv1x1").gemm
+        n, c, h, wd = x.shape
+        cout = w.size(0)
+        gy2 = gy.permute(0, 2, 3, 1).reshape(-1, cout)  # a view when gy is channels_last contiguous
+        dx = dw = None
+        if need_x:
+            dx = g.linear_dgrad(gy2, w.view(cout, c), g.EPI_NONE, None).view(n, h, wd, c).permute(0, 3, 1, 2)
+        if need_w:
+            dw = g.linear_wgrad(gy2, x.permute(0, 2, 3, 1).reshape(-1, c)).view_as(w)
+        return dx, dw, None, None
+
+
+class Conv1x1NHWC(nn.Conv2d):
+    """``nn.Conv2d(in_channels, out_channels, 1, stride, bias=False)`` with per-shape native routing."""
+
+    def __init__(self, in_channels, out_channels, stride=1):
+        super().__init__(in_channels, out_channels, kernel_size=1, stride=stride, bias=False)
+
+    def _native_ok(self, x):
+        w = self.weight
+        return (_ENABLED and self.stride == (1, 1) and x.is_cuda and x.dim() == 4 and x.dtype == w.dtype
+                and x.dtype in (torch.bfloat16, torch.float16) and self.in_channels % 64 == 0
+                and self.out_channels % 64 == 0 and x.is_contiguous(memory_format=torch.channels_last)
+                and not torch.is_autocast_enabled("cuda") and _native.available())
+
+    def forward(self, x):
+        if self._native_ok(x):
+            n, _, h, wd = x.shape
+            fwd, bwd = route(n * h * wd, self.in_channels, self.out_channels)
+            if fwd or bwd:
+                return _Conv1x1Fn.apply(x, self.weight, fwd, bwd)
+        return super().forward(x)
