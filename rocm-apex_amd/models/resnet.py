@@ -19,7 +19,7 @@ and are summed inside its backward reduction instead of by an autograd add over 
 import torch
 import torch.nn as nn
 
-from ..ops.conv import Conv1x1NHWC
+from ..ops.conv import ChannelPadConv2d, Conv1x1NHWC
 from ..ops.pooling import MaxPool2dNHWC
 
 __all__ = ["ResNet", "BasicBlock", "Bottleneck", "resnet18", "resnet34", "resnet50", "resnet101", "resnet152"]
@@ -118,7 +118,9 @@ class ResNet(nn.Module):
         self.dilation = 1
         self.groups = groups
         self.base_width = width_per_group
-        self.conv1 = nn.Conv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
+        # fused path: stem input channels padded 3 -> 4 on the GPU (MIOpen's NHWC kernels, ops/conv.py)
+        stem = ChannelPadConv2d if fused_bn else nn.Conv2d
+        self.conv1 = stem(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
         self.bn1 = _fused_bn(self.inplanes, True) if fused_bn else self._norm_layer(self.inplanes)
         self.relu = nn.ReLU(inplace=True)
         # fused path (channels_last): gfx950 NHWC max pool with 1-byte indices

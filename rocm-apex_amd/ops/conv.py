@@ -27,6 +27,7 @@ import torch.nn.functional as F
 from .. import _native
 
 _ENABLED = os.environ.get("APEX_AMD_CONV1X1", "1") != "0"
+_STEM_PAD = os.environ.get("APEX_AMD_STEM_PAD", "1") != "0"
 
 
 def route(m, cin, cout):
@@ -91,4 +92,34 @@ class Conv1x1NHWC(nn.Conv2d):
             fwd, bwd = route(n * h * wd, self.in_channels, self.out_channels)
             if fwd or bwd:
                 return _Conv1x1Fn.apply(x, self.weight, fwd, bwd)
+        return super().forward(x)
+
+
+class ChannelPadConv2d(nn.Conv2d):
+    """``nn.Conv2d`` whose input channels are zero-padded to ``pad_to`` on the GPU path.
+
+    The ResNet stem (7x7/2, 3 -> 64) is MIOpen's slowest convolution per FLOP on gfx950 because
+    3 input channels break its NHWC vector loads; with a 4th zero channel (and a zero weight slice)
+    the same convolution's forward + weight gradient runs 0.64 ms instead of 0.83 ms at bs 256
+    (``tools/stem_bench.py``).  The padded copy of the input costs one 100 MB write.  Parameters
+    and state_dict are those of the unpadded ``nn.Conv2d``; the weight gradient flows back through
+    the concatenation to the real slice only.  Used only when the input needs no gradient
+    (images), so the padding never sits on a backward path.  ``APEX_AMD_STEM_PAD=0`` disables it."""
+
+    def __init__(self, *args, pad_to=4, **kw):
+        super().__init__(*args, **kw)
+        self.pad_to = pad_to
+
+    def forward(self, x):
+        c = self.in_channels
+        if (_STEM_PAD and x.is_cuda and x.dim() == 4 and self.groups == 1 and c < self.pad_to and not x.requires_grad
+                and x.is_contiguous(memory_format=torch.channels_last)):
+            n, _, h, w = x.shape
+            xp = torch.empty((n, self.pad_to, h, w), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+            xp[:, :c].copy_(x)
+            xp[:, c:].zero_()
+            wt = self.weight
+            wp = torch.cat([wt, wt.new_zeros((wt.size(0), self.pad_to - c) + tuple(wt.shape[2:]))], dim=1)
+            wp = wp.contiguous(memory_format=torch.channels_last)
+            return F.conv2d(xp, wp, self.bias, self.stride, self.padding, self.dilation, 1)
         return super().forward(x)

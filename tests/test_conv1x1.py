@@ -81,3 +81,35 @@ def test_gpu_conv1x1_module_routes_native_backward():
     _close(y, yr)
     _close(x.grad, dxr)
     _close(m.weight.grad, dwr)
+
+
+def test_channel_pad_conv_cpu_is_plain_conv():
+    from apex.ops.conv import ChannelPadConv2d
+
+    torch.manual_seed(0)
+    m = ChannelPadConv2d(3, 16, kernel_size=7, stride=2, padding=3, bias=False)
+    ref = torch.nn.Conv2d(3, 16, 7, 2, 3, bias=False)
+    assert list(m.state_dict()) == list(ref.state_dict())
+    ref.load_state_dict(m.state_dict())
+    x = torch.randn(2, 3, 32, 32)
+    torch.testing.assert_close(m(x), ref(x))
+
+
+@pytest.mark.gpu
+def test_gpu_channel_pad_stem_matches_conv():
+    from apex.ops.conv import ChannelPadConv2d
+
+    torch.manual_seed(0)
+    m = ChannelPadConv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False).cuda().to(torch.bfloat16)
+    m = m.to(memory_format=torch.channels_last)
+    x = torch.randn(4, 3, 64, 64, device="cuda", dtype=torch.bfloat16).to(memory_format=torch.channels_last)
+    y = m(x)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    xr = x.float()
+    wr = m.weight.detach().float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, None, 2, 3)
+    yr.backward(gy.float())
+    _close(y, yr)
+    _close(m.weight.grad, wr.grad)
+    assert m.weight.grad.shape == (64, 3, 7, 7)
