@@ -14,11 +14,17 @@ push/flag-wait kernel per layer (``apex.parallel.peer_memory``) — or, with ``p
 by an RCCL sub-group all-gather / all-reduce.  CPU tensors
 and channel counts that are not a multiple of 8 use the generic SyncBatchNorm primitives.
 """
+import os
+
 import torch
 from torch.nn.modules.batchnorm import _BatchNorm
 
 from ... import _native
 from ...ops import batchnorm as bnops
+
+
+# APEX_BN_BITS=0: recompute the residual ReLU mask from x and z in backward instead (A/B switch)
+_BITS = os.environ.get("APEX_BN_BITS", "1") != "0"
 
 
 def _ext():
@@ -54,12 +60,17 @@ class _BnNHWCFunction(torch.autograd.Function):
         z2 = _to_2d(z, torch_channels_last)
         ext = _ext()
         if training:
-            y2, save_mean, save_invstd, coef = ext.fwd_train(x2, z2, weight, bias, running_mean, running_var,
-                                                             float(momentum), float(eps), bool(fuse_relu))
-            ctx.save_for_backward(x2, z2, weight, save_mean, save_invstd, coef)
+            # residual add + ReLU: the forward also writes the ReLU mask as bits and the backward
+            # reads those instead of z (z is not kept alive for this layer's backward at all)
+            bits = _BITS and bool(fuse_relu) and z2 is not None
+            y2, save_mean, save_invstd, coef, mask = ext.fwd_train(x2, z2, weight, bias, running_mean, running_var,
+                                                                   float(momentum), float(eps), bool(fuse_relu),
+                                                                   bits)
+            ctx.save_for_backward(x2, None if bits else z2, weight, save_mean, save_invstd, coef,
+                                  mask if bits else None)
         else:
             y2 = ext.fwd_eval(x2, z2, weight, bias, running_mean, running_var, float(eps), bool(fuse_relu))
-            ctx.save_for_backward(x2, z2, weight, None, None, None)
+            ctx.save_for_backward(x2, z2, weight, None, None, None, None)
         ctx.fuse_relu = fuse_relu
         ctx.training = training
         ctx.has_z = z is not None
@@ -74,7 +85,7 @@ class _BnNHWCFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_y, grad_y2=None):
-        x2, z2, weight, save_mean, save_invstd, coef = ctx.saved_tensors
+        x2, z2, weight, save_mean, save_invstd, coef, mask = ctx.saved_tensors
         if not ctx.training:
             raise RuntimeError("BatchNorm2d_NHWC: backward through an eval-mode forward is not supported")
         if grad_y is None:
@@ -86,7 +97,7 @@ class _BnNHWCFunction(torch.autograd.Function):
         gg2 = _to_2d(grad_y2, tcl) if grad_y2 is not None else None
         need_dz = ctx.has_z and ctx.needs_input_grad[1]
         dx2, dz2, gw, gb = _ext().bwd(g2, x2, z2, weight, save_mean, save_invstd, coef, bool(ctx.fuse_relu),
-                                      bool(need_dz), gg2)
+                                      bool(need_dz), gg2, mask)
         like = torch.empty(shape, device="meta")
         dx = _from_2d(dx2, like, tcl)
         dz = _from_2d(dz2, like, tcl) if need_dz else None

@@ -26,7 +26,8 @@ void check_param(const OT& t, int64_t c) {
 }
 
 std::vector<at::Tensor> fwd_train(at::Tensor x, OT z, OT w, OT b, OT running_mean, OT running_var, double momentum,
-                                  double eps, bool relu) {
+                                  double eps, bool relu, bool want_mask) {
+  TORCH_CHECK(!want_mask || relu, "bn_nhwc: the ReLU bit mask needs relu=True");
   check2d(x, "input");
   const c10::hip::HIPGuard g(x.get_device());
   const int64_t m = x.size(0);
@@ -47,9 +48,11 @@ std::vector<at::Tensor> fwd_train(at::Tensor x, OT z, OT w, OT b, OT running_mea
   bn_nhwc_stats(x.data_ptr(), dt, m, c, fptr(w), fptr(b), (float)eps, (float)momentum, fptr_mut(running_mean),
                 fptr_mut(running_var), save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
                 coef.data_ptr<float>(), ws.data_ptr<float>(), gy, cus, cur_stream());
+  at::Tensor mask;
+  if (want_mask) mask = at::empty({m * c / 8}, x.options().dtype(at::kByte));
   bn_nhwc_apply(x.data_ptr(), dt, has(z) ? z->data_ptr() : nullptr, coef.data_ptr<float>(), relu, y.data_ptr(), m, c,
-                cus, cur_stream());
-  return {y, save_mean, save_invstd, coef};
+                cus, cur_stream(), want_mask ? mask.data_ptr<uint8_t>() : nullptr);
+  return {y, save_mean, save_invstd, coef, mask};
 }
 
 at::Tensor fwd_eval(at::Tensor x, OT z, OT w, OT b, at::Tensor running_mean, at::Tensor running_var, double eps,
@@ -71,7 +74,7 @@ at::Tensor fwd_eval(at::Tensor x, OT z, OT w, OT b, at::Tensor running_mean, at:
 }
 
 std::vector<at::Tensor> bwd(at::Tensor dy_, at::Tensor x, OT z, OT w, at::Tensor save_mean, at::Tensor save_invstd,
-                            at::Tensor coef_fwd, bool relu, bool need_dz, OT dy2_) {
+                            at::Tensor coef_fwd, bool relu, bool need_dz, OT dy2_, OT mask_) {
   check2d(x, "input");
   const c10::hip::HIPGuard g(x.get_device());
   at::Tensor dy = dy_.contiguous();
@@ -96,15 +99,22 @@ std::vector<at::Tensor> bwd(at::Tensor dy_, at::Tensor x, OT z, OT w, at::Tensor
   auto ws = at::empty({wsf}, fo);
   auto gw = at::empty({c}, fo), gb = at::empty({c}, fo), coef_bwd = at::empty({3, c}, fo);
   const bool has_z = has(z);
+  // ReLU bit mask from the forward: the masked gradient is written by the reduction pass and the
+  // apply pass reads it, so z is never touched
+  const bool bits = has(mask_);
+  if (bits)
+    TORCH_CHECK(relu && mask_->scalar_type() == at::kByte && mask_->numel() * 8 == m * c && mask_->is_contiguous(),
+                "bn_nhwc: mask must be a contiguous uint8 [M*C/8] tensor of a relu forward");
   // the residual branch needs the masked gradient itself (grad_z); without it the mask is
   // recomputed in registers by both passes
   at::Tensor dz;
-  if (relu && (need_dz || dy2.defined())) dz = at::empty_like(x);
+  if (relu && (need_dz || dy2.defined() || bits)) dz = at::empty_like(x);
   const int dt = dtype_code(x.scalar_type());
   bn_nhwc_bwd_reduce(dy.data_ptr(), x.data_ptr(), dt, has_z ? z->data_ptr() : nullptr, coef_fwd.data_ptr<float>(),
                      relu, save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(), fptr(w), gw.data_ptr<float>(),
                      gb.data_ptr<float>(), coef_bwd.data_ptr<float>(), dz.defined() ? dz.data_ptr() : nullptr, m, c,
-                     ws.data_ptr<float>(), gy, cus, cur_stream(), dy2.defined() ? dy2.data_ptr() : nullptr);
+                     ws.data_ptr<float>(), gy, cus, cur_stream(), dy2.defined() ? dy2.data_ptr() : nullptr,
+                     bits ? mask_->data_ptr<uint8_t>() : nullptr);
   auto dx = at::empty_like(x);
   if (dz.defined()) {
     bn_nhwc_bwd_apply(dz.data_ptr(), true, x.data_ptr(), dt, nullptr, coef_fwd.data_ptr<float>(), relu,
@@ -123,11 +133,13 @@ std::vector<at::Tensor> bwd(at::Tensor dy_, at::Tensor x, OT z, OT w, at::Tensor
 
 void bind_bn_nhwc(pybind11::module_& root) {
   auto m = root.def_submodule("bn_nhwc", "gfx950 fused NHWC batch norm (+add+ReLU)");
-  m.def("fwd_train", &fwd_train);
+  m.def("fwd_train", &fwd_train, pybind11::arg("x"), pybind11::arg("z"), pybind11::arg("w"), pybind11::arg("b"),
+        pybind11::arg("running_mean"), pybind11::arg("running_var"), pybind11::arg("momentum"), pybind11::arg("eps"),
+        pybind11::arg("relu"), pybind11::arg("want_mask") = false);
   m.def("fwd_eval", &fwd_eval);
   m.def("bwd", &bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("z"), pybind11::arg("w"),
         pybind11::arg("save_mean"), pybind11::arg("save_invstd"), pybind11::arg("coef_fwd"), pybind11::arg("relu"),
-        pybind11::arg("need_dz"), pybind11::arg("dy2") = c10::nullopt);
+        pybind11::arg("need_dz"), pybind11::arg("dy2") = c10::nullopt, pybind11::arg("mask") = c10::nullopt);
 }
 
 }  // namespace apex_amd

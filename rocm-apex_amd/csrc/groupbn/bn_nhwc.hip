@@ -184,10 +184,12 @@ __global__ void coef_from_stats(const float* __restrict__ mean, const float* __r
 }
 
 // ------------------------------------------------------------------------------------------
-template <typename T, bool HAS_Z, bool RELU>
+// MASKOUT: also write the ReLU mask as one bit per element (bit k of byte i = element 8i+k), so
+// the backward of a residual add+ReLU needs neither z nor a recompute (1/16 of a bf16 tensor)
+template <typename T, bool HAS_Z, bool RELU, bool MASKOUT>
 __global__ void __launch_bounds__(256) apply_kernel(const T* __restrict__ x, const T* __restrict__ z,
                                                     const float* __restrict__ coef, T* __restrict__ y, int64_t nvec,
-                                                    int c) {
+                                                    int c, uint8_t* __restrict__ mask) {
   const int64_t stride = (int64_t)gridDim.x * 256;
   const int cstep = (int)((stride * 8) % c);
   int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -208,18 +210,26 @@ __global__ void __launch_bounds__(256) apply_kernel(const T* __restrict__ x, con
       v[k] = o;
     }
     Vec8<T>::store(y + e, v);
+    if constexpr (MASKOUT) {
+      unsigned b = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) b |= (v[k] > 0.f ? 1u : 0u) << k;
+      mask[i] = (uint8_t)b;
+    }
   }
 }
 
 // ------------------------------------------------------------------------------------------
 // DY2: the output fed two consumers (a residual block's main and shortcut branches) and its
 // gradient arrives as two tensors, summed here in registers instead of by a separate add pass
-template <typename T, bool HAS_Z, bool RELU, bool WRITE_MASKED, bool DY2>
+// BITS: the ReLU mask comes from the forward's bit mask instead of a recompute from x (and z)
+template <typename T, bool HAS_Z, bool RELU, bool WRITE_MASKED, bool DY2, bool BITS>
 __global__ void __launch_bounds__(256) bwd_partial(const T* __restrict__ dy, const T* __restrict__ dy2,
                                                    const T* __restrict__ x,
                                                    const T* __restrict__ z, const float* __restrict__ coef,
                                                    const float* __restrict__ mean, T* __restrict__ dym, int64_t m,
-                                                   int c, float* __restrict__ part) {
+                                                   int c, float* __restrict__ part,
+                                                   const uint8_t* __restrict__ bits) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int TX = blockDim.x, TY = blockDim.y, tx = threadIdx.x, ty = threadIdx.y;
   const int c0 = (blockIdx.x * TX + tx) * 8;
@@ -229,7 +239,7 @@ __global__ void __launch_bounds__(256) bwd_partial(const T* __restrict__ dy, con
   for (int k = 0; k < 8; ++k) a1[k] = a2[k] = 0.f;
   if (active) {
     load8f(mu, mean + c0);
-    if constexpr (RELU) {
+    if constexpr (RELU && !BITS) {
       load8f(sc, coef + c0);
       load8f(sh, coef + c + c0);
     }
@@ -237,6 +247,7 @@ __global__ void __launch_bounds__(256) bwd_partial(const T* __restrict__ dy, con
   const int64_t R = (int64_t)TY * kU;
   for (int64_t base = (int64_t)blockIdx.y * R; base < m; base += R * gridDim.y) {
     float g[kU][8], v[kU][8];
+    unsigned mb[kU];
     bool ok[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
@@ -245,6 +256,7 @@ __global__ void __launch_bounds__(256) bwd_partial(const T* __restrict__ dy, con
       if (ok[u]) {
         Vec8<T>::load(g[u], dy + r * c + c0);
         Vec8<T>::load(v[u], x + r * c + c0);
+        if constexpr (BITS) mb[u] = bits[(r * c + c0) >> 3];
         if constexpr (DY2) {
           float h[8];
           Vec8<T>::load(h, dy2 + r * c + c0);
@@ -257,7 +269,12 @@ __global__ void __launch_bounds__(256) bwd_partial(const T* __restrict__ dy, con
     for (int u = 0; u < kU; ++u) {
       if (!ok[u]) continue;
       const int64_t e = (base + ty + (int64_t)u * TY) * c + c0;
-      if constexpr (RELU) {
+      if constexpr (RELU && BITS) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (!((mb[u] >> k) & 1u)) g[u][k] = 0.f;
+        if constexpr (WRITE_MASKED) Vec8<T>::store(dym + e, g[u]);
+      } else if constexpr (RELU) {
         float zz[8];
         if constexpr (HAS_Z) Vec8<T>::load(zz, z + e);
 #pragma unroll
@@ -396,17 +413,25 @@ void bn_nhwc_coef_from_stats(const float* mean, const float* v, bool is_var, con
 }
 
 void bn_nhwc_apply(const void* x, int x_t, const void* z, const float* coef_fwd, bool relu, void* y, int64_t m, int c,
-                   int cus, hipStream_t s) {
+                   int cus, hipStream_t s, uint8_t* mask_out) {
+  if (mask_out && !relu) throw std::runtime_error("bn_nhwc apply: a ReLU bit mask needs the fused ReLU");
   bnh::check_shape(m, c);
   const int64_t nvec = m * c / 8;
   const unsigned grid = bnh::ew_grid(nvec, cus);
   dispatch_float(x_t, [&](auto tag) {
     using T = typename decltype(tag)::type;
     auto go = [&](auto hz, auto rl) {
-      hipLaunchKernelGGL((bnh::apply_kernel<T, decltype(hz)::value, decltype(rl)::value>), dim3(grid), dim3(256), 0, s,
-                         (const T*)x, (const T*)z, coef_fwd, (T*)y, nvec, c);
+      hipLaunchKernelGGL((bnh::apply_kernel<T, decltype(hz)::value, decltype(rl)::value, false>), dim3(grid), dim3(256),
+                         0, s, (const T*)x, (const T*)z, coef_fwd, (T*)y, nvec, c, nullptr);
     };
-    if (z) {
+    if (mask_out) {
+      if (z)
+        hipLaunchKernelGGL((bnh::apply_kernel<T, true, true, true>), dim3(grid), dim3(256), 0, s, (const T*)x,
+                           (const T*)z, coef_fwd, (T*)y, nvec, c, mask_out);
+      else
+        hipLaunchKernelGGL((bnh::apply_kernel<T, false, true, true>), dim3(grid), dim3(256), 0, s, (const T*)x,
+                           (const T*)z, coef_fwd, (T*)y, nvec, c, mask_out);
+    } else if (z) {
       if (relu) go(std::true_type{}, std::true_type{});
       else go(std::true_type{}, std::false_type{});
     } else {
@@ -420,7 +445,9 @@ void bn_nhwc_apply(const void* x, int x_t, const void* z, const float* coef_fwd,
 void bn_nhwc_bwd_reduce(const void* dy, const void* x, int x_t, const void* z, const float* coef_fwd, bool relu,
                         const float* save_mean, const float* save_invstd, const float* w, float* grad_w, float* grad_b,
                         float* coef_bwd, void* dy_masked_out, int64_t m, int c, float* ws, int gy, int cus,
-                        hipStream_t s, const void* dy2) {
+                        hipStream_t s, const void* dy2, const uint8_t* mask_in) {
+  if (mask_in && !(relu && dy_masked_out))
+    throw std::runtime_error("bn_nhwc bwd: the ReLU bit mask path writes the masked gradient");
   if (dy2 && !(relu && dy_masked_out))
     throw std::runtime_error("bn_nhwc bwd: a second gradient needs the fused-ReLU masked-gradient path");
   bnh::check_shape(m, c);
@@ -431,13 +458,21 @@ void bn_nhwc_bwd_reduce(const void* dy, const void* x, int x_t, const void* z, c
     using T = typename decltype(tag)::type;
     auto go = [&](auto hz, auto rl, auto wm, auto d2) {
       hipLaunchKernelGGL((bnh::bwd_partial<T, decltype(hz)::value, decltype(rl)::value, decltype(wm)::value,
-                                           decltype(d2)::value>),
+                                           decltype(d2)::value, false>),
                          dim3(g.gx, g.gy), dim3(g.tx, g.ty), lds, s, (const T*)dy, (const T*)dy2, (const T*)x,
-                         (const T*)z, coef_fwd, save_mean, (T*)dy_masked_out, m, c, ws);
+                         (const T*)z, coef_fwd, save_mean, (T*)dy_masked_out, m, c, ws, nullptr);
+    };
+    auto go_bits = [&](auto d2) {
+      hipLaunchKernelGGL((bnh::bwd_partial<T, false, true, true, decltype(d2)::value, true>), dim3(g.gx, g.gy),
+                         dim3(g.tx, g.ty), lds, s, (const T*)dy, (const T*)dy2, (const T*)x, nullptr, coef_fwd,
+                         save_mean, (T*)dy_masked_out, m, c, ws, mask_in);
     };
     using F = std::false_type;
     using Tr = std::true_type;
-    if (!relu) go(F{}, F{}, F{}, F{});
+    if (mask_in) {
+      if (dy2) go_bits(Tr{});
+      else go_bits(F{});
+    } else if (!relu) go(F{}, F{}, F{}, F{});
     else if (z && dy_masked_out) {
       if (dy2) go(Tr{}, Tr{}, Tr{}, Tr{});
       else go(Tr{}, Tr{}, Tr{}, F{});

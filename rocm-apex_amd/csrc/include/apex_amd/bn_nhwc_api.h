@@ -32,8 +32,9 @@ void bn_nhwc_stats(const void* x, int x_t, int64_t m, int c, const float* w, con
 void bn_nhwc_coef_from_stats(const float* mean, const float* var_or_invstd, bool is_var, const float* w,
                              const float* b, float eps, int c, float* coef_fwd, hipStream_t s);
 
+// mask_out (relu only, optional): one bit per element of (y > 0), [m * c / 8] bytes
 void bn_nhwc_apply(const void* x, int x_t, const void* z, const float* coef_fwd, bool relu, void* y, int64_t m, int c,
-                   int cus, hipStream_t s);
+                   int cus, hipStream_t s, uint8_t* mask_out = nullptr);
 
 // backward reduction: grad_w / grad_b (fp32) and coef_bwd; optionally writes the ReLU-masked dy
 // (needed as grad_z for the add+relu variant); dy2 (optional, relu + dy_masked_out only) is a
@@ -41,7 +42,7 @@ void bn_nhwc_apply(const void* x, int x_t, const void* z, const float* coef_fwd,
 void bn_nhwc_bwd_reduce(const void* dy, const void* x, int x_t, const void* z, const float* coef_fwd, bool relu,
                         const float* save_mean, const float* save_invstd, const float* w, float* grad_w,
                         float* grad_b, float* coef_bwd, void* dy_masked_out, int64_t m, int c, float* ws, int gy,
-                        int cus, hipStream_t s, const void* dy2 = nullptr);
+                        int cus, hipStream_t s, const void* dy2 = nullptr, const uint8_t* mask_in = nullptr);
 
 // dx = A * dy' + B * x + K   (dy' masked in registers when relu && !dy_is_masked)
 void bn_nhwc_bwd_apply(const void* dy, bool dy_is_masked, const void* x, int x_t, const void* z,

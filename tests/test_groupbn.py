@@ -183,3 +183,30 @@ def test_gpu_fused_resnet50_step_matches_plain():
         # conv1 sits under all of them): allow 5e-2
         rel = float((q.grad - p.grad).norm() / p.grad.norm().clamp_min(1e-12))
         assert rel < 5e-2, (n, rel)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("two_grads", [False, True])
+def test_gpu_bn_relu_bitmask_matches_recompute(two_grads):
+    """Residual add+ReLU backward from the forward's 1-bit ReLU mask == mask recomputed from x, z."""
+    from apex import _native
+
+    ext = _native.require("bn_nhwc").bn_nhwc
+    torch.manual_seed(0)
+    m, c = 4 * 14 * 14, 256
+    x = torch.randn(m, c, device="cuda", dtype=torch.bfloat16)
+    z = torch.randn(m, c, device="cuda", dtype=torch.bfloat16)
+    w = torch.rand(c, device="cuda") + 0.5
+    b = torch.randn(c, device="cuda") * 0.1
+    y, sm, si, coef, mask = ext.fwd_train(x, z, w, b, None, None, 0.1, 1e-5, True, True)
+    assert mask.dtype == torch.uint8 and mask.numel() * 8 == m * c
+    bits = torch.stack([(mask >> k) & 1 for k in range(8)], dim=1).reshape(m, c).bool()
+    assert torch.equal(bits, y > 0)
+    y_ref, _, _, _, none_mask = ext.fwd_train(x, z, w, b, None, None, 0.1, 1e-5, True, False)
+    assert torch.equal(y, y_ref) and (none_mask is None or none_mask.numel() == 0)
+    dy = torch.randn_like(x)
+    dy2 = torch.randn_like(x) if two_grads else None
+    ref = ext.bwd(dy, x, z, w, sm, si, coef, True, True, dy2)
+    got = ext.bwd(dy, x, None, w, sm, si, coef, True, True, dy2, mask)
+    for a, r in zip(got, ref):
+        assert torch.equal(a, r)

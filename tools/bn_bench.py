@@ -45,12 +45,14 @@ def main():
         b = torch.randn(c, device=dev) * 0.1
         rm, rv = torch.zeros(c, device=dev), torch.ones(c, device=dev)
         relu = kind != "plain"
-        y, sm, si, coef = ext.fwd_train(x, z, w, b, rm, rv, 0.1, 1e-5, relu)
-        tf = timeit(lambda: ext.fwd_train(x, z, w, b, rm, rv, 0.1, 1e-5, relu))
+        bits = z is not None and os.environ.get("APEX_BN_BITS", "1") != "0"
+        y, sm, si, coef, mask = ext.fwd_train(x, z, w, b, rm, rv, 0.1, 1e-5, relu, bits)
+        tf = timeit(lambda: ext.fwd_train(x, z, w, b, rm, rv, 0.1, 1e-5, relu, bits))
         dy = torch.randn_like(x)
         dy2 = torch.randn_like(x) if kind == "zrelu2" else None
         need_dz = kind == "zrelu2"
-        tb = timeit(lambda: ext.bwd(dy, x, z, w, sm, si, coef, relu, need_dz, dy2))
+        zb = None if bits else z
+        tb = timeit(lambda: ext.bwd(dy, x, zb, w, sm, si, coef, relu, need_dz, dy2, mask if bits else None))
         e = m * c * 2
         nf = 3 + (1 if z is not None else 0)
         # bwd passes: reduce reads dy[,dy2],x[,z] (+writes dz); apply reads dy|dz, x [,z], writes dx
