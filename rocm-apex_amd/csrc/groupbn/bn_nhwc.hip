@@ -18,7 +18,9 @@
 //            2. bwd_finalize  : grad_w, grad_b and dx = A*dy' + B*x + K constants
 //            3. bwd_apply     : dx in one FMA pair per element
 // Passes over the activation per layer: fwd 3 (x, x, y) [+z], bwd 5 (dy, x, dy, x, dx) — vs
-// 5 / 8 for MIOpen BN + separate ReLU / threshold-backward kernels.
+// 5 / 8 for MIOpen BN + separate ReLU / threshold-backward kernels.  Residual add+ReLU layers
+// also write the ReLU mask as 1 bit per element in the apply pass (1/16 of a bf16 pass); their
+// backward reduction masks dy with those bits, so z is neither re-read nor kept alive.
 #include "apex_amd/bn_nhwc_api.h"
 #include "apex_amd/device.h"
 #include "apex_amd/dispatch.h"
