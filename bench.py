@@ -103,10 +103,14 @@ def main():
         return timed(args, step, dev, world, rank, distributed, B, "apex", desc)
     if args.impl == "torch":
         return run_torch_baseline(args, dev, world, rank, distributed, resnet_mod)
-    fused_bn = args.bn == "fused" and not (args.sync_bn and distributed) and not args.no_channels_last
-    model = getattr(resnet_mod, args.arch)(fused_bn=fused_bn)
-    if args.sync_bn and distributed:
-        model = apex.parallel.convert_syncbn_model(model, channel_last=not args.no_channels_last)
+    fused_bn = args.bn == "fused" and not args.no_channels_last
+    sync_bn = args.sync_bn and distributed
+    # --sync-bn: with the fused NHWC batch norm every BN layer reduces its statistics over the
+    # whole job (bn_group = world, exchanged through xGMI peer memory, RCCL fallback); otherwise
+    # torch BNs are converted to apex SyncBatchNorm (channels_last memory is auto-detected)
+    model = getattr(resnet_mod, args.arch)(fused_bn=fused_bn, bn_group=world if (sync_bn and fused_bn) else 1)
+    if sync_bn and not fused_bn:
+        model = apex.parallel.convert_syncbn_model(model)
     model = model.to(dev)
     mf = torch.contiguous_format if args.no_channels_last else torch.channels_last
     model = model.to(memory_format=mf)
@@ -225,8 +229,10 @@ def timed(args, step, dev, world, rank, distributed, B, impl, desc=None):
                 if impl == "apex" else "torch.optim.AdamW(fused=True)",
                 "channels_last": not args.no_channels_last,
                 "sync_bn": bool(args.sync_bn and distributed),
-                "batchnorm": ("apex fused NHWC BN+ReLU/add+ReLU (gfx950)" if (impl == "apex" and args.bn == "fused"
-                              and not args.no_channels_last) else "torch BatchNorm2d (MIOpen)"),
+                "batchnorm": (("apex fused NHWC BN+ReLU/add+ReLU (gfx950)" + (
+                    ", stats synchronized over all ranks (bn_group=world)" if (args.sync_bn and distributed) else ""))
+                    if (impl == "apex" and args.bn == "fused" and not args.no_channels_last)
+                    else ("apex SyncBatchNorm" if (args.sync_bn and distributed) else "torch BatchNorm2d (MIOpen)")),
                 "parallelism": f"dp{world}",
                 "final_loss": round(float(loss.item()), 4),
             },

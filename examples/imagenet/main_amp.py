@@ -112,10 +112,14 @@ def main():
     if distributed:
         dist.init_process_group(backend="nccl", init_method="env://")
     torch.backends.cudnn.benchmark = True
-    fused_bn = args.bn == "fused" and args.channels_last and not args.sync_bn
-    model = getattr(resnet_mod, args.arch)(fused_bn=fused_bn)
-    if args.sync_bn:
-        model = apex.parallel.convert_syncbn_model(model, channel_last=args.channels_last)
+    fused_bn = args.bn == "fused" and args.channels_last
+    sync = args.sync_bn and distributed
+    # fused NHWC BN: --sync_bn shares the statistics over all ranks inside the fused kernels
+    # (bn_group = world); torch BN: converted to apex SyncBatchNorm, which detects channels_last
+    # memory by itself
+    model = getattr(resnet_mod, args.arch)(fused_bn=fused_bn, bn_group=world if (sync and fused_bn) else 1)
+    if sync and not fused_bn:
+        model = apex.parallel.convert_syncbn_model(model)
     model = model.cuda()
     if args.channels_last:
         model = model.to(memory_format=torch.channels_last)

@@ -12,7 +12,10 @@ class AmpState(object):
         self.verbosity = 1
         # MI355X addition: keep the dynamic loss scaler on the device (no per-step .item()) when
         # every optimizer handed to amp can consume a device skip flag.
+        # "0" = reference (sync) scaler; "force" = sync-free even without a GPU (the device-side
+        # scaler then runs its torch reference ops on the CPU: used by the CPU test tier)
         self.sync_free_requested = os.environ.get("APEX_AMD_AMP_SYNC_FREE", "1") != "0"
+        self.sync_free_force = os.environ.get("APEX_AMD_AMP_SYNC_FREE", "1") == "force"
         self.sync_free = False
         self.loss_scalers = []
 

@@ -190,7 +190,8 @@ def _initialize(models, optimizers, properties, num_losses=1, cast_model_outputs
 
     # sync-free scaler when every optimizer consumes a device skip flag
     all_capable = len(optimizers) > 0 and all(getattr(o, "_amp_fused_capable", False) for o in optimizers)
-    _amp_state.sync_free = bool(_amp_state.sync_free_requested and all_capable and torch.cuda.is_available())
+    _amp_state.sync_free = bool(_amp_state.sync_free_requested and all_capable and (
+        torch.cuda.is_available() or getattr(_amp_state, "sync_free_force", False)))
     for o in optimizers:
         o._amp_stash.fused_ok = _amp_state.sync_free
 

@@ -4,6 +4,12 @@ Reference behaviour is kept: with master weights, fp16/bf16 params are replaced 
 groups by fp32 masters, grads are unscaled into fp32 master grads after backward, and the
 masters are copied back into the model after ``step()``.
 
+Data parallel: gradients of parameters owned by ``apex.parallel.DistributedDataParallel`` are
+views into its persistent all-reduce buckets.  Where the single-GPU fused path drops grads (sets
+them to None, letting autograd hand over fresh buffers), DDP-owned grads are instead zeroed in
+place, one memset per bucket (``parallel.distributed.zero_bucketed_grads``), so backward keeps
+accumulating into the buckets and nothing is copied per parameter.
+
 MI355X fast path ("fused amp"): when the optimizer is one of this package's fused optimizers
 constructed with ``materialize_master_grads=False`` and the loss scaler runs sync-free, no fp32
 master grads are materialized at all.  After backward only a read-only overflow probe runs
@@ -30,6 +36,29 @@ class AmpOptimizerState(object):
 
 def _is_fused_amp(opt):
     return bool(getattr(opt, "_amp_fused_capable", False)) and not getattr(opt, "materialize_master_grads", True)
+
+
+def _ddp():
+    from ..parallel import distributed
+
+    return distributed
+
+
+def _reset_grads(params, to_none):
+    """Reset model grads after a step / on zero_grad: DDP-owned ones are zeroed in their buckets
+    (views kept), the rest set to None (``to_none``) or zeroed in place."""
+    owned = _ddp().zero_bucketed_grads(params)
+    for param in params:
+        if id(param) in owned or param.grad is None:
+            continue
+        if to_none:
+            param.grad = None
+        else:
+            if param.grad.grad_fn is not None:
+                param.grad.detach_()
+            else:
+                param.grad.requires_grad_(False)
+            param.grad.zero_()
 
 
 def _master_params_to_model_params(self):
@@ -118,14 +147,20 @@ def prepare_backward_with_master_weights(self):
     stash.exit_mode = "ref"
     if _is_fused_amp(self) and stash.fused_ok and not any(
             p.grad is not None for p in stash.all_fp32_from_fp16_params):
-        # fused exit: keep existing (still scaled) grads aside; fresh grads land in .grad
+        # fused exit: keep existing (still scaled) grads aside; fresh grads land in .grad.  A
+        # DDP bucket view known to be zero stays attached (backward accumulates into the bucket);
+        # a non-zero one is stashed as a copy, since the bucket is about to be overwritten
         stash.exit_mode = "fused"
-        for i, param in enumerate(stash.all_fp16_params):
-            stash.all_fp16_grad_stash[i] = param.grad
-            param.grad = None
-        for i, param in enumerate(stash.all_fp32_from_fp32_params):
-            stash.all_fp32_from_fp32_grad_stash[i] = param.grad
-            param.grad = None
+        zero_views = _ddp().zeroed_bucket_params(stash.all_fp16_params + stash.all_fp32_from_fp32_params)
+        for params, stashed in ((stash.all_fp16_params, stash.all_fp16_grad_stash),
+                                (stash.all_fp32_from_fp32_params, stash.all_fp32_from_fp32_grad_stash)):
+            for i, param in enumerate(params):
+                g = param.grad
+                if g is None or id(param) in zero_views:
+                    stashed[i] = None
+                    continue
+                stashed[i] = g.clone() if getattr(param, "_apex_ddp_owner", None) is not None else g
+                param.grad = None
         return
     for param in stash.all_fp16_params:
         param.grad = None
@@ -328,10 +363,7 @@ def _process_optimizer(optimizer, properties):
                 param.grad = None
             if st.fused_pending:
                 # model grads were consumed directly by the fused kernel
-                for param in st.all_fp16_params:
-                    param.grad = None
-                for param in st.all_fp32_from_fp32_params:
-                    param.grad = None
+                _reset_grads(st.all_fp16_params + st.all_fp32_from_fp32_params, True)
                 st.fused_pending = False
             return retval
 
@@ -341,19 +373,7 @@ def _process_optimizer(optimizer, properties):
             st = self._amp_stash
             self._amp_lazy_init()
             to_none = _is_fused_amp(self) if set_to_none is None else set_to_none
-            for param in st.all_fp16_params + st.all_fp32_from_fp32_params:
-                if param.grad is not None:
-                    if to_none:
-                        param.grad = None
-                    else:
-                        # as torch.optim.Optimizer.zero_grad: grads may be views into a DDP
-                        # bucket (apex.parallel.DistributedDataParallel keeps them there), which
-                        # cannot be detached in place
-                        if param.grad.grad_fn is not None:
-                            param.grad.detach_()
-                        else:
-                            param.grad.requires_grad_(False)
-                        param.grad.zero_()
+            _reset_grads(st.all_fp16_params + st.all_fp32_from_fp32_params, to_none)
             for param in st.all_fp32_from_fp16_params:
                 param.grad = None
 

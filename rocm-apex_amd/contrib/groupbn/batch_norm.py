@@ -8,11 +8,21 @@ NCHW-shaped tensor in ``torch.channels_last`` memory (what convolutions produce)
 to the kernels as the same zero-copy ``[M, C]`` view and the output keeps the input's layout.
 
 ``bn_group > 1`` (statistics shared by groups of adjacent ranks; the reference does this through
-CUDA-IPC peer memory and compiles it out on HIP): the per-rank (mean, var, count) and the backward
-(sum_dy, sum_dy_xmu) are exchanged through hipIpc peer buffers over xGMI — one single-workgroup
-push/flag-wait kernel per layer (``apex.parallel.peer_memory``) — or, with ``peer_memory=False``,
-by an RCCL sub-group all-gather / all-reduce.  CPU tensors
-and channel counts that are not a multiple of 8 use the generic SyncBatchNorm primitives.
+CUDA-IPC peer memory and compiles it out on HIP): the SAME fused kernels run in two halves around
+one tiny exchange per direction (``_BnNHWCGroupFunction``):
+
+* forward: stats pass -> local payload [mean | M2 | count] (2C+1 floats) -> exchange -> a merge
+  kernel that combines the group's payloads in rank order (identical result on every member) and
+  writes the apply constants -> the fused apply pass (+z, +ReLU, +ReLU bit mask);
+* backward: reduction pass (masking, second-gradient sum) -> local [sum_dy | sum_dy_xmu] ->
+  exchange -> coefficient kernel -> the fused dx pass.
+
+The exchange is a hipIpc peer-memory push/flag-wait kernel over xGMI (``apex.parallel.peer_memory``,
+one single-workgroup launch, no RCCL protocol round trip per layer) or, with ``peer_memory=False``
+/ no peer support, an RCCL sub-group ``all_gather_into_tensor`` / ``all_reduce``.  Weight / bias
+gradients stay LOCAL (the data-parallel reduction averages them like every other gradient), as in
+the reference's SyncBatchNorm.  CPU tensors and channel counts that are not a multiple of 8 use the
+generic SyncBatchNorm primitives.
 """
 import os
 
@@ -106,6 +116,100 @@ class _BnNHWCFunction(torch.autograd.Function):
         return dx, dz, gw, gb, None, None, None, None, None, None, None, None
 
 
+def _exchange_gather(payload, group):
+    """[world, n] fp32: every group member's ``payload`` (peer memory, else RCCL / gloo)."""
+    import torch.distributed as dist
+
+    from ...parallel.peer_memory import get_peer_exchange
+
+    peer = get_peer_exchange(group)
+    if peer is not None:
+        return peer.all_gather(payload)
+    world = dist.get_world_size(group)
+    if dist.get_backend(group) == "nccl":
+        out = torch.empty(world, payload.numel(), dtype=payload.dtype, device=payload.device)
+        dist.all_gather_into_tensor(out, payload, group=group)
+        return out
+    host = payload.cpu()  # gloo (rehearsal / tests): host staging
+    parts = [torch.empty_like(host) for _ in range(world)]
+    dist.all_gather(parts, host, group=group)
+    return torch.stack(parts, 0).to(payload.device)
+
+
+def _exchange_sum(payload, group):
+    """Group sums as [rows, n] rows to be added in order by the consumer kernel: the peer path
+    hands back every member's row (summed in rank order in-kernel, identical on all members),
+    the collective path one all-reduced row."""
+    import torch.distributed as dist
+
+    from ...parallel.peer_memory import get_peer_exchange
+
+    peer = get_peer_exchange(group)
+    if peer is not None:
+        return peer.all_gather(payload)
+    if dist.get_backend(group) == "nccl":
+        out = payload.clone()
+        dist.all_reduce(out, dist.ReduceOp.SUM, group=group)
+        return out.view(1, -1)
+    host = payload.cpu()
+    dist.all_reduce(host, dist.ReduceOp.SUM, group=group)
+    return host.to(payload.device).view(1, -1)
+
+
+class _BnNHWCGroupFunction(torch.autograd.Function):
+    """bn_group > 1: fused NHWC batch norm with the statistics reduced over ``group``."""
+
+    @staticmethod
+    def forward(ctx, x, z, weight, bias, running_mean, running_var, momentum, eps, fuse_relu, group,
+                torch_channels_last, fork=False):
+        ctx.set_materialize_grads(False)
+        x2 = _to_2d(x, torch_channels_last)
+        z2 = _to_2d(z, torch_channels_last)
+        ext = _ext()
+        gathered = _exchange_gather(ext.fwd_group_local(x2), group)
+        bits = bool(fuse_relu) and z2 is not None
+        y2, save_mean, save_invstd, coef, mask, inv_count = ext.fwd_group_finish(
+            x2, z2, gathered, weight, bias, running_mean, running_var, float(momentum), float(eps), bool(fuse_relu),
+            bits)
+        ctx.save_for_backward(x2, None if bits else z2, weight, save_mean, save_invstd, coef,
+                              mask if bits else None, inv_count)
+        ctx.fuse_relu = fuse_relu
+        ctx.has_z = z is not None
+        ctx.group = group
+        ctx.layout = (torch_channels_last, x.shape)
+        y = _from_2d(y2, x, torch_channels_last)
+        if fork:
+            return y, y.view_as(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, grad_y, grad_y2=None):
+        x2, z2, weight, save_mean, save_invstd, coef, mask, inv_count = ctx.saved_tensors
+        if grad_y is None:
+            grad_y, grad_y2 = grad_y2, None
+        if grad_y is None:
+            # every member must still join the exchange: contribute zero gradient sums
+            grad_y = torch.zeros_like(x2)
+            g2 = grad_y
+        else:
+            g2 = _to_2d(grad_y, ctx.layout[0])
+        gg2 = _to_2d(grad_y2, ctx.layout[0]) if grad_y2 is not None else None
+        ext = _ext()
+        payload, gw, gb, dym = ext.bwd_group_local(g2, x2, z2, weight, save_mean, save_invstd, coef,
+                                                   bool(ctx.fuse_relu), gg2, mask)
+        sums = _exchange_sum(payload, ctx.group)
+        dx2 = ext.bwd_group_finish(dym, x2, sums, inv_count, weight, save_mean, save_invstd, coef)
+        tcl, shape = ctx.layout
+        like = torch.empty(shape, device="meta")
+        dx = _from_2d(dx2, like, tcl)
+        dz = None
+        if ctx.has_z and ctx.needs_input_grad[1]:
+            dz = _from_2d(dym, like, tcl)
+        gw = gw if (weight is not None and ctx.needs_input_grad[2]) else None
+        gb = gb if (weight is not None and ctx.needs_input_grad[3]) else None
+        return dx, dz, gw, gb, None, None, None, None, None, None, None, None
+
+
 def _reference_bn(x, z, weight, bias, running_mean, running_var, momentum, eps, fuse_relu, training, channels_last_dim):
     """torch / generic-kernel path (CPU, C % 8 != 0): SyncBatchNorm primitives on an [M, C] view."""
     from ...parallel.optimized_sync_batchnorm import SyncBatchnormFunction
@@ -165,6 +269,20 @@ class BatchNorm2d_NHWC(_BatchNorm):
 
                 enable_peer_memory(self.process_group)
 
+    def synchronize_over(self, process_group=None, peer_memory=True):
+        """Share the training statistics over ``process_group`` (None = every rank) — what
+        ``apex.parallel.convert_syncbn_model`` does to this module.  Collective when peer memory
+        is enabled (every member must call it in the same order)."""
+        import torch.distributed as dist
+
+        self.process_group = process_group
+        self.bn_group = dist.get_world_size(process_group)
+        if self.bn_group > 1 and peer_memory and torch.cuda.is_available():
+            from ...parallel.peer_memory import enable_peer_memory
+
+            enable_peer_memory(self.process_group)
+        return self
+
     def _check_input_dim(self, input):
         if input.dim() != 4:
             raise ValueError("expected 4D input (got {}D input)".format(input.dim()))
@@ -174,6 +292,12 @@ class BatchNorm2d_NHWC(_BatchNorm):
             assert self.fuse_relu, "BatchNorm2d_NHWC: z (residual) requires fuse_relu=True"
         training = self.training or not self.track_running_stats
         if self.bn_group > 1 and training:
+            c = x.size(1) if (self.torch_channels_last and x.dim() == 4) else x.size(-1)
+            if (_native.use_native(x) and c % 8 == 0 and self.weight is not None
+                    and self.weight.dtype == torch.float32):
+                return _BnNHWCGroupFunction.apply(x, z, self.weight, self.bias, self.running_mean, self.running_var,
+                                                  self.momentum, self.eps, self.fuse_relu, self.process_group,
+                                                  self.torch_channels_last, fork)
             from ...parallel.optimized_sync_batchnorm import SyncBatchnormFunction
 
             xv = x.permute(0, 2, 3, 1) if self.torch_channels_last else x

@@ -23,6 +23,12 @@ MI355X design:
     (``all_gather_into_tensor`` — stock RCCL, no ``no_copy`` extension).
   * optional e5m2 (fp8) all-gather compression, global grad-norm clipping, and sync-free
     overflow handling (device skip flag + inverse scale consumed by the kernels).
+  * two-level data parallelism (reference ``dwu_group_size``: shard within groups of G ranks,
+    replicate across the world/G groups): each block is reduce-scattered inside the group, then
+    this rank's shard is all-reduced across the groups over ``ar_group`` (the ranks holding the
+    same shard index; reference :409-418).  Optional fp32 accumulation (``reduce_dtype``) and
+    pre-division by the data-parallel size before the sum (``predivide``).
+  * ``mode="ar"`` (reference v3): all-reduce the whole block, keep this rank's slice.
 """
 import math
 
@@ -34,7 +40,7 @@ _ALIGN = 128  # elements; keeps every param / shard 16-byte aligned for the vect
 
 class FlatShardedBuffers:
     def __init__(self, params, process_group=None, num_blocks=4, min_block_elems=1 << 20, grad_dtype=None,
-                 overlap_reductions=True):
+                 overlap_reductions=True, ar_group=None, reduce_dtype=None, predivide=False, mode="rs"):
         params = [p for p in params if p.requires_grad]
         assert params, "no trainable parameters"
         dtypes = {p.dtype for p in params}
@@ -49,6 +55,13 @@ class FlatShardedBuffers:
         self.params = params
         self.overlap = overlap_reductions
         self._gloo = dist.is_initialized() and dist.get_backend(process_group) == "gloo"
+        assert mode in ("rs", "ar"), mode
+        self.mode = mode
+        self.ar_pg = ar_group
+        self.ar_world = dist.get_world_size(ar_group) if (ar_group is not None and dist.is_initialized()) else 1
+        self.dp_size = self.world * self.ar_world  # ranks whose gradients are averaged
+        self.reduce_dtype = reduce_dtype or self.grad_dtype
+        self.predivide = bool(predivide)
 
         # layout: reverse order (gradients arrive roughly last-layer-first)
         order = list(reversed(range(len(params))))
@@ -85,8 +98,7 @@ class FlatShardedBuffers:
         self.param_blocks = [[b for b in range(nb) if i in self.block_params[b]] for i in range(len(params))]
 
         # this rank's shards: [num_blocks, shard] fp32 masters + reduced-grad staging
-        self.shard_grad = torch.zeros(nb, self.shard, dtype=torch.float32 if self.grad_dtype == torch.float32
-                                      else self.grad_dtype, device=self.device)
+        self.shard_grad = torch.zeros(nb, self.shard, dtype=self.reduce_dtype, device=self.device)
         self.master = torch.empty(nb, self.shard, dtype=torch.float32, device=self.device)
         with torch.no_grad():
             for b in range(nb):
@@ -162,24 +174,63 @@ class FlatShardedBuffers:
                     self._reduce_block(b)
         return hook
 
-    def _reduce_block(self, b):
-        if self._handles[b] is not None:
-            return
+    def _issue_block(self, b, again=False):
+        """Queue block ``b``'s reduction; returns (pending works, reduced shard tensor)."""
         src = self.block_view(self.flat_grad, b)
         dst = self.shard_grad[b]
+        # the gradient buffer itself is never modified (a shared parameter can make a block be
+        # reduced twice); scaling / widening / the in-place all-reduce work on a copy
+        pre = self.predivide and self.dp_size > 1
+        red = src
+        if self.reduce_dtype != src.dtype:
+            red = src.to(self.reduce_dtype)
+            if pre:
+                red.mul_(1.0 / self.dp_size)
+        elif pre:
+            red = src * (1.0 / self.dp_size)
+        elif again or self.mode == "ar":
+            red = src.clone()
         if self.world == 1:
-            dst.copy_(src)
+            out = red
+        elif self.mode == "rs":
+            out = dst if dst.dtype == red.dtype else torch.empty(self.shard, dtype=red.dtype, device=self.device)
+            w = dist.reduce_scatter_tensor(out, red, group=self.pg, async_op=True)
+            if self.ar_pg is None:
+                return [w], out
+            w.wait()  # NCCL: the issuing (side) stream waits on the reduce-scatter, not the host
+        else:  # "ar" (reference v3): whole-block all-reduce, keep this rank's slice
+            w = dist.all_reduce(red, group=self.pg, async_op=True)
+            out = red[self.rank * self.shard:(self.rank + 1) * self.shard]
+            if self.ar_pg is None:
+                return [w], out
+            w.wait()
+        if self.ar_pg is not None:
+            # inter-group: the same shard index of every group (reference :409-418)
+            return [dist.all_reduce(out, group=self.ar_pg, async_op=True)], out
+        return [], out
+
+    def _reduce_block(self, b, again=False):
+        if self._handles[b] is not None:
+            return
+        dst = self.shard_grad[b]
+        if self.dp_size == 1:
+            dst.copy_(self.block_view(self.flat_grad, b))
             self._handles[b] = True
             return
         if self._stream is not None:
             self._stream.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(self._stream):
-                out = dst if dst.dtype == src.dtype else torch.empty_like(src[:self.shard])
-                self._handles[b] = (dist.reduce_scatter_tensor(out, src, group=self.pg, async_op=True), out, dst)
+                works, out = self._issue_block(b, again)
         else:
-            out = dst if dst.dtype == src.dtype else torch.empty_like(src[:self.shard])
-            dist.reduce_scatter_tensor(out, src, group=self.pg)
-            self._handles[b] = (None, out, dst)
+            works, out = self._issue_block(b, again)
+        self._handles[b] = (works, out, dst)
+
+    def _finish(self, h):
+        works, out, dst = h
+        for w in works:
+            w.wait()
+        if out is not dst:
+            dst.copy_(out)
 
     def complete_reductions(self):
         """Reduce every block not reduced yet and wait for all of them."""
@@ -192,21 +243,14 @@ class FlatShardedBuffers:
         for b in range(self.num_blocks):
             h = self._handles[b]
             if isinstance(h, tuple):
-                work, out, dst = h
-                if work is not None:
-                    work.wait()
-                if out is not dst:
-                    dst.copy_(out)
+                self._finish(h)
         if self._stream is not None:
             torch.cuda.current_stream(self.device).wait_stream(self._stream)
         for b in sorted(self._dirty):
             self._handles[b] = None
-            self._reduce_block(b)
-            work, out, dst = self._handles[b] if isinstance(self._handles[b], tuple) else (None, None, None)
-            if work is not None:
-                work.wait()
-            if out is not None and out is not dst:
-                dst.copy_(out)
+            self._reduce_block(b, again=True)
+            if isinstance(self._handles[b], tuple):
+                self._finish(self._handles[b])
         if self._dirty and self._stream is not None:
             torch.cuda.current_stream(self.device).wait_stream(self._stream)
         self._dirty = set()

@@ -10,12 +10,42 @@ overflow anywhere skips the step on every rank through a device flag.
 Constructor keywords of the reference that only tune its CUDA pipeline (``dwu_num_rs_pg``,
 ``dwu_num_ar_pg``, ``dwu_num_ag_pg``, ``dwu_num_chunks``, ``flat_mt``, ``do_not_flatten_model``,
 ``num_process_groups``...) are accepted and ignored; ``dwu_num_blocks`` sets the number of
-reduce-scatter blocks and ``dwu_group_size`` / ``current_process_group`` the sharding group."""
+reduce-scatter blocks and ``dwu_group_size`` / ``current_process_group`` the sharding group.
+
+``dwu_group_size = G < world`` (reference :306-371, :397-441): optimizer state is sharded over
+groups of G consecutive ranks and replicated across the world/G groups; every block is
+reduce-scattered inside the group and the shard is then all-reduced across groups (ranks with
+the same index in their group), so every replica trains on the gradient of the whole job.
+``reduce_dtype=torch.float32`` accumulates the reduction in fp32 (bf16/fp16 grads are widened
+before the collective); ``predivide`` divides by the data-parallel size before the sum."""
 import torch
 import torch.distributed as dist
 
 from ... import amp_C
 from ._sharded import FlatShardedBuffers
+
+_TWO_LEVEL = {}
+
+
+def two_level_groups(group_size):
+    """(intra-group, inter-group) process groups for sharding over ``group_size`` consecutive
+    ranks: the caller's block of ranks, and the ranks that hold the same shard index in every
+    block.  Collective (every rank creates every group, same order); cached per size."""
+    if group_size in _TWO_LEVEL:
+        return _TWO_LEVEL[group_size]
+    world, rank = dist.get_world_size(), dist.get_rank()
+    assert world % group_size == 0, "world size must be a multiple of dwu_group_size"
+    intra = inter = None
+    for start in range(0, world, group_size):
+        g = dist.new_group(list(range(start, start + group_size)))
+        if start <= rank < start + group_size:
+            intra = g
+    for k in range(group_size):
+        g = dist.new_group(list(range(k, world, group_size)))
+        if rank % group_size == k:
+            inter = g
+    _TWO_LEVEL[group_size] = (intra, inter)
+    return intra, inter
 
 
 class DistributedFusedAdam(torch.optim.Optimizer):
@@ -25,7 +55,8 @@ class DistributedFusedAdam(torch.optim.Optimizer):
                  dwu_num_ar_pg=4, dwu_num_ag_pg=0, predivide=True, e5m2_allgather=False, do_not_flatten_model=False,
                  step_supports_amp_scaling=True, num_process_groups=1, current_process_group=None,
                  process_group_id=0, process_group_size=0, clip_grad_norm=True, model_parallel=False,
-                 adam_w_mode=True, min_block_elems=1 << 22):
+                 adam_w_mode=True, min_block_elems=1 << 22, reduce_dtype=None, grad_sync_dtype=None,
+                 _reduction_mode="rs"):
         if amsgrad:
             raise RuntimeError("DistributedFusedAdam does not support the AMSGrad variant.")
         defaults = dict(lr=lr, bias_correction=bias_correction, betas=betas, eps=eps, weight_decay=weight_decay,
@@ -42,15 +73,16 @@ class DistributedFusedAdam(torch.optim.Optimizer):
         self._L2_grad_norm = None
         self._global_scale = None
         self._last_step = False
-        pg = current_process_group
+        pg, ar_pg = current_process_group, None
         if pg is None and dwu_group_size and dist.is_initialized() and dwu_group_size < dist.get_world_size():
-            from ...contrib.groupbn.batch_norm import _bn_group
-
-            pg = _bn_group(dwu_group_size)
+            pg, ar_pg = two_level_groups(dwu_group_size)
         all_params = [p for g in self.param_groups for p in g["params"]]
         self._flat = FlatShardedBuffers(all_params, pg, num_blocks=dwu_num_blocks, min_block_elems=min_block_elems,
-                                        overlap_reductions=overlap_reductions)
+                                        overlap_reductions=overlap_reductions, ar_group=ar_pg,
+                                        reduce_dtype=reduce_dtype or grad_sync_dtype, predivide=predivide,
+                                        mode=_reduction_mode)
         self._pg = pg
+        self._ar_pg = ar_pg
         dev = self._flat.device
         self._m = torch.zeros_like(self._flat.master)
         self._v = torch.zeros_like(self._flat.master)
@@ -106,8 +138,8 @@ class DistributedFusedAdam(torch.optim.Optimizer):
         grads = flat.grad_shard_views()
         dev = flat.device
         inv = torch.ones(1, dtype=torch.float32, device=dev)
-        if self._predivide and flat.world > 1:
-            inv = inv / flat.world
+        if not flat.predivide and flat.dp_size > 1:
+            inv = inv / flat.dp_size  # average over every data-parallel rank (both levels)
         scale = None
         if grad_scaler is not None and grad_scaler.is_enabled():
             scale = grad_scaler._get_scale_async()
@@ -224,5 +256,11 @@ class DistributedFusedAdamV2(DistributedFusedAdam):
 
 
 class DistributedFusedAdamV3(DistributedFusedAdam):
-    """Reference v3 (flat all-reduce, sharded step, all-gather): identical results; the
-    reduce-scatter formulation moves half the bytes of all-reduce + slice."""
+    """Reference v3 (apex/contrib/optimizers/distributed_fused_adam_v3.py:7-325): every block is
+    ALL-REDUCED whole, the sharded fused step runs on this rank's slice of the result and the
+    parameters are all-gathered.  Moves twice the reduce bytes of the reduce-scatter
+    variant; results are identical."""
+
+    def __init__(self, *args, **kwargs):
+        kwargs["_reduction_mode"] = "ar"
+        super().__init__(*args, **kwargs)

@@ -20,13 +20,14 @@ class DistributedFusedLAMB(DistributedFusedAdam):
                  weight_decay=0.0, max_grad_norm=0.0, adam_w_mode=True, use_nvlamb=False,
                  step_supports_amp_scaling=True, overlap_reductions=True, dwu_group_size=0, dwu_num_blocks=4,
                  dwu_num_chunks=4, dwu_num_rs_pg=1, dwu_num_ar_pg=4, dwu_num_ag_pg=0, e5m2_allgather=False,
-                 verbose=False, clip_after_ar=True, min_block_elems=1 << 22, current_process_group=None):
+                 verbose=False, clip_after_ar=True, min_block_elems=1 << 22, current_process_group=None,
+                 reduce_dtype=None, predivide=True):
         super().__init__(params, lr=lr, bias_correction=bias_correction, betas=betas, eps=eps,
                          weight_decay=weight_decay, max_grad_norm=max_grad_norm, overlap_reductions=overlap_reductions,
                          compute_L2_grad_norm=True, dwu_group_size=dwu_group_size, dwu_num_blocks=dwu_num_blocks,
                          e5m2_allgather=e5m2_allgather, step_supports_amp_scaling=step_supports_amp_scaling,
                          clip_grad_norm=clip_after_ar, adam_w_mode=adam_w_mode, min_block_elems=min_block_elems,
-                         current_process_group=current_process_group)
+                         current_process_group=current_process_group, reduce_dtype=reduce_dtype, predivide=predivide)
         for g in self.param_groups:
             g["grad_averaging"] = grad_averaging
         self._use_nvlamb = use_nvlamb

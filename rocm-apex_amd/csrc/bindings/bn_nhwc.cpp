@@ -129,6 +129,121 @@ std::vector<at::Tensor> bwd(at::Tensor dy_, at::Tensor x, OT z, OT w, at::Tensor
   return {dx, dz, gw, gb};
 }
 
+// ---- bn_group > 1: the python layer exchanges the payloads between the two halves ----------
+
+// forward, step 1: [mean(C) | M2(C) | count] of this rank's batch
+at::Tensor fwd_group_local(at::Tensor x) {
+  check2d(x, "input");
+  const c10::hip::HIPGuard g(x.get_device());
+  const int64_t m = x.size(0);
+  const int c = (int)x.size(1);
+  const int cus = device_cus(x.get_device());
+  int64_t wsf = 0;
+  const int gy = bn_nhwc_plan(m, c, cus, &wsf);
+  auto fo = x.options().dtype(at::kFloat);
+  auto ws = at::empty({wsf}, fo);
+  auto payload = at::empty({2 * (int64_t)c + 1}, fo);
+  bn_nhwc_stats_local(x.data_ptr(), dtype_code(x.scalar_type()), m, c, payload.data_ptr<float>(),
+                      ws.data_ptr<float>(), gy, cus, cur_stream());
+  return payload;
+}
+
+// forward, step 2: merge the group's [world, 2C+1] payloads, then normalize (+z, +ReLU, +mask)
+std::vector<at::Tensor> fwd_group_finish(at::Tensor x, OT z, at::Tensor gathered, OT w, OT b, OT running_mean,
+                                         OT running_var, double momentum, double eps, bool relu, bool want_mask) {
+  TORCH_CHECK(!want_mask || relu, "bn_nhwc: the ReLU bit mask needs relu=True");
+  check2d(x, "input");
+  const c10::hip::HIPGuard g(x.get_device());
+  const int64_t m = x.size(0);
+  const int c = (int)x.size(1);
+  for (const OT* p : {&w, &b, &running_mean, &running_var}) check_param(*p, c);
+  TORCH_CHECK(gathered.is_cuda() && gathered.scalar_type() == at::kFloat && gathered.is_contiguous() &&
+                  gathered.dim() == 2 && gathered.size(1) == 2 * (int64_t)c + 1,
+              "bn_nhwc: gathered statistics must be a contiguous fp32 [world, 2C+1] GPU tensor");
+  if (has(z)) {
+    check2d(*z, "z");
+    TORCH_CHECK(z->sizes() == x.sizes() && z->scalar_type() == x.scalar_type(), "bn_nhwc: z must match input");
+  }
+  auto fo = x.options().dtype(at::kFloat);
+  auto save_mean = at::empty({c}, fo), save_invstd = at::empty({c}, fo), coef = at::empty({2, c}, fo);
+  auto inv_count = at::empty({1}, fo);
+  bn_nhwc_stats_merge(gathered.data_ptr<float>(), (int)gathered.size(0), c, fptr(w), fptr(b), (float)eps,
+                      (float)momentum, fptr_mut(running_mean), fptr_mut(running_var), save_mean.data_ptr<float>(),
+                      save_invstd.data_ptr<float>(), coef.data_ptr<float>(), inv_count.data_ptr<float>(),
+                      cur_stream());
+  at::Tensor mask;
+  if (want_mask) mask = at::empty({m * c / 8}, x.options().dtype(at::kByte));
+  auto y = at::empty_like(x);
+  bn_nhwc_apply(x.data_ptr(), dtype_code(x.scalar_type()), has(z) ? z->data_ptr() : nullptr, coef.data_ptr<float>(),
+                relu, y.data_ptr(), m, c, device_cus(x.get_device()), cur_stream(),
+                want_mask ? mask.data_ptr<uint8_t>() : nullptr);
+  return {y, save_mean, save_invstd, coef, mask, inv_count};
+}
+
+// backward, step 1: local [sum_dy | sum_dy_xmu] payload, local grad_w / grad_b and (when the
+// ReLU is fused) the masked gradient the apply pass reads
+std::vector<at::Tensor> bwd_group_local(at::Tensor dy_, at::Tensor x, OT z, OT w, at::Tensor save_mean,
+                                        at::Tensor save_invstd, at::Tensor coef_fwd, bool relu, OT dy2_, OT mask_) {
+  check2d(x, "input");
+  const c10::hip::HIPGuard g(x.get_device());
+  at::Tensor dy = dy_.contiguous();
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "bn_nhwc: grad must match input");
+  at::Tensor dy2;
+  if (has(dy2_)) {
+    dy2 = dy2_->contiguous();
+    TORCH_CHECK(dy2.sizes() == x.sizes() && dy2.scalar_type() == x.scalar_type(), "bn_nhwc: grad2 must match input");
+    if (!relu) {
+      dy = dy + dy2;
+      dy2 = at::Tensor();
+    }
+  }
+  const int64_t m = x.size(0);
+  const int c = (int)x.size(1);
+  const int cus = device_cus(x.get_device());
+  int64_t wsf = 0;
+  const int gy = bn_nhwc_plan(m, c, cus, &wsf);
+  auto fo = x.options().dtype(at::kFloat);
+  auto ws = at::empty({wsf}, fo);
+  auto gw = at::empty({c}, fo), gb = at::empty({c}, fo), payload = at::empty({2 * (int64_t)c}, fo);
+  const bool bits = has(mask_);
+  if (bits)
+    TORCH_CHECK(relu && mask_->scalar_type() == at::kByte && mask_->numel() * 8 == m * c && mask_->is_contiguous(),
+                "bn_nhwc: mask must be a contiguous uint8 [M*C/8] tensor of a relu forward");
+  // with a fused ReLU the masked gradient is always materialized here (it is grad_z of a
+  // residual layer and the apply pass's input), so the second half never needs z
+  at::Tensor dym;
+  if (relu) dym = at::empty_like(x);
+  bn_nhwc_bwd_reduce(dy.data_ptr(), x.data_ptr(), dtype_code(x.scalar_type()), has(z) ? z->data_ptr() : nullptr,
+                     coef_fwd.data_ptr<float>(), relu, save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
+                     fptr(w), gw.data_ptr<float>(), gb.data_ptr<float>(), nullptr,
+                     dym.defined() ? dym.data_ptr() : nullptr, m, c, ws.data_ptr<float>(), gy, cus, cur_stream(),
+                     dy2.defined() ? dy2.data_ptr() : nullptr, bits ? mask_->data_ptr<uint8_t>() : nullptr,
+                     payload.data_ptr<float>());
+  return {payload, gw, gb, dym.defined() ? dym : dy};
+}
+
+// backward, step 2: dx from the group's sums (`sums` [rows, 2C], summed in row order)
+at::Tensor bwd_group_finish(at::Tensor dy_masked, at::Tensor x, at::Tensor sums, at::Tensor inv_count, OT w,
+                            at::Tensor save_mean, at::Tensor save_invstd, at::Tensor coef_fwd) {
+  check2d(x, "input");
+  check2d(dy_masked, "grad");
+  const c10::hip::HIPGuard g(x.get_device());
+  const int64_t m = x.size(0);
+  const int c = (int)x.size(1);
+  TORCH_CHECK(sums.is_cuda() && sums.scalar_type() == at::kFloat && sums.is_contiguous() &&
+                  sums.numel() % (2 * (int64_t)c) == 0 && sums.numel() > 0,
+              "bn_nhwc: group sums must be a contiguous fp32 [rows, 2C] GPU tensor");
+  auto coef_bwd = at::empty({3, c}, x.options().dtype(at::kFloat));
+  bn_nhwc_bwd_coef_group(sums.data_ptr<float>(), (int)(sums.numel() / (2 * (int64_t)c)), c,
+                         inv_count.data_ptr<float>(), save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
+                         fptr(w), coef_bwd.data_ptr<float>(), cur_stream());
+  auto dx = at::empty_like(x);
+  bn_nhwc_bwd_apply(dy_masked.data_ptr(), true, x.data_ptr(), dtype_code(x.scalar_type()), nullptr,
+                    coef_fwd.data_ptr<float>(), false, coef_bwd.data_ptr<float>(), dx.data_ptr(), m, c,
+                    device_cus(x.get_device()), cur_stream());
+  return dx;
+}
+
 }  // namespace
 
 void bind_bn_nhwc(pybind11::module_& root) {
@@ -140,6 +255,12 @@ void bind_bn_nhwc(pybind11::module_& root) {
   m.def("bwd", &bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("z"), pybind11::arg("w"),
         pybind11::arg("save_mean"), pybind11::arg("save_invstd"), pybind11::arg("coef_fwd"), pybind11::arg("relu"),
         pybind11::arg("need_dz"), pybind11::arg("dy2") = c10::nullopt, pybind11::arg("mask") = c10::nullopt);
+  m.def("fwd_group_local", &fwd_group_local);
+  m.def("fwd_group_finish", &fwd_group_finish);
+  m.def("bwd_group_local", &bwd_group_local, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("z"),
+        pybind11::arg("w"), pybind11::arg("save_mean"), pybind11::arg("save_invstd"), pybind11::arg("coef_fwd"),
+        pybind11::arg("relu"), pybind11::arg("dy2") = c10::nullopt, pybind11::arg("mask") = c10::nullopt);
+  m.def("bwd_group_finish", &bwd_group_finish);
 }
 
 }  // namespace apex_amd

@@ -19,7 +19,7 @@ void* peer_open(const std::string& handle);
 void peer_close(void* p);
 int peer_max_group();
 void peer_allgather(const float* local, int n, int nmax, float* const* bufs, int me, int group, uint32_t epoch,
-                    float* out, int* err, hipStream_t s);
+                    float* out, int* err, double timeout_s, hipStream_t s);
 
 namespace {
 
@@ -32,7 +32,7 @@ void pm_close(int64_t p) { peer_close((void*)(uintptr_t)p); }
 
 // out[group][n] = every member's `local` [n] (fp32), exchanged through the members' buffers
 void pm_allgather(const at::Tensor& local, const std::vector<int64_t>& bufs, int64_t nmax, int64_t me,
-                  int64_t epoch, at::Tensor& out, at::Tensor& err) {
+                  int64_t epoch, at::Tensor& out, at::Tensor& err, double timeout_s) {
   TORCH_CHECK(local.is_cuda() && local.scalar_type() == at::kFloat && local.is_contiguous(), "peer: fp32 local");
   TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() &&
                   out.numel() == (int64_t)bufs.size() * local.numel(), "peer: out must be [group, n] fp32");
@@ -41,7 +41,7 @@ void pm_allgather(const at::Tensor& local, const std::vector<int64_t>& bufs, int
   std::vector<float*> ptrs;
   for (int64_t b : bufs) ptrs.push_back((float*)(uintptr_t)b);
   peer_allgather(local.data_ptr<float>(), (int)local.numel(), (int)nmax, ptrs.data(), (int)me, (int)bufs.size(),
-                 (uint32_t)epoch, out.data_ptr<float>(), err.data_ptr<int>(), cur_stream());
+                 (uint32_t)epoch, out.data_ptr<float>(), err.data_ptr<int>(), timeout_s, cur_stream());
 }
 
 // out = residual + dropout(x + bias) with a regenerable counter-hash mask (csrc/transformer/bias_dropout_add.hip)

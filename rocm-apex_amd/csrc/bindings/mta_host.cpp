@@ -1,5 +1,11 @@
 // Host side of the multi-tensor-apply engine: builds the device work table for a tensor
-// list-of-lists and caches it, keyed by (device, depth, chunk_size, addresses, sizes).
+// list-of-lists and caches it, keyed by (device, STREAM, depth, chunk_size, addresses, sizes).
+//
+// The table also holds the scratch of the single-pass reductions (per-chunk partials + the
+// last-block ticket).  Keying by the launching stream gives every stream its own scratch, so two
+// reductions over the same tensor list that are in flight on different streams (e.g. a norm on a
+// side stream beside one on the compute stream) never share a ticket; launches on one stream are
+// ordered, so they can share one.
 //
 // An optimizer steps the same parameter/state tensors every iteration, so after the first step
 // every multi-tensor launch finds its table resident on the device: no per-step H2D traffic and
@@ -51,6 +57,7 @@ MtaMeta mta_meta(const std::vector<std::vector<at::Tensor>>& lists, int chunk_si
   std::vector<uint64_t> key;
   key.reserve(4 + (size_t)nt * (depth + 1));
   key.push_back((uint64_t)dev.index());
+  key.push_back((uint64_t)(uintptr_t)cur_stream());
   key.push_back((uint64_t)depth);
   key.push_back((uint64_t)chunk_size);
   key.push_back((uint64_t)nt);

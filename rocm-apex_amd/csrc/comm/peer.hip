@@ -13,8 +13,15 @@
 //      buffer carry the epoch (system-scope acquire);
 //   3. read: copy the `group` payloads into the output [group][n].
 // Parity = epoch & 1 double-buffers the slots: a rank can only reach epoch e+2 after every member
-// published e+1, which each member does only after it finished reading epoch e.  A spin that runs
-// out (a member never arrived) sets *err and returns, so the kernel always terminates.
+// published e+1, which each member does only after it finished reading epoch e.
+//
+// Failure handling: the wait is bounded in WALL time (kTimeoutTicks of the 100 MHz real-time
+// counter, 30 s by default: far above any legitimate skew between ranks such as a first-step convolution
+// search or a rank-0 checkpoint, so the kernel always terminates even if a member died).  A wait
+// that runs out never hands back stale slots: the whole output is POISONED with NaN and *err is
+// incremented.  NaN statistics propagate into the loss and the gradients, so the dynamic loss
+// scaler skips that step instead of training on garbage, and PeerExchange polls *err without a
+// device sync and raises.
 #include "apex_amd/device.h"
 #include "apex_amd/dispatch.h"
 
@@ -27,7 +34,7 @@ namespace peer {
 
 constexpr int kHeaderFloats = 4;
 constexpr int kMaxGroup = 8;
-constexpr uint32_t kSpinLimit = 1u << 22;  // x ~64-cycle s_sleep => O(100 ms) before giving up
+constexpr uint64_t kTicksPerSecond = 100000000ull;  // the 100 MHz real-time counter (wall_clock64)
 
 struct Ptrs {
   float* buf[kMaxGroup];
@@ -35,7 +42,7 @@ struct Ptrs {
 
 __global__ void __launch_bounds__(256) allgather_kernel(const float* __restrict__ local, int n, int nmax, Ptrs bufs,
                                                         int me, int group, uint32_t epoch, float* __restrict__ out,
-                                                        int* __restrict__ err) {
+                                                        int* __restrict__ err, uint64_t timeout_ticks) {
   const int tid = threadIdx.x;
   const int slot = nmax + kHeaderFloats;
   const int parity = (int)(epoch & 1u);
@@ -56,19 +63,21 @@ __global__ void __launch_bounds__(256) allgather_kernel(const float* __restrict_
   __syncthreads();
   if (tid < group) {
     uint32_t* flag = reinterpret_cast<uint32_t*>(bufs.buf[me] + (int64_t)(parity * group + tid) * slot);
-    uint32_t it = 0;
-    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
-      if (++it >= kSpinLimit) {
+    const uint64_t t0 = wall_clock64();
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+      if (wall_clock64() - t0 > timeout_ticks) {
         timed_out = 1;
         break;
       }
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(8);
     }
   }
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: no stale L1 / L2 lines of the slots
   if (timed_out) {
-    if (tid == 0) atomicExch(err, 1);
+    const float qnan = __builtin_nanf("");
+    for (int i = tid; i < group * n; i += 256) out[i] = qnan;
+    if (tid == 0) atomicAdd(err, 1);
     return;
   }
   // 3. read
@@ -111,12 +120,15 @@ void peer_close(void* p) { (void)hipIpcCloseMemHandle(p); }
 int peer_max_group() { return peer::kMaxGroup; }
 
 void peer_allgather(const float* local, int n, int nmax, float* const* bufs, int me, int group, uint32_t epoch,
-                    float* out, int* err, hipStream_t s) {
+                    float* out, int* err, double timeout_s, hipStream_t s) {
+  if (!(timeout_s > 0.0) || timeout_s > 600.0) throw std::runtime_error("peer_allgather: timeout must be in (0, 600] s");
+  const uint64_t ticks = (uint64_t)(timeout_s * (double)peer::kTicksPerSecond);
   if (group < 1 || group > peer::kMaxGroup || me < 0 || me >= group || n > nmax)
     throw std::runtime_error("peer_allgather: bad group / size");
   peer::Ptrs p{};
   for (int j = 0; j < group; ++j) p.buf[j] = bufs[j];
-  hipLaunchKernelGGL(peer::allgather_kernel, dim3(1), dim3(256), 0, s, local, n, nmax, p, me, group, epoch, out, err);
+  hipLaunchKernelGGL(peer::allgather_kernel, dim3(1), dim3(256), 0, s, local, n, nmax, p, me, group, epoch, out, err,
+                     ticks);
   check_launch("peer_allgather");
 }
 

@@ -174,6 +174,62 @@ __global__ void __launch_bounds__(256) stats_finalize(const float* __restrict__ 
   if (rvar) rvar[ch] = (1.f - momentum) * rvar[ch] + momentum * (n > 1.f ? var_b * n / (n - 1.f) : var_b);
 }
 
+// ------------------------------------------------------------------------------------------
+// Group (cross-rank) statistics, bn_group > 1.  Each rank reduces its own partials to a payload
+// [mean(C) | M2(C) | count] (M2 = sum of squared deviations from the local mean), the payloads
+// of the group are exchanged (xGMI peer memory or RCCL all-gather), and every rank merges the
+// SAME gathered block in the same fixed order (Chan et al. pairwise update), so all members end
+// with bit-identical mean / inv_std / running statistics.
+template <typename T>
+__global__ void __launch_bounds__(256) stats_local(const float* __restrict__ part, int gy, int c, float n,
+                                                   const T* __restrict__ x, float* __restrict__ payload) {
+  __shared__ float red[2][16][17];
+  const int g = threadIdx.x >> 4;
+  const int ch = blockIdx.x * 16 + (threadIdx.x & 15);
+  float s1, s2;
+  sum_partials(part, gy, c, ch, g, red, s1, s2);
+  if (g != 0 || ch >= c) return;
+  const float shift = to_f(x[ch]);
+  const float dm = s1 / n;
+  payload[ch] = shift + dm;
+  payload[c + ch] = fmaxf(s2 - s1 * dm, 0.f);
+  if (ch == 0) payload[2 * c] = n;
+}
+
+__global__ void __launch_bounds__(256) stats_merge(const float* __restrict__ gathered, int world, int c,
+                                                   const float* __restrict__ w, const float* __restrict__ b,
+                                                   float eps, float momentum, float* __restrict__ rmean,
+                                                   float* __restrict__ rvar, float* __restrict__ save_mean,
+                                                   float* __restrict__ save_invstd, float* __restrict__ coef,
+                                                   float* __restrict__ inv_count) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= c) return;
+  const int64_t row = 2 * (int64_t)c + 1;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  for (int r = 0; r < world; ++r) {
+    const float* p = gathered + r * row;
+    const double nr = (double)p[2 * c];
+    if (nr <= 0.0) continue;
+    const double mr = (double)p[ch];
+    const double nt = n + nr;
+    const double d = mr - mean;
+    mean += d * (nr / nt);
+    m2 += (double)p[c + ch] + d * d * (n * nr / nt);
+    n = nt;
+  }
+  const float var_b = (float)(n > 0.0 ? m2 / n : 0.0);
+  const float mm = (float)mean;
+  const float istd = rsqrtf(var_b + eps);
+  save_mean[ch] = mm;
+  save_invstd[ch] = istd;
+  const float sc = istd * (w ? w[ch] : 1.f);
+  coef[ch] = sc;
+  coef[c + ch] = (b ? b[ch] : 0.f) - mm * sc;
+  if (rmean) rmean[ch] = (1.f - momentum) * rmean[ch] + momentum * mm;
+  if (rvar) rvar[ch] = (1.f - momentum) * rvar[ch] + momentum * (float)(n > 1.0 ? m2 / (n - 1.0) : var_b);
+  if (ch == 0) inv_count[0] = (float)(n > 0.0 ? 1.0 / n : 0.0);
+}
+
 __global__ void coef_from_stats(const float* __restrict__ mean, const float* __restrict__ v, int is_var,
                                 const float* __restrict__ w, const float* __restrict__ b, float eps, int c,
                                 float* __restrict__ coef) {
@@ -338,6 +394,46 @@ __global__ void __launch_bounds__(256) bwd_finalize(const float* __restrict__ pa
   coef[2 * c + ch] = -A * (sdy * inv_n) - B * mean[ch];
 }
 
+// group backward, step 1: this rank's sums as the exchange payload [sum_dy(C) | sum_dy_xmu(C)]
+// plus the LOCAL weight / bias gradients (data-parallel averages those like any other grad)
+__global__ void __launch_bounds__(256) bwd_local(const float* __restrict__ part, int gy, int c,
+                                                 const float* __restrict__ istd, float* __restrict__ gw,
+                                                 float* __restrict__ gb, float* __restrict__ payload) {
+  __shared__ float red[2][16][17];
+  const int g = threadIdx.x >> 4;
+  const int ch = blockIdx.x * 16 + (threadIdx.x & 15);
+  float sdy, sdyx;
+  sum_partials(part, gy, c, ch, g, red, sdy, sdyx);
+  if (g != 0 || ch >= c) return;
+  if (gw) gw[ch] = sdyx * istd[ch];
+  if (gb) gb[ch] = sdy;
+  payload[ch] = sdy;
+  payload[c + ch] = sdyx;
+}
+
+// group backward, step 2: dx coefficients from the group's sums; `rows` payload rows (one per
+// rank after a peer all-gather, summed here in rank order; 1 after an RCCL all-reduce)
+__global__ void __launch_bounds__(256) bwd_coef_group(const float* __restrict__ sums, int rows, int c,
+                                                      const float* __restrict__ inv_count,
+                                                      const float* __restrict__ mean,
+                                                      const float* __restrict__ istd, const float* __restrict__ w,
+                                                      float* __restrict__ coef) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= c) return;
+  float sdy = 0.f, sdyx = 0.f;
+  for (int r = 0; r < rows; ++r) {
+    sdy += sums[(int64_t)r * 2 * c + ch];
+    sdyx += sums[(int64_t)r * 2 * c + c + ch];
+  }
+  const float inv_n = inv_count[0];
+  const float is = istd[ch];
+  const float A = is * (w ? w[ch] : 1.f);
+  const float B = -A * is * is * (sdyx * inv_n);
+  coef[ch] = A;
+  coef[c + ch] = B;
+  coef[2 * c + ch] = -A * (sdy * inv_n) - B * mean[ch];
+}
+
 template <typename T, bool HAS_Z, bool MASK>
 __global__ void __launch_bounds__(256) bwd_apply(const T* __restrict__ dy, const T* __restrict__ x,
                                                  const T* __restrict__ z, const float* __restrict__ cf,
@@ -407,6 +503,38 @@ void bn_nhwc_stats(const void* x, int x_t, int64_t m, int c, const float* w, con
   check_launch("bn_nhwc_stats");
 }
 
+void bn_nhwc_stats_local(const void* x, int x_t, int64_t m, int c, float* payload, float* ws, int gy, int cus,
+                         hipStream_t s) {
+  bnh::check_shape(m, c);
+  bnh::Geo g = bnh::geo(m, c, cus);
+  g.gy = gy;
+  const size_t lds = (size_t)2 * g.ty * g.tx * 8 * sizeof(float);
+  dispatch_float(x_t, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    hipLaunchKernelGGL((bnh::stats_partial<T>), dim3(g.gx, g.gy), dim3(g.tx, g.ty), lds, s, (const T*)x, m, c, ws);
+    hipLaunchKernelGGL((bnh::stats_local<T>), dim3((c + 15) / 16), dim3(256), 0, s, ws, g.gy, c, (float)m, (const T*)x,
+                       payload);
+  }, "bn_nhwc stats local");
+  check_launch("bn_nhwc_stats_local");
+}
+
+void bn_nhwc_stats_merge(const float* gathered, int world, int c, const float* w, const float* b, float eps,
+                         float momentum, float* running_mean, float* running_var, float* save_mean, float* save_invstd,
+                         float* coef_fwd, float* inv_count, hipStream_t s) {
+  if (world < 1 || c <= 0) throw std::runtime_error("bn_nhwc stats merge: bad group / channels");
+  hipLaunchKernelGGL(bnh::stats_merge, dim3((c + 255) / 256), dim3(256), 0, s, gathered, world, c, w, b, eps, momentum,
+                     running_mean, running_var, save_mean, save_invstd, coef_fwd, inv_count);
+  check_launch("bn_nhwc_stats_merge");
+}
+
+void bn_nhwc_bwd_coef_group(const float* sums, int rows, int c, const float* inv_count, const float* save_mean,
+                            const float* save_invstd, const float* w, float* coef_bwd, hipStream_t s) {
+  if (rows < 1 || c <= 0) throw std::runtime_error("bn_nhwc bwd coef: bad rows / channels");
+  hipLaunchKernelGGL(bnh::bwd_coef_group, dim3((c + 255) / 256), dim3(256), 0, s, sums, rows, c, inv_count, save_mean,
+                     save_invstd, w, coef_bwd);
+  check_launch("bn_nhwc_bwd_coef_group");
+}
+
 void bn_nhwc_coef_from_stats(const float* mean, const float* v, bool is_var, const float* w, const float* b, float eps,
                              int c, float* coef_fwd, hipStream_t s) {
   hipLaunchKernelGGL(bnh::coef_from_stats, dim3((c + 255) / 256), dim3(256), 0, s, mean, v, is_var ? 1 : 0, w, b, eps,
@@ -447,7 +575,7 @@ void bn_nhwc_apply(const void* x, int x_t, const void* z, const float* coef_fwd,
 void bn_nhwc_bwd_reduce(const void* dy, const void* x, int x_t, const void* z, const float* coef_fwd, bool relu,
                         const float* save_mean, const float* save_invstd, const float* w, float* grad_w, float* grad_b,
                         float* coef_bwd, void* dy_masked_out, int64_t m, int c, float* ws, int gy, int cus,
-                        hipStream_t s, const void* dy2, const uint8_t* mask_in) {
+                        hipStream_t s, const void* dy2, const uint8_t* mask_in, float* group_payload) {
   if (mask_in && !(relu && dy_masked_out))
     throw std::runtime_error("bn_nhwc bwd: the ReLU bit mask path writes the masked gradient");
   if (dy2 && !(relu && dy_masked_out))
@@ -484,8 +612,12 @@ void bn_nhwc_bwd_reduce(const void* dy, const void* x, int x_t, const void* z, c
       else go(F{}, Tr{}, Tr{}, F{});
     } else go(F{}, Tr{}, F{}, F{});
   }, "bn_nhwc bwd reduce");
-  hipLaunchKernelGGL(bnh::bwd_finalize, dim3((c + 15) / 16), dim3(256), 0, s, ws, g.gy, c, 1.f / (float)m, save_mean,
-                     save_invstd, w, grad_w, grad_b, coef_bwd);
+  if (group_payload)  // bn_group > 1: local sums for the exchange, coefficients after it
+    hipLaunchKernelGGL(bnh::bwd_local, dim3((c + 15) / 16), dim3(256), 0, s, ws, g.gy, c, save_invstd, grad_w, grad_b,
+                       group_payload);
+  else
+    hipLaunchKernelGGL(bnh::bwd_finalize, dim3((c + 15) / 16), dim3(256), 0, s, ws, g.gy, c, 1.f / (float)m, save_mean,
+                       save_invstd, w, grad_w, grad_b, coef_bwd);
   check_launch("bn_nhwc_bwd_reduce");
 }
 

@@ -42,7 +42,23 @@ void bn_nhwc_apply(const void* x, int x_t, const void* z, const float* coef_fwd,
 void bn_nhwc_bwd_reduce(const void* dy, const void* x, int x_t, const void* z, const float* coef_fwd, bool relu,
                         const float* save_mean, const float* save_invstd, const float* w, float* grad_w,
                         float* grad_b, float* coef_bwd, void* dy_masked_out, int64_t m, int c, float* ws, int gy,
-                        int cus, hipStream_t s, const void* dy2 = nullptr, const uint8_t* mask_in = nullptr);
+                        int cus, hipStream_t s, const void* dy2 = nullptr, const uint8_t* mask_in = nullptr,
+                        float* group_payload = nullptr);
+
+// ---- bn_group > 1 (statistics shared by a group of ranks) ----
+// forward, step 1: local payload [mean(C) | M2(C) | count] (fp32, 2C+1) for the group exchange
+void bn_nhwc_stats_local(const void* x, int x_t, int64_t m, int c, float* payload, float* ws, int gy, int cus,
+                         hipStream_t s);
+// forward, step 2: merge the gathered [world][2C+1] payloads (fixed rank order: identical on every
+// member) into save_mean / save_invstd / coef_fwd / running stats and 1/N_group (inv_count[1])
+void bn_nhwc_stats_merge(const float* gathered, int world, int c, const float* w, const float* b, float eps,
+                         float momentum, float* running_mean, float* running_var, float* save_mean, float* save_invstd,
+                         float* coef_fwd, float* inv_count, hipStream_t s);
+// backward: bn_nhwc_bwd_reduce(..., group_payload) writes [sum_dy | sum_dy_xmu] (2C) and the LOCAL
+// grad_w / grad_b instead of coef_bwd; after the exchange, coef_bwd from the group's sums (`rows`
+// payload rows summed in order: world after a peer all-gather, 1 after an all-reduce)
+void bn_nhwc_bwd_coef_group(const float* sums, int rows, int c, const float* inv_count, const float* save_mean,
+                            const float* save_invstd, const float* w, float* coef_bwd, hipStream_t s);
 
 // dx = A * dy' + B * x + K   (dy' masked in registers when relu && !dy_is_masked)
 void bn_nhwc_bwd_apply(const void* dy, bool dy_is_masked, const void* x, int x_t, const void* z,

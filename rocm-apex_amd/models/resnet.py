@@ -12,6 +12,10 @@ apex/contrib/groupbn, the NHWC BN with fused add+ReLU used for ResNet-50).  Para
 and state_dict keys are identical to the torch.nn.BatchNorm2d model; the math is the same
 training-mode batch norm, computed by the gfx950 kernels in fewer HBM passes.
 
+``bn_group=N`` (fused only) makes every batch norm a synchronized one over groups of N adjacent
+ranks (the reference's groupbn ``bn_group``; ``bn_group=world`` is SyncBatchNorm over the whole
+job): same fused kernels, statistics exchanged over xGMI peer memory (or RCCL).
+
 In the fused model every block but the last hands its output on as a ``(main, shortcut)`` pair of
 aliases (``BatchNorm2d_NHWC(..., fork=True)``): the next block's conv1 reads one and its shortcut
 the other, so the two gradients of the block output reach the producing batch norm separately
@@ -38,25 +42,25 @@ def conv1x1(cin, cout, stride=1, native=False):
     return nn.Conv2d(cin, cout, kernel_size=1, stride=stride, bias=False)
 
 
-def _fused_bn(planes, relu):
+def _fused_bn(planes, relu, bn_group=1):
     from ..contrib.groupbn import BatchNorm2d_NHWC
 
-    return BatchNorm2d_NHWC(planes, fuse_relu=relu, torch_channels_last=True)
+    return BatchNorm2d_NHWC(planes, fuse_relu=relu, torch_channels_last=True, bn_group=bn_group)
 
 
 class BasicBlock(nn.Module):
     expansion = 1
 
     def __init__(self, inplanes, planes, stride=1, downsample=None, groups=1, base_width=64, dilation=1,
-                 norm_layer=None, fused_bn=False):
+                 norm_layer=None, fused_bn=False, bn_group=1):
         super().__init__()
         norm_layer = norm_layer or nn.BatchNorm2d
         self.fused_bn = fused_bn
         self.conv1 = conv3x3(inplanes, planes, stride)
-        self.bn1 = _fused_bn(planes, True) if fused_bn else norm_layer(planes)
+        self.bn1 = _fused_bn(planes, True, bn_group) if fused_bn else norm_layer(planes)
         self.relu = nn.ReLU(inplace=True)
         self.conv2 = conv3x3(planes, planes)
-        self.bn2 = _fused_bn(planes, True) if fused_bn else norm_layer(planes)
+        self.bn2 = _fused_bn(planes, True, bn_group) if fused_bn else norm_layer(planes)
         self.downsample = downsample
         self.stride = stride
         self.fork_out = False
@@ -77,12 +81,12 @@ class Bottleneck(nn.Module):
     expansion = 4
 
     def __init__(self, inplanes, planes, stride=1, downsample=None, groups=1, base_width=64, dilation=1,
-                 norm_layer=None, fused_bn=False):
+                 norm_layer=None, fused_bn=False, bn_group=1):
         super().__init__()
         norm_layer = norm_layer or nn.BatchNorm2d
         self.fused_bn = fused_bn
         width = int(planes * (base_width / 64.0)) * groups
-        nl = (lambda c, relu: _fused_bn(c, relu)) if fused_bn else (lambda c, relu: norm_layer(c))  # noqa: E731
+        nl = (lambda c, relu: _fused_bn(c, relu, bn_group)) if fused_bn else (lambda c, relu: norm_layer(c))  # noqa: E731
         self.conv1 = conv1x1(inplanes, width, native=fused_bn)
         self.bn1 = nl(width, True)
         self.conv2 = conv3x3(width, width, stride, groups, dilation)
@@ -110,10 +114,11 @@ class Bottleneck(nn.Module):
 
 class ResNet(nn.Module):
     def __init__(self, block, layers, num_classes=1000, zero_init_residual=False, groups=1, width_per_group=64,
-                 norm_layer=None, fused_bn=False):
+                 norm_layer=None, fused_bn=False, bn_group=1):
         super().__init__()
         self._norm_layer = norm_layer or nn.BatchNorm2d
         self.fused_bn = fused_bn
+        self.bn_group = bn_group
         self.inplanes = 64
         self.dilation = 1
         self.groups = groups
@@ -121,7 +126,7 @@ class ResNet(nn.Module):
         # fused path: stem input channels padded 3 -> 4 on the GPU (MIOpen's NHWC kernels, ops/conv.py)
         stem = ChannelPadConv2d if fused_bn else nn.Conv2d
         self.conv1 = stem(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
-        self.bn1 = _fused_bn(self.inplanes, True) if fused_bn else self._norm_layer(self.inplanes)
+        self.bn1 = _fused_bn(self.inplanes, True, bn_group) if fused_bn else self._norm_layer(self.inplanes)
         self.relu = nn.ReLU(inplace=True)
         # fused path (channels_last): gfx950 NHWC max pool with 1-byte indices
         self.maxpool = MaxPool2dNHWC(kernel_size=3, stride=2, padding=1) if fused_bn else \
@@ -154,14 +159,16 @@ class ResNet(nn.Module):
         norm_layer = self._norm_layer
         downsample = None
         if stride != 1 or self.inplanes != planes * block.expansion:
-            bn = _fused_bn(planes * block.expansion, False) if self.fused_bn else norm_layer(planes * block.expansion)
+            bn = (_fused_bn(planes * block.expansion, False, self.bn_group) if self.fused_bn
+                  else norm_layer(planes * block.expansion))
             downsample = nn.Sequential(conv1x1(self.inplanes, planes * block.expansion, stride), bn)
         layers = [block(self.inplanes, planes, stride, downsample, self.groups, self.base_width, self.dilation,
-                        norm_layer, fused_bn=self.fused_bn)]
+                        norm_layer, fused_bn=self.fused_bn, bn_group=self.bn_group)]
         self.inplanes = planes * block.expansion
         for _ in range(1, blocks):
             layers.append(block(self.inplanes, planes, groups=self.groups, base_width=self.base_width,
-                                dilation=self.dilation, norm_layer=norm_layer, fused_bn=self.fused_bn))
+                                dilation=self.dilation, norm_layer=norm_layer, fused_bn=self.fused_bn,
+                                bn_group=self.bn_group))
         return nn.Sequential(*layers)
 
     def forward(self, x):

@@ -77,8 +77,11 @@ class FusedAdam(AmpFusedMixin, torch.optim.Optimizer):
                 step_t = device_step(group, st, device)
             else:
                 step_t = group.get("_step_t")
-                if step_t is None:
-                    step_t = group["_step_t"] = torch.zeros(1, dtype=torch.float32, device=device)
+                if step_t is None or step_t.device != device:
+                    # seeded from the host count (a resumed optimizer continues its bias
+                    # correction); group['step'] was already bumped for this call
+                    step_t = group["_step_t"] = torch.full((1,), float(group["step"] - 1), dtype=torch.float32,
+                                                           device=device)
                 step_t.add_(1.0)
             lr_t = lr_tensor(group, device)
             key = lambda it: (it[0].dtype, it[1].dtype, None if it[2] is None else it[2].dtype)  # noqa: E731

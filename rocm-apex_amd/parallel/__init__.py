@@ -10,9 +10,21 @@ from .LARC import LARC  # noqa: E402,F401
 
 
 def convert_syncbn_model(module, process_group=None, channel_last=False):
-    """Recursively replace every ``_BatchNorm`` with :class:`SyncBatchNorm` (state copied)."""
+    """Recursively replace every ``_BatchNorm`` with :class:`SyncBatchNorm` (state copied).
+
+    ``channel_last`` selects the explicit-NHWC reading for 4-D inputs whose last dim is the
+    channel dim; NCHW-shaped tensors in torch ``channels_last`` memory are recognised either way.
+    The fused NHWC batch norm (``apex.contrib.groupbn.BatchNorm2d_NHWC``, which carries fused
+    ReLU / residual inputs) is kept and synchronized in place over ``process_group`` instead."""
     mod = module
     if isinstance(module, torch.nn.modules.instancenorm._InstanceNorm):
+        return module
+    from ..contrib.groupbn.batch_norm import BatchNorm2d_NHWC
+
+    if isinstance(module, BatchNorm2d_NHWC):
+        module.synchronize_over(process_group)
+        for name, child in module.named_children():
+            module.add_module(name, convert_syncbn_model(child, process_group, channel_last))
         return module
     if isinstance(module, torch.nn.modules.batchnorm._BatchNorm):
         mod = SyncBatchNorm(module.num_features, module.eps, module.momentum, module.affine,

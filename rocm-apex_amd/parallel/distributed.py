@@ -16,6 +16,11 @@ MI355X design (not a port of the reference's flatten / side-stream / unflatten p
   matching collectives); out-of-order readiness is held back until predecessors fire.
 * **Averaging in the collective** with ``ReduceOp.AVG`` (ncclAvg) when no predivide factor is
   requested; otherwise pre/post scaling as in the reference.
+* **Zero-copy under amp.**  A DDP-owned parameter carries a weak back-reference to its DDP; amp's
+  ``zero_grad`` / post-``step`` reset call :func:`zero_bucketed_grads`, which zeroes each bucket
+  with ONE memset and re-attaches every gradient as its bucket view (instead of setting grads to
+  None), so the next backward accumulates straight into the buckets: no per-parameter copy and no
+  allocation per step.  Buckets already known to be zero are not cleared twice.
 * Bucket membership defaults to reverse registration order (a good proxy for backward order,
   identical on every rank with no communication); after the first iteration it is re-derived
   from rank 0's observed gradient-arrival order, broadcast to all ranks (reference behaviour,
@@ -23,6 +28,7 @@ MI355X design (not a port of the reference's flatten / side-stream / unflatten p
 """
 import os
 import warnings
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -105,9 +111,40 @@ class Reducer(object):
             flat_dist_call(self.grads, dist.all_reduce)
 
 
+def _owner(param):
+    ref = getattr(param, "_apex_ddp_owner", None)
+    return ref() if ref is not None else None
+
+
+def zero_bucketed_grads(params):
+    """Zero the gradients of the DDP-owned ``params`` in place (one memset per bucket, views
+    re-attached); returns the set of ``id(param)`` handled — the caller resets the others."""
+    done, owners = set(), {}
+    for p in params:
+        d = _owner(p)
+        if d is not None:
+            owners[id(d)] = d
+            done.add(id(p))
+    for d in owners.values():
+        d.zero_grad_buckets()
+    return done
+
+
+def zeroed_bucket_params(params):
+    """``id(param)`` of the DDP-owned ``params`` whose gradient is a bucket view known to be zero."""
+    out = set()
+    for p in params:
+        d = _owner(p)
+        if d is not None and p.grad is not None:
+            b, i = d._slot[id(p)]
+            if b.zeroed and p.grad.data_ptr() == b.buffer.data_ptr() + b.offsets[i] * b.buffer.element_size():
+                out.add(id(p))
+    return out
+
+
 class _Bucket(object):
     __slots__ = ("index", "params", "offsets", "numel", "dtype", "buffer", "fp32_buffer", "ready", "fired",
-                 "work", "group")
+                 "work", "group", "zeroed")
 
     def __init__(self, index, params, dtype, device, group, fp32_copy):
         self.index = index
@@ -126,6 +163,7 @@ class _Bucket(object):
         self.fired = False
         self.work = None
         self.group = group
+        self.zeroed = True
 
     def view_for(self, i):
         p = self.params[i]
@@ -199,8 +237,12 @@ class DistributedDataParallel(Module):
         self._hooks = []
         self._callback_queued = False
         self._sync_enabled = True
+        self.grad_copies = 0  # grads that arrived outside their bucket and were copied in
         self._build_buckets(list(reversed(range(len(self._params)))))
         self._create_hooks()
+        me = weakref.ref(self)
+        for p in self._params:
+            p._apex_ddp_owner = me
         flat_dist_call([p.data for p in module.parameters()], dist.broadcast, (0,))
 
     # ------------------------------------------------------------------------------ buckets
@@ -245,6 +287,7 @@ class DistributedDataParallel(Module):
                 v = b.view_for(i)
                 v.copy_(p.grad)
                 p.grad = v
+                b.zeroed = False
 
     # ------------------------------------------------------------------------------ hooks
     def _create_hooks(self):
@@ -263,11 +306,14 @@ class DistributedDataParallel(Module):
             if self._iteration == 0 and self.rebucket_by_arrival:
                 self._arrival.append(pid)
             b, i = self._slot[pid]
-            v = b.view_for(i)
+            b.zeroed = False
             g = param.grad
-            if g.data_ptr() != v.data_ptr():
+            if g.data_ptr() != b.buffer.data_ptr() + b.offsets[i] * b.buffer.element_size():
+                # a freshly allocated grad (first iteration, or grads reset to None): one copy
+                v = b.view_for(i)
                 v.copy_(g)
                 param.grad = v
+                self.grad_copies += 1
             b.ready += 1
             if self.delay_allreduce or (self._iteration == 0 and self.rebucket_by_arrival):
                 return
@@ -326,6 +372,7 @@ class DistributedDataParallel(Module):
                         if p.grad is None:
                             v.zero_()
                             p.grad = v
+                            b.zeroed = False
                         elif p.grad.data_ptr() != v.data_ptr():
                             v.copy_(p.grad)
                             p.grad = v
@@ -343,6 +390,18 @@ class DistributedDataParallel(Module):
             self._iteration += 1
 
     # ------------------------------------------------------------------------------ API
+    def zero_grad_buckets(self):
+        """Zero every bucket (one memset each, skipped when already zero) and attach each
+        parameter's gradient as its bucket view, so backward accumulates in place."""
+        for b in self._buckets:
+            if not b.zeroed:
+                b.buffer.zero_()
+                b.zeroed = True
+            for i, p in enumerate(b.params):
+                g = p.grad
+                if g is None or g.data_ptr() != b.buffer.data_ptr() + b.offsets[i] * b.buffer.element_size():
+                    p.grad = b.view_for(i)
+
     def forward(self, *inputs, **kwargs):
         if self.prof:
             torch.cuda.nvtx.range_push("forward pass DDP logic")

@@ -131,10 +131,25 @@ class SyncBatchNorm(_BatchNorm):
         if input.dim() < 2:
             raise ValueError("expected at least 2D input (got {}D input)".format(input.dim()))
 
+    def _torch_channels_last(self, input):
+        """True for an NCHW-shaped tensor in torch ``channels_last`` memory (what a channels_last
+        convolution produces).  With ``channel_last=True`` the module also accepts an explicit
+        NHWC tensor ([N, H, W, C], contiguous); the two are told apart by where ``num_features``
+        sits and by the strides, so ``convert_syncbn_model(model, channel_last=True)`` on a
+        channels_last model works."""
+        if input.dim() != 4 or input.size(1) != self.num_features:
+            return False
+        if not input.is_contiguous(memory_format=torch.channels_last):
+            return False
+        if not input.is_contiguous():
+            return True
+        # both layouts are dense (e.g. H = W = 1): only an explicit-NHWC request whose last dim
+        # really is the channel dim keeps the NHWC reading
+        return not (self.channel_last and input.size(-1) == self.num_features)
+
     def forward(self, input, z=None):
         self._check_input_dim(input)
-        if (not self.channel_last and input.dim() == 4 and not input.is_contiguous()
-                and input.is_contiguous(memory_format=torch.channels_last)):
+        if self._torch_channels_last(input):
             # torch channels_last memory: run the c_last kernels on a zero-copy NHWC view and
             # hand back an NCHW-shaped, channels_last-strided result
             zv = z.permute(0, 2, 3, 1) if z is not None else None

@@ -166,3 +166,171 @@ def _amp_master_worker(rank, world):
 
 def test_amp_o2_master_params_equal_across_ranks_gloo():
     run_multiprocess(_amp_master_worker, 2, ())
+
+
+# ------------------------------------------------------------------ SyncBN on a channels_last ResNet
+# (round-1 bug: convert_syncbn_model(..., channel_last=True) on channels_last NCHW tensors read W as
+# the channel dim; reference usage examples/imagenet/main_amp.py:118 passes channel_last this way)
+def _syncbn_resnet_worker(rank, world, channel_last):
+    import apex
+    from apex.models import resnet18
+
+    torch.manual_seed(0)
+    base = resnet18(num_classes=10)
+    ref = resnet18(num_classes=10)
+    ref.load_state_dict(base.state_dict())
+    model = apex.parallel.convert_syncbn_model(base, channel_last=channel_last).to(memory_format=torch.channels_last)
+    full = torch.randn(4, 3, 32, 32, generator=torch.Generator().manual_seed(3))
+    x = full[rank * 2:(rank + 1) * 2].contiguous(memory_format=torch.channels_last)
+    out = model(x)
+    out.sum().backward()
+    ro = ref(full)
+    ro.sum().backward()
+    torch.testing.assert_close(out, ro[rank * 2:(rank + 1) * 2], rtol=2e-3, atol=2e-3)
+    g = model.conv1.weight.grad.clone()
+    dist.all_reduce(g)
+    # fp32 sums over a different reduction order: compare relative to the gradient's scale
+    scale = ref.conv1.weight.grad.abs().max().item()
+    torch.testing.assert_close(g, ref.conv1.weight.grad, rtol=1e-2, atol=1e-2 * scale)
+    for m, r in zip(model.modules(), ref.modules()):
+        if isinstance(m, apex.parallel.SyncBatchNorm):
+            torch.testing.assert_close(m.running_mean, r.running_mean, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("channel_last", [True, False])
+def test_convert_syncbn_channels_last_resnet_fwd_bwd_gloo(channel_last):
+    run_multiprocess(_syncbn_resnet_worker, 2, (channel_last,))
+
+
+def _fused_bn_group_worker(rank, world):
+    """The fused-BN ResNet with bn_group = world (bench.py --sync-bn): on CPU the group batch
+    norm takes the SyncBatchNorm primitives; the result must equal the single-process model on
+    the concatenated batch."""
+    import apex
+    from apex.models import resnet18
+
+    torch.manual_seed(0)
+    model = resnet18(num_classes=10, fused_bn=True, bn_group=world)
+    ref = resnet18(num_classes=10)
+    ref.load_state_dict(model.state_dict())
+    full = torch.randn(4, 3, 32, 32, generator=torch.Generator().manual_seed(5))
+    x = full[rank * 2:(rank + 1) * 2].contiguous(memory_format=torch.channels_last)
+    model = model.to(memory_format=torch.channels_last)
+    out = model(x)
+    out.sum().backward()
+    ro = ref(full)
+    ro.sum().backward()
+    torch.testing.assert_close(out, ro[rank * 2:(rank + 1) * 2], rtol=2e-3, atol=2e-3)
+    g = model.conv1.weight.grad.clone()
+    dist.all_reduce(g)
+    scale = ref.conv1.weight.grad.abs().max().item()
+    torch.testing.assert_close(g, ref.conv1.weight.grad, rtol=1e-2, atol=1e-2 * scale)
+    # convert_syncbn_model keeps the fused modules (fused ReLU / residual inputs) and syncs them
+    m2 = apex.parallel.convert_syncbn_model(resnet18(fused_bn=True))
+    from apex.contrib.groupbn import BatchNorm2d_NHWC
+
+    bns = [m for m in m2.modules() if isinstance(m, BatchNorm2d_NHWC)]
+    assert bns and all(b.bn_group == world for b in bns)
+    assert not any(isinstance(m, apex.parallel.SyncBatchNorm) for m in m2.modules())
+
+
+def test_fused_resnet_bn_group_world_gloo():
+    run_multiprocess(_fused_bn_group_worker, 2, ())
+
+
+# ------------------------------------------------------------------ zero-copy DDP under fused amp
+def _ddp_zero_copy_worker(rank, world):
+    import os
+
+    os.environ["APEX_AMD_AMP_SYNC_FREE"] = "force"
+    from apex import amp
+    from apex.amp._amp_state import _amp_state
+    from apex.optimizers import FusedAdam
+    from apex.parallel import DistributedDataParallel as DDP
+
+    _amp_state.sync_free_force = True
+    torch.manual_seed(rank)
+    model = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 4))
+    opt = FusedAdam(model.parameters(), lr=1e-2, materialize_master_grads=False)
+    model, opt = amp.initialize(model, opt, opt_level="O2", cast_model_type=torch.bfloat16, verbosity=0)
+    assert _amp_state.sync_free, "fused (sync-free) amp path not active"
+    ddp = DDP(model, message_size=1)  # one bucket per parameter
+    params = list(model.parameters())
+    copies = {"n": 0}
+    orig_copy = torch.Tensor.copy_
+
+    for it in range(5):
+        x = torch.randn(8, 16, generator=torch.Generator().manual_seed(100 * rank + it))
+        loss = ddp(x).float().pow(2).mean()
+        opt.zero_grad()
+        if it >= 2:
+            # from the second step on every grad is its bucket view before backward ...
+            for p in params:
+                b, i = ddp._slot[id(p)]
+                assert p.grad is not None and p.grad.data_ptr() == b.view_for(i).data_ptr(), it
+        copies_before = ddp.grad_copies
+        with amp.scale_loss(loss, opt) as s:
+            s.backward()
+        if it >= 1:
+            assert ddp.grad_copies == copies_before, (it, "per-parameter grad copies on the steady-state path")
+        # ... and after it (autograd accumulated in place: the hook copied nothing)
+        for p in params:
+            b, i = ddp._slot[id(p)]
+            lo = b.buffer.data_ptr()
+            hi = lo + b.buffer.numel() * b.buffer.element_size()
+            assert lo <= p.grad.data_ptr() < hi, (it, "grad outside its bucket")
+        opt.step()
+    masters = list(amp.master_params(opt))
+    flat = torch.cat([p.detach().reshape(-1) for p in masters])
+    gathered = [torch.empty_like(flat) for _ in range(world)]
+    dist.all_gather(gathered, flat)
+    assert torch.equal(gathered[0], gathered[1]), "master params diverged across ranks"
+
+
+def test_ddp_zero_copy_under_fused_amp_gloo():
+    run_multiprocess(_ddp_zero_copy_worker, 2, ())
+
+
+def _ddp_zero_copy_matches_reference_worker(rank, world):
+    """Same training with DDP (zero-copy buckets) and with manual all-reduce of plain grads: the
+    master weights must agree bit for bit."""
+    import os
+
+    os.environ["APEX_AMD_AMP_SYNC_FREE"] = "force"
+    from apex import amp
+    from apex.amp._amp_state import _amp_state
+    from apex.optimizers import FusedAdam
+    from apex.parallel import DistributedDataParallel as DDP
+
+    _amp_state.sync_free_force = True
+
+    def make():
+        torch.manual_seed(0)
+        return torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 4))
+
+    def run(use_ddp):
+        model = make()
+        opt = FusedAdam(model.parameters(), lr=1e-2, materialize_master_grads=False)
+        model, opt = amp.initialize(model, opt, opt_level="O2", cast_model_type=torch.bfloat16, verbosity=0,
+                                    loss_scale=128.0)
+        net = DDP(model) if use_ddp else model
+        for it in range(4):
+            x = torch.randn(8, 16, generator=torch.Generator().manual_seed(100 * rank + it))
+            loss = net(x).float().pow(2).mean()
+            opt.zero_grad()
+            with amp.scale_loss(loss, opt) as s:
+                s.backward()
+                if not use_ddp:
+                    for p in model.parameters():
+                        dist.all_reduce(p.grad)
+                        p.grad.div_(world)
+            opt.step()
+        return torch.cat([p.detach().reshape(-1) for p in amp.master_params(opt)])
+
+    a = run(True)
+    b = run(False)
+    torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
+def test_ddp_zero_copy_matches_manual_allreduce_gloo():
+    run_multiprocess(_ddp_zero_copy_matches_reference_worker, 2, ())

@@ -37,15 +37,21 @@ def _ref_lamb_step(params, grads, state, lr, b1, b2, eps, wd, step):
         p.sub_(lr * ratio * u)
 
 
-def _worker(rank, world, kind, num_blocks, max_grad_norm):
-    from apex.contrib.optimizers import DistributedFusedAdam, DistributedFusedLAMB
+def _worker(rank, world, kind, num_blocks, max_grad_norm, extra=None):
+    from apex.contrib.optimizers import DistributedFusedAdam, DistributedFusedAdamV3, DistributedFusedLAMB
 
     model = _model()
     ref = copy.deepcopy(model)
     kw = dict(lr=1e-2, betas=(0.9, 0.99), eps=1e-8, weight_decay=0.01, dwu_num_blocks=num_blocks,
               min_block_elems=256)
+    kw.update(extra or {})
     if kind == "adam":
         opt = DistributedFusedAdam(model.parameters(), max_grad_norm=max_grad_norm, **kw)
+        ref_opt = torch.optim.AdamW(ref.parameters(), lr=1e-2, betas=(0.9, 0.99), eps=1e-8, weight_decay=0.01)
+    elif kind == "adam_v3":
+        opt = DistributedFusedAdamV3(model.parameters(), max_grad_norm=max_grad_norm, **kw)
+        assert opt._flat.mode == "ar"
+        ref_opt = torch.optim.AdamW(ref.parameters(), lr=1e-2, betas=(0.9, 0.99), eps=1e-8, weight_decay=0.01)
         ref_opt = torch.optim.AdamW(ref.parameters(), lr=1e-2, betas=(0.9, 0.99), eps=1e-8, weight_decay=0.01)
     else:
         opt = DistributedFusedLAMB(model.parameters(), max_grad_norm=max_grad_norm, **kw)
@@ -65,7 +71,7 @@ def _worker(rank, world, kind, num_blocks, max_grad_norm):
             grads.append(p.grad)
         if max_grad_norm > 0:
             torch.nn.utils.clip_grad_norm_(list(ref.parameters()), max_grad_norm)
-        if kind == "adam":
+        if kind in ("adam", "adam_v3"):
             ref_opt.step()
         else:
             with torch.no_grad():
@@ -77,12 +83,35 @@ def _worker(rank, world, kind, num_blocks, max_grad_norm):
             assert opt.L2_grad_norm is not None
     # model params are views into the flat buffer; grads were zeroed into the buffer
     assert all(p.grad is not None and float(p.grad.abs().sum()) == 0 for p in model.parameters())
+    if (extra or {}).get("dwu_group_size"):
+        g = extra["dwu_group_size"]
+        assert opt._flat.world == g and opt._flat.ar_world == world // g and opt._flat.dp_size == world
+        # replicas in different groups hold identical parameters
+        flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+        parts = [torch.empty_like(flat) for _ in range(world)]
+        dist.all_gather(parts, flat)
+        for q in parts[1:]:
+            torch.testing.assert_close(q, parts[0], rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("kind", ["adam", "lamb"])
 @pytest.mark.parametrize("num_blocks,max_grad_norm", [(1, 0.0), (3, 0.0), (2, 0.05)])
 def test_distributed_optimizer_matches_full_model(kind, num_blocks, max_grad_norm):
     run_multiprocess(_worker, world=2, args=(kind, num_blocks, max_grad_norm))
+
+
+@pytest.mark.parametrize("kind", ["adam", "lamb", "adam_v3"])
+@pytest.mark.parametrize("extra", [dict(dwu_group_size=2), dict(dwu_group_size=2, reduce_dtype=torch.float64),
+                                   dict(dwu_group_size=2, predivide=False)])
+def test_distributed_optimizer_two_level_world4(kind, extra):
+    """world 4 sharded over groups of 2 (reference dwu_group_size): reduce-scatter inside the group
+    plus all-reduce across groups must train exactly like the full model on the global batch."""
+    run_multiprocess(_worker, world=4, args=(kind, 2, 0.05 if kind == "lamb" else 0.0, extra))
+
+
+@pytest.mark.parametrize("num_blocks", [1, 3])
+def test_distributed_adam_v3_allreduce_mode(num_blocks):
+    run_multiprocess(_worker, world=2, args=("adam_v3", num_blocks, 0.0))
 
 
 def _overflow_worker(rank, world):
