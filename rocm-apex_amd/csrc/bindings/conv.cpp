@@ -1,0 +1,95 @@
+// pybind surface of the gfx950 implicit-GEMM convolutions (csrc/conv/conv_igemm.hip):
+// submodule ``_C.conv`` used by apex.ops.conv (ResNet 3x3 / strided convolutions, NHWC).
+// Activations are dense NHWC [N, H, W, C] tensors (the python layer passes zero-copy views of
+// torch channels_last tensors); weights are [K, taps, C] (k contiguous per tap).
+#include "common.h"
+#include "apex_amd/conv_api.h"
+
+namespace apex_amd {
+namespace {
+
+void check_nhwc(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 4 && t.is_contiguous(), "conv: ", what,
+              " must be a contiguous NHWC [N, H, W, C] GPU tensor");
+}
+
+ConvTapArgs make_args(const at::Tensor& in, const at::Tensor& w, const at::Tensor& out, int64_t oh, int64_t ow,
+                      int64_t ish, int64_t isw, int64_t osh, int64_t osw, int64_t oph, int64_t opw,
+                      const std::vector<int64_t>& dh, const std::vector<int64_t>& dw) {
+  check_nhwc(in, "input");
+  check_nhwc(out, "output");
+  TORCH_CHECK(w.is_cuda() && w.dim() == 3 && w.is_contiguous(), "conv: weight must be a contiguous [K, taps, C] tensor");
+  TORCH_CHECK(in.scalar_type() == w.scalar_type() && in.scalar_type() == out.scalar_type(),
+              "conv: input, weight and output must share a dtype");
+  TORCH_CHECK(dh.size() == dw.size() && !dh.empty() && (int64_t)dh.size() <= kConvMaxTaps, "conv: 1..9 taps");
+  TORCH_CHECK(w.size(1) == (int64_t)dh.size() && w.size(2) == in.size(3) && w.size(0) == out.size(3),
+              "conv: weight [K, taps, C] does not match input / output");
+  TORCH_CHECK(in.size(0) == out.size(0), "conv: batch mismatch");
+  ConvTapArgs a{};
+  a.in = in.data_ptr();
+  a.wt = w.data_ptr();
+  a.out = out.data_ptr();
+  a.n = (int)in.size(0);
+  a.ih = (int)in.size(1);
+  a.iw = (int)in.size(2);
+  a.c = (int)in.size(3);
+  a.oh = (int)oh;
+  a.ow = (int)ow;
+  a.oht = (int)out.size(1);
+  a.owt = (int)out.size(2);
+  a.kout = (int)out.size(3);
+  a.ish = (int)ish;
+  a.isw = (int)isw;
+  a.osh = (int)osh;
+  a.osw = (int)osw;
+  a.oph = (int)oph;
+  a.opw = (int)opw;
+  a.ntaps = (int)dh.size();
+  for (size_t t = 0; t < dh.size(); ++t) {
+    a.dh[t] = (int)dh[t];
+    a.dw[t] = (int)dw[t];
+  }
+  a.dtype = dtype_code(in.scalar_type());
+  TORCH_CHECK((oh - 1) * osh + oph < a.oht && (ow - 1) * osw + opw < a.owt, "conv: output grid exceeds the output");
+  return a;
+}
+
+// out[n, oh*osh+oph, ow*osw+opw, k] = sum_t,c in[n, oh*ish+dh[t], ow*isw+dw[t], c] * w[k, t, c]
+void tap_fprop(const at::Tensor& in, const at::Tensor& w, at::Tensor& out, int64_t oh, int64_t ow, int64_t ish,
+               int64_t isw, int64_t osh, int64_t osw, int64_t oph, int64_t opw, std::vector<int64_t> dh,
+               std::vector<int64_t> dw) {
+  ConvTapArgs a = make_args(in, w, out, oh, ow, ish, isw, osh, osw, oph, opw, dh, dw);
+  const c10::hip::HIPGuard g(in.get_device());
+  TORCH_CHECK(conv_tap_supported(a), "conv tap_fprop: unsupported (C and K must be multiples of 64, bf16/fp16)");
+  conv_tap_fprop(a, device_cus(in.get_device()), cur_stream());
+}
+
+// dw[k, t, c] (fp32-accumulated, written in dw's dtype) for the forward `in` -> dy geometry
+void wgrad(const at::Tensor& in, const at::Tensor& dy, at::Tensor& dw_out, int64_t ish, int64_t isw,
+           std::vector<int64_t> dh, std::vector<int64_t> dw) {
+  check_nhwc(dy, "grad");
+  TORCH_CHECK(dw_out.is_cuda() && dw_out.dim() == 3 && dw_out.is_contiguous(), "conv wgrad: dw must be [K, taps, C]");
+  TORCH_CHECK(dw_out.size(0) == dy.size(3) && dw_out.size(1) == (int64_t)dh.size() && dw_out.size(2) == in.size(3),
+              "conv wgrad: dw must be [K, taps, C]");
+  TORCH_CHECK(dw_out.scalar_type() == in.scalar_type() || dw_out.scalar_type() == at::kFloat,
+              "conv wgrad: dw must be fp32 or the activation dtype");
+  ConvTapArgs a = make_args(in, dw_out.scalar_type() == in.scalar_type() ? dw_out : dw_out.to(in.scalar_type()), dy,
+                            dy.size(1), dy.size(2), ish, isw, 1, 1, 0, 0, dh, dw);
+  a.wt = nullptr;
+  const c10::hip::HIPGuard g(in.get_device());
+  TORCH_CHECK(conv_wgrad_supported(a), "conv wgrad: unsupported shape");
+  const int cus = device_cus(in.get_device());
+  auto ws = at::empty({conv_wgrad_workspace_floats(a, cus)}, in.options().dtype(at::kFloat));
+  conv_wgrad(a, dy.data_ptr(), dw_out.data_ptr(), dtype_code(dw_out.scalar_type()), ws.data_ptr<float>(), cus,
+             cur_stream());
+}
+
+}  // namespace
+
+void bind_conv(pybind11::module_& root) {
+  auto m = root.def_submodule("conv", "gfx950 implicit-GEMM NHWC convolutions");
+  m.def("tap_fprop", &tap_fprop);
+  m.def("wgrad", &wgrad);
+}
+
+}  // namespace apex_amd

@@ -12,6 +12,7 @@ void bind_xentropy(pybind11::module_& m);
 void bind_attn(pybind11::module_& m);
 void bind_contrib(pybind11::module_& m);
 void bind_bn_nhwc(pybind11::module_& m);
+void bind_conv(pybind11::module_& m);
 }  // namespace apex_amd
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -38,6 +39,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 #endif
 #ifdef APEX_AMD_WITH_BN_NHWC
   apex_amd::bind_bn_nhwc(m);
+#endif
+#ifdef APEX_AMD_WITH_CONV
+  apex_amd::bind_conv(m);
 #endif
 #ifdef APEX_AMD_WITH_CONTRIB
   apex_amd::bind_contrib(m);

@@ -1,0 +1,49 @@
+// Torch-free launchers for the gfx950 implicit-GEMM convolutions (csrc/conv/conv_igemm.hip) on
+// NHWC (torch channels_last) bf16/fp16 activations.  They replace MIOpen for the ResNet 3x3 /
+// strided convolutions, where MIOpen runs at 20-30 % of the MFMA roofline on MI355X
+// (profiles/conv_shapes_miopen_r02.jsonl).  Reference capability: the fused convolutions of
+// apex/contrib/bottleneck (cudnn-frontend graphs, apex/contrib/csrc/bottleneck/bottleneck.cpp).
+//
+// ONE "tap" formulation covers forward and data-gradient:
+//   out[n, oh*osh + oph, ow*osw + opw, k] = sum_{t < ntaps, c} in[n, oh*ish + dh[t], ow*isw + dw[t], c]
+//                                                             * w[k][t][c]
+// with zero padding outside `in`.  Forward: taps (r - pad, s - pad), ish = stride.  Data gradient
+// of a stride-1 conv: the forward over dY with the flipped, transposed weight w'[c][t][k].  Data
+// gradient of a stride-2 conv: one launch per output phase (oph, opw), each with the 1-4 taps
+// that reach that phase (osh = osw = 2).  Weight gradient: its own kernel (split over pixels).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace apex_amd {
+
+constexpr int kConvMaxTaps = 9;
+
+struct ConvTapArgs {
+  const void* in;   // [n][h][w][c]
+  const void* wt;   // [kout][ntaps][c]
+  void* out;        // [n][oht][owt][kout]
+  int n, ih, iw, c;  // input tensor
+  int oh, ow;       // output grid computed (per image)
+  int oht, owt;     // output tensor spatial dims
+  int kout;
+  int ish, isw;     // input step per output step
+  int osh, osw, oph, opw;  // output placement
+  int ntaps;
+  int dh[kConvMaxTaps], dw[kConvMaxTaps];
+  int dtype;        // kBF16 / kF16
+};
+
+// shape constraints: c % 64 == 0, kout % 64 == 0, 16-byte aligned pointers
+bool conv_tap_supported(const ConvTapArgs& a);
+void conv_tap_fprop(const ConvTapArgs& a, int cus, hipStream_t s);
+
+// weight gradient: dw[k][t][c] = sum_{n,oh,ow} dy[n,oh,ow,k] * x[n, oh*ish + dh[t], ow*isw + dw[t], c]
+// (dy = `out` geometry with osh = osw = 1, oph = opw = 0; x = `in`).  fp32 result [kout][ntaps][c]
+// through split-K partials in `ws` (conv_wgrad_workspace_floats), summed in a fixed order.
+bool conv_wgrad_supported(const ConvTapArgs& a);
+int64_t conv_wgrad_workspace_floats(const ConvTapArgs& a, int cus);
+void conv_wgrad(const ConvTapArgs& a, const void* dy, void* dw_out, int out_dtype, float* ws, int cus,
+                hipStream_t s);
+
+}  // namespace apex_amd

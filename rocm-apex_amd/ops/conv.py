@@ -95,6 +95,151 @@ class Conv1x1NHWC(nn.Conv2d):
         return super().forward(x)
 
 
+# ------------------------------------------------------------------------------------------------
+# Implicit-GEMM convolutions (csrc/conv/conv_igemm.hip): 3x3 stride 1/2 and strided 1x1, NHWC.
+# ------------------------------------------------------------------------------------------------
+_TAP_ENABLED = os.environ.get("APEX_AMD_CONV_IGEMM", "1") != "0"
+
+
+def _conv_ext():
+    return _native.require("conv").conv
+
+
+def _nhwc(t):
+    """[N, H, W, C] zero-copy view of an NCHW-shaped channels_last tensor."""
+    return t.permute(0, 2, 3, 1)
+
+
+def _fwd_taps(k, pad):
+    return [(r - pad, s - pad) for r in range(k) for s in range(k)]
+
+
+def _w_krc(w):
+    """[K, taps, C] view of a channels_last [K, C, R, S] weight (copy only if not channels_last)."""
+    k, c, r, s = w.shape
+    return w.permute(0, 2, 3, 1).reshape(k, r * s, c)
+
+
+def _dgrad_phases(k, stride, pad, h, w):
+    """Per output phase (ph, pw) of the data gradient: (oh, ow, [(r, s, dh, dw)]).  dX[h] collects
+    dY[p] * W[r] over h = stride*p + r - pad; for h = stride*a + ph the contributing r satisfy
+    (ph + pad - r) % stride == 0 and read dY[a + (ph + pad - r) // stride]."""
+    out = []
+    for ph in range(stride):
+        for pw in range(stride):
+            taps = [(r, s_, (ph + pad - r) // stride, (pw + pad - s_) // stride)
+                    for r in range(k) for s_ in range(k)
+                    if (ph + pad - r) % stride == 0 and (pw + pad - s_) % stride == 0]
+            oh, ow = (h - ph + stride - 1) // stride, (w - pw + stride - 1) // stride
+            out.append((ph, pw, oh, ow, taps))
+    return out
+
+
+def conv_tap_forward(x, w, stride, pad):
+    """NHWC conv through the native tap kernel: x [N,C,H,W] channels_last, w [K,C,R,S]."""
+    n, c, h, wd = x.shape
+    kout, _, k, _ = w.shape
+    oh, ow = (h + 2 * pad - k) // stride + 1, (wd + 2 * pad - k) // stride + 1
+    y = torch.empty((n, kout, oh, ow), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    taps = _fwd_taps(k, pad)
+    _conv_ext().tap_fprop(_nhwc(x), _w_krc(w).contiguous(), _nhwc(y), oh, ow, stride, stride, 1, 1, 0, 0,
+                          [t[0] for t in taps], [t[1] for t in taps])
+    return y
+
+
+def conv_tap_dgrad(gy, w, x_shape, stride, pad):
+    n, c, h, wd = x_shape
+    kout, _, k, _ = w.shape
+    ext = _conv_ext()
+    phases = _dgrad_phases(k, stride, pad, h, wd)
+    covered = all(p[4] for p in phases)
+    alloc = torch.empty if covered else torch.zeros  # phases no tap reaches get zero gradient
+    dx = alloc((n, h, wd, c), dtype=gy.dtype, device=gy.device).permute(0, 3, 1, 2)
+    wk = w.permute(1, 2, 3, 0)  # [C, R, S, K] view
+    for ph, pw, oh, ow, taps in phases:
+        if not taps or oh <= 0 or ow <= 0:
+            continue
+        wt = torch.stack([wk[:, r, s_, :] for r, s_, _, _ in taps], 1).contiguous()  # [C, taps, K]
+        ext.tap_fprop(_nhwc(gy), wt, _nhwc(dx), oh, ow, 1, 1, stride, stride, ph, pw,
+                      [t[2] for t in taps], [t[3] for t in taps])
+    return dx
+
+
+def conv_tap_wgrad(gy, x, w_shape, stride, pad, out_dtype):
+    kout, c, k, _ = w_shape
+    dw = torch.empty((kout, k, k, c), dtype=out_dtype, device=gy.device)
+    taps = _fwd_taps(k, pad)
+    _conv_ext().wgrad(_nhwc(x), _nhwc(gy), dw.view(kout, k * k, c), stride, stride, [t[0] for t in taps],
+                      [t[1] for t in taps])
+    return dw.permute(0, 3, 1, 2)  # [K, C, R, S] in channels_last memory
+
+
+def tap_route(cin, cout, k, stride, h):
+    """(fwd, dgrad, wgrad) through the native kernels for this ResNet-style shape."""
+    if not _TAP_ENABLED:
+        return False, False, False
+    if k == 3:
+        return True, True, True
+    if k == 1 and stride == 2:
+        return True, False, True
+    return False, False, False
+
+
+class _ConvTapFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride, pad, route):
+        fwd, dg, wg = route
+        y = conv_tap_forward(x, w, stride, pad) if fwd else F.conv2d(x, w, None, stride, pad)
+        ctx.save_for_backward(x, w)
+        ctx.conf = (stride, pad, dg, wg)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        stride, pad, dg, wg = ctx.conf
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        dx = dw = None
+        if (need_x and not dg) or (need_w and not wg):
+            dx_m, dw_m, _ = torch.ops.aten.convolution_backward(
+                gy, x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
+                [need_x and not dg, need_w and not wg, False])
+            dx, dw = dx_m, dw_m
+        if need_x and dg:
+            dx = conv_tap_dgrad(gy, w, x.shape, stride, pad)
+        if need_w and wg:
+            dw = conv_tap_wgrad(gy, x, w.shape, stride, pad, w.dtype)
+        return dx, dw, None, None, None
+
+
+class Conv2dNHWC(nn.Conv2d):
+    """``nn.Conv2d(cin, cout, k, stride, padding=k // 2, bias=False)`` whose forward / data
+    gradient / weight gradient run on the gfx950 implicit-GEMM kernels (``tap_route`` per shape)
+    for channels_last bf16/fp16 activations; same parameter and state_dict as nn.Conv2d, plain
+    nn.Conv2d everywhere else (CPU, fp32, autocast, odd channel counts)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1):
+        super().__init__(in_channels, out_channels, kernel_size=kernel_size, stride=stride,
+                         padding=kernel_size // 2, bias=False)
+
+    def _native_ok(self, x):
+        w = self.weight
+        return (x.is_cuda and x.dim() == 4 and x.dtype == w.dtype and x.dtype in (torch.bfloat16, torch.float16)
+                and self.in_channels % 64 == 0 and self.out_channels % 64 == 0 and self.groups == 1
+                and self.dilation == (1, 1) and self.stride[0] == self.stride[1]
+                and x.is_contiguous(memory_format=torch.channels_last)
+                and w.is_contiguous(memory_format=torch.channels_last)
+                and not torch.is_autocast_enabled("cuda") and _native.available())
+
+    def forward(self, x):
+        if self._native_ok(x):
+            route = tap_route(self.in_channels, self.out_channels, self.kernel_size[0], self.stride[0], x.shape[2])
+            if any(route):
+                return _ConvTapFn.apply(x, self.weight, self.stride[0], self.padding[0], route)
+        return super().forward(x)
+
+
 class ChannelPadConv2d(nn.Conv2d):
     """``nn.Conv2d`` whose input channels are zero-padded to ``pad_to`` on the GPU path.
 

@@ -39,6 +39,7 @@ SUBSYSTEMS = {
     "attn.cpp": "APEX_AMD_WITH_ATTN",
     "contrib.cpp": "APEX_AMD_WITH_CONTRIB",
     "bn_nhwc.cpp": "APEX_AMD_WITH_BN_NHWC",
+    "conv.cpp": "APEX_AMD_WITH_CONV",
 }
 
 

@@ -1,0 +1,44 @@
+#!/bin/bash
+# One GPU-box session (gpurun): selected steps, each under its own time limit, chained so that a
+# crash / timeout / fault ends the call.  STEPS is a space-separated list of:
+#   tests      pytest -m gpu (TESTS selects files; default all)
+#   smoke      __graft_entry__.smoke()
+#   bench      1-GPU headline bench (BENCH_ARGS appended)
+#   syncbn2    2 ranks sharing the GPU, gloo, --sync-bn (fused bn_group=world over peer memory)
+#   prof       rocprofv3 --kernel-trace --stats of a short bench (after the APEX_BENCH_MARK spin)
+#   script     python $SCRIPT (a tools/ micro-benchmark), output to gpurun_out/script.log
+# Test failures (rc 1) do not stop the chain; anything >= 2 does.
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+export MIOPEN_USER_DB_PATH=$R/gpurun_out/miopen_udb
+export MIOPEN_CUSTOM_CACHE_DIR=$R/gpurun_out/miopen_cache
+mkdir -p $MIOPEN_USER_DB_PATH $MIOPEN_CUSTOM_CACHE_DIR
+stop() { echo "STOP: $1 rc=$2"; exit $2; }
+for s in ${STEPS:-tests smoke bench}; do
+  case $s in
+  tests)
+    timeout -k 10 ${TESTS_TIMEOUT:-600} python -u -m pytest ${TESTS:-tests} -m gpu -x -q -p no:cacheprovider \
+      --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+    rc=$?; tail -25 gpurun_out/pytest_gpu.log; [ $rc -ge 2 ] && stop pytest $rc ;;
+  smoke)
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+    rc=$?; tail -3 gpurun_out/smoke.log; [ $rc -ne 0 ] && stop smoke $rc ;;
+  bench)
+    timeout -k 10 400 python bench.py --steps ${BSTEPS:-20} --warmup ${BWARM:-8} ${BENCH_ARGS} > gpurun_out/bench.log 2>&1
+    rc=$?; tail -3 gpurun_out/bench.log; [ $rc -ne 0 ] && stop bench $rc ;;
+  syncbn2)
+    APEX_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+      --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --sync-bn --steps 4 --warmup 3 --batch-size 64 \
+      > gpurun_out/syncbn2.log 2>&1
+    rc=$?; tail -4 gpurun_out/syncbn2.log; [ $rc -ne 0 ] && stop syncbn2 $rc ;;
+  prof)
+    cd /tmp && APEX_BENCH_MARK=1 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_bench -o bench -- python3 $R/bench.py --steps 10 --warmup 6 ${BENCH_ARGS} > $R/gpurun_out/prof_bench.log 2>&1
+    rc=$?; cd $R; tail -3 gpurun_out/prof_bench.log; [ $rc -ne 0 ] && stop prof $rc ;;
+  script)
+    timeout -k 10 ${SCRIPT_TIMEOUT:-400} python $SCRIPT > gpurun_out/script.log 2>&1
+    rc=$?; tail -20 gpurun_out/script.log; [ $rc -ne 0 ] && stop script $rc ;;
+  esac
+done
+du -sh gpurun_out/miopen_udb gpurun_out/miopen_cache 2>/dev/null
+echo ALL_DONE
