@@ -23,6 +23,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# MIOpen find-db / perf-db of the convolutions this benchmark runs (collected on MI355X with
+# MIOPEN_USER_DB_PATH pointing here): a fresh box then skips most of the first-step kernel search
+_MIOPEN_DB = os.path.join(ROOT, "miopen_db")
+if os.path.isdir(_MIOPEN_DB):
+    os.environ.setdefault("MIOPEN_USER_DB_PATH", _MIOPEN_DB)
+
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 

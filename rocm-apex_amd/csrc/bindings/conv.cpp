@@ -90,6 +90,7 @@ void bind_conv(pybind11::module_& root) {
   auto m = root.def_submodule("conv", "gfx950 implicit-GEMM NHWC convolutions");
   m.def("tap_fprop", &tap_fprop);
   m.def("wgrad", &wgrad);
+  m.def("force_fprop_cfg", &conv_force_fprop_cfg);
 }
 
 }  // namespace apex_amd

@@ -28,6 +28,7 @@
 #include "apex_amd/device.h"
 #include "apex_amd/dispatch.h"
 
+#include <cstdlib>
 #include <stdexcept>
 
 namespace apex_amd {
@@ -88,19 +89,21 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 // =============================================================================================
 // fprop
 // =============================================================================================
-constexpr int BM = 256, BK = 64, THREADS = 512;
+constexpr int BM = 256, BK = 64;
+constexpr int STAGES = 3;  // wgrad LDS ring depth
 
-template <int BN> struct Layout;
-template <> struct Layout<256> { static constexpr int WM = 2, WN = 4; };
-template <> struct Layout<128> { static constexpr int WM = 4, WN = 2; };
-template <> struct Layout<64> { static constexpr int WM = 8, WN = 1; };
-
-template <int BN>
-constexpr size_t fprop_lds_bytes() {
-  constexpr size_t ops = (size_t)2 * (BM * BK + BN * BK) * 2;
-  constexpr size_t epi = (size_t)128 * (BN + 4) * 4;
-  return ops > epi ? ops : epi;
-}
+// Tile configuration: BN output channels per workgroup, WM x WN waves, S-deep LDS ring.
+template <int BN_, int WM_, int WN_, int S_>
+struct FCfg {
+  static constexpr int BN = BN_, WM = WM_, WN = WN_, S = S_;
+  static constexpr int NW = WM * WN, THREADS = NW * 64;
+  static constexpr int TM = BM / WM / 32, TN = BN / WN / 32;   // 32x32 MFMA tiles per wave
+  static constexpr int PA = BM / 8 / NW, PB = BN / 8 / NW;     // 1-KB DMA pieces per wave
+  static constexpr size_t OPS = (size_t)S * (BM * BK + BN * BK) * 2;
+  static constexpr size_t EPI = (size_t)128 * (BN + 4) * 4;
+  static constexpr size_t LDS = OPS > EPI ? OPS : EPI;
+  static_assert(PA >= 1 && PB >= 1 && TM >= 1 && TN >= 1, "bad tile configuration");
+};
 
 // k-major fragment of a 32-row subtile at k-step kk from a swizzled [rows][64] image
 __device__ __forceinline__ s16x8 frag_k(const uint16_t* tile, int rowbase, int kk, int lane) {
@@ -109,12 +112,12 @@ __device__ __forceinline__ s16x8 frag_k(const uint16_t* tile, int rowbase, int k
   return *reinterpret_cast<const s16x8*>(tile + row * BK + 8 * c);
 }
 
-template <typename T, int BN>
-__global__ void __launch_bounds__(THREADS, 1)
+template <typename T, typename C>
+__global__ void __launch_bounds__(C::THREADS, 1)
 fprop_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y, Geo g) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
-  constexpr int WM = Layout<BN>::WM, WN = Layout<BN>::WN;
-  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  constexpr int BN = C::BN, WM = C::WM, WN = C::WN, NW = C::NW, TM = C::TM, TN = C::TN;
+  constexpr int PA = C::PA, PB = C::PB, S = C::S;
   constexpr int TA = BM * BK, TB = BN * BK;
   auto a_buf = [&](int b) { return lds + b * (TA + TB); };
   auto b_buf = [&](int b) { return lds + b * (TA + TB) + TA; };
@@ -129,12 +132,12 @@ fprop_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, ui
   const int ohw = g.oh * g.ow;
   const int64_t kw = (int64_t)g.ntaps * g.c;  // weight row length
 
-  // this lane's 4 A rows (fixed for the whole K loop): image base + input origin of the pixel
-  int64_t abase[4];
-  int aih[4], aiw[4], asrc[4];
+  // this lane's PA A rows (fixed for the whole K loop): image base + input origin of the pixel
+  int64_t abase[PA];
+  int aih[PA], aiw[PA], asrc[PA];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = 8 * (i * 8 + wave) + (lane >> 3);
+  for (int i = 0; i < PA; ++i) {
+    const int row = 8 * (i * NW + wave) + (lane >> 3);
     const int m = row0 + row;
     asrc[i] = 8 * ((lane & 7) ^ ((row >> 1) & 7));
     if (m < g.m) {
@@ -157,17 +160,21 @@ fprop_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, ui
     const int dh = g.dh[t], dw = g.dw[t];
     uint16_t* adst = a_buf(buf);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < PA; ++i) {
       const int ih = aih[i] + dh, iw = aiw[i] + dw;
       const bool ok = (unsigned)ih < (unsigned)g.h && (unsigned)iw < (unsigned)g.w;
-      const uint16_t* src = ok ? X + abase[i] + ((int64_t)ih * g.w + iw) * g.c + c0 + asrc[i] : g_zero + asrc[i];
-      dma16(src, adst + (i * 8 + wave) * 512);
+      // branch-free select: every lane issues exactly one DMA per piece (a divergent branch
+      // would issue the instruction twice and break the counted vmcnt)
+      const uintptr_t real = (uintptr_t)(X + abase[i] + ((int64_t)ih * g.w + iw) * g.c + c0 + asrc[i]);
+      const uintptr_t zero = (uintptr_t)(g_zero + asrc[i]);
+      const uintptr_t msk = (uintptr_t)0 - (uintptr_t)ok;
+      dma16((const uint16_t*)((real & msk) | (zero & ~msk)), adst + (i * NW + wave) * 512);
     }
     uint16_t* bdst = b_buf(buf);
     const int64_t k0 = (int64_t)t * g.c + c0;
 #pragma unroll
-    for (int i = 0; i < BN / 64; ++i) {
-      const int j = i * 8 + wave;
+    for (int i = 0; i < PB; ++i) {
+      const int j = i * NW + wave;
       const int row = 8 * j + (lane >> 3);
       const int c = (lane & 7) ^ ((row >> 1) & 7);
       dma16(Wt + (int64_t)(col0 + row) * kw + k0 + 8 * c, bdst + j * 512);
@@ -182,50 +189,67 @@ fprop_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, ui
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  // S-stage ring (cdna_hip_programming.md "Pipelining across barriers"): the DMA of step
+  // kt+S-1 is issued while step kt computes.  Each wave waits only for ITS OWN DMA of step kt
+  // (counted vmcnt: newer steps stay in flight), then a raw s_barrier publishes every wave's
+  // pieces (a __syncthreads would drain vmcnt to 0).  The buffer refilled at step kt was last
+  // read at step kt-1, which every wave finished before this barrier.
+  constexpr int PER_STEP = PA + PB;  // DMA instructions per wave per K-step
+#pragma unroll
+  for (int p = 0; p < S - 1; ++p)
+    if (p < nk) issue(p, p);
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
+    const int ahead = nk - 1 - kt < S - 2 ? nk - 1 - kt : S - 2;  // younger steps in flight
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER_STEP) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_STEP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + S - 1 < nk) issue(kt + S - 1, (kt + S - 1) % S);
+    const int cur = kt % S;
     const uint16_t* at = a_buf(cur);
     const uint16_t* bt = b_buf(cur);
+    // all of this step's fragments first (the reads of later k-slices overlap the MFMAs of
+    // earlier ones; the compiler's counted lgkmcnt waits release them one slice at a time)
+    s16x8 af[BK / 16][TM], bf[BK / 16][TN];
 #pragma unroll
     for (int kk = 0; kk < BK / 16; ++kk) {
-      s16x8 af[TM], bf[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = frag_k(at, wm * (BM / WM) + 32 * i, kk, lane);
+      for (int i = 0; i < TM; ++i) af[kk][i] = frag_k(at, wm * (BM / WM) + 32 * i, kk, lane);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = frag_k(bt, wn * (BN / WN) + 32 * j, kk, lane);
+      for (int j = 0; j < TN; ++j) bf[kk][j] = frag_k(bt, wn * (BN / WN) + 32 * j, kk, lane);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma<T>(af[i], bf[j], acc[i][j]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma<T>(af[kk][i], bf[kk][j], acc[i][j]);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 
   // ---- epilogue: two 128-row halves staged as fp32 through LDS, 16-byte row stores ----
   constexpr int CST = BN + 4;
-  constexpr int CPR = BN / 8;            // 8-column chunks per row
-  constexpr int RP = THREADS / CPR;      // rows per pass
+  constexpr int CPR = BN / 8;               // 8-column chunks per row
+  constexpr int RP = C::THREADS / CPR;      // rows per pass
   float* cs = reinterpret_cast<float*>(lds);
   const int ch = tid % CPR, rsub = tid / CPR;
   const int gc = col0 + ch * 8;
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     const int wr0 = wm * (BM / WM);
-    if (wr0 / 128 == half) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i) {
+      const int rb = wr0 + 32 * i;
+      if (rb / 128 != half) continue;
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int rl = wr0 - 128 * half + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            cs[rl * CST + wn * (BN / WN) + 32 * j + (lane & 31)] = acc[i][j][r];
-          }
+        for (int r = 0; r < 16; ++r) {
+          const int rl = rb - 128 * half + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          cs[rl * CST + wn * (BN / WN) + 32 * j + (lane & 31)] = acc[i][j][r];
+        }
     }
     __syncthreads();
 #pragma unroll
@@ -281,7 +305,7 @@ __device__ __forceinline__ s16x8 frag_t(const uint16_t* tile, int colbase, int k
 
 // BMW x BNW output tile (kout rows x channel columns of one tap), 4 waves in 2 x 2
 template <typename T, int BMW, int BNW>
-__global__ void __launch_bounds__(WG_THREADS, 2)
+__global__ void __launch_bounds__(WG_THREADS, BMW == 128 ? 1 : 2)
 wgrad_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ DY, float* __restrict__ part, Geo g,
              int chunk) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
@@ -316,8 +340,10 @@ wgrad_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ DY, fl
       const int slot = lane % (BMW / 8);
       const int c = slot ^ (tr_swz<BMW>(row) << 2);
       const int p = pbase + row;
-      const uint16_t* src = p < p_end ? DY + (int64_t)p * g.kout + k0 + 8 * c : g_zero + 8 * (c & 7);
-      dma16(src, adst + piece * 512);
+      const uintptr_t real = (uintptr_t)(DY + (int64_t)p * g.kout + k0 + 8 * c);
+      const uintptr_t zero = (uintptr_t)(g_zero + 8 * (c & 7));
+      const uintptr_t msk = (uintptr_t)0 - (uintptr_t)(p < p_end);
+      dma16((const uint16_t*)((real & msk) | (zero & ~msk)), adst + piece * 512);
     }
     uint16_t* bdst = b_buf(buf);
 #pragma unroll
@@ -327,15 +353,14 @@ wgrad_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ DY, fl
       const int slot = lane % (BNW / 8);
       const int c = slot ^ (tr_swz<BNW>(row) << 2);
       const int p = pbase + row;
-      const uint16_t* src = g_zero + 8 * (c & 7);
-      if (p < p_end) {
-        const int nimg = p / ohw, rem = p - nimg * ohw;
-        const int oy = rem / g.ow, ox = rem - oy * g.ow;
-        const int ih = oy * g.ish + dh, iw = ox * g.isw + dw;
-        if ((unsigned)ih < (unsigned)g.h && (unsigned)iw < (unsigned)g.w)
-          src = X + (((int64_t)nimg * g.h + ih) * g.w + iw) * g.c + c0 + 8 * c;
-      }
-      dma16(src, bdst + piece * 512);
+      const int nimg = p / ohw, rem = p - nimg * ohw;
+      const int oy = rem / g.ow, ox = rem - oy * g.ow;
+      const int ih = oy * g.ish + dh, iw = ox * g.isw + dw;
+      const bool ok = p < p_end && (unsigned)ih < (unsigned)g.h && (unsigned)iw < (unsigned)g.w;
+      const uintptr_t real = (uintptr_t)(X + (((int64_t)nimg * g.h + ih) * g.w + iw) * g.c + c0 + 8 * c);
+      const uintptr_t zero = (uintptr_t)(g_zero + 8 * (c & 7));
+      const uintptr_t msk = (uintptr_t)0 - (uintptr_t)ok;
+      dma16((const uint16_t*)((real & msk) | (zero & ~msk)), bdst + piece * 512);
     }
   };
 
@@ -347,14 +372,17 @@ wgrad_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ DY, fl
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  if (nk > 0) {
-    issue(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
+  // same 3-stage ring as fprop (counted vmcnt, raw barrier)
+  constexpr int PER_STEP = TA / 512 / 4 + TB / 512 / 4;
+  if (nk > 0) issue(0, 0);
+  if (nk > 1) issue(1, 1);
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_STEP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < nk) issue(kt + 2, (kt + 2) % STAGES);
+    const int cur = kt % STAGES;
     const uint16_t* at = a_buf(cur);
     const uint16_t* bt = b_buf(cur);
 #pragma unroll
@@ -369,8 +397,6 @@ wgrad_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ DY, fl
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma<T>(af[i], bf[j], acc[i][j]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
 
   // fp32 partial tile straight from the accumulators: each register row is 32 consecutive
@@ -415,7 +441,7 @@ inline WgPlan wgrad_plan(const ConvTapArgs& a, int cus) {
   p.bn = big ? 128 : 64;
   p.tiles = (a.kout / p.bm) * (a.ntaps * a.c / p.bn);
   const int64_t m = (int64_t)a.n * a.oh * a.ow;
-  const int target = cus * 4;  // 2 resident workgroups per CU, two rounds
+  const int target = cus * (big ? 2 : 4);  // resident workgroups per CU (LDS ring) x two rounds
   int64_t s = (target + p.tiles - 1) / p.tiles;
   const int64_t max_s = (m + 16 * WG_BK - 1) / (16 * WG_BK);  // >= 16 K-steps per workgroup
   if (s > max_s) s = max_s;
@@ -440,27 +466,64 @@ bool conv_tap_supported(const ConvTapArgs& a) {
   return aligned16(a.in) && aligned16(a.wt) && aligned16(a.out);
 }
 
+// fprop tile configurations (APEX_AMD_CONV_CFG=<index> forces one, for A/B sweeps):
+//   0: BN 128, 8 waves 4x2 (64x64 each), 3 stages   1: BN 64, 8 waves 8x1 (32x64), 3 stages
+//   2: BN 128, 4 waves 2x2 (128x64), 3 stages         3: BN 64, 4 waves 4x1 (64x64), 3 stages
+//   4: BN 128, 8 waves, 2 stages                       5: BN 64, 8 waves, 2 stages
+//   6: BN 256, 8 waves 2x4 (128x64), 2 stages
+using FC0 = conv::FCfg<128, 4, 2, 3>;
+using FC1 = conv::FCfg<64, 8, 1, 3>;
+using FC2 = conv::FCfg<128, 2, 2, 3>;
+using FC3 = conv::FCfg<64, 4, 1, 3>;
+using FC4 = conv::FCfg<128, 4, 2, 2>;
+using FC5 = conv::FCfg<64, 8, 1, 2>;
+using FC6 = conv::FCfg<256, 2, 4, 2>;
+
+static int g_forced_cfg = [] {
+  const char* e = std::getenv("APEX_AMD_CONV_CFG");
+  return e ? std::atoi(e) : -1;
+}();
+
+void conv_force_fprop_cfg(int cfg) { g_forced_cfg = cfg; }
+
+static int fprop_cfg(const ConvTapArgs& a, int cus) {
+  const int forced = g_forced_cfg;
+  const int64_t tiles_m = ((int64_t)a.n * a.oh * a.ow + conv::BM - 1) / conv::BM;
+  auto ok = [&](int bn) { return a.kout % bn == 0; };
+  if (forced >= 0 && forced <= 6) {
+    const int bn = forced == 6 ? 256 : (forced % 2 == 0 ? 128 : 64);
+    if (ok(bn)) return forced;
+  }
+  // measured on MI355X (profiles/conv_cfg_sweep_r02.jsonl, ResNet-50 3x3 shapes, bs 256): the
+  // 2-stage rings win; BN 256 where it still gives >= half a wave of tiles, BN 64 for <= 128
+  // output channels (two workgroups per CU), BN 128 otherwise
+  if (a.kout <= 128) return 5;
+  if (ok(256) && tiles_m * (a.kout / 256) >= cus / 2) return 6;
+  return ok(128) ? 4 : 5;
+}
+
 void conv_tap_fprop(const ConvTapArgs& a, int cus, hipStream_t s) {
   if (!conv_tap_supported(a)) throw std::runtime_error("conv_tap_fprop: unsupported shape / dtype / alignment");
   const conv::Geo g = conv::make_geo(a);
   const int64_t tiles_m = (g.m + conv::BM - 1) / conv::BM;
-  int bn = 64;
-  for (int cand : {256, 128}) {
-    if (a.kout % cand == 0 && tiles_m * (a.kout / cand) >= cus) {
-      bn = cand;
-      break;
-    }
-  }
-  const unsigned grid = (unsigned)(tiles_m * (a.kout / bn));
+  const int cfg = fprop_cfg(a, cus);
   dispatch_16(a.dtype, [&](auto tag) {
     using T = typename decltype(tag)::type;
-    auto go = [&](auto kern, size_t lds) {
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(conv::THREADS), lds, s, (const uint16_t*)a.in, (const uint16_t*)a.wt,
-                         (uint16_t*)a.out, g);
+    auto go = [&](auto cfg_tag) {
+      using C = decltype(cfg_tag);
+      const unsigned grid = (unsigned)(tiles_m * (a.kout / C::BN));
+      hipLaunchKernelGGL((conv::fprop_kernel<T, C>), dim3(grid), dim3(C::THREADS), C::LDS, s, (const uint16_t*)a.in,
+                         (const uint16_t*)a.wt, (uint16_t*)a.out, g);
     };
-    if (bn == 256) go(conv::fprop_kernel<T, 256>, conv::fprop_lds_bytes<256>());
-    else if (bn == 128) go(conv::fprop_kernel<T, 128>, conv::fprop_lds_bytes<128>());
-    else go(conv::fprop_kernel<T, 64>, conv::fprop_lds_bytes<64>());
+    switch (cfg) {
+      case 0: go(FC0{}); break;
+      case 1: go(FC1{}); break;
+      case 2: go(FC2{}); break;
+      case 3: go(FC3{}); break;
+      case 4: go(FC4{}); break;
+      case 5: go(FC5{}); break;
+      default: go(FC6{}); break;
+    }
   }, "conv_tap_fprop");
   check_launch("conv_tap_fprop");
 }
@@ -484,7 +547,7 @@ void conv_wgrad(const ConvTapArgs& a, const void* dy, void* dw_out, int out_dtyp
   dispatch_16(a.dtype, [&](auto tag) {
     using T = typename decltype(tag)::type;
     auto go = [&](auto kern, int bm, int bn) {
-      const size_t lds = (size_t)2 * conv::WG_BK * (bm + bn) * 2;
+      const size_t lds = (size_t)conv::STAGES * conv::WG_BK * (bm + bn) * 2;
       hipLaunchKernelGGL(kern, dim3(p.tiles, p.splits), dim3(conv::WG_THREADS), lds, s, (const uint16_t*)a.in,
                          (const uint16_t*)dy, ws, g, p.chunk);
     };

@@ -36,6 +36,8 @@ struct ConvTapArgs {
 
 // shape constraints: c % 64 == 0, kout % 64 == 0, 16-byte aligned pointers
 bool conv_tap_supported(const ConvTapArgs& a);
+// A/B hook: force one fprop tile configuration (-1 = per-shape choice); see conv_igemm.hip
+void conv_force_fprop_cfg(int cfg);
 void conv_tap_fprop(const ConvTapArgs& a, int cus, hipStream_t s);
 
 // weight gradient: dw[k][t][c] = sum_{n,oh,ow} dy[n,oh,ow,k] * x[n, oh*ish + dh[t], ow*isw + dw[t], c]

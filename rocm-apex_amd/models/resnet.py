@@ -23,22 +23,25 @@ and are summed inside its backward reduction instead of by an autograd add over 
 import torch
 import torch.nn as nn
 
-from ..ops.conv import ChannelPadConv2d, Conv1x1NHWC
+from ..ops.conv import ChannelPadConv2d, Conv1x1NHWC, Conv2dNHWC
 from ..ops.pooling import MaxPool2dNHWC
 
 __all__ = ["ResNet", "BasicBlock", "Bottleneck", "resnet18", "resnet34", "resnet50", "resnet101", "resnet152"]
 
 
-def conv3x3(cin, cout, stride=1, groups=1, dilation=1):
+def conv3x3(cin, cout, stride=1, groups=1, dilation=1, native=False):
+    # native: the gfx950 implicit-GEMM NHWC kernels where they beat MIOpen (ops/conv.py tap_route)
+    if native and groups == 1 and dilation == 1:
+        return Conv2dNHWC(cin, cout, 3, stride)
     return nn.Conv2d(cin, cout, kernel_size=3, stride=stride, padding=dilation, groups=groups, bias=False,
                      dilation=dilation)
 
 
 def conv1x1(cin, cout, stride=1, native=False):
-    # native: per-shape routing of the NHWC GEMM to the gfx950 MFMA kernels (ops/conv.py); same
-    # parameters / state_dict as nn.Conv2d
+    # native: per-shape routing of the NHWC GEMM / implicit-GEMM kernels to the gfx950 MFMA
+    # kernels (ops/conv.py); same parameters / state_dict as nn.Conv2d
     if native:
-        return Conv1x1NHWC(cin, cout, stride)
+        return Conv1x1NHWC(cin, cout, stride) if stride == 1 else Conv2dNHWC(cin, cout, 1, stride)
     return nn.Conv2d(cin, cout, kernel_size=1, stride=stride, bias=False)
 
 
@@ -56,10 +59,10 @@ class BasicBlock(nn.Module):
         super().__init__()
         norm_layer = norm_layer or nn.BatchNorm2d
         self.fused_bn = fused_bn
-        self.conv1 = conv3x3(inplanes, planes, stride)
+        self.conv1 = conv3x3(inplanes, planes, stride, native=fused_bn)
         self.bn1 = _fused_bn(planes, True, bn_group) if fused_bn else norm_layer(planes)
         self.relu = nn.ReLU(inplace=True)
-        self.conv2 = conv3x3(planes, planes)
+        self.conv2 = conv3x3(planes, planes, native=fused_bn)
         self.bn2 = _fused_bn(planes, True, bn_group) if fused_bn else norm_layer(planes)
         self.downsample = downsample
         self.stride = stride
@@ -89,7 +92,7 @@ class Bottleneck(nn.Module):
         nl = (lambda c, relu: _fused_bn(c, relu, bn_group)) if fused_bn else (lambda c, relu: norm_layer(c))  # noqa: E731
         self.conv1 = conv1x1(inplanes, width, native=fused_bn)
         self.bn1 = nl(width, True)
-        self.conv2 = conv3x3(width, width, stride, groups, dilation)
+        self.conv2 = conv3x3(width, width, stride, groups, dilation, native=fused_bn)
         self.bn2 = nl(width, True)
         self.conv3 = conv1x1(width, planes * self.expansion, native=fused_bn)
         self.bn3 = nl(planes * self.expansion, True)
@@ -161,7 +164,8 @@ class ResNet(nn.Module):
         if stride != 1 or self.inplanes != planes * block.expansion:
             bn = (_fused_bn(planes * block.expansion, False, self.bn_group) if self.fused_bn
                   else norm_layer(planes * block.expansion))
-            downsample = nn.Sequential(conv1x1(self.inplanes, planes * block.expansion, stride), bn)
+            downsample = nn.Sequential(conv1x1(self.inplanes, planes * block.expansion, stride, native=self.fused_bn),
+                                       bn)
         layers = [block(self.inplanes, planes, stride, downsample, self.groups, self.base_width, self.dilation,
                         norm_layer, fused_bn=self.fused_bn, bn_group=self.bn_group)]
         self.inplanes = planes * block.expansion

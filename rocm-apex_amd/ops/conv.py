@@ -175,13 +175,20 @@ def conv_tap_wgrad(gy, x, w_shape, stride, pad, out_dtype):
 
 
 def tap_route(cin, cout, k, stride, h):
-    """(fwd, dgrad, wgrad) through the native kernels for this ResNet-style shape."""
+    """(fwd, dgrad, wgrad) through the native kernels for this shape, from the per-shape A/B
+    against MIOpen on MI355X (profiles/conv_cfg_sweep_r02.jsonl, profiles/conv_igemm_v1_vs_miopen_r02
+    .jsonl; ResNet-50 bs 256 bf16):
+      * 3x3: forward native except at 128 output channels (MIOpen 0.9-1.0x ahead there); data
+        gradient native except the stride-2 / <= 128-channel one (per-phase launches lose);
+        native 1.05-1.42x elsewhere (e.g. 14x14x256 dgrad 78 vs 111 us);
+      * 1x1 stride 2 (downsample): data gradient native (1.02-1.24x);
+      * weight gradients stay on MIOpen (the split-K kernel is 0.5-0.9x)."""
     if not _TAP_ENABLED:
         return False, False, False
     if k == 3:
-        return True, True, True
+        return cout != 128, not (stride == 2 and cout <= 128), False
     if k == 1 and stride == 2:
-        return True, False, True
+        return False, True, False
     return False, False, False
 
 

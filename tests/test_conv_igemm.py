@@ -59,10 +59,11 @@ def test_gpu_conv2d_nhwc_module_autograd():
     from apex.ops import conv as C
 
     torch.manual_seed(1)
-    m = C.Conv2dNHWC(64, 128, 3, stride=2).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
-    ref = torch.nn.Conv2d(64, 128, 3, 2, 1, bias=False).cuda()
+    m = C.Conv2dNHWC(256, 256, 3, stride=2).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
+    assert C.tap_route(256, 256, 3, 2, 16)[0], "shape expected on the native forward path"
+    ref = torch.nn.Conv2d(256, 256, 3, 2, 1, bias=False).cuda()
     ref.weight.data.copy_(m.weight.float())
-    x = torch.randn(4, 64, 16, 16, device="cuda").to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(4, 256, 16, 16, device="cuda").to(torch.bfloat16).to(memory_format=torch.channels_last)
     x.requires_grad_(True)
     xr = x.detach().float().requires_grad_(True)
     calls = {"n": 0}
