@@ -116,36 +116,48 @@ __global__ void __launch_bounds__(256) stats_partial(const T* __restrict__ x, in
   }
 }
 
-// Sum the gy partial rows of two [gy][C] slabs for 16 channels per block: thread (ch, g) sums rows
-// g, g+16, ... (4 independent accumulators keep loads in flight), then a fixed-order LDS reduce.
+// Sum the gy partial rows of two [gy][C] slabs for kFinC channels per block: thread (ch, g) sums
+// rows g, g + kFinG, ... (4 independent accumulators keep loads in flight), then a fixed-order
+// LDS reduce over the kFinG row groups (deterministic).  8 channels x 32 row groups per block:
+// the finalize is latency-bound (a few KB per block), so it spreads the rows over many lanes.
+constexpr int kFinC = 8, kFinG = 256 / kFinC;
+
 __device__ __forceinline__ void sum_partials(const float* __restrict__ part, int gy, int c, int ch, int g,
-                                             float (&red)[2][16][17], float& a, float& b) {
+                                             float (&red)[2][kFinG][kFinC + 1], float& a, float& b) {
   float a4[4] = {0.f, 0.f, 0.f, 0.f}, b4[4] = {0.f, 0.f, 0.f, 0.f};
   if (ch < c) {
     int j = g;
-    for (; j + 48 < gy; j += 64) {
+    for (; j + 3 * kFinG < gy; j += 4 * kFinG) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        a4[u] += part[(int64_t)(j + 16 * u) * c + ch];
-        b4[u] += part[(int64_t)(gy + j + 16 * u) * c + ch];
+        a4[u] += part[(int64_t)(j + kFinG * u) * c + ch];
+        b4[u] += part[(int64_t)(gy + j + kFinG * u) * c + ch];
       }
     }
-    for (; j < gy; j += 16) {
+    for (; j < gy; j += kFinG) {
       a4[0] += part[(int64_t)j * c + ch];
       b4[0] += part[(int64_t)(gy + j) * c + ch];
     }
   }
-  red[0][g][threadIdx.x & 15] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
-  red[1][g][threadIdx.x & 15] = (b4[0] + b4[1]) + (b4[2] + b4[3]);
+  const int lc = threadIdx.x % kFinC;
+  red[0][g][lc] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+  red[1][g][lc] = (b4[0] + b4[1]) + (b4[2] + b4[3]);
   __syncthreads();
   a = 0.f;
   b = 0.f;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    a += red[0][i][threadIdx.x & 15];
-    b += red[1][i][threadIdx.x & 15];
+  if (g == 0) {
+#pragma unroll 8
+    for (int i = 0; i < kFinG; ++i) {
+      a += red[0][i][lc];
+      b += red[1][i][lc];
+    }
   }
 }
+
+#define BN_FIN_INDEX                               \
+  __shared__ float red[2][kFinG][kFinC + 1];       \
+  const int g = threadIdx.x / kFinC;               \
+  const int ch = blockIdx.x * kFinC + (threadIdx.x % kFinC)
 
 template <typename T>
 __global__ void __launch_bounds__(256) stats_finalize(const float* __restrict__ part, int gy, int c, float n,
@@ -154,9 +166,7 @@ __global__ void __launch_bounds__(256) stats_finalize(const float* __restrict__ 
                                                       float* __restrict__ rvar, float* __restrict__ save_mean,
                                                       float* __restrict__ save_invstd, float* __restrict__ coef,
                                                       const T* __restrict__ x) {
-  __shared__ float red[2][16][17];
-  const int g = threadIdx.x >> 4;
-  const int ch = blockIdx.x * 16 + (threadIdx.x & 15);
+  BN_FIN_INDEX;
   float s1, s2;
   sum_partials(part, gy, c, ch, g, red, s1, s2);
   if (g != 0 || ch >= c) return;
@@ -183,9 +193,7 @@ __global__ void __launch_bounds__(256) stats_finalize(const float* __restrict__ 
 template <typename T>
 __global__ void __launch_bounds__(256) stats_local(const float* __restrict__ part, int gy, int c, float n,
                                                    const T* __restrict__ x, float* __restrict__ payload) {
-  __shared__ float red[2][16][17];
-  const int g = threadIdx.x >> 4;
-  const int ch = blockIdx.x * 16 + (threadIdx.x & 15);
+  BN_FIN_INDEX;
   float s1, s2;
   sum_partials(part, gy, c, ch, g, red, s1, s2);
   if (g != 0 || ch >= c) return;
@@ -378,9 +386,7 @@ __global__ void __launch_bounds__(256) bwd_finalize(const float* __restrict__ pa
                                                     const float* __restrict__ mean, const float* __restrict__ istd,
                                                     const float* __restrict__ w, float* __restrict__ gw,
                                                     float* __restrict__ gb, float* __restrict__ coef) {
-  __shared__ float red[2][16][17];
-  const int g = threadIdx.x >> 4;
-  const int ch = blockIdx.x * 16 + (threadIdx.x & 15);
+  BN_FIN_INDEX;
   float sdy, sdyx;
   sum_partials(part, gy, c, ch, g, red, sdy, sdyx);
   if (g != 0 || ch >= c) return;
@@ -399,9 +405,7 @@ __global__ void __launch_bounds__(256) bwd_finalize(const float* __restrict__ pa
 __global__ void __launch_bounds__(256) bwd_local(const float* __restrict__ part, int gy, int c,
                                                  const float* __restrict__ istd, float* __restrict__ gw,
                                                  float* __restrict__ gb, float* __restrict__ payload) {
-  __shared__ float red[2][16][17];
-  const int g = threadIdx.x >> 4;
-  const int ch = blockIdx.x * 16 + (threadIdx.x & 15);
+  BN_FIN_INDEX;
   float sdy, sdyx;
   sum_partials(part, gy, c, ch, g, red, sdy, sdyx);
   if (g != 0 || ch >= c) return;
@@ -497,7 +501,7 @@ void bn_nhwc_stats(const void* x, int x_t, int64_t m, int c, const float* w, con
   dispatch_float(x_t, [&](auto tag) {
     using T = typename decltype(tag)::type;
     hipLaunchKernelGGL((bnh::stats_partial<T>), dim3(g.gx, g.gy), dim3(g.tx, g.ty), lds, s, (const T*)x, m, c, ws);
-    hipLaunchKernelGGL((bnh::stats_finalize<T>), dim3((c + 15) / 16), dim3(256), 0, s, ws, g.gy, c, (float)m, w, b,
+    hipLaunchKernelGGL((bnh::stats_finalize<T>), dim3((c + bnh::kFinC - 1) / bnh::kFinC), dim3(256), 0, s, ws, g.gy, c, (float)m, w, b,
                        eps, momentum, running_mean, running_var, save_mean, save_invstd, coef_fwd, (const T*)x);
   }, "bn_nhwc stats");
   check_launch("bn_nhwc_stats");
@@ -512,7 +516,7 @@ void bn_nhwc_stats_local(const void* x, int x_t, int64_t m, int c, float* payloa
   dispatch_float(x_t, [&](auto tag) {
     using T = typename decltype(tag)::type;
     hipLaunchKernelGGL((bnh::stats_partial<T>), dim3(g.gx, g.gy), dim3(g.tx, g.ty), lds, s, (const T*)x, m, c, ws);
-    hipLaunchKernelGGL((bnh::stats_local<T>), dim3((c + 15) / 16), dim3(256), 0, s, ws, g.gy, c, (float)m, (const T*)x,
+    hipLaunchKernelGGL((bnh::stats_local<T>), dim3((c + bnh::kFinC - 1) / bnh::kFinC), dim3(256), 0, s, ws, g.gy, c, (float)m, (const T*)x,
                        payload);
   }, "bn_nhwc stats local");
   check_launch("bn_nhwc_stats_local");
@@ -613,10 +617,10 @@ void bn_nhwc_bwd_reduce(const void* dy, const void* x, int x_t, const void* z, c
     } else go(F{}, Tr{}, F{}, F{});
   }, "bn_nhwc bwd reduce");
   if (group_payload)  // bn_group > 1: local sums for the exchange, coefficients after it
-    hipLaunchKernelGGL(bnh::bwd_local, dim3((c + 15) / 16), dim3(256), 0, s, ws, g.gy, c, save_invstd, grad_w, grad_b,
+    hipLaunchKernelGGL(bnh::bwd_local, dim3((c + bnh::kFinC - 1) / bnh::kFinC), dim3(256), 0, s, ws, g.gy, c, save_invstd, grad_w, grad_b,
                        group_payload);
   else
-    hipLaunchKernelGGL(bnh::bwd_finalize, dim3((c + 15) / 16), dim3(256), 0, s, ws, g.gy, c, 1.f / (float)m, save_mean,
+    hipLaunchKernelGGL(bnh::bwd_finalize, dim3((c + bnh::kFinC - 1) / bnh::kFinC), dim3(256), 0, s, ws, g.gy, c, 1.f / (float)m, save_mean,
                        save_invstd, w, grad_w, grad_b, coef_bwd);
   check_launch("bn_nhwc_bwd_reduce");
 }

@@ -34,7 +34,11 @@ for s in ${STEPS:-tests smoke bench}; do
     rc=$?; tail -4 gpurun_out/syncbn2.log; [ $rc -ne 0 ] && stop syncbn2 $rc ;;
   prof)
     cd /tmp && APEX_BENCH_MARK=1 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_bench -o bench -- python3 $R/bench.py --steps 10 --warmup 6 ${BENCH_ARGS} > $R/gpurun_out/prof_bench.log 2>&1
-    rc=$?; cd $R; tail -3 gpurun_out/prof_bench.log; [ $rc -ne 0 ] && stop prof $rc ;;
+    rc=$?; cd $R; tail -3 gpurun_out/prof_bench.log; [ $rc -ne 0 ] && stop prof $rc
+    # summarize on the box (the raw trace db can exceed what gpurun merges back)
+    python tools/prof_summary.py gpurun_out/prof_bench/bench_results.db --after spin_kernel --steps 10 --top 60 \
+      --md gpurun_out/prof_summary.md --title "${PROF_TITLE:-ResNet-50 bench kernel trace}" > /dev/null 2>&1
+    head -12 gpurun_out/prof_summary.md; rm -rf gpurun_out/prof_bench ;;
   script)
     timeout -k 10 ${SCRIPT_TIMEOUT:-400} python $SCRIPT > gpurun_out/script.log 2>&1
     rc=$?; tail -20 gpurun_out/script.log; [ $rc -ne 0 ] && stop script $rc ;;
