@@ -25,6 +25,7 @@
 #include "apex_amd/device.h"
 #include "apex_amd/dispatch.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace apex_amd {
@@ -37,7 +38,19 @@ struct Geo {
   int tx, ty, gx, gy;
 };
 
-inline Geo geo(int64_t m, int c, int cus) {
+// workgroups per CU of the partial passes: the read-only statistics pass keeps twice as many
+// bytes in flight (4 per CU) as the two-tensor gradient pass (2 per CU), which otherwise reads at
+// ~3 TB/s (profiles/resnet50_steady_r02b.md)
+// (APEX_BN_STATS_BPC / APEX_BN_BWD_BPC override them for A/B sweeps, tools/bn_bench.py)
+inline int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  const int v = e ? std::atoi(e) : 0;
+  return v > 0 ? v : dflt;
+}
+static const int kStatsBlocksPerCu = env_int("APEX_BN_STATS_BPC", 4);
+static const int kBwdBlocksPerCu = env_int("APEX_BN_BWD_BPC", 2);
+
+inline Geo geo(int64_t m, int c, int cus, int blocks_per_cu = kBwdBlocksPerCu) {
   Geo g;
   const int cv = c / 8;
   g.tx = cv < 64 ? cv : 64;
@@ -45,7 +58,7 @@ inline Geo geo(int64_t m, int c, int cus) {
   if (g.ty > 32) g.ty = 32;
   g.gx = (cv + g.tx - 1) / g.tx;
   const int64_t rows_per_iter = (int64_t)g.ty * kU;
-  int64_t gy = ((int64_t)cus * 2 + g.gx - 1) / g.gx;
+  int64_t gy = ((int64_t)cus * blocks_per_cu + g.gx - 1) / g.gx;
   const int64_t cap = (m + rows_per_iter - 1) / rows_per_iter;
   if (gy > cap) gy = cap;
   if (gy > 1024) gy = 1024;
@@ -487,7 +500,8 @@ inline void check_shape(int64_t m, int c) {
 
 int bn_nhwc_plan(int64_t m, int c, int cus, int64_t* ws_floats) {
   const bnh::Geo g = bnh::geo(m, c, cus);
-  if (ws_floats) *ws_floats = 2 * (int64_t)g.gy * c;
+  const bnh::Geo gs = bnh::geo(m, c, cus, bnh::kStatsBlocksPerCu);
+  if (ws_floats) *ws_floats = 2 * (int64_t)(g.gy > gs.gy ? g.gy : gs.gy) * c;
   return g.gy;
 }
 
@@ -495,8 +509,8 @@ void bn_nhwc_stats(const void* x, int x_t, int64_t m, int c, const float* w, con
                    float* running_mean, float* running_var, float* save_mean, float* save_invstd, float* coef_fwd,
                    float* ws, int gy, int cus, hipStream_t s) {
   bnh::check_shape(m, c);
-  bnh::Geo g = bnh::geo(m, c, cus);
-  g.gy = gy;
+  (void)gy;  // the statistics pass has its own (deeper) geometry; ws is sized for it by bn_nhwc_plan
+  const bnh::Geo g = bnh::geo(m, c, cus, bnh::kStatsBlocksPerCu);
   const size_t lds = (size_t)2 * g.ty * g.tx * 8 * sizeof(float);
   dispatch_float(x_t, [&](auto tag) {
     using T = typename decltype(tag)::type;
@@ -510,8 +524,8 @@ void bn_nhwc_stats(const void* x, int x_t, int64_t m, int c, const float* w, con
 void bn_nhwc_stats_local(const void* x, int x_t, int64_t m, int c, float* payload, float* ws, int gy, int cus,
                          hipStream_t s) {
   bnh::check_shape(m, c);
-  bnh::Geo g = bnh::geo(m, c, cus);
-  g.gy = gy;
+  (void)gy;
+  const bnh::Geo g = bnh::geo(m, c, cus, bnh::kStatsBlocksPerCu);
   const size_t lds = (size_t)2 * g.ty * g.tx * 8 * sizeof(float);
   dispatch_float(x_t, [&](auto tag) {
     using T = typename decltype(tag)::type;

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Fused NHWC BN passes at the ResNet-50 (bs 256) shapes: time and effective HBM GB/s of the
 forward (stats + apply) and backward (reduce + apply) of ``_C.bn_nhwc``, one JSON line per case.
-Tuning knobs (APEX_BN_BLOCKS_PER_CU, APEX_BN_BWD_ROWS) are read from the environment.
+Tuning knobs (APEX_BN_STATS_BPC, APEX_BN_BWD_BPC: workgroups per CU of the partial passes) are read from the environment.
 Run on the GPU box: python tools/bn_bench.py"""
 import json
 import os
@@ -34,7 +34,7 @@ def main():
     # output forks into two consumers (two incoming gradients, grad_z needed)
     cases = [(112, 64, "relu"), (56, 64, "relu"), (56, 256, "zrelu2"), (56, 256, "plain"), (28, 128, "relu"),
              (28, 512, "zrelu2"), (14, 256, "relu"), (14, 1024, "zrelu2"), (7, 512, "relu"), (7, 2048, "zrelu2")]
-    knobs = {k: os.environ.get(k) for k in ("APEX_BN_BLOCKS_PER_CU", "APEX_BN_BWD_ROWS")}
+    knobs = {k: os.environ.get(k) for k in ("APEX_BN_STATS_BPC", "APEX_BN_BWD_BPC")}
     tot_f = tot_b = 0.0
     for hw, c, kind in cases:
         m = 256 * hw * hw
