@@ -107,30 +107,62 @@ def disable_casts():
             h._is_active = prev
 
 
-class AmpHandle(object):
-    """Legacy handle (reference apex/amp/handle.py:170-251).  Holds the O1 cast cache."""
+class NoOpHandle(object):
+    """Legacy handle when amp is disabled: casts inactive, loss passed through unscaled."""
+
+    has_cache = False
+    verbose = False
+
+    def is_active(self):
+        return False
+
+    @contextlib.contextmanager
+    def _disable_casts(self):
+        yield
+
+    def wrap_optimizer(self, optimizer, num_loss=1):
+        return OptimWrapper(optimizer, self, num_loss)
+
+    @contextlib.contextmanager
+    def scale_loss(self, loss, optimizer):
+        yield loss
+
+    def _clear_cache(self):
+        pass
+
+    def _deactivate(self):
+        pass
+
+
+class AmpHandle(NoOpHandle):
+    """Legacy handle (reference apex/amp/handle.py:170-251): owns the O1 weight-cast cache, the
+    default loss scaler and the list of patched functions (uninstalled by ``_deactivate``)."""
 
     def __init__(self, loss_scale="dynamic", enable_caching=True, verbose=False):
         self._enable_caching = enable_caching
         self._verbose = verbose
-        self._cache = dict()
+        self._cache = {}
         self._default_scaler = LossScaler(loss_scale)
         self._is_active = True
         self._all_wrappers = []
+
+    has_cache = property(lambda self: self._enable_caching)
+    cache = property(lambda self: self._cache)
+    verbose = property(lambda self: self._verbose)
 
     def is_active(self):
         return self._is_active
 
     @contextlib.contextmanager
     def _disable_casts(self):
-        self._is_active = False
+        prev, self._is_active = self._is_active, False
         try:
             yield
         finally:
-            self._is_active = True
+            self._is_active = prev
 
     def wrap_optimizer(self, optimizer, num_loss=1):
-        self._default_scaler = None
+        self._default_scaler = None  # scaling moves to the per-loss scalers of the wrapper
         return OptimWrapper(optimizer, self, num_loss)
 
     @contextlib.contextmanager
@@ -151,48 +183,6 @@ class AmpHandle(object):
         _amp._uninstall()
         self._all_wrappers = []
 
-    @property
-    def has_cache(self):
-        return self._enable_caching
-
-    @property
-    def cache(self):
-        return self._cache
-
     def remove_cache(self, param):
-        if self.has_cache and param in self.cache:
-            del self.cache[param]
-
-    @property
-    def verbose(self):
-        return self._verbose
-
-
-class NoOpHandle(object):
-    def is_active(self):
-        return False
-
-    @contextlib.contextmanager
-    def _disable_casts(self):
-        yield
-
-    def wrap_optimizer(self, optimizer, num_loss=1):
-        return OptimWrapper(optimizer, self, num_loss)
-
-    @contextlib.contextmanager
-    def scale_loss(self, loss, optimizer):
-        yield loss
-
-    @property
-    def has_cache(self):
-        return False
-
-    @property
-    def verbose(self):
-        return False
-
-    def _clear_cache(self):
-        pass
-
-    def _deactivate(self):
-        pass
+        if self._enable_caching:
+            self._cache.pop(param, None)

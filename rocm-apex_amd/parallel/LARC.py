@@ -1,26 +1,41 @@
-"""LARC optimizer wrapper (reference apex/parallel/LARC.py:5-107): layer-wise adaptive rate
-scaling with 'clip' (min with the global lr) or 'scale' mode; weight decay is absorbed into the
-adaptive rate and removed from the inner optimizer for the step."""
+"""LARC: layer-wise adaptive rate control around any optimizer (reference
+apex/parallel/LARC.py:5-107).
+
+Per parameter tensor p with gradient g (and the group's weight decay wd, which LARC absorbs —
+the wrapped optimizer steps with wd = 0):
+
+    ratio = trust_coefficient * ||p|| / (||g|| + wd * ||p|| + eps)
+    clip mode:  ratio = min(ratio / lr, 1)
+    g <- (g + wd * p) * ratio          (ratio = 1 where ||p|| or ||g|| is zero)
+
+MI355X form: all tensor norms of a dtype group come from ONE multi-tensor L2-norm launch per
+list (params, grads; ``amp_C.multi_tensor_l2norm`` per-tensor mode) and the update of every
+gradient is two foreach kernels with the ratios kept on the device — no per-parameter norm
+launches and no host synchronization.  Everything else (state, param_groups, state_dict, ...)
+is the wrapped optimizer's, by delegation."""
 import torch
-from torch.optim import Optimizer
+
+from .. import amp_C
 
 
 class LARC(object):
     def __init__(self, optimizer, trust_coefficient=0.02, clip=True, eps=1e-8):
         self.optim = optimizer
         self.trust_coefficient = trust_coefficient
-        self.eps = eps
         self.clip = clip
+        self.eps = eps
+
+    # ---- everything not LARC-specific is the wrapped optimizer's ----
+    def __getattr__(self, name):
+        if name == "optim":
+            raise AttributeError(name)
+        return getattr(self.optim, name)
 
     def __getstate__(self):
         return self.optim.__getstate__()
 
     def __setstate__(self, state):
         self.optim.__setstate__(state)
-
-    @property
-    def state(self):
-        return self.optim.state
 
     def __repr__(self):
         return self.optim.__repr__()
@@ -33,38 +48,50 @@ class LARC(object):
     def param_groups(self, value):
         self.optim.param_groups = value
 
-    def state_dict(self):
-        return self.optim.state_dict()
+    @property
+    def state(self):
+        return self.optim.state
 
-    def load_state_dict(self, state_dict):
-        self.optim.load_state_dict(state_dict)
+    # ---- the adaptive step ----
+    @staticmethod
+    def _norms(tensors):
+        if tensors[0].is_cuda:
+            flag = torch.zeros(1, dtype=torch.int32, device=tensors[0].device)
+            _, per = amp_C.multi_tensor_l2norm(65536, flag, [tensors], True)
+            return per.float()
+        return torch.stack([t.float().norm() for t in tensors])
 
-    def zero_grad(self):
-        self.optim.zero_grad()
+    def _scale_group(self, group, wd):
+        params = [p for p in group["params"] if p.grad is not None]
+        if not params:
+            return
+        by_dtype = {}
+        for p in params:
+            by_dtype.setdefault((p.dtype, p.grad.dtype, p.device), []).append(p)
+        for ps in by_dtype.values():
+            grads = [p.grad.data for p in ps]
+            pn = self._norms([p.data for p in ps])
+            gn = self._norms(grads)
+            ratio = self.trust_coefficient * pn / (gn + pn * wd + self.eps)
+            if self.clip:
+                ratio = torch.clamp(ratio / group["lr"], max=1.0)
+            live = (pn != 0) & (gn != 0)
+            ratio = torch.where(live, ratio, torch.ones_like(ratio)).to(grads[0].dtype)
+            if wd != 0:
+                wdv = (live.to(grads[0].dtype) * wd).unbind(0)
+                torch._foreach_add_(grads, torch._foreach_mul([p.data for p in ps], list(wdv)))
+            torch._foreach_mul_(grads, list(ratio.unbind(0)))
 
-    def add_param_group(self, param_group):
-        self.optim.add_param_group(param_group)
-
-    def step(self):
+    def step(self, closure=None):
+        saved = []
         with torch.no_grad():
-            weight_decays = []
             for group in self.optim.param_groups:
-                wd = group["weight_decay"] if "weight_decay" in group else 0
-                weight_decays.append(wd)
+                wd = group.get("weight_decay", 0)
+                saved.append(wd)
                 group["weight_decay"] = 0
-                for p in group["params"]:
-                    if p.grad is None:
-                        continue
-                    param_norm = torch.norm(p.data)
-                    grad_norm = torch.norm(p.grad.data)
-                    # adaptive lr computed on device (no host sync)
-                    adaptive_lr = self.trust_coefficient * param_norm / (grad_norm + param_norm * wd + self.eps)
-                    if self.clip:
-                        adaptive_lr = torch.minimum(adaptive_lr / group["lr"], torch.ones_like(adaptive_lr))
-                    ok = (param_norm != 0) & (grad_norm != 0)
-                    adaptive_lr = torch.where(ok, adaptive_lr, torch.ones_like(adaptive_lr))
-                    p.grad.data.add_(p.data * wd * ok.to(p.dtype))
-                    p.grad.data.mul_(adaptive_lr.to(p.grad.dtype))
-        self.optim.step()
-        for i, group in enumerate(self.optim.param_groups):
-            group["weight_decay"] = weight_decays[i]
+                self._scale_group(group, wd)
+        try:
+            return self.optim.step(closure) if closure is not None else self.optim.step()
+        finally:
+            for group, wd in zip(self.optim.param_groups, saved):
+                group["weight_decay"] = wd
