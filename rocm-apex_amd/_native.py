@@ -5,6 +5,7 @@ and a GPU op is requested we raise (no silent eager fallback); CPU tensors use t
 reference implementations in :mod:`apex.ops` (that is what the CPU test tier exercises).
 Set ``APEX_AMD_ALLOW_FALLBACK=1`` to permit the torch path on GPU for debugging.
 """
+import contextlib
 import importlib
 import os
 
@@ -37,8 +38,26 @@ def submodule(name: str):
     return getattr(_C, name, None)
 
 
+_force_reference = False
+
+
+@contextlib.contextmanager
+def reference_mode(enabled=True):
+    """Route GPU tensors through the torch reference implementations (``apex.ops``) inside the
+    block.  Parity harness only: tests run one training loop on the HIP kernels and once more
+    on the reference ops on the same device and bound the difference."""
+    global _force_reference
+    prev, _force_reference = _force_reference, bool(enabled)
+    try:
+        yield
+    finally:
+        _force_reference = prev
+
+
 def use_native(*tensors) -> bool:
     """True when the op must run on the HIP path (any GPU tensor among the inputs)."""
+    if _force_reference:
+        return False
     for t in tensors:
         if t is not None and getattr(t, "is_cuda", False):
             if _C is None and ALLOW_FALLBACK:

@@ -1,0 +1,502 @@
+"""amp behaviour matrix (reference tests/L0/run_amp/test_checkpointing.py:73-223,
+test_multiple_models_optimizers_losses.py, test_add_param_group.py, test_fused_sgd.py and
+tests/L0/run_optimizers/test_fused_novograd.py).
+
+* checkpoint / restore across every (opt_level, restore_opt_level) pair, with amp initialised
+  before or after the load and one or two losses.  Same-level pairs must continue training in
+  lock-step with the uninterrupted model (the reference skips this test; it runs here);
+  cross-level pairs must load, keep an fp32 state_dict and keep training.
+* forced overflow: each dynamic scaler is halved exactly once per skipped step and reports
+  ``unskipped == 0`` through ``amp.state_dict()``; ``amp.load_state_dict`` restores it.
+* several models / optimizers / losses with an inf injected into one backward at one
+  iteration: that step (only) is skipped, unskipped steps see exactly the fp32 reference
+  gradients and the final weights match the fp32 reference run.  The same matrix runs with
+  ``FusedSGD`` (the amp hooks that hand the unscale to the optimizer).
+* ``add_param_group`` in the middle of amp training.
+* FusedNovoGrad against an in-test NovoGrad.
+* GPU: one small conv/BN/linear training loop run on the HIP kernels and again on the torch
+  reference ops on the same device (``apex._native.reference_mode``): per-step losses and the
+  final weights must agree to a few ulps.
+
+The models of the multi-loss tests keep every quantity dyadic (integer inputs, power-of-two
+learning rates and loss scales), so the fp32 reference and the mixed-precision runs agree
+exactly and the comparisons are ``torch.equal``."""
+import itertools
+
+import pytest
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from apex import _native, amp
+from apex.amp._amp_state import _amp_state
+from apex.optimizers import FusedAdam, FusedNovoGrad, FusedSGD
+
+LEVELS = ("O0", "O1", "O2", "O3", "O4", "O5")
+GPU = pytest.param("cuda", marks=pytest.mark.gpu)
+
+
+def _reset():
+    _amp_state.loss_scalers = []
+    _amp_state.allow_incoming_model_not_fp32 = False
+    h = getattr(_amp_state, "handle", None)
+    if h is not None:
+        h._deactivate()
+        _amp_state.handle = None
+
+
+@pytest.fixture(autouse=True)
+def _clean():
+    _reset()
+    yield
+    _reset()
+
+
+def _low(level):
+    return torch.bfloat16 if level in ("O4", "O5") else torch.float16
+
+
+# ====================================================================== checkpoint / restore
+class ConvBN(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.conv = nn.Conv2d(3, 6, 3, 1, 1)
+        self.bn = nn.BatchNorm2d(6)
+        self.gain = nn.Parameter(torch.randn(1))
+
+    def forward(self, x):
+        return self.bn(F.relu(self.conv(x * self.gain)))
+
+
+def _train_step(model, opt, x, loss_ids):
+    opt.zero_grad()
+    out = model(x)
+    for i in loss_ids:
+        with amp.scale_loss(out.float().mean(), opt, loss_id=i) as scaled:
+            scaled.backward(retain_graph=True)
+    opt.step()
+    return out
+
+
+def _assert_fp32_state(sd):
+    for k, v in sd.items():
+        if "num_batches_tracked" not in k:
+            assert v.dtype == torch.float32, k
+
+
+def _build(level, num_losses, dev, load=None, amp_first=True):
+    model = ConvBN().to(dev)
+    opt = torch.optim.SGD(model.parameters(), lr=1e-3)
+    if amp_first:
+        model, opt = amp.initialize(model, opt, opt_level=level, num_losses=num_losses, verbosity=0)
+    if load is not None:
+        model.load_state_dict(load["model"])
+        opt.load_state_dict(load["optimizer"])
+    if not amp_first:
+        model, opt = amp.initialize(model, opt, opt_level=level, num_losses=num_losses, verbosity=0)
+    return model, opt
+
+
+@pytest.mark.parametrize("dev", ["cpu", GPU])
+@pytest.mark.parametrize("num_losses", [1, 2])
+@pytest.mark.parametrize("amp_first", [True, False])
+@pytest.mark.parametrize("level", LEVELS)
+def test_restore_same_level_continues_in_lockstep(level, amp_first, num_losses, dev):
+    steps, cut = 8, 4
+    torch.manual_seed(2809)
+    # 2*num_losses scalers: ids [0, n) drive the original model, [n, 2n) the restored one
+    model, opt = _build(level, 2 * num_losses, dev)
+    restored = None
+    for step in range(steps):
+        x = torch.randn(8, 3, 12, 12, device=dev)
+        out = _train_step(model, opt, x, range(num_losses))
+        if step == cut - 1:
+            ckpt = {"model": model.state_dict(), "optimizer": opt.state_dict()}
+            _assert_fp32_state(ckpt["model"])
+            restored, ropt = _build(level, 2 * num_losses, dev, load=ckpt, amp_first=amp_first)
+        elif step >= cut:
+            rout = _train_step(restored, ropt, x, range(num_losses, 2 * num_losses))
+            mine, theirs = model.state_dict(), restored.state_dict()
+            assert mine.keys() == theirs.keys()
+            if amp._amp_state.opt_properties.master_weights:
+                # the checkpoint holds the model's low-precision weights (not the fp32 masters,
+                # as in the reference), so the two runs may drift by rounding of the masters
+                tol = dict(rtol=2e-2, atol=2e-2) if _low(level) == torch.bfloat16 else dict(rtol=2e-3, atol=2e-3)
+                torch.testing.assert_close(out.float(), rout.float(), **tol)
+                for k in mine:
+                    torch.testing.assert_close(mine[k], theirs[k], **tol)
+            else:
+                assert torch.equal(out.float(), rout.float())
+                for k in mine:
+                    assert torch.equal(mine[k], theirs[k]), k
+
+
+@pytest.mark.parametrize("amp_first", [True, False])
+@pytest.mark.parametrize("level,restore_level",
+                         [p for p in itertools.product(LEVELS, LEVELS) if p[0] != p[1]])
+def test_restore_cross_level(level, restore_level, amp_first):
+    torch.manual_seed(7)
+    model, opt = _build(level, 1, "cpu")
+    x = torch.randn(8, 3, 12, 12)
+    for _ in range(3):
+        _train_step(model, opt, x, [0])
+    ckpt = {"model": model.state_dict(), "optimizer": opt.state_dict()}
+    _assert_fp32_state(ckpt["model"])
+    _reset()
+    restored, ropt = _build(restore_level, 1, "cpu", load=ckpt, amp_first=amp_first)
+    sd = restored.state_dict()
+    _assert_fp32_state(sd)
+    # restore-level storage rounding is the only allowed difference
+    tol = dict(rtol=1e-2, atol=1e-2) if restore_level in ("O3", "O4", "O5") else dict(rtol=1e-3, atol=1e-3)
+    for k, v in ckpt["model"].items():
+        torch.testing.assert_close(sd[k].float(), v.float(), **tol)
+    before = {k: v.clone() for k, v in sd.items()}
+    for _ in range(2):
+        out = _train_step(restored, ropt, x, [0])
+        assert torch.isfinite(out.float()).all()
+    after = restored.state_dict()
+    assert not torch.equal(after["bn.bias"], before["bn.bias"])  # d mean(bn(.)) only reaches the shift
+
+
+@pytest.mark.parametrize("dev", ["cpu", GPU])
+@pytest.mark.parametrize("level", ["O1", "O2"])  # the dynamic-scale presets
+def test_forced_overflow_halves_each_scaler(level, dev):
+    """Loss ``idx`` overflows ``idx`` times (input scaled by 2**17 saturates fp16)."""
+    torch.manual_seed(0)
+    num_losses, decreases = 3, [0, 1, 2]
+    model = ConvBN().to(dev)
+    opt = torch.optim.SGD(model.parameters(), lr=1e-3)
+    model, opt = amp.initialize(model, opt, opt_level=level, num_losses=num_losses, verbosity=0)
+    assert _amp_state.opt_properties.loss_scale == "dynamic"
+    init = [s.loss_scale() for s in _amp_state.loss_scalers]
+    w0 = model.conv.weight.detach().clone()
+    x = torch.randn(8, 3, 12, 12, device=dev)
+    for idx in range(num_losses):
+        for _ in range(decreases[idx]):
+            opt.zero_grad()
+            out = model(x * 2 ** 17)
+            with amp.scale_loss(out.float().mean(), opt, loss_id=idx) as scaled:
+                scaled.backward(retain_graph=True)
+            opt.step()
+    assert torch.equal(model.conv.weight.detach(), w0)  # every step was skipped
+    sd = amp.state_dict()
+    assert list(sd.keys()) == ["loss_scaler%d" % i for i in range(num_losses)]
+    for i, (k, d, s0) in enumerate(zip(sd, decreases, init)):
+        assert _amp_state.loss_scalers[i].loss_scale() == s0 / 2 ** d
+        assert sd[k]["loss_scale"] == s0 / 2 ** d
+        assert sd[k]["unskipped"] == 0
+    # a clean step counts as unskipped and the state round-trips through load_state_dict
+    opt.zero_grad()
+    with amp.scale_loss(model(x).float().mean(), opt, loss_id=2) as scaled:
+        scaled.backward()
+    opt.step()
+    sd = amp.state_dict()
+    assert sd["loss_scaler2"]["unskipped"] == 1
+    for s in _amp_state.loss_scalers:
+        s._loss_scale, s._unskipped = 123.0, 7
+        s._state = None if dev == "cpu" else s._state
+    amp.load_state_dict(sd)
+    assert [s.loss_scale() for s in _amp_state.loss_scalers] == [sd[k]["loss_scale"] for k in sd]
+    assert amp.state_dict()["loss_scaler2"]["unskipped"] == 1
+
+
+# ====================================================================== multiple models / losses
+class Dyadic(nn.Module):
+    """loss = sum(x * w0 * w1); fp32 ``w0`` and a low-precision ``w1`` (integers, exact)."""
+
+    def __init__(self, unique, low, dev):
+        super().__init__()
+        self.w0 = nn.Parameter(unique + torch.arange(2, device=dev, dtype=torch.float32))
+        self.w1 = nn.Parameter(1.0 + unique + torch.arange(2, device=dev, dtype=low))
+
+    def forward(self, x):
+        return (x * self.w0.float() * self.w1.float()).sum()
+
+
+LR = (0.25, 0.5, 0.125)
+# loss k = sum of the listed models
+LAYOUTS = {"2m2l": [[0], [1]], "3m2l": [[0, 2], [1, 2]], "2m3l": [[0], [1], [0, 1]]}
+
+
+def _make_opts(models, opt_cls, per_model):
+    kw = dict(momentum=0.125)
+    if per_model:
+        return [opt_cls([{"params": m.parameters(), "lr": LR[i]}], **kw) for i, m in enumerate(models)]
+    return [opt_cls([{"params": m.parameters(), "lr": LR[i]} for i, m in enumerate(models)], **kw)]
+
+
+def _zero(models, opts, how):
+    if how == "none":
+        for m in models:
+            for p in m.parameters():
+                p.grad = None
+    elif how == "model":
+        for m in models:
+            m.zero_grad()
+    else:
+        for o in opts:
+            o.zero_grad()
+
+
+def _losses_opts(layout, opts, per_model):
+    """Which optimizers each loss's ``scale_loss`` is told about."""
+    if not per_model:
+        return [opts] * len(layout)
+    return [[opts[m] for m in ms] for ms in layout]
+
+
+def _opt_params(o):
+    return [p for g in o.param_groups for p in g["params"]]
+
+
+def _reference(layout, low, dev, per_model, iters, skip=None):
+    """fp32-semantics run with torch SGD; ``skip`` = (iteration, indices of the optimizers that
+    do not step then).  Returns per-iteration, per-optimizer grads and the final weights."""
+    n = 1 + max(max(ms) for ms in layout)
+    models = [Dyadic(i + 1, low, dev) for i in range(n)]
+    opts = _make_opts(models, torch.optim.SGD, per_model)
+    x = torch.ones(2, device=dev)
+    grads = []
+    for it in range(iters):
+        _zero(models, opts, "optimizer")
+        for ms in layout:
+            sum(models[m](x) for m in ms).backward()
+        grads.append([[p.grad.detach().float().clone() for p in _opt_params(o)] for o in opts])
+        for j, o in enumerate(opts):
+            if skip is None or it != skip[0] or j not in skip[1]:
+                o.step()
+    return grads, [p.detach().float().clone() for m in models for p in m.parameters()]
+
+
+def _amp_run(level, layout, opt_cls, per_model, how, multi_scalers, inject, skipped, ref_grads, dev):
+    """One amp run; ``inject`` = (iteration, loss index, 'w0'|'w1') or None; ``skipped`` = the
+    optimizer indices that must skip at the injected iteration."""
+    low = _low(level)
+    n = 1 + max(max(ms) for ms in layout)
+    models = [Dyadic(i + 1, low, dev) for i in range(n)]
+    opts = _make_opts(models, opt_cls, per_model)
+    _amp_state.allow_incoming_model_not_fp32 = True
+    models, opts = amp.initialize(models, opts, opt_level=level, verbosity=0, cast_model_type=False,
+                                  num_losses=len(layout) if multi_scalers else 1)
+    _amp_state.allow_incoming_model_not_fp32 = False
+    for i, s in enumerate(_amp_state.loss_scalers):
+        s._loss_scale = 4.0 * 4 ** i
+    x = torch.ones(2, device=dev)
+    loss_opts = _losses_opts(layout, opts, per_model)
+    # FusedSGD with master weights unscales inside its kernel: the fp32 grads never materialise
+    check_grads = opt_cls is torch.optim.SGD or not _amp_state.opt_properties.master_weights
+    for it in range(len(ref_grads)):
+        _zero(models, opts, how)
+        for k, ms in enumerate(layout):
+            loss = sum(models[m](x) for m in ms)
+            lo = loss_opts[k] if len(loss_opts[k]) > 1 else loss_opts[k][0]
+            with amp.scale_loss(loss, lo, loss_id=k if multi_scalers else 0) as scaled:
+                scaled.backward()
+                if inject and it == inject[0] and k == inject[1]:
+                    getattr(models[layout[k][0]], inject[2]).grad[0] = float("inf")
+        for j, o in enumerate(opts):
+            if check_grads and not (inject and it == inject[0] and j in skipped):
+                for p, g in zip(amp.master_params(o), ref_grads[it][j]):
+                    assert torch.equal(p.grad.float(), g), (it, j, p.grad, g)
+        for o in opts:
+            o.step()
+    flat = [p for m in models for p in m.parameters()]
+    masters = [p for o in opts for p in amp.master_params(o)]
+    return flat, masters
+
+
+def _matrix(level, layout_name, opt_cls, per_model, dev):
+    layout = LAYOUTS[layout_name]
+    low = _low(level)
+    injects = [None]
+    if level in ("O1", "O2"):  # dynamic scalers
+        injects += [(it, k, w) for it in (0, 1) for k in range(len(layout)) for w in ("w0", "w1")]
+    refs = {}
+    for how, multi, inj in itertools.product(("none", "model", "optimizer"), (True, False), injects):
+        skipped = () if inj is None else (tuple(layout[inj[1]]) if per_model else (0,))
+        key = None if inj is None else (inj[0], skipped)
+        if key not in refs:
+            refs[key] = _reference(layout, low, dev, per_model, 2 if inj is None else 3, key)
+        ref_grads, ref_final = refs[key]
+        _reset()
+        flat, masters = _amp_run(level, layout, opt_cls, per_model, how, multi, inj, skipped, ref_grads, dev)
+        ctx = (level, layout_name, how, multi, inj)
+        for p, r in zip(flat, ref_final):
+            assert torch.equal(p.detach().float(), r), (ctx, p, r)
+        for p, m in zip(flat, masters):
+            assert torch.equal(p.detach(), m.detach().to(p.dtype)), ctx
+
+
+@pytest.mark.parametrize("dev", ["cpu", GPU])
+@pytest.mark.parametrize("layout_name,per_model", [("2m2l", False), ("3m2l", False), ("2m3l", False),
+                                                   ("2m2l", True)])
+@pytest.mark.parametrize("level", LEVELS)
+def test_multiple_models_optimizers_losses(level, layout_name, per_model, dev):
+    _matrix(level, layout_name, torch.optim.SGD, per_model, dev)
+
+
+@pytest.mark.parametrize("dev", ["cpu", GPU])
+@pytest.mark.parametrize("layout_name,per_model", [("2m2l", False), ("2m2l", True), ("3m2l", False)])
+@pytest.mark.parametrize("level", LEVELS)
+def test_fused_sgd_matrix(level, layout_name, per_model, dev):
+    _matrix(level, layout_name, FusedSGD, per_model, dev)
+
+
+# ====================================================================== add_param_group
+@pytest.mark.parametrize("dev", ["cpu", GPU])
+@pytest.mark.parametrize("level", LEVELS)
+def test_add_param_group_mid_training(level, dev):
+    low = _low(level)
+    x = torch.ones(2, device=dev)
+
+    def run(use_amp, zero_before_add, accumulate, how):
+        m0, m1 = Dyadic(1, low, dev), Dyadic(2, low, dev)
+        opt = torch.optim.SGD([{"params": m0.parameters(), "lr": 0.25}], momentum=0.125)
+        if use_amp:
+            _amp_state.allow_incoming_model_not_fp32 = True
+            (m0, m1), opt = amp.initialize([m0, m1], opt, opt_level=level, verbosity=0, cast_model_type=False)
+            _amp_state.allow_incoming_model_not_fp32 = False
+            _amp_state.loss_scalers[0]._loss_scale = 4.0
+
+        def backward(loss, retain=False):
+            if use_amp:
+                with amp.scale_loss(loss, opt) as scaled:
+                    scaled.backward(retain_graph=retain)
+            else:
+                loss.backward(retain_graph=retain)
+
+        _zero([m0, m1], [opt], how)
+        backward(m0(x))
+        opt.step()
+        if zero_before_add:
+            _zero([m0, m1], [opt], how)
+        opt.add_param_group({"params": m1.parameters(), "lr": 0.5})
+        if not zero_before_add:
+            _zero([m0, m1], [opt], how)
+        for step in range(2):  # twice: the new group must pick up momentum
+            if step:
+                _zero([m0, m1], [opt], how)
+            loss = m0(x) + m1(x)
+            backward(loss, retain=accumulate)
+            if accumulate:
+                backward(loss)
+            opt.step()
+        return [p.detach().float().clone() for m in (m0, m1) for p in m.parameters()]
+
+    for zero_before_add, accumulate in itertools.product((True, False), (True, False)):
+        ref = run(False, zero_before_add, accumulate, "optimizer")
+        for how in ("none", "model", "optimizer"):
+            _reset()
+            got = run(True, zero_before_add, accumulate, how)
+            for a, b in zip(got, ref):
+                assert torch.equal(a, b), (level, zero_before_add, accumulate, how, a, b)
+
+
+# ====================================================================== FusedNovoGrad
+class RefNovoGrad(torch.optim.Optimizer):
+    """Layer-wise NovoGrad: the second moment is one scalar per tensor, an EMA of the squared
+    grad norm seeded with the first step's value; the step is normalised by its square root."""
+
+    def __init__(self, params, lr, betas, eps, weight_decay, grad_averaging):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
+                                      grad_averaging=grad_averaging))
+
+    @torch.no_grad()
+    def step(self):
+        for group in self.param_groups:
+            b1, b2 = group["betas"]
+            for p in group["params"]:
+                g = p.grad.float()
+                st = self.state[p]
+                sq = float((g * g).sum())
+                if not st:
+                    st["m"] = torch.zeros_like(p, dtype=torch.float32)
+                    st["v"] = sq
+                else:
+                    st["v"] = b2 * st["v"] + (1 - b2) * sq
+                g = g / (st["v"] ** 0.5 + group["eps"])
+                if group["weight_decay"]:
+                    g = g + group["weight_decay"] * p.float()
+                if group["grad_averaging"]:
+                    g = g * (1 - b1)
+                st["m"].mul_(b1).add_(g)
+                p.copy_(p.float() - group["lr"] * st["m"])
+
+
+@pytest.mark.parametrize("dev", ["cpu", GPU])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("betas,wd,avg", [((0.95, 0.0), 0.0, False), ((0.9, 0.98), 0.01, True)])
+def test_fused_novograd_matches_reference(betas, wd, avg, dtype, dev):
+    torch.manual_seed(3)
+    sizes = [(64, 32), (64,), (33, 7), (1,)]
+    base = [torch.rand(s, device=dev) for s in sizes]
+    ref_p = [nn.Parameter(t.clone().to(dtype)) for t in base]
+    tst_p = [nn.Parameter(t.clone().to(dtype)) for t in base]
+    ref = RefNovoGrad(ref_p, lr=1e-3, betas=betas, eps=1e-8, weight_decay=wd, grad_averaging=avg)
+    tst = FusedNovoGrad(tst_p, lr=1e-3, betas=betas, eps=1e-8, weight_decay=wd, grad_averaging=avg,
+                        bias_correction=False, reg_inside_moment=True, norm_type=2, init_zero=False)
+    tol = {torch.float32: 1e-5, torch.float16: 2e-3, torch.bfloat16: 1.6e-2}[dtype]
+    for _ in range(7):
+        for a, b in zip(ref_p, tst_p):
+            g = torch.randn_like(a, dtype=torch.float32)
+            a.grad, b.grad = g.to(dtype), g.to(dtype).clone()
+        ref.step()
+        tst.step()
+        for a, b in zip(ref_p, tst_p):
+            torch.testing.assert_close(b.float(), a.float(), rtol=tol, atol=tol)
+
+
+# ====================================================================== HIP vs reference ops (GPU)
+class SmallNet(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.c1 = nn.Conv2d(3, 16, 3, padding=1, bias=False)
+        self.b1 = nn.BatchNorm2d(16)
+        self.c2 = nn.Conv2d(16, 32, 3, stride=2, padding=1, bias=False)
+        self.b2 = nn.BatchNorm2d(32)
+        self.c3 = nn.Conv2d(32, 32, 3, padding=1, bias=False)
+        self.b3 = nn.BatchNorm2d(32)
+        self.fc = nn.Linear(32, 10)
+
+    def forward(self, x):
+        y = F.relu(self.b1(self.c1(x)))
+        y = F.relu(self.b2(self.c2(y)))
+        y = F.relu(self.b3(self.c3(y)) + y)
+        return self.fc(y.mean((2, 3)))
+
+
+def _parity_run(level, opt_name, reference, steps=6):
+    _reset()
+    torch.manual_seed(11)
+    model = SmallNet().cuda().to(memory_format=torch.channels_last)
+    opt = (FusedAdam(model.parameters(), lr=1e-3, weight_decay=0.01) if opt_name == "adam"
+           else FusedSGD(model.parameters(), lr=0.05, momentum=0.9))
+    model, opt = amp.initialize(model, opt, opt_level=level, verbosity=0)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    losses = []
+    with _native.reference_mode(reference):
+        for _ in range(steps):
+            x = torch.randn(16, 3, 16, 16, device="cuda", generator=g).to(memory_format=torch.channels_last)
+            t = torch.randint(0, 10, (16,), device="cuda", generator=g)
+            opt.zero_grad()
+            loss = F.cross_entropy(model(x).float(), t)
+            with amp.scale_loss(loss, opt) as scaled:
+                scaled.backward()
+            opt.step()
+            losses.append(loss.detach().float())
+    torch.cuda.synchronize()
+    return torch.stack(losses).cpu(), [p.detach().float().cpu() for p in amp.master_params(opt)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt_name", ["adam", "sgd"])
+@pytest.mark.parametrize("level", ["O1", "O2", "O5"])
+def test_hip_path_matches_reference_ops_gpu(level, opt_name):
+    torch.backends.cudnn.deterministic = True
+    hip_losses, hip_params = _parity_run(level, opt_name, reference=False)
+    ref_losses, ref_params = _parity_run(level, opt_name, reference=True)
+    # step 0 runs before any optimizer update: bitwise
+    assert torch.equal(hip_losses[0], ref_losses[0])
+    torch.testing.assert_close(hip_losses, ref_losses, rtol=1e-3, atol=1e-4)
+    for a, b in zip(hip_params, ref_params):
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4)
