@@ -393,6 +393,19 @@ def _process_optimizer(optimizer, properties):
 
     optimizer._amp_lazy_init = types.MethodType(_amp_lazy_init, optimizer)
 
+    # sync-free skip flags of the scale_loss exits feeding one step are OR-ed (handle.py);
+    # the step closes that window
+    stash.exits_since_step = 0
+    step_before_count = optimizer.step
+
+    def counted_step(self, *args, **kwargs):
+        try:
+            return step_before_count(*args, **kwargs)
+        finally:
+            self._amp_stash.exits_since_step = 0
+
+    optimizer.step = types.MethodType(counted_step, optimizer)
+
     old_add_param_group = optimizer.add_param_group
 
     def new_add_param_group(self, new_group):

@@ -38,59 +38,74 @@ def _patch_skip_step(opt, loss_scaler, loss_id):
     opt._amp_stash.already_patched = True
 
 
+def _passthrough(scaler):
+    """Nothing to scale or unscale: no master weights and a static scale of 1."""
+    props = _amp_state.opt_properties
+    return (not props.master_weights) and (not scaler.dynamic) and scaler.loss_scale() == 1.0
+
+
+def _finish_backward(optimizers, scaler, loss_id, delay_overflow_check):
+    """Unscale into the master grads, update the scale and arm the skip (device flag in
+    sync-free mode, patched ``step`` otherwise)."""
+    scaler.clear_overflow_state()
+    for opt in optimizers:
+        opt._post_amp_backward(scaler)
+        opt._amp_stash.params_have_scaled_gradients = False
+    if scaler.sync_free:
+        scaler.detach_waiting_holders()
+    skip = scaler.update_scale() if not delay_overflow_check else False
+    if scaler.sync_free:
+        for opt in optimizers:
+            st = opt._amp_stash
+            # several backward passes may feed one step (several losses / scalers): the step
+            # must skip if any of them overflowed, so the device flags are OR-ed until it runs
+            if st.skip_flag is None or st.exits_since_step == 0:
+                st.skip_flag = scaler.skip_flag
+            else:
+                st.skip_flag = torch.maximum(st.skip_flag, scaler.skip_flag)
+            st.exits_since_step += 1
+            st.inv_scale = scaler.inv_scale_used
+            scaler.add_holder(st)
+        return
+    if skip:
+        for opt in (o for o in optimizers if not o._amp_stash.already_patched):
+            _patch_skip_step(opt, scaler, loss_id)
+
+
 @contextlib.contextmanager
 def scale_loss(loss, optimizers, loss_id=0, model=None, delay_unscale=False, delay_overflow_check=False):
     """Yields ``loss.float() * loss_scale``; on exit (unless ``delay_unscale``) checks the grads
     for inf/NaN, unscales them into the master grads and updates the loss scale.
 
     ``model`` is accepted for API compatibility and unused (as in the reference)."""
-    if not hasattr(_amp_state, "opt_properties"):
+    props = getattr(_amp_state, "opt_properties", None)
+    if props is None:
         raise RuntimeError("Invoked 'with amp.scale_loss`, but internal Amp state has not been initialized.  "
                            "model, optimizer = amp.initialize(model, optimizer, opt_level=...) must be called "
                            "before `with amp.scale_loss`.")
-    if not _amp_state.opt_properties.enabled:
+    if not props.enabled:
         yield loss
         return
-
-    optimizers = _as_list(optimizers)
-    loss_scaler = _amp_state.loss_scalers[loss_id]
-
-    if ((not _amp_state.opt_properties.master_weights) and (not loss_scaler.dynamic)
-            and loss_scaler.loss_scale() == 1.0):
-        yield loss.float()
-        if _amp_state.opt_properties.patch_torch_functions:
+    opts = _as_list(optimizers)
+    scaler = _amp_state.loss_scalers[loss_id]
+    try:
+        if _passthrough(scaler):
+            yield loss.float()
+            return
+        if not delay_unscale:
+            for opt in (o for o in opts if not o._amp_stash.params_have_scaled_gradients):
+                opt._prepare_amp_backward()
+        if loss.is_cuda:
+            scaler._ensure(loss.device)
+        yield scaler.scale_loss_value(loss)
+        if delay_unscale:
+            for opt in opts:
+                opt._amp_stash.params_have_scaled_gradients = True
+        else:
+            _finish_backward(opts, scaler, loss_id, delay_overflow_check)
+    finally:
+        if props.patch_torch_functions:
             _amp_state.handle._clear_cache()
-        return
-
-    if not delay_unscale:
-        for optimizer in optimizers:
-            if not optimizer._amp_stash.params_have_scaled_gradients:
-                optimizer._prepare_amp_backward()
-
-    if loss.is_cuda:
-        loss_scaler._ensure(loss.device)
-    yield loss_scaler.scale_loss_value(loss)
-
-    if delay_unscale:
-        for optimizer in optimizers:
-            optimizer._amp_stash.params_have_scaled_gradients = True
-    else:
-        loss_scaler.clear_overflow_state()
-        for optimizer in optimizers:
-            optimizer._post_amp_backward(loss_scaler)
-            optimizer._amp_stash.params_have_scaled_gradients = False
-        should_skip = False if delay_overflow_check else loss_scaler.update_scale()
-        if loss_scaler.sync_free:
-            for optimizer in optimizers:
-                optimizer._amp_stash.skip_flag = loss_scaler.skip_flag
-                optimizer._amp_stash.inv_scale = loss_scaler.inv_scale_used
-        elif should_skip:
-            for optimizer in optimizers:
-                if not optimizer._amp_stash.already_patched:
-                    _patch_skip_step(optimizer, loss_scaler, loss_id)
-
-    if _amp_state.opt_properties.patch_torch_functions:
-        _amp_state.handle._clear_cache()
 
 
 @contextlib.contextmanager

@@ -65,6 +65,8 @@ class LossScaler(object):
         self._state = None        # float32[4]: scale, inv_scale_used, unskipped, skipped_total
         self._device_ahead = False
         self._seen_skips = 0
+        self._inv_view = None
+        self._holders = []        # optimizer stashes whose pending step reads our flag / inverse scale
         self.sync_free = False
 
     # ------------------------------------------------------------------ device buffers
@@ -76,6 +78,7 @@ class LossScaler(object):
             self._skip_flag = torch.zeros(1, dtype=torch.int32, device=device)
             self._state = torch.tensor([self._loss_scale, 1.0 / self._loss_scale, float(self._unskipped), 0.0],
                                        dtype=torch.float32, device=device)
+            self._inv_view = self._state[1:2]
             self._seen_skips = 0
         return self._overflow_buf
 
@@ -91,7 +94,24 @@ class LossScaler(object):
     @property
     def inv_scale_used(self):
         """Device float32[1]: 1/scale that the current gradients carry (sync-free mode)."""
-        return self._state[1:2]
+        return self._inv_view
+
+    def add_holder(self, stash):
+        if not any(h is stash for h in self._holders):
+            self._holders.append(stash)
+
+    def detach_waiting_holders(self):
+        """Before ``update_scale`` rewrites the flag / inverse scale in place: optimizers that
+        still wait for their step (another loss fed them through this scaler) get private
+        copies.  The single-loss loop never gets here with a waiting holder, so it copies
+        nothing."""
+        waiting = [h for h in self._holders if h.exits_since_step > 0]
+        for h in waiting:
+            if h.skip_flag is self._skip_flag:
+                h.skip_flag = self._skip_flag.clone()
+            if h.inv_scale is self._inv_view:
+                h.inv_scale = self._inv_view.clone()
+        self._holders = waiting
 
     def scale_tensor(self):
         return self._state[0:1]

@@ -342,6 +342,22 @@ def test_fused_sgd_matrix(level, layout_name, per_model, dev):
     _matrix(level, layout_name, FusedSGD, per_model, dev)
 
 
+@pytest.fixture
+def sync_free_on_cpu(monkeypatch):
+    """Run the device-flag (sync-free) scaler path on CPU tensors: the path the GPU takes with
+    the fused optimizers, whose skip flags must survive several losses per step."""
+    monkeypatch.setattr(_amp_state, "sync_free_force", True)
+    monkeypatch.setattr(_amp_state, "sync_free_requested", True)
+
+
+@pytest.mark.parametrize("layout_name,per_model", [("2m2l", False), ("2m2l", True), ("3m2l", False),
+                                                   ("2m3l", False)])
+@pytest.mark.parametrize("level", ["O1", "O2", "O5"])
+def test_fused_sgd_matrix_sync_free(level, layout_name, per_model, sync_free_on_cpu):
+    _matrix(level, layout_name, FusedSGD, per_model, "cpu")
+    assert _amp_state.sync_free
+
+
 # ====================================================================== add_param_group
 @pytest.mark.parametrize("dev", ["cpu", GPU])
 @pytest.mark.parametrize("level", LEVELS)
@@ -498,5 +514,11 @@ def test_hip_path_matches_reference_ops_gpu(level, opt_name):
     # step 0 runs before any optimizer update: bitwise
     assert torch.equal(hip_losses[0], ref_losses[0])
     torch.testing.assert_close(hip_losses, ref_losses, rtol=1e-3, atol=1e-4)
+    # Adam's normalised update m/sqrt(v) turns last-bit differences (fma contraction in the
+    # kernel) into up to ~lr differences for elements whose gradient is near eps: bound those to
+    # half a learning-rate step and require all but a sliver to agree to 1e-4
+    loose = 5e-4 if opt_name == "adam" else 1e-4
     for a, b in zip(hip_params, ref_params):
-        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4)
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=loose)
+        off = ((a - b).abs() > 1e-4 + 1e-3 * b.abs()).float().mean().item()
+        assert off < 0.01, off

@@ -9,7 +9,14 @@ ours are HIP/CDNA4-native already, so we drive ``hipcc`` directly:
 * link -> ``rocm-apex_amd/_C.<abi>.so`` IN-TREE (it travels to the GPU box with the repo snapshot)
 
 Incremental: an object is rebuilt when its source or any header under csrc/ is newer.
-Usage: ``python tools/build_native.py [-j N] [--clean] [--verbose]``
+
+Per-extension selection (the reference's ``setup.py --cpp_ext --cuda_ext --fast_layer_norm ...``
+flags, /root/reference/setup.py:87-555): ``--extensions norm,gemm`` or
+``APEX_AMD_EXTENSIONS=norm,gemm`` builds the always-on core (multi-tensor engine, amp_C) plus
+the named subsystems only; the Python side sees the others as absent (``apex._native.submodule``
+returns None and the op raises on a GPU tensor).  Names: see ``EXTENSIONS``.
+
+Usage: ``python tools/build_native.py [-j N] [--clean] [--verbose] [--extensions a,b] [--out PATH]``
 """
 from __future__ import annotations
 
@@ -29,7 +36,21 @@ BUILD = os.path.join(ROOT, "build", "native")
 ARCH = os.environ.get("APEX_AMD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-# optional subsystems: binding file -> macro that module.cpp keys on
+# optional subsystems: name -> (binding file, device source dirs under csrc/)
+EXTENSIONS = {
+    "norm": ("norm.cpp", ("norm",)),
+    "softmax": ("softmax.cpp", ("softmax",)),
+    "syncbn": ("syncbn.cpp", ("syncbn",)),
+    "gemm": ("gemm.cpp", ("gemm",)),
+    "xentropy": ("xentropy.cpp", ("xentropy",)),
+    "attn": ("attn.cpp", ("attn",)),
+    "bn_nhwc": ("bn_nhwc.cpp", ("groupbn",)),
+    "conv": ("conv.cpp", ("conv",)),
+    "contrib": ("contrib.cpp", ("comm", "pool", "transducer", "transformer")),
+}
+CORE_DIRS = ("mta",)
+
+# binding file -> macro that module.cpp keys on
 SUBSYSTEMS = {
     "norm.cpp": "APEX_AMD_WITH_NORM",
     "softmax.cpp": "APEX_AMD_WITH_SOFTMAX",
@@ -47,8 +68,8 @@ def ext_suffix() -> str:
     return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 
 
-def output_path() -> str:
-    return os.path.join(PKG, "_C" + ext_suffix())
+def output_path(out=None) -> str:
+    return out or os.environ.get("APEX_AMD_OUT") or os.path.join(PKG, "_C" + ext_suffix())
 
 
 def torch_paths():
@@ -60,14 +81,29 @@ def torch_paths():
     return tdir, inc, abi
 
 
-def sources():
+def selected_extensions(spec=None):
+    spec = spec if spec is not None else os.environ.get("APEX_AMD_EXTENSIONS", "all")
+    if spec in ("", "all"):
+        return sorted(EXTENSIONS)
+    names = sorted({n.strip() for n in spec.split(",") if n.strip()})
+    bad = [n for n in names if n not in EXTENSIONS]
+    if bad:
+        raise RuntimeError(f"unknown extension(s) {bad}; choose from {sorted(EXTENSIONS)}")
+    return names
+
+
+def sources(extensions=None):
+    names = selected_extensions(extensions)
+    dirs = set(CORE_DIRS) | {d for n in names for d in EXTENSIONS[n][1]}
+    skip_bind = {EXTENSIONS[n][0] for n in EXTENSIONS if n not in names}
     hip, cpp = [], []
     for d, _, files in os.walk(CSRC):
+        top = os.path.relpath(d, CSRC).split(os.sep)[0]
         for f in sorted(files):
             p = os.path.join(d, f)
-            if f.endswith(".hip"):
+            if f.endswith(".hip") and top in dirs:
                 hip.append(p)
-            elif f.endswith(".cpp") and os.sep + "bindings" + os.sep in p + os.sep:
+            elif f.endswith(".cpp") and top == "bindings" and f not in skip_bind:
                 cpp.append(p)
     return sorted(hip), sorted(cpp)
 
@@ -81,15 +117,15 @@ def newest_header() -> float:
     return t
 
 
-def obj_for(src: str) -> str:
+def obj_for(src: str, build_dir: str = BUILD) -> str:
     rel = os.path.relpath(src, CSRC).replace(os.sep, "__")
-    return os.path.join(BUILD, rel + ".o")
+    return os.path.join(build_dir, rel + ".o")
 
 
-def compile_cmds(verbose: bool):
+def compile_cmds(verbose: bool, extensions=None, out=None, build_dir=BUILD):
     tdir, tinc, abi = torch_paths()
     py_inc = sysconfig.get_paths()["include"]
-    hip, cpp = sources()
+    hip, cpp = sources(extensions)
     present = {os.path.basename(p) for p in cpp}
     macros = [f"-D{m}" for f, m in SUBSYSTEMS.items() if f in present]
     common = ["-std=c++17", "-O3", "-fPIC", f"-I{os.path.join(CSRC, 'include')}", "-Wno-unused-result",
@@ -101,11 +137,11 @@ def compile_cmds(verbose: bool):
             *[f"-isystem{p}" for p in tinc], f"-isystem{py_inc}", "-fvisibility=hidden"]
     jobs = []
     for s in hip:
-        jobs.append((s, [*dev, "-c", s, "-o", obj_for(s)]))
+        jobs.append((s, [*dev, "-c", s, "-o", obj_for(s, build_dir)]))
     for s in cpp:
-        jobs.append((s, [*host, "-c", s, "-o", obj_for(s)]))
-    link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", output_path(),
-            *[obj_for(s) for s, _ in jobs],
+        jobs.append((s, [*host, "-c", s, "-o", obj_for(s, build_dir)]))
+    link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", output_path(out),
+            *[obj_for(s, build_dir) for s, _ in jobs],
             f"-L{os.path.join(tdir, 'lib')}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
             "-ltorch_python", "-lamdhip64", f"-Wl,-rpath,{os.path.join(tdir, 'lib')}"]
     return jobs, link
@@ -119,22 +155,26 @@ def run(cmd, verbose):
     return r.returncode, r.stdout, time.time() - t0
 
 
-def build(jobs_n: int | None = None, clean: bool = False, verbose: bool = False) -> str:
-    if clean and os.path.isdir(BUILD):
-        shutil.rmtree(BUILD)
-    os.makedirs(BUILD, exist_ok=True)
-    jobs, link = compile_cmds(verbose)
+def build(jobs_n: int | None = None, clean: bool = False, verbose: bool = False, extensions=None,
+          out=None) -> str:
+    names = selected_extensions(extensions)
+    # a partial selection gets its own object dir so it never poisons the full build's objects
+    build_dir = BUILD if names == sorted(EXTENSIONS) else os.path.join(BUILD, "sel_" + "_".join(names))
+    if clean and os.path.isdir(build_dir):
+        shutil.rmtree(build_dir)
+    os.makedirs(build_dir, exist_ok=True)
+    jobs, link = compile_cmds(verbose, extensions, out, build_dir)
     hdr = newest_header()
     # module.cpp's registrations depend on which subsystem bindings exist (-D macros): rebuild it
     # whenever that set changes
-    _, cpp = sources()
+    _, cpp = sources(extensions)
     present = sorted(os.path.basename(p) for p in cpp)
-    stamp = os.path.join(BUILD, "subsystems.stamp")
+    stamp = os.path.join(build_dir, "subsystems.stamp")
     prev = open(stamp).read() if os.path.exists(stamp) else ""
     subsystems_changed = prev != ",".join(present)
     todo = []
     for src, cmd in jobs:
-        o = obj_for(src)
+        o = obj_for(src, build_dir)
         stale = not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(src), hdr)
         if stale or (subsystems_changed and src.endswith("module.cpp")):
             todo.append((src, cmd))
@@ -158,8 +198,8 @@ def build(jobs_n: int | None = None, clean: bool = False, verbose: bool = False)
         raise RuntimeError(f"native build failed: {failed}")
     with open(stamp, "w") as f:
         f.write(",".join(present))
-    out = output_path()
-    objs_newest = max(os.path.getmtime(obj_for(s)) for s, _ in jobs)
+    out = output_path(out)
+    objs_newest = max(os.path.getmtime(obj_for(s, build_dir)) for s, _ in jobs)
     if todo or not os.path.exists(out) or os.path.getmtime(out) < objs_newest:
         rc, log, dt = run(link, verbose)
         if rc != 0:
@@ -174,9 +214,11 @@ def main(argv=None):
     ap.add_argument("-j", type=int, default=None)
     ap.add_argument("--clean", action="store_true")
     ap.add_argument("--verbose", "-v", action="store_true")
+    ap.add_argument("--extensions", default=None, help="comma list of " + ",".join(sorted(EXTENSIONS)))
+    ap.add_argument("--out", default=None, help="output .so path (default: in-tree)")
     a = ap.parse_args(argv)
     try:
-        build(a.j, a.clean, a.verbose)
+        build(a.j, a.clean, a.verbose, a.extensions, a.out)
     except RuntimeError as e:
         print(f"[build_native] {e}", file=sys.stderr)
         return 1

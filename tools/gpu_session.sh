@@ -18,7 +18,7 @@ stop() { echo "STOP: $1 rc=$2"; exit $2; }
 for s in ${STEPS:-tests smoke bench}; do
   case $s in
   tests)
-    timeout -k 10 ${TESTS_TIMEOUT:-600} python -u -m pytest ${TESTS:-tests} -m gpu -x -q -p no:cacheprovider \
+    timeout -k 10 ${TESTS_TIMEOUT:-600} python -u -m pytest ${TESTS:-tests} -m gpu ${PYTEST_FLAGS--x} -q -p no:cacheprovider \
       --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
     rc=$?; tail -25 gpurun_out/pytest_gpu.log; [ $rc -ge 2 ] && stop pytest $rc ;;
   smoke)
