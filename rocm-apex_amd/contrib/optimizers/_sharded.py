@@ -21,8 +21,13 @@ MI355X design:
     (``[num_blocks, shard]``), updates them with one fused multi-tensor launch that also writes
     the model-dtype copy in place, and the updated shards are all-gathered per block
     (``all_gather_into_tensor`` — stock RCCL, no ``no_copy`` extension).
-  * optional e5m2 (fp8) all-gather compression, global grad-norm clipping, and sync-free
-    overflow handling (device skip flag + inverse scale consumed by the kernels).
+  * optional fp8 all-gather compression (e5m2 as in the reference, or e4m3): the optimizer
+    kernel's epilogue converts the updated fp32 master straight into this rank's slice of an
+    fp8 gather buffer (gfx950 ``v_cvt_pk_bf8/fp8_f32``), the uint8 buffer is all-gathered in
+    place, and one multi-tensor cast (``v_cvt_pk_f32_bf8/fp8``) expands every block into the
+    model-dtype parameters — no torch casts, no staging copies.  Every rank (the owner
+    included) ends up with the same dequantised weights.  Global grad-norm clipping and
+    sync-free overflow handling (device skip flag + inverse scale consumed by the kernels).
   * two-level data parallelism (reference ``dwu_group_size``: shard within groups of G ranks,
     replicate across the world/G groups): each block is reduce-scattered inside the group, then
     this rank's shard is all-reduced across the groups over ``ar_group`` (the ranks holding the
@@ -34,6 +39,8 @@ import math
 
 import torch
 import torch.distributed as dist
+
+from ... import amp_C
 
 _ALIGN = 128  # elements; keeps every param / shard 16-byte aligned for the vector kernels
 
@@ -111,6 +118,7 @@ class FlatShardedBuffers:
         self._dirty = set()
         self._stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
         self.is_accumulation_step = False
+        self.generation = 0  # bumped whenever a reduction (re)writes shard_grad
         self._hooks = []
         if overlap_reductions:
             for i, p in enumerate(params):
@@ -139,6 +147,25 @@ class FlatShardedBuffers:
         r = self.rank if rank is None else rank
         s = b * self.block + r * self.shard
         return self.flat_param[s:s + self.shard]
+
+    # ---- compressed all-gather payload ----
+    def payload(self, dtype):
+        """fp8 gather buffer laid out like ``flat_param`` (allocated on first use)."""
+        buf = getattr(self, "_payload", None)
+        if buf is None or buf.dtype != dtype:
+            buf = torch.zeros(self.total, dtype=dtype, device=self.device)
+            self._payload = buf
+        return buf
+
+    def out_shards(self, gather_dtype=None):
+        """Where the optimizer epilogue writes this rank's updated weights: the model-dtype
+        shards of ``flat_param``, or the fp8 payload shards when gathering compressed."""
+        src = self.flat_param if gather_dtype is None or self.world == 1 else self.payload(gather_dtype)
+        return [src[b * self.block + self.rank * self.shard:][:self.shard] for b in range(self.num_blocks)]
+
+    def out_fragments(self, frags, gather_dtype=None):
+        rows = self.out_shards(gather_dtype)
+        return [rows[b][lo:hi] for (_, b, lo, hi) in frags]
 
     def grad_shard_views(self):
         return [self.shard_grad[b] for b in range(self.num_blocks)]
@@ -212,6 +239,7 @@ class FlatShardedBuffers:
     def _reduce_block(self, b, again=False):
         if self._handles[b] is not None:
             return
+        self.generation += 1  # shard_grad is about to be overwritten
         dst = self.shard_grad[b]
         if self.dp_size == 1:
             dst.copy_(self.block_view(self.flat_grad, b))
@@ -263,21 +291,25 @@ class FlatShardedBuffers:
         self.attach_grads()
 
     # ---- parameter all-gather ----
-    def all_gather_params(self, e5m2=False):
+    def all_gather_params(self, gather_dtype=None):
+        """Gather every rank's updated shards.  ``gather_dtype`` (an fp8 dtype) means the
+        optimizer wrote fp8 shards into ``payload``; they are gathered as bytes and expanded
+        into ``flat_param`` by one multi-tensor cast."""
         if self.world == 1:
             return
+        src_buf = self.flat_param if gather_dtype is None else self.payload(gather_dtype)
         for b in range(self.num_blocks):
-            full = self.block_view(self.flat_param, b)
-            mine = self.param_shard(b)
-            if e5m2:
-                q = mine.to(torch.float8_e5m2)
-                buf = torch.empty(self.block, dtype=torch.float8_e5m2, device=self.device)
-                dist.all_gather_into_tensor(buf.view(torch.uint8), q.view(torch.uint8), group=self.pg)
-                full.copy_(buf.to(self.dtype))
-            else:
-                # RCCL gathers in place when the input is this rank's slice of the output
-                src = mine.clone() if self._gloo else mine
-                dist.all_gather_into_tensor(full, src, group=self.pg)
+            full = self.block_view(src_buf, b)
+            mine = full[self.rank * self.shard:(self.rank + 1) * self.shard]
+            if gather_dtype is not None:
+                full, mine = full.view(torch.uint8), mine.view(torch.uint8)
+            # RCCL gathers in place when the input is this rank's slice of the output
+            dist.all_gather_into_tensor(full, mine.clone() if self._gloo else mine, group=self.pg)
+        if gather_dtype is not None:
+            noop = torch.zeros(1, dtype=torch.int32, device=self.device)
+            amp_C.multi_tensor_cast(65536, noop, [[self.block_view(src_buf, b) for b in range(self.num_blocks)],
+                                                  [self.block_view(self.flat_param, b)
+                                                   for b in range(self.num_blocks)]])
 
     def state_dict_shards(self):
         return {"rank": self.rank, "world": self.world, "block": self.block, "num_blocks": self.num_blocks,

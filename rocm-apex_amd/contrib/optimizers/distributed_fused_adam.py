@@ -56,7 +56,7 @@ class DistributedFusedAdam(torch.optim.Optimizer):
                  step_supports_amp_scaling=True, num_process_groups=1, current_process_group=None,
                  process_group_id=0, process_group_size=0, clip_grad_norm=True, model_parallel=False,
                  adam_w_mode=True, min_block_elems=1 << 22, reduce_dtype=None, grad_sync_dtype=None,
-                 _reduction_mode="rs"):
+                 allgather_dtype=None, _reduction_mode="rs"):
         if amsgrad:
             raise RuntimeError("DistributedFusedAdam does not support the AMSGrad variant.")
         defaults = dict(lr=lr, bias_correction=bias_correction, betas=betas, eps=eps, weight_decay=weight_decay,
@@ -67,6 +67,12 @@ class DistributedFusedAdam(torch.optim.Optimizer):
         self.adam_w_mode = 1 if adam_w_mode else 0
         self._predivide = predivide
         self._e5m2_allgather = e5m2_allgather
+        # fp8 parameter all-gather (reference e5m2_allgather; e4m3 also accepted): the Adam
+        # epilogue writes the fp8 payload directly (see _sharded.py)
+        self._ag_dtype = allgather_dtype if allgather_dtype is not None else (
+            torch.float8_e5m2 if e5m2_allgather else None)
+        if self._ag_dtype not in (None, torch.float8_e5m2, torch.float8_e4m3fn):
+            raise ValueError("allgather_dtype must be torch.float8_e5m2 or torch.float8_e4m3fn")
         self._compute_L2_grad_norm = compute_L2_grad_norm
         self._clip_grad_norm = clip_grad_norm
         self._step_supports_amp_scaling = step_supports_amp_scaling
@@ -185,16 +191,20 @@ class DistributedFusedAdam(torch.optim.Optimizer):
         for g in self.param_groups:
             g["step"] = g.get("step", 0) + 1
         nb = flat.num_blocks
-        lists = [grads, [flat.master[b] for b in range(nb)], [self._m[b] for b in range(nb)],
-                 [self._v[b] for b in range(nb)], [flat.param_shard(b) for b in range(nb)]]
-        amp_C.multi_tensor_adam_capturable(65536, self._skip, lists, self._lr_t, beta1, beta2, g0["eps"],
-                                           self._step_t, self.adam_w_mode, 1 if g0["bias_correction"] else 0,
-                                           g0["weight_decay"], self._inv)
-        flat.all_gather_params(self._e5m2_allgather)
+        amp_C.multi_tensor_adam_capturable(65536, self._skip, self._adam_lists(grads), self._lr_t, beta1, beta2,
+                                           g0["eps"], self._step_t, self.adam_w_mode,
+                                           1 if g0["bias_correction"] else 0, g0["weight_decay"], self._inv)
+        self._stepped_generation = flat.generation
+        flat.all_gather_params(self._ag_dtype)
         flat.zero_grad()
         if grad_scaler is not None and grad_scaler.is_enabled():
             _record_found_inf(grad_scaler, self, self._skip)
         return loss
+
+    def _adam_lists(self, grads):
+        flat, nb = self._flat, self._flat.num_blocks
+        return [grads, [flat.master[b] for b in range(nb)], [self._m[b] for b in range(nb)],
+                [self._v[b] for b in range(nb)], flat.out_shards(self._ag_dtype)]
 
     # ---- checkpointing (sharded, like the reference :598-636) ----
     def state_dict(self):
@@ -230,29 +240,36 @@ def _record_found_inf(grad_scaler, optimizer, skip):
 
 
 class DistributedFusedAdamV2(DistributedFusedAdam):
-    """Reference v2 (reversible step + full pipeline) — same algorithm here; ``revert_step`` is
-    provided by keeping the pre-step master shard when ``revertible=True``."""
+    """Reference v2 (reversible step, distributed_fused_adam_v2.py + the
+    ``maybe_adam_undo`` kernel, apex/contrib/csrc/optimizers/fused_adam_cuda_kernel.cu:657).
 
-    def __init__(self, *args, revertible=False, **kwargs):
+    ``revert_step()`` rolls the last step back in place with the inverse-Adam kernel
+    (``amp_C.multi_tensor_adam_undo``): it reuses the reduced gradient shard that is still in the
+    reduce-scatter staging buffer, so no copy of the master / moment shards is ever kept.  Valid
+    until the next backward starts reducing (checked); a skipped step reverts to a no-op."""
+
+    def __init__(self, *args, revertible=True, **kwargs):
         super().__init__(*args, **kwargs)
         self._revertible = revertible
-        self._prev = None
-
-    def step(self, closure=None, grad_scaler=None):
-        if self._revertible:
-            self._prev = (self._flat.master.clone(), self._m.clone(), self._v.clone(), self._step_t.clone())
-        return super().step(closure, grad_scaler)
+        self._stepped_generation = None
 
     def revert_step(self):
-        assert self._prev is not None, "revert_step needs revertible=True and a previous step"
-        m, e1, e2, st = self._prev
-        self._flat.master.copy_(m)
-        self._m.copy_(e1)
-        self._v.copy_(e2)
-        self._step_t.copy_(st)
-        for b in range(self._flat.num_blocks):
-            self._flat.param_shard(b).copy_(m[b].to(self._flat.dtype))
-        self._flat.all_gather_params()
+        flat = self._flat
+        if not self._revertible or self._stepped_generation is None:
+            raise RuntimeError("revert_step needs revertible=True and a previous step")
+        if flat.generation != self._stepped_generation:
+            raise RuntimeError("revert_step: gradients of a later backward already replaced the step's "
+                               "reduced gradients")
+        g0 = self.param_groups[0]
+        beta1, beta2 = g0["betas"]
+        amp_C.multi_tensor_adam_undo(65536, self._skip, self._adam_lists(flat.grad_shard_views()), self._lr_t,
+                                     beta1, beta2, g0["eps"], self._step_t, self.adam_w_mode,
+                                     1 if g0["bias_correction"] else 0, g0["weight_decay"], self._inv)
+        self._step_t.sub_(1 - self._skip.float())
+        for g in self.param_groups:
+            g["step"] = max(0, g.get("step", 1) - 1)
+        self._stepped_generation = None
+        flat.all_gather_params(self._ag_dtype)
 
 
 class DistributedFusedAdamV3(DistributedFusedAdam):

@@ -21,13 +21,14 @@ class DistributedFusedLAMB(DistributedFusedAdam):
                  step_supports_amp_scaling=True, overlap_reductions=True, dwu_group_size=0, dwu_num_blocks=4,
                  dwu_num_chunks=4, dwu_num_rs_pg=1, dwu_num_ar_pg=4, dwu_num_ag_pg=0, e5m2_allgather=False,
                  verbose=False, clip_after_ar=True, min_block_elems=1 << 22, current_process_group=None,
-                 reduce_dtype=None, predivide=True):
+                 reduce_dtype=None, predivide=True, allgather_dtype=None):
         super().__init__(params, lr=lr, bias_correction=bias_correction, betas=betas, eps=eps,
                          weight_decay=weight_decay, max_grad_norm=max_grad_norm, overlap_reductions=overlap_reductions,
                          compute_L2_grad_norm=True, dwu_group_size=dwu_group_size, dwu_num_blocks=dwu_num_blocks,
                          e5m2_allgather=e5m2_allgather, step_supports_amp_scaling=step_supports_amp_scaling,
                          clip_grad_norm=clip_after_ar, adam_w_mode=adam_w_mode, min_block_elems=min_block_elems,
-                         current_process_group=current_process_group, reduce_dtype=reduce_dtype, predivide=predivide)
+                         current_process_group=current_process_group, reduce_dtype=reduce_dtype, predivide=predivide,
+                         allgather_dtype=allgather_dtype)
         for g in self.param_groups:
             g["grad_averaging"] = grad_averaging
         self._use_nvlamb = use_nvlamb
@@ -77,22 +78,21 @@ class DistributedFusedLAMB(DistributedFusedAdam):
             rows = lambda t: [t[b] for b in range(nb)]  # noqa: E731
             noclip = torch.zeros(1, dtype=torch.float32, device=flat.device)
             beta3 = (1.0 - beta1) if self._grad_averaging else 1.0
-            if beta3 != 1.0 - beta1:
-                raise NotImplementedError("grad_averaging=False is not supported by the staged kernels")
             st = self._step_host if g0["bias_correction"] else 10 ** 9
             amp_C.multi_tensor_lamb_stage1_cuda(65536, self._skip, [rows(grads), rows(flat.master), rows(self._m),
                                                                     rows(self._v), rows(self._u)],
-                                                self._decay, st, beta1, beta2, g0["eps"], noclip, 1.0)
+                                                self._decay, st, beta1, beta2, g0["eps"], noclip, 1.0, beta3)
             p_frags = self._frag_views(flat.master)
             u_frags = self._frag_views(self._u)
             pn = self._param_norms(p_frags)
             un = self._param_norms(u_frags)
             if p_frags:
-                amp_C.multi_tensor_lamb_stage2_cuda(65536, self._skip, [p_frags, u_frags], pn[self._frag_param],
-                                                    un[self._frag_param], float(g0["lr"]), wd, self._use_nvlamb)
-            for b in range(nb):
-                flat.param_shard(b).copy_(flat.master[b])
-            flat.all_gather_params(self._e5m2_allgather)
+                # stage 2 also writes the model-dtype (or fp8 gather payload) copy of each fragment
+                out_frags = flat.out_fragments(self._frags, self._ag_dtype)
+                amp_C.multi_tensor_lamb_stage2_cuda(65536, self._skip, [p_frags, u_frags, out_frags],
+                                                    pn[self._frag_param], un[self._frag_param], float(g0["lr"]),
+                                                    wd, self._use_nvlamb)
+            flat.all_gather_params(self._ag_dtype)
         flat.zero_grad()
         if grad_scaler is not None and grad_scaler.is_enabled():
             _record_found_inf(grad_scaler, self, self._skip)

@@ -163,6 +163,31 @@ void multi_tensor_adam_capturable(int chunk_size, at::Tensor noop, TL tl, at::Te
           make_launch(tl[0][0]));
 }
 
+void multi_tensor_adam_undo(int chunk_size, at::Tensor noop, TL tl, at::Tensor lr, double beta1, double beta2,
+                            double eps, at::Tensor step, int64_t mode, int64_t bias_correction, double weight_decay,
+                            c10::optional<at::Tensor> inv_scale) {
+  if (!prepare(tl)) return;
+  TORCH_CHECK(tl.size() == 4 || tl.size() == 5, "multi_tensor_adam_undo expects 4 or 5 lists");
+  TORCH_CHECK(tl[1][0].scalar_type() == at::kFloat, "multi_tensor_adam_undo: fp32 master params required");
+  TORCH_CHECK(step.scalar_type() == at::kFloat && step.is_cuda(), "step must be a float32 GPU tensor");
+  const c10::hip::HIPGuard g(tl[0][0].get_device());
+  auto m = mta_meta(tl, chunk_size);
+  AdamArgs a{};
+  a.beta1 = (float)beta1;
+  a.beta2 = (float)beta2;
+  a.eps = (float)eps;
+  a.weight_decay = (float)weight_decay;
+  a.lr = dev_scalar(lr, 0.f);
+  a.inv_scale = dev_scalar(inv_scale, 1.f);
+  a.step_dev = step.data_ptr<float>();
+  a.bias_correction = (int)bias_correction;
+  a.bc1 = a.bc2 = 1.f;
+  a.mode = (int)mode;
+  a.skip_on_noop = true;
+  const int out_t = tl.size() == 5 ? dtype_code(tl[4][0].scalar_type()) : -1;
+  mt_adam_undo(m, dtype_code(tl[0][0].scalar_type()), out_t, noop_ptr(noop), a, make_launch(tl[0][0]));
+}
+
 void multi_tensor_sgd(int chunk_size, at::Tensor noop, TL tl, double wd, double momentum, double dampening,
                       double lr, bool nesterov, bool first_run, bool wd_after_momentum, double scale) {
   if (!prepare(tl)) return;
@@ -310,7 +335,7 @@ void multi_tensor_lamb_mp(int chunk_size, at::Tensor noop, TL tl, at::Tensor lr,
 
 void multi_tensor_lamb_stage1_cuda(int chunk_size, at::Tensor noop, TL tl, at::Tensor per_tensor_decay,
                                    int64_t step, double beta1, double beta2, double eps, at::Tensor global_grad_norm,
-                                   double max_global_grad_norm) {
+                                   double max_global_grad_norm, c10::optional<double> beta3) {
   if (!prepare(tl)) return;
   TORCH_CHECK(tl.size() == 5, "multi_tensor_lamb_stage1 expects 5 lists (g, p, m, v, update)");
   const c10::hip::HIPGuard g(tl[0][0].get_device());
@@ -318,7 +343,8 @@ void multi_tensor_lamb_stage1_cuda(int chunk_size, at::Tensor noop, TL tl, at::T
   const float bc1 = (float)(1.0 - std::pow(beta1, (double)step));
   const float bc2 = (float)(1.0 - std::pow(beta2, (double)step));
   mt_lamb_legacy_stage1(m, dtype_code(tl[0][0].scalar_type()), dtype_code(tl[1][0].scalar_type()), noop_ptr(noop),
-                        per_tensor_decay.data_ptr<float>(), (float)beta1, (float)beta2, bc1, bc2, (float)eps,
+                        per_tensor_decay.data_ptr<float>(), (float)beta1, (float)beta2,
+                        (float)beta3.value_or(1.0 - beta1), bc1, bc2, (float)eps,
                         global_grad_norm.data_ptr<float>(), (float)max_global_grad_norm, make_launch(tl[0][0]));
 }
 
@@ -326,10 +352,12 @@ void multi_tensor_lamb_stage2_cuda(int chunk_size, at::Tensor noop, TL tl, at::T
                                    at::Tensor per_tensor_update_norm, double lr, double weight_decay,
                                    c10::optional<bool> use_nvlamb) {
   if (!prepare(tl)) return;
-  TORCH_CHECK(tl.size() == 2, "multi_tensor_lamb_stage2 expects 2 lists (p, update)");
+  TORCH_CHECK(tl.size() == 2 || tl.size() == 3, "multi_tensor_lamb_stage2 expects 2 or 3 lists (p, update[, out])");
   const c10::hip::HIPGuard g(tl[0][0].get_device());
   auto m = mta_meta(tl, chunk_size);
-  mt_lamb_legacy_stage2(m, dtype_code(tl[0][0].scalar_type()), dtype_code(tl[1][0].scalar_type()), noop_ptr(noop),
+  const int out_t = tl.size() == 3 ? dtype_code(tl[2][0].scalar_type()) : -1;
+  mt_lamb_legacy_stage2(m, dtype_code(tl[0][0].scalar_type()), dtype_code(tl[1][0].scalar_type()), out_t,
+                        noop_ptr(noop),
                         per_tensor_param_norm.data_ptr<float>(), per_tensor_update_norm.data_ptr<float>(), (float)lr,
                         (float)weight_decay, use_nvlamb.value_or(false), make_launch(tl[0][0]));
 }
@@ -387,7 +415,12 @@ void bind_amp_C(pybind11::module_& root) {
         pybind11::arg("global_grad_norm"), pybind11::arg("max_grad_norm"),
         pybind11::arg("use_nvlamb_python") = c10::nullopt);
   m.def("multi_tensor_lamb_mp", &multi_tensor_lamb_mp, "LAMB with device lr/step, found_inf and inv_scale");
-  m.def("multi_tensor_lamb_stage1_cuda", &multi_tensor_lamb_stage1_cuda, "legacy LAMB stage 1");
+  m.def("multi_tensor_adam_undo", &multi_tensor_adam_undo, "invert the last Adam step in place");
+  m.def("multi_tensor_lamb_stage1_cuda", &multi_tensor_lamb_stage1_cuda, "legacy LAMB stage 1",
+        pybind11::arg("chunk_size"), pybind11::arg("noop_flag"), pybind11::arg("tensor_lists"),
+        pybind11::arg("per_tensor_decay"), pybind11::arg("step"), pybind11::arg("beta1"), pybind11::arg("beta2"),
+        pybind11::arg("epsilon"), pybind11::arg("global_grad_norm"), pybind11::arg("max_global_grad_norm"),
+        pybind11::arg("beta3") = c10::nullopt);
   m.def("multi_tensor_lamb_stage2_cuda", &multi_tensor_lamb_stage2_cuda, "legacy LAMB stage 2");
   m.def("multi_tensor_cast", &multi_tensor_cast, "out = in (dtype conversion)");
   m.def("amp_update_scale_", &amp_update_scale_, "device-side dynamic loss scale update");

@@ -19,11 +19,18 @@ enum DType : int { kF32 = 0, kF16 = 1, kBF16 = 2, kF64 = 3, kU8 = 4, kI32 = 5, k
 
 struct f16_t { uint16_t x; };
 struct bf16_t { uint16_t x; };
+// OCP fp8 storage (gfx950 converts natively: v_cvt_pk_{bf8,fp8}_f32 / v_cvt_[pk_]f32_{bf8,fp8}).
+// e5m2 == torch.float8_e5m2, e4m3 == torch.float8_e4m3fn.
+struct fp8e5m2_t { uint8_t x; };
+struct fp8e4m3_t { uint8_t x; };
 
 __device__ __forceinline__ float to_f(float v) { return v; }
 __device__ __forceinline__ float to_f(double v) { return (float)v; }
 __device__ __forceinline__ float to_f(f16_t v) { return (float)__builtin_bit_cast(_Float16, v.x); }
 __device__ __forceinline__ float to_f(bf16_t v) { return __uint_as_float(((uint32_t)v.x) << 16); }
+
+__device__ __forceinline__ float to_f(fp8e5m2_t v) { return __builtin_amdgcn_cvt_f32_bf8((int)v.x, 0); }
+__device__ __forceinline__ float to_f(fp8e4m3_t v) { return __builtin_amdgcn_cvt_f32_fp8((int)v.x, 0); }
 
 template <typename T> __device__ __forceinline__ T from_f(float v);
 template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
@@ -33,6 +40,13 @@ template <> __device__ __forceinline__ f16_t from_f<f16_t>(float v) {
 }
 template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float v) {
   return bf16_t{__builtin_bit_cast(uint16_t, (__bf16)v)};
+}
+
+template <> __device__ __forceinline__ fp8e5m2_t from_f<fp8e5m2_t>(float v) {
+  return fp8e5m2_t{(uint8_t)(__builtin_amdgcn_cvt_pk_bf8_f32(v, v, 0, false) & 0xffu)};
+}
+template <> __device__ __forceinline__ fp8e4m3_t from_f<fp8e4m3_t>(float v) {
+  return fp8e4m3_t{(uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(v, v, 0, false) & 0xffu)};
 }
 
 __device__ __forceinline__ bool is_finite(float v) { return __builtin_isfinite(v); }
@@ -76,6 +90,43 @@ template <typename T16> struct Vec8_16 {
 };
 template <> struct Vec8<f16_t> : Vec8_16<f16_t> {};
 template <> struct Vec8<bf16_t> : Vec8_16<bf16_t> {};
+
+// fp8: 8 elements = one dwordx2; packed converts handle two values per instruction
+template <bool E5M2> struct Vec8_8 {
+  static __device__ __forceinline__ void load(float (&r)[8], const void* p) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    const uint32_t w[2] = {u.x, u.y};
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const auto lo = E5M2 ? __builtin_amdgcn_cvt_pk_f32_bf8((int)w[i], false)
+                           : __builtin_amdgcn_cvt_pk_f32_fp8((int)w[i], false);
+      const auto hi = E5M2 ? __builtin_amdgcn_cvt_pk_f32_bf8((int)w[i], true)
+                           : __builtin_amdgcn_cvt_pk_f32_fp8((int)w[i], true);
+      r[4 * i] = lo[0];
+      r[4 * i + 1] = lo[1];
+      r[4 * i + 2] = hi[0];
+      r[4 * i + 3] = hi[1];
+    }
+  }
+  static __device__ __forceinline__ void store(void* p, const float (&r)[8]) {
+    uint32_t w[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int acc = 0;
+      if constexpr (E5M2) {
+        acc = __builtin_amdgcn_cvt_pk_bf8_f32(r[4 * i], r[4 * i + 1], acc, false);
+        acc = __builtin_amdgcn_cvt_pk_bf8_f32(r[4 * i + 2], r[4 * i + 3], acc, true);
+      } else {
+        acc = __builtin_amdgcn_cvt_pk_fp8_f32(r[4 * i], r[4 * i + 1], acc, false);
+        acc = __builtin_amdgcn_cvt_pk_fp8_f32(r[4 * i + 2], r[4 * i + 3], acc, true);
+      }
+      w[i] = (uint32_t)acc;
+    }
+    *reinterpret_cast<uint2*>(p) = make_uint2(w[0], w[1]);
+  }
+};
+template <> struct Vec8<fp8e5m2_t> : Vec8_8<true> {};
+template <> struct Vec8<fp8e4m3_t> : Vec8_8<false> {};
 
 // ---------------------------------------------------------------------------------------------
 // wave64 / block reductions

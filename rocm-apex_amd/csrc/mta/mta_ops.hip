@@ -253,7 +253,7 @@ static void launch_adam(const MtaMeta& m, int g_t, int p_t, int out_t, int* noop
   dispatch_float(g_t, [&](auto tg) {
     using TG = typename decltype(tg)::type;
     if constexpr (D == 5) {
-      dispatch_16(out_t, [&](auto to) {
+      dispatch_model_out(out_t, [&](auto to) {
         using TO = typename decltype(to)::type;
         mta_elementwise_kernel<AdamOp<D, SKIP>, TG, float, float, float, TO><<<grid, kMtaBlock, 0, s>>>(m, noop, op);
       }, "multi_tensor_adam(model out)");
@@ -277,6 +277,69 @@ void mt_adam(const MtaMeta& m, int g_t, int p_t, int out_t, int* noop, const Ada
     else launch_adam<4, false>(m, g_t, p_t, out_t, noop, a, grid, L.stream);
   }
   check_launch("multi_tensor_adam");
+}
+
+// ---------------------------------------------------------------------------------------------
+// Adam undo (capability of the reference's maybe_adam_undo, apex/contrib/csrc/optimizers/
+// fused_adam_cuda_kernel.cu:657): given the gradient g of the step just taken and the post-step
+// p, m, v, recompute that step's update from (m, v) and invert it in place, so a step can be
+// rolled back without keeping copies of the master / moment shards.  Exact for p up to fp32
+// rounding; m and v are recovered up to the cancellation in (m - (1-b1) g) / b1 (v is clamped
+// at 0).  Skipped entirely when *noop (the reverted step's skip flag) is set.
+// ---------------------------------------------------------------------------------------------
+template <int D>
+struct AdamUndoOp : MtaOpBase {
+  static constexpr unsigned kRead = 0b1111, kWrite = (D == 5) ? 0b11110 : 0b1110;
+  static constexpr bool kSkipOnNoop = true;
+  AdamArgs a;
+  using TS = typename AdamOp<D, true>::TS;
+  __device__ __forceinline__ TS tensor_state(int t) const {
+    AdamOp<D, true> fwd;
+    fwd.a = a;
+    return fwd.tensor_state(t);
+  }
+  template <int N>
+  __device__ __forceinline__ void apply(float (&r)[D][N], const TS& s, bool&, float*) const {
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      float g = r[0][k] * s.inv;
+      const float p = r[1][k], mm = r[2][k], vv = r[3][k];
+      const float denom = sqrtf(vv / s.bc2) + a.eps;
+      const float upd = (mm / s.bc1) / denom;
+      float p0;
+      if (a.mode == 0) {
+        p0 = p + s.lr * upd;
+        g = g + a.weight_decay * p0;
+      } else {
+        p0 = (p + s.lr * upd) / (1.f - s.lr * a.weight_decay);
+      }
+      r[1][k] = p0;
+      r[2][k] = (mm - (1.f - a.beta1) * g) / a.beta1;
+      r[3][k] = fmaxf((vv - (1.f - a.beta2) * g * g) / a.beta2, 0.f);
+      if constexpr (D == 5) r[4][k] = p0;
+    }
+  }
+};
+
+void mt_adam_undo(const MtaMeta& m, int g_t, int out_t, int* noop, const AdamArgs& a, const Launch& L) {
+  const int grid = mta_grid(m.nchunks, L.max_blocks);
+  dispatch_float(g_t, [&](auto tg) {
+    using TG = typename decltype(tg)::type;
+    if (m.depth == 5) {
+      dispatch_model_out(out_t, [&](auto to) {
+        using TO = typename decltype(to)::type;
+        AdamUndoOp<5> op;
+        op.a = a;
+        mta_elementwise_kernel<AdamUndoOp<5>, TG, float, float, float, TO><<<grid, kMtaBlock, 0, L.stream>>>(m, noop,
+                                                                                                           op);
+      }, "multi_tensor_adam_undo(model out)");
+    } else {
+      AdamUndoOp<4> op;
+      op.a = a;
+      mta_elementwise_kernel<AdamUndoOp<4>, TG, float, float, float><<<grid, kMtaBlock, 0, L.stream>>>(m, noop, op);
+    }
+  }, "multi_tensor_adam_undo(grad)");
+  check_launch("multi_tensor_adam_undo");
 }
 
 // =============================================================================================
@@ -321,7 +384,7 @@ void mt_sgd(const MtaMeta& m, int g_t, int w_t, int out_t, int* noop, const SgdA
       if (m.depth == 4) {
         SgdOp<4> op;
         op.a = a;
-        dispatch_16(out_t, [&](auto to) {
+        dispatch_model_out(out_t, [&](auto to) {
           using TO = typename decltype(to)::type;
           mta_elementwise_kernel<SgdOp<4>, TG, TW, TW, TO><<<grid, kMtaBlock, 0, L.stream>>>(m, noop, op);
         }, "multi_tensor_sgd(model out)");
@@ -539,7 +602,7 @@ void mt_lamb_stage2(const MtaMeta& m, int u_t, int p_t, int out_t, int* noop, co
         if (m.depth == 3) {
           LambStage2Op<3, S> op;
           op.a = a;
-          dispatch_16(out_t, [&](auto to) {
+          dispatch_model_out(out_t, [&](auto to) {
             using TO = typename decltype(to)::type;
             mta_elementwise_kernel<LambStage2Op<3, S>, TU, TP, TO><<<grid, kMtaBlock, 0, L.stream>>>(m, noop, op);
           }, "multi_tensor_lamb(model out)");
@@ -564,7 +627,7 @@ struct LambLegacy1Op : MtaOpBase {
   static constexpr unsigned kRead = 0b01111, kWrite = 0b11100;
   static constexpr bool kSkipOnNoop = false;
   const float* decay;
-  float beta1, beta2, bc1, bc2, eps, max_norm;
+  float beta1, beta2, beta3, bc1, bc2, eps, max_norm;
   const float* gnorm;
   struct TS { float clip, decay; };
   __device__ __forceinline__ TS tensor_state(int t) const {
@@ -576,7 +639,7 @@ struct LambLegacy1Op : MtaOpBase {
 #pragma unroll
     for (int k = 0; k < N; ++k) {
       const float sg = r[0][k] / s.clip;
-      const float mm = r[2][k] * beta1 + (1.f - beta1) * sg;
+      const float mm = r[2][k] * beta1 + beta3 * sg;
       const float vv = r[3][k] * beta2 + (1.f - beta2) * sg * sg;
       r[4][k] = (mm / bc1) / (sqrtf(vv / bc2) + eps) + s.decay * r[1][k];
       r[2][k] = mm;
@@ -586,12 +649,13 @@ struct LambLegacy1Op : MtaOpBase {
 };
 
 void mt_lamb_legacy_stage1(const MtaMeta& m, int g_t, int p_t, int* noop, const float* per_tensor_decay,
-                           float beta1, float beta2, float bc1, float bc2, float eps,
+                           float beta1, float beta2, float beta3, float bc1, float bc2, float eps,
                            const float* global_grad_norm, float max_global_grad_norm, const Launch& L) {
   LambLegacy1Op op;
   op.decay = per_tensor_decay;
   op.beta1 = beta1;
   op.beta2 = beta2;
+  op.beta3 = beta3;
   op.bc1 = bc1;
   op.bc2 = bc2;
   op.eps = eps;
@@ -608,8 +672,10 @@ void mt_lamb_legacy_stage1(const MtaMeta& m, int g_t, int p_t, int* noop, const 
   check_launch("multi_tensor_lamb_stage1_cuda");
 }
 
+// D == 3: the updated master is also written to a model-dtype (16-bit or fp8) copy
+template <int D>
 struct LambLegacy2Op : MtaOpBase {
-  static constexpr unsigned kRead = 0b11, kWrite = 0b01;
+  static constexpr unsigned kRead = 0b011, kWrite = (D == 3) ? 0b101 : 0b001;
   static constexpr bool kSkipOnNoop = false;
   const float* pn;
   const float* un;
@@ -625,27 +691,42 @@ struct LambLegacy2Op : MtaOpBase {
     return {ratio};
   }
   template <int N>
-  __device__ __forceinline__ void apply(float (&r)[2][N], const TS& s, bool&, float*) const {
+  __device__ __forceinline__ void apply(float (&r)[D][N], const TS& s, bool&, float*) const {
 #pragma unroll
-    for (int k = 0; k < N; ++k) r[0][k] = r[0][k] - s.ratio * r[1][k];
+    for (int k = 0; k < N; ++k) {
+      r[0][k] = r[0][k] - s.ratio * r[1][k];
+      if constexpr (D == 3) r[2][k] = r[0][k];
+    }
   }
 };
 
-void mt_lamb_legacy_stage2(const MtaMeta& m, int p_t, int u_t, int* noop, const float* per_tensor_param_norm,
-                           const float* per_tensor_update_norm, float lr, float weight_decay, bool use_nvlamb,
-                           const Launch& L) {
-  LambLegacy2Op op;
-  op.pn = per_tensor_param_norm;
-  op.un = per_tensor_update_norm;
-  op.lr = lr;
-  op.wd = weight_decay;
-  op.nv = use_nvlamb;
+void mt_lamb_legacy_stage2(const MtaMeta& m, int p_t, int u_t, int out_t, int* noop,
+                           const float* per_tensor_param_norm, const float* per_tensor_update_norm, float lr,
+                           float weight_decay, bool use_nvlamb, const Launch& L) {
+  auto fill = [&](auto& op) {
+    op.pn = per_tensor_param_norm;
+    op.un = per_tensor_update_norm;
+    op.lr = lr;
+    op.wd = weight_decay;
+    op.nv = use_nvlamb;
+  };
   const int grid = mta_grid(m.nchunks, L.max_blocks);
   dispatch_float(p_t, [&](auto tp) {
     dispatch_float(u_t, [&](auto tu) {
       using TP = typename decltype(tp)::type;
       using TU = typename decltype(tu)::type;
-      mta_elementwise_kernel<LambLegacy2Op, TP, TU><<<grid, kMtaBlock, 0, L.stream>>>(m, noop, op);
+      if (out_t < 0) {
+        LambLegacy2Op<2> op;
+        fill(op);
+        mta_elementwise_kernel<LambLegacy2Op<2>, TP, TU><<<grid, kMtaBlock, 0, L.stream>>>(m, noop, op);
+      } else {
+        dispatch_model_out(out_t, [&](auto to) {
+          using TO = typename decltype(to)::type;
+          LambLegacy2Op<3> op;
+          fill(op);
+          mta_elementwise_kernel<LambLegacy2Op<3>, TP, TU, TO><<<grid, kMtaBlock, 0, L.stream>>>(m, noop, op);
+        }, "multi_tensor_lamb_stage2(model out)");
+      }
     }, "multi_tensor_lamb_stage2(update)");
   }, "multi_tensor_lamb_stage2(param)");
   check_launch("multi_tensor_lamb_stage2_cuda");
@@ -666,8 +747,8 @@ struct CastOp : MtaOpBase {
 
 void mt_cast(const MtaMeta& m, int in_t, int out_t, int* noop, const Launch& L) {
   const int grid = mta_grid(m.nchunks, L.max_blocks);
-  dispatch_float(in_t, [&](auto ti) {
-    dispatch_float(out_t, [&](auto to) {
+  dispatch_any(in_t, [&](auto ti) {
+    dispatch_any(out_t, [&](auto to) {
       using TI = typename decltype(ti)::type;
       using TO = typename decltype(to)::type;
       mta_elementwise_kernel<CastOp, TI, TO><<<grid, kMtaBlock, 0, L.stream>>>(m, noop, CastOp{});

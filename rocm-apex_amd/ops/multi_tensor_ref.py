@@ -163,6 +163,33 @@ def multi_tensor_adam_capturable(chunk_size, noop, tl, lr, beta1, beta2, eps, st
             o.copy_(pn)
 
 
+def multi_tensor_adam_undo(chunk_size, noop, tl, lr, beta1, beta2, eps, step, mode, bias_correction,
+                           weight_decay, inv_scale=None):
+    """Inverse of one fp32-master Adam step (lists g, p, m, v[, model copy]); the HIP op is
+    csrc/mta/mta_ops.hip AdamUndoOp (capability of the reference's maybe_adam_undo)."""
+    if int(noop.reshape(-1)[0]) != 0:
+        return
+    st = float(step.reshape(-1)[0])
+    lrv = float(lr.reshape(-1)[0])
+    inv = float(inv_scale.reshape(-1)[0]) if inv_scale is not None else 1.0
+    bc1 = 1 - beta1 ** st if bias_correction else 1.0
+    bc2 = 1 - beta2 ** st if bias_correction else 1.0
+    outs = tl[4] if len(tl) == 5 else [None] * len(tl[0])
+    for g, p, m, v, o in zip(tl[0], tl[1], tl[2], tl[3], outs):
+        gf, pf, mf, vf = _f(g) * inv, _f(p), _f(m), _f(v)
+        upd = (mf / bc1) / ((vf / bc2).sqrt() + eps)
+        if mode == 0:
+            p0 = pf + lrv * upd
+            gf = gf + weight_decay * p0
+        else:
+            p0 = (pf + lrv * upd) / (1.0 - lrv * weight_decay)
+        p.copy_(p0)
+        m.copy_((mf - (1 - beta1) * gf) / beta1)
+        v.copy_(((vf - (1 - beta2) * gf * gf) / beta2).clamp_min(0.0))
+        if o is not None:
+            o.copy_(p0)
+
+
 def _sgd(tl, wd, momentum, dampening, lr, nesterov, first_run, wd_after_momentum, scale):
     outs = tl[3] if len(tl) == 4 else [None] * len(tl[0])
     for g, w, mom, o in zip(tl[0], tl[1], tl[2], outs):
@@ -292,15 +319,17 @@ def multi_tensor_lamb_mp(chunk_size, noop, tl, lr, beta1, beta2, epsilon, step, 
 
 
 def multi_tensor_lamb_stage1_cuda(chunk_size, noop, tl, per_tensor_decay, step, beta1, beta2, epsilon,
-                                  global_grad_norm, max_global_grad_norm):
-    """reference csrc/multi_tensor_lamb_stage_1.cu:17-151 (lists g, p, m, v, update)"""
+                                  global_grad_norm, max_global_grad_norm, beta3=None):
+    """reference csrc/multi_tensor_lamb_stage_1.cu:17-151 (lists g, p, m, v, update); ``beta3``
+    (default 1 - beta1) is the gradient weight in the first moment (1 for grad_averaging=False)"""
     bc1 = 1 - beta1 ** step
     bc2 = 1 - beta2 ** step
+    b3 = (1 - beta1) if beta3 is None else beta3
     gn = float(global_grad_norm.reshape(-1)[0])
     clip = gn / max_global_grad_norm if gn > max_global_grad_norm else 1.0
     for i, (g, p, m, v, u) in enumerate(zip(*tl)):
         sg = _f(g) / clip
-        mf = _f(m) * beta1 + (1 - beta1) * sg
+        mf = _f(m) * beta1 + b3 * sg
         vf = _f(v) * beta2 + (1 - beta2) * sg * sg
         u.copy_((mf / bc1) / ((vf / bc2).sqrt() + epsilon) + float(per_tensor_decay[i]) * _f(p))
         m.copy_(mf)
@@ -309,13 +338,16 @@ def multi_tensor_lamb_stage1_cuda(chunk_size, noop, tl, per_tensor_decay, step, 
 
 def multi_tensor_lamb_stage2_cuda(chunk_size, noop, tl, per_tensor_param_norm, per_tensor_update_norm, lr,
                                   weight_decay, use_nvlamb_python=None):
-    """reference csrc/multi_tensor_lamb_stage_2.cu:20-125 (lists p, update)"""
-    for i, (p, u) in enumerate(zip(tl[0], tl[1])):
+    """reference csrc/multi_tensor_lamb_stage_2.cu:20-125 (lists p, update[, model-dtype copy])"""
+    outs = tl[2] if len(tl) == 3 else [None] * len(tl[0])
+    for i, (p, u, o) in enumerate(zip(tl[0], tl[1], outs)):
         ratio = lr
         if use_nvlamb_python or weight_decay != 0:
             pn, un = float(per_tensor_param_norm[i]), float(per_tensor_update_norm[i])
             ratio = lr * (pn / un) if (pn != 0 and un != 0) else lr
         p.copy_(_f(p) - ratio * _f(u))
+        if o is not None:
+            o.copy_(p)
 
 
 def multi_tensor_cast(chunk_size, noop, tl):

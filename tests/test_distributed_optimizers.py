@@ -24,10 +24,10 @@ def _batches(rank, n=4):
     return [(torch.randn(8, 13, generator=g), torch.randn(8, 5, generator=g)) for _ in range(n)]
 
 
-def _ref_lamb_step(params, grads, state, lr, b1, b2, eps, wd, step):
+def _ref_lamb_step(params, grads, state, lr, b1, b2, eps, wd, step, grad_averaging=True):
     for p, g in zip(params, grads):
         st = state.setdefault(id(p), {"m": torch.zeros_like(p), "v": torch.zeros_like(p)})
-        st["m"].mul_(b1).add_(g, alpha=1 - b1)
+        st["m"].mul_(b1).add_(g, alpha=(1 - b1) if grad_averaging else 1.0)
         st["v"].mul_(b2).addcmul_(g, g, value=1 - b2)
         mh = st["m"] / (1 - b1 ** step)
         vh = st["v"] / (1 - b2 ** step)
@@ -54,6 +54,8 @@ def _worker(rank, world, kind, num_blocks, max_grad_norm, extra=None):
         ref_opt = torch.optim.AdamW(ref.parameters(), lr=1e-2, betas=(0.9, 0.99), eps=1e-8, weight_decay=0.01)
         ref_opt = torch.optim.AdamW(ref.parameters(), lr=1e-2, betas=(0.9, 0.99), eps=1e-8, weight_decay=0.01)
     else:
+        if kind == "lamb_noavg":
+            kw["grad_averaging"] = False
         opt = DistributedFusedLAMB(model.parameters(), max_grad_norm=max_grad_norm, **kw)
         ref_state = {}
     assert opt._flat.num_blocks >= 1
@@ -76,7 +78,7 @@ def _worker(rank, world, kind, num_blocks, max_grad_norm, extra=None):
         else:
             with torch.no_grad():
                 _ref_lamb_step(list(ref.parameters()), [p.grad for p in ref.parameters()], ref_state, 1e-2, 0.9, 0.99,
-                               1e-8, 0.01, step)
+                               1e-8, 0.01, step, grad_averaging=(kind != "lamb_noavg"))
         for p, q in zip(model.parameters(), ref.parameters()):
             torch.testing.assert_close(p, q, atol=2e-5, rtol=1e-4)
         if max_grad_norm > 0:
@@ -94,7 +96,7 @@ def _worker(rank, world, kind, num_blocks, max_grad_norm, extra=None):
             torch.testing.assert_close(q, parts[0], rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("kind", ["adam", "lamb"])
+@pytest.mark.parametrize("kind", ["adam", "lamb", "lamb_noavg"])
 @pytest.mark.parametrize("num_blocks,max_grad_norm", [(1, 0.0), (3, 0.0), (2, 0.05)])
 def test_distributed_optimizer_matches_full_model(kind, num_blocks, max_grad_norm):
     run_multiprocess(_worker, world=2, args=(kind, num_blocks, max_grad_norm))
@@ -144,6 +146,94 @@ def _overflow_worker(rank, world):
 
 def test_distributed_adam_overflow_skip_and_checkpoint():
     run_multiprocess(_overflow_worker, world=2)
+
+
+def _gathered_master(opt):
+    """The full fp32 master vector in flat-buffer layout (every rank's shards)."""
+    flat = opt._flat
+    parts = [torch.empty_like(flat.master) for _ in range(flat.world)]
+    dist.all_gather(parts, flat.master.contiguous())
+    rows = []
+    for b in range(flat.num_blocks):
+        rows += [parts[r][b] for r in range(flat.world)]
+    return torch.cat(rows)
+
+
+def _fp8_worker(rank, world, kind, fp8):
+    from apex.contrib.optimizers import DistributedFusedAdam, DistributedFusedLAMB
+
+    model = _model(3)
+    plain = copy.deepcopy(model)
+    cls = DistributedFusedAdam if kind == "adam" else DistributedFusedLAMB
+    kw = dict(lr=1e-2, weight_decay=0.01, dwu_num_blocks=2, min_block_elems=256)
+    if fp8 == "e5m2":
+        opt = cls(model.parameters(), e5m2_allgather=True, **kw)
+    else:
+        opt = cls(model.parameters(), allgather_dtype=torch.float8_e4m3fn, **kw)
+    ref_opt = cls(plain.parameters(), **kw)
+    dt = torch.float8_e5m2 if fp8 == "e5m2" else torch.float8_e4m3fn
+    for x, y in _batches(rank, 3):
+        for m, o in ((model, opt), (plain, ref_opt)):
+            torch.nn.functional.mse_loss(m(x), y).backward()
+            o.step()
+        # every rank (the owner included) holds exactly the fp8-rounded master
+        master = _gathered_master(opt)
+        flat = opt._flat.flat_param
+        for p, off in zip(opt._flat.params, opt._flat.offsets):
+            n = p.numel()
+            want = master[off:off + n].to(dt).to(p.dtype)
+            assert torch.equal(p.detach().reshape(-1), want)
+        # and stays close to uncompressed training (fp8 rounding of the weights only)
+        for p, q in zip(model.parameters(), plain.parameters()):
+            tol = 0.13 if fp8 == "e5m2" else 0.07
+            torch.testing.assert_close(p, q, rtol=tol, atol=0.03)
+    parts = [torch.empty_like(flat) for _ in range(world)]
+    dist.all_gather(parts, flat)
+    assert all(torch.equal(parts[0], q) for q in parts[1:])
+
+
+@pytest.mark.parametrize("kind", ["adam", "lamb"])
+@pytest.mark.parametrize("fp8", ["e5m2", "e4m3"])
+def test_distributed_fp8_allgather(kind, fp8):
+    run_multiprocess(_fp8_worker, world=2, args=(kind, fp8))
+
+
+def _revert_worker(rank, world, wd_mode):
+    from apex.contrib.optimizers import DistributedFusedAdamV2
+
+    model = _model(4)
+    opt = DistributedFusedAdamV2(model.parameters(), lr=1e-2, weight_decay=0.05, min_block_elems=256,
+                                 dwu_num_blocks=2, adam_w_mode=(wd_mode == "adamw"))
+    b = _batches(rank, 3)
+    for x, y in b[:2]:
+        torch.nn.functional.mse_loss(model(x), y).backward()
+        opt.step()
+    snap = dict(master=opt._flat.master.clone(), m=opt._m.clone(), v=opt._v.clone(), step=opt._step_t.clone(),
+                params=[p.detach().clone() for p in model.parameters()])
+    x, y = b[2]
+    torch.nn.functional.mse_loss(model(x), y).backward()
+    opt.step()
+    assert not torch.equal(opt._flat.master, snap["master"])
+    opt.revert_step()
+    torch.testing.assert_close(opt._flat.master, snap["master"], rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(opt._m, snap["m"], rtol=1e-4, atol=1e-7)
+    torch.testing.assert_close(opt._v, snap["v"], rtol=1e-3, atol=1e-9)
+    assert torch.equal(opt._step_t, snap["step"])
+    for p, q in zip(model.parameters(), snap["params"]):
+        torch.testing.assert_close(p, q, rtol=1e-5, atol=1e-7)
+    with pytest.raises(RuntimeError):
+        opt.revert_step()  # one step back only
+    # redoing the step lands where the first attempt did
+    torch.nn.functional.mse_loss(model(x), y).backward()
+    opt.step()
+    torch.nn.functional.mse_loss(model(x), y).backward()  # a later backward invalidates the revert
+    with pytest.raises(RuntimeError):
+        opt.revert_step()
+
+
+@pytest.mark.parametrize("wd_mode", ["adamw", "l2"])
+def test_distributed_adam_revert_step_without_clones(wd_mode):
+    run_multiprocess(_revert_worker, world=2, args=(wd_mode,))
 
 
 def _accum_worker(rank, world):
