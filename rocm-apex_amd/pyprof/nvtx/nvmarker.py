@@ -3,13 +3,27 @@
 ``init()`` monkey-patches ``torch.*``, ``torch.Tensor.*``, ``torch.nn.functional.*`` and the
 ``forward`` of every ``torch.nn`` module class so each call pushes a ROCTX range (the ROCm
 build of ``torch.cuda.nvtx`` emits roctx, which ``rocprofv3 --marker-trace`` records) whose
-text is a python-literal dict: ``{'mod': ..., 'op': ..., 'args': [...], 'traceMarker': [...]}``
-with the shapes / dtypes / scalar values of the arguments.  ``apex.pyprof.parse`` attaches the
-innermost enclosing marker to every kernel and ``apex.pyprof.prof`` turns the argument shapes
-into FLOP / byte counts.  Without roctx (CPU builds) the ranges go to
-``torch.autograd.profiler.record_function`` instead."""
+text is a python-literal dict::
+
+    {'mod': 'torch.nn.functional', 'op': 'linear', 'dir': 'fprop', 'seqId': 17,
+     'args': [{'name': '', 'type': 'tensor', 'shape': (64, 128), 'dtype': 'bfloat16'}, ...],
+     'traceMarker': ['train.py:42', ...]}
+
+Backward attribution (the reference leans on PyTorch's autograd ``seq=`` NVTX ranges and
+matches sequence numbers afterwards, prof.py:171-256): here the wrapper registers a pre-hook and
+a post-hook on the ``grad_fn`` of the op's outputs, so the backward node runs inside a range
+with the SAME description, ``'dir': 'bprop'`` and the same ``seqId``.  The kernels the autograd
+thread launches for it are therefore attributed directly, with no sequence matching.
+
+``layer(name)`` (context manager / decorator) pushes ``layer:<name>`` ranges; the parse stage
+reports the enclosing layer path of every kernel (reference "layer" column).  ``wrap(mod, fn)``
+annotates a user function the same way (reference ``pyprof.nvtx.wrap``).  Without roctx (CPU
+builds) the ranges go to ``torch.autograd.profiler.record_function`` instead."""
+import contextlib
 import functools
 import inspect
+import itertools
+import threading
 import traceback
 
 import torch
@@ -31,10 +45,18 @@ _SKIP = {"__all__", "__array__", "__array_priority__", "__array_wrap__", "__bool
          "__path__", "__reduce__", "__reduce_ex__", "__repr__", "__reversed__", "__setattr__", "__setitem__",
          "__setstate__", "__sizeof__", "__spec__", "__str__", "__subclasshook__", "__version__", "__weakref__",
          "size", "tolist", "dim", "is_storage", "item", "data_ptr", "stride", "numel", "element_size",
-         "is_contiguous", "storage_offset", "__torch_function__", "type", "get_device"}
+         "is_contiguous", "storage_offset", "__torch_function__", "type", "get_device", "register_hook",
+         "requires_grad_", "backward", "register_post_accumulate_grad_hook"}
 
-_depth = [0]
+_grad_enabled = torch.is_grad_enabled  # captured before init() patches torch.*
+_local = threading.local()
+_seq = itertools.count(1)
 _wrapped = set()
+BACKWARD_MARKERS = True
+
+
+def _depth():
+    return getattr(_local, "depth", 0)
 
 
 def isfunc(mod, f):
@@ -50,12 +72,16 @@ def isfunc(mod, f):
 
 
 def describe(x, name=""):
+    """Argument description carried in the marker (shapes, dtypes, scalar values)."""
     if isinstance(x, torch.Tensor):
         return {"name": name, "type": "tensor", "shape": tuple(x.shape), "dtype": str(x.dtype).split(".")[-1]}
-    if isinstance(x, (int, float, bool)):
+    if isinstance(x, (bool, int, float)):
         return {"name": name, "type": type(x).__name__, "value": x}
-    if isinstance(x, (list, tuple)):
-        return {"name": name, "type": type(x).__name__, "value": [describe(e) for e in x]}
+    if isinstance(x, str):
+        return {"name": name, "type": "str", "value": x}
+    if isinstance(x, (list, tuple, torch.Size)):
+        return {"name": name, "type": "tuple" if isinstance(x, (tuple, torch.Size)) else "list",
+                "value": [describe(e) for e in x]}
     if x is None:
         return {"name": name, "type": "NoneType", "value": None}
     if isinstance(x, torch.dtype):
@@ -79,8 +105,42 @@ def _pop(handle):
         _nvtx.range_pop()
 
 
+def _outputs(out):
+    if isinstance(out, torch.Tensor):
+        yield out
+    elif isinstance(out, (list, tuple)):
+        for o in out:
+            yield from _outputs(o)
+
+
+def _attach_backward(out, desc):
+    """Bracket the backward node(s) that produce this op's input grads with a bprop range."""
+    seen = set()
+    text = str(dict(desc, dir="bprop"))
+    for t in _outputs(out):
+        fn = t.grad_fn if t.requires_grad else None
+        if fn is None or id(fn) in seen:
+            continue
+        seen.add(id(fn))
+        handles = []
+
+        def pre(_grad_outputs, _handles=handles):
+            _handles.append(_push(text))
+
+        def post(_grad_inputs, _grad_outputs, _handles=handles):
+            if _handles:
+                _pop(_handles.pop())
+
+        try:
+            fn.register_prehook(pre)
+            fn.register_hook(post)
+        except (AttributeError, RuntimeError):  # pragma: no cover - exotic grad_fns
+            pass
+
+
 def add_wrapper(mod, fn_name):
-    """Wrap ``mod.fn_name`` so each call is one marker range carrying its argument description."""
+    """Wrap ``mod.fn_name`` so each call is one marker range carrying its argument description
+    (and, when its outputs require grad, a matching backward range)."""
     key = (id(mod), fn_name)
     if key in _wrapped:
         return
@@ -89,25 +149,51 @@ def add_wrapper(mod, fn_name):
 
     @functools.wraps(func)
     def wrapper(*args, **kwargs):
-        if _depth[0] > 0:  # only the outermost torch call of a nest is annotated
+        if _depth() > 0:  # only the outermost torch call of a nest is annotated
             return func(*args, **kwargs)
         stack = traceback.extract_stack()[:-1]
         trace = ["{}:{}".format(f.filename, f.lineno) for f in stack[-4:]]
-        desc = {"mod": mod_name, "op": fn_name, "args": [describe(a) for a in args] +
-                [describe(v, k) for k, v in kwargs.items()], "traceMarker": trace}
+        desc = {"mod": mod_name, "op": fn_name, "dir": "fprop", "seqId": next(_seq),
+                "args": [describe(a) for a in args] + [describe(v, k) for k, v in kwargs.items()],
+                "traceMarker": trace}
         if fn_name == "forward" and args and hasattr(args[0], "extra_repr"):
             desc["strRepr"] = args[0].extra_repr()
             desc["args"] = desc["args"][1:]
         h = _push(str(desc))
-        _depth[0] += 1
+        _local.depth = _depth() + 1
         try:
-            return func(*args, **kwargs)
+            out = func(*args, **kwargs)
         finally:
-            _depth[0] -= 1
+            _local.depth -= 1
             _pop(h)
+        if BACKWARD_MARKERS and _grad_enabled():
+            _attach_backward(out, desc)
+        return out
 
     setattr(mod, fn_name, wrapper)
     _wrapped.add(key)
+
+
+def wrap(mod, fn_name):
+    """Annotate a user function / custom module function (reference ``pyprof.nvtx.wrap``)."""
+    add_wrapper(mod, fn_name)
+
+
+class layer(contextlib.ContextDecorator):
+    """``with layer("encoder.3"):`` or ``@layer("attn")``: a user annotation that the parse
+    stage reports as the kernel's layer path."""
+
+    def __init__(self, name):
+        self.name = name
+        self._h = None
+
+    def __enter__(self):
+        self._h = _push("layer:" + str(self.name))
+        return self
+
+    def __exit__(self, *exc):
+        _pop(self._h)
+        return False
 
 
 def init():
@@ -123,3 +209,10 @@ def init():
         cls = getattr(torch.nn, name)
         if inspect.isclass(cls) and issubclass(cls, torch.nn.Module) and "forward" in cls.__dict__:
             add_wrapper(cls, "forward")
+    # this package's multi-tensor entry points (fused optimizers, amp unscale, norms): their
+    # markers carry the tensor lists, which the optim models price
+    from ... import amp_C
+
+    for name in getattr(amp_C, "__all__", []):
+        if name.startswith("multi_tensor"):
+            add_wrapper(amp_C, name)

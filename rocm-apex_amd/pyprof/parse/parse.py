@@ -140,9 +140,33 @@ def attach_markers(kernels, markers, api):
         ranges = by_tid.get(tid, any_tid)
         starts = [r[0] for r in ranges]
         i = bisect.bisect_right(starts, t)
-        enclosing = [r for r in ranges[max(0, i - 64):i] if r[0] <= t <= r[1]]
+        enclosing = [r for r in ranges[max(0, i - 256):i] if r[0] <= t <= r[1]]
         k["markers"] = [r[2] for r in enclosing]
-        k["marker"] = min(enclosing, key=lambda r: r[1] - r[0])[2] if enclosing else None
+        k["ranges"] = enclosing
+    return split_markers(kernels)
+
+
+def _is_layer(text):
+    return isinstance(text, str) and text.startswith("layer:")
+
+
+def split_markers(kernels):
+    """Per kernel: the innermost op marker (ignoring ``layer:`` annotations), the enclosing
+    layer path, and the sub-index of the kernel among those launched inside the same op range."""
+    counters = {}
+    for k in kernels:
+        ranges = k.get("ranges", [])
+        ops = [r for r in ranges if not _is_layer(r[2])]
+        layers = sorted((r for r in ranges if _is_layer(r[2])), key=lambda r: r[0])
+        k["layer"] = [r[2][len("layer:"):] for r in layers]
+        if ops:
+            inner = min(ops, key=lambda r: r[1] - r[0])
+            k["marker"] = inner[2]
+            key = (k.get("tid"), inner[0], inner[2])
+            k["sub"] = counters.get(key, 0)
+            counters[key] = k["sub"] + 1
+        else:
+            k["marker"], k["sub"] = None, 0
     return kernels
 
 
@@ -170,7 +194,9 @@ def parse(path):
         m = decode_marker(k["marker"])
         out.append({"index": i, "kName": k["name"], "kStartTime": k["start"], "kEndTime": k["end"],
                     "kDuration": k["end"] - k["start"], "grid": k["grid"], "block": k["block"],
-                    "device": k["device"], "stream": k["stream"], "mod": m.get("mod", ""), "op": m.get("op", ""),
+                    "device": k["device"], "stream": k["stream"], "tid": k.get("tid", -1),
+                    "mod": m.get("mod", ""), "op": m.get("op", ""), "dir": m.get("dir", "fprop" if m else ""),
+                    "seqId": m.get("seqId", -1), "sub": k.get("sub", 0), "layer": k.get("layer", []),
                     "args": m.get("args", []), "strRepr": m.get("strRepr", ""),
                     "trace": m.get("traceMarker", []), "marker": k["marker"]})
     return out

@@ -1,2 +1,4 @@
 """FLOP / byte report (reference apex/pyprof/prof)."""
-from .prof import annotate, main, render  # noqa: F401
+from .ops import model, model_for  # noqa: F401
+from .output import render, summary  # noqa: F401
+from .prof import annotate, main  # noqa: F401

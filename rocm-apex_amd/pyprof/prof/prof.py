@@ -1,30 +1,32 @@
-"""Second stage of pyprof (reference apex/pyprof/prof/prof.py + output.py): read the parse
-stage's per-kernel records, attach FLOP / byte estimates from the op models and print a
-columned table or CSV.
+"""Second stage of pyprof (reference apex/pyprof/prof/prof.py:171-256): read the parse stage's
+per-kernel records, price each with its op model (FLOPs, bytes, parameters, MFMA use) and print
+a columned table, CSV, or an aggregate summary.
 
-``python -m apex.pyprof.prof [-c idx,op,kernel,sil,flops,bytes] [--csv] [-w 160] parsed.txt``
-(``parsed.txt`` = the output of ``python -m apex.pyprof.parse``; ``-`` reads stdin)."""
-import argparse
+``python -m apex.pyprof.prof [-c idx,dir,op,kernel,params,sil,tc,flops,bytes] [--csv | -w N]
+[--summary op] parsed.txt``"""
 import ast
-import sys
 
-from .ops import model_for
-
-COLUMNS = {
-    "idx": ("Idx", "index", 6), "mod": ("Module", "mod", 14), "op": ("Op", "op", 18),
-    "kernel": ("Kernel", "kName", 0), "params": ("Params", "params", 0), "sil": ("Sil(ns)", "kDuration", 10),
-    "grid": ("Grid", "grid", 14), "block": ("Block", "block", 12), "stream": ("Stream", "stream", 6),
-    "device": ("Device", "device", 6), "flops": ("FLOPs", "flops", 14), "bytes": ("Bytes", "bytes", 14),
-    "tflops": ("TFLOP/s", "tflops", 9), "gbps": ("GB/s", "gbps", 9),
-}
+from .base import param_string
+from .ops import model
+from .output import render, summary
+from .usage import parse_args
 
 
 def annotate(rec):
-    flops, nbytes, params = model_for(rec)
-    rec["flops"], rec["bytes"], rec["params"] = flops, nbytes, params
-    dur = max(1, int(rec.get("kDuration", 0)))
-    rec["tflops"] = "{:.1f}".format(flops / dur / 1e3) if flops else "-"
-    rec["gbps"] = "{:.0f}".format(nbytes / dur) if nbytes else "-"
+    """Attach flops / bytes / params / tc / achieved rates to one parsed record (in place)."""
+    if rec.get("op"):
+        m = model(rec)
+        rec["flops"], rec["bytes"] = m.flops(), m.bytes()
+        rec["params"], rec["tc"], rec["kind"] = param_string(m.params()), m.tc(), m.kind
+    else:  # kernel outside any annotated op
+        rec["flops"], rec["bytes"], rec["params"], rec["tc"], rec["kind"] = 0, 0, "", "-", "-"
+    dur = max(1, int(rec.get("kDuration", 0) or 0))
+    rec["tflops"] = "{:.1f}".format(rec["flops"] / dur / 1e3) if rec["flops"] else "-"
+    rec["gbps"] = "{:.0f}".format(rec["bytes"] / dur) if rec["bytes"] else "-"
+    rec["layerStr"] = "/".join(rec.get("layer", []) or [])
+    rec["traceStr"] = ";".join((rec.get("trace", []) or [])[-1:])
+    rec["gridStr"] = ",".join(str(x) for x in rec.get("grid", ()))
+    rec["blockStr"] = ",".join(str(x) for x in rec.get("block", ()))
     return rec
 
 
@@ -35,31 +37,11 @@ def read_records(f):
             yield ast.literal_eval(line)
 
 
-def render(records, cols, csv=False, width=0):
-    out = []
-    if csv:
-        out.append(",".join(COLUMNS[c][0] for c in cols))
-        for r in records:
-            out.append(",".join('"{}"'.format(r.get(COLUMNS[c][1], "")) for c in cols))
-        return "\n".join(out)
-    fixed = sum(COLUMNS[c][2] for c in cols)
-    flex = [c for c in cols if COLUMNS[c][2] == 0]
-    fw = max(20, (width - fixed) // max(1, len(flex))) if width else 60
-    widths = [COLUMNS[c][2] or fw for c in cols]
-    out.append(" ".join(COLUMNS[c][0].ljust(w) for c, w in zip(cols, widths)))
-    for r in records:
-        out.append(" ".join(str(r.get(COLUMNS[c][1], ""))[:w].ljust(w) for c, w in zip(cols, widths)))
-    return "\n".join(out)
-
-
 def main(argv=None):
-    ap = argparse.ArgumentParser(description="per-kernel FLOP / byte report from apex.pyprof.parse output")
-    ap.add_argument("file", nargs="?", default="-")
-    ap.add_argument("-c", default="idx,mod,op,kernel,sil,flops,bytes,tflops")
-    ap.add_argument("--csv", action="store_true")
-    ap.add_argument("-w", type=int, default=180)
-    a = ap.parse_args(argv)
-    f = sys.stdin if a.file == "-" else open(a.file)
-    recs = [annotate(r) for r in read_records(f)]
-    print(render(recs, a.c.split(","), a.csv, a.w))
+    a = parse_args(argv)
+    recs = [annotate(r) for r in read_records(a.file)]
+    if a.summary:
+        print(summary(recs, a.summary, a.top))
+    else:
+        print(render(recs, a.c, a.csv, a.w))
     return 0

@@ -6,6 +6,7 @@
 #   bench      1-GPU headline bench (BENCH_ARGS appended)
 #   syncbn2    2 ranks sharing the GPU, gloo, --sync-bn (fused bn_group=world over peer memory)
 #   prof       rocprofv3 --kernel-trace --stats of a short bench (after the APEX_BENCH_MARK spin)
+#   pyprof     rocprofv3 marker + kernel trace of examples/pyprof/lenet.py through apex.pyprof parse/prof
 #   script     python $SCRIPT (a tools/ micro-benchmark), output to gpurun_out/script.log
 # Test failures (rc 1) do not stop the chain; anything >= 2 does.
 mkdir -p gpurun_out
@@ -39,6 +40,16 @@ for s in ${STEPS:-tests smoke bench}; do
     python tools/prof_summary.py gpurun_out/prof_bench/bench_results.db --after spin_kernel --steps 10 --top 60 \
       --md gpurun_out/prof_summary.md --title "${PROF_TITLE:-ResNet-50 bench kernel trace}" > /dev/null 2>&1
     head -12 gpurun_out/prof_summary.md; rm -rf gpurun_out/prof_bench ;;
+  pyprof)
+    # apex.pyprof end to end: roctx op markers (fwd + bwd) -> rocprofv3 -> parse -> prof
+    cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --marker-trace --hip-runtime-trace --output-format csv \
+      -d $R/gpurun_out/pyprof_trace -o run -- python3 $R/examples/pyprof/lenet.py > $R/gpurun_out/pyprof_run.log 2>&1
+    rc=$?; cd $R; tail -2 gpurun_out/pyprof_run.log; [ $rc -ne 0 ] && stop pyprof $rc
+    python -m apex.pyprof.parse gpurun_out/pyprof_trace > gpurun_out/pyprof_parsed.txt && \
+      python -m apex.pyprof.prof -c idx,dir,sub,layer,mod,op,kernel,params,sil,tc,flops,bytes -w 240 \
+        gpurun_out/pyprof_parsed.txt > gpurun_out/pyprof_report.txt && \
+      python -m apex.pyprof.prof --summary op gpurun_out/pyprof_parsed.txt > gpurun_out/pyprof_summary.txt
+    rc=$?; head -20 gpurun_out/pyprof_summary.txt; rm -rf gpurun_out/pyprof_trace; [ $rc -ne 0 ] && stop pyprof_post $rc ;;
   script)
     timeout -k 10 ${SCRIPT_TIMEOUT:-400} python $SCRIPT > gpurun_out/script.log 2>&1
     rc=$?; tail -20 gpurun_out/script.log; [ $rc -ne 0 ] && stop script $rc ;;
