@@ -15,8 +15,9 @@ a post-hook on the ``grad_fn`` of the op's outputs, so the backward node runs in
 with the SAME description, ``'dir': 'bprop'`` and the same ``seqId``.  The kernels the autograd
 thread launches for it are therefore attributed directly, with no sequence matching.
 
-``layer(name)`` (context manager / decorator) pushes ``layer:<name>`` ranges; the parse stage
-reports the enclosing layer path of every kernel (reference "layer" column).  ``wrap(mod, fn)``
+``layer(name)`` (context manager / decorator) pushes ``layer:<name>`` ranges and records the
+layer path in every op marker opened inside it, so backward kernels (which run outside the
+user's ``with`` block) still report the layer of their forward op (reference "layer" column).  ``wrap(mod, fn)``
 annotates a user function the same way (reference ``pyprof.nvtx.wrap``).  Without roctx (CPU
 builds) the ranges go to ``torch.autograd.profiler.record_function`` instead."""
 import contextlib
@@ -154,6 +155,7 @@ def add_wrapper(mod, fn_name):
         stack = traceback.extract_stack()[:-1]
         trace = ["{}:{}".format(f.filename, f.lineno) for f in stack[-4:]]
         desc = {"mod": mod_name, "op": fn_name, "dir": "fprop", "seqId": next(_seq),
+                "layer": list(getattr(_local, "layers", ())),
                 "args": [describe(a) for a in args] + [describe(v, k) for k, v in kwargs.items()],
                 "traceMarker": trace}
         if fn_name == "forward" and args and hasattr(args[0], "extra_repr"):
@@ -189,9 +191,11 @@ class layer(contextlib.ContextDecorator):
 
     def __enter__(self):
         self._h = _push("layer:" + str(self.name))
+        _local.layers = getattr(_local, "layers", ()) + (str(self.name),)
         return self
 
     def __exit__(self, *exc):
+        _local.layers = getattr(_local, "layers", ())[:-1]
         _pop(self._h)
         return False
 

@@ -196,7 +196,7 @@ def parse(path):
                     "kDuration": k["end"] - k["start"], "grid": k["grid"], "block": k["block"],
                     "device": k["device"], "stream": k["stream"], "tid": k.get("tid", -1),
                     "mod": m.get("mod", ""), "op": m.get("op", ""), "dir": m.get("dir", "fprop" if m else ""),
-                    "seqId": m.get("seqId", -1), "sub": k.get("sub", 0), "layer": k.get("layer", []),
+                    "seqId": m.get("seqId", -1), "sub": k.get("sub", 0), "layer": m.get("layer") or k.get("layer", []),
                     "args": m.get("args", []), "strRepr": m.get("strRepr", ""),
                     "trace": m.get("traceMarker", []), "marker": k["marker"]})
     return out

@@ -30,6 +30,23 @@ def annotate(rec):
     return rec
 
 
+def attribute_to_main_kernel(records):
+    """An op launches several kernels (fills, transposes, the GEMM, a reduction); its modelled
+    FLOPs / bytes are charged once, to the longest kernel of the op instance (same thread,
+    seqId and direction), so per-kernel rates and aggregates are not multiplied."""
+    groups = {}
+    for r in records:
+        if r.get("op") and r.get("seqId", -1) >= 0:
+            groups.setdefault((r.get("tid"), r.get("seqId"), r.get("dir")), []).append(r)
+    for rs in groups.values():
+        main = max(rs, key=lambda r: int(r.get("kDuration", 0) or 0))
+        for r in rs:
+            if r is not main:
+                r["flops"] = r["bytes"] = 0
+                r["tflops"] = r["gbps"] = "-"
+    return records
+
+
 def read_records(f):
     for line in f:
         line = line.strip()
@@ -39,7 +56,7 @@ def read_records(f):
 
 def main(argv=None):
     a = parse_args(argv)
-    recs = [annotate(r) for r in read_records(a.file)]
+    recs = attribute_to_main_kernel([annotate(r) for r in read_records(a.file)])
     if a.summary:
         print(summary(recs, a.summary, a.top))
     else:

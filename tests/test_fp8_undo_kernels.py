@@ -101,9 +101,10 @@ def test_adam_undo_restores_pre_step_state_gpu(mode, with_out):
     ref.multi_tensor_adam_undo(65536, _noop(), cp, *args)
     amp_C.multi_tensor_adam_undo(65536, _noop(), lists, *args)
     for (p0, m0, v0), p, m, v, rp, rm, rv in zip(before, ps, ms, vs, cp[1], cp[2], cp[3]):
+        # kernel vs torch math: fma contraction differs, and (m - (1-b1) g) / b1 cancels
         torch.testing.assert_close(p, rp, rtol=1e-6, atol=1e-7)
-        torch.testing.assert_close(m, rm, rtol=1e-5, atol=1e-8)
-        torch.testing.assert_close(v, rv, rtol=1e-4, atol=1e-10)
+        torch.testing.assert_close(m, rm, rtol=1e-4, atol=1e-7)
+        torch.testing.assert_close(v, rv, rtol=1e-3, atol=1e-9)
         torch.testing.assert_close(p, p0, rtol=1e-6, atol=1e-6)
         torch.testing.assert_close(m, m0, rtol=1e-4, atol=1e-7)
         torch.testing.assert_close(v, v0, rtol=1e-3, atol=1e-8)
