@@ -12,8 +12,19 @@ import os
 _C = None
 import_error = None
 try:
-    _C = importlib.import_module(__package__ + "._C")
+    _variant = os.environ.get("APEX_AMD_NATIVE_SO")  # A/B experiments: a variant build's .so
+    if _variant:
+        import importlib.util
+        import sys
+
+        _spec = importlib.util.spec_from_file_location(__package__ + "._C", _variant)
+        _C = importlib.util.module_from_spec(_spec)
+        _spec.loader.exec_module(_C)
+        sys.modules[__package__ + "._C"] = _C
+    else:
+        _C = importlib.import_module(__package__ + "._C")
 except Exception as e:  # pragma: no cover - depends on build state
+    _C = None
     import_error = e
 
 ALLOW_FALLBACK = os.environ.get("APEX_AMD_ALLOW_FALLBACK", "0") == "1"

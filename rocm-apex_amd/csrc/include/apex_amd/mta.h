@@ -31,7 +31,12 @@ struct MtaMeta {
 
 template <typename T>
 __device__ __forceinline__ T* mta_ptr(const MtaMeta& m, int d, int t, int64_t start) {
-  return reinterpret_cast<T*>(m.ptrs[(size_t)d * m.ntensors + t]) + start;
+  // the table holds plain addresses; going through a global (addrspace 1) pointer lets the
+  // compiler's address-space inference emit global_load/store instead of flat_* (flat ops also
+  // count against lgkmcnt, which serialises them with LDS traffic)
+  using GT = __attribute__((address_space(1))) T;
+  GT* g = (GT*)(m.ptrs[(size_t)d * m.ntensors + t]);
+  return (T*)(g + start);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -48,11 +53,60 @@ template <int I, typename T0, typename... Ts> struct TypeAt<I, T0, Ts...> {
   using type = typename TypeAt<I - 1, Ts...>::type;
 };
 
+// Streaming IO for the multi-tensor ops.  APEX_MTA_NT=1 (variant build) issues the loads /
+// stores as nontemporal (the data is touched once per step); the default is plain vector IO.
+#ifndef APEX_MTA_NT
+#define APEX_MTA_NT 0
+#endif
+#ifndef APEX_MTA_ILP
+#define APEX_MTA_ILP 1
+#endif
+#ifndef APEX_MTA_NOFENCE_EXPERIMENT
+#define APEX_MTA_NOFENCE_EXPERIMENT 0
+#endif
+#ifndef APEX_MTA_RED_UNROLL
+#define APEX_MTA_RED_UNROLL 1
+#endif
+typedef unsigned mta_u4 __attribute__((ext_vector_type(4)));
+typedef unsigned mta_u2 __attribute__((ext_vector_type(2)));
+
+template <typename T>
+struct MtaIO {
+  static constexpr int kBytes = (int)sizeof(T) * kVec;
+  static __device__ __forceinline__ void load(float (&r)[kVec], const T* p) {
+    if constexpr (!APEX_MTA_NT) {
+      Vec8<T>::load(r, p);
+    } else if constexpr (kBytes >= 16) {
+      mta_u4 buf[kBytes / 16];
+#pragma unroll
+      for (int i = 0; i < kBytes / 16; ++i) buf[i] = __builtin_nontemporal_load(reinterpret_cast<const mta_u4*>(p) + i);
+      Vec8<T>::load(r, reinterpret_cast<const T*>(buf));
+    } else {
+      mta_u2 buf = __builtin_nontemporal_load(reinterpret_cast<const mta_u2*>(p));
+      Vec8<T>::load(r, reinterpret_cast<const T*>(&buf));
+    }
+  }
+  static __device__ __forceinline__ void store(T* p, const float (&r)[kVec]) {
+    if constexpr (!APEX_MTA_NT) {
+      Vec8<T>::store(p, r);
+    } else if constexpr (kBytes >= 16) {
+      mta_u4 buf[kBytes / 16];
+      Vec8<T>::store(reinterpret_cast<T*>(buf), r);
+#pragma unroll
+      for (int i = 0; i < kBytes / 16; ++i) __builtin_nontemporal_store(buf[i], reinterpret_cast<mta_u4*>(p) + i);
+    } else {
+      mta_u2 buf;
+      Vec8<T>::store(reinterpret_cast<T*>(&buf), r);
+      __builtin_nontemporal_store(buf, reinterpret_cast<mta_u2*>(p));
+    }
+  }
+};
+
 template <typename Op, int D, int I, typename... Ts>
 struct ListIO {
   using T = typename TypeAt<I, Ts...>::type;
   static __device__ __forceinline__ void load_vec(float (&r)[D][kVec], void* const (&base)[D], int i) {
-    if constexpr ((Op::kRead >> I) & 1u) Vec8<T>::load(r[I], reinterpret_cast<const T*>(base[I]) + i);
+    if constexpr ((Op::kRead >> I) & 1u) MtaIO<T>::load(r[I], reinterpret_cast<const T*>(base[I]) + i);
     else {
 #pragma unroll
       for (int k = 0; k < kVec; ++k) r[I][k] = 0.f;
@@ -60,7 +114,7 @@ struct ListIO {
     if constexpr (I + 1 < D) ListIO<Op, D, I + 1, Ts...>::load_vec(r, base, i);
   }
   static __device__ __forceinline__ void store_vec(const float (&r)[D][kVec], void* const (&base)[D], int i) {
-    if constexpr ((Op::kWrite >> I) & 1u) Vec8<T>::store(reinterpret_cast<T*>(base[I]) + i, r[I]);
+    if constexpr ((Op::kWrite >> I) & 1u) MtaIO<T>::store(reinterpret_cast<T*>(base[I]) + i, r[I]);
     if constexpr (I + 1 < D) ListIO<Op, D, I + 1, Ts...>::store_vec(r, base, i);
   }
   static __device__ __forceinline__ void load_one(float (&r)[D][1], void* const (&base)[D], int i) {
@@ -117,7 +171,31 @@ __global__ void __launch_bounds__(kMtaBlock) mta_elementwise_kernel(MtaMeta meta
 #pragma unroll
     for (int a = 0; a < (NA > 0 ? NA : 1); ++a) acc[a] = 0.f;
     const int nvec = meta.aligned ? (len / kVec) : 0;
-    for (int v = threadIdx.x; v < nvec; v += kMtaBlock) {
+    int v = threadIdx.x;
+    if constexpr (APEX_MTA_ILP > 1) {
+      // two vectors per thread per trip: both loads are in flight before either is stored
+      for (; v + kMtaBlock < nvec; v += 2 * kMtaBlock) {
+        float r0[D][kVec], r1[D][kVec];
+        ListIO<Op, D, 0, Ts...>::load_vec(r0, base, v * kVec);
+        ListIO<Op, D, 0, Ts...>::load_vec(r1, base, (v + kMtaBlock) * kVec);
+        op.template apply<kVec>(r0, ts, bad, acc);
+        op.template apply<kVec>(r1, ts, bad, acc);
+        ListIO<Op, D, 0, Ts...>::store_vec(r0, base, v * kVec);
+        ListIO<Op, D, 0, Ts...>::store_vec(r1, base, (v + kMtaBlock) * kVec);
+      }
+    }
+    if constexpr (Op::kWrite == 0 && APEX_MTA_RED_UNROLL > 1) {
+      // read-only ops (norms, finite checks): several independent loads in flight per lane
+      constexpr int U = APEX_MTA_RED_UNROLL;
+      for (; v + (U - 1) * kMtaBlock < nvec; v += U * kMtaBlock) {
+        float r[U][D][kVec];
+#pragma unroll
+        for (int u = 0; u < U; ++u) ListIO<Op, D, 0, Ts...>::load_vec(r[u], base, (v + u * kMtaBlock) * kVec);
+#pragma unroll
+        for (int u = 0; u < U; ++u) op.template apply<kVec>(r[u], ts, bad, acc);
+      }
+    }
+    for (; v < nvec; v += kMtaBlock) {
       float r[D][kVec];
       ListIO<Op, D, 0, Ts...>::load_vec(r, base, v * kVec);
       op.template apply<kVec>(r, ts, bad, acc);
@@ -177,12 +255,16 @@ __device__ __forceinline__ bool mta_last_block(unsigned* ticket, int* smem_flag)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
+#if !APEX_MTA_NOFENCE_EXPERIMENT  // timing experiment only: results are not guaranteed without the fences
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int last = (prev == gridDim.x - 1);
     if (last) {
+#if !APEX_MTA_NOFENCE_EXPERIMENT
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     *smem_flag = last;

@@ -104,10 +104,10 @@ def test_adam_undo_restores_pre_step_state_gpu(mode, with_out):
         # kernel vs torch math: fma contraction differs, and (m - (1-b1) g) / b1 cancels
         torch.testing.assert_close(p, rp, rtol=1e-6, atol=1e-7)
         torch.testing.assert_close(m, rm, rtol=1e-4, atol=1e-7)
-        torch.testing.assert_close(v, rv, rtol=1e-3, atol=1e-9)
+        torch.testing.assert_close(v, rv, rtol=1e-3, atol=3e-8)
         torch.testing.assert_close(p, p0, rtol=1e-6, atol=1e-6)
         torch.testing.assert_close(m, m0, rtol=1e-4, atol=1e-7)
-        torch.testing.assert_close(v, v0, rtol=1e-3, atol=1e-8)
+        torch.testing.assert_close(v, v0, rtol=1e-3, atol=3e-8)
     if with_out:
         for p, o in zip(ps, outs):
             assert torch.equal(o, p.to(torch.bfloat16))

@@ -122,14 +122,14 @@ def obj_for(src: str, build_dir: str = BUILD) -> str:
     return os.path.join(build_dir, rel + ".o")
 
 
-def compile_cmds(verbose: bool, extensions=None, out=None, build_dir=BUILD):
+def compile_cmds(verbose: bool, extensions=None, out=None, build_dir=BUILD, defines=()):
     tdir, tinc, abi = torch_paths()
     py_inc = sysconfig.get_paths()["include"]
     hip, cpp = sources(extensions)
     present = {os.path.basename(p) for p in cpp}
     macros = [f"-D{m}" for f, m in SUBSYSTEMS.items() if f in present]
     common = ["-std=c++17", "-O3", "-fPIC", f"-I{os.path.join(CSRC, 'include')}", "-Wno-unused-result",
-              "-Wno-deprecated-declarations", "-Wno-unused-command-line-argument"]
+              "-Wno-deprecated-declarations", "-Wno-unused-command-line-argument", *[f"-D{d}" for d in defines]]
     dev = [HIPCC, *common, f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-ffp-contract=fast",
            "--no-offload-compress", "-x", "hip"]
     host = [HIPCC, *common, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_EXTENSION_NAME=_C",
@@ -156,14 +156,17 @@ def run(cmd, verbose):
 
 
 def build(jobs_n: int | None = None, clean: bool = False, verbose: bool = False, extensions=None,
-          out=None) -> str:
+          out=None, defines=()) -> str:
     names = selected_extensions(extensions)
-    # a partial selection gets its own object dir so it never poisons the full build's objects
+    # a partial selection / extra defines get their own object dir so they never poison the
+    # full build's objects
     build_dir = BUILD if names == sorted(EXTENSIONS) else os.path.join(BUILD, "sel_" + "_".join(names))
+    if defines:
+        build_dir = os.path.join(build_dir, "def_" + "_".join(d.replace("=", "-") for d in sorted(defines)))
     if clean and os.path.isdir(build_dir):
         shutil.rmtree(build_dir)
     os.makedirs(build_dir, exist_ok=True)
-    jobs, link = compile_cmds(verbose, extensions, out, build_dir)
+    jobs, link = compile_cmds(verbose, extensions, out, build_dir, tuple(defines))
     hdr = newest_header()
     # module.cpp's registrations depend on which subsystem bindings exist (-D macros): rebuild it
     # whenever that set changes
@@ -216,9 +219,13 @@ def main(argv=None):
     ap.add_argument("--verbose", "-v", action="store_true")
     ap.add_argument("--extensions", default=None, help="comma list of " + ",".join(sorted(EXTENSIONS)))
     ap.add_argument("--out", default=None, help="output .so path (default: in-tree)")
+    ap.add_argument("--define", "-D", action="append", default=[],
+                    help="extra preprocessor define for an A/B variant build (use with --out)")
     a = ap.parse_args(argv)
+    if a.define and not a.out:
+        ap.error("--define builds a variant: give it its own --out path")
     try:
-        build(a.j, a.clean, a.verbose, a.extensions, a.out)
+        build(a.j, a.clean, a.verbose, a.extensions, a.out, a.define)
     except RuntimeError as e:
         print(f"[build_native] {e}", file=sys.stderr)
         return 1

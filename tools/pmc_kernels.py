@@ -63,6 +63,15 @@ def main():
     rep(lambda: bn(xb))
     rep(lambda: torch.autograd.grad(yb, [xb, bn.weight, bn.bias], gb, retain_graph=True))
     del xb, yb, gb
+    # the small late-stage layers (latency-bound in the step profile)
+    for (nb, cb, hw) in ((256, 256, 14), (256, 2048, 7)):
+        xs = torch.randn(nb, cb, hw, hw, device="cuda", dtype=dt).to(memory_format=torch.channels_last)
+        xs.requires_grad_(True)
+        bns = BatchNorm2d_NHWC(cb, fuse_relu=True, torch_channels_last=True).cuda()
+        ys = bns(xs)
+        gs = torch.randn_like(ys)
+        rep(lambda: bns(xs))
+        rep(lambda: torch.autograd.grad(ys, [xs, bns.weight, bns.bias], gs, retain_graph=True))
 
     from apex import amp_C
     from apex.optimizers import FusedAdam
