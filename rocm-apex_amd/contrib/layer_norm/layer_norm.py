@@ -10,7 +10,7 @@ returns dgamma / dbeta in the parameter dtype."""
 import torch
 from torch.nn import init
 
-from ..._autocast_utils import _cast_if_autocast_enabled
+from ..._autocast_utils import _autocast_disabled, _cast_if_autocast_enabled
 from ...ops.layer_norm import ln_bwd, ln_fwd
 
 
@@ -35,7 +35,7 @@ class FastLayerNormFN(torch.autograd.Function):
 
 def _fast_layer_norm(x, weight, bias, epsilon):
     args = _cast_if_autocast_enabled(x, weight, bias, epsilon)
-    with torch.autocast("cuda", enabled=False):
+    with _autocast_disabled():
         return FastLayerNormFN.apply(*args)
 
 

@@ -119,7 +119,8 @@ MtaMeta mta_meta(const std::vector<std::vector<at::Tensor>>& lists, int chunk_si
   const size_t off_chunks = align8(off_ptrs + sizeof(uint64_t) * (size_t)depth * nt);
   const size_t off_first = align8(off_chunks + sizeof(int2) * (size_t)std::max(nchunks, 1));
   const size_t off_part = align8(off_first + sizeof(int) * (size_t)(nt + 1));
-  const size_t off_ticket = align8(off_part + sizeof(float) * 2 * (size_t)std::max(nchunks, 1));
+  const size_t off_stage = align8(off_part + sizeof(uint64_t) * 2 * (size_t)std::max(nchunks, 1));
+  const size_t off_ticket = align8(off_stage + sizeof(float) * 2 * (size_t)std::max(nchunks, 1));
   const size_t bytes = off_ticket + 64;
 
   auto host = at::zeros({(int64_t)bytes}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
@@ -148,8 +149,10 @@ MtaMeta mta_meta(const std::vector<std::vector<at::Tensor>>& lists, int chunk_si
   m.ptrs = reinterpret_cast<const uint64_t*>(db + off_ptrs);
   m.chunks = reinterpret_cast<const int2*>(db + off_chunks);
   m.first_chunk = reinterpret_cast<const int*>(db + off_first);
-  m.partials = reinterpret_cast<float*>(db + off_part);
+  m.partials = reinterpret_cast<uint64_t*>(db + off_part);
+  m.stage = reinterpret_cast<float*>(db + off_stage);
   m.ticket = reinterpret_cast<unsigned*>(db + off_ticket);
+  m.epoch = reinterpret_cast<unsigned*>(db + off_ticket + 4);
   m.ntensors = nt;
   m.nchunks = nchunks;
   m.chunk_size = chunk_size;

@@ -20,8 +20,10 @@ struct MtaMeta {
   const uint64_t* ptrs;   // [depth][ntensors] base addresses
   const int2* chunks;     // [nchunks] {tensor index, chunk index within tensor}
   const int* first_chunk; // [ntensors + 1] prefix of chunk counts (chunks of a tensor are contiguous)
-  float* partials;        // [2 * nchunks] scratch for per-chunk reductions
+  uint64_t* partials;     // [2 * nchunks] tagged per-chunk partials: (launch tag << 32) | float bits
+  float* stage;           // [2 * nchunks] the finalizing block's verified copy of the partials
   unsigned* ticket;       // arrival counter for single-pass grid reductions (reset by last block)
+  unsigned* epoch;        // tag of the previous launch over this table (bumped by the last block)
   int ntensors;
   int nchunks;
   int chunk_size;
@@ -60,9 +62,6 @@ template <int I, typename T0, typename... Ts> struct TypeAt<I, T0, Ts...> {
 #endif
 #ifndef APEX_MTA_ILP
 #define APEX_MTA_ILP 1
-#endif
-#ifndef APEX_MTA_NOFENCE_EXPERIMENT
-#define APEX_MTA_NOFENCE_EXPERIMENT 0
 #endif
 #ifndef APEX_MTA_RED_UNROLL
 #define APEX_MTA_RED_UNROLL 1
@@ -133,10 +132,12 @@ struct ListIO {
 };
 
 // ---------------------------------------------------------------------------------------------
-// Single-pass grid reduction support: every block writes its partial(s), the last arriving
-// block (agent-scope release/acquire ticket, cdna_hip_programming.md Guideline 16) finalizes.
+// Single-pass grid reduction support: every block writes its partial(s) as tagged agent-scope
+// atomics, takes a ticket, and the last arriving block finalizes (mta_tensor_reduce below).
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ bool mta_last_block(unsigned* ticket, int* smem_flag);
+__device__ __forceinline__ void mta_put_partial(uint64_t* p, float v, unsigned tag);
+__device__ __forceinline__ void mta_collect_partials(const MtaMeta& m, int num_acc, unsigned tag);
 
 // Ops with kNumAcc > 0 accumulate per-element sums (or maxima when Op::kAccMax) which are
 // reduced per chunk into meta.partials; the last block then calls op.finalize(meta, smem).
@@ -159,6 +160,8 @@ __global__ void __launch_bounds__(kMtaBlock) mta_elementwise_kernel(MtaMeta meta
     }
   }
   bool bad = false;
+  unsigned tag = 0;
+  if constexpr (NA > 0) tag = __hip_atomic_load(meta.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   for (int w = blockIdx.x; w < meta.nchunks; w += gridDim.x) {
     const int2 tc = meta.chunks[w];
     const int64_t start = (int64_t)tc.y * meta.chunk_size;
@@ -213,7 +216,7 @@ __global__ void __launch_bounds__(kMtaBlock) mta_elementwise_kernel(MtaMeta meta
         float s = op.acc_is_max() ? block_max(acc[a], smem + a * (kMtaBlock / 64))
                                   : block_sum(acc[a], smem + a * (kMtaBlock / 64));
         if (threadIdx.x == 0) {
-          meta.partials[(size_t)a * meta.nchunks + w] = s;
+          mta_put_partial(meta.partials + (size_t)a * meta.nchunks + w, s, tag);
           if (Op::kCheckPartial && !is_finite(s)) bad = true;
         }
       }
@@ -222,8 +225,12 @@ __global__ void __launch_bounds__(kMtaBlock) mta_elementwise_kernel(MtaMeta meta
   if (bad) *noop = 1;  // benign race: every writer stores the same value
   if constexpr (NA > 0) {
     if (mta_last_block(meta.ticket, reinterpret_cast<int*>(&smem[kMtaBlock / 64 * 2]))) {
-      op.finalize(meta);
-      if (threadIdx.x == 0) __hip_atomic_store(meta.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      mta_collect_partials(meta, NA, tag);
+      op.finalize(meta, tag);
+      if (threadIdx.x == 0) {
+        __hip_atomic_store(meta.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(meta.epoch, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
 }
@@ -238,35 +245,55 @@ struct MtaOpBase {
   struct TS {};
   __device__ __forceinline__ TS tensor_state(int) const { return {}; }
   __device__ __forceinline__ bool acc_is_max() const { return false; }
-  __device__ __forceinline__ void finalize(const MtaMeta&) const {}
+  __device__ __forceinline__ void finalize(const MtaMeta&, unsigned) const {}
   __device__ __forceinline__ void finalize_skipped(const MtaMeta&) const {}
 };
 
 // Sum (or max) partial slot `a` over the chunks of tensor t, in chunk order (deterministic).
-__device__ __forceinline__ float mta_tensor_reduce(const MtaMeta& m, int a, int t, bool is_max) {
-  const float* p = m.partials + (size_t)a * m.nchunks;
+// Cross-XCD hand-off of the per-chunk partials without an L2 writeback: every partial is ONE
+// 64-bit agent-scope atomic word carrying its value and the launch tag, so it is self-validating
+// (no ordering between different locations is needed).  The finalizing block reads each word
+// with an agent-scope atomic load and re-reads until the tag matches this launch — normally
+// immediately, since every block's stores were acknowledged before it took its ticket.  An
+// agent-scope release fence instead writes back the whole XCD L2 per block (measured ~30 us on
+// a 1.5k-block norm).
+__device__ __forceinline__ void mta_put_partial(uint64_t* p, float v, unsigned tag) {
+  const uint64_t w = ((uint64_t)tag << 32) | (uint64_t)__float_as_uint(v);
+  __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ float mta_get_partial(const uint64_t* p, unsigned tag) {
+  uint64_t w = __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int spin = 0; (unsigned)(w >> 32) != tag && spin < (1 << 22); ++spin) {
+    __builtin_amdgcn_s_sleep(1);
+    w = __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return __uint_as_float((unsigned)(w & 0xffffffffu));
+}
+
+// Finalizing block, all threads: validate every tagged partial in parallel and stage the
+// values for the per-tensor sums (read back by this same block after the barrier).
+__device__ __forceinline__ void mta_collect_partials(const MtaMeta& m, int num_acc, unsigned tag) {
+  const int n = num_acc * m.nchunks;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) m.stage[i] = mta_get_partial(m.partials + i, tag);
+  __syncthreads();
+}
+
+__device__ __forceinline__ float mta_tensor_reduce(const MtaMeta& m, int a, int t, bool is_max, unsigned) {
+  const float* p = m.stage + (size_t)a * m.nchunks;
   float s = 0.f;
   for (int c = m.first_chunk[t]; c < m.first_chunk[t + 1]; ++c) s = is_max ? fmaxf(s, p[c]) : s + p[c];
   return s;
 }
 
 __device__ __forceinline__ bool mta_last_block(unsigned* ticket, int* smem_flag) {
-  // every storing wave drains its stores, then one lane publishes with an agent-scope release
+  // every storing wave drains its stores (the tagged partials are acknowledged) before the ticket
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-#if !APEX_MTA_NOFENCE_EXPERIMENT  // timing experiment only: results are not guaranteed without the fences
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#endif
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the partials are self-validating tagged atomics (mta_get_partial), so no fence here
     unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int last = (prev == gridDim.x - 1);
-    if (last) {
-#if !APEX_MTA_NOFENCE_EXPERIMENT
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
     *smem_flag = last;
   }
   __syncthreads();

@@ -131,12 +131,12 @@ struct NormOp {
       if constexpr (D == 2) r[1][k] = x * ts.s;
     }
   }
-  __device__ void finalize(const MtaMeta& m) const {
+  __device__ void finalize(const MtaMeta& m, unsigned tag) const {
     __shared__ float red[kMtaBlock / 64];
     const bool is_max = mode == 1;
     float mine = 0.f;
     for (int t = threadIdx.x; t < m.ntensors; t += blockDim.x) {
-      const float s = mta_tensor_reduce(m, 0, t, is_max);
+      const float s = mta_tensor_reduce(m, 0, t, is_max, tag);
       mine = is_max ? fmaxf(mine, s) : mine + s;
       if (per_tensor) {
         if (blend) {
@@ -536,10 +536,10 @@ struct LambStage1Op {
       r[3][k] = vv;
     }
   }
-  __device__ void finalize(const MtaMeta& m) const {
+  __device__ void finalize(const MtaMeta& m, unsigned tag) const {
     for (int t = threadIdx.x; t < m.ntensors; t += blockDim.x) {
-      a.param_norm[t] = sqrtf(mta_tensor_reduce(m, 0, t, false));
-      a.update_norm[t] = sqrtf(mta_tensor_reduce(m, 1, t, false));
+      a.param_norm[t] = sqrtf(mta_tensor_reduce(m, 0, t, false, tag));
+      a.update_norm[t] = sqrtf(mta_tensor_reduce(m, 1, t, false, tag));
     }
   }
   __device__ void finalize_skipped(const MtaMeta&) const {}

@@ -11,7 +11,7 @@ from torch.nn import functional as F
 from torch.nn import init
 from torch.nn.parameter import Parameter
 
-from .._autocast_utils import _cast_if_autocast_enabled
+from .._autocast_utils import _autocast_disabled, _cast_if_autocast_enabled
 from ..ops import layer_norm as lnops
 
 
@@ -109,37 +109,37 @@ class FusedRMSNormFunction(torch.autograd.Function):
 
 def fused_layer_norm_affine(input, weight, bias, normalized_shape, eps=1e-6):
     args = _cast_if_autocast_enabled(input, weight, bias, normalized_shape, eps)
-    with torch.autocast("cuda", enabled=False):
+    with _autocast_disabled():
         return FusedLayerNormAffineFunction.apply(*args)
 
 
 def fused_layer_norm(input, normalized_shape, eps=1e-6):
     args = _cast_if_autocast_enabled(input, normalized_shape, eps)
-    with torch.autocast("cuda", enabled=False):
+    with _autocast_disabled():
         return FusedLayerNormFunction.apply(*args)
 
 
 def mixed_dtype_fused_layer_norm_affine(input, weight, bias, normalized_shape, eps=1e-6):
     args = _cast_if_autocast_enabled(input, weight, bias, normalized_shape, eps)
-    with torch.autocast("cuda", enabled=False):
+    with _autocast_disabled():
         return FusedLayerNormAffineMixedDtypesFunction.apply(*args)
 
 
 def fused_rms_norm_affine(input, weight, normalized_shape, eps=1e-6):
     args = _cast_if_autocast_enabled(input, weight, normalized_shape, eps)
-    with torch.autocast("cuda", enabled=False):
+    with _autocast_disabled():
         return FusedRMSNormAffineFunction.apply(*args)
 
 
 def fused_rms_norm(input, normalized_shape, eps=1e-6):
     args = _cast_if_autocast_enabled(input, normalized_shape, eps)
-    with torch.autocast("cuda", enabled=False):
+    with _autocast_disabled():
         return FusedRMSNormFunction.apply(*args)
 
 
 def mixed_dtype_fused_rms_norm_affine(input, weight, normalized_shape, eps=1e-6):
     args = _cast_if_autocast_enabled(input, weight, normalized_shape, eps)
-    with torch.autocast("cuda", enabled=False):
+    with _autocast_disabled():
         return FusedRMSNormAffineMixedDtypesFunction.apply(*args)
 
 

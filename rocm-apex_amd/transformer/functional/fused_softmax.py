@@ -6,7 +6,7 @@ module works in the CPU test tier."""
 import torch
 
 from ... import _native
-from ..._autocast_utils import _cast_if_autocast_enabled
+from ..._autocast_utils import _autocast_disabled, _cast_if_autocast_enabled
 from ..enums import AttnMaskType
 
 MAX_FUSED_KEYS = 16384
@@ -58,7 +58,7 @@ def scaled_upper_triang_masked_softmax(inputs, _, scale):
     assert sq == sk, "causal mask is only for self attention"
     inputs = inputs.view(-1, sq, sk)
     args = _cast_if_autocast_enabled(inputs, scale)
-    with torch.autocast("cuda", enabled=False):
+    with _autocast_disabled():
         probs = ScaledUpperTriangMaskedSoftmax.apply(*args)
     return probs.view(b, np_, sq, sk)
 
@@ -86,7 +86,7 @@ class ScaledMaskedSoftmax(torch.autograd.Function):
 
 def scaled_masked_softmax(inputs, mask, scale):
     args = _cast_if_autocast_enabled(inputs, mask, scale)
-    with torch.autocast("cuda", enabled=False):
+    with _autocast_disabled():
         return ScaledMaskedSoftmax.apply(*args)
 
 
@@ -113,7 +113,7 @@ class ScaledSoftmax(torch.autograd.Function):
 
 def scaled_softmax(inputs, scale):
     args = _cast_if_autocast_enabled(inputs, scale)
-    with torch.autocast("cuda", enabled=False):
+    with _autocast_disabled():
         return ScaledSoftmax.apply(*args)
 
 

@@ -17,7 +17,7 @@ import torch.nn.functional as F
 from torch.nn import init
 from torch.nn.parameter import Parameter
 
-from ..._autocast_utils import _cast_if_autocast_enabled
+from ..._autocast_utils import _autocast_disabled, _cast_if_autocast_enabled
 from ..parallel_state import get_tensor_model_parallel_group, get_tensor_model_parallel_rank, \
     get_tensor_model_parallel_world_size
 from ..utils import divide
@@ -185,7 +185,7 @@ class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
 def linear_with_grad_accumulation_and_async_allreduce(input, weight, bias, async_grad_allreduce,
                                                       sequence_parallel_enabled=False):
     args = _cast_if_autocast_enabled(input, weight, bias, async_grad_allreduce, sequence_parallel_enabled)
-    with torch.autocast("cuda", enabled=False):
+    with _autocast_disabled():
         return LinearWithGradAccumulationAndAsyncCommunication.apply(*args)
 
 
