@@ -64,7 +64,7 @@ template <int I, typename T0, typename... Ts> struct TypeAt<I, T0, Ts...> {
 #define APEX_MTA_ILP 1
 #endif
 #ifndef APEX_MTA_RED_UNROLL
-#define APEX_MTA_RED_UNROLL 1
+#define APEX_MTA_RED_UNROLL 4
 #endif
 typedef unsigned mta_u4 __attribute__((ext_vector_type(4)));
 typedef unsigned mta_u2 __attribute__((ext_vector_type(2)));
