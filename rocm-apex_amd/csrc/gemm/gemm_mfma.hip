@@ -356,7 +356,7 @@ void launch_epi(const GemmArgs& g, hipStream_t s) {
 // =============================================================================================
 namespace g256 {
 
-constexpr int BM = 256, BN = 256, BK = 64, THREADS = 512;
+constexpr int BM = 256, BN = 256, BK = 64;
 constexpr int TILE = BM * BK;          // elements per operand tile (32 KB)
 constexpr int CST = BN + 4;            // epilogue fp32 row stride
 constexpr size_t LDS_BYTES = (size_t)128 * CST * 4 > (size_t)4 * TILE * 2 ? (size_t)128 * CST * 4 : (size_t)4 * TILE * 2;
@@ -372,12 +372,12 @@ __device__ __forceinline__ void dma16(const uint16_t* src, uint16_t* lds_dst) {
 // m-major operand (k rows, M/N contiguous): image [64][256], 1-KB piece = 2 k-rows of 512 B,
 //   chunk c of k-row r at c ^ ((r & 3) << 1) (transposed ds_read_b64_tr_b16: the 4 k-rows a
 //   16-lane group reads start 32 B apart -> conflict-free).
-template <bool KMAJ>
+template <bool KMAJ, int NW = 8>
 __device__ __forceinline__ void issue_tile(const uint16_t* __restrict__ X, int64_t ld, int rows, int r0, int k0,
                                            uint16_t* dst, int wave, int lane) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int j = i * 8 + wave;
+  for (int i = 0; i < 32 / NW; ++i) {
+    const int j = i * NW + wave;
     if constexpr (KMAJ) {
       const int row = 8 * j + (lane >> 3);
       const int c = (lane & 7) ^ ((row >> 1) & 7);
@@ -412,62 +412,68 @@ __device__ __forceinline__ s16x8 frag_sw(const uint16_t* tile, int rowbase, int 
   }
 }
 
-template <typename T, bool AK, bool BKM, int EPI>
-__global__ void __launch_bounds__(512, 1)
+// NW = 8: 2 x 4 waves of 128 x 64 (two waves per SIMD hide each other's LDS latency);
+// NW = 4: 2 x 2 waves of 128 x 128 (one wave per SIMD, 256 fp32 accumulators each, half the
+// LDS fragment traffic per MFMA: every A/B fragment read feeds 4 MFMAs instead of 2 / 4).
+template <typename T, bool AK, bool BKM, int EPI, int NW>
+__global__ void __launch_bounds__(NW * 64, 1)
 gemm256_nt(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, T* __restrict__ C, int64_t lda,
            int64_t ldb, int64_t ldc, int M, int N, int K, const T* __restrict__ bias, const T* __restrict__ aux_in,
            T* __restrict__ aux_out, float* __restrict__ part, int kchunk) {
+  constexpr int WN = NW / 2;           // waves along N
+  constexpr int NJ = BN / WN / 32;     // 32-wide column fragments per wave (2 or 4)
+  constexpr int NT = NW * 64;
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   auto a_buf = [&](int b) { return lds + b * 2 * TILE; };
   auto b_buf = [&](int b) { return lds + b * 2 * TILE + TILE; };
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave / WN, wn = wave % WN;
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
   int bm, bn;
   tile_coords(tiles_m * tiles_n, tiles_m, tiles_n, bm, bn);
   const int row0 = bm * BM, col0 = bn * BN;
 
-  f32x16 acc[4][2];
+  f32x16 acc[4][NJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   // split-K (part != null): blockIdx.y picks the K chunk, the epilogue stores an fp32 partial
   const int kbeg = (int)blockIdx.y * kchunk;
   const int nk = (min(K, kbeg + kchunk) - kbeg) / BK;
-  issue_tile<AK>(A, lda, M, row0, kbeg, a_buf(0), wave, lane);
-  issue_tile<BKM>(B, ldb, N, col0, kbeg, b_buf(0), wave, lane);
+  issue_tile<AK, NW>(A, lda, M, row0, kbeg, a_buf(0), wave, lane);
+  issue_tile<BKM, NW>(B, ldb, N, col0, kbeg, b_buf(0), wave, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) {
-      issue_tile<AK>(A, lda, M, row0, kbeg + (kt + 1) * BK, a_buf(cur ^ 1), wave, lane);
-      issue_tile<BKM>(B, ldb, N, col0, kbeg + (kt + 1) * BK, b_buf(cur ^ 1), wave, lane);
+      issue_tile<AK, NW>(A, lda, M, row0, kbeg + (kt + 1) * BK, a_buf(cur ^ 1), wave, lane);
+      issue_tile<BKM, NW>(B, ldb, N, col0, kbeg + (kt + 1) * BK, b_buf(cur ^ 1), wave, lane);
     }
     const uint16_t* at = a_buf(cur);
     const uint16_t* bt = b_buf(cur);
 #pragma unroll
     for (int kk = 0; kk < BK / 16; ++kk) {
-      s16x8 af[4], bf[2];
+      s16x8 af[4], bf[NJ];
 #pragma unroll
       for (int i = 0; i < 4; ++i) af[i] = frag_sw<AK>(at, wm * 128 + 32 * i, kk, lane);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bf[j] = frag_sw<BKM>(bt, wn * 64 + 32 * j, kk, lane);
+      for (int j = 0; j < NJ; ++j) bf[j] = frag_sw<BKM>(bt, wn * (32 * NJ) + 32 * j, kk, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma<T>(af[i], bf[j], acc[i][j]);
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma<T>(af[i], bf[j], acc[i][j]);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
   float* cs = reinterpret_cast<float*>(lds);
-  const int ch = tid & 31, rsub = tid >> 5;
+  const int ch = tid & 31, rsub = tid >> 5;  // rsub in [0, NT / 32)
   const int gc = col0 + ch * 8;
   float bv[8];
 #pragma unroll
@@ -479,17 +485,17 @@ gemm256_nt(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, T* __
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int rl = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            cs[rl * CST + wn * 64 + 32 * j + (lane & 31)] = acc[i][j][r];
+            cs[rl * CST + wn * (32 * NJ) + 32 * j + (lane & 31)] = acc[i][j][r];
           }
     }
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
-      const int rl = rsub + 16 * it;
+    for (int it = 0; it < 128 / (NT / 32); ++it) {
+      const int rl = rsub + (NT / 32) * it;
       const int gr = row0 + half * 128 + rl;
       if (gr < M && gc < N) {
         float v[8];
@@ -574,13 +580,29 @@ inline int splitk_parts(const GemmArgs& g, int cus, int* kchunk) {
   return (g.k + chunk - 1) / chunk;
 }
 
+// waves per 256 x 256 tile: 8 (default) or 4 (APEX_AMD_GEMM256_WAVES=4, A/B)
+inline int waves_cfg() {
+  const char* e = std::getenv("APEX_AMD_GEMM256_WAVES");
+  return (e != nullptr && e[0] == '4') ? 4 : 8;
+}
+
+template <typename T, bool AK, bool BKM, int NW>
+void launch_nw(const GemmArgs& g, hipStream_t s, int cus);
+
 template <typename T, bool AK, bool BKM>
 void launch(const GemmArgs& g, hipStream_t s, int cus) {
+  if (waves_cfg() == 4) launch_nw<T, AK, BKM, 4>(g, s, cus);
+  else launch_nw<T, AK, BKM, 8>(g, s, cus);
+}
+
+template <typename T, bool AK, bool BKM, int NW>
+void launch_nw(const GemmArgs& g, hipStream_t s, int cus) {
   const int tiles = ((g.m + BM - 1) / BM) * ((g.n + BN - 1) / BN);
+  constexpr int THREADS = NW * 64;
   int kchunk = g.k;
   const int sp = g.splitk_ws != nullptr ? splitk_parts(g, cus, &kchunk) : 1;
   if (sp > 1) {
-    hipLaunchKernelGGL((gemm256_nt<T, AK, BKM, kEpiNone>), dim3(tiles, sp), dim3(THREADS), LDS_BYTES, s,
+    hipLaunchKernelGGL((gemm256_nt<T, AK, BKM, kEpiNone, NW>), dim3(tiles, sp), dim3(THREADS), LDS_BYTES, s,
                        (const uint16_t*)g.a, (const uint16_t*)g.b, (T*)g.c, g.lda, g.ldb, g.ldc, g.m, g.n, g.k,
                        (const T*)nullptr, (const T*)nullptr, (T*)nullptr, g.splitk_ws, kchunk);
     const int64_t nvec = (int64_t)g.m * g.n / 8;
@@ -596,13 +618,13 @@ void launch(const GemmArgs& g, hipStream_t s, int cus) {
                        (T*)g.aux_out, (float*)nullptr, g.k);
   };
   switch (g.epilogue) {
-    case kEpiNone: go(gemm256_nt<T, AK, BKM, kEpiNone>); break;
-    case kEpiGelu: go(gemm256_nt<T, AK, BKM, kEpiGelu>); break;
-    case kEpiRelu: go(gemm256_nt<T, AK, BKM, kEpiRelu>); break;
-    case kEpiSigmoid: go(gemm256_nt<T, AK, BKM, kEpiSigmoid>); break;
-    case kEpiDGelu: go(gemm256_nt<T, AK, BKM, kEpiDGelu>); break;
-    case kEpiDRelu: go(gemm256_nt<T, AK, BKM, kEpiDRelu>); break;
-    case kEpiDSigmoid: go(gemm256_nt<T, AK, BKM, kEpiDSigmoid>); break;
+    case kEpiNone: go(gemm256_nt<T, AK, BKM, kEpiNone, NW>); break;
+    case kEpiGelu: go(gemm256_nt<T, AK, BKM, kEpiGelu, NW>); break;
+    case kEpiRelu: go(gemm256_nt<T, AK, BKM, kEpiRelu, NW>); break;
+    case kEpiSigmoid: go(gemm256_nt<T, AK, BKM, kEpiSigmoid, NW>); break;
+    case kEpiDGelu: go(gemm256_nt<T, AK, BKM, kEpiDGelu, NW>); break;
+    case kEpiDRelu: go(gemm256_nt<T, AK, BKM, kEpiDRelu, NW>); break;
+    case kEpiDSigmoid: go(gemm256_nt<T, AK, BKM, kEpiDSigmoid, NW>); break;
     default: throw std::runtime_error("gemm256: unknown epilogue");
   }
 }

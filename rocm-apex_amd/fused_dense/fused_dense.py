@@ -10,7 +10,16 @@ reference's ROCm build leaves d_bias uninitialised and makes the GeLU variants n
 
 Runs the native path for fp16/bf16 GPU tensors with K, N multiples of 8; otherwise (CPU, fp32,
 odd sizes) the same math in torch.  GeLU is the tanh approximation (the cuBLASLt GELU epilogue
-the reference targets)."""
+the reference targets).
+
+Per-shape routing: on the GPU, the first forward and the first backward of every distinct
+(op, shape, dtype) time the native kernels against the library path (hipBLASLt through
+``torch.addmm`` / ``matmul``) on the live tensors and keep the faster one
+(``route_table()`` lists the decisions).  ``APEX_AMD_DENSE_ROUTE=native|library|auto``
+(default auto) pins the choice; ``profiles/gemm_waves_ab_r02.md`` has the per-shape numbers.
+No timing happens under hipGraph capture (native path)."""
+import os
+
 import torch
 from torch import nn
 
@@ -47,29 +56,89 @@ def _gelu_tanh(x):
     return torch.nn.functional.gelu(x, approximate="tanh")
 
 
+_ROUTES = {}
+
+
+def route_mode():
+    return os.environ.get("APEX_AMD_DENSE_ROUTE", "auto")
+
+
+def route_table():
+    """{(op, M, N, K, dtype): 'native' | 'library'} decided so far in this process."""
+    return {k: ("native" if v else "library") for k, v in _ROUTES.items()}
+
+
+def _time_ms(fn, reps=5):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def _use_native(key, native_fn, library_fn):
+    """Measured per-shape choice between the native kernels and the library GEMMs."""
+    mode = route_mode()
+    if mode == "native":
+        return True
+    if mode == "library":
+        return False
+    hit = _ROUTES.get(key)
+    if hit is not None:
+        return hit
+    if torch.cuda.is_current_stream_capturing():
+        return True
+    with torch.no_grad():
+        t_native, t_lib = _time_ms(native_fn), _time_ms(library_fn)
+    _ROUTES[key] = t_native <= t_lib
+    return _ROUTES[key]
+
+
+def _lib_dense_fwd(x, w, b):
+    x2 = x.reshape(-1, x.shape[-1])
+    out = torch.addmm(b, x2, w.t()) if b is not None else x2.matmul(w.t())
+    return out.view(x.shape[:-1] + (w.shape[0],))
+
+
+def _lib_dense_bwd(x, w, gy, has_bias):
+    g2 = gy.reshape(-1, gy.shape[-1])
+    x2 = x.reshape(-1, x.shape[-1])
+    return g2.matmul(w).view(x.shape), g2.t().matmul(x2), (g2.sum(0) if has_bias else None)
+
+
+def _shape_key(op, x, w):
+    return (op, x.numel() // x.shape[-1], w.shape[0], w.shape[1], str(x.dtype))
+
+
 class FusedDenseFunc(torch.autograd.Function):
     @staticmethod
     def forward(ctx, input, weight, bias):
         ctx.save_for_backward(input, weight)
         ctx.native = fused_linear_available(input, weight, bias)
         ctx.has_bias = bias is not None
-        if ctx.native:
+        if ctx.native and _use_native(_shape_key("dense_fwd", input, weight) + (bias is not None,),
+                                      lambda: linear_bias_forward(input, weight, bias),
+                                      lambda: _lib_dense_fwd(input, weight, bias)):
             return linear_bias_forward(input, weight, bias)
+        if input.is_cuda:
+            return _lib_dense_fwd(input, weight, bias)
         out = torch.matmul(input, weight.t())
         return out + bias if bias is not None else out
 
     @staticmethod
     def backward(ctx, grad_output):
         input, weight = ctx.saved_tensors
-        if ctx.native:
-            dx, dw, db = _fd().linear_bias_backward(input, weight, grad_output.contiguous())
+        gy = grad_output.contiguous()
+        if ctx.native and _use_native(_shape_key("dense_bwd", input, weight) + (ctx.has_bias,),
+                                      lambda: _fd().linear_bias_backward(input, weight, gy),
+                                      lambda: _lib_dense_bwd(input, weight, gy, ctx.has_bias)):
+            dx, dw, db = _fd().linear_bias_backward(input, weight, gy)
             return dx.view(input.shape), dw, (db if ctx.has_bias else None)
-        g2 = grad_output.reshape(-1, grad_output.shape[-1])
-        x2 = input.reshape(-1, input.shape[-1])
-        grad_input = grad_output.matmul(weight)
-        grad_weight = g2.t().matmul(x2)
-        grad_bias = g2.sum(0) if ctx.has_bias else None
-        return grad_input, grad_weight, grad_bias
+        return _lib_dense_bwd(input, weight, gy, ctx.has_bias)
 
 
 class DenseNoBiasFunc(torch.autograd.Function):
@@ -83,14 +152,27 @@ class DenseNoBiasFunc(torch.autograd.Function):
         return dx, dw
 
 
+def _lib_gelu_dense_fwd(x, w1, b1, w2, b2):
+    x2 = x.reshape(-1, x.shape[-1])
+    gelu_in = torch.addmm(b1, x2, w1.t())
+    out1 = _gelu_tanh(gelu_in)
+    out2 = torch.addmm(b2, out1, w2.t())
+    return out1, out2.view(x.shape[:-1] + (w2.shape[0],)), gelu_in
+
+
 class FusedDenseGeluDenseFunc(torch.autograd.Function):
     @staticmethod
     def forward(ctx, input, weight1, bias1, weight2, bias2):
         ctx.native = (fused_linear_available(input, weight1, bias1) and weight2.dtype == input.dtype
                       and bias2.dtype == input.dtype and weight2.shape[0] % 8 == 0 and weight2.shape[1] % 8 == 0)
-        if ctx.native:
+        key = _shape_key("gelu_dense_fwd", input, weight1) + (weight2.shape[0],)
+        if ctx.native and _use_native(key,
+                                      lambda: _fd().linear_gelu_linear_forward(input, weight1, bias1, weight2, bias2),
+                                      lambda: _lib_gelu_dense_fwd(input, weight1, bias1, weight2, bias2)):
             out1, out2, gelu_in = _fd().linear_gelu_linear_forward(input, weight1, bias1, weight2, bias2)
             out2 = out2.view(input.shape[:-1] + (weight2.shape[0],))
+        elif input.is_cuda:
+            out1, out2, gelu_in = _lib_gelu_dense_fwd(input, weight1, bias1, weight2, bias2)
         else:
             gelu_in = torch.matmul(input, weight1.t()) + bias1
             out1 = _gelu_tanh(gelu_in)
@@ -101,10 +183,19 @@ class FusedDenseGeluDenseFunc(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_output):
         input, weight1, weight2, gelu_in, output1 = ctx.saved_tensors
-        if ctx.native:
-            dx, dw1, db1, dw2, db2 = _fd().linear_gelu_linear_backward(input, gelu_in, output1, weight1, weight2,
-                                                                        grad_output.contiguous())
+        gy = grad_output.contiguous()
+        key = _shape_key("gelu_dense_bwd", input, weight1) + (weight2.shape[0],)
+        if ctx.native and _use_native(key,
+                                      lambda: _fd().linear_gelu_linear_backward(input, gelu_in, output1, weight1,
+                                                                                weight2, gy),
+                                      lambda: FusedDenseGeluDenseFunc._lib_backward(input, weight1, weight2,
+                                                                                    gelu_in, output1, gy)):
+            dx, dw1, db1, dw2, db2 = _fd().linear_gelu_linear_backward(input, gelu_in, output1, weight1, weight2, gy)
             return dx.view(input.shape), dw1, db1, dw2, db2
+        return FusedDenseGeluDenseFunc._lib_backward(input, weight1, weight2, gelu_in, output1, gy)
+
+    @staticmethod
+    def _lib_backward(input, weight1, weight2, gelu_in, output1, grad_output):
         g2 = grad_output.reshape(-1, grad_output.shape[-1])
         h = output1.reshape(-1, output1.shape[-1])
         dw2 = g2.t().matmul(h)

@@ -98,9 +98,14 @@ def test_gpu_gemm_epilogues(dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("route", ["native", "auto"])
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
-def test_gpu_fused_dense_reference_test(dtype):
-    """The reference's test shapes: 3 x 512 tokens, 1024 -> 3072 (dx, dw, db all checked)."""
+def test_gpu_fused_dense_reference_test(dtype, route, monkeypatch):
+    """The reference's test shapes: 3 x 512 tokens, 1024 -> 3072 (dx, dw, db all checked), on the
+    native kernels and under the measured per-shape routing."""
+    from apex.fused_dense import fused_dense as fd
+
+    monkeypatch.setenv("APEX_AMD_DENSE_ROUTE", route)
     torch.manual_seed(0)
     x = torch.randn(3 * 512, 1024, device="cuda").to(dtype).requires_grad_(True)
     dense = FusedDense(1024, 3072).cuda().to(dtype)
@@ -116,11 +121,16 @@ def test_gpu_fused_dense_reference_test(dtype):
     torch.testing.assert_close(x.grad.float() / 8, dx_ref / 8, atol=2e-2, rtol=2e-2)
     torch.testing.assert_close(dense.weight.grad.float() / 40, dw_ref / 40, atol=2e-2, rtol=2e-2)
     torch.testing.assert_close(dense.bias.grad.float() / 40, db_ref / 40, atol=2e-2, rtol=2e-2)
+    if route == "auto":
+        keys = [k for k in fd.route_table() if k[0] in ("dense_fwd", "dense_bwd") and k[1:4] == (1536, 3072, 1024)]
+        assert len(keys) >= 2  # forward and backward were both timed and decided
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("route", ["native", "auto"])
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
-def test_gpu_fused_dense_gelu_dense(dtype):
+def test_gpu_fused_dense_gelu_dense(dtype, route, monkeypatch):
+    monkeypatch.setenv("APEX_AMD_DENSE_ROUTE", route)
     torch.manual_seed(2)
     x = (torch.randn(2, 256, 512, device="cuda") * 0.5).to(dtype).requires_grad_(True)
     mod = FusedDenseGeluDense(512, 2048, 512).cuda().to(dtype)

@@ -71,6 +71,39 @@ def bench_gemm():
              speedup=t_ref / t_ours)
 
 
+def bench_dense_route():
+    """FusedDense / FusedDenseGeluDense forward+backward per shape: native kernels, library
+    GEMMs (hipBLASLt) and the measured per-shape routing."""
+    from apex.fused_dense import FusedDense, FusedDenseGeluDense
+    from apex.fused_dense import fused_dense as fd
+
+    dt = torch.bfloat16
+    for (tokens, hin, hout) in [(16384, 1024, 3072), (16384, 1024, 4096), (16384, 4096, 1024), (8192, 1024, 1024)]:
+        x = torch.randn(tokens, hin, device="cuda", dtype=dt, requires_grad=True)
+        m = FusedDense(hin, hout).cuda().to(dt)
+        gy = torch.randn(tokens, hout, device="cuda", dtype=dt)
+        res = {}
+        for mode in ("native", "library", "auto"):
+            os.environ["APEX_AMD_DENSE_ROUTE"] = mode
+            res[mode] = timeit(lambda: torch.autograd.backward(m(x), gy))
+        os.environ.pop("APEX_AMD_DENSE_ROUTE")
+        emit(kernel="fused_dense_fwd_bwd", tokens=tokens, k=hin, n=hout, native_ms=res["native"],
+             library_ms=res["library"], routed_ms=res["auto"], routed_vs_library=res["library"] / res["auto"],
+             routes={"/".join(map(str, k)): v for k, v in fd.route_table().items()
+                     if k[1:4] == (tokens, hout, hin)})
+    for (tokens, h, f) in [(16384, 1024, 4096)]:
+        x = torch.randn(tokens, h, device="cuda", dtype=dt, requires_grad=True)
+        m = FusedDenseGeluDense(h, f, h).cuda().to(dt)
+        gy = torch.randn(tokens, h, device="cuda", dtype=dt)
+        res = {}
+        for mode in ("native", "library", "auto"):
+            os.environ["APEX_AMD_DENSE_ROUTE"] = mode
+            res[mode] = timeit(lambda: torch.autograd.backward(m(x), gy))
+        os.environ.pop("APEX_AMD_DENSE_ROUTE")
+        emit(kernel="fused_dense_gelu_dense_fwd_bwd", tokens=tokens, h=h, ffn=f, native_ms=res["native"],
+             library_ms=res["library"], routed_ms=res["auto"], routed_vs_library=res["library"] / res["auto"])
+
+
 def bench_ln():
     from apex.normalization import FusedLayerNorm
 
@@ -192,7 +225,7 @@ def bench_attn():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="attn,gemm,ln,softmax,bn,adam")
+    ap.add_argument("--only", default="attn,gemm,ln,softmax,bn,adam,dense_route")
     a = ap.parse_args()
     torch.manual_seed(0)
     for name in a.only.split(","):
