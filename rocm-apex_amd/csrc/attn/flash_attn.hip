@@ -134,8 +134,18 @@ __device__ __forceinline__ void xcd_remap(int& bx, int& by, int& bz) {
 // =============================================================================================
 // forward
 // =============================================================================================
-template <typename T, int D, bool PLAIN>
-__global__ void __launch_bounds__(256, (D == 128 && !PLAIN) ? 1 : ((D <= 64 && PLAIN) ? 3 : 2)) fwd_kernel(const AttnArgs a) {
+// QF query fragments (32 queries each) per wave: a block covers 128 * QF queries.  QF = 2 feeds
+// every K / V fragment read from LDS into two MFMAs (half the LDS traffic per FLOP) at the cost
+// of one wave per SIMD for d = 128.
+// LO = true: one resident block less than the default (more registers per lane, no spills)
+template <int D, bool PLAIN, int QF, bool LO>
+constexpr int fwd_occupancy() {
+  constexpr int base = QF == 2 ? (D == 128 ? 1 : 2) : ((D == 128 && !PLAIN) ? 1 : ((D <= 64 && PLAIN) ? 3 : 2));
+  return LO && base > 1 ? base - 1 : base;
+}
+
+template <typename T, int D, bool PLAIN, int QF, bool LO>
+__global__ void __launch_bounds__(256, (fwd_occupancy<D, PLAIN, QF, LO>())) fwd_kernel(const AttnArgs a) {
   int bx, by, bz;
   xcd_remap(bx, by, bz);
   using G = Geo<D>;
@@ -143,6 +153,7 @@ __global__ void __launch_bounds__(256, (D == 128 && !PLAIN) ? 1 : ((D <= 64 && P
   constexpr int KT = BN * KSTR, VT = BN * VSTR;
   constexpr int CPR = D / 8;                 // 16-B chunks per row
   constexpr int CPT = BN * CPR / 256;        // chunks per thread per tensor (D >= 32 -> >= 1)
+  constexpr int QB = 128 * QF;               // queries per block
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   auto kbuf = [&](int i) { return lds + i * (KT + VT); };
   auto vbuf = [&](int i) { return lds + i * (KT + VT) + KT; };
@@ -154,11 +165,11 @@ __global__ void __launch_bounds__(256, (D == 128 && !PLAIN) ? 1 : ((D <= 64 && P
   seq_of(a, b, a.q.sb, a.q.ss, a.k.sb, a.k.ss, sq);
   // causal: workgroup x also runs block n-1-x (work per block grows / shrinks linearly with x), so
   // every workgroup does the same number of tiles
-  const int nblk = (a.sq + 127) / 128;
+  const int nblk = (a.sq + QB - 1) / QB;
   for (int pass = 0; pass < (a.causal ? 2 : 1); ++pass) {
     const int blk = pass == 0 ? (int)bx : nblk - 1 - (int)bx;
     if (pass == 1 && blk <= (int)bx) break;
-    const int q_start = blk * 128;
+    const int q_start = blk * QB;
     if (q_start >= sq.lq) continue;  // uniform over the workgroup
     const bool varq = a.cu_q != nullptr, vark = a.cu_k != nullptr;
     const uint16_t* qp = (const uint16_t*)a.q.p + tensor_off(a.q, sq, true, varq, b) + (int64_t)hq * a.q.sh;
@@ -166,21 +177,26 @@ __global__ void __launch_bounds__(256, (D == 128 && !PLAIN) ? 1 : ((D <= 64 && P
     const uint16_t* vp = (const uint16_t*)a.v.p + tensor_off(a.v, sq, false, vark, b) + (int64_t)hk * a.v.sh;
     T* op = (T*)a.o.p + tensor_off(a.o, sq, true, varq, b) + (int64_t)hq * a.o.sh;
 
-    const int myq = q_start + wave * 32 + ql;
-    const bool qvalid = myq < sq.lq;
-    s16x8 qf[NKK];
+    const int wq0 = q_start + wave * 32 * QF;  // first query of this wave
+    int myq[QF];
+    bool qvalid[QF];
+    s16x8 qf[QF][NKK];
     #pragma unroll
-    for (int kk = 0; kk < NKK; ++kk) {
-      if (qvalid) qf[kk] = *reinterpret_cast<const s16x8*>(qp + (int64_t)myq * a.q.ss + kk * 16 + 8 * h2);
-      else
-        #pragma unroll
-        for (int j = 0; j < 8; ++j) qf[kk][j] = 0;
+    for (int f = 0; f < QF; ++f) {
+      myq[f] = wq0 + 32 * f + ql;
+      qvalid[f] = myq[f] < sq.lq;
+      #pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        if (qvalid[f]) qf[f][kk] = *reinterpret_cast<const s16x8*>(qp + (int64_t)myq[f] * a.q.ss + kk * 16 + 8 * h2);
+        else
+          #pragma unroll
+          for (int j = 0; j < 8; ++j) qf[f][kk][j] = 0;
+      }
     }
 
     int k_end = sq.lk;
-    if (a.causal) k_end = min(k_end, q_start + 128);
+    if (a.causal) k_end = min(k_end, q_start + QB);
     const int nkb = (k_end + BN - 1) / BN;
-    const int wave_q_last = min(q_start + wave * 32 + 31, sq.lq - 1);
 
     uint4 rk[CPT], rv[CPT];
     auto gload = [&](int kb0) {
@@ -202,18 +218,22 @@ __global__ void __launch_bounds__(256, (D == 128 && !PLAIN) ? 1 : ((D <= 64 && P
       }
     };
 
-    f32x16 o[NDT];
+    f32x16 o[QF][NDT];
+    float m_i[QF], l_i[QF];
     #pragma unroll
-    for (int i = 0; i < NDT; ++i) o[i] = zero16();
-    float m_i = -INFINITY, l_i = 0.f;
+    for (int f = 0; f < QF; ++f) {
+      m_i[f] = -INFINITY;
+      l_i[f] = 0.f;
+      #pragma unroll
+      for (int i = 0; i < NDT; ++i) o[f][i] = zero16();
+    }
     const float c = a.scale * kLog2e;
     const bool dropout = !PLAIN && a.p_drop > 0.f;  // PLAIN: no bias, no dropout (compiled out)
     const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
     const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
     const uint32_t smix = seed_mix_of(a.seed, a.offset);
     const uint32_t bh = (uint32_t)(b * a.h + hq);
-    const float* biasp = (!PLAIN && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh + (int64_t)myq * a.bias_sq
-                                : nullptr;
+    const float* biasb = (!PLAIN && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh : nullptr;
 
     if (nkb > 0) {
       gload(0);
@@ -227,102 +247,123 @@ __global__ void __launch_bounds__(256, (D == 128 && !PLAIN) ? 1 : ((D <= 64 && P
       const uint16_t* Kl = kbuf(cur);
       const uint16_t* Vl = vbuf(cur);
 
-      f32x16 s[2] = {zero16(), zero16()};
+      // S^T[key][q] = K Q^T: every K fragment read feeds QF MFMAs
+      f32x16 sacc[QF][2];
+      #pragma unroll
+      for (int f = 0; f < QF; ++f) sacc[f][0] = sacc[f][1] = zero16();
       #pragma unroll
       for (int kk = 0; kk < NKK; ++kk) {
         const s16x8 a0 = frag_rows<KSTR>(Kl, 0, kk, lane);
         const s16x8 a1 = frag_rows<KSTR>(Kl, 32, kk, lane);
-        s[0] = mma<T>(a0, qf[kk], s[0]);
-        s[1] = mma<T>(a1, qf[kk], s[1]);
-      }
-      float x[2][16];
-      const bool need_mask = (kb0 + BN > sq.lk) || (a.causal && kb0 + BN - 1 > q_start + wave * 32) || biasp != nullptr;
-      #pragma unroll
-      for (int t = 0; t < 2; ++t)
         #pragma unroll
-        for (int r = 0; r < 16; ++r) x[t][r] = s[t][r] * c;
-      if (need_mask) {
-        #pragma unroll
-        for (int t = 0; t < 2; ++t)
-          #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = kb0 + 32 * t + crow(r, h2);
-            const bool ok = key < sq.lk && (!a.causal || key <= myq);
-            float v = x[t][r];
-            if (biasp != nullptr && ok && qvalid) v += biasp[(int64_t)key * a.bias_sk] * kLog2e;
-            x[t][r] = ok ? v : -INFINITY;
-          }
-      }
-      float mx = -INFINITY;
-      #pragma unroll
-      for (int t = 0; t < 2; ++t)
-        #pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, x[t][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_i, mx);
-      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-      const float alpha = fast_exp2(m_i - m_use);
-      float ls = 0.f;
-      #pragma unroll
-      for (int t = 0; t < 2; ++t)
-        #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = fast_exp2(x[t][r] - m_use);
-          ls += p;
-          x[t][r] = p;
+        for (int f = 0; f < QF; ++f) {
+          sacc[f][0] = mma<T>(a0, qf[f][kk], sacc[f][0]);
+          sacc[f][1] = mma<T>(a1, qf[f][kk], sacc[f][1]);
         }
-      ls += __shfl_xor(ls, 32, 64);
-      l_i = l_i * alpha + ls;
-      m_i = m_new;
-      // skip the O rescale when no lane's running max moved (after the first tiles it rarely does;
-      // measured equal or faster at every head dim: profiles/kernels_attn_r01e.jsonl lazy0/lazy1)
-      if (__any(alpha != 1.f)) {
-        #pragma unroll
-        for (int i = 0; i < NDT; ++i)
-          #pragma unroll
-          for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
       }
-      if (dropout) {
+      const bool need_mask = (kb0 + BN > sq.lk) || (a.causal && kb0 + BN - 1 > wq0) || biasb != nullptr;
+      // probabilities are packed to 16-bit right away (P fragments), so the fp32 scores of one
+      // query fragment are dead before the next fragment's softmax starts
+      s16x8 pf[QF][2][2];
+      #pragma unroll
+      for (int f = 0; f < QF; ++f) {
+        float x[1][2][16];
+        #pragma unroll
+        for (int t = 0; t < 2; ++t)
+          #pragma unroll
+          for (int r = 0; r < 16; ++r) x[0][t][r] = sacc[f][t][r] * c;
+        if (need_mask) {
+          #pragma unroll
+          for (int t = 0; t < 2; ++t)
+            #pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int key = kb0 + 32 * t + crow(r, h2);
+              const bool ok = key < sq.lk && (!a.causal || key <= myq[f]);
+              float v = x[0][t][r];
+              if (biasb != nullptr && ok && qvalid[f])
+                v += biasb[(int64_t)myq[f] * a.bias_sq + (int64_t)key * a.bias_sk] * kLog2e;
+              x[0][t][r] = ok ? v : -INFINITY;
+            }
+        }
+        float mx = -INFINITY;
+        #pragma unroll
+        for (int t = 0; t < 2; ++t)
+          #pragma unroll
+          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, x[0][t][r]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float m_new = fmaxf(m_i[f], mx);
+        const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+        const float alpha = fast_exp2(m_i[f] - m_use);
+        float ls = 0.f;
         #pragma unroll
         for (int t = 0; t < 2; ++t)
           #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const uint32_t key = (uint32_t)(kb0 + 32 * t + crow(r, h2));
-            x[t][r] *= drop_hash(smix, bh, (uint32_t)myq, key) >= thresh ? inv_keep : 0.f;
+            const float pr = fast_exp2(x[0][t][r] - m_use);
+            ls += pr;
+            x[0][t][r] = pr;
           }
+        ls += __shfl_xor(ls, 32, 64);
+        l_i[f] = l_i[f] * alpha + ls;
+        m_i[f] = m_new;
+        // skip the O rescale when no lane's running max moved (after the first tiles it rarely does;
+        // measured equal or faster at every head dim: profiles/kernels_attn_r01e.jsonl lazy0/lazy1)
+        if (__any(alpha != 1.f)) {
+          #pragma unroll
+          for (int i = 0; i < NDT; ++i)
+            #pragma unroll
+            for (int r = 0; r < 16; ++r) o[f][i][r] *= alpha;
+        }
+        if (dropout) {
+          #pragma unroll
+          for (int t = 0; t < 2; ++t)
+            #pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const uint32_t key = (uint32_t)(kb0 + 32 * t + crow(r, h2));
+              x[0][t][r] *= drop_hash(smix, bh, (uint32_t)myq[f], key) >= thresh ? inv_keep : 0.f;
+            }
+        }
+        #pragma unroll
+        for (int t = 0; t < 2; ++t)
+          #pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) pf[f][t][s2] = pack8<T>(&x[0][t][8 * s2]);
       }
-      // O^T[d][q] += V^T[d][key] P^T[key][q]
+      // O^T[d][q] += V^T[d][key] P^T[key][q]: every V fragment read feeds QF MFMAs
       #pragma unroll
       for (int t = 0; t < 2; ++t)
         #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const s16x8 pf = pack8<T>(&x[t][8 * s2]);
           const int klo = 32 * t + 16 * s2 + 4 * h2;
           #pragma unroll
           for (int dt = 0; dt < NDT; ++dt) {
             const s16x8 vf = frag_tr<VSTR>(Vl, 32 * dt, klo, klo + 8, lane);
-            o[dt] = mma<T>(vf, pf, o[dt]);
+            #pragma unroll
+            for (int f = 0; f < QF; ++f) o[f][dt] = mma<T>(vf, pf[f][t][s2], o[f][dt]);
           }
         }
       if (more) lstore(cur ^ 1);
       __syncthreads();
     }
-    (void)wave_q_last;
 
-    if (qvalid) {
-      const float inv_l = l_i > 0.f ? 1.f / l_i : 0.f;
-      T* orow = op + (int64_t)myq * a.o.ss;
+    #pragma unroll
+    for (int f = 0; f < QF; ++f) {
+      if (!qvalid[f]) continue;
+      const float inv_l = l_i[f] > 0.f ? 1.f / l_i[f] : 0.f;
+      T* orow = op + (int64_t)myq[f] * a.o.ss;
       #pragma unroll
       for (int dt = 0; dt < NDT; ++dt)
         #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           const int d0 = 32 * dt + 8 * g4 + 4 * h2;
-          uint32_t w0 = (uint32_t)from_f<T>(o[dt][4 * g4] * inv_l).x | ((uint32_t)from_f<T>(o[dt][4 * g4 + 1] * inv_l).x << 16);
-          uint32_t w1 = (uint32_t)from_f<T>(o[dt][4 * g4 + 2] * inv_l).x | ((uint32_t)from_f<T>(o[dt][4 * g4 + 3] * inv_l).x << 16);
+          uint32_t w0 = (uint32_t)from_f<T>(o[f][dt][4 * g4] * inv_l).x |
+                        ((uint32_t)from_f<T>(o[f][dt][4 * g4 + 1] * inv_l).x << 16);
+          uint32_t w1 = (uint32_t)from_f<T>(o[f][dt][4 * g4 + 2] * inv_l).x |
+                        ((uint32_t)from_f<T>(o[f][dt][4 * g4 + 3] * inv_l).x << 16);
           *reinterpret_cast<uint2*>(orow + d0) = make_uint2(w0, w1);
         }
       if (h2 == 0 && a.lse != nullptr)
-        a.lse[(int64_t)hq * a.rows_q + sq.qrow0 + myq] = l_i > 0.f ? (m_i + log2f(l_i)) * kLn2 : INFINITY;
+        a.lse[(int64_t)hq * a.rows_q + sq.qrow0 + myq[f]] =
+            l_i[f] > 0.f ? (m_i[f] + log2f(l_i[f])) * kLn2 : INFINITY;
     }
     __syncthreads();  // LDS is reused by the paired block
   }
@@ -959,12 +1000,32 @@ constexpr size_t bwd_lds() {
   return (size_t)(128 * Geo<D>::TSTR + 2 * 32 * Geo<D>::KSTR + 32 * (128 + 8)) * 2 + 2 * 32 * 4;
 }
 
+// query fragments per wave: APEX_ATTN_FWD_QF=1|2 (A/B; default 1)
+inline int fwd_qf() {
+  const char* e = std::getenv("APEX_ATTN_FWD_QF");
+  return (e != nullptr && e[0] == '2') ? 2 : 1;
+}
+
+// occupancy: APEX_ATTN_FWD_OCC=lo (A/B; default the per-shape rule in fwd_occupancy)
+inline bool fwd_lo() {
+  const char* e = std::getenv("APEX_ATTN_FWD_OCC");
+  return e != nullptr && e[0] == 'l';
+}
+
+template <typename T, int D, int QF, bool LO>
+void launch_fwd_qf(const AttnArgs& a, hipStream_t s) {
+  const int nqb = (a.sq + 128 * QF - 1) / (128 * QF);
+  const dim3 grid(a.causal ? (nqb + 1) / 2 : nqb, a.h, a.b);
+  if (a.bias == nullptr && !(a.p_drop > 0.f))
+    hipLaunchKernelGGL((fwd_kernel<T, D, true, QF, LO>), grid, dim3(256), fwd_lds<D>(), s, a);
+  else hipLaunchKernelGGL((fwd_kernel<T, D, false, QF, LO>), grid, dim3(256), fwd_lds<D>(), s, a);
+}
+
 template <typename T, int D>
 void launch_fwd(const AttnArgs& a, hipStream_t s) {
-  const int nqb = (a.sq + 127) / 128;
-  const dim3 grid(a.causal ? (nqb + 1) / 2 : nqb, a.h, a.b);
-  if (a.bias == nullptr && !(a.p_drop > 0.f)) hipLaunchKernelGGL((fwd_kernel<T, D, true>), grid, dim3(256), fwd_lds<D>(), s, a);
-  else hipLaunchKernelGGL((fwd_kernel<T, D, false>), grid, dim3(256), fwd_lds<D>(), s, a);
+  if (fwd_qf() == 2) launch_fwd_qf<T, D, 2, false>(a, s);
+  else if (fwd_lo()) launch_fwd_qf<T, D, 1, true>(a, s);
+  else launch_fwd_qf<T, D, 1, false>(a, s);
 }
 
 template <int D>

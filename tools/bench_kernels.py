@@ -206,7 +206,8 @@ def bench_attn():
         flops = 4.0 * b * h * s * s * d * (0.5 if causal else 1.0)
         fwd = lambda: flash_attn_func(q, k, v, causal=causal)  # noqa: E731
         t = timeit(fwd)
-        var = {f"lazy{x}_ms": _with_env("APEX_ATTN_FWD_LAZY", str(x), lambda: timeit(fwd)) for x in (0, 1)}
+        var = {"qf2_ms": _with_env("APEX_ATTN_FWD_QF", "2", lambda: timeit(fwd)),
+               "occ_lo_ms": _with_env("APEX_ATTN_FWD_OCC", "lo", lambda: timeit(fwd))}
         qt, kt, vt = (x.detach().transpose(1, 2).contiguous().requires_grad_(True) for x in (q, k, v))
         tr = timeit(lambda: F.scaled_dot_product_attention(qt, kt, vt, is_causal=causal))
         emit(kernel="flash_fwd", b=b, s=s, h=h, d=d, causal=causal, ms=t, tflops=flops / t / 1e9, sdpa_ms=tr,
