@@ -53,6 +53,9 @@ def parse():
                     help="fused: apex.contrib.groupbn NHWC BN with fused ReLU / add+ReLU (gfx950 kernels); "
                          "torch: nn.BatchNorm2d + ReLU (MIOpen)")
     ap.add_argument("--lr", type=float, default=1e-3)
+    ap.add_argument("--no-graph", dest="graph", action="store_false",
+                    help="time eager steps instead of replaying the hipGraph-captured step (single-process runs "
+                         "capture one full training step after warm-up by default; APEX_BENCH_GRAPH=0 also disables)")
     ap.add_argument("--impl", default="apex", choices=["apex", "torch"],
                     help="torch = stock PyTorch-ROCm baseline (autocast bf16 + AdamW(fused) + torch DDP)")
     a = ap.parse_args()
@@ -173,12 +176,52 @@ def run_torch_baseline(args, dev, world, rank, distributed, resnet_mod):
     return timed(args, step, dev, world, rank, distributed, B, "torch")
 
 
+def _graphed(step):
+    """Capture one full training step (forward, backward, unscale + overflow check, optimizer)
+    in a hipGraph and return a callable that replays it.  Everything in the step is sync-free
+    (device loss scale, device skip flag, device step counter), so a replay is exactly one
+    training step.  Warm-up on the capture stream first so lazily built state (MTA work tables,
+    MIOpen solutions, workspaces) exists before capture."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        static_loss = step()
+
+    def replay():
+        g.replay()
+        return static_loss
+    return replay
+
+
 def timed(args, step, dev, world, rank, distributed, B, impl, desc=None):
     t0 = time.time()
     for i in range(args.warmup):
         step()
         if rank == 0 and (time.time() - t0) > 30 and i % 4 == 0:
             print(f"[bench] warmup step {i + 1}/{args.warmup}", file=sys.stderr, flush=True)
+    # the headline ResNet step only (the stock-torch baseline stays eager; the transformer
+    # benches draw dropout seeds on the host)
+    use_graph = (args.graph and impl == "apex" and desc is None and not distributed
+                 and os.environ.get("APEX_BENCH_GRAPH", "1") != "0")
+    args.graph = use_graph
+    if use_graph:
+        try:
+            step = _graphed(step)
+            step()
+        except Exception as e:
+            # a failed capture can leave the HIP context unusable: redo the whole run eagerly in a
+            # fresh child process and report its result
+            print(f"[bench] hipGraph capture failed ({type(e).__name__}: {e}); re-running eagerly",
+                  file=sys.stderr, flush=True)
+            import subprocess
+
+            r = subprocess.run([sys.executable, os.path.abspath(__file__)] + sys.argv[1:] + ["--no-graph"])
+            os._exit(r.returncode)
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
@@ -240,6 +283,7 @@ def timed(args, step, dev, world, rank, distributed, B, impl, desc=None):
                     if (impl == "apex" and args.bn == "fused" and not args.no_channels_last)
                     else ("apex SyncBatchNorm" if (args.sync_bn and distributed) else "torch BatchNorm2d (MIOpen)")),
                 "parallelism": f"dp{world}",
+                "hip_graph": bool(getattr(args, "graph", False)),
                 "final_loss": round(float(loss.item()), 4),
             },
         }

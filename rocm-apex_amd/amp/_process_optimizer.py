@@ -114,9 +114,20 @@ def lazy_init_with_master_weights(self):
     self.load_state_dict(self.state_dict())
 
 
+def _host_scale(scaler):
+    """The host copy of the loss scale when it is authoritative without a device read: always
+    for a static scaler; for a sync-free dynamic scaler the device value is read only when a
+    caller really needs the number (accumulated grads), never on the common path — a device
+    read would serialise the step and break hipGraph capture."""
+    if not scaler.dynamic:
+        return scaler._loss_scale
+    return None if scaler.sync_free else scaler.loss_scale()
+
+
 def post_backward_models_are_masters(scaler, params, stashed_grads, scale_override=None):
-    grads_have_scale, stashed_have_scale, out_scale = scaler.loss_scale(), 1.0, 1.0
-    if scaler.loss_scale() == 1.0 and not scaler.dynamic:
+    host = _host_scale(scaler)
+    grads_have_scale, stashed_have_scale, out_scale = host, 1.0, 1.0
+    if host == 1.0 and not scaler.dynamic:
         for i in range(len(stashed_grads)):
             stashed_grads[i] = None
         return
@@ -131,6 +142,8 @@ def post_backward_models_are_masters(scaler, params, stashed_grads, scale_overri
         elif param.grad is not None and stashed_grad is not None:
             needing_with_stash.append(param.grad)
             stashed.append(stashed_grad)
+    if needing_with_stash and grads_have_scale is None:
+        grads_have_scale = scaler.loss_scale()  # accumulation across losses needs the number
     if needing:
         scaler.unscale(needing, needing, None, models_are_masters=True,
                        scale_override=None if scale_override is None else grads_have_scale / out_scale)
@@ -230,7 +243,7 @@ def post_backward_with_master_weights(self, scaler):
             fp16_with_stash.append(fp16_param.grad)
             preexisting.append(fp32_param.grad)
     if fp16_needing:
-        scaler.unscale(fp16_needing, new_fp32, scaler.loss_scale(), models_are_masters=False)
+        scaler.unscale(fp16_needing, new_fp32, _host_scale(scaler), models_are_masters=False)
     if fp16_with_stash:
         scaler.unscale_with_stashed(fp16_with_stash, preexisting, preexisting)
     post_backward_models_are_masters(scaler, stash.all_fp32_from_fp32_params, stash.all_fp32_from_fp32_grad_stash)

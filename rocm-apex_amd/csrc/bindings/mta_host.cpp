@@ -22,7 +22,6 @@ namespace {
 struct Entry {
   std::vector<uint64_t> key;
   at::Tensor dev;   // the table
-  at::Tensor host;  // kept only for tables built during graph capture (replayed memcpy source)
   MtaMeta meta;
   bool pinned_forever = false;
   std::list<uint64_t>::iterator lru_it;
@@ -123,8 +122,8 @@ MtaMeta mta_meta(const std::vector<std::vector<at::Tensor>>& lists, int chunk_si
   const size_t off_ticket = align8(off_stage + sizeof(float) * 2 * (size_t)std::max(nchunks, 1));
   const size_t bytes = off_ticket + 64;
 
-  auto host = at::zeros({(int64_t)bytes}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
-  uint8_t* hb = host.data_ptr<uint8_t>();
+  std::vector<uint8_t> host(bytes, 0);
+  uint8_t* hb = host.data();
   auto* sizes = reinterpret_cast<int64_t*>(hb + off_sizes);
   auto* ptrs = reinterpret_cast<uint64_t*>(hb + off_ptrs);
   auto* chunks = reinterpret_cast<int2*>(hb + off_chunks);
@@ -138,7 +137,9 @@ MtaMeta mta_meta(const std::vector<std::vector<at::Tensor>>& lists, int chunk_si
 
   const c10::hip::HIPGuard guard(dev.index());
   auto devbuf = at::empty({(int64_t)bytes}, at::TensorOptions().dtype(at::kByte).device(dev));
-  devbuf.copy_(host, /*non_blocking=*/true);
+  // through kernel arguments: no pinned staging buffer whose allocator events would break
+  // hipGraph capture, and nothing to keep alive for replays
+  mta_upload_bytes(devbuf.data_ptr(), hb, bytes, cur_stream());
 
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   hipStreamIsCapturing(cur_stream(), &cap);
@@ -182,10 +183,7 @@ MtaMeta mta_meta(const std::vector<std::vector<at::Tensor>>& lists, int chunk_si
   e.dev = devbuf;
   e.meta = m;
   e.lru_it = g_lru.begin();
-  if (cap != hipStreamCaptureStatusNone) {
-    e.pinned_forever = true;
-    e.host = host;
-  }
+  if (cap != hipStreamCaptureStatusNone) e.pinned_forever = true;
   g_cache[h] = std::move(e);
   return m;
 }

@@ -13,6 +13,9 @@ struct Launch {
 };
 
 // out = in * scale; noop |= !finite(in)   (reference csrc/multi_tensor_scale_kernel.cu:30-111)
+// copy a host-built work table to the device through kernel arguments (capture-safe)
+void mta_upload_bytes(void* dst, const void* src, size_t bytes, hipStream_t s);
+
 void mt_scale(const MtaMeta& m, int in_t, int out_t, int* noop, DevScalar scale, const Launch& L);
 // out = a*x + b*y; arg_to_check: -1 both, 0 x, 1 y   (reference csrc/multi_tensor_axpby_kernel.cu:28-126)
 void mt_axpby(const MtaMeta& m, int x_t, int y_t, int out_t, int* noop, float a, float b, int arg_to_check,

@@ -3,10 +3,39 @@
 // Reference semantics (what each op computes) come from the reference's csrc/multi_tensor_*.cu;
 // the execution model is our own: one persistent launch per op over a cached device work table
 // (mta.h), 8 elements per lane per step, reductions finalized in-launch by the last block.
+#include <cstring>
+
 #include "apex_amd/mta_api.h"
 #include "apex_amd/dispatch.h"
 
 namespace apex_amd {
+
+// =============================================================================================
+// table upload without host staging memory: the bytes travel as kernel arguments, so building a
+// work table is capturable in a hipGraph (no pinned-allocator events, no memcpy node)
+// =============================================================================================
+constexpr int kUploadChunk = 2048;
+struct UploadPayload {
+  uint32_t w[kUploadChunk / 4];
+};
+
+__global__ void __launch_bounds__(256) mta_upload_kernel(uint32_t* __restrict__ dst, int nwords, UploadPayload p) {
+  for (int i = threadIdx.x; i < nwords; i += 256) dst[i] = p.w[i];
+}
+
+void mta_upload_bytes(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  // tables are 8-byte aligned and sized in 8-byte units
+  const uint8_t* in = static_cast<const uint8_t*>(src);
+  uint8_t* out = static_cast<uint8_t*>(dst);
+  for (size_t off = 0; off < bytes; off += kUploadChunk) {
+    const size_t n = bytes - off < (size_t)kUploadChunk ? bytes - off : (size_t)kUploadChunk;
+    UploadPayload p;
+    std::memcpy(p.w, in + off, n);
+    hipLaunchKernelGGL(mta_upload_kernel, dim3(1), dim3(256), 0, s, reinterpret_cast<uint32_t*>(out + off),
+                       (int)((n + 3) / 4), p);
+  }
+  check_launch("mta_upload");
+}
 
 // =============================================================================================
 // scale / axpby / check_finite
