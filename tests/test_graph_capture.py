@@ -45,11 +45,21 @@ def test_graph_replay_matches_eager_steps():
             return loss
         return step
 
-    # eager reference: 3 warm-up steps + 4 steps
-    model_e, opt_e = _build(1, dev)
-    step_e = make_step(model_e, opt_e)
-    eager_losses = [float(step_e()) for _ in range(7)]
-    ref = [p.detach().float().clone() for p in model_e.parameters()]
+    # eager reference: 3 warm-up steps + 4 steps, twice (run-to-run spread of the eager path:
+    # library conv algorithms and Adam's ~lr-sized steps on near-zero gradients)
+    runs = []
+    for _ in range(2):
+        _amp_state.loss_scalers = []
+        model_e, opt_e = _build(1, dev)
+        step_e = make_step(model_e, opt_e)
+        eager_losses = [float(step_e()) for _ in range(7)]
+        runs.append([p.detach().float().clone() for p in model_e.parameters()])
+    ref = runs[0]
+
+    def max_rel(xs, ys):
+        return max(float((a - b).norm() / b.norm().clamp_min(1e-6)) for a, b in zip(xs, ys))
+
+    spread = max_rel(runs[1], runs[0])
 
     _amp_state.loss_scalers = []
     model_g, opt_g = _build(1, dev)
@@ -68,8 +78,9 @@ def test_graph_replay_matches_eager_steps():
         losses.append(float(static_loss))
     torch.cuda.synchronize()
     torch.testing.assert_close(torch.tensor(warm + losses), torch.tensor(eager_losses), rtol=2e-2, atol=2e-2)
-    for a, b in zip(model_g.parameters(), ref):
-        torch.testing.assert_close(a.detach().float(), b, rtol=2e-2, atol=2e-3)
+    # whole-tensor relative error, bounded by the eager run-to-run spread
+    got = max_rel([p.detach().float() for p in model_g.parameters()], ref)
+    assert got <= max(3 * spread, 5e-3), (got, spread)
     # the device step counter advanced once per replay
     st = opt_g.param_groups[0]["_step_t"]
     assert int(st.item()) == 7
