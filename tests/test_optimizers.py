@@ -175,3 +175,40 @@ def test_adam_capturable_matches_plain_gpu():
                                        step_t, 1, 1, 0.01, inv)
     for a, b in zip(snap, p2):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_adam_capturable_resume_continues_bias_correction(dev):
+    """save -> load -> continue equals uninterrupted training (the device step counter is seeded
+    from the checkpointed step, so bias correction does not restart)."""
+    from apex.optimizers import FusedAdam
+
+    def params():
+        torch.manual_seed(0)
+        return [torch.nn.Parameter(torch.randn(257, device=dev)), torch.nn.Parameter(torch.randn(33, 7, device=dev))]
+
+    def grads(i, ps):
+        g = torch.Generator(device="cpu").manual_seed(100 + i)
+        for p in ps:
+            p.grad = torch.randn(p.shape, generator=g).to(dev)
+
+    ref_p = params()
+    ref = FusedAdam(ref_p, lr=1e-2, capturable=True)
+    for i in range(5):
+        grads(i, ref_p)
+        ref.step()
+    a_p = params()
+    a = FusedAdam(a_p, lr=1e-2, capturable=True)
+    for i in range(3):
+        grads(i, a_p)
+        a.step()
+    sd = a.state_dict()
+    assert sd["param_groups"][0]["step"] == 3
+    b_p = [torch.nn.Parameter(p.detach().clone()) for p in a_p]
+    b = FusedAdam(b_p, lr=1e-2, capturable=True)
+    b.load_state_dict(sd)
+    for i in range(3, 5):
+        grads(i, b_p)
+        b.step()
+    for x, y in zip(b_p, ref_p):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
