@@ -2,10 +2,13 @@
 (reference apex/contrib/bottleneck/bottleneck.py:10-520).
 
 The reference's fast path (``use_cudnn=True``) is a cuDNN-frontend fused graph of
-conv -> scale/bias -> ReLU chains.  Here the frozen BN is folded into the convolution (w * s,
-bias b) inside the autograd graph — exact for frozen statistics, and the gradient w.r.t. the
-raw weight flows through the fold — so each stage is ONE MIOpen conv-with-bias (+ ReLU) in
-channels_last, with the residual add + ReLU as one fused elementwise op.  ``explicit_nhwc``
+conv -> scale/bias -> ReLU chains (apex/contrib/csrc/bottleneck/bottleneck.cpp).  Here every
+stage is ONE native implicit-GEMM launch (``apex.ops.conv.conv_bn_act``,
+csrc/conv/conv_igemm.hip) whose epilogue applies the frozen-BN scale / bias, the residual add of
+the last stage and the ReLU to the fp32 accumulator — channels_last bf16/fp16, C and K multiples
+of 64.  Other shapes / dtypes fold the frozen BN into the convolution (w * s, bias b) inside the
+autograd graph — exact for frozen statistics, the raw-weight gradient flows through the fold —
+and run one MIOpen conv-with-bias per stage.  ``explicit_nhwc``
 tensors ([N, H, W, C] inputs, [K, R, S, C] weights) are consumed as zero-copy channels_last
 views.  ``SpatialBottleneck`` splits H over ``spatial_group_size`` ranks with a 1-row halo
 exchange before the 3x3 conv (see :mod:`.halo_exchangers`)."""
@@ -14,7 +17,8 @@ import torch.distributed as dist
 import torch.nn.functional as F
 from torch import nn
 
-from .halo_exchangers import halo_pad
+from ...ops.conv import conv_bn_act, conv_bn_act_supported
+from .halo_exchangers import halo_pad, make_exchanger
 
 
 def kaiming_uniform_(tensor, a=0, mode="fan_in", nonlinearity="leaky_relu"):
@@ -90,6 +94,9 @@ class _BottleneckBase(nn.Module):
         for w in self.w_conv:
             kaiming_uniform_(w, a=1)
         self.explicit_nhwc = explicit_nhwc
+        # native conv + scale/bias/residual/ReLU kernels on the fused path (False: MIOpen with the
+        # BN folded into the weights; the A/B switch)
+        self.use_native = True
         if explicit_nhwc:
             for p in self.parameters():
                 with torch.no_grad():
@@ -109,26 +116,37 @@ class _BottleneckBase(nn.Module):
     def _conv2_plain(self, out):
         return self.conv2(out)
 
-    def _conv2_folded(self, out, w2, b2):
-        return F.conv2d(out, w2, b2, padding=1)
+    def _conv2_input(self, out):
+        """(input, padding) of the 3x3 conv (the spatial variant pads H with neighbour halos)."""
+        return out, (1, 1)
 
-    # ---- fused path: frozen BN folded into every conv ----
+    def _stage(self, x, conv, bn, residual=None, relu=True, stride=1, padding=(0, 0)):
+        """act(conv(x) * s + b [+ residual]) for a frozen BN (s, b): one native conv launch with
+        the scale / bias / residual / ReLU epilogue where supported, else the BN folded into a
+        MIOpen conv-with-bias."""
+        w = conv.weight.permute(0, 3, 1, 2) if self.explicit_nhwc else conv.weight
+        if self.use_native and conv_bn_act_supported(x, w, residual):
+            s, b = bn.get_scale_bias(False)
+            return conv_bn_act(x, w, s.reshape(-1), b.reshape(-1), residual, relu, stride, padding)
+        wf, bf = _fold(conv.weight, bn, self.explicit_nhwc)
+        y = F.conv2d(x, wf, bf, stride=stride, padding=padding)
+        if residual is not None:
+            y = y + residual
+        return F.relu(y) if relu else y
+
+    # ---- fused path: conv -> frozen-BN scale/bias -> (+ residual) -> ReLU per stage ----
     def _forward_fused(self, x):
         nhwc = self.explicit_nhwc
         if nhwc:
             x = x.permute(0, 3, 1, 2)  # [N, H, W, C] -> channels_last NCHW view
-        w1, b1 = _fold(self.conv1.weight, self.bn1, nhwc)
-        w2, b2 = _fold(self.conv2.weight, self.bn2, nhwc)
-        w3, b3 = _fold(self.conv3.weight, self.bn3, nhwc)
-        out = F.relu(F.conv2d(x, w1, b1, stride=self.stride))
-        out = F.relu(self._conv2_folded(out, w2, b2))
-        out = F.conv2d(out, w3, b3)
         if self.downsample is not None:
-            w4, b4 = _fold(self.downsample[0].weight, self.downsample[1], nhwc)
-            identity = F.conv2d(x, w4, b4, stride=self.stride)
+            identity = self._stage(x, self.downsample[0], self.downsample[1], relu=False, stride=self.stride)
         else:
             identity = x
-        out = F.relu(out + identity)
+        out = self._stage(x, self.conv1, self.bn1, stride=self.stride)
+        inp, pad = self._conv2_input(out)
+        out = self._stage(inp, self.conv2, self.bn2, padding=pad)
+        out = self._stage(out, self.conv3, self.bn3, residual=identity)
         return out.permute(0, 2, 3, 1) if nhwc else out
 
     def forward(self, x):
@@ -143,7 +161,8 @@ class Bottleneck(_BottleneckBase):
 
 class SpatialBottleneck(_BottleneckBase):
     def __init__(self, in_channels, bottleneck_channels, out_channels, stride=1, groups=1, dilation=1,
-                 norm_func=None, use_cudnn=False, explicit_nhwc=False, spatial_group_size=1, communicator=None):
+                 norm_func=None, use_cudnn=False, explicit_nhwc=False, spatial_group_size=1, communicator=None,
+                 halo_ex="sendrecv"):
         super().__init__(in_channels, bottleneck_channels, out_channels, stride, groups, dilation, norm_func,
                          use_cudnn, explicit_nhwc)
         self.spatial_group_size = spatial_group_size
@@ -163,16 +182,19 @@ class SpatialBottleneck(_BottleneckBase):
         else:
             self.local_rank = 0
             self.communicator = None
+        # "sendrecv" (neighbour P2P over xGMI, default), "allgather", "nocomm" or a HaloExchanger
+        self.halo_ex = make_exchanger(halo_ex, self.communicator, self.local_rank, spatial_group_size) \
+            if spatial_group_size > 1 else None
 
     def _halo(self, out):
-        return halo_pad(out, 1, self.communicator, self.local_rank, self.spatial_group_size)
+        return halo_pad(out, 1, self.communicator, self.local_rank, self.spatial_group_size, self.halo_ex)
 
     def _conv2_plain(self, out):
         if self.spatial_group_size == 1:
             return self.conv2(out)
         return F.conv2d(self._halo(out), self.conv2.weight, None, padding=(0, 1))
 
-    def _conv2_folded(self, out, w2, b2):
+    def _conv2_input(self, out):
         if self.spatial_group_size == 1:
-            return F.conv2d(out, w2, b2, padding=1)
-        return F.conv2d(self._halo(out), w2, b2, padding=(0, 1))
+            return out, (1, 1)
+        return self._halo(out), (0, 1)

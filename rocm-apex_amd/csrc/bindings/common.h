@@ -32,7 +32,7 @@ inline int device_cus(int dev) {
   if (dev < 0 || dev >= 64) dev = 0;
   if (!cache[dev]) {
     int n = 0;
-    hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 0;
     cache[dev] = n > 0 ? n : 256;
   }
   return cache[dev];

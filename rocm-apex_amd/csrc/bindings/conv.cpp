@@ -57,8 +57,25 @@ ConvTapArgs make_args(const at::Tensor& in, const at::Tensor& w, const at::Tenso
 // out[n, oh*osh+oph, ow*osw+opw, k] = sum_t,c in[n, oh*ish+dh[t], ow*isw+dw[t], c] * w[k, t, c]
 void tap_fprop(const at::Tensor& in, const at::Tensor& w, at::Tensor& out, int64_t oh, int64_t ow, int64_t ish,
                int64_t isw, int64_t osh, int64_t osw, int64_t oph, int64_t opw, std::vector<int64_t> dh,
-               std::vector<int64_t> dw) {
+               std::vector<int64_t> dw, const c10::optional<at::Tensor>& scale,
+               const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& residual, bool relu) {
   ConvTapArgs a = make_args(in, w, out, oh, ow, ish, isw, osh, osw, oph, opw, dh, dw);
+  auto per_channel = [&](const c10::optional<at::Tensor>& t, const char* what) -> const float* {
+    if (!t.has_value()) return nullptr;
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == out.size(3),
+                "conv tap_fprop: ", what, " must be a contiguous fp32 [K] tensor on the output's device");
+    return t->data_ptr<float>();
+  };
+  a.scale = per_channel(scale, "scale");
+  a.bias = per_channel(bias, "bias");
+  if (residual.has_value()) {
+    check_nhwc(*residual, "residual");
+    TORCH_CHECK(residual->sizes() == out.sizes() && residual->strides() == out.strides() &&
+                    residual->scalar_type() == out.scalar_type(),
+                "conv tap_fprop: residual must match the output's shape, layout and dtype");
+    a.residual = residual->data_ptr();
+  }
+  a.relu = relu ? 1 : 0;
   const c10::hip::HIPGuard g(in.get_device());
   TORCH_CHECK(conv_tap_supported(a), "conv tap_fprop: unsupported (C and K must be multiples of 64, bf16/fp16)");
   conv_tap_fprop(a, device_cus(in.get_device()), cur_stream());
@@ -88,7 +105,11 @@ void wgrad(const at::Tensor& in, const at::Tensor& dy, at::Tensor& dw_out, int64
 
 void bind_conv(pybind11::module_& root) {
   auto m = root.def_submodule("conv", "gfx950 implicit-GEMM NHWC convolutions");
-  m.def("tap_fprop", &tap_fprop);
+  m.def("tap_fprop", &tap_fprop, pybind11::arg("input"), pybind11::arg("weight"), pybind11::arg("out"),
+        pybind11::arg("oh"), pybind11::arg("ow"), pybind11::arg("ish"), pybind11::arg("isw"), pybind11::arg("osh"),
+        pybind11::arg("osw"), pybind11::arg("oph"), pybind11::arg("opw"), pybind11::arg("dh"), pybind11::arg("dw"),
+        pybind11::arg("scale") = pybind11::none(), pybind11::arg("bias") = pybind11::none(),
+        pybind11::arg("residual") = pybind11::none(), pybind11::arg("relu") = false);
   m.def("wgrad", &wgrad);
   m.def("force_fprop_cfg", &conv_force_fprop_cfg);
 }

@@ -46,6 +46,10 @@ __device__ __attribute__((aligned(16))) uint16_t g_zero[64];
 struct Geo {
   int n, h, w, c, oh, ow, oht, owt, kout, ish, isw, osh, osw, oph, opw, ntaps, m;
   int dh[kConvMaxTaps], dw[kConvMaxTaps];
+  const float* scale;
+  const float* bias;
+  const uint16_t* res;
+  int relu;
 };
 
 inline Geo make_geo(const ConvTapArgs& a) {
@@ -54,6 +58,10 @@ inline Geo make_geo(const ConvTapArgs& a) {
   g.kout = a.kout; g.ish = a.ish; g.isw = a.isw; g.osh = a.osh; g.osw = a.osw; g.oph = a.oph; g.opw = a.opw;
   g.ntaps = a.ntaps;
   g.m = a.n * a.oh * a.ow;
+  g.scale = a.scale;
+  g.bias = a.bias;
+  g.res = reinterpret_cast<const uint16_t*>(a.residual);
+  g.relu = a.relu;
   for (int t = 0; t < kConvMaxTaps; ++t) {
     g.dh[t] = t < a.ntaps ? a.dh[t] : 0;
     g.dw[t] = t < a.ntaps ? a.dw[t] : 0;
@@ -236,6 +244,16 @@ fprop_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, ui
   float* cs = reinterpret_cast<float*>(lds);
   const int ch = tid % CPR, rsub = tid / CPR;
   const int gc = col0 + ch * 8;
+  // fused epilogue operands of this thread's 8 columns (folded-BN scale/bias: per channel)
+  float sc[8], bi[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = 1.f;
+    bi[e] = 0.f;
+  }
+  if (g.scale) Vec8<float>::load(sc, g.scale + gc);
+  if (g.bias) Vec8<float>::load(bi, g.bias + gc);
+  const bool affine = g.scale || g.bias;
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     const int wr0 = wm * (BM / WM);
@@ -265,6 +283,20 @@ fprop_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, ui
         const float4 hi = *reinterpret_cast<const float4*>(cs + rl * CST + ch * 8 + 4);
         v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
         v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+        if (affine) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaf(v[e], sc[e], bi[e]);
+        }
+        if (g.res) {
+          float r[8];
+          Vec8<T>::load(r, reinterpret_cast<const T*>(g.res) + pix * g.kout + gc);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += r[e];
+        }
+        if (g.relu) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
         Vec8<T>::store(reinterpret_cast<T*>(Y) + pix * g.kout + gc, v);
       }
     }
@@ -463,6 +495,8 @@ bool conv_tap_supported(const ConvTapArgs& a) {
   if (a.ntaps < 1 || a.ntaps > kConvMaxTaps) return false;
   if (a.n <= 0 || a.oh <= 0 || a.ow <= 0) return false;
   if ((int64_t)a.n * a.oh * a.ow >= (1ll << 31) || (int64_t)a.n * a.ih * a.iw >= (1ll << 31)) return false;
+  if ((a.scale && !aligned16(a.scale)) || (a.bias && !aligned16(a.bias)) || (a.residual && !aligned16(a.residual)))
+    return false;
   return aligned16(a.in) && aligned16(a.wt) && aligned16(a.out);
 }
 

@@ -22,6 +22,7 @@
 // also write the ReLU mask as 1 bit per element in the apply pass (1/16 of a bf16 pass); their
 // backward reduction masks dy with those bits, so z is neither re-read nor kept alive.
 #include "apex_amd/bn_nhwc_api.h"
+#include "apex_amd/colsum.h"
 #include "apex_amd/device.h"
 #include "apex_amd/dispatch.h"
 
@@ -105,28 +106,10 @@ __global__ void __launch_bounds__(256) stats_partial(const T* __restrict__ x, in
       }
     }
   }
-  const int W = TX * 8;
-  if (active) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      smem[ty * W + tx * 8 + k] = s[k];
-      smem[TY * W + ty * W + tx * 8 + k] = ss[k];
-    }
-  }
+  ColSum<8>::stash(smem, 0, s, tx, ty, TX, TY);
+  ColSum<8>::stash(smem, 1, ss, tx, ty, TX, TY);
   __syncthreads();
-  if (ty == 0 && active) {
-    const int gy = gridDim.y;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float a = 0.f, b = 0.f;
-      for (int j = 0; j < TY; ++j) {
-        a += smem[j * W + tx * 8 + k];
-        b += smem[TY * W + j * W + tx * 8 + k];
-      }
-      part[(int64_t)blockIdx.y * c + c0 + k] = a;
-      part[(int64_t)gy * c + (int64_t)blockIdx.y * c + c0 + k] = b;
-    }
-  }
+  ColSum<8>::reduce_store(smem, 2, TX, TY, c, blockIdx.x * TX * 8, part, (int64_t)gridDim.y * c, blockIdx.y);
 }
 
 // Sum the gy partial rows of two [gy][C] slabs for kFinC channels per block: thread (ch, g) sums
@@ -371,28 +354,10 @@ __global__ void __launch_bounds__(256) bwd_partial(const T* __restrict__ dy, con
       }
     }
   }
-  const int W = TX * 8;
-  if (active) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      smem[ty * W + tx * 8 + k] = a1[k];
-      smem[TY * W + ty * W + tx * 8 + k] = a2[k];
-    }
-  }
+  ColSum<8>::stash(smem, 0, a1, tx, ty, TX, TY);
+  ColSum<8>::stash(smem, 1, a2, tx, ty, TX, TY);
   __syncthreads();
-  if (ty == 0 && active) {
-    const int gy = gridDim.y;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float p = 0.f, q = 0.f;
-      for (int j = 0; j < TY; ++j) {
-        p += smem[j * W + tx * 8 + k];
-        q += smem[TY * W + j * W + tx * 8 + k];
-      }
-      part[(int64_t)blockIdx.y * c + c0 + k] = p;
-      part[(int64_t)gy * c + (int64_t)blockIdx.y * c + c0 + k] = q;
-    }
-  }
+  ColSum<8>::reduce_store(smem, 2, TX, TY, c, blockIdx.x * TX * 8, part, (int64_t)gridDim.y * c, blockIdx.y);
 }
 
 __global__ void __launch_bounds__(256) bwd_finalize(const float* __restrict__ part, int gy, int c, float inv_n,
@@ -511,7 +476,7 @@ void bn_nhwc_stats(const void* x, int x_t, int64_t m, int c, const float* w, con
   bnh::check_shape(m, c);
   (void)gy;  // the statistics pass has its own (deeper) geometry; ws is sized for it by bn_nhwc_plan
   const bnh::Geo g = bnh::geo(m, c, cus, bnh::kStatsBlocksPerCu);
-  const size_t lds = (size_t)2 * g.ty * g.tx * 8 * sizeof(float);
+  const size_t lds = ColSum<8>::lds_floats(g.tx, g.ty, 2) * sizeof(float);
   dispatch_float(x_t, [&](auto tag) {
     using T = typename decltype(tag)::type;
     hipLaunchKernelGGL((bnh::stats_partial<T>), dim3(g.gx, g.gy), dim3(g.tx, g.ty), lds, s, (const T*)x, m, c, ws);
@@ -526,7 +491,7 @@ void bn_nhwc_stats_local(const void* x, int x_t, int64_t m, int c, float* payloa
   bnh::check_shape(m, c);
   (void)gy;
   const bnh::Geo g = bnh::geo(m, c, cus, bnh::kStatsBlocksPerCu);
-  const size_t lds = (size_t)2 * g.ty * g.tx * 8 * sizeof(float);
+  const size_t lds = ColSum<8>::lds_floats(g.tx, g.ty, 2) * sizeof(float);
   dispatch_float(x_t, [&](auto tag) {
     using T = typename decltype(tag)::type;
     hipLaunchKernelGGL((bnh::stats_partial<T>), dim3(g.gx, g.gy), dim3(g.tx, g.ty), lds, s, (const T*)x, m, c, ws);
@@ -601,7 +566,7 @@ void bn_nhwc_bwd_reduce(const void* dy, const void* x, int x_t, const void* z, c
   bnh::check_shape(m, c);
   bnh::Geo g = bnh::geo(m, c, cus);
   g.gy = gy;
-  const size_t lds = (size_t)2 * g.ty * g.tx * 8 * sizeof(float);
+  const size_t lds = ColSum<8>::lds_floats(g.tx, g.ty, 2) * sizeof(float);
   dispatch_float(x_t, [&](auto tag) {
     using T = typename decltype(tag)::type;
     auto go = [&](auto hz, auto rl, auto wm, auto d2) {

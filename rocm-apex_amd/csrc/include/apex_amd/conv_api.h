@@ -32,6 +32,13 @@ struct ConvTapArgs {
   int ntaps;
   int dh[kConvMaxTaps], dw[kConvMaxTaps];
   int dtype;        // kBF16 / kF16
+  // optional fprop epilogue, applied to the fp32 accumulator before the store (null = off):
+  //   y = act(acc * scale[k] + bias[k] + residual[pix, k]),  act = ReLU when relu != 0
+  // scale / bias are fp32 [kout]; residual has the output tensor's layout and dtype
+  const float* scale = nullptr;
+  const float* bias = nullptr;
+  const void* residual = nullptr;
+  int relu = 0;
 };
 
 // shape constraints: c % 64 == 0, kout % 64 == 0, 16-byte aligned pointers

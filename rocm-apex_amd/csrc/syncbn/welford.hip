@@ -14,6 +14,7 @@
 //  * fused ReLU: forward writes relu(bn(x)+z); backward kernels recompute that value in
 //    registers to mask dy instead of materialising the masked gradient.
 //  * elementwise kernels are grid-stride over 8-element vectors, grid sized to the 256 CUs.
+#include "apex_amd/colsum.h"
 #include "apex_amd/device.h"
 #include "apex_amd/dispatch.h"
 #include "apex_amd/syncbn_api.h"
@@ -98,33 +99,31 @@ __global__ void __launch_bounds__(256) welford_clast_kernel(const T* __restrict_
       }
     }
   }
-  const int W = TX * VEC;
-  float* sm = smem;
-  float* s2 = smem + TY * W;
-  float* sn = smem + 2 * TY * W;
-  if (active) {
-#pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-      sm[ty * W + tx * VEC + k] = mean[k];
-      s2[ty * W + tx * VEC + k] = m2[k];
-    }
-  }
+  // (mean, M2) staged component-major (apex_amd/colsum.h layout), merged over ty with Chan's
+  // formula in a fixed order by lanes o = (tx, k), k fastest
+  using CS = ColSum<VEC>;
+  const int KS = CS::ks(TX, TY);
+  float* sn = smem + CS::lds_floats(TX, TY, 2);
+  CS::stash(smem, 0, mean, tx, ty, TX, TY);
+  CS::stash(smem, 1, m2, tx, ty, TX, TY);
   if (tx == 0) sn[ty] = n;
   __syncthreads();
-  if (ty == 0 && active) {
-    const int gy = gridDim.y;
-#pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-      float nn = sn[0], mm = sm[tx * VEC + k], MM = s2[tx * VEC + k];
-      for (int j = 1; j < TY; ++j) chan_merge(nn, mm, MM, sn[j], sm[j * W + tx * VEC + k], s2[j * W + tx * VEC + k]);
-      ws[(int64_t)blockIdx.y * c + c0 + k] = mm;
-      ws[(int64_t)gy * c + (int64_t)blockIdx.y * c + c0 + k] = MM;
-    }
-    if (blockIdx.x == 0 && tx == 0) {
-      float nn = 0.f;
-      for (int j = 0; j < TY; ++j) nn += sn[j];
-      ws[2 * (int64_t)gy * c + blockIdx.y] = nn;
-    }
+  const int gy = gridDim.y, tid = ty * TX + tx;
+  for (int o = tid; o < VEC * TX; o += TX * TY) {
+    const int txo = o / VEC, k = o - txo * VEC;
+    const int ch = (blockIdx.x * TX + txo) * VEC + k;
+    if (ch >= c) continue;
+    const float* pm = smem + k * KS + txo;
+    const float* p2 = smem + (VEC + k) * KS + txo;
+    float nn = sn[0], mm = pm[0], MM = p2[0];
+    for (int j = 1; j < TY; ++j) chan_merge(nn, mm, MM, sn[j], pm[j * TX], p2[j * TX]);
+    ws[(int64_t)blockIdx.y * c + ch] = mm;
+    ws[(int64_t)gy * c + (int64_t)blockIdx.y * c + ch] = MM;
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    float nn = 0.f;
+    for (int j = 0; j < TY; ++j) nn += sn[j];
+    ws[2 * (int64_t)gy * c + blockIdx.y] = nn;
   }
 }
 
@@ -301,28 +300,10 @@ __global__ void __launch_bounds__(256) reduce_clast_kernel(const T* __restrict__
       }
     }
   }
-  const int W = TX * VEC;
-  if (active) {
-#pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-      smem[ty * W + tx * VEC + k] = s1[k];
-      smem[TY * W + ty * W + tx * VEC + k] = s2[k];
-    }
-  }
+  ColSum<VEC>::stash(smem, 0, s1, tx, ty, TX, TY);
+  ColSum<VEC>::stash(smem, 1, s2, tx, ty, TX, TY);
   __syncthreads();
-  if (ty == 0 && active) {
-    const int gy = gridDim.y;
-#pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-      float a = 0.f, b = 0.f;
-      for (int j = 0; j < TY; ++j) {
-        a += smem[j * W + tx * VEC + k];
-        b += smem[TY * W + j * W + tx * VEC + k];
-      }
-      ws[(int64_t)blockIdx.y * c + c0 + k] = a;
-      ws[(int64_t)gy * c + (int64_t)blockIdx.y * c + c0 + k] = b;
-    }
-  }
+  ColSum<VEC>::reduce_store(smem, 2, TX, TY, c, blockIdx.x * TX * VEC, ws, (int64_t)gridDim.y * c, blockIdx.y);
 }
 
 template <typename T>
@@ -453,7 +434,7 @@ void bn_welford(const void* x, int x_t, const BnShape& sh, float* mean, float* v
     if (sh.c_last) {
       const bool v8 = bn::use_vec8(sh, {x});
       const bn::Tiling t = bn::clast_tiling(sh.n, sh.c, v8, cus);
-      const size_t lds = ((size_t)2 * t.ty * t.tx * t.vec + t.ty) * sizeof(float);
+      const size_t lds = ((t.vec == 8 ? ColSum<8>::lds_floats(t.tx, t.ty, 2) : ColSum<1>::lds_floats(t.tx, t.ty, 2)) + t.ty) * sizeof(float);
       if (v8)
         hipLaunchKernelGGL((bn::welford_clast_kernel<T, 8>), dim3(t.gx, t.gy), dim3(t.tx, t.ty), lds, s, (const T*)x,
                            sh.n, sh.c, ws);
@@ -527,7 +508,7 @@ void bn_reduce(const void* dy, const void* x, int x_t, const BnParams& p, const 
     if (sh.c_last) {
       const bool v8 = bn::use_vec8(sh, {x, dy, r.z});
       const bn::Tiling t = bn::clast_tiling(sh.n, sh.c, v8, cus);
-      const size_t lds = (size_t)2 * t.ty * t.tx * t.vec * sizeof(float);
+      const size_t lds = (t.vec == 8 ? ColSum<8>::lds_floats(t.tx, t.ty, 2) : ColSum<1>::lds_floats(t.tx, t.ty, 2)) * sizeof(float);
       if (v8)
         hipLaunchKernelGGL((bn::reduce_clast_kernel<T, TW, 8>), dim3(t.gx, t.gy), dim3(t.tx, t.ty), lds, s,
                            (const T*)dy, (const T*)x, p, r, sh.n, sh.c, ws);

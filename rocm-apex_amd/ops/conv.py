@@ -147,6 +147,87 @@ def conv_tap_forward(x, w, stride, pad):
     return y
 
 
+# ------------------------------------------------------------------------------------------------
+# conv -> per-channel scale/bias (frozen BN) -> (+ residual) -> ReLU in ONE kernel: the fprop
+# epilogue applies the chain to the fp32 accumulator before the bf16/fp16 store.  Capability of
+# the reference's cudnn-frontend conv+scale+bias+ReLU graphs
+# (apex/contrib/csrc/bottleneck/bottleneck.cpp:1-120, run_conv_scale_bias_add_activation).
+# ------------------------------------------------------------------------------------------------
+def conv_bn_act_supported(x, w, residual=None):
+    """True when ``conv_bn_act`` runs the native fused kernel for these operands."""
+    k = w.shape[2] if w.dim() == 4 else 0
+    return (x.is_cuda and x.dim() == 4 and w.dim() == 4 and x.dtype == w.dtype
+            and x.dtype in (torch.bfloat16, torch.float16) and x.shape[1] % 64 == 0 and w.shape[0] % 64 == 0
+            and w.shape[2] == w.shape[3] and k in (1, 3)
+            and x.is_contiguous(memory_format=torch.channels_last)
+            and (residual is None or residual.dtype == x.dtype) and _native.available())
+
+
+def _conv_bn_act_reference(x, w, scale, bias, residual, relu, stride, padding):
+    """fp32-accumulated torch composition of the fused op (CPU / unsupported-shape path)."""
+    y = F.conv2d(x, w, None, stride, padding)
+    y = y * scale.to(y.dtype).view(1, -1, 1, 1) + bias.to(y.dtype).view(1, -1, 1, 1)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y
+
+
+class _ConvBnActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, scale, bias, residual, relu, stride, padding):
+        n, c, h, wd = x.shape
+        kout, _, k, _ = w.shape
+        ph, pw = padding
+        oh, ow = (h + 2 * ph - k) // stride + 1, (wd + 2 * pw - k) // stride + 1
+        y = torch.empty((n, kout, oh, ow), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+        taps = [(r - ph, s_ - pw) for r in range(k) for s_ in range(k)]
+        res = None
+        if residual is not None:
+            res = _nhwc(residual.contiguous(memory_format=torch.channels_last))
+        _conv_ext().tap_fprop(_nhwc(x), _w_krc(w).contiguous(), _nhwc(y), oh, ow, stride, stride, 1, 1, 0, 0,
+                              [t[0] for t in taps], [t[1] for t in taps], scale.float().contiguous(),
+                              bias.float().contiguous(), res, bool(relu))
+        ctx.save_for_backward(x, w, scale, y if relu else None)
+        ctx.conf = (relu, stride, padding, residual is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, scale, y = ctx.saved_tensors
+        relu, stride, padding, has_res = ctx.conf
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        if relu:
+            gy = torch.where(y > 0, gy, torch.zeros((), dtype=gy.dtype, device=gy.device))
+        g_res = gy if has_res and ctx.needs_input_grad[4] else None
+        g = gy * scale.to(gy.dtype).view(1, -1, 1, 1)
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        dx = dw = None
+        if need_x or need_w:
+            dx, dw, _ = torch.ops.aten.convolution_backward(g, x, w, None, [stride, stride], list(padding), [1, 1],
+                                                            False, [0, 0], 1, [need_x, need_w, False])
+        return dx, dw, None, None, g_res, None, None, None
+
+
+def conv_bn_act(x, w, scale, bias, residual=None, relu=True, stride=1, padding=0):
+    """``act(conv2d(x, w) * scale + bias [+ residual])`` with per-output-channel fp32 ``scale`` /
+    ``bias`` (a frozen BatchNorm), no conv bias, groups = dilation = 1, square 1x1 / 3x3 kernels.
+
+    On a channels_last bf16/fp16 GPU activation with C, K multiples of 64 the whole chain is one
+    native implicit-GEMM launch (the scale / bias / residual / ReLU run on the fp32 accumulator);
+    the backward masks with the saved output and runs the MIOpen data / weight gradients of the
+    scaled gradient.  ``scale`` and ``bias`` receive no gradient (frozen statistics).  Elsewhere
+    (CPU, fp32, odd channel counts) it is the equivalent torch composition."""
+    from .._autocast_utils import _autocast_disabled, _cast_if_autocast_enabled
+
+    padding = (padding, padding) if isinstance(padding, int) else tuple(padding)
+    x, w, residual = _cast_if_autocast_enabled(x, w, residual)
+    with _autocast_disabled():
+        if conv_bn_act_supported(x, w, residual):
+            return _ConvBnActFn.apply(x, w.contiguous(memory_format=torch.channels_last), scale.detach(),
+                                      bias.detach(), residual, relu, stride, padding)
+        return _conv_bn_act_reference(x, w, scale.detach(), bias.detach(), residual, relu, stride, padding)
+
+
 def conv_tap_dgrad(gy, w, x_shape, stride, pad):
     n, c, h, wd = x_shape
     kout, _, k, _ = w.shape

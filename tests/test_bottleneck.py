@@ -51,11 +51,11 @@ def test_explicit_nhwc():
     torch.testing.assert_close(y2, y.permute(0, 2, 3, 1), atol=1e-5, rtol=1e-4)
 
 
-def _spatial_worker(rank, world, use_cudnn):
+def _spatial_worker(rank, world, use_cudnn, halo_ex="sendrecv"):
     torch.manual_seed(0)
     full = Bottleneck(32, 16, 32)
     _randomize_bn(full)
-    sp = SpatialBottleneck(32, 16, 32, use_cudnn=use_cudnn, spatial_group_size=world)
+    sp = SpatialBottleneck(32, 16, 32, use_cudnn=use_cudnn, spatial_group_size=world, halo_ex=halo_ex)
     sp.load_state_dict(full.state_dict())
     x = torch.randn(2, 32, 8, 6, requires_grad=True)
     y = full(x)
@@ -75,5 +75,126 @@ def _spatial_worker(rank, world, use_cudnn):
 
 
 @pytest.mark.parametrize("use_cudnn", [False, True])
-def test_spatial_bottleneck_two_ranks(use_cudnn):
-    run_multiprocess(_spatial_worker, world=2, args=(use_cudnn,))
+@pytest.mark.parametrize("halo_ex", ["sendrecv", "allgather"])
+def test_spatial_bottleneck_two_ranks(use_cudnn, halo_ex):
+    run_multiprocess(_spatial_worker, world=2, args=(use_cudnn, halo_ex))
+
+
+def test_spatial_bottleneck_four_ranks_sendrecv():
+    """Interior ranks exchange with both neighbours."""
+    run_multiprocess(_spatial_worker, world=4, args=(True, "sendrecv"))
+
+
+def _halo_worker(rank, world):
+    from apex.contrib.bottleneck.halo_exchangers import HaloExchangerAllGather, HaloExchangerSendRecv
+    x = torch.arange(2 * 3 * 4 * 5, dtype=torch.float32).view(2, 3, 4, 5) + 1000 * rank
+    outs = []
+    for cls in (HaloExchangerSendRecv, HaloExchangerAllGather):
+        ex = cls(None, rank, world)
+        outs.append(ex.left_right_halo_exchange(x[:, :, :1], x[:, :, -1:]))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    left, right = outs[0]
+    if rank > 0:
+        assert torch.equal(left, x[:, :, -1:] - 1000)  # the rank above's last row
+    else:
+        assert not left.any()
+    if rank + 1 < world:
+        assert torch.equal(right, x[:, :, :1] + 1000)  # the rank below's first row
+    else:
+        assert not right.any()
+
+
+def test_halo_exchangers_agree():
+    run_multiprocess(_halo_worker, world=3)
+
+
+# ---- native conv + frozen-BN scale/bias + residual + ReLU epilogue (csrc/conv/conv_igemm.hip) ----
+def _conv_bn_act_fp32(x, w, s, b, res, relu, stride, padding):
+    y = torch.nn.functional.conv2d(x.float(), w.float(), None, stride, padding)
+    y = y * s.view(1, -1, 1, 1) + b.view(1, -1, 1, 1)
+    if res is not None:
+        y = y + res.float()
+    return torch.relu(y) if relu else y
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,stride,padding", [(1, 1, (0, 0)), (1, 2, (0, 0)), (3, 1, (1, 1)), (3, 2, (1, 1)),
+                                              (3, 1, (0, 1))])
+@pytest.mark.parametrize("res,relu", [(False, True), (True, True), (False, False)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_conv_bn_act_native_gpu(k, stride, padding, res, relu, dt):
+    from apex.ops import conv as C
+    from apex import _native
+    assert _native.available(), "native extension missing on a GPU box"
+    torch.manual_seed(0)
+    n, c, h, wd, kout = 3, 64, 15, 13, 128
+    x = torch.randn(n, c, h, wd, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(kout, c, k, k, device="cuda") / (c * k * k) ** 0.5).to(dt)
+    w = w.contiguous(memory_format=torch.channels_last)
+    s = torch.rand(kout, device="cuda") + 0.5
+    b = torch.randn(kout, device="cuda") * 0.2
+    oh = (h + 2 * padding[0] - k) // stride + 1
+    ow = (wd + 2 * padding[1] - k) // stride + 1
+    r = None
+    if res:
+        r = torch.randn(n, kout, oh, ow, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
+    assert C.conv_bn_act_supported(x, w, r)
+    xa, wa = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    ra = r.clone().requires_grad_(True) if res else None
+    y = C.conv_bn_act(xa, wa, s, b, ra, relu, stride, padding)
+    xr, wr = x.float().requires_grad_(True), w.float().requires_grad_(True)
+    rr = r.float().requires_grad_(True) if res else None
+    yr = _conv_bn_act_fp32(xr, wr, s, b, rr, relu, stride, padding)
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
+    tol = 2e-2 if dt == torch.bfloat16 else 4e-3
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dt))
+    yr.backward(g)
+    # relu masks taken from the rounded output: compare off the decision boundary only
+    torch.testing.assert_close(xa.grad.float(), xr.grad, atol=8 * tol, rtol=8 * tol)
+    torch.testing.assert_close(wa.grad.float(), wr.grad, atol=0.5, rtol=8 * tol)
+    if res:
+        torch.testing.assert_close(ra.grad.float(), rr.grad, atol=tol, rtol=tol)
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stride,cin,nhwc", [(1, 256, False), (2, 256, False), (2, 128, True)])
+def test_bottleneck_native_vs_folded_gpu(stride, cin, nhwc):
+    """bf16 native-epilogue block and bf16 folded-MIOpen block, both against the fp32 block: the
+    fused path must be at least as accurate (ReLU masks near zero flip between any two bf16
+    evaluations, so elementwise bf16-vs-bf16 comparison is not meaningful)."""
+    torch.manual_seed(0)
+    blk32 = Bottleneck(cin, 64, 256, stride=stride, use_cudnn=True, explicit_nhwc=nhwc)
+    _randomize_bn(blk32)
+    blk32 = blk32.cuda()
+    if not nhwc:
+        blk32 = blk32.to(memory_format=torch.channels_last)
+    nat = copy.deepcopy(blk32).to(torch.bfloat16)
+    fold = copy.deepcopy(nat)
+    fold.use_native = False
+    x = torch.randn(4, cin, 14, 14, device="cuda")
+    x = x.permute(0, 2, 3, 1).contiguous() if nhwc else x.contiguous(memory_format=torch.channels_last)
+    from apex.ops import conv as C
+    w1 = nat.conv1.weight.permute(0, 3, 1, 2) if nhwc else nat.conv1.weight
+    xb = x.to(torch.bfloat16)
+    assert C.conv_bn_act_supported(xb.permute(0, 3, 1, 2) if nhwc else xb, w1)
+    x32 = x.clone().requires_grad_(True)
+    xa, xf = xb.clone().requires_grad_(True), xb.clone().requires_grad_(True)
+    y32, ya, yf = blk32(x32), nat(xa), fold(xf)
+    g = torch.randn_like(y32)
+    y32.backward(g)
+    ya.backward(g.to(torch.bfloat16))
+    yf.backward(g.to(torch.bfloat16))
+    ea, ef = _rel(ya, y32), _rel(yf, y32)
+    assert ea < 0.02 and ea <= 1.5 * ef + 1e-3, (ea, ef)
+    ea, ef = _rel(xa.grad, x32.grad), _rel(xf.grad, x32.grad)
+    assert ea < 0.05 and ea <= 1.5 * ef + 1e-3, (ea, ef)
+    for a, f, r in zip(nat.w_conv, fold.w_conv, blk32.w_conv):
+        ea, ef = _rel(a.grad, r.grad), _rel(f.grad, r.grad)
+        assert ea < 0.05 and ea <= 1.5 * ef + 1e-3, (ea, ef)

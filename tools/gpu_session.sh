@@ -7,7 +7,7 @@
 #   syncbn2    2 ranks sharing the GPU, gloo, --sync-bn (fused bn_group=world over peer memory)
 #   prof       rocprofv3 --kernel-trace --stats of a short bench (after the APEX_BENCH_MARK spin)
 #   pyprof     rocprofv3 marker + kernel trace of examples/pyprof/lenet.py through apex.pyprof parse/prof
-#   script     python $SCRIPT (a tools/ micro-benchmark), output to gpurun_out/script.log
+#   script     python $SCRIPT (comma-separated tools/ micro-benchmarks), output to gpurun_out/script_<i>.log
 # Test failures (rc 1) do not stop the chain; anything >= 2 does.
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -51,8 +51,12 @@ for s in ${STEPS:-tests smoke bench}; do
       python -m apex.pyprof.prof --summary op gpurun_out/pyprof_parsed.txt > gpurun_out/pyprof_summary.txt
     rc=$?; head -20 gpurun_out/pyprof_summary.txt; rm -rf gpurun_out/pyprof_trace; [ $rc -ne 0 ] && stop pyprof_post $rc ;;
   script)
-    timeout -k 10 ${SCRIPT_TIMEOUT:-400} python $SCRIPT > gpurun_out/script.log 2>&1
-    rc=$?; tail -20 gpurun_out/script.log; [ $rc -ne 0 ] && stop script $rc ;;
+    # SCRIPT: one or more comma-separated "tool.py args" entries, logs script_<i>.log
+    IFS=',' read -ra scripts <<< "$SCRIPT"; i=0
+    for sc in "${scripts[@]}"; do
+      timeout -k 10 ${SCRIPT_TIMEOUT:-400} python $sc > gpurun_out/script_$i.log 2>&1
+      rc=$?; tail -20 gpurun_out/script_$i.log; [ $rc -ne 0 ] && stop "script $sc" $rc; i=$((i+1))
+    done ;;
   esac
 done
 du -sh gpurun_out/miopen_udb gpurun_out/miopen_cache 2>/dev/null
