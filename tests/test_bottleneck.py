@@ -184,7 +184,8 @@ def test_bottleneck_native_vs_folded_gpu(stride, cin, nhwc):
     w1 = nat.conv1.weight.permute(0, 3, 1, 2) if nhwc else nat.conv1.weight
     xb = x.to(torch.bfloat16)
     assert C.conv_bn_act_supported(xb.permute(0, 3, 1, 2) if nhwc else xb, w1)
-    x32 = x.clone().requires_grad_(True)
+    # the fp32 block sees the same bf16-rounded input (input rounding is not under test)
+    x32 = xb.float().requires_grad_(True)
     xa, xf = xb.clone().requires_grad_(True), xb.clone().requires_grad_(True)
     y32, ya, yf = blk32(x32), nat(xa), fold(xf)
     g = torch.randn_like(y32)
@@ -193,8 +194,10 @@ def test_bottleneck_native_vs_folded_gpu(stride, cin, nhwc):
     yf.backward(g.to(torch.bfloat16))
     ea, ef = _rel(ya, y32), _rel(yf, y32)
     assert ea < 0.02 and ea <= 1.5 * ef + 1e-3, (ea, ef)
+    # dgrad passes through two ReLU masks computed from bf16 activations: the folded-MIOpen
+    # block itself measures 0.04-0.07 here, so the absolute bound is looser than the forward's
     ea, ef = _rel(xa.grad, x32.grad), _rel(xf.grad, x32.grad)
-    assert ea < 0.05 and ea <= 1.5 * ef + 1e-3, (ea, ef)
+    assert ea < 0.08 and ea <= 1.5 * ef + 1e-3, (ea, ef)
     for a, f, r in zip(nat.w_conv, fold.w_conv, blk32.w_conv):
         ea, ef = _rel(a.grad, r.grad), _rel(f.grad, r.grad)
         assert ea < 0.05 and ea <= 1.5 * ef + 1e-3, (ea, ef)
