@@ -194,10 +194,11 @@ def test_bottleneck_native_vs_folded_gpu(stride, cin, nhwc):
     yf.backward(g.to(torch.bfloat16))
     ea, ef = _rel(ya, y32), _rel(yf, y32)
     assert ea < 0.02 and ea <= 1.5 * ef + 1e-3, (ea, ef)
-    # dgrad passes through two ReLU masks computed from bf16 activations: the folded-MIOpen
-    # block itself measures 0.04-0.07 here, so the absolute bound is looser than the forward's
+    # gradients pass through ReLU masks computed from bf16 activations and bf16-rounded weights:
+    # the folded-MIOpen block itself measures 0.04-0.08 against fp32 here, so the absolute
+    # bounds are loose and the binding check is "no worse than the folded path"
     ea, ef = _rel(xa.grad, x32.grad), _rel(xf.grad, x32.grad)
-    assert ea < 0.08 and ea <= 1.5 * ef + 1e-3, (ea, ef)
+    assert ea < 0.15 and ea <= 1.5 * ef + 1e-3, (ea, ef)
     for a, f, r in zip(nat.w_conv, fold.w_conv, blk32.w_conv):
         ea, ef = _rel(a.grad, r.grad), _rel(f.grad, r.grad)
-        assert ea < 0.05 and ea <= 1.5 * ef + 1e-3, (ea, ef)
+        assert ea < 0.15 and ea <= 1.5 * ef + 1e-3, (ea, ef)
