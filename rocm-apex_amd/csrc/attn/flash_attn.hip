@@ -618,13 +618,13 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
 
 // dK, dV: one workgroup = 4 waves = 128 keys (K, V of the wave's 32 keys in registers); 32-query
 // slices of Q / dO (+ lse, delta) double-buffered in LDS, one barrier per slice.
-template <typename T, int D, bool PLAIN>
+template <typename T, int D, bool PLAIN, int QS>
 __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const AttnBwdArgs ba) {
   int bx, by, bz;
   xcd_remap(bx, by, bz);
   const AttnArgs& a = ba.f;
   using G = Geo<D>;
-  constexpr int BK = 128, QB = 32, NKK = G::NKK, NDT = G::NDT;
+  constexpr int BK = 128, QB = QS, NKK = G::NKK, NDT = G::NDT;  // QB queries per LDS slice
   constexpr int QSTR = G::KSTR;  // row reads (S, dP) and transposed reads (dK, dV)
   constexpr int CPR = D / 8;
   constexpr int SLICE = 2 * QB * QSTR + 4 * QB;  // Q, dO images + lse, delta (fp32) in 16-bit units
@@ -724,10 +724,15 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
       for (int q0 = q_begin; q0 < sq.lq; q0 += QB, buf ^= 1) {
         const bool more = q0 + QB < sq.lq;
         if (more) fetch(q0 + QB);
-        const uint16_t* Qb = Ql(buf);
-        const uint16_t* Gb = dOl(buf);
-        const float* lb = lse_l(buf);
-        const float* db = del_l(buf);
+        // 32-query sub-slices of the LDS slice (QB = 64 halves the barriers / commits per query)
+        #pragma unroll
+        for (int sub = 0; sub < QB / 32; ++sub) {
+        const int q0s = q0 + 32 * sub;
+        if (q0s >= sq.lq) break;  // uniform over the workgroup
+        const uint16_t* Qb = Ql(buf) + 32 * sub * QSTR;
+        const uint16_t* Gb = dOl(buf) + 32 * sub * QSTR;
+        const float* lb = lse_l(buf) + 32 * sub;
+        const float* db = del_l(buf) + 32 * sub;
         f32x16 sacc = zero16(), dpacc = zero16();
         #pragma unroll
         for (int kk = 0; kk < NKK; ++kk) {
@@ -735,14 +740,14 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
           dpacc = mma<T>(frag_rows<QSTR>(Gb, 0, kk, lane), vf[kk], dpacc);
         }
         float p[16], ds[16];
-        const bool edge = !kvalid || q0 + QB > sq.lq || (a.causal && q0 < k_start + wave * 32 + 32) ||
+        const bool edge = !kvalid || q0s + 32 > sq.lq || (a.causal && q0s < k_start + wave * 32 + 32) ||
                           biash != nullptr;
         #pragma unroll
         for (int r = 0; r < 16; ++r) p[r] = sacc[r] * c - lb[crow(r, h2)];
         if (edge) {  // wave-uniform: interior slices run the element loop branch-free
           #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int q = q0 + crow(r, h2);
+            const int q = q0s + crow(r, h2);
             const bool ok = kvalid && q < sq.lq && (!a.causal || mykey <= q);
             float xv = p[r];
             if (biash != nullptr && ok) xv += biash[(int64_t)q * a.bias_sq + (int64_t)mykey * a.bias_sk] * kLog2e;
@@ -751,7 +756,7 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
         }
         #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int qr = crow(r, h2), q = q0 + qr;
+          const int qr = crow(r, h2), q = q0s + qr;
           const float pv = fast_exp2(p[r]);
           float dpv = dpacc[r];
           float pd = pv;
@@ -773,6 +778,7 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
             dv[dt] = mma<T>(frag_tr<QSTR>(Gb, 32 * dt, klo, klo + 8, lane), pf, dv[dt]);
             dk[dt] = mma<T>(frag_tr<QSTR>(Qb, 32 * dt, klo, klo + 8, lane), dsf, dk[dt]);
           }
+        }
         }
         if (more) commit(buf ^ 1);
         __syncthreads();
@@ -1028,9 +1034,20 @@ void launch_fwd(const AttnArgs& a, hipStream_t s) {
   else launch_fwd_qf<T, D, 1, false>(a, s);
 }
 
-template <int D>
+template <int D, int QS>
 constexpr size_t dkdv_lds() {
-  return (size_t)2 * (2 * 32 * Geo<D>::KSTR + 4 * 32) * 2;
+  return (size_t)2 * (2 * QS * Geo<D>::KSTR + 4 * QS) * 2;
+}
+
+// dK/dV LDS slice depth in queries (APEX_ATTN_DKDV_QS=32|64 overrides, A/B).  Measured on MI355X
+// (profiles/attn_dkdv_qs_r02.jsonl): at head dim 128 (one wave per SIMD) 64-query slices halve
+// the per-slice commit + barrier stalls, bwd 1.94 -> 1.39 ms (b8 s2048 h16), 1.17-1.23x causal; at
+// head dim <= 64 (two waves per SIMD hide them already) 32 stays 1-5 % faster
+template <int D>
+inline int dkdv_qs() {
+  const char* e = std::getenv("APEX_ATTN_DKDV_QS");
+  if (e != nullptr) return e[0] == '3' ? 32 : 64;
+  return D == 128 ? 64 : 32;
 }
 template <int D>
 constexpr size_t dq_lds() {
@@ -1044,8 +1061,9 @@ void launch_bwd_v(const AttnBwdArgs& ba, hipStream_t s) {
   hipLaunchKernelGGL((bwd_delta_kernel<T, D>), dim3((a.sq + RPB - 1) / RPB, a.h, a.b), dim3(256), 0, s, ba);
   if (ba.dq_acc == nullptr) {  // split, atomic-free path
     const int nkb = (a.sk + 127) / 128, nqb = (a.sq + 127) / 128;
-    hipLaunchKernelGGL((bwd_dkdv_kernel<T, D, PLAIN>), dim3(a.causal ? (nkb + 1) / 2 : nkb, a.h_k, a.b), dim3(256),
-                       dkdv_lds<D>(), s, ba);
+    const dim3 grid(a.causal ? (nkb + 1) / 2 : nkb, a.h_k, a.b);
+    if (dkdv_qs<D>() == 64) hipLaunchKernelGGL((bwd_dkdv_kernel<T, D, PLAIN, 64>), grid, dim3(256), (dkdv_lds<D, 64>()), s, ba);
+    else hipLaunchKernelGGL((bwd_dkdv_kernel<T, D, PLAIN, 32>), grid, dim3(256), (dkdv_lds<D, 32>()), s, ba);
     hipLaunchKernelGGL((bwd_dq_kernel<T, D, PLAIN>), dim3(nqb, a.h, a.b), dim3(256), dq_lds<D>(), s, ba);
     return;
   }

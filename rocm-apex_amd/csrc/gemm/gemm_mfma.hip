@@ -123,15 +123,17 @@ __device__ __forceinline__ f32x16 mfma<f16_t>(s16x8 a, s16x8 b, f32x16 c) {
                                                 0);
 }
 
-__device__ __forceinline__ float gelu_tanh(float x) {
+// tanh-GeLU as x * sigmoid(2u), u = k0 (x + k1 x^3): one v_exp_f32 + one v_rcp_f32 instead of a
+// libm tanhf in the epilogue
+__device__ __forceinline__ float gelu_sig(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+  return __builtin_amdgcn_rcpf(1.f + __expf(-2.f * k0 * (x + k1 * x * x * x)));
 }
+__device__ __forceinline__ float gelu_tanh(float x) { return x * gelu_sig(x); }
 __device__ __forceinline__ float dgelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float u = k0 * (x + k1 * x * x * x);
-  const float t = tanhf(u);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
+  const float s = gelu_sig(x);  // (1 + tanh u) / 2;  1 - tanh^2 u = 4 s (1 - s)
+  return s + 2.f * x * s * (1.f - s) * k0 * (1.f + 3.f * k1 * x * x);
 }
 
 // XCD-aware, bijective remap of the linear workgroup id, then GROUP_M-grouped tile order
@@ -643,6 +645,297 @@ inline bool usable(const GemmArgs& g, int cus) {
 
 }  // namespace g256
 
+// =============================================================================================
+// g8p: 256 x 256 x 64 tile for two k-major operands, phase-pipelined ("ping-pong") main loop.
+//
+// 8 waves as 2 (M) x 4 (N), each a 128 x 64 block of 16x16 accumulators (v_mfma_f32_16x16x32).
+// A K-tile is computed in 4 phases, one 64 x 32 output quadrant each (16 MFMAs):
+//   phase 0: (rows 0-63,  cols 0-31)  reads A rows 0-63 (8 x ds_read_b128) + B cols 0-31 (4)
+//   phase 1: (rows 0-63,  cols 32-63) reads B cols 32-63 (4)
+//   phase 2: (rows 64-127, cols 32-63) reads A rows 64-127 (8)
+//   phase 3: (rows 64-127, cols 0-31)  no reads (operands still in registers)
+// so the tile is staged as four 16-KB "half-tiles" in the order the phases consume them:
+//   h0 = A rows {0-63, 128-191}, h1 = B cols {0-31} of every wave column, h2 = B cols {32-63},
+//   h3 = A rows {64-127, 192-255}
+// and every phase issues ONE half-tile of LDS-DMA (2 global_load_lds_dwordx4 per lane) six
+// half-tiles ahead, into a 2 x 4 ring (128 KB).  Each phase then waits with a counted
+// vmcnt(8) — 4 half-tiles stay in flight across every barrier — and the data it retired is
+// read one phase later at the earliest; a slot is refilled >= 2 phases after its last read.
+// Measured (profiles/gemm8p_r02.jsonl): 1180 TF at 8192^3 vs 1085 for g256; moving the DMA
+// issue into the MFMA block (1098 TF) or the next phase's ds_reads into it (984 TF) lost.
+// The two wave rows run one barrier apart (group 1 takes an extra barrier up front): while
+// one group's MFMAs run between its two barriers, the other group issues its ds_reads and
+// DMA, so each SIMD (one wave of each group) alternates MFMA and load work.
+// =============================================================================================
+namespace g8p {
+
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int HT = 128 * BK;  // elements per half-tile image (16 KB)
+constexpr int CST = BN + 4;
+constexpr size_t LDS_BYTES = (size_t)128 * CST * 4 > (size_t)8 * HT * 2 ? (size_t)128 * CST * 4 : (size_t)8 * HT * 2;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T>
+__device__ __forceinline__ f32x4 mfma16(s16x8 a, s16x8 b, f32x4 c);
+template <>
+__device__ __forceinline__ f32x4 mfma16<bf16_t>(s16x8 a, s16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                 0, 0);
+}
+template <>
+__device__ __forceinline__ f32x4 mfma16<f16_t>(s16x8 a, s16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                0);
+}
+
+__device__ __forceinline__ void barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// wait until at most n (wave-uniform, even, 0..8) of this wave's DMAs are outstanding
+__device__ __forceinline__ void wait_vm(int n) {
+  if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (n == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (n == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Issue this lane's 2 DMA pieces of half-tile h (0..3) of the K-tile at k0 into dst.
+// Image: [128 rows][64 k], 128-B rows, 16-B chunk c of row r stored at c ^ ((r >> 1) & 7).
+__device__ __forceinline__ void issue_half(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, int64_t lda,
+                                           int64_t ldb, int M, int N, int row0, int col0, int k0, int h,
+                                           uint16_t* dst, int wave, int lane) {
+  const bool isA = (h == 0 || h == 3);
+  const int s = (h == 0 || h == 1) ? 0 : 1;  // first / second half of the rows (A) or columns (B)
+  const uint16_t* X = isA ? A : B;
+  const int64_t ld = isA ? lda : ldb;
+  const int lim = isA ? M : N;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int j = i * 8 + wave;
+    const int r = 8 * j + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int t = isA ? (r & 63) + (r >> 6) * 128 + s * 64 : (r >> 5) * 64 + (r & 31) + s * 32;
+    int gr = (isA ? row0 : col0) + t;
+    gr = gr < lim ? gr : lim - 1;  // rows past the edge are computed but never stored
+    g256::dma16(X + (int64_t)gr * ld + k0 + 8 * c, dst + j * 512);
+  }
+}
+
+// fragment (16 rows x 32 k) at image row rb, k-step kk of a swizzled half-tile image:
+// lane l gets row rb + (l & 15), k = 32 kk + 8 (l >> 4) + e
+__device__ __forceinline__ s16x8 frag16(const uint16_t* img, int rb, int kk, int lane) {
+  const int r = rb + (lane & 15);
+  const int c = (4 * kk + (lane >> 4)) ^ ((r >> 1) & 7);
+  return *reinterpret_cast<const s16x8*>(img + r * BK + 8 * c);
+}
+
+template <typename T, int EPI>
+__global__ void __launch_bounds__(512, 1)
+gemm8p_nt(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, T* __restrict__ C, int64_t lda, int64_t ldb,
+          int64_t ldc, int M, int N, int K, const T* __restrict__ bias, const T* __restrict__ aux_in,
+          T* __restrict__ aux_out, float* __restrict__ part, int kchunk) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  int bm, bn;
+  tile_coords(tiles_m * tiles_n, tiles_m, tiles_n, bm, bn);
+  const int row0 = bm * BM, col0 = bn * BN;
+  const int kbeg = (int)blockIdx.y * kchunk;
+  const int nk = (min(K, kbeg + kchunk) - kbeg) / BK;
+  const int nloads = 4 * nk;  // half-tile loads of this workgroup
+  auto slot = [&](int load) { return lds + ((load >> 2) & 1) * 4 * HT + (load & 3) * HT; };
+  auto issue = [&](int load) {
+    issue_half(A, B, lda, ldb, M, N, row0, col0, kbeg + (load >> 2) * BK, load & 3, slot(load), wave, lane);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: loads 0..5 (K-tile 0 and the first two half-tiles of K-tile 1); retire 0 and 1
+  const int pre = nloads < 6 ? nloads : 6;
+  for (int l = 0; l < pre; ++l) issue(l);
+  wait_vm(2 * (pre - 2));
+  barrier();
+  if (wr == 1) barrier();  // stagger the second wave row by one barrier
+
+  s16x8 af[4][2], bf0[2][2], bf1[2][2];
+  for (int kt = 0; kt < nk; ++kt) {
+    const uint16_t* tA0 = slot(4 * kt + 0);
+    const uint16_t* tB0 = slot(4 * kt + 1);
+    const uint16_t* tB1 = slot(4 * kt + 2);
+    const uint16_t* tA1 = slot(4 * kt + 3);
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      const int p = 4 * kt + ph;
+      // 1. this phase's operand fragments (they land while the other wave row runs its MFMAs)
+      if (ph == 0) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) bf0[j][kk] = frag16(tB0, wc * 32 + 16 * j, kk, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) af[i][kk] = frag16(tA0, wr * 64 + 16 * i, kk, lane);
+      } else if (ph == 1) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) bf1[j][kk] = frag16(tB1, wc * 32 + 16 * j, kk, lane);
+      } else if (ph == 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) af[i][kk] = frag16(tA1, wr * 64 + 16 * i, kk, lane);
+      }
+      // 2. one half-tile of DMA six loads ahead; retire the load issued four phases ago
+      const int l = p + 6;
+      if (l < nloads) issue(l);
+      const int last = (l < nloads ? l : nloads - 1);
+      const int fly = last - (p + 2);
+      wait_vm(fly > 0 ? 2 * fly : 0);
+      barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // 3. 16 MFMAs of this phase's 64 x 32 quadrant
+      __builtin_amdgcn_s_setprio(1);
+      const int qm = (ph >= 2) ? 1 : 0;
+      const int qn = (ph == 1 || ph == 2) ? 1 : 0;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const s16x8 b = qn ? bf1[j][kk] : bf0[j][kk];
+            acc[4 * qm + i][2 * qn + j] = mfma16<T>(af[i][kk], b, acc[4 * qm + i][2 * qn + j]);
+          }
+      __builtin_amdgcn_s_setprio(0);
+      barrier();
+    }
+  }
+  if (wr == 0) barrier();  // re-align the two wave rows
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue: two 128-row halves staged as fp32 through LDS, 16-byte row stores ----
+  float* cs = reinterpret_cast<float*>(lds);
+  const int ch = tid & 31, rsub = tid >> 5;  // 16 rows per pass
+  const int gc = col0 + ch * 8;
+  float bv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bv[e] = 0.f;
+  if (bias != nullptr && gc < N) Vec8<T>::load(bv, bias + gc);
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    if (wr == half) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            cs[(16 * i + 4 * (lane >> 4) + r) * CST + wc * 64 + 16 * j + (lane & 15)] = acc[i][j][r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int rl = rsub + 16 * it;
+      const int gr = row0 + half * 128 + rl;
+      if (gr < M && gc < N) {
+        float v[8];
+        const float4 lo = *reinterpret_cast<const float4*>(cs + rl * CST + ch * 8);
+        const float4 hi = *reinterpret_cast<const float4*>(cs + rl * CST + ch * 8 + 4);
+        v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+        v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+        const int64_t off = (int64_t)gr * ldc + gc;
+        if (EPI == kEpiNone && part != nullptr) {
+          float* dst = part + ((int64_t)blockIdx.y * M + gr) * N + gc;
+          *reinterpret_cast<float4*>(dst) = lo;
+          *reinterpret_cast<float4*>(dst + 4) = hi;
+          continue;
+        }
+        if constexpr (EPI == kEpiNone) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += bv[e];
+        } else if constexpr (EPI == kEpiGelu) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += bv[e];
+          if (aux_out != nullptr) Vec8<T>::store(aux_out + off, v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
+        } else if constexpr (EPI == kEpiRelu) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] + bv[e], 0.f);
+        } else if constexpr (EPI == kEpiSigmoid) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = 1.f / (1.f + __expf(-(v[e] + bv[e])));
+        } else {
+          float a[8];
+          Vec8<T>::load(a, aux_in + off);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            if constexpr (EPI == kEpiDGelu) v[e] *= dgelu_tanh(a[e]);
+            else if constexpr (EPI == kEpiDRelu) v[e] = a[e] > 0.f ? v[e] : 0.f;
+            else v[e] *= a[e] * (1.f - a[e]);
+          }
+        }
+        Vec8<T>::store(C + off, v);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// APEX_AMD_GEMM8P=0 routes k-major x k-major GEMMs back to the g256 kernel (A/B timing)
+inline bool enabled() {
+  const char* e = std::getenv("APEX_AMD_GEMM8P");
+  return e == nullptr || e[0] != '0';
+}
+
+template <typename T>
+void launch(const GemmArgs& g, hipStream_t s, int cus) {
+  const int tiles = ((g.m + BM - 1) / BM) * ((g.n + BN - 1) / BN);
+  int kchunk = g.k;
+  const int sp = g.splitk_ws != nullptr ? g256::splitk_parts(g, cus, &kchunk) : 1;
+  if (sp > 1) {
+    hipLaunchKernelGGL((gemm8p_nt<T, kEpiNone>), dim3(tiles, sp), dim3(512), LDS_BYTES, s, (const uint16_t*)g.a,
+                       (const uint16_t*)g.b, (T*)g.c, g.lda, g.ldb, g.ldc, g.m, g.n, g.k, (const T*)nullptr,
+                       (const T*)nullptr, (T*)nullptr, g.splitk_ws, kchunk);
+    const int64_t nvec = (int64_t)g.m * g.n / 8;
+    int64_t grid = (nvec + 255) / 256;
+    if (grid > (int64_t)cus * 8) grid = (int64_t)cus * 8;
+    hipLaunchKernelGGL((g256::splitk_reduce<T>), dim3((unsigned)grid), dim3(256), 0, s, (const float*)g.splitk_ws, sp,
+                       g.m, g.n, (const T*)g.bias, (T*)g.c, g.ldc);
+    return;
+  }
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(tiles), dim3(512), LDS_BYTES, s, (const uint16_t*)g.a, (const uint16_t*)g.b,
+                       (T*)g.c, g.lda, g.ldb, g.ldc, g.m, g.n, g.k, (const T*)g.bias, (const T*)g.aux_in,
+                       (T*)g.aux_out, (float*)nullptr, g.k);
+  };
+  switch (g.epilogue) {
+    case kEpiNone: go(gemm8p_nt<T, kEpiNone>); break;
+    case kEpiGelu: go(gemm8p_nt<T, kEpiGelu>); break;
+    case kEpiRelu: go(gemm8p_nt<T, kEpiRelu>); break;
+    case kEpiSigmoid: go(gemm8p_nt<T, kEpiSigmoid>); break;
+    case kEpiDGelu: go(gemm8p_nt<T, kEpiDGelu>); break;
+    case kEpiDRelu: go(gemm8p_nt<T, kEpiDRelu>); break;
+    case kEpiDSigmoid: go(gemm8p_nt<T, kEpiDSigmoid>); break;
+    default: throw std::runtime_error("gemm8p: unknown epilogue");
+  }
+}
+
+}  // namespace g8p
+
 }  // namespace gemm
 
 bool gemm_supported(const GemmArgs& g) {
@@ -665,7 +958,8 @@ void gemm_mfma(const GemmArgs& g, int cus, hipStream_t s) {
   dispatch_16(g.dtype, [&](auto tag) {
     using T = typename decltype(tag)::type;
     if (gemm::g256::usable(g, cus)) {
-      if (g.a_kmajor && g.b_kmajor) gemm::g256::launch<T, true, true>(g, s, cus);
+      if (g.a_kmajor && g.b_kmajor && gemm::g8p::enabled()) gemm::g8p::launch<T>(g, s, cus);
+      else if (g.a_kmajor && g.b_kmajor) gemm::g256::launch<T, true, true>(g, s, cus);
       else if (g.a_kmajor) gemm::g256::launch<T, true, false>(g, s, cus);
       else if (g.b_kmajor) gemm::g256::launch<T, false, true>(g, s, cus);
       else gemm::g256::launch<T, false, false>(g, s, cus);

@@ -175,6 +175,29 @@ def test_gpu_flash_fwd_bwd(d, dtype, causal):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("qs", ["32", "64"])
+@pytest.mark.parametrize("d", [64, 128])
+@pytest.mark.parametrize("causal,sq,sk", [(False, 200, 333), (True, 200, 200), (False, 40, 97), (True, 40, 40)])
+def test_gpu_flash_bwd_dkdv_slices(qs, d, causal, sq, sk, monkeypatch):
+    """dK/dV kernel with 32- and 64-query LDS slices forced (default: 64 at head dim 128, 32
+    below): ragged query counts end a 64-slice after its first 32-query half."""
+    monkeypatch.setenv("APEX_ATTN_DKDV_QS", qs)
+    torch.manual_seed(d + sq)
+    b, h, dtype = 2, 3, torch.bfloat16
+    q = torch.randn(b, sq, h, d, device="cuda", dtype=dtype, requires_grad=True)
+    k = torch.randn(b, sk, h, d, device="cuda", dtype=dtype, requires_grad=True)
+    v = torch.randn(b, sk, h, d, device="cuda", dtype=dtype, requires_grad=True)
+    out = flash_attn_func(q, k, v, causal=causal)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    ref = naive(qr, kr, vr, d ** -0.5, causal)
+    g = torch.randn_like(ref)
+    out.backward(g.to(dtype))
+    ref.backward(g)
+    for a, r in ((q.grad, qr.grad), (k.grad, kr.grad), (v.grad, vr.grad)):
+        _close(a, r, 2e-2)
+
+
+@pytest.mark.gpu
 def test_gpu_flash_bias_gqa_dropout_varlen():
     torch.manual_seed(5)
     dtype = torch.bfloat16

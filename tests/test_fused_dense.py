@@ -252,3 +252,59 @@ def test_gpu_gemm_splitk(m, n, k, a_kmajor, b_kmajor, splitk, monkeypatch):
     ref = _ref_mm(a, a_kmajor, b, b_kmajor, m, n, k)
     scale = k ** 0.5
     torch.testing.assert_close(c.float() / scale, ref / scale, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,n,k", [(256, 256, 64), (300, 520, 128), (512, 768, 192), (77, 4104, 320),
+                                   (2048, 2304, 1024)])
+@pytest.mark.parametrize("g8p", ["1", "0"])
+def test_gpu_gemm8p_nt(m, n, k, g8p, monkeypatch):
+    """Phase-pipelined 256x256 kernel for two k-major operands (APEX_AMD_GEMM8P=1, default) and
+    the g256 kernel it replaces, forced on every shape: K = 1..16 tiles (prologue/tail counted
+    waits), ragged M / N, every epilogue incl. the activation-gradient ones reading aux."""
+    import apex
+
+    monkeypatch.setenv("APEX_AMD_GEMM256", "force")
+    monkeypatch.setenv("APEX_AMD_GEMM8P", g8p)
+    g = apex._native.require("gemm").gemm
+    torch.manual_seed(m + n + k)
+    x = (torch.randn(m, k, device="cuda") * 0.5).to(torch.bfloat16)
+    w = (torch.randn(n, k, device="cuda") * 0.2).to(torch.bfloat16)
+    b = torch.randn(n, device="cuda").to(torch.bfloat16)
+    z = x.float() @ w.float().t() + b.float()
+    tol = dict(atol=3e-2, rtol=3e-2)
+    y, _ = g.linear(x, w, b, g.EPI_NONE, False)
+    torch.testing.assert_close(y.float(), z, **tol)
+    y, aux = g.linear(x, w, b, g.EPI_GELU, True)
+    torch.testing.assert_close(aux.float(), z, **tol)
+    torch.testing.assert_close(y.float(), torch.nn.functional.gelu(z, approximate="tanh"), **tol)
+    y, _ = g.linear(x, w, b, g.EPI_RELU, False)
+    torch.testing.assert_close(y.float(), torch.relu(z), **tol)
+    c, _ = g.matmul(x.reshape(-1), True, w.reshape(-1), True, m, n, k)
+    mm = x.float() @ w.float().t()
+    torch.testing.assert_close(c.float(), mm, **tol)
+    pre = torch.randn(m, n, device="cuda").to(torch.bfloat16)
+    c, _ = g.matmul(x.reshape(-1), True, w.reshape(-1), True, m, n, k, g.EPI_DRELU, None, pre, False)
+    torch.testing.assert_close(c.float(), mm * (pre.float() > 0), **tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,n,k", [(4096, 4096, 2048), (2304, 3072, 4096)])
+def test_gpu_gemm8p_race_screen(m, n, k, monkeypatch):
+    """The phase pipeline reads LDS-DMA data by counted vmcnt + barrier placement only: repeat
+    the launch and require bit-identical results (a mis-placed read shows as a varying tile)
+    that also match fp32 math."""
+    import apex
+
+    monkeypatch.setenv("APEX_AMD_GEMM8P", "1")
+    g = apex._native.require("gemm").gemm
+    torch.manual_seed(7)
+    a = (torch.rand(m * k, device="cuda") * 2 - 1).to(torch.bfloat16)
+    b = (torch.rand(n * k, device="cuda") * 2 - 1).to(torch.bfloat16)
+    first, _ = g.matmul(a, True, b, True, m, n, k)
+    ref = a.float().view(m, k) @ b.float().view(n, k).t()
+    scale = k ** 0.5
+    torch.testing.assert_close(first.float() / scale, ref / scale, atol=2e-2, rtol=2e-2)
+    for _ in range(30):
+        c, _ = g.matmul(a, True, b, True, m, n, k)
+        assert torch.equal(c, first)

@@ -4,7 +4,8 @@
 Each pass directory holds a ``*counter_collection.csv`` (one row per dispatch x counter) and the
 kernel-trace pass a ``*kernel_trace.csv``.  Per kernel (name truncated) we report mean duration
 and the mean of every counter, plus derived metrics:
-  MFMA % peak = SQ_INSTS_MFMA x 32768 FLOP (every MFMA here is v_mfma_f32_32x32x16 bf16/f16)
+  MFMA % peak = SQ_INSTS_MFMA x FLOP per MFMA (32768 for v_mfma_f32_32x32x16, 16384 for the
+  v_mfma_f32_16x16x32 of the g8p GEMM kernels)
                 / duration / 2.5 PFLOP/s dense bf16 peak
   LDS conf   = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (extra LDS cycles per LDS-array cycle)
   HBM GB/s   = (FETCH_SIZE + WRITE_SIZE) KiB / duration  (FETCH_SIZE under-counts wide streams on
@@ -55,7 +56,8 @@ def main():
         c = {n: sum(v) / len(v) for n, v in counters[k].items()}
         dur = sorted(durations.get(k, [0.0]))[len(durations.get(k, [0.0])) // 2]
         nm = c.get("SQ_INSTS_MFMA")
-        util = 100.0 * nm * 32768 / (dur * 1e-6) / 2.5e15 if nm and dur else (0.0 if nm == 0 else None)
+        flop = 16384 if "g8p::" in k else 32768
+        util = 100.0 * nm * flop / (dur * 1e-6) / 2.5e15 if nm and dur else (0.0 if nm == 0 else None)
         lds = c.get("SQ_LDS_BANK_CONFLICT"), c.get("SQ_LDS_IDX_ACTIVE")
         conf = 100.0 * lds[0] / lds[1] if lds[0] is not None and lds[1] else None
         fetch, write = c.get("FETCH_SIZE"), c.get("WRITE_SIZE")
