@@ -627,12 +627,14 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
   constexpr int BK = 128, QB = QS, NKK = G::NKK, NDT = G::NDT;  // QB queries per LDS slice
   constexpr int QSTR = G::KSTR;  // row reads (S, dP) and transposed reads (dK, dV)
   constexpr int CPR = D / 8;
-  constexpr int SLICE = 2 * QB * QSTR + 4 * QB;  // Q, dO images + lse, delta (fp32) in 16-bit units
+  // Q, dO images + lse, delta (fp32) + per-row dropout hash prefix (u32), in 16-bit units
+  constexpr int SLICE = 2 * QB * QSTR + 6 * QB;
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   auto Ql = [&](int i) { return lds + i * SLICE; };
   auto dOl = [&](int i) { return lds + i * SLICE + QB * QSTR; };
   auto lse_l = [&](int i) { return reinterpret_cast<float*>(lds + i * SLICE + 2 * QB * QSTR); };
   auto del_l = [&](int i) { return lse_l(i) + QB; };
+  auto hq_l = [&](int i) { return reinterpret_cast<uint32_t*>(del_l(i) + QB); };
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h2 = lane >> 5, ql = lane & 31;
   const int hk = by, b = bz;
@@ -684,6 +686,8 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
       const int q_begin = a.causal ? (k_start / QB) * QB : 0;
       uint4 pq[QCPT], pg[QCPT];
       float plse = INFINITY, pdel = 0.f;
+      uint32_t phq = 0;
+      const uint32_t hbh = mix32(smix ^ (bh * 0x9E3779B9u));
       auto fetch = [&](int q0n) {
         #pragma unroll
         for (int i = 0; i < QCPT; ++i) {
@@ -699,6 +703,8 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
           const int q = q0n + tid;
           plse = q < sq.lq ? lse_h[q] : INFINITY;
           pdel = q < sq.lq ? del_h[q] : 0.f;
+          // the (bh, q) part of drop_hash, once per row instead of once per element
+          if (dropout) phq = mix32(hbh ^ ((uint32_t)q * 0x85EBCA6Bu));
         }
       };
       auto commit = [&](int buf) {
@@ -714,6 +720,7 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
         if (tid < QB) {
           lse_l(buf)[tid] = plse * kLog2e;
           del_l(buf)[tid] = pdel;
+          if (dropout) hq_l(buf)[tid] = phq;
         }
       };
       // the previous head's last slice ended with a barrier: both buffers are free
@@ -733,6 +740,7 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
         const uint16_t* Gb = dOl(buf) + 32 * sub * QSTR;
         const float* lb = lse_l(buf) + 32 * sub;
         const float* db = del_l(buf) + 32 * sub;
+        const uint32_t* hb = hq_l(buf) + 32 * sub;
         f32x16 sacc = zero16(), dpacc = zero16();
         #pragma unroll
         for (int kk = 0; kk < NKK; ++kk) {
@@ -761,7 +769,8 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
           float dpv = dpacc[r];
           float pd = pv;
           if (dropout) {
-            const float mk = drop_hash(smix, bh, (uint32_t)q, (uint32_t)mykey) >= thresh ? inv_keep : 0.f;
+            // == drop_hash(smix, bh, q, mykey), the (bh, q) prefix read from LDS
+            const float mk = mix32(hb[qr] ^ ((uint32_t)mykey * 0xC2B2AE35u)) >= thresh ? inv_keep : 0.f;
             pd = pv * mk;
             dpv *= mk;
           }
@@ -1036,7 +1045,7 @@ void launch_fwd(const AttnArgs& a, hipStream_t s) {
 
 template <int D, int QS>
 constexpr size_t dkdv_lds() {
-  return (size_t)2 * (2 * QS * Geo<D>::KSTR + 4 * QS) * 2;
+  return (size_t)2 * (2 * QS * Geo<D>::KSTR + 6 * QS) * 2;
 }
 
 // dK/dV LDS slice depth in queries (APEX_ATTN_DKDV_QS=32|64 overrides, A/B).  Measured on MI355X

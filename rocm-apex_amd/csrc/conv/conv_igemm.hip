@@ -27,6 +27,7 @@
 #include "apex_amd/conv_api.h"
 #include "apex_amd/device.h"
 #include "apex_amd/dispatch.h"
+#include "apex_amd/launch_plan.h"
 
 #include <cstdlib>
 #include <stdexcept>
@@ -97,7 +98,7 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 // =============================================================================================
 // fprop
 // =============================================================================================
-constexpr int BM = 256, BK = 64;
+constexpr int BM = plan::kConvBM, BK = 64;
 constexpr int STAGES = 3;  // wgrad LDS ring depth
 
 // Tile configuration: BN output channels per workgroup, WM x WN waves, S-deep LDS ring.
@@ -307,7 +308,7 @@ fprop_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, ui
 // =============================================================================================
 // wgrad
 // =============================================================================================
-constexpr int WG_THREADS = 256, WG_BK = 64;
+constexpr int WG_THREADS = 256, WG_BK = plan::kWgradBK;
 
 // quarter-of-a-bank-row swizzle for pixel-major images read by ds_read_b64_tr_b16: the four
 // consecutive rows a 16-lane group reads land in four different 64-byte bank quarters
@@ -462,28 +463,8 @@ __global__ void __launch_bounds__(256) wgrad_reduce(const float* __restrict__ pa
   }
 }
 
-struct WgPlan {
-  int bm, bn, tiles, splits, chunk;
-};
-
-inline WgPlan wgrad_plan(const ConvTapArgs& a, int cus) {
-  WgPlan p;
-  const bool big = a.kout % 128 == 0 && a.c % 128 == 0;
-  p.bm = big ? 128 : 64;
-  p.bn = big ? 128 : 64;
-  p.tiles = (a.kout / p.bm) * (a.ntaps * a.c / p.bn);
-  const int64_t m = (int64_t)a.n * a.oh * a.ow;
-  const int target = cus * (big ? 2 : 4);  // resident workgroups per CU (LDS ring) x two rounds
-  int64_t s = (target + p.tiles - 1) / p.tiles;
-  const int64_t max_s = (m + 16 * WG_BK - 1) / (16 * WG_BK);  // >= 16 K-steps per workgroup
-  if (s > max_s) s = max_s;
-  if (s < 1) s = 1;
-  int64_t chunk = (m + s - 1) / s;
-  chunk = (chunk + WG_BK - 1) / WG_BK * WG_BK;
-  p.chunk = (int)chunk;
-  p.splits = (int)((m + chunk - 1) / chunk);
-  return p;
-}
+using plan::WgPlan;
+inline WgPlan wgrad_plan(const ConvTapArgs& a, int cus) { return plan::conv_wgrad(a, cus); }
 
 }  // namespace conv
 
@@ -520,21 +501,7 @@ static int g_forced_cfg = [] {
 
 void conv_force_fprop_cfg(int cfg) { g_forced_cfg = cfg; }
 
-static int fprop_cfg(const ConvTapArgs& a, int cus) {
-  const int forced = g_forced_cfg;
-  const int64_t tiles_m = ((int64_t)a.n * a.oh * a.ow + conv::BM - 1) / conv::BM;
-  auto ok = [&](int bn) { return a.kout % bn == 0; };
-  if (forced >= 0 && forced <= 6) {
-    const int bn = forced == 6 ? 256 : (forced % 2 == 0 ? 128 : 64);
-    if (ok(bn)) return forced;
-  }
-  // measured on MI355X (profiles/conv_cfg_sweep_r02.jsonl, ResNet-50 3x3 shapes, bs 256): the
-  // 2-stage rings win; BN 256 where it still gives >= half a wave of tiles, BN 64 for <= 128
-  // output channels (two workgroups per CU), BN 128 otherwise
-  if (a.kout <= 128) return 5;
-  if (ok(256) && tiles_m * (a.kout / 256) >= cus / 2) return 6;
-  return ok(128) ? 4 : 5;
-}
+static int fprop_cfg(const ConvTapArgs& a, int cus) { return plan::conv_fprop_cfg(a, cus, g_forced_cfg); }
 
 void conv_tap_fprop(const ConvTapArgs& a, int cus, hipStream_t s) {
   if (!conv_tap_supported(a)) throw std::runtime_error("conv_tap_fprop: unsupported shape / dtype / alignment");

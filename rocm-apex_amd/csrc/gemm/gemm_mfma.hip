@@ -27,6 +27,7 @@
 #include "apex_amd/device.h"
 #include "apex_amd/dispatch.h"
 #include "apex_amd/gemm_api.h"
+#include "apex_amd/launch_plan.h"
 
 namespace apex_amd {
 namespace gemm {
@@ -312,14 +313,7 @@ __global__ void __launch_bounds__(256) colsum_finalize(const float* __restrict__
   if ((threadIdx.x >> 4) == 0 && c < n) out[c] = from_f<TO>(v);
 }
 
-inline int colsum_parts(int64_t m, int n, int cus) {
-  const int gx = (n / 8 + 31) / 32;
-  int64_t p = ((int64_t)cus * 4 + gx - 1) / gx;
-  const int64_t cap = (m + 7) / 8;
-  if (p > cap) p = cap;
-  if (p > 512) p = 512;
-  return (int)(p < 1 ? 1 : p);
-}
+inline int colsum_parts(int64_t m, int n, int cus) { return plan::colsum_parts(m, n, cus); }
 
 template <typename T, bool AK, bool BKM>
 void launch_epi(const GemmArgs& g, hipStream_t s) {
@@ -358,7 +352,7 @@ void launch_epi(const GemmArgs& g, hipStream_t s) {
 // =============================================================================================
 namespace g256 {
 
-constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int BM = plan::kGemmBM, BN = plan::kGemmBN, BK = plan::kGemmBK;
 constexpr int TILE = BM * BK;          // elements per operand tile (32 KB)
 constexpr int CST = BN + 4;            // epilogue fp32 row stride
 constexpr size_t LDS_BYTES = (size_t)128 * CST * 4 > (size_t)4 * TILE * 2 ? (size_t)128 * CST * 4 : (size_t)4 * TILE * 2;
@@ -483,6 +477,20 @@ gemm256_nt(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, T* __
   if (bias != nullptr && gc < N) Vec8<T>::load(bv, bias + gc);
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
+    // activation-gradient epilogues: this half's aux_in rows are fetched before the LDS staging
+    // (clamped addresses, no per-row branch) so their HBM latency overlaps it instead of
+    // serializing one row load per pass
+    constexpr int IT = 128 / (NT / 32);
+    uint4 apre[EPI >= kEpiDGelu ? IT : 1];
+    if constexpr (EPI >= kEpiDGelu) {
+      const int gcc = gc < N ? gc : N - 8;
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        int gr = row0 + half * 128 + rsub + (NT / 32) * it;
+        gr = gr < M ? gr : M - 1;
+        apre[it] = *reinterpret_cast<const uint4*>(aux_in + (int64_t)gr * ldc + gcc);
+      }
+    }
     if (wm == half) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -529,7 +537,7 @@ gemm256_nt(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, T* __
           for (int e = 0; e < 8; ++e) v[e] = 1.f / (1.f + __expf(-(v[e] + bv[e])));
         } else {
           float a[8];
-          Vec8<T>::load(a, aux_in + off);
+          Vec8<T>::load(a, reinterpret_cast<const T*>(&apre[it]));
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             if constexpr (EPI == kEpiDGelu) v[e] *= dgelu_tanh(a[e]);
@@ -568,19 +576,7 @@ __global__ void __launch_bounds__(256) splitk_reduce(const float* __restrict__ p
   }
 }
 
-// number of K chunks for a split-K launch of g (1 = no split); chunk length in *kchunk
-inline int splitk_parts(const GemmArgs& g, int cus, int* kchunk) {
-  *kchunk = g.k;
-  if (g.epilogue != kEpiNone || g.k % BK || g.n % 8) return 1;
-  const int64_t tiles = (int64_t)((g.m + BM - 1) / BM) * ((g.n + BN - 1) / BN);
-  if (tiles >= cus || g.k < 2048) return 1;
-  int64_t sp = (cus + tiles - 1) / tiles;
-  if (sp > g.k / 1024) sp = g.k / 1024;
-  if (sp < 2) return 1;
-  const int chunk = (int)(((g.k + sp - 1) / sp + BK - 1) / BK * BK);
-  *kchunk = chunk;
-  return (g.k + chunk - 1) / chunk;
-}
+inline int splitk_parts(const GemmArgs& g, int cus, int* kchunk) { return plan::gemm_splitk_parts(g, cus, kchunk); }
 
 // waves per 256 x 256 tile: 8 (default) or 4 (APEX_AMD_GEMM256_WAVES=4, A/B)
 inline int waves_cfg() {
@@ -836,6 +832,16 @@ gemm8p_nt(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, T* __r
   if (bias != nullptr && gc < N) Vec8<T>::load(bv, bias + gc);
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
+    uint4 apre[EPI >= kEpiDGelu ? 8 : 1];  // aux_in rows fetched ahead of the staging (see g256)
+    if constexpr (EPI >= kEpiDGelu) {
+      const int gcc = gc < N ? gc : N - 8;
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        int gr = row0 + half * 128 + rsub + 16 * it;
+        gr = gr < M ? gr : M - 1;
+        apre[it] = *reinterpret_cast<const uint4*>(aux_in + (int64_t)gr * ldc + gcc);
+      }
+    }
     if (wr == half) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -880,7 +886,7 @@ gemm8p_nt(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, T* __r
           for (int e = 0; e < 8; ++e) v[e] = 1.f / (1.f + __expf(-(v[e] + bv[e])));
         } else {
           float a[8];
-          Vec8<T>::load(a, aux_in + off);
+          Vec8<T>::load(a, reinterpret_cast<const T*>(&apre[it]));
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             if constexpr (EPI == kEpiDGelu) v[e] *= dgelu_tanh(a[e]);

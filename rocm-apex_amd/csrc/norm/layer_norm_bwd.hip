@@ -10,16 +10,14 @@
 // partial row per quantity; a small column-reduce kernel sums the partials in a fixed order
 // (bitwise deterministic, no float atomics).
 #include "norm_common.h"
+#include "apex_amd/launch_plan.h"
 
 namespace apex_amd {
 namespace norm {
 
 // Persistent grid: enough resident blocks to saturate HBM, few enough that the partial slab
 // stays small relative to the activations.
-inline int bwd_grid(int64_t ngroups, int cus) {
-  const int64_t cap = (int64_t)cus * 2;
-  return (int)(ngroups < cap ? (ngroups > 0 ? ngroups : 1) : cap);
-}
+inline int bwd_grid(int64_t ngroups, int cus) { return plan::ln_bwd_grid(ngroups, cus); }
 
 template <typename TI, typename TW, typename TO, int W, int VPT>
 __global__ void __launch_bounds__(block_threads<W>())
