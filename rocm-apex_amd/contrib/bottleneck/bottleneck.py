@@ -63,7 +63,7 @@ def _fold(w, bn, explicit_nhwc):
     return w * s.reshape(-1, 1, 1, 1).to(w.dtype), b.reshape(-1).to(w.dtype)
 
 
-class _BottleneckBase(nn.Module):
+class Bottleneck(nn.Module):
     def __init__(self, in_channels, bottleneck_channels, out_channels, stride=1, groups=1, dilation=1,
                  norm_func=None, use_cudnn=False, explicit_nhwc=False):
         super().__init__()
@@ -155,11 +155,7 @@ class _BottleneckBase(nn.Module):
         return self._forward_modules(x)
 
 
-class Bottleneck(_BottleneckBase):
-    pass
-
-
-class SpatialBottleneck(_BottleneckBase):
+class SpatialBottleneck(Bottleneck):
     def __init__(self, in_channels, bottleneck_channels, out_channels, stride=1, groups=1, dilation=1,
                  norm_func=None, use_cudnn=False, explicit_nhwc=False, spatial_group_size=1, communicator=None,
                  halo_ex="sendrecv"):
