@@ -144,8 +144,10 @@ constexpr int fwd_occupancy() {
   return LO && base > 1 ? base - 1 : base;
 }
 
-template <typename T, int D, bool PLAIN, int QF, bool LO>
-__global__ void __launch_bounds__(256, (fwd_occupancy<D, PLAIN, QF, LO>())) fwd_kernel(const AttnArgs a) {
+// MODE: 0 = PLAIN (no bias, no dropout), 1 = dropout without bias, 2 = bias (+ dropout); the
+// variants compile out what they do not use (register pressure of the element loops)
+template <typename T, int D, int MODE, int QF, bool LO>
+__global__ void __launch_bounds__(256, (fwd_occupancy<D, MODE == 0, QF, LO>())) fwd_kernel(const AttnArgs a) {
   int bx, by, bz;
   xcd_remap(bx, by, bz);
   using G = Geo<D>;
@@ -228,12 +230,12 @@ __global__ void __launch_bounds__(256, (fwd_occupancy<D, PLAIN, QF, LO>())) fwd_
       for (int i = 0; i < NDT; ++i) o[f][i] = zero16();
     }
     const float c = a.scale * kLog2e;
-    const bool dropout = !PLAIN && a.p_drop > 0.f;  // PLAIN: no bias, no dropout (compiled out)
+    const bool dropout = MODE >= 1 && a.p_drop > 0.f;  // MODE 0: no dropout (compiled out)
     const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
     const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
     const uint32_t smix = seed_mix_of(a.seed, a.offset);
     const uint32_t bh = (uint32_t)(b * a.h + hq);
-    const float* biasb = (!PLAIN && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh : nullptr;
+    const float* biasb = (MODE == 2 && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh : nullptr;
 
     if (nkb > 0) {
       gload(0);
@@ -618,7 +620,7 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
 
 // dK, dV: one workgroup = 4 waves = 128 keys (K, V of the wave's 32 keys in registers); 32-query
 // slices of Q / dO (+ lse, delta) double-buffered in LDS, one barrier per slice.
-template <typename T, int D, bool PLAIN, int QS>
+template <typename T, int D, int MODE, int QS>
 __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const AttnBwdArgs ba) {
   int bx, by, bz;
   xcd_remap(bx, by, bz);
@@ -668,7 +670,7 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
     #pragma unroll
     for (int i = 0; i < NDT; ++i) dk[i] = dv[i] = zero16();
     const float c = a.scale * kLog2e;
-    const bool dropout = !PLAIN && a.p_drop > 0.f;  // PLAIN: no bias, no dropout (compiled out)
+    const bool dropout = MODE >= 1 && a.p_drop > 0.f;  // MODE 0: no dropout (compiled out)
     const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
     const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
     const uint32_t smix = seed_mix_of(a.seed, a.offset);
@@ -682,7 +684,7 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
       const float* lse_h = a.lse + (int64_t)hq * a.rows_q + sq.qrow0;
       const float* del_h = ba.delta + (int64_t)hq * a.rows_q + sq.qrow0;
       const uint32_t bh = (uint32_t)(b * a.h + hq);
-      const float* biash = (!PLAIN && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh : nullptr;
+      const float* biash = (MODE == 2 && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh : nullptr;
       const int q_begin = a.causal ? (k_start / QB) * QB : 0;
       uint4 pq[QCPT], pg[QCPT];
       float plse = INFINITY, pdel = 0.f;
@@ -820,7 +822,7 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
 // registers.  Per tile: S^T = K Q^T and dP^T = V dO^T (query on the lane), P from the saved lse,
 // dS = P (dP - delta), then dQ^T += K^T dS^T with dS fed from registers (crow() k order).  K is
 // kept as two LDS images: row-read (S) and transposed-read (dQ) paddings differ.
-template <typename T, int D, bool PLAIN>
+template <typename T, int D, int MODE>
 __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dq_kernel(const AttnBwdArgs ba) {
   int bx, by, bz;
   xcd_remap(bx, by, bz);
@@ -899,12 +901,12 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dq_kernel(const A
     #pragma unroll
     for (int i = 0; i < NDT; ++i) dq[i] = zero16();
     const float c = a.scale * kLog2e;
-    const bool dropout = !PLAIN && a.p_drop > 0.f;  // PLAIN: no bias, no dropout (compiled out)
+    const bool dropout = MODE >= 1 && a.p_drop > 0.f;  // MODE 0: no dropout (compiled out)
     const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
     const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
     const uint32_t smix = seed_mix_of(a.seed, a.offset);
     const uint32_t bh = (uint32_t)(b * a.h + hq);
-    const float* biasp = (!PLAIN && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh + (int64_t)myq * a.bias_sq
+    const float* biasp = (MODE == 2 && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh + (int64_t)myq * a.bias_sq
                                 : nullptr;
 
     if (nkb > 0) {
@@ -1032,8 +1034,9 @@ void launch_fwd_qf(const AttnArgs& a, hipStream_t s) {
   const int nqb = (a.sq + 128 * QF - 1) / (128 * QF);
   const dim3 grid(a.causal ? (nqb + 1) / 2 : nqb, a.h, a.b);
   if (a.bias == nullptr && !(a.p_drop > 0.f))
-    hipLaunchKernelGGL((fwd_kernel<T, D, true, QF, LO>), grid, dim3(256), fwd_lds<D>(), s, a);
-  else hipLaunchKernelGGL((fwd_kernel<T, D, false, QF, LO>), grid, dim3(256), fwd_lds<D>(), s, a);
+    hipLaunchKernelGGL((fwd_kernel<T, D, 0, QF, LO>), grid, dim3(256), fwd_lds<D>(), s, a);
+  else if (a.bias == nullptr) hipLaunchKernelGGL((fwd_kernel<T, D, 1, QF, LO>), grid, dim3(256), fwd_lds<D>(), s, a);
+  else hipLaunchKernelGGL((fwd_kernel<T, D, 2, QF, LO>), grid, dim3(256), fwd_lds<D>(), s, a);
 }
 
 template <typename T, int D>
@@ -1063,17 +1066,18 @@ constexpr size_t dq_lds() {
   return (size_t)2 * 64 * (2 * Geo<D>::KSTR + Geo<D>::TSTR) * 2;
 }
 
-template <typename T, int D, bool PLAIN>
+template <typename T, int D, int MODE>
 void launch_bwd_v(const AttnBwdArgs& ba, hipStream_t s) {
+  constexpr bool PLAIN = MODE == 0;
   const AttnArgs& a = ba.f;
   constexpr int RPB = 256 / (D / 8);
   hipLaunchKernelGGL((bwd_delta_kernel<T, D>), dim3((a.sq + RPB - 1) / RPB, a.h, a.b), dim3(256), 0, s, ba);
   if (ba.dq_acc == nullptr) {  // split, atomic-free path
     const int nkb = (a.sk + 127) / 128, nqb = (a.sq + 127) / 128;
     const dim3 grid(a.causal ? (nkb + 1) / 2 : nkb, a.h_k, a.b);
-    if (dkdv_qs<D>() == 64) hipLaunchKernelGGL((bwd_dkdv_kernel<T, D, PLAIN, 64>), grid, dim3(256), (dkdv_lds<D, 64>()), s, ba);
-    else hipLaunchKernelGGL((bwd_dkdv_kernel<T, D, PLAIN, 32>), grid, dim3(256), (dkdv_lds<D, 32>()), s, ba);
-    hipLaunchKernelGGL((bwd_dq_kernel<T, D, PLAIN>), dim3(nqb, a.h, a.b), dim3(256), dq_lds<D>(), s, ba);
+    if (dkdv_qs<D>() == 64) hipLaunchKernelGGL((bwd_dkdv_kernel<T, D, MODE, 64>), grid, dim3(256), (dkdv_lds<D, 64>()), s, ba);
+    else hipLaunchKernelGGL((bwd_dkdv_kernel<T, D, MODE, 32>), grid, dim3(256), (dkdv_lds<D, 32>()), s, ba);
+    hipLaunchKernelGGL((bwd_dq_kernel<T, D, MODE>), dim3(nqb, a.h, a.b), dim3(256), dq_lds<D>(), s, ba);
     return;
   }
   (void)hipMemsetAsync(ba.dq_acc, 0, (size_t)a.rows_q * a.h * D * sizeof(float), s);
@@ -1083,8 +1087,9 @@ void launch_bwd_v(const AttnBwdArgs& ba, hipStream_t s) {
 
 template <typename T, int D>
 void launch_bwd(const AttnBwdArgs& ba, hipStream_t s) {
-  if (ba.f.bias == nullptr && !(ba.f.p_drop > 0.f)) launch_bwd_v<T, D, true>(ba, s);
-  else launch_bwd_v<T, D, false>(ba, s);
+  if (ba.f.bias == nullptr && !(ba.f.p_drop > 0.f)) launch_bwd_v<T, D, 0>(ba, s);
+  else if (ba.f.bias == nullptr) launch_bwd_v<T, D, 1>(ba, s);
+  else launch_bwd_v<T, D, 2>(ba, s);
 }
 
 }  // namespace attn

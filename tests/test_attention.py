@@ -198,6 +198,28 @@ def test_gpu_flash_bwd_dkdv_slices(qs, d, causal, sq, sk, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("d,causal,sq,sk", [(64, True, 200, 200), (128, False, 150, 333), (64, False, 70, 45)])
+def test_gpu_flash_dropout_causal_ragged(d, causal, sq, sk):
+    """Dropout (counter-hash decisions, regenerated in the backward) with causal masking and
+    ragged key blocks, against the fp32 reference with the same keep mask."""
+    torch.manual_seed(d + sq)
+    b, h, dtype, p = 2, 3, torch.bfloat16, 0.25
+    q = torch.randn(b, sq, h, d, device="cuda", dtype=dtype, requires_grad=True)
+    k = torch.randn(b, sk, h, d, device="cuda", dtype=dtype, requires_grad=True)
+    v = torch.randn(b, sk, h, d, device="cuda", dtype=dtype, requires_grad=True)
+    out = flash_attn_func(q, k, v, dropout_p=p, causal=causal, seed=21, offset=3)
+    keep = dropout_keep_mask(21, 3, torch.arange(b * h), sq, sk, p, "cuda").view(b, h, sq, sk).float()
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    ref = naive(qr, kr, vr, d ** -0.5, causal, keep=keep, p=p)
+    _close(out, ref, 2e-2)
+    g = torch.randn_like(ref)
+    out.backward(g.to(dtype))
+    ref.backward(g)
+    for a, r in ((q.grad, qr.grad), (k.grad, kr.grad), (v.grad, vr.grad)):
+        _close(a, r, 3e-2)
+
+
+@pytest.mark.gpu
 def test_gpu_flash_bias_gqa_dropout_varlen():
     torch.manual_seed(5)
     dtype = torch.bfloat16
