@@ -138,16 +138,18 @@ __device__ __forceinline__ void xcd_remap(int& bx, int& by, int& bz) {
 // every K / V fragment read from LDS into two MFMAs (half the LDS traffic per FLOP) at the cost
 // of one wave per SIMD for d = 128.
 // LO = true: one resident block less than the default (more registers per lane, no spills)
-template <int D, bool PLAIN, int QF, bool LO>
+template <int D, int MODE, int QF, bool LO>
 constexpr int fwd_occupancy() {
-  constexpr int base = QF == 2 ? (D == 128 ? 1 : 2) : ((D == 128 && !PLAIN) ? 1 : ((D <= 64 && PLAIN) ? 3 : 2));
+  constexpr bool PLAIN = MODE == 0;
+  constexpr int base = QF == 2 ? (D == 128 ? 1 : 2)
+                               : ((D == 128 && !PLAIN) ? 1 : ((D <= 64 && MODE <= 1) ? 3 : 2));
   return LO && base > 1 ? base - 1 : base;
 }
 
 // MODE: 0 = PLAIN (no bias, no dropout), 1 = dropout without bias, 2 = bias (+ dropout); the
 // variants compile out what they do not use (register pressure of the element loops)
 template <typename T, int D, int MODE, int QF, bool LO>
-__global__ void __launch_bounds__(256, (fwd_occupancy<D, MODE == 0, QF, LO>())) fwd_kernel(const AttnArgs a) {
+__global__ void __launch_bounds__(256, (fwd_occupancy<D, MODE, QF, LO>())) fwd_kernel(const AttnArgs a) {
   int bx, by, bz;
   xcd_remap(bx, by, bz);
   using G = Geo<D>;
