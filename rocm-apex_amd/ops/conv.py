@@ -10,7 +10,7 @@ or to MIOpen per shape, from the measurements in ``profiles/conv1x1_miopen_vs_ge
 
 * backward: native 1.14-1.24x MIOpen at 14x14 / 7x7 (M <= 50k) and for Cin >= 512 at 28x28;
   MIOpen ahead at 56x56 where Cout = 64 leaves the 256-wide MFMA tiles half empty;
-* forward: native ahead only for the Cin = 1024 reductions at 14x14.
+* forward: the Cin >= 1024 reductions at 14x14 / 7x7 run as NHWC GEMMs (hipBLASLt by default).
 
 Everything else (CPU, autocast, other layouts / dtypes, odd channel counts) is plain
 ``nn.Conv2d``.  ``APEX_AMD_CONV1X1=0`` disables the native routing (A/B switch).
@@ -30,10 +30,21 @@ _ENABLED = os.environ.get("APEX_AMD_CONV1X1", "1") != "0"
 _STEM_PAD = os.environ.get("APEX_AMD_STEM_PAD", "1") != "0"
 
 
+# forward of the Cin >= 1024 reductions at 14x14 / 7x7: "lib" = the NHWC GEMM on hipBLASLt
+# (torch.matmul on the [pixels, Cin] view), "native" = the gfx950 GEMM, "miopen" = F.conv2d.
+# Measured (profiles/conv1x1_miopen_vs_gemm_r01f.jsonl, profiles/gemm8p_shapes_ab_r02.jsonl):
+# 1024->256 @14: lib 29.9 us, native 37.4, MIOpen 42.9; 1024->512 @14: 53.8 / 67.7 / 77.2;
+# 2048->512 @7: lib 31.5, MIOpen 46.1.  APEX_AMD_CONV1X1_FWD selects (A/B).
+_FWD_BIG = os.environ.get("APEX_AMD_CONV1X1_FWD", "lib")
+
+
 def route(m, cin, cout):
-    """(forward_native, backward_native) for a 1x1 stride-1 conv with M = N*H*W rows."""
+    """(forward, backward_native) for a 1x1 stride-1 conv with M = N*H*W rows; forward is False
+    (MIOpen) or one of "lib" / "native"."""
     bwd = m <= 65536 or (cin >= 512 and cout >= 256 and m <= 262144)
-    fwd = cin >= 1024 and 32768 <= m <= 65536
+    fwd = False
+    if cin >= 1024 and m <= 65536 and _FWD_BIG in ("lib", "native"):
+        fwd = _FWD_BIG if (_FWD_BIG == "lib" or m >= 32768) else False
     return fwd, bwd
 
 
@@ -44,7 +55,9 @@ class _Conv1x1Fn(torch.autograd.Function):
         cout = w.size(0)
         x2 = x.permute(0, 2, 3, 1).reshape(-1, c)  # zero-copy: x is channels_last contiguous
         w2 = w.view(cout, c)
-        if fwd_native:
+        if fwd_native == "lib":
+            y = torch.matmul(x2, w2.t()).view(n, h, wd, cout).permute(0, 3, 1, 2)
+        elif fwd_native:
             g = _native.require("conv1x1").gemm
             y = g.linear(x2, w2, None, g.EPI_NONE, False)[0].view(n, h, wd, cout).permute(0, 3, 1, 2)
         else:

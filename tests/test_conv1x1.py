@@ -18,9 +18,9 @@ def test_cpu_falls_back_and_matches_conv2d_state():
 
 def test_route_policy():
     # ResNet-50 bs 256: native backward at 14x14 / 7x7 and for the 512->256 reduction at 28x28,
-    # MIOpen at 56x56; native forward only for the 1024-channel reductions at 14x14
-    assert route(256 * 7 * 7, 2048, 512) == (False, True)
-    assert route(256 * 14 * 14, 1024, 256) == (True, True)
+    # MIOpen at 56x56; the Cin >= 1024 reductions at 14x14 / 7x7 forward as hipBLASLt NHWC GEMMs
+    assert route(256 * 7 * 7, 2048, 512) == ("lib", True)
+    assert route(256 * 14 * 14, 1024, 256) == ("lib", True)
     assert route(256 * 28 * 28, 512, 256) == (False, True)
     assert route(256 * 28 * 28, 512, 128) == (False, False)
     assert route(256 * 56 * 56, 64, 256) == (False, False)
@@ -44,7 +44,7 @@ def _close(a, b, tol=2e-2):
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,cin,cout,hw", [(4, 1024, 256, 14), (2, 512, 2048, 7), (8, 2048, 512, 7),
                                            (2, 256, 64, 9)])
-@pytest.mark.parametrize("fwd_native", [True, False])
+@pytest.mark.parametrize("fwd_native", [True, "lib", False])
 def test_gpu_conv1x1_native(n, cin, cout, hw, fwd_native):
     from apex import _native
 
