@@ -107,9 +107,16 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         import bench_transformer
 
-        step, B, S, params = bench_transformer.build(args, dev, distributed)
+        if args.impl == "torch":
+            step, B, S, params = bench_transformer.build_torch_baseline(args, dev, distributed)
+        else:
+            step, B, S, params = bench_transformer.build(args, dev, distributed)
         desc = bench_transformer.describe(args, B, S, world, params)
-        return timed(args, step, dev, world, rank, distributed, B, "apex", desc)
+        if args.impl == "torch":
+            desc["metric"] += " [stock torch baseline: HF model, SDPA, autocast, AdamW(fused)]"
+            desc["config"]["optimizer"] = "torch.optim.AdamW(fused=True)"
+            desc["config"]["attention"] = "torch SDPA"
+        return timed(args, step, dev, world, rank, distributed, B, args.impl, desc)
     if args.impl == "torch":
         return run_torch_baseline(args, dev, world, rank, distributed, resnet_mod)
     fused_bn = args.bn == "fused" and not args.no_channels_last

@@ -107,3 +107,50 @@ def describe(args, B, S, world, params):
                    "attention": "gfx950 flash (causal)" if gpt else "gfx950 flash (key-padding bias)",
                    "parallelism": f"dp{world}"},
     }
+
+
+def build_torch_baseline(args, dev, distributed):
+    """Stock reference point for configs 4 / 5 on the same box: Hugging Face GPT-2 medium /
+    BERT-large (random init, same sizes, seq, micro-batch and dropout 0.1) with PyTorch SDPA
+    attention, torch.autocast bf16, torch.optim.AdamW(fused=True) / AdamW for BERT (torch has no
+    LAMB), torch DDP.  ``bench.py --model gpt2-medium --impl torch``."""
+    from transformers import BertConfig, BertForPreTraining, GPT2Config, GPT2LMHeadModel
+
+    cfg = CONFIGS[args.model]
+    B = args.batch_size if args.batch_size_set else cfg["micro_batch"]
+    S = cfg["seq"]
+    V = cfg["vocab"]
+    if cfg["kind"] == "gpt":
+        conf = GPT2Config(n_layer=cfg["layers"], n_embd=cfg["hidden"], n_head=cfg["heads"], n_positions=S,
+                          vocab_size=V, resid_pdrop=0.1, embd_pdrop=0.1, attn_pdrop=0.1,
+                          bos_token_id=V - 1, eos_token_id=V - 1, attn_implementation="sdpa")
+        model = GPT2LMHeadModel(conf).to(dev)
+    else:
+        conf = BertConfig(num_hidden_layers=cfg["layers"], hidden_size=cfg["hidden"],
+                          num_attention_heads=cfg["heads"], intermediate_size=4 * cfg["hidden"],
+                          max_position_embeddings=S, vocab_size=V, hidden_dropout_prob=0.1,
+                          attention_probs_dropout_prob=0.1, attn_implementation="sdpa")
+        model = BertForPreTraining(conf).to(dev)
+    if distributed:
+        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index])
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.01, fused=True)
+    tokens = torch.randint(0, V, (B, S), device=dev)
+    labels = torch.randint(0, V, (B, S), device=dev)
+    if cfg["kind"] == "bert":
+        mask = torch.ones(B, S, device=dev, dtype=torch.long)
+        mask[::4, S * 3 // 4:] = 0
+        nsp = torch.randint(0, 2, (B,), device=dev)
+
+    def step():
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            if cfg["kind"] == "gpt":
+                loss = model(input_ids=tokens, labels=labels).loss
+            else:
+                loss = model(input_ids=tokens, attention_mask=mask, labels=labels, next_sentence_label=nsp).loss
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        return loss
+
+    params = sum(p.numel() for p in model.parameters())
+    return step, B, S, params
