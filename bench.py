@@ -53,9 +53,11 @@ def parse():
                     help="fused: apex.contrib.groupbn NHWC BN with fused ReLU / add+ReLU (gfx950 kernels); "
                          "torch: nn.BatchNorm2d + ReLU (MIOpen)")
     ap.add_argument("--lr", type=float, default=1e-3)
-    ap.add_argument("--no-graph", dest="graph", action="store_false",
-                    help="time eager steps instead of replaying the hipGraph-captured step (single-process runs "
-                         "capture one full training step after warm-up by default; APEX_BENCH_GRAPH=0 also disables)")
+    ap.add_argument("--graph", dest="graph", action="store_true", default=False,
+                    help="single process only: replay one hipGraph-captured training step instead of timing eager "
+                         "steps.  Off by default so every GPU count (1..8, DDP included) is timed the same way "
+                         "(eager; the two agree within 0.1%% at N=1: profiles/bench_resnet50_r02c_fresh_box.log)")
+    ap.add_argument("--no-graph", dest="graph", action="store_false", help=argparse.SUPPRESS)
     ap.add_argument("--impl", default="apex", choices=["apex", "torch"],
                     help="torch = stock PyTorch-ROCm baseline (autocast bf16 + AdamW(fused) + torch DDP)")
     a = ap.parse_args()
@@ -138,6 +140,12 @@ def main():
     if distributed:
         model = apex.parallel.DistributedDataParallel(model)
     criterion = torch.nn.CrossEntropyLoss().to(dev)
+    args.bn_exchange = None
+    if sync_bn:
+        from apex.parallel.peer_memory import exchange_path
+
+        groups = [m.process_group for m in model.modules() if hasattr(m, "bn_group") and m.bn_group > 1]
+        args.bn_exchange = exchange_path(groups[0]) if groups else "rccl"
 
     B = args.batch_size
     images = torch.randn(B, 3, 224, 224, device=dev).to(memory_format=mf)
@@ -227,7 +235,7 @@ def timed(args, step, dev, world, rank, distributed, B, impl, desc=None):
                   file=sys.stderr, flush=True)
             import subprocess
 
-            r = subprocess.run([sys.executable, os.path.abspath(__file__)] + sys.argv[1:] + ["--no-graph"])
+            r = subprocess.run([sys.executable, os.path.abspath(__file__)] + [a for a in sys.argv[1:] if a != "--graph"])
             os._exit(r.returncode)
     if distributed:
         dist.barrier()
@@ -290,7 +298,8 @@ def timed(args, step, dev, world, rank, distributed, B, impl, desc=None):
                     if (impl == "apex" and args.bn == "fused" and not args.no_channels_last)
                     else ("apex SyncBatchNorm" if (args.sync_bn and distributed) else "torch BatchNorm2d (MIOpen)")),
                 "parallelism": f"dp{world}",
-                "hip_graph": bool(getattr(args, "graph", False)),
+                "timing": "hipgraph-replay" if getattr(args, "graph", False) else "eager",
+                "bn_exchange": getattr(args, "bn_exchange", None),
                 "final_loss": round(float(loss.item()), 4),
             },
         }

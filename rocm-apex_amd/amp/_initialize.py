@@ -1,6 +1,22 @@
-"""Model/optimizer processing behind ``amp.initialize`` (reference apex/amp/_initialize.py:21-265)."""
+"""What ``amp.initialize`` does to the models and optimizers once the opt-level properties are
+settled (capability of reference apex/amp/_initialize.py:21-265).
+
+Steps, in order:
+
+1. normalise ``models`` / ``optimizers`` to lists (remembering how they were passed, since the
+   return value mirrors it) and refuse what amp cannot wrap: models already inside a parallel
+   wrapper, optimizers already inside a legacy FP16_Optimizer;
+2. audit the incoming model: every floating parameter / buffer must be fp32 and on the GPU
+   (``allow_incoming_model_not_fp32`` waives it);
+3. cast the model (BN kept fp32 when ``keep_batchnorm_fp32``), wrap ``forward`` with a
+   :class:`_Caster` for inputs and outputs, re-cast the optimizer state, and make every module's
+   ``state_dict`` emit fp32 (:class:`O2StateDictHook`);
+4. patch each optimizer for master weights / the fused amp step (``_process_optimizer``);
+5. create one :class:`LossScaler` per loss, sync-free when every optimizer can take the device
+   skip flag;
+6. O1/O4: install the function-cast patches and keep the optimizer step outside them.
+"""
 import functools
-import sys
 import types
 import warnings
 from collections.abc import Iterable, Mapping
@@ -13,209 +29,199 @@ from ._process_optimizer import _process_optimizer
 from .handle import disable_casts
 from .scaler import LossScaler
 
+_HALF = (torch.float16, torch.bfloat16)
 
+
+class _Caster(object):
+    """Casts every floating tensor found in (nested) call arguments / results to ``dtype``;
+    containers keep their type, strings / arrays / non-tensors pass through."""
+
+    def __init__(self, dtype, warn_host=False):
+        self.dtype = dtype
+        self.warn_host = warn_host
+
+    def tensor(self, t):
+        if isinstance(t, torch.Tensor):
+            if self.warn_host and not t.is_cuda and torch.cuda.is_available():
+                warnings.warn("amp: a model input is not on the GPU.")
+            return t.to(self.dtype) if t.is_floating_point() else t
+        return t.to(self.dtype)  # objects that only provide .to()
+
+    def __call__(self, value):
+        if isinstance(value, torch.Tensor):
+            return self.tensor(value)
+        if isinstance(value, (str, bytes, np.ndarray)):
+            return value
+        if hasattr(value, "to"):
+            return self.tensor(value)
+        if isinstance(value, Mapping):
+            return {self(k): self(v) for k, v in value.items()}
+        if isinstance(value, Iterable):
+            return type(value)(self(v) for v in value)
+        return value
+
+
+# kept for callers of the reference-named helpers
 def to_type(dtype, t):
-    if isinstance(t, torch.Tensor):
-        if not t.is_cuda and torch.cuda.is_available():
-            warnings.warn("An input tensor was not cuda.")
-        if t.is_floating_point():
-            return t.to(dtype)
-        return t
-    return t.to(dtype)
+    return _Caster(dtype, warn_host=True).tensor(t)
 
 
 def applier(value, fn):
-    """Apply ``fn`` to every tensor (or object with ``.to``) inside nested containers."""
-    if isinstance(value, torch.Tensor):
+    if isinstance(fn, _Caster):
         return fn(value)
-    if isinstance(value, (str, bytes)):
-        return value
-    if isinstance(value, np.ndarray):
-        return value
-    if hasattr(value, "to"):
-        return fn(value)
-    if isinstance(value, Mapping):
-        return {applier(k, fn): applier(v, fn) for k, v in value.items()}
-    if isinstance(value, Iterable):
-        return type(value)(applier(v, fn) for v in value)
-    return value
+    caster = _Caster(None)
+    caster.tensor = fn
+    return caster(value)
+
+
+def _as_list(obj, what, accept):
+    """(list, passed_as_list) for a single ``accept`` instance, a list of them, or None."""
+    if obj is None:
+        return [], False
+    if isinstance(obj, list):
+        return obj, True
+    if isinstance(obj, accept):
+        return [obj], False
+    raise TypeError("{} must be either a single {} or a list of them.".format(what, accept[0].__name__))
 
 
 def check_models(models):
-    from ..parallel import DistributedDataParallel as apex_DDP
+    from ..parallel import DistributedDataParallel as ApexDDP
 
+    wrappers = ((torch.nn.parallel.DistributedDataParallel, "torch.nn.parallel.DistributedDataParallel"),
+                (ApexDDP, "apex.parallel.DistributedDataParallel"),
+                (torch.nn.parallel.DataParallel, "torch.nn.parallel.DataParallel"))
     for model in models:
-        parallel_type = None
-        if isinstance(model, torch.nn.parallel.DistributedDataParallel):
-            parallel_type = "torch.nn.parallel.DistributedDataParallel"
-        if isinstance(model, apex_DDP):
-            parallel_type = "apex.parallel.DistributedDataParallel"
-        if isinstance(model, torch.nn.parallel.DataParallel):
-            parallel_type = "torch.nn.parallel.DataParallel"
-        if parallel_type is not None:
-            raise RuntimeError("Incoming model is an instance of {}. ".format(parallel_type) +
-                               "Parallel wrappers should only be applied to the model(s) AFTER \n"
-                               "the model(s) have been returned from amp.initialize.")
+        for cls, name in wrappers:
+            if isinstance(model, cls):
+                raise RuntimeError("amp.initialize got a model already wrapped in {}: apply parallel wrappers to "
+                                   "the model(s) that amp.initialize returns, not before.".format(name))
 
 
 def check_params_fp32(models):
+    """Every floating parameter / buffer must arrive fp32 and on the GPU."""
+    on_gpu = torch.cuda.is_available()
     for model in models:
-        for name, param in model.named_parameters():
-            if param.is_floating_point():
-                if param.dtype in (torch.float16, torch.bfloat16):
-                    warn_or_err("Found param {} with type {}, expected torch.cuda.FloatTensor.\n"
-                                "When using amp.initialize, you do not need to call .half() or .bfloat16()\n"
-                                "on your model before passing it, no matter what optimization level you "
-                                "choose.".format(name, param.type()))
-                elif not param.is_cuda and torch.cuda.is_available():
-                    warn_or_err("Found param {} with type {}, expected torch.cuda.FloatTensor.\n"
-                                "When using amp.initialize, you need to provide a model with parameters\n"
-                                "located on a CUDA device before passing it no matter what optimization level\n"
-                                "you chose. Use model.to('cuda') to use the default device.".format(
-                                    name, param.type()))
-        for name, buf in model.named_buffers():
-            if buf.is_floating_point():
-                if buf.dtype == torch.float16:
-                    warn_or_err("Found buffer {} with type {}, expected torch.cuda.FloatTensor.\n"
-                                "When using amp.initialize, you do not need to call .half() on your model\n"
-                                "before passing it, no matter what optimization level you choose.".format(
-                                    name, buf.type()))
-                elif not buf.is_cuda and torch.cuda.is_available():
-                    warn_or_err("Found buffer {} with type {}, expected torch.cuda.FloatTensor.\n"
-                                "When using amp.initialize, you need to provide a model with buffers\n"
-                                "located on a CUDA device before passing it no matter what optimization level\n"
-                                "you chose. Use model.to('cuda') to use the default device.".format(
-                                    name, buf.type()))
+        tensors = [("param", n, t) for n, t in model.named_parameters()]
+        tensors += [("buffer", n, t) for n, t in model.named_buffers()]
+        for kind, name, t in tensors:
+            if not t.is_floating_point():
+                continue
+            low = t.dtype in _HALF if kind == "param" else t.dtype == torch.float16
+            if low:
+                warn_or_err("amp.initialize: {} {} is {} — pass the model in fp32; amp does any .half() / "
+                            ".bfloat16() casting itself, whatever the opt_level.".format(kind, name, t.type()))
+            elif on_gpu and not t.is_cuda:
+                warn_or_err("amp.initialize: {} {} is {} on the host — move the model to the GPU "
+                            "(model.to('cuda')) before amp.initialize.".format(kind, name, t.type()))
 
 
 def check_optimizers(optimizers):
-    from ..contrib.optimizers import FP16_Optimizer as FP16_Optimizer_for_fused
-    from ..fp16_utils import FP16_Optimizer as FP16_Optimizer_general
+    from ..contrib.optimizers import FP16_Optimizer as FusedFP16Optimizer
+    from ..fp16_utils import FP16_Optimizer as GeneralFP16Optimizer
 
     for optim in optimizers:
-        bad = None
-        if isinstance(optim, FP16_Optimizer_general):
-            bad = "apex.fp16_utils.FP16_Optimizer"
-        if isinstance(optim, FP16_Optimizer_for_fused):
-            bad = "apex.optimizers.FP16_Optimizer"
-        if bad is not None:
-            raise RuntimeError("An incoming optimizer is an instance of {}. ".format(bad) +
-                               "The optimizer(s) passed to amp.initialize() must be bare \n"
-                               "instances of either ordinary Pytorch optimizers, or Apex fused \n"
-                               "optimizers.\n")
+        if isinstance(optim, (GeneralFP16Optimizer, FusedFP16Optimizer)):
+            raise RuntimeError("amp.initialize takes plain PyTorch or apex fused optimizers; got a {} — pass "
+                               "the optimizer it wraps instead.".format(type(optim).__name__))
 
 
 class O2StateDictHook(object):
-    """Makes ``model.state_dict()`` emit fp32 tensors under O2/O3/O5."""
+    """``state_dict`` hook: half / bfloat16 entries are emitted as fp32 (O2/O3/O5 checkpoints stay
+    loadable into an fp32 model)."""
 
-    def __init__(self, fn):
+    def __init__(self, fn=None):
         self.fn = fn
 
     def __call__(self, module, state_dict, prefix, local_metadata):
-        for key in state_dict:
-            param = state_dict[key]
-            if isinstance(param, torch.Tensor) and param.dtype in (torch.float16, torch.bfloat16):
-                state_dict[key] = param.to(torch.float32)
+        for key, value in state_dict.items():
+            if isinstance(value, torch.Tensor) and value.dtype in _HALF:
+                state_dict[key] = value.float()
 
 
-def _initialize(models, optimizers, properties, num_losses=1, cast_model_outputs=None):
+def _wrap_forward(model, in_caster, out_caster):
+    fwd = model.forward
+
+    @functools.wraps(fwd)
+    def forward(*args, **kwargs):
+        if in_caster is not None:
+            args, kwargs = in_caster(args), in_caster(kwargs)
+        return out_caster(fwd(*args, **kwargs))
+
+    model.forward = forward
+
+
+def _cast_models(models, properties, cast_model_outputs, optimizers):
     from ..fp16_utils import convert_network
-    from ..parallel.LARC import LARC
-    from .amp import init as amp_init
-
-    optimizers_was_list = False
-    if isinstance(optimizers, torch.optim.Optimizer) or isinstance(optimizers, LARC):
-        optimizers = [optimizers]
-    elif optimizers is None:
-        optimizers = []
-    elif isinstance(optimizers, list):
-        optimizers_was_list = True
-        check_optimizers(optimizers)
-    else:
-        check_optimizers([optimizers])
-        raise TypeError("optimizers must be either a single optimizer or a list of optimizers.")
-
-    if isinstance(models, torch.nn.Module):
-        models_was_list = False
-        models = [models]
-    elif isinstance(models, list):
-        models_was_list = True
-    else:
-        raise TypeError("models must be either a single model or a list of models.")
-
-    check_models(models)
-    if not _amp_state.allow_incoming_model_not_fp32:
-        check_params_fp32(models)
 
     if properties.cast_model_type:
-        if properties.keep_batchnorm_fp32:
-            for model in models:
-                convert_network(model, properties.cast_model_type)
-        else:
-            for model in models:
-                model.to(properties.cast_model_type)
-
-        input_caster = functools.partial(to_type, properties.cast_model_type)
-        output_caster = functools.partial(to_type, cast_model_outputs if cast_model_outputs is not None
-                                          else torch.float32)
-
         for model in models:
-            def patch_forward(old_fwd):
-                def new_fwd(*args, **kwargs):
-                    output = old_fwd(*applier(args, input_caster), **applier(kwargs, input_caster))
-                    return applier(output, output_caster)
-                return new_fwd
-
-            model.forward = patch_forward(model.forward)
-
-        for optimizer in optimizers:
+            if properties.keep_batchnorm_fp32:
+                convert_network(model, properties.cast_model_type)
+            else:
+                model.to(properties.cast_model_type)
+        out = _Caster(cast_model_outputs if cast_model_outputs is not None else torch.float32)
+        for model in models:
+            _wrap_forward(model, _Caster(properties.cast_model_type, warn_host=True), out)
+        for optimizer in optimizers:  # re-cast any existing state to the params' new dtypes
             optimizer.load_state_dict(optimizer.state_dict())
-
+        hook = O2StateDictHook()
         for model in models:
             for module in model.modules():
-                module._register_state_dict_hook(O2StateDictHook(functools.partial(to_type, torch.float32)))
-
+                module._register_state_dict_hook(hook)
     elif cast_model_outputs is not None:
-        output_caster = functools.partial(to_type, cast_model_outputs)
         for model in models:
-            def patch_forward(old_fwd):
-                def new_fwd(*args, **kwargs):
-                    return applier(old_fwd(*args, **kwargs), output_caster)
-                return new_fwd
+            _wrap_forward(model, None, _Caster(cast_model_outputs))
 
-            model.forward = patch_forward(model.forward)
 
-    for i, optimizer in enumerate(optimizers):
-        optimizers[i] = _process_optimizer(optimizer, properties)
-
-    # sync-free scaler when every optimizer consumes a device skip flag
-    all_capable = len(optimizers) > 0 and all(getattr(o, "_amp_fused_capable", False) for o in optimizers)
-    _amp_state.sync_free = bool(_amp_state.sync_free_requested and all_capable and (
-        torch.cuda.is_available() or getattr(_amp_state, "sync_free_force", False)))
+def _make_loss_scalers(properties, optimizers, num_losses):
+    fused = bool(optimizers) and all(getattr(o, "_amp_fused_capable", False) for o in optimizers)
+    device_ok = torch.cuda.is_available() or getattr(_amp_state, "sync_free_force", False)
+    _amp_state.sync_free = bool(_amp_state.sync_free_requested and fused and device_ok)
     for o in optimizers:
         o._amp_stash.fused_ok = _amp_state.sync_free
-
-    _amp_state.loss_scalers = []
+    scalers = []
     for _ in range(num_losses):
         s = LossScaler(properties.loss_scale, min_loss_scale=_amp_state.min_loss_scale,
                        max_loss_scale=_amp_state.max_loss_scale)
         s.sync_free = _amp_state.sync_free
-        _amp_state.loss_scalers.append(s)
+        scalers.append(s)
+    _amp_state.loss_scalers = scalers
 
+
+def _step_without_casts(optimizer):
+    inner = optimizer.step
+
+    def step(self, *args, **kwargs):
+        with disable_casts():
+            return inner(*args, **kwargs)
+
+    optimizer.step = types.MethodType(step, optimizer)
+
+
+def _initialize(models, optimizers, properties, num_losses=1, cast_model_outputs=None):
+    from ..parallel.LARC import LARC
+    from .amp import init as amp_init
+
+    if optimizers is not None and not isinstance(optimizers, (list, torch.optim.Optimizer, LARC)):
+        check_optimizers([optimizers])
+    opts, opts_listed = _as_list(optimizers, "optimizers", (torch.optim.Optimizer, LARC))
+    check_optimizers(opts)
+    mods, mods_listed = _as_list(models, "models", (torch.nn.Module,))
+
+    check_models(mods)
+    if not _amp_state.allow_incoming_model_not_fp32:
+        check_params_fp32(mods)
+    _cast_models(mods, properties, cast_model_outputs, opts)
+    opts = [_process_optimizer(o, properties) for o in opts]
+    _make_loss_scalers(properties, opts, num_losses)
     if properties.patch_torch_functions:
         amp_init(loss_scale=properties.loss_scale, patch_type=properties.patch_torch_functions_type,
                  verbose=(_amp_state.verbosity == 2))
-        for optimizer in optimizers:
-            def patch_step(old_step):
-                def new_step(self, *args, **kwargs):
-                    with disable_casts():
-                        return old_step(*args, **kwargs)
-                return new_step
+        for o in opts:
+            _step_without_casts(o)
 
-            optimizer.step = types.MethodType(patch_step(optimizer.step), optimizer)
-
-    if optimizers_was_list:
-        return (models, optimizers) if models_was_list else (models[0], optimizers)
-    if models_was_list:
-        return models if len(optimizers) == 0 else (models, optimizers[0])
-    return models[0] if len(optimizers) == 0 else (models[0], optimizers[0])
+    model_out = mods if mods_listed else mods[0]
+    if opts_listed:
+        return model_out, opts
+    return model_out if not opts else (model_out, opts[0])

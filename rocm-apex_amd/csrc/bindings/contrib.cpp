@@ -12,7 +12,7 @@ void bias_dropout_add_fwd(const void* x, const void* bias, const void* res, void
 void bias_dropout_add_bwd(const void* g, void* dx, int64_t n, int dtype, float p, uint64_t seed, uint64_t offset, int cus,
                           hipStream_t s);
 
-void* peer_alloc(size_t bytes);
+void* peer_alloc(size_t bytes, int* kind);
 void peer_free(void* p);
 std::string peer_handle(void* p);
 void* peer_open(const std::string& handle);
@@ -24,7 +24,11 @@ void peer_allgather(const float* local, int n, int nmax, float* const* bufs, int
 namespace {
 
 // ---- peer memory (hipIpc over xGMI) exchange: csrc/comm/peer.hip ----
-int64_t pm_alloc(int64_t bytes) { return (int64_t)(uintptr_t)peer_alloc((size_t)bytes); }
+pybind11::tuple pm_alloc(int64_t bytes) {
+  int kind = 0;
+  void* p = peer_alloc((size_t)bytes, &kind);
+  return pybind11::make_tuple((int64_t)(uintptr_t)p, kind);
+}
 void pm_free(int64_t p) { peer_free((void*)(uintptr_t)p); }
 pybind11::bytes pm_handle(int64_t p) { return pybind11::bytes(peer_handle((void*)(uintptr_t)p)); }
 int64_t pm_open(const std::string& h) { return (int64_t)(uintptr_t)peer_open(h); }

@@ -10,8 +10,15 @@
 //   1. push: write the local payload into slot `me` of EVERY member's buffer (remote stores go
 //      straight over xGMI), system-scope release fence, then store the epoch into each header;
 //   2. wait: spin (bounded, with s_sleep) until all `group` headers of this parity in the LOCAL
-//      buffer carry the epoch (system-scope acquire);
+//      buffer carry the epoch (system-scope ACQUIRE loads of the flags, then a system acquire
+//      fence for the whole workgroup);
 //   3. read: copy the `group` payloads into the output [group][n].
+// The exchange buffers are allocated UNCACHED (hipExtMallocWithFlags(hipDeviceMallocUncached),
+// the allocation RCCL uses for its cross-GPU flags): coarse-grained device memory is only coherent
+// at kernel boundaries, while these slots are written by remote GPUs over xGMI and polled by a
+// running kernel.  If the driver refuses an uncached (or fine-grained) IPC-exportable buffer the
+// allocation falls back to plain device memory and reports it (peer_alloc_kind); the Python side
+// then validates the protocol with a short handshake before trusting it (PeerExchange).
 // Parity = epoch & 1 double-buffers the slots: a rank can only reach epoch e+2 after every member
 // published e+1, which each member does only after it finished reading epoch e.
 //
@@ -64,7 +71,7 @@ __global__ void __launch_bounds__(256) allgather_kernel(const float* __restrict_
   if (tid < group) {
     uint32_t* flag = reinterpret_cast<uint32_t*>(bufs.buf[me] + (int64_t)(parity * group + tid) * slot);
     const uint64_t t0 = wall_clock64();
-    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
       if (wall_clock64() - t0 > timeout_ticks) {
         timed_out = 1;
         break;
@@ -89,11 +96,34 @@ __global__ void __launch_bounds__(256) allgather_kernel(const float* __restrict_
 
 }  // namespace peer
 
-void* peer_alloc(size_t bytes) {
+// kind: 2 = uncached, 1 = fine-grained, 0 = plain coarse-grained device memory.  A kind is only
+// accepted when the buffer can also be exported for IPC (hipIpcGetMemHandle succeeds on it).
+void* peer_alloc(size_t bytes, int* kind) {
+  const unsigned flags[2] = {hipDeviceMallocUncached, hipDeviceMallocFinegrained};
   void* p = nullptr;
-  if (hipMalloc(&p, bytes) != hipSuccess) throw std::runtime_error("peer_alloc: hipMalloc failed");
+  int k = -1;
+  for (int i = 0; i < 2 && k < 0; ++i) {
+    if (hipExtMallocWithFlags(&p, bytes, flags[i]) != hipSuccess) {
+      (void)hipGetLastError();
+      p = nullptr;
+      continue;
+    }
+    hipIpcMemHandle_t h;
+    if (hipIpcGetMemHandle(&h, p) == hipSuccess) {
+      k = 2 - i;
+    } else {
+      (void)hipGetLastError();
+      (void)hipFree(p);
+      p = nullptr;
+    }
+  }
+  if (k < 0) {
+    if (hipMalloc(&p, bytes) != hipSuccess) throw std::runtime_error("peer_alloc: hipMalloc failed");
+    k = 0;
+  }
   if (hipMemset(p, 0, bytes) != hipSuccess) throw std::runtime_error("peer_alloc: hipMemset failed");
   if (hipDeviceSynchronize() != hipSuccess) throw std::runtime_error("peer_alloc: sync failed");
+  if (kind) *kind = k;
   return p;
 }
 

@@ -229,8 +229,11 @@ __global__ void __launch_bounds__(256) stats_merge(const float* __restrict__ gat
   const float sc = istd * (w ? w[ch] : 1.f);
   coef[ch] = sc;
   coef[c + ch] = (b ? b[ch] : 0.f) - mm * sc;
-  if (rmean) rmean[ch] = (1.f - momentum) * rmean[ch] + momentum * mm;
-  if (rvar) rvar[ch] = (1.f - momentum) * rvar[ch] + momentum * (float)(n > 1.0 ? m2 / (n - 1.0) : var_b);
+  // a timed-out peer exchange hands back NaN payloads (csrc/comm/peer.hip): the step's outputs are
+  // poisoned so the loss scaler skips it, but the running statistics must survive unchanged
+  const bool finite = isfinite(mm) && isfinite(var_b);
+  if (rmean && finite) rmean[ch] = (1.f - momentum) * rmean[ch] + momentum * mm;
+  if (rvar && finite) rvar[ch] = (1.f - momentum) * rvar[ch] + momentum * (float)(n > 1.0 ? m2 / (n - 1.0) : var_b);
   if (ch == 0) inv_count[0] = (float)(n > 0.0 ? 1.0 / n : 0.0);
 }
 

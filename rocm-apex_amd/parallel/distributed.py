@@ -117,16 +117,20 @@ def _owner(param):
 
 
 def zero_bucketed_grads(params):
-    """Zero the gradients of the DDP-owned ``params`` in place (one memset per bucket, views
-    re-attached); returns the set of ``id(param)`` handled — the caller resets the others."""
+    """Zero the gradients of the DDP-owned ``params`` in place (views re-attached); returns the
+    set of ``id(param)`` handled — the caller resets the others.
+
+    Only the gradients of ``params`` are touched: a bucket is cleared with one memset when every
+    parameter in it belongs to ``params``, otherwise just the views of the listed parameters are
+    zeroed, so a second optimizer over the same DDP model keeps its not-yet-consumed gradients."""
     done, owners = set(), {}
     for p in params:
         d = _owner(p)
         if d is not None:
-            owners[id(d)] = d
+            owners.setdefault(id(d), (d, set()))[1].add(id(p))
             done.add(id(p))
-    for d in owners.values():
-        d.zero_grad_buckets()
+    for d, ids in owners.values():
+        d.zero_grad_buckets(ids)
     return done
 
 
@@ -137,14 +141,15 @@ def zeroed_bucket_params(params):
         d = _owner(p)
         if d is not None and p.grad is not None:
             b, i = d._slot[id(p)]
-            if b.zeroed and p.grad.data_ptr() == b.buffer.data_ptr() + b.offsets[i] * b.buffer.element_size():
+            known_zero = b.zeroed or id(p) in b.zeroed_ids
+            if known_zero and p.grad.data_ptr() == b.buffer.data_ptr() + b.offsets[i] * b.buffer.element_size():
                 out.add(id(p))
     return out
 
 
 class _Bucket(object):
     __slots__ = ("index", "params", "offsets", "numel", "dtype", "buffer", "fp32_buffer", "ready", "fired",
-                 "work", "group", "zeroed")
+                 "work", "group", "zeroed", "zeroed_ids")
 
     def __init__(self, index, params, dtype, device, group, fp32_copy):
         self.index = index
@@ -164,6 +169,11 @@ class _Bucket(object):
         self.work = None
         self.group = group
         self.zeroed = True
+        self.zeroed_ids = set()  # params zeroed one by one since the bucket was last written
+
+    def dirty(self):
+        self.zeroed = False
+        self.zeroed_ids.clear()
 
     def view_for(self, i):
         p = self.params[i]
@@ -287,7 +297,7 @@ class DistributedDataParallel(Module):
                 v = b.view_for(i)
                 v.copy_(p.grad)
                 p.grad = v
-                b.zeroed = False
+                b.dirty()
 
     # ------------------------------------------------------------------------------ hooks
     def _create_hooks(self):
@@ -306,7 +316,7 @@ class DistributedDataParallel(Module):
             if self._iteration == 0 and self.rebucket_by_arrival:
                 self._arrival.append(pid)
             b, i = self._slot[pid]
-            b.zeroed = False
+            b.dirty()
             g = param.grad
             if g.data_ptr() != b.buffer.data_ptr() + b.offsets[i] * b.buffer.element_size():
                 # a freshly allocated grad (first iteration, or grads reset to None): one copy
@@ -372,7 +382,7 @@ class DistributedDataParallel(Module):
                         if p.grad is None:
                             v.zero_()
                             p.grad = v
-                            b.zeroed = False
+                            b.dirty()
                         elif p.grad.data_ptr() != v.data_ptr():
                             v.copy_(p.grad)
                             p.grad = v
@@ -390,17 +400,29 @@ class DistributedDataParallel(Module):
             self._iteration += 1
 
     # ------------------------------------------------------------------------------ API
-    def zero_grad_buckets(self):
-        """Zero every bucket (one memset each, skipped when already zero) and attach each
-        parameter's gradient as its bucket view, so backward accumulates in place."""
+    def zero_grad_buckets(self, only=None):
+        """Zero the buckets (one memset each, skipped when already zero) and attach each
+        parameter's gradient as its bucket view, so backward accumulates in place.
+
+        ``only``: a set of ``id(param)``; a bucket holding parameters outside it is not cleared
+        as a whole — only the listed parameters' views are zeroed (and re-attached)."""
         for b in self._buckets:
-            if not b.zeroed:
-                b.buffer.zero_()
-                b.zeroed = True
+            whole = only is None or all(id(p) in only for p in b.params)
+            if whole:
+                if not b.zeroed:
+                    b.buffer.zero_()
+                    b.zeroed = True
+                b.zeroed_ids.clear()
             for i, p in enumerate(b.params):
+                if not whole and id(p) not in only:
+                    continue
                 g = p.grad
-                if g is None or g.data_ptr() != b.buffer.data_ptr() + b.offsets[i] * b.buffer.element_size():
+                attached = g is not None and g.data_ptr() == b.buffer.data_ptr() + b.offsets[i] * b.buffer.element_size()
+                if not attached:
                     p.grad = b.view_for(i)
+                if not whole and not b.zeroed and id(p) not in b.zeroed_ids:
+                    p.grad.zero_()
+                    b.zeroed_ids.add(id(p))
 
     def forward(self, *inputs, **kwargs):
         if self.prof:

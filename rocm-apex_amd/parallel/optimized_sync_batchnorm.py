@@ -23,6 +23,7 @@ class SyncBatchnormFunction(Function):
         if channel_last and not input.is_contiguous():
             input = input.contiguous()
         world_size = 0
+        peer_used = False
         if track_running_stats:
             num_channels = input.size(-1) if channel_last else input.size(1)
             count = input.numel() // num_channels
@@ -35,6 +36,7 @@ class SyncBatchnormFunction(Function):
                 peer = get_peer_exchange(process_group)
                 if peer is not None:  # hipIpc exchange over xGMI (parallel/peer_memory.py)
                     gathered = peer.all_gather(combined).to(combined.dtype)
+                    peer_used = True
                 elif dist.get_backend(pg) == "nccl":
                     gathered = torch.empty(world_size * combined.numel(), dtype=combined.dtype,
                                            device=combined.device)
@@ -57,8 +59,17 @@ class SyncBatchnormFunction(Function):
             if running_mean is not None:
                 r_m = mean if running_mean.dtype != torch.float16 else mean.half()
                 r_v = var if running_variance.dtype != torch.float16 else var.half()
-                running_mean.data.mul_(1 - momentum).add_(momentum * r_m)
-                running_variance.data.mul_(1 - momentum).add_(momentum * r_v)
+                if peer_used:
+                    # a timed-out peer exchange poisons mean/var with NaN (the step is skipped by
+                    # the loss scaler); keep the running statistics as they were, sync-free
+                    keep = torch.isfinite(r_m) & torch.isfinite(r_v)
+                    running_mean.data.copy_(torch.where(keep, running_mean.data * (1 - momentum) + momentum * r_m,
+                                                        running_mean.data))
+                    running_variance.data.copy_(torch.where(
+                        keep, running_variance.data * (1 - momentum) + momentum * r_v, running_variance.data))
+                else:
+                    running_mean.data.mul_(1 - momentum).add_(momentum * r_m)
+                    running_variance.data.mul_(1 - momentum).add_(momentum * r_v)
         else:
             mean = running_mean.data.float()
             inv_std = 1.0 / torch.sqrt(running_variance.data.float() + eps)

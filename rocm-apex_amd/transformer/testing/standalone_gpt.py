@@ -16,11 +16,13 @@ def post_language_model_processing(lm_output, labels, logit_weights, parallel_ou
         return output
     # labels [b, s]; logits [s, b, v/tp]
     labels = labels.transpose(0, 1).contiguous()
+    # fp16_lm_cross_entropy: hand the half logits to the loss as they are (its reductions run in
+    # fp32 registers either way); otherwise upcast first, as the reference does
     if fp16_lm_cross_entropy:
         assert output.dtype == torch.half
-        loss = tensor_parallel.vocab_parallel_cross_entropy(output, labels)
     else:
-        loss = tensor_parallel.vocab_parallel_cross_entropy(output, labels)  # fp32 math inside
+        output = output.float()
+    loss = tensor_parallel.vocab_parallel_cross_entropy(output, labels)
     return loss.transpose(0, 1).contiguous()  # [b, s]
 
 

@@ -343,3 +343,43 @@ def test_ddp_zero_copy_matches_manual_allreduce_gloo():
     # per-tensor all-reduce agree bit for bit; at 8 ranks gloo's ring order differs between the two
     # and Adam amplifies the last-bit differences (world 8 is covered by the exact-sum race test)
     run_multiprocess(_ddp_zero_copy_matches_reference_worker, 2, ())
+
+
+# ------------------------------------------------------- two amp optimizers over one DDP model
+def _ddp_two_optimizers_worker(rank, world):
+    import os
+
+    os.environ["APEX_AMD_AMP_SYNC_FREE"] = "force"
+    from apex import amp
+    from apex.amp._amp_state import _amp_state
+    from apex.optimizers import FusedAdam
+    from apex.parallel import DistributedDataParallel as DDP
+
+    _amp_state.sync_free_force = True
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 4))
+    first, second = list(model[0].parameters()), list(model[2].parameters())
+    opt1 = FusedAdam(first, lr=1e-2, materialize_master_grads=False)
+    opt2 = FusedAdam(second, lr=1e-2, materialize_master_grads=False)
+    model, (opt1, opt2) = amp.initialize(model, [opt1, opt2], opt_level="O2", cast_model_type=torch.bfloat16,
+                                         verbosity=0)
+    ddp = DDP(model)  # default message size: ONE bucket shared by both optimizers' params
+    assert len(ddp.buckets) == 1
+    for it in range(3):
+        x = torch.randn(8, 16, generator=torch.Generator().manual_seed(10 * rank + it))
+        loss = ddp(x).float().pow(2).mean()
+        opt1.zero_grad()
+        opt2.zero_grad()
+        with amp.scale_loss(loss, [opt1, opt2]) as s:
+            s.backward()
+        g2 = [p.grad.detach().clone() for p in model[2].parameters()]
+        assert all(g.abs().sum() > 0 for g in g2), "second optimizer's grads are zero before any step"
+        opt1.step()
+        # opt1's post-step reset must not wipe the grads opt2 has not consumed yet
+        for p, g in zip(model[2].parameters(), g2):
+            assert p.grad is not None and torch.equal(p.grad, g), (it, "opt1.step() zeroed opt2's gradients")
+        opt2.step()
+
+
+def test_ddp_two_amp_optimizers_keep_each_others_grads_gloo():
+    run_multiprocess(_ddp_two_optimizers_worker, 2, ())

@@ -14,6 +14,9 @@ def _exchange_worker(rank, world):
     torch.cuda.set_device(0)
     ex = enable_peer_memory(None)
     assert ex is not None and get_peer_exchange(None) is ex
+    # the exchange slots are written by remote GPUs while a kernel polls them: never plain
+    # coarse-grained memory (coherent only at kernel boundaries)
+    assert ex.alloc_kind in ("uncached", "fine-grained"), ex.alloc_kind
     for it in range(6):
         n = 100 + 37 * it
         local = torch.arange(n, device="cuda", dtype=torch.float32) + 1000.0 * (rank + 1) + it
@@ -159,3 +162,78 @@ def _timeout_worker(rank, world):
 @pytest.mark.gpu
 def test_gpu_peer_exchange_timeout_poisons_and_raises():
     run_multiprocess(_timeout_worker, 2, (), timeout=180)
+
+
+def _forced_handshake_failure_worker(rank, world):
+    """A handshake that fails on ONE member: every member agrees on the RCCL/gloo path (no hang,
+    no half-enabled group), the fused group BN runs through the collective fallback with the same
+    numerics, and the bench-facing path report says "rccl"."""
+    import apex
+    from apex.contrib.groupbn import BatchNorm2d_NHWC
+    from apex.contrib.groupbn.batch_norm import _bn_group
+    from apex.parallel import peer_memory
+
+    torch.cuda.set_device(0)
+    group = _bn_group(world)
+    ex = peer_memory.enable_peer_memory(group, _fail_handshake=(rank == 1))
+    assert ex is None and peer_memory.get_peer_exchange(group) is None
+    assert peer_memory.exchange_path(group) == "rccl"
+    torch.manual_seed(0)
+    C = 32
+    full = torch.randn(8, C, 5, 5, device="cuda")
+    gy = torch.randn(8, C, 5, 5, device="cuda")
+    sl = slice(rank * 4, (rank + 1) * 4)
+    x = full[sl].clone().to(memory_format=torch.channels_last).requires_grad_(True)
+    bn = BatchNorm2d_NHWC(C, fuse_relu=True, bn_group=world, torch_channels_last=True).cuda()
+    assert bn.process_group is group and peer_memory.get_peer_exchange(group) is None
+    y = bn(x)
+    (y * gy[sl]).sum().backward()
+    ref = torch.nn.BatchNorm2d(C).cuda()
+    fr = full.clone().requires_grad_(True)
+    yr = torch.relu(ref(fr))
+    (yr * gy).sum().backward()
+    torch.testing.assert_close(y, yr[sl], rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(x.grad, fr.grad[sl], rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(bn.running_var, ref.running_var, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_gpu_peer_handshake_failure_falls_back_to_collectives():
+    run_multiprocess(_forced_handshake_failure_worker, 2, (), timeout=180)
+
+
+def _poisoned_running_stats_worker(rank, world):
+    """A timed-out exchange poisons the step's statistics with NaN but leaves the running
+    statistics of the group BN untouched (stats_merge skips non-finite merges)."""
+    import time
+
+    import torch.distributed as dist
+
+    import apex
+    from apex.contrib.groupbn import BatchNorm2d_NHWC
+    from apex.parallel import peer_memory
+
+    torch.cuda.set_device(0)
+    bn = BatchNorm2d_NHWC(16, fuse_relu=False, bn_group=world, torch_channels_last=True).cuda()
+    ex = peer_memory.get_peer_exchange(bn.process_group)
+    assert ex is not None
+    ex.timeout_s = 0.25
+    x = torch.randn(2, 16, 3, 3, device="cuda").to(memory_format=torch.channels_last)
+    bn(x)
+    torch.cuda.synchronize()
+    rm, rv = bn.running_mean.clone(), bn.running_var.clone()
+    dist.barrier()
+    if rank == 1:
+        time.sleep(1.5)
+    y = bn(x)
+    torch.cuda.synchronize()
+    if rank == 0:
+        assert torch.isnan(y).all()
+        torch.testing.assert_close(bn.running_mean, rm, rtol=0, atol=0)
+        torch.testing.assert_close(bn.running_var, rv, rtol=0, atol=0)
+    dist.barrier()
+
+
+@pytest.mark.gpu
+def test_gpu_peer_timeout_keeps_running_stats():
+    run_multiprocess(_poisoned_running_stats_worker, 2, (), timeout=180)
