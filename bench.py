@@ -144,7 +144,9 @@ def main():
     if sync_bn:
         from apex.parallel.peer_memory import exchange_path
 
-        groups = [m.process_group for m in model.modules() if hasattr(m, "bn_group") and m.bn_group > 1]
+        from apex.contrib.groupbn import BatchNorm2d_NHWC
+
+        groups = [m.process_group for m in model.modules() if isinstance(m, BatchNorm2d_NHWC) and m.bn_group > 1]
         args.bn_exchange = exchange_path(groups[0]) if groups else "rccl"
 
     B = args.batch_size

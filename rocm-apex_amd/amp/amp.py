@@ -99,48 +99,55 @@ def register_promote_function(module, name):
 
 
 # --------------------------------------------------------------------------- policy table
-_LOW, _FP32, _PROMOTE, _SEQ, _BANNED, _RNN = range(6)
+# kinds: cast to the low type / to fp32, promote to the widest type (plain and sequence forms),
+# banned (error on low-precision input), RNN kernels (low), and the in-place forms: match the
+# self tensor's type (MATCH0), or refuse a low-precision self / any low input (ERR_ARG0 /
+# ERR_ANY) because an fp32-policy op cannot run in place on a half tensor.
+_LOW, _FP32, _PROMOTE, _SEQ, _BANNED, _RNN, _MATCH0, _ERR_ARG0, _ERR_ANY = range(9)
+_LOW_TYPES = (torch.float16, torch.bfloat16)
 
 
-def _resolve(module, names):
-    out = []
-    for n in names:
-        f = getattr(module, n, None)
-        if f is not None:
-            out.append(f)
-        # in-place and torch.* aliases of the same op
-        f2 = getattr(module, n + "_", None)
-        if f2 is not None and module is not torch.nn.functional:
-            out.append(f2)
-    return out
+def _attrs(module, names):
+    return [f for f in (getattr(module, n, None) for n in names) if f is not None]
+
+
+def _inplace(names):
+    return [n + "_" for n in names if not n.startswith("__")]
 
 
 def _build_policy(patch_type, allow_banned):
+    """{callable: (kind, message)}, assembled in the same order of precedence as the reference's
+    patching passes (apex/amp/amp.py:111-192): casts, promotion, in-place rules, RNNs, banned."""
     low_attr = "BFLOAT16_FUNCS" if patch_type == torch.bfloat16 else "FP16_FUNCS"
     table = {}
+
+    def put(fns, kind, msg=None):
+        for f in fns:
+            table[f] = (kind, msg)
+
+    T, tensor = torch.Tensor, tensor_overrides
     for mod in (functional_overrides, torch_overrides, tensor_overrides):
-        for f in _resolve(mod.MODULE, getattr(mod, low_attr)):
-            table[f] = (_LOW, None)
-        for f in _resolve(mod.MODULE, mod.FP32_FUNCS):
-            table[f] = (_FP32, None)
-        for f in _resolve(mod.MODULE, getattr(mod, "CASTS", [])):
-            table[f] = (_PROMOTE, None)
-        for f in _resolve(mod.MODULE, getattr(mod, "SEQUENCE_CASTS", [])):
-            table[f] = (_SEQ, None)
-    if not allow_banned:
-        for name, msg in functional_overrides.BANNED_FUNCS:
-            f = getattr(torch.nn.functional, name, None)
-            if f is not None:
-                table[f] = (_BANNED, msg)
-            tf = getattr(torch._C._nn, name, None)
-            if tf is not None:
-                table[tf] = (_BANNED, msg)
-    # RNN kernels: cast input + flat weights to the low type
+        put(_attrs(mod.MODULE, getattr(mod, low_attr)), _LOW)
+        put(_attrs(mod.MODULE, mod.FP32_FUNCS), _FP32)
+    for mod in (torch_overrides, tensor_overrides):
+        casts = getattr(mod, "CASTS", [])
+        put(_attrs(mod.MODULE, [n for n in casts if not n.startswith("__i")]), _PROMOTE)
+        put(_attrs(mod.MODULE, getattr(mod, "SEQUENCE_CASTS", [])), _SEQ)
+    put(_attrs(torch, _inplace(torch_overrides.FP32_FUNCS)), _ERR_ANY)
+    put(_attrs(T, _inplace(tensor.FP32_FUNCS)), _ERR_ARG0)
+    inplace_match = _inplace(list(getattr(tensor, low_attr)) + list(tensor.CASTS))
+    inplace_match += [n for n in tensor.CASTS if n.startswith("__i")]
+    put(_attrs(T, inplace_match), _MATCH0)
     for n in ("lstm", "gru", "rnn_tanh", "rnn_relu", "lstm_cell", "gru_cell", "rnn_tanh_cell", "rnn_relu_cell"):
-        f = getattr(torch, n, None)
-        if f is not None:
-            table[f] = (_RNN, None)
+        put(_attrs(torch, [n]), _RNN)
+    for name, msg in functional_overrides.BANNED_FUNCS:
+        fns = _attrs(torch.nn.functional, [name]) + _attrs(torch._C._nn, [name])
+        put(fns, _FP32 if allow_banned else _BANNED, msg)
     return table
+
+
+def _any_low(args, kwargs):
+    return any(t in _LOW_TYPES for t in utils.collect_fp_tensor_types(args, kwargs))
 
 
 class _AmpCastMode(TorchFunctionMode):
@@ -157,9 +164,24 @@ class _AmpCastMode(TorchFunctionMode):
         if ent is None or not self.handle.is_active():
             return func(*args, **kwargs)
         kind, msg = ent
-        if kind == _BANNED:
-            raise NotImplementedError(msg)
         name = getattr(func, "__name__", str(func))
+        if kind == _BANNED:
+            if _any_low(args, kwargs):
+                raise NotImplementedError(msg)
+            return func(*args, **kwargs)
+        if kind in (_ERR_ANY, _ERR_ARG0):
+            bad = _any_low(args, kwargs) if kind == _ERR_ANY else (
+                len(args) > 0 and utils.is_fp_tensor(args[0]) and args[0].dtype in _LOW_TYPES)
+            if bad:
+                raise NotImplementedError("amp: in-place {} on a {} tensor is not supported under O1 (the op runs "
+                                          "in fp32)".format(name, "low-precision"))
+            return func(*args, **kwargs)
+        if kind == _MATCH0:
+            if len(args) > 0 and utils.is_fp_tensor(args[0]):
+                target = args[0].dtype
+                a, k = utils.casted_args(lambda x: x.to(target) if utils.is_fp_tensor(x) else x, args[1:], kwargs)
+                return func(args[0], *a, **k)
+            return func(*args, **kwargs)
         if kind in (_LOW, _RNN):
             cast = utils.verbosify(self.low, name, self.verbose)
             fn = functools.partial(utils.cached_cast, cast, cache=self.handle.cache) \
@@ -178,6 +200,24 @@ class _AmpCastMode(TorchFunctionMode):
                 return func(*a, **k)
             return func(*args, **kwargs)
         return func(*args, **kwargs)
+
+
+def _rnn_check_input_relaxed(orig):
+    """nn.RNNBase.check_input rejects an input whose dtype differs from the weights' unless torch
+    autocast is on; under O1 the RNN kernel call itself casts input and flat weights to the low
+    type (the _RNN policy), so the dtype part of the check is waived while the handle is active."""
+
+    @functools.wraps(orig)
+    def check_input(self, input, batch_sizes):
+        h = _DECORATOR_HANDLE
+        if h is not None and h.is_active() and input.is_floating_point():
+            w = self._flat_weights[0] if self._flat_weights else None
+            if w is not None and w.dtype != input.dtype:
+                # shape-only stand-in with the weights' dtype (an expanded 0-d tensor: no copy)
+                input = torch.empty((), dtype=w.dtype, device=input.device).expand(input.shape)
+        return orig(self, input, batch_sizes)
+
+    return check_input
 
 
 def _install_user_registries(handle, patch_type, verbose):
@@ -222,6 +262,8 @@ def init(enabled=True, loss_scale="dynamic", enable_caching=True, verbose=False,
         _uninstall()
     handle = AmpHandle(loss_scale, enable_caching, verbose)
     _install_user_registries(handle, patch_type, verbose)
+    rnn_base = torch.nn.modules.rnn.RNNBase
+    utils.set_func_save(handle, rnn_base, "check_input", _rnn_check_input_relaxed(rnn_base.check_input))
     table = _build_policy(patch_type, allow_banned)
     mode = _AmpCastMode(handle, patch_type, table, verbose)
     mode.__enter__()

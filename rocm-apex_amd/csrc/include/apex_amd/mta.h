@@ -139,6 +139,23 @@ __device__ __forceinline__ bool mta_last_block(unsigned* ticket, int* smem_flag)
 __device__ __forceinline__ void mta_put_partial(uint64_t* p, float v, unsigned tag);
 __device__ __forceinline__ void mta_collect_partials(const MtaMeta& m, int num_acc, unsigned tag);
 
+// The last-arriving block of a reduction launch: either the real finalize over the collected
+// partials, or (the skip flag is set: this step is skipped anyway) the op's skipped result.
+// Both reset the ticket and advance the epoch, so the next launch's partials carry a fresh tag.
+template <typename Op>
+__device__ __forceinline__ void mta_finish(const MtaMeta& meta, const Op& op, unsigned tag, bool skipped) {
+  if (skipped) {
+    op.finalize_skipped(meta);
+  } else {
+    mta_collect_partials(meta, Op::kNumAcc, tag);
+    op.finalize(meta, tag);
+  }
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(meta.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(meta.epoch, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // Ops with kNumAcc > 0 accumulate per-element sums (or maxima when Op::kAccMax) which are
 // reduced per chunk into meta.partials; the last block then calls op.finalize(meta, smem).
 template <typename Op, typename... Ts>
@@ -147,14 +164,18 @@ __global__ void __launch_bounds__(kMtaBlock) mta_elementwise_kernel(MtaMeta meta
   constexpr int NA = Op::kNumAcc;
   __shared__ float smem[kMtaBlock / 64 * 2 + 2];
   if constexpr (Op::kSkipOnNoop) {
-    // uniform early exit; a reduction op still has to take part in the ticket protocol
-    if (*reinterpret_cast<volatile int*>(noop) != 0) {
+    // uniform early exit; a reduction op still has to take part in the ticket protocol.  The
+    // flag can also be raised DURING this launch (kCheckPartial ops set it on a non-finite
+    // chunk), so a skipping block still publishes tagged (zero) partials for its chunks: a
+    // finalizer that did not skip then never waits on a slot nobody writes.
+    if (__hip_atomic_load(noop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
       if constexpr (NA == 0) return;
       else {
-        if (mta_last_block(meta.ticket, reinterpret_cast<int*>(&smem[kMtaBlock / 64 * 2]))) {
-          op.finalize_skipped(meta);
-          if (threadIdx.x == 0) __hip_atomic_store(meta.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        const unsigned tag = __hip_atomic_load(meta.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+        for (int w = blockIdx.x; w < meta.nchunks; w += gridDim.x)
+          if (threadIdx.x < NA) mta_put_partial(meta.partials + (size_t)threadIdx.x * meta.nchunks + w, 0.f, tag);
+        if (mta_last_block(meta.ticket, reinterpret_cast<int*>(&smem[kMtaBlock / 64 * 2])))
+          mta_finish(meta, op, tag, true);
         return;
       }
     }
@@ -222,15 +243,15 @@ __global__ void __launch_bounds__(kMtaBlock) mta_elementwise_kernel(MtaMeta meta
       }
     }
   }
-  if (bad) *noop = 1;  // benign race: every writer stores the same value
+  // benign race (every writer stores the same value); an agent-scope (write-through) store so
+  // the finalizing block's agent-scope re-read below sees it on any XCD
+  if (bad) __hip_atomic_store(noop, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if constexpr (NA > 0) {
     if (mta_last_block(meta.ticket, reinterpret_cast<int*>(&smem[kMtaBlock / 64 * 2]))) {
-      mta_collect_partials(meta, NA, tag);
-      op.finalize(meta, tag);
-      if (threadIdx.x == 0) {
-        __hip_atomic_store(meta.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(meta.epoch, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      bool skipped = false;
+      if constexpr (Op::kSkipOnNoop)
+        skipped = __hip_atomic_load(noop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+      mta_finish(meta, op, tag, skipped);
     }
   }
 }

@@ -79,11 +79,14 @@ def multi_tensor_l2norm(chunk_size, noop, tl, per_tensor=False):
 
 
 def multi_tensor_l2norm_mp(chunk_size, noop, tl, per_tensor=False):
-    """reference csrc/multi_tensor_l2norm_kernel_mp.cu (no-op when noop is set)"""
+    """reference csrc/multi_tensor_l2norm_kernel_mp.cu: a no-op when noop is set — before the
+    call, or by a non-finite value found during it (the step is skipped; norms read as 0)."""
+    dev = tl[0][0].device
+    skipped = (torch.zeros(1, device=dev), torch.zeros(len(tl[0]) if per_tensor else 0, device=dev))
     if int(noop.reshape(-1)[0]) != 0:
-        dev = tl[0][0].device
-        return torch.zeros(1, device=dev), torch.zeros(len(tl[0]) if per_tensor else 0, device=dev)
-    return multi_tensor_l2norm(chunk_size, noop, tl, per_tensor)
+        return skipped
+    total, per = multi_tensor_l2norm(chunk_size, noop, tl, per_tensor)
+    return skipped if int(noop.reshape(-1)[0]) != 0 else (total, per)
 
 
 def multi_tensor_maxnorm(chunk_size, noop, tl, per_tensor=False):

@@ -52,8 +52,9 @@ def test_o1_cast_lists(low):
         assert a.dtype == torch.float32  # promote
         c = torch.cat([torch.randn(2, dtype=low), torch.randn(2)])
         assert c.dtype == torch.float32  # sequence promote
-        with pytest.raises(NotImplementedError):
-            F.binary_cross_entropy(torch.rand(4), torch.rand(4))
+        with pytest.raises(NotImplementedError):  # banned on low-precision input ...
+            F.binary_cross_entropy(torch.rand(4, dtype=low), torch.rand(4, dtype=low))
+        assert F.binary_cross_entropy(torch.rand(4), torch.rand(4)).dtype == torch.float32  # ... fp32 runs
         with amp.disable_casts():
             assert lin(torch.randn(2, 16)).dtype == torch.float32
     finally:

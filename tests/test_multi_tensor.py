@@ -191,3 +191,36 @@ def test_update_scale_device():
             ref.amp_update_scale_(o_g.cpu(), s_c, st_c, 2.0, 0.5, 2000, 0.0, 2.0 ** 24, dynamic)
             torch.testing.assert_close(st_g.cpu(), st_c)
             assert s_g.item() == s_c.item()
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_l2norm_mp_inf_in_early_chunk_many_chunks(device):
+    """multi_tensor_l2norm_mp (skip-on-noop reduction) with far more chunks than blocks and an inf
+    in the first chunk: blocks that start after the flag is raised skip their chunks, the
+    launch still terminates promptly, reports the skipped result (norm 0, flag set), and the
+    next clean launch over the same table gets the exact norm (fresh partial tags)."""
+    import time
+
+    chunk = 64  # tiny chunks: ~16k chunks, many per block
+    xs = [torch.randn(1 << 20, device=device), torch.randn(3000, device=device)]
+    ref = torch.cat([x.reshape(-1) for x in xs]).norm()
+    noop = _noop(device)
+    total, _ = amp_C.multi_tensor_l2norm_mp(chunk, noop, [xs], False)
+    torch.testing.assert_close(total, ref.reshape(1), rtol=1e-4, atol=1e-4)
+    for rep in range(3):
+        xs[0][1] = float("inf")
+        noop.zero_()
+        t0 = time.time()
+        total, per = amp_C.multi_tensor_l2norm_mp(chunk, noop, [xs], True)
+        if device == "cuda":
+            torch.cuda.synchronize()
+        assert time.time() - t0 < 5.0, "finalizer waited on partials nobody wrote"
+        assert int(noop.item()) == 1
+        assert float(total) == 0.0 and torch.count_nonzero(per) == 0
+        xs[0][1] = 0.5
+        noop.zero_()
+        total, per = amp_C.multi_tensor_l2norm_mp(chunk, noop, [xs], True)
+        exp = torch.cat([x.reshape(-1) for x in xs]).norm()
+        torch.testing.assert_close(total, exp.reshape(1), rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(per, torch.stack([x.norm() for x in xs]), rtol=1e-4, atol=1e-4)
+        assert int(noop.item()) == 0
