@@ -116,6 +116,107 @@ class _BnNHWCFunction(torch.autograd.Function):
         return dx, dz, gw, gb, None, None, None, None, None, None, None, None
 
 
+class _BnDualAddReluFunction(torch.autograd.Function):
+    """y = relu(bn_x(x) + bn_z(z)) for a residual block whose shortcut is conv -> BN: statistics of
+    both inputs, then ONE output pass (``fwd_train_dual``) — the shortcut's normalized tensor is
+    never materialized.  Backward: the main BN's reduction writes the ReLU-masked gradient (read
+    from the forward's bit mask), which is at once the shortcut BN's incoming gradient."""
+
+    @staticmethod
+    def forward(ctx, x, z, w, b, rm, rv, wz, bz, rmz, rvz, momentum, eps, momentum_z, eps_z, torch_channels_last,
+                fork=False):
+        ctx.set_materialize_grads(False)
+        x2 = _to_2d(x, torch_channels_last)
+        z2 = _to_2d(z, torch_channels_last)
+        y2, sm, si, coef, smz, siz, coefz, mask = _ext().fwd_train_dual(
+            x2, z2, w, b, rm, rv, float(momentum), float(eps), wz, bz, rmz, rvz, float(momentum_z), float(eps_z), True)
+        ctx.save_for_backward(x2, z2, w, sm, si, coef, wz, smz, siz, coefz, mask)
+        ctx.layout = (torch_channels_last, x.shape)
+        y = _from_2d(y2, x, torch_channels_last)
+        if fork:
+            return y, y.view_as(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, grad_y, grad_y2=None):
+        x2, z2, w, sm, si, coef, wz, smz, siz, coefz, mask = ctx.saved_tensors
+        if grad_y is None:
+            grad_y, grad_y2 = grad_y2, None
+        if grad_y is None:
+            return (None,) * 16
+        tcl, shape = ctx.layout
+        g2 = _to_2d(grad_y, tcl)
+        gg2 = _to_2d(grad_y2, tcl) if grad_y2 is not None else None
+        ext = _ext()
+        dx2, dym, gw, gb = ext.bwd(g2, x2, None, w, sm, si, coef, True, True, gg2, mask)
+        dz2, _, gwz, gbz = ext.bwd(dym, z2, None, wz, smz, siz, coefz, False, False)
+        like = torch.empty(shape, device="meta")
+        return (_from_2d(dx2, like, tcl), _from_2d(dz2, like, tcl), gw, gb, None, None, gwz, gbz, None, None, None,
+                None, None, None, None, None)
+
+
+def bn_add_bn_relu(x, z, bn_x, bn_z, fork=False):
+    """``relu(bn_x(x) + bn_z(z))`` — the output of a downsampling residual block — as one fused
+    output pass when both are single-rank training-mode BatchNorm2d_NHWC on the native path;
+    otherwise the two modules in sequence (bn_z first, its output as bn_x's residual input)."""
+    ok = (bn_x.training and bn_z.training and bn_x.fuse_relu and not bn_z.fuse_relu and bn_x.bn_group == 1
+          and bn_z.bn_group == 1 and bn_x.torch_channels_last and bn_z.torch_channels_last
+          and x.dim() == 4 and z.shape == x.shape and z.dtype == x.dtype and _native.use_native(x)
+          and x.size(1) % 8 == 0 and bn_x.weight is not None and bn_z.weight is not None
+          and bn_x.weight.dtype == torch.float32 and bn_z.weight.dtype == torch.float32
+          and bn_x.track_running_stats and bn_z.track_running_stats)
+    if not ok:
+        return bn_x(x, bn_z(z), fork=fork)
+    return _BnDualAddReluFunction.apply(x, z, bn_x.weight, bn_x.bias, bn_x.running_mean, bn_x.running_var,
+                                        bn_z.weight, bn_z.bias, bn_z.running_mean, bn_z.running_var, bn_x.momentum,
+                                        bn_x.eps, bn_z.momentum, bn_z.eps, True, fork)
+
+
+class _BnReluMaxPoolFunction(torch.autograd.Function):
+    """maxpool(relu(bn(x))) for the ResNet stem: BN statistics, then ONE pass that normalizes,
+    applies the ReLU and pools (``fwd_train_relu_maxpool``), so the full-resolution activation is
+    only read once and never written.  Backward: the NHWC pool's gather backward (1-byte window
+    indices) gives the gradient of the BN+ReLU output, then the fused BN backward with the ReLU
+    mask recomputed from x."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, rm, rv, momentum, eps, k, st, pad):
+        y, idx, sm, si, coef = _ext().fwd_train_relu_maxpool(x, w, b, rm, rv, float(momentum), float(eps), list(k),
+                                                             list(st), list(pad))
+        ctx.save_for_backward(x, w, sm, si, coef, idx)
+        ctx.pool = (k, st, pad)
+        ctx.mark_non_differentiable(idx)
+        return y
+
+    @staticmethod
+    def backward(ctx, gp):
+        x, w, sm, si, coef, idx = ctx.saved_tensors
+        k, st, pad = ctx.pool
+        gy = _native.require("maxpool_nhwc").maxpool_nhwc.backward(gp, idx, x, list(k), list(st), list(pad))
+        dx2, _, gw, gb = _ext().bwd(_to_2d(gy, True), _to_2d(x, True), None, w, sm, si, coef, True, False)
+        like = torch.empty(x.shape, device="meta")
+        return _from_2d(dx2, like, True), gw, gb, None, None, None, None, None, None, None
+
+
+def bn_relu_maxpool(x, bn, pool):
+    """``pool(bn(x))`` for a ReLU-fused training-mode ``BatchNorm2d_NHWC`` followed by a max pool
+    (the ResNet stem) in one fused pass on the native path; otherwise the two modules in turn."""
+    def _pair(v):
+        return (v, v) if isinstance(v, int) else tuple(v)
+
+    k, st, pad = _pair(pool.kernel_size), _pair(pool.stride if pool.stride is not None else pool.kernel_size), \
+        _pair(pool.padding)
+    ok = (bn.training and bn.fuse_relu and bn.bn_group == 1 and bn.torch_channels_last and x.dim() == 4
+          and x.is_contiguous(memory_format=torch.channels_last) and _native.use_native(x) and x.size(1) % 8 == 0
+          and bn.weight is not None and bn.weight.dtype == torch.float32 and bn.track_running_stats
+          and getattr(pool, "dilation", 1) in (1, (1, 1)) and not getattr(pool, "ceil_mode", False)
+          and not getattr(pool, "return_indices", False) and _native.submodule("maxpool_nhwc") is not None)
+    if not ok:
+        return pool(bn(x))
+    return _BnReluMaxPoolFunction.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps,
+                                        k, st, pad)
+
+
 def _exchange_gather(payload, group):
     """[world, n] fp32: every group member's ``payload`` (peer memory, else RCCL / gloo)."""
     import torch.distributed as dist

@@ -55,6 +55,77 @@ std::vector<at::Tensor> fwd_train(at::Tensor x, OT z, OT w, OT b, OT running_mea
   return {y, save_mean, save_invstd, coef, mask};
 }
 
+// y = relu(bn(x) + bn_z(z)): a residual block whose shortcut is itself conv -> BN (downsampling
+// blocks).  Statistics of both inputs, then ONE apply pass for the pair.
+std::vector<at::Tensor> fwd_train_dual(at::Tensor x, at::Tensor z, OT w, OT b, OT running_mean, OT running_var,
+                                       double momentum, double eps, OT wz, OT bz, OT running_mean_z,
+                                       OT running_var_z, double momentum_z, double eps_z, bool want_mask) {
+  check2d(x, "input");
+  check2d(z, "z");
+  TORCH_CHECK(z.sizes() == x.sizes() && z.scalar_type() == x.scalar_type(), "bn_nhwc dual: z must match input");
+  const c10::hip::HIPGuard g(x.get_device());
+  const int64_t m = x.size(0);
+  const int c = (int)x.size(1);
+  for (const OT* p : {&w, &b, &running_mean, &running_var, &wz, &bz, &running_mean_z, &running_var_z})
+    check_param(*p, c);
+  const int cus = device_cus(x.get_device());
+  int64_t wsf = 0;
+  const int gy = bn_nhwc_plan(m, c, cus, &wsf);
+  auto fo = x.options().dtype(at::kFloat);
+  auto ws = at::empty({wsf}, fo);
+  auto sm = at::empty({c}, fo), si = at::empty({c}, fo), coef = at::empty({2, c}, fo);
+  auto smz = at::empty({c}, fo), siz = at::empty({c}, fo), coefz = at::empty({2, c}, fo);
+  const int dt = dtype_code(x.scalar_type());
+  bn_nhwc_stats(x.data_ptr(), dt, m, c, fptr(w), fptr(b), (float)eps, (float)momentum, fptr_mut(running_mean),
+                fptr_mut(running_var), sm.data_ptr<float>(), si.data_ptr<float>(), coef.data_ptr<float>(),
+                ws.data_ptr<float>(), gy, cus, cur_stream());
+  bn_nhwc_stats(z.data_ptr(), dt, m, c, fptr(wz), fptr(bz), (float)eps_z, (float)momentum_z, fptr_mut(running_mean_z),
+                fptr_mut(running_var_z), smz.data_ptr<float>(), siz.data_ptr<float>(), coefz.data_ptr<float>(),
+                ws.data_ptr<float>(), gy, cus, cur_stream());
+  at::Tensor mask;
+  if (want_mask) mask = at::empty({m * c / 8}, x.options().dtype(at::kByte));
+  auto y = at::empty_like(x);
+  bn_nhwc_apply_dual(x.data_ptr(), z.data_ptr(), dt, coef.data_ptr<float>(), coefz.data_ptr<float>(), y.data_ptr(),
+                     m, c, cus, cur_stream(), want_mask ? mask.data_ptr<uint8_t>() : nullptr);
+  return {y, sm, si, coef, smz, siz, coefz, mask};
+}
+
+// stem: training BN statistics of x [N, C, H, W] (channels_last), then relu(bn(x)) max-pooled in
+// the same pass that normalizes; returns (pooled [N, C, OH, OW] channels_last, 1-byte argmax
+// indices, save_mean, save_invstd, coef)
+std::vector<at::Tensor> fwd_train_relu_maxpool(at::Tensor x4, OT w, OT b, OT running_mean, OT running_var,
+                                               double momentum, double eps, std::vector<int64_t> k,
+                                               std::vector<int64_t> st, std::vector<int64_t> pad) {
+  TORCH_CHECK(x4.is_cuda() && x4.dim() == 4 && x4.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "bn_nhwc apply+pool: channels_last 4-D GPU input expected");
+  TORCH_CHECK(k.size() == 2 && st.size() == 2 && pad.size() == 2, "bn_nhwc apply+pool: 2-D window expected");
+  const c10::hip::HIPGuard g(x4.get_device());
+  const int n = (int)x4.size(0), c = (int)x4.size(1), h = (int)x4.size(2), wd = (int)x4.size(3);
+  at::Tensor x = x4.permute({0, 2, 3, 1}).reshape({-1, c});
+  check2d(x, "input");
+  for (const OT* p : {&w, &b, &running_mean, &running_var}) check_param(*p, c);
+  const int64_t m = x.size(0);
+  const int cus = device_cus(x.get_device());
+  int64_t wsf = 0;
+  const int gy = bn_nhwc_plan(m, c, cus, &wsf);
+  auto fo = x.options().dtype(at::kFloat);
+  auto ws = at::empty({wsf}, fo);
+  auto sm = at::empty({c}, fo), si = at::empty({c}, fo), coef = at::empty({2, c}, fo);
+  const int dt = dtype_code(x.scalar_type());
+  bn_nhwc_stats(x.data_ptr(), dt, m, c, fptr(w), fptr(b), (float)eps, (float)momentum, fptr_mut(running_mean),
+                fptr_mut(running_var), sm.data_ptr<float>(), si.data_ptr<float>(), coef.data_ptr<float>(),
+                ws.data_ptr<float>(), gy, cus, cur_stream());
+  const int oh = (h + 2 * (int)pad[0] - (int)k[0]) / (int)st[0] + 1;
+  const int ow = (wd + 2 * (int)pad[1] - (int)k[1]) / (int)st[1] + 1;
+  auto opts = x4.options().memory_format(at::MemoryFormat::ChannelsLast);
+  auto y = at::empty({n, c, oh, ow}, opts);
+  auto idx = at::empty({n, c, oh, ow}, opts.dtype(at::kByte));
+  bn_nhwc_apply_relu_maxpool(x.data_ptr(), dt, coef.data_ptr<float>(), n, h, wd, c, (int)k[0], (int)k[1], (int)st[0],
+                             (int)st[1], (int)pad[0], (int)pad[1], oh, ow, y.data_ptr(), idx.data_ptr<uint8_t>(), cus,
+                             cur_stream());
+  return {y, idx, sm, si, coef};
+}
+
 at::Tensor fwd_eval(at::Tensor x, OT z, OT w, OT b, at::Tensor running_mean, at::Tensor running_var, double eps,
                     bool relu) {
   check2d(x, "input");
@@ -252,6 +323,8 @@ void bind_bn_nhwc(pybind11::module_& root) {
         pybind11::arg("running_mean"), pybind11::arg("running_var"), pybind11::arg("momentum"), pybind11::arg("eps"),
         pybind11::arg("relu"), pybind11::arg("want_mask") = false);
   m.def("fwd_eval", &fwd_eval);
+  m.def("fwd_train_dual", &fwd_train_dual);
+  m.def("fwd_train_relu_maxpool", &fwd_train_relu_maxpool);
   m.def("bwd", &bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("z"), pybind11::arg("w"),
         pybind11::arg("save_mean"), pybind11::arg("save_invstd"), pybind11::arg("coef_fwd"), pybind11::arg("relu"),
         pybind11::arg("need_dz"), pybind11::arg("dy2") = c10::nullopt, pybind11::arg("mask") = c10::nullopt);

@@ -99,7 +99,10 @@ at::Tensor linear_wgrad(const at::Tensor& dy2, const at::Tensor& x2) {
 
 }  // namespace
 
+void bind_lt(pybind11::module_& root);  // lt_epilogue.cpp
+
 void bind_gemm(pybind11::module_& root) {
+  bind_lt(root);
   namespace py = pybind11;
   auto g = root.def_submodule("gemm", "gfx950 MFMA GEMM with fused epilogues");
   g.attr("EPI_NONE") = (int)kEpiNone;

@@ -1,0 +1,240 @@
+// hipBLASLt GEMMs with fused epilogues for the dense layers (library route of fused_dense / mlp).
+//
+// Capability of the reference's cuBLASLt paths (csrc/fused_dense_cuda.cu:220 gemm_bias_lt, :471
+// gemm_bias_gelu_lt (GELU_AUX_BIAS), :843 gemm_bgradb_lt (BGRADB), :977 gemm_dgelu_bgradb_lt
+// (DGELU_BGRAD)) — which the reference compiles out on ROCm (:1290) — on gfx950's hipBLASLt:
+//   linear        y = x W^T (+ b) [GeLU, with the pre-activation written as aux]   one launch
+//   dgelu_bgrad   dz = (g W2) * gelu'(aux),  db = sum_rows dz                     one launch
+//   wgrad_bgrad   dW = g^T x,                db = sum_rows g                      one launch
+// so the library route of FusedDense / FusedDenseGeluDense has no separate GeLU, GeLU-backward
+// or bias-gradient kernels.  Row-major tensors are handed to the column-major library as their
+// transposes (no copies).  Every (shape, epilogue) asks the heuristic once and caches the algo;
+// a shape the library has no kernel for reports "unsupported" and the Python side falls back.
+#include "common.h"
+
+#include <hipblaslt/hipblaslt.h>
+
+#include <mutex>
+#include <tuple>
+#include <unordered_map>
+
+namespace apex_amd {
+
+namespace {
+
+#define LT_CHECK(expr, what)                                                              \
+  do {                                                                                    \
+    hipblasStatus_t st_ = (expr);                                                         \
+    TORCH_CHECK(st_ == HIPBLAS_STATUS_SUCCESS, "hipBLASLt ", what, " failed (status ", (int)st_, ")"); \
+  } while (0)
+
+constexpr size_t kWorkspace = 32ull << 20;
+
+hipblasLtHandle_t lt_handle(int dev) {
+  static hipblasLtHandle_t handles[64] = {nullptr};
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lock(mu);
+  if (!handles[dev]) LT_CHECK(hipblasLtCreate(&handles[dev]), "create");
+  return handles[dev];
+}
+
+hipDataType lt_type(at::ScalarType t) {
+  if (t == at::kBFloat16) return HIP_R_16BF;
+  if (t == at::kHalf) return HIP_R_16F;
+  TORCH_CHECK(false, "hipBLASLt epilogue GEMM: bf16 / fp16 only");
+  return HIP_R_16BF;
+}
+
+// col-major problem: D[m x n] = op(A) op(B), A stored (ta ? k x m : m x k), B (tb ? n x k : k x n)
+struct Problem {
+  int64_t m, n, k, lda, ldb, ldd;
+  bool ta, tb;
+  hipDataType type;
+  hipblasLtEpilogue_t epi;
+  int dev;
+  bool operator==(const Problem& o) const {
+    return std::tie(m, n, k, lda, ldb, ldd, ta, tb, type, epi, dev) ==
+           std::tie(o.m, o.n, o.k, o.lda, o.ldb, o.ldd, o.ta, o.tb, o.type, o.epi, o.dev);
+  }
+};
+
+struct ProblemHash {
+  size_t operator()(const Problem& p) const {
+    size_t h = std::hash<int64_t>()(p.m) * 1000003u ^ std::hash<int64_t>()(p.n) * 10007u ^ std::hash<int64_t>()(p.k);
+    h ^= ((size_t)p.ta << 1) ^ ((size_t)p.tb << 2) ^ ((size_t)p.epi << 4) ^ ((size_t)p.type << 20) ^ ((size_t)p.dev << 28);
+    return h ^ std::hash<int64_t>()(p.lda * 31 + p.ldb * 17 + p.ldd);
+  }
+};
+
+struct Plan {
+  bool ok = false;
+  hipblasLtMatmulAlgo_t algo;
+};
+
+struct Descs {
+  hipblasLtMatmulDesc_t op = nullptr;
+  hipblasLtMatrixLayout_t a = nullptr, b = nullptr, d = nullptr;
+  ~Descs() {
+    if (a) hipblasLtMatrixLayoutDestroy(a);
+    if (b) hipblasLtMatrixLayoutDestroy(b);
+    if (d) hipblasLtMatrixLayoutDestroy(d);
+    if (op) hipblasLtMatmulDescDestroy(op);
+  }
+};
+
+void make_descs(const Problem& p, Descs& ds, const void* bias, hipDataType bias_t, void* aux, int64_t aux_ld) {
+  LT_CHECK(hipblasLtMatmulDescCreate(&ds.op, HIPBLAS_COMPUTE_32F, HIP_R_32F), "desc");
+  const int32_t ta = p.ta ? HIPBLAS_OP_T : HIPBLAS_OP_N, tb = p.tb ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(ds.op, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)), "transa");
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(ds.op, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)), "transb");
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(ds.op, HIPBLASLT_MATMUL_DESC_EPILOGUE, &p.epi, sizeof(p.epi)), "epilogue");
+  if (bias) {
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(ds.op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)), "bias");
+    const int32_t bt = bias_t;
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(ds.op, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)), "bias type");
+  }
+  if (aux) {
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(ds.op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &aux, sizeof(aux)),
+             "aux");
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(ds.op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_LD, &aux_ld, sizeof(aux_ld)),
+             "aux ld");
+  }
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&ds.a, p.type, p.ta ? p.k : p.m, p.ta ? p.m : p.k, p.lda), "layout a");
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&ds.b, p.type, p.tb ? p.n : p.k, p.tb ? p.k : p.n, p.ldb), "layout b");
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&ds.d, p.type, p.m, p.n, p.ldd), "layout d");
+}
+
+std::unordered_map<Problem, Plan, ProblemHash>& plans() {
+  static std::unordered_map<Problem, Plan, ProblemHash> m;
+  return m;
+}
+std::mutex g_plan_mu;
+
+// Runs the problem; returns false (nothing launched) when the library has no kernel for it.
+bool lt_run(const Problem& p, const void* a, const void* b, void* d, const void* bias, hipDataType bias_t, void* aux,
+            int64_t aux_ld) {
+  hipblasLtHandle_t h = lt_handle(p.dev);
+  Descs ds;
+  make_descs(p, ds, bias, bias_t, aux, aux_ld);
+  Plan plan;
+  {
+    std::lock_guard<std::mutex> lock(g_plan_mu);
+    auto it = plans().find(p);
+    if (it != plans().end()) {
+      plan = it->second;
+    } else {
+      hipblasLtMatmulPreference_t pref;
+      LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref), "preference");
+      const uint64_t ws = kWorkspace;
+      LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws, sizeof(ws)),
+               "workspace pref");
+      hipblasLtMatmulHeuristicResult_t res[1];
+      int found = 0;
+      const hipblasStatus_t st =
+          hipblasLtMatmulAlgoGetHeuristic(h, ds.op, ds.a, ds.b, ds.d, ds.d, pref, 1, res, &found);
+      hipblasLtMatmulPreferenceDestroy(pref);
+      plan.ok = st == HIPBLAS_STATUS_SUCCESS && found > 0 && res[0].state == HIPBLAS_STATUS_SUCCESS;
+      if (plan.ok) plan.algo = res[0].algo;
+      plans()[p] = plan;
+    }
+  }
+  if (!plan.ok) return false;
+  auto ws = at::empty({(int64_t)kWorkspace}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, p.dev));
+  const float alpha = 1.f, beta = 0.f;
+  LT_CHECK(hipblasLtMatmul(h, ds.op, &alpha, a, ds.a, b, ds.b, &beta, d, ds.d, d, ds.d, &plan.algo, ws.data_ptr(),
+                           kWorkspace, cur_stream()),
+           "matmul");
+  return true;
+}
+
+void check2d(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.is_contiguous(), "hipBLASLt epilogue GEMM: ", what,
+              " must be a contiguous 2-D GPU tensor");
+}
+
+// y[M, N] = x[M, K] W[N, K]^T (+ b)  [GeLU]; returns (y, aux or undefined) or an empty list when
+// unsupported.  epilogue: 0 none, 1 bias, 2 bias + GeLU with aux (pre-activation), 3 bias + GeLU
+std::vector<at::Tensor> lt_linear(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> bias, int64_t epilogue) {
+  check2d(x, "x");
+  check2d(w, "weight");
+  const c10::hip::HIPGuard guard(x.get_device());
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && w.scalar_type() == x.scalar_type(), "lt_linear: weight mismatch");
+  const bool hb = bias.has_value() && bias->defined();
+  TORCH_CHECK(epilogue == 0 || hb, "lt_linear: this epilogue needs a bias");
+  at::Tensor b = hb ? bias->contiguous() : at::Tensor();
+  if (hb) TORCH_CHECK(b.numel() == N && b.scalar_type() == x.scalar_type(), "lt_linear: bias mismatch");
+  auto y = at::empty({M, N}, x.options());
+  at::Tensor aux;
+  hipblasLtEpilogue_t epi = HIPBLASLT_EPILOGUE_DEFAULT;
+  if (epilogue == 1) epi = HIPBLASLT_EPILOGUE_BIAS;
+  if (epilogue == 2) {
+    epi = HIPBLASLT_EPILOGUE_GELU_AUX_BIAS;
+    aux = at::empty({M, N}, x.options());
+  }
+  if (epilogue == 3) epi = HIPBLASLT_EPILOGUE_GELU_BIAS;
+  // col-major: y^T[N x M] = W^T... as stored: A = W (col-major K x N, transposed), B = x (K x M)
+  Problem p{N, M, K, K, K, N, true, false, lt_type(x.scalar_type()), epi, x.get_device()};
+  if (!lt_run(p, w.data_ptr(), x.data_ptr(), y.data_ptr(), hb ? b.data_ptr() : nullptr, p.type,
+              aux.defined() ? aux.data_ptr() : nullptr, N))
+    return {};
+  if (aux.defined()) return {y, aux};
+  return {y};
+}
+
+// dz[M, N1] = (g[M, N2] W2[N2, N1]) * gelu'(aux[M, N1]);  db[N1] = column sums of dz
+std::vector<at::Tensor> lt_dgelu_bgrad(at::Tensor g, at::Tensor w2, at::Tensor aux) {
+  check2d(g, "grad");
+  check2d(w2, "weight");
+  check2d(aux, "aux");
+  const c10::hip::HIPGuard guard(g.get_device());
+  const int64_t M = g.size(0), N2 = g.size(1), N1 = w2.size(1);
+  TORCH_CHECK(w2.size(0) == N2 && aux.size(0) == M && aux.size(1) == N1, "lt_dgelu_bgrad: shape mismatch");
+  auto dz = at::empty({M, N1}, g.options());
+  auto db = at::empty({N1}, g.options());
+  // col-major: dz^T[N1 x M] = W2^T (A = W2 stored col-major N1 x N2) * g^T (B = g stored N2 x M)
+  Problem p{N1, M, N2, N1, N2, N1, false, false, lt_type(g.scalar_type()), HIPBLASLT_EPILOGUE_DGELU_BGRAD,
+            g.get_device()};
+  if (!lt_run(p, w2.data_ptr(), g.data_ptr(), dz.data_ptr(), db.data_ptr(), p.type, aux.data_ptr(), N1)) return {};
+  return {dz, db};
+}
+
+// dW[N, K] = g[M, N]^T x[M, K];  db[N] = column sums of g (BGRADB)
+std::vector<at::Tensor> lt_wgrad_bgrad(at::Tensor g, at::Tensor x, bool with_bias) {
+  check2d(g, "grad");
+  check2d(x, "input");
+  const c10::hip::HIPGuard guard(g.get_device());
+  const int64_t M = g.size(0), N = g.size(1), K = x.size(1);
+  TORCH_CHECK(x.size(0) == M && x.scalar_type() == g.scalar_type(), "lt_wgrad_bgrad: shape mismatch");
+  auto dw = at::empty({N, K}, g.options());
+  at::Tensor db = with_bias ? at::empty({N}, g.options()) : at::Tensor();
+  // col-major: dW^T[K x N] = x^T (A = x stored K x M) * g (B = g stored N x M, transposed)
+  Problem p{K, N, M, K, N, K, false, true, lt_type(g.scalar_type()),
+            with_bias ? HIPBLASLT_EPILOGUE_BGRADB : HIPBLASLT_EPILOGUE_DEFAULT, g.get_device()};
+  if (!lt_run(p, x.data_ptr(), g.data_ptr(), dw.data_ptr(), with_bias ? db.data_ptr() : nullptr, p.type, nullptr, 0))
+    return {};
+  if (with_bias) return {dw, db};
+  return {dw};
+}
+
+void lt_clear_cache() {
+  std::lock_guard<std::mutex> lock(g_plan_mu);
+  plans().clear();
+}
+
+}  // namespace
+
+void bind_lt(pybind11::module_& root) {
+  auto m = root.def_submodule("lt_gemm", "hipBLASLt GEMMs with fused bias / GeLU-aux / dGeLU-bgrad / bgradb epilogues");
+  m.def("linear", &lt_linear, pybind11::arg("x"), pybind11::arg("weight"), pybind11::arg("bias"),
+        pybind11::arg("epilogue"));
+  m.def("dgelu_bgrad", &lt_dgelu_bgrad);
+  m.def("wgrad_bgrad", &lt_wgrad_bgrad);
+  m.def("clear_cache", &lt_clear_cache);
+  m.attr("EPI_NONE") = 0;
+  m.attr("EPI_BIAS") = 1;
+  m.attr("EPI_GELU_AUX_BIAS") = 2;
+  m.attr("EPI_GELU_BIAS") = 3;
+}
+
+}  // namespace apex_amd

@@ -285,6 +285,102 @@ __global__ void __launch_bounds__(256) apply_kernel(const T* __restrict__ x, con
 }
 
 // ------------------------------------------------------------------------------------------
+// Two batch norms summed under one ReLU (a downsampling residual block's output:
+// y = relu(bn_main(x) + bn_short(z))): both normalizations in the single output pass, so the
+// shortcut branch's normalized tensor is never written or re-read.
+template <typename T, bool MASKOUT>
+__global__ void __launch_bounds__(256) apply_dual_kernel(const T* __restrict__ x, const T* __restrict__ z,
+                                                         const float* __restrict__ cx, const float* __restrict__ cz,
+                                                         T* __restrict__ y, int64_t nvec, int c,
+                                                         uint8_t* __restrict__ mask) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int cstep = (int)((stride * 8) % c);
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (int c0 = (int)((i * 8) % c); i < nvec; i += stride, c0 = c0 + cstep >= c ? c0 + cstep - c : c0 + cstep) {
+    const int64_t e = i * 8;
+    float v[8], w[8], sx[8], hx[8], sz[8], hz[8];
+    Vec8<T>::load(v, x + e);
+    Vec8<T>::load(w, z + e);
+    load8f(sx, cx + c0);
+    load8f(hx, cx + c + c0);
+    load8f(sz, cz + c0);
+    load8f(hz, cz + c + c0);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = fmaxf(fmaf(v[k], sx[k], hx[k]) + fmaf(w[k], sz[k], hz[k]), 0.f);
+    Vec8<T>::store(y + e, v);
+    if constexpr (MASKOUT) {
+      unsigned b = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) b |= (v[k] > 0.f ? 1u : 0u) << k;
+      mask[i] = (uint8_t)b;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// BN apply + ReLU + max pool in one pass (the ResNet stem: conv -> BN -> ReLU -> 3x3/2 max pool):
+// every window element is normalized in registers as it is loaded, so the full-resolution
+// normalized tensor is never written nor re-read by the pool.  One lane per (n, oh, ow, 8
+// channels); 16-byte loads; 1-byte window indices as in the standalone NHWC pool
+// (csrc/pool/maxpool_nhwc.hip), so the pool backward and the BN backward are unchanged.
+struct PoolGeo {
+  int n, h, w, c, oh, ow, kh, kw, sh, sw, ph, pw;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256) apply_relu_maxpool_kernel(const T* __restrict__ x,
+                                                                 const float* __restrict__ coef, PoolGeo g,
+                                                                 T* __restrict__ y, uint8_t* __restrict__ idx) {
+  const uint32_t cv = (uint32_t)(g.c / 8);
+  const uint32_t total = (uint32_t)g.n * g.oh * g.ow * cv;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const int c8 = (int)(i % cv) * 8;
+    uint32_t r = i / cv;
+    const int ow = (int)(r % (uint32_t)g.ow);
+    r /= (uint32_t)g.ow;
+    const int oh = (int)(r % (uint32_t)g.oh);
+    const int n = (int)(r / (uint32_t)g.oh);
+    float sc[8], sh[8], best[8];
+    uint8_t bi[8];
+    load8f(sc, coef + c8);
+    load8f(sh, coef + g.c + c8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      best[e] = -INFINITY;
+      bi[e] = 0;
+    }
+    const int h0 = oh * g.sh - g.ph, w0 = ow * g.sw - g.pw;
+    for (int a = 0; a < g.kh; ++a) {
+      const int ih = h0 + a;
+      if (ih < 0 || ih >= g.h) continue;
+      for (int b = 0; b < g.kw; ++b) {
+        const int iw = w0 + b;
+        if (iw < 0 || iw >= g.w) continue;
+        float v[8];
+        Vec8<T>::load(v, x + (((int64_t)n * g.h + ih) * g.w + iw) * g.c + c8);
+        const uint8_t k = (uint8_t)(a * g.kw + b);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          // normalized + ReLU value, rounded to the storage type exactly as the unfused apply
+          // pass would store it, so argmax ties resolve identically
+          const float o = to_f(from_f<T>(fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f)));
+          if (o > best[e] || (o != o && best[e] == best[e])) {
+            best[e] = o;
+            bi[e] = k;
+          }
+        }
+      }
+    }
+    const int64_t o = (((int64_t)n * g.oh + oh) * g.ow + ow) * g.c + c8;
+    Vec8<T>::store(y + o, best);
+    uint2 w;
+    w.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    w.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    *reinterpret_cast<uint2*>(idx + o) = w;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // DY2: the output fed two consumers (a residual block's main and shortcut branches) and its
 // gradient arrives as two tensors, summed here in registers instead of by a separate add pass
 // BITS: the ReLU mask comes from the forward's bit mask instead of a recompute from x (and z)
@@ -556,6 +652,42 @@ void bn_nhwc_apply(const void* x, int x_t, const void* z, const float* coef_fwd,
     }
   }, "bn_nhwc apply");
   check_launch("bn_nhwc_apply");
+}
+
+void bn_nhwc_apply_relu_maxpool(const void* x, int x_t, const float* coef_fwd, int n, int h, int w, int c, int kh,
+                                int kw, int sh, int sw, int ph, int pw, int oh, int ow, void* y, uint8_t* idx, int cus,
+                                hipStream_t s) {
+  if (c % 8 || c <= 0) throw std::runtime_error("bn_nhwc apply+pool: C must be a positive multiple of 8");
+  if (kh * kw > 255 || kh <= 0 || kw <= 0) throw std::runtime_error("bn_nhwc apply+pool: bad window");
+  const int64_t total = (int64_t)n * oh * ow * (c / 8);
+  int64_t grid = (total + 255) / 256;
+  if (grid > (int64_t)cus * 16) grid = (int64_t)cus * 16;
+  if (grid < 1) grid = 1;
+  if (total + grid * 256 >= (int64_t)UINT32_MAX) throw std::runtime_error("bn_nhwc apply+pool: tensor too large");
+  const bnh::PoolGeo g{n, h, w, c, oh, ow, kh, kw, sh, sw, ph, pw};
+  dispatch_float(x_t, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    hipLaunchKernelGGL((bnh::apply_relu_maxpool_kernel<T>), dim3((unsigned)grid), dim3(256), 0, s, (const T*)x,
+                       coef_fwd, g, (T*)y, idx);
+  }, "bn_nhwc apply+pool");
+  check_launch("bn_nhwc_apply_relu_maxpool");
+}
+
+void bn_nhwc_apply_dual(const void* x, const void* z, int x_t, const float* coef_x, const float* coef_z, void* y,
+                        int64_t m, int c, int cus, hipStream_t s, uint8_t* mask_out) {
+  bnh::check_shape(m, c);
+  const int64_t nvec = m * c / 8;
+  const unsigned grid = bnh::ew_grid(nvec, cus);
+  dispatch_float(x_t, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    if (mask_out)
+      hipLaunchKernelGGL((bnh::apply_dual_kernel<T, true>), dim3(grid), dim3(256), 0, s, (const T*)x, (const T*)z,
+                         coef_x, coef_z, (T*)y, nvec, c, mask_out);
+    else
+      hipLaunchKernelGGL((bnh::apply_dual_kernel<T, false>), dim3(grid), dim3(256), 0, s, (const T*)x, (const T*)z,
+                         coef_x, coef_z, (T*)y, nvec, c, nullptr);
+  }, "bn_nhwc apply dual");
+  check_launch("bn_nhwc_apply_dual");
 }
 
 void bn_nhwc_bwd_reduce(const void* dy, const void* x, int x_t, const void* z, const float* coef_fwd, bool relu,

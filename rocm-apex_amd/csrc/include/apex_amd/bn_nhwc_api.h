@@ -36,6 +36,17 @@ void bn_nhwc_coef_from_stats(const float* mean, const float* var_or_invstd, bool
 void bn_nhwc_apply(const void* x, int x_t, const void* z, const float* coef_fwd, bool relu, void* y, int64_t m, int c,
                    int cus, hipStream_t s, uint8_t* mask_out = nullptr);
 
+// y = relu(x * coef_x + z * coef_z) — two batch norms (coef_* = {scale, shift}[2][C]) summed under
+// one ReLU in a single pass; optional ReLU bit mask as in bn_nhwc_apply
+void bn_nhwc_apply_dual(const void* x, const void* z, int x_t, const float* coef_x, const float* coef_z, void* y,
+                        int64_t m, int c, int cus, hipStream_t s, uint8_t* mask_out = nullptr);
+
+// pooled = maxpool(relu(x * coef)) over an [n, h, w, c] NHWC tensor, plus the 1-byte window
+// argmax per output element (the layout of csrc/pool/maxpool_nhwc.hip, so its backward applies)
+void bn_nhwc_apply_relu_maxpool(const void* x, int x_t, const float* coef_fwd, int n, int h, int w, int c, int kh,
+                                int kw, int sh, int sw, int ph, int pw, int oh, int ow, void* y, uint8_t* idx, int cus,
+                                hipStream_t s);
+
 // backward reduction: grad_w / grad_b (fp32) and coef_bwd; optionally writes the ReLU-masked dy
 // (needed as grad_z for the add+relu variant); dy2 (optional, relu + dy_masked_out only) is a
 // second gradient of the same output, summed into dy in registers

@@ -12,12 +12,21 @@ Runs the native path for fp16/bf16 GPU tensors with K, N multiples of 8; otherwi
 odd sizes) the same math in torch.  GeLU is the tanh approximation (the cuBLASLt GELU epilogue
 the reference targets).
 
-Per-shape routing: on the GPU, the first forward and the first backward of every distinct
-(op, shape, dtype) time the native kernels against the library path (hipBLASLt through
-``torch.addmm`` / ``matmul``) on the live tensors and keep the faster one
-(``route_table()`` lists the decisions).  ``APEX_AMD_DENSE_ROUTE=native|library|auto``
-(default auto) pins the choice; ``profiles/gemm_waves_ab_r02.md`` has the per-shape numbers.
-No timing happens under hipGraph capture (native path)."""
+Routing (static, identical on every rank and every run; ``APEX_AMD_DENSE_ROUTE``):
+
+* ``lt`` (default): hipBLASLt with the fused epilogues of ``csrc/bindings/lt_epilogue.cpp`` —
+  forward GEMM+bias / GEMM+bias+GeLU writing the pre-activation aux in ONE launch, backward
+  dGeLU+bias-grad and weight-grad+bias-grad epilogues (the reference's cuBLASLt
+  GELU_AUX_BIAS / DGELU_BGRAD / BGRADB, csrc/fused_dense_cuda.cu:220,471,843,977).  At the
+  GPT-2 / BERT MLP shapes hipBLASLt's main loop is ahead of the native MFMA kernel
+  (profiles/gemm8p_shapes_ab_r02.jsonl), so the epilogue fusion rides on the faster GEMM; a shape
+  the library has no kernel for falls back to the unfused torch ops;
+* ``native``: every GEMM on the gfx950 MFMA kernels (``csrc/gemm/gemm_mfma.hip``) with their
+  own fused epilogues;
+* ``library``: plain torch ops (addmm + GeLU + sum) — the A/B baseline;
+* ``auto``: opt-in per-shape timing of native vs lt on the live tensors (first call of each shape;
+  the decision may differ between ranks, so it is never the default).
+``route_table()`` lists the decisions taken so far."""
 import os
 
 import torch
@@ -60,7 +69,14 @@ _ROUTES = {}
 
 
 def route_mode():
-    return os.environ.get("APEX_AMD_DENSE_ROUTE", "auto")
+    return os.environ.get("APEX_AMD_DENSE_ROUTE", "lt")
+
+
+def _lt():
+    """hipBLASLt epilogue GEMMs (None when the route is not lt / the extension lacks them)."""
+    if route_mode() not in ("lt", "auto"):
+        return None
+    return _native.submodule("lt_gemm")
 
 
 def route_table():
@@ -81,12 +97,11 @@ def _time_ms(fn, reps=5):
 
 
 def _use_native(key, native_fn, library_fn):
-    """Measured per-shape choice between the native kernels and the library GEMMs."""
+    """Static route, or (APEX_AMD_DENSE_ROUTE=auto only) a measured per-shape choice."""
     mode = route_mode()
-    if mode == "native":
-        return True
-    if mode == "library":
-        return False
+    if mode != "auto":
+        _ROUTES.setdefault(key, mode == "native")
+        return mode == "native"
     hit = _ROUTES.get(key)
     if hit is not None:
         return hit
@@ -100,14 +115,30 @@ def _use_native(key, native_fn, library_fn):
 
 def _lib_dense_fwd(x, w, b):
     x2 = x.reshape(-1, x.shape[-1])
+    lt = _lt()
+    if lt is not None and x2.is_cuda and x2.is_contiguous():
+        r = lt.linear(x2, w.contiguous(), b, lt.EPI_BIAS if b is not None else lt.EPI_NONE)
+        if r:
+            return r[0].view(x.shape[:-1] + (w.shape[0],))
     out = torch.addmm(b, x2, w.t()) if b is not None else x2.matmul(w.t())
     return out.view(x.shape[:-1] + (w.shape[0],))
+
+
+def _lib_wgrad(g2, x2, has_bias):
+    """(dW, db): one hipBLASLt launch with the BGRADB epilogue, else matmul + column sum."""
+    lt = _lt()
+    if lt is not None and g2.is_cuda:
+        r = lt.wgrad_bgrad(g2.contiguous(), x2.contiguous(), has_bias)
+        if r:
+            return r[0], (r[1] if has_bias else None)
+    return g2.t().matmul(x2), (g2.sum(0) if has_bias else None)
 
 
 def _lib_dense_bwd(x, w, gy, has_bias):
     g2 = gy.reshape(-1, gy.shape[-1])
     x2 = x.reshape(-1, x.shape[-1])
-    return g2.matmul(w).view(x.shape), g2.t().matmul(x2), (g2.sum(0) if has_bias else None)
+    dw, db = _lib_wgrad(g2, x2, has_bias)
+    return g2.matmul(w).view(x.shape), dw, db
 
 
 def _shape_key(op, x, w):
@@ -154,6 +185,14 @@ class DenseNoBiasFunc(torch.autograd.Function):
 
 def _lib_gelu_dense_fwd(x, w1, b1, w2, b2):
     x2 = x.reshape(-1, x.shape[-1])
+    lt = _lt()
+    if lt is not None and x2.is_cuda and x2.is_contiguous():
+        r1 = lt.linear(x2, w1.contiguous(), b1, lt.EPI_GELU_AUX_BIAS)
+        if r1:
+            out1, gelu_in = r1
+            r2 = lt.linear(out1, w2.contiguous(), b2, lt.EPI_BIAS)
+            out2 = r2[0] if r2 else torch.addmm(b2, out1, w2.t())
+            return out1, out2.view(x.shape[:-1] + (w2.shape[0],)), gelu_in
     gelu_in = torch.addmm(b1, x2, w1.t())
     out1 = _gelu_tanh(gelu_in)
     out2 = torch.addmm(b2, out1, w2.t())
@@ -198,14 +237,20 @@ class FusedDenseGeluDenseFunc(torch.autograd.Function):
     def _lib_backward(input, weight1, weight2, gelu_in, output1, grad_output):
         g2 = grad_output.reshape(-1, grad_output.shape[-1])
         h = output1.reshape(-1, output1.shape[-1])
-        dw2 = g2.t().matmul(h)
-        db2 = g2.sum(0)
-        z = gelu_in.reshape(-1, gelu_in.shape[-1]).detach().requires_grad_(True)
-        with torch.enable_grad():
-            gz = torch.autograd.grad(_gelu_tanh(z), z, g2.matmul(weight2))[0]
         x2 = input.reshape(-1, input.shape[-1])
-        dw1 = gz.t().matmul(x2)
-        db1 = gz.sum(0)
+        dw2, db2 = _lib_wgrad(g2, h, True)
+        lt = _lt()
+        r = None
+        if lt is not None and g2.is_cuda:
+            r = lt.dgelu_bgrad(g2.contiguous(), weight2.contiguous(), gelu_in.reshape(h.shape).contiguous())
+        if r:
+            gz, db1 = r  # dGeLU and the bias gradient in the dgrad GEMM's epilogue
+            dw1, _ = _lib_wgrad(gz, x2, False)
+        else:
+            z = gelu_in.reshape(h.shape).detach().requires_grad_(True)
+            with torch.enable_grad():
+                gz = torch.autograd.grad(_gelu_tanh(z), z, g2.matmul(weight2))[0]
+            dw1, db1 = _lib_wgrad(gz, x2, True)
         dx = gz.matmul(weight1).view(input.shape)
         return dx, dw1, db1, dw2, db2
 

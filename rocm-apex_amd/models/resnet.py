@@ -45,6 +45,12 @@ def conv1x1(cin, cout, stride=1, native=False):
     return nn.Conv2d(cin, cout, kernel_size=1, stride=stride, bias=False)
 
 
+def _bn_add_bn_relu(x, z, bn_x, bn_z, fork):
+    from ..contrib.groupbn import bn_add_bn_relu
+
+    return bn_add_bn_relu(x, z, bn_x, bn_z, fork=fork)
+
+
 def _fused_bn(planes, relu, bn_group=1):
     from ..contrib.groupbn import BatchNorm2d_NHWC
 
@@ -71,9 +77,11 @@ class BasicBlock(nn.Module):
     def forward(self, x):
         if self.fused_bn:
             xm, xr = x if isinstance(x, tuple) else (x, x)
-            identity = xr if self.downsample is None else self.downsample(xr)
+            zds = None if self.downsample is None else self.downsample[0](xr)
             out = self.bn1(self.conv1(xm))
-            return self.bn2(self.conv2(out), identity, fork=self.fork_out)
+            if zds is not None:
+                return _bn_add_bn_relu(self.conv2(out), zds, self.bn2, self.downsample[1], self.fork_out)
+            return self.bn2(self.conv2(out), xr, fork=self.fork_out)
         identity = x if self.downsample is None else self.downsample(x)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.bn2(self.conv2(out))
@@ -104,10 +112,15 @@ class Bottleneck(nn.Module):
     def forward(self, x):
         if self.fused_bn:
             xm, xr = x if isinstance(x, tuple) else (x, x)
-            identity = xr if self.downsample is None else self.downsample(xr)
+            # downsampling block: the shortcut's conv output goes straight into the fused
+            # relu(bn3(.) + bn_ds(.)) pass (contrib.groupbn.bn_add_bn_relu) — its normalized
+            # tensor is never written
+            zds = None if self.downsample is None else self.downsample[0](xr)
             out = self.bn1(self.conv1(xm))
             out = self.bn2(self.conv2(out))
-            return self.bn3(self.conv3(out), identity, fork=self.fork_out)
+            if zds is not None:
+                return _bn_add_bn_relu(self.conv3(out), zds, self.bn3, self.downsample[1], self.fork_out)
+            return self.bn3(self.conv3(out), xr, fork=self.fork_out)
         identity = x if self.downsample is None else self.downsample(x)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.relu(self.bn2(self.conv2(out)))
@@ -177,7 +190,10 @@ class ResNet(nn.Module):
 
     def forward(self, x):
         if self.fused_bn:
-            x = self.maxpool(self.bn1(self.conv1(x)))
+            # stem: BN statistics, then normalize + ReLU + 3x3/2 max pool in one pass
+            from ..contrib.groupbn import bn_relu_maxpool
+
+            x = bn_relu_maxpool(self.conv1(x), self.bn1, self.maxpool)
         else:
             x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))

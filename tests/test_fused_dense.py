@@ -98,7 +98,7 @@ def test_gpu_gemm_epilogues(dtype):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("route", ["native", "auto"])
+@pytest.mark.parametrize("route", ["native", "lt", "library", "auto"])
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 def test_gpu_fused_dense_reference_test(dtype, route, monkeypatch):
     """The reference's test shapes: 3 x 512 tokens, 1024 -> 3072 (dx, dw, db all checked), on the
@@ -127,7 +127,7 @@ def test_gpu_fused_dense_reference_test(dtype, route, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("route", ["native", "auto"])
+@pytest.mark.parametrize("route", ["native", "lt", "library", "auto"])
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 def test_gpu_fused_dense_gelu_dense(dtype, route, monkeypatch):
     monkeypatch.setenv("APEX_AMD_DENSE_ROUTE", route)
@@ -308,3 +308,50 @@ def test_gpu_gemm8p_race_screen(m, n, k, monkeypatch):
     for _ in range(30):
         c, _ = g.matmul(a, True, b, True, m, n, k)
         assert torch.equal(c, first)
+
+
+# ------------------------------------------------------------------ hipBLASLt epilogue GEMMs
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("m,k,n", [(16384, 1024, 4096), (1000, 512, 2048), (3 * 512, 1024, 3072)])
+def test_gpu_lt_epilogues_vs_fp32(m, k, n, dtype):
+    """Each hipBLASLt epilogue GEMM (csrc/bindings/lt_epilogue.cpp) against fp32 torch math, and
+    the library really has a fused kernel for the GPT-2 / BERT MLP shapes (a non-empty result:
+    no silent fall back to the unfused ops)."""
+    from apex import _native
+
+    lt = _native.submodule("lt_gemm")
+    assert lt is not None, "lt_gemm not built"
+    torch.manual_seed(0)
+    x = (torch.randn(m, k, device="cuda") * 0.5).to(dtype)
+    w = (torch.randn(n, k, device="cuda") / k ** 0.5).to(dtype)
+    b = (torch.randn(n, device="cuda") * 0.1).to(dtype)
+    pre = x.float() @ w.float().t() + b.float()
+
+    def close(got, ref, tol=2e-2):
+        s = max(1.0, float(ref.abs().max()))
+        torch.testing.assert_close(got.float() / s, ref / s, atol=tol, rtol=tol)
+
+    r = lt.linear(x, w, b, lt.EPI_BIAS)
+    assert len(r) == 1
+    close(r[0], pre)
+    r = lt.linear(x, w, None, lt.EPI_NONE)
+    close(r[0], x.float() @ w.float().t())
+    r = lt.linear(x, w, b, lt.EPI_GELU_AUX_BIAS)
+    assert len(r) == 2, "no hipBLASLt GELU_AUX_BIAS kernel for this shape"
+    close(r[1], pre)
+    close(r[0], torch.nn.functional.gelu(pre, approximate="tanh"))
+    # backward epilogues: dz = (g W2) * gelu'(aux), db = colsum(dz);  dW = g^T x, db = colsum(g)
+    n2 = 1024
+    w2 = (torch.randn(n2, n, device="cuda") / n ** 0.5).to(dtype)
+    g = (torch.randn(m, n2, device="cuda") * 0.1).to(dtype)
+    z = r[1].float().requires_grad_(True)
+    gz = torch.autograd.grad(torch.nn.functional.gelu(z, approximate="tanh"), z, g.float() @ w2.float())[0]
+    rr = lt.dgelu_bgrad(g, w2, r[1])
+    assert len(rr) == 2, "no hipBLASLt DGELU_BGRAD kernel for this shape"
+    close(rr[0], gz)
+    close(rr[1], gz.sum(0), tol=3e-2)
+    rw = lt.wgrad_bgrad(g, x, True)
+    assert len(rw) == 2, "no hipBLASLt BGRADB kernel for this shape"
+    close(rw[0], g.float().t() @ x.float())
+    close(rw[1], g.float().sum(0), tol=3e-2)

@@ -210,3 +210,105 @@ def test_gpu_bn_relu_bitmask_matches_recompute(two_grads):
     got = ext.bwd(dy, x, None, w, sm, si, coef, True, True, dy2, mask)
     for a, r in zip(got, ref):
         assert torch.equal(a, r)
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("fork", [False, True])
+def test_bn_add_bn_relu_matches_two_torch_bns(device, fork):
+    """relu(bn_x(x) + bn_z(z)) — the downsampling block output — through contrib.groupbn.bn_add_bn_relu
+    (one fused output pass on the GPU) against two torch BatchNorm2d in fp32: outputs, input
+    gradients (two incoming gradients when forked), parameter gradients and running statistics."""
+    from apex.contrib.groupbn import bn_add_bn_relu
+    from apex.contrib.groupbn import batch_norm as bnm
+
+    torch.manual_seed(1)
+    C = 64
+    dt = torch.bfloat16 if device == "cuda" else torch.float32
+    x = (torch.randn(4, C, 7, 7, device=device) * 2 + 0.5).to(dt).to(memory_format=torch.channels_last)
+    z = (torch.randn(4, C, 7, 7, device=device) - 0.3).to(dt).to(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    z.requires_grad_(True)
+    bx = BatchNorm2d_NHWC(C, fuse_relu=True, torch_channels_last=True).to(device)
+    bz = BatchNorm2d_NHWC(C, fuse_relu=False, torch_channels_last=True).to(device)
+    rx, rz = torch.nn.BatchNorm2d(C).to(device), torch.nn.BatchNorm2d(C).to(device)
+    with torch.no_grad():
+        for m, r, s in ((bx, rx, 0.7), (bz, rz, 1.3)):
+            m.weight.copy_(torch.linspace(0.5, 1.5, C) * s)
+            m.bias.copy_(torch.linspace(-0.2, 0.3, C) * s)
+            r.weight.copy_(m.weight)
+            r.bias.copy_(m.bias)
+    calls = {"n": 0}
+    orig = bnm._BnDualAddReluFunction.forward
+
+    def counting(*a, **k):
+        calls["n"] += 1
+        return orig(*a, **k)
+
+    bnm._BnDualAddReluFunction.forward = staticmethod(counting)
+    try:
+        out = bn_add_bn_relu(x, z, bx, bz, fork=fork)
+    finally:
+        bnm._BnDualAddReluFunction.forward = staticmethod(orig)
+    assert calls["n"] == (1 if device == "cuda" else 0)
+    g1 = torch.randn(4, C, 7, 7, device=device)
+    g2 = torch.randn(4, C, 7, 7, device=device)
+    if fork:
+        y, y2 = out
+        ((y.float() * g1).sum() + (y2.float() * g2).sum()).backward()
+    else:
+        y = out
+        (y.float() * g1).sum().backward()
+    xr = x.detach().float().requires_grad_(True)
+    zr = z.detach().float().requires_grad_(True)
+    yr = torch.relu(rx(xr) + rz(zr))
+    ((yr * g1).sum() + ((yr * g2).sum() if fork else 0)).backward()
+    tol = 3e-2 if dt == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    for got, ref in ((x.grad, xr.grad), (z.grad, zr.grad)):
+        s = max(1.0, float(ref.abs().max()))
+        torch.testing.assert_close(got.float() / s, ref / s, atol=tol, rtol=tol)
+    for m, r in ((bx, rx), (bz, rz)):
+        torch.testing.assert_close(m.running_mean, r.running_mean, atol=1e-3, rtol=1e-3)
+        torch.testing.assert_close(m.running_var, r.running_var, atol=1e-3, rtol=1e-3)
+        s = max(1.0, float(r.weight.grad.abs().max()))
+        torch.testing.assert_close(m.weight.grad / s, r.weight.grad / s, atol=tol, rtol=tol)
+        torch.testing.assert_close(m.bias.grad / s, r.bias.grad / s, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_bn_relu_maxpool_matches_torch(device):
+    """maxpool(relu(bn(x))) — the ResNet stem — through contrib.groupbn.bn_relu_maxpool (one fused
+    normalize+ReLU+pool pass on the GPU) against torch BatchNorm2d + ReLU + MaxPool2d in fp32."""
+    from apex.contrib.groupbn import bn_relu_maxpool
+    from apex.ops.pooling import MaxPool2dNHWC
+
+    torch.manual_seed(3)
+    C = 64
+    dt = torch.bfloat16 if device == "cuda" else torch.float32
+    x = (torch.randn(2, C, 29, 31, device=device) * 1.5 + 0.2).to(dt).to(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    bn = BatchNorm2d_NHWC(C, fuse_relu=True, torch_channels_last=True).to(device)
+    ref = torch.nn.BatchNorm2d(C).to(device)
+    with torch.no_grad():
+        bn.weight.copy_(torch.linspace(0.5, 1.5, C))
+        bn.bias.copy_(torch.linspace(-0.3, 0.3, C))
+        ref.weight.copy_(bn.weight)
+        ref.bias.copy_(bn.bias)
+    pool = MaxPool2dNHWC(kernel_size=3, stride=2, padding=1)
+    y = bn_relu_maxpool(x, bn, pool)
+    xr = x.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.max_pool2d(torch.relu(ref(xr)), 3, 2, 1)
+    tol = 3e-2 if dt == torch.bfloat16 else 1e-5
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    g = torch.randn_like(yr)
+    (y.float() * g).sum().backward()
+    (yr * g).sum().backward()
+    s = max(1.0, float(xr.grad.abs().max()))
+    # bf16 ties inside a window can pick another equal element: compare the gradient mass
+    torch.testing.assert_close(x.grad.float().sum((0, 2, 3)) / s, xr.grad.sum((0, 2, 3)) / s, atol=tol, rtol=tol)
+    if dt == torch.float32:
+        torch.testing.assert_close(x.grad, xr.grad, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, atol=1e-3, rtol=1e-3)
+    torch.testing.assert_close(bn.running_var, ref.running_var, atol=1e-3, rtol=1e-3)
+    sw = max(1.0, float(ref.weight.grad.abs().max()))
+    torch.testing.assert_close(bn.weight.grad / sw, ref.weight.grad / sw, atol=tol, rtol=tol)

@@ -41,7 +41,7 @@ EXTENSIONS = {
     "norm": ("norm.cpp", ("norm",)),
     "softmax": ("softmax.cpp", ("softmax",)),
     "syncbn": ("syncbn.cpp", ("syncbn",)),
-    "gemm": ("gemm.cpp", ("gemm",)),
+    "gemm": ("gemm.cpp", ("gemm",)),  # + lt_epilogue.cpp (hipBLASLt epilogue GEMMs)
     "xentropy": ("xentropy.cpp", ("xentropy",)),
     "attn": ("attn.cpp", ("attn",)),
     "bn_nhwc": ("bn_nhwc.cpp", ("groupbn",)),
@@ -143,7 +143,8 @@ def compile_cmds(verbose: bool, extensions=None, out=None, build_dir=BUILD, defi
     link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", output_path(out),
             *[obj_for(s, build_dir) for s, _ in jobs],
             f"-L{os.path.join(tdir, 'lib')}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
-            "-ltorch_python", "-lamdhip64", f"-Wl,-rpath,{os.path.join(tdir, 'lib')}"]
+            "-ltorch_python", "-lamdhip64", "-L/opt/rocm/lib", "-lhipblaslt", "-Wl,-rpath,/opt/rocm/lib",
+            f"-Wl,-rpath,{os.path.join(tdir, 'lib')}"]
     return jobs, link
 
 
