@@ -221,9 +221,9 @@ def timed(args, step, dev, world, rank, distributed, B, impl, desc=None):
         step()
         if rank == 0 and (time.time() - t0) > 30 and i % 4 == 0:
             print(f"[bench] warmup step {i + 1}/{args.warmup}", file=sys.stderr, flush=True)
-    # the headline ResNet step only (the stock-torch baseline stays eager; the transformer
-    # benches draw dropout seeds on the host)
-    use_graph = (args.graph and impl == "apex" and desc is None and not distributed
+    # --graph: apex steps only (the stock-torch baseline stays eager); the transformer steps are
+    # capturable because their dropout kernels take the device RNG step (apex.ops.dropout_rng)
+    use_graph = (args.graph and impl == "apex" and not distributed
                  and os.environ.get("APEX_BENCH_GRAPH", "1") != "0")
     args.graph = use_graph
     if use_graph:
@@ -262,7 +262,8 @@ def timed(args, step, dev, world, rank, distributed, B, impl, desc=None):
     value = world * B * args.steps / elapsed
     if rank == 0 and desc is not None:
         value = world * desc["items_per_gpu_step"] * args.steps / elapsed
-        cfg = dict(desc["config"], final_loss=round(float(loss.item()), 4))
+        cfg = dict(desc["config"], final_loss=round(float(loss.item()), 4),
+                   timing="hipgraph-replay" if getattr(args, "graph", False) else "eager")
         res = {"metric": desc["metric"], "value": round(value, 2), "unit": desc["unit"], "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,

@@ -77,6 +77,11 @@ __host__ __device__ inline uint32_t seed_mix_of(uint64_t seed, uint64_t offset) 
   return x;
 }
 
+// host offset + the device RNG step (graph-safe dropout, AttnArgs::rng_step)
+__device__ __forceinline__ uint64_t drop_offset(const AttnArgs& a) {
+  return a.offset + (a.rng_step ? ((uint64_t)(*a.rng_step) << 32) : 0ull);
+}
+
 // v_exp_f32 directly (inputs here are <= 0 or -inf; no denormal range reduction needed)
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
@@ -235,7 +240,7 @@ __global__ void __launch_bounds__(256, (fwd_occupancy<D, MODE, QF, LO>())) fwd_k
     const bool dropout = MODE >= 1 && a.p_drop > 0.f;  // MODE 0: no dropout (compiled out)
     const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
     const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
-    const uint32_t smix = seed_mix_of(a.seed, a.offset);
+    const uint32_t smix = seed_mix_of(a.seed, drop_offset(a));
     const uint32_t bh = (uint32_t)(b * a.h + hq);
     const float* biasb = (MODE == 2 && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh : nullptr;
 
@@ -456,7 +461,7 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
   const bool dropout = !PLAIN && a.p_drop > 0.f;  // PLAIN: no bias, no dropout (compiled out)
   const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
   const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
-  const uint32_t smix = seed_mix_of(a.seed, a.offset);
+  const uint32_t smix = seed_mix_of(a.seed, drop_offset(a));
   const int group = a.h / a.h_k;
   // dQ tile ownership: d-tile dtq, key part kpart of kparts (NDT * kparts == 4 waves)
   constexpr int KPARTS = 4 / NDT, KPL = BK / KPARTS;
@@ -675,7 +680,7 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
     const bool dropout = MODE >= 1 && a.p_drop > 0.f;  // MODE 0: no dropout (compiled out)
     const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
     const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
-    const uint32_t smix = seed_mix_of(a.seed, a.offset);
+    const uint32_t smix = seed_mix_of(a.seed, drop_offset(a));
     const int group = a.h / a.h_k;
     constexpr int QCH = QB * CPR, QCPT = (QCH + 255) / 256;
 
@@ -906,7 +911,7 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dq_kernel(const A
     const bool dropout = MODE >= 1 && a.p_drop > 0.f;  // MODE 0: no dropout (compiled out)
     const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
     const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
-    const uint32_t smix = seed_mix_of(a.seed, a.offset);
+    const uint32_t smix = seed_mix_of(a.seed, drop_offset(a));
     const uint32_t bh = (uint32_t)(b * a.h + hq);
     const float* biasp = (MODE == 2 && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh + (int64_t)myq * a.bias_sq
                                 : nullptr;

@@ -41,7 +41,7 @@ struct Common {
 
 void fill_common(Common& c, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const OT& cu_q,
                  const OT& cu_k, int64_t max_sq, int64_t max_sk, double scale, bool causal, const OT& bias,
-                 double p_drop, int64_t seed, int64_t offset) {
+                 double p_drop, int64_t seed, int64_t offset, const OT& rng_step = c10::nullopt) {
   const bool varlen = has(cu_q);
   TORCH_CHECK(varlen == has(cu_k), "attn: cu_seqlens_q and cu_seqlens_k go together");
   TORCH_CHECK(q.scalar_type() == k.scalar_type() && q.scalar_type() == v.scalar_type(), "attn: dtype mismatch");
@@ -90,14 +90,20 @@ void fill_common(Common& c, const at::Tensor& q, const at::Tensor& k, const at::
   a.p_drop = (float)p_drop;
   a.seed = (uint64_t)seed;
   a.offset = (uint64_t)offset;
+  a.rng_step = nullptr;
+  if (has(rng_step)) {
+    TORCH_CHECK(rng_step->is_cuda() && rng_step->scalar_type() == at::kLong && rng_step->numel() >= 1,
+                "attn: rng_step must be an int64 GPU tensor");
+    a.rng_step = rng_step->data_ptr<int64_t>();
+  }
 }
 
 std::tuple<at::Tensor, at::Tensor> fwd(at::Tensor q, at::Tensor k, at::Tensor v, OT cu_q, OT cu_k, int64_t max_sq,
                                        int64_t max_sk, double scale, bool causal, OT bias, double p_drop, int64_t seed,
-                                       int64_t offset, OT out) {
+                                       int64_t offset, OT out, OT rng_step) {
   const c10::hip::HIPGuard guard(q.get_device());
   Common c;
-  fill_common(c, q, k, v, cu_q, cu_k, max_sq, max_sk, scale, causal, bias, p_drop, seed, offset);
+  fill_common(c, q, k, v, cu_q, cu_k, max_sq, max_sk, scale, causal, bias, p_drop, seed, offset, rng_step);
   at::Tensor o = has(out) ? *out : at::empty(q.sizes(), q.options());
   c.a.o = view_of(o, has(cu_q), "out");
   at::Tensor lse = at::empty({c.a.h, c.a.rows_q}, q.options().dtype(at::kFloat));
@@ -108,10 +114,11 @@ std::tuple<at::Tensor, at::Tensor> fwd(at::Tensor q, at::Tensor k, at::Tensor v,
 
 std::vector<at::Tensor> bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor out, at::Tensor lse,
                             OT cu_q, OT cu_k, int64_t max_sq, int64_t max_sk, double scale, bool causal, OT bias,
-                            double p_drop, int64_t seed, int64_t offset, OT dq_out, OT dk_out, OT dv_out) {
+                            double p_drop, int64_t seed, int64_t offset, OT dq_out, OT dk_out, OT dv_out,
+                            OT rng_step) {
   const c10::hip::HIPGuard guard(q.get_device());
   Common c;
-  fill_common(c, q, k, v, cu_q, cu_k, max_sq, max_sk, scale, causal, bias, p_drop, seed, offset);
+  fill_common(c, q, k, v, cu_q, cu_k, max_sq, max_sk, scale, causal, bias, p_drop, seed, offset, rng_step);
   const bool varlen = has(cu_q);
   AttnBwdArgs ba{};
   ba.f = c.a;
@@ -152,7 +159,7 @@ std::vector<at::Tensor> fmha_fwd(at::Tensor qkv, at::Tensor cu_seqlens, double p
   const int64_t d = qkv.size(3);
   auto q = qkv.select(1, 0), k = qkv.select(1, 1), v = qkv.select(1, 2);
   auto r = fwd(q, k, v, cu_seqlens, cu_seqlens, max_s, max_s, 1.0 / std::sqrt((double)d), false, c10::nullopt, p, seed,
-               offset, c10::nullopt);
+               offset, c10::nullopt, c10::nullopt);
   // "S_dmask" slot carries what the backward needs: lse + the dropout seed/offset
   auto meta = at::empty({2}, qkv.options().dtype(at::kLong).device(at::kCPU));
   meta[0] = seed;
@@ -167,7 +174,7 @@ std::vector<at::Tensor> fmha_bwd(at::Tensor dout, at::Tensor qkv, at::Tensor out
   auto q = qkv.select(1, 0), k = qkv.select(1, 1), v = qkv.select(1, 2);
   bwd(dout, q, k, v, out, lse, cu_seqlens, cu_seqlens, max_s, max_s, 1.0 / std::sqrt((double)d), false, c10::nullopt,
       p_dropout, meta[0].item<int64_t>(), meta[1].item<int64_t>(), dqkv.select(1, 0), dqkv.select(1, 1),
-      dqkv.select(1, 2));
+      dqkv.select(1, 2), c10::nullopt);
   return {dqkv};
 }
 
@@ -179,12 +186,13 @@ void bind_attn(pybind11::module_& root) {
   m.def("fwd", &fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("cu_seqlens_q") = c10::nullopt,
         py::arg("cu_seqlens_k") = c10::nullopt, py::arg("max_seqlen_q") = 0, py::arg("max_seqlen_k") = 0,
         py::arg("scale"), py::arg("causal") = false, py::arg("bias") = c10::nullopt, py::arg("dropout_p") = 0.0,
-        py::arg("seed") = 0, py::arg("offset") = 0, py::arg("out") = c10::nullopt);
+        py::arg("seed") = 0, py::arg("offset") = 0, py::arg("out") = c10::nullopt, py::arg("rng_step") = c10::nullopt);
   m.def("bwd", &bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("out"), py::arg("lse"),
         py::arg("cu_seqlens_q") = c10::nullopt, py::arg("cu_seqlens_k") = c10::nullopt,
         py::arg("max_seqlen_q") = 0, py::arg("max_seqlen_k") = 0, py::arg("scale"), py::arg("causal") = false,
         py::arg("bias") = c10::nullopt, py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0,
-        py::arg("dq") = c10::nullopt, py::arg("dk") = c10::nullopt, py::arg("dv") = c10::nullopt);
+        py::arg("dq") = c10::nullopt, py::arg("dk") = c10::nullopt, py::arg("dv") = c10::nullopt,
+        py::arg("rng_step") = c10::nullopt);
   m.def("supported", [](int64_t d, at::ScalarType t) {
     return (t == at::kHalf || t == at::kBFloat16) && attn_supported((int)d, dtype_code(t));
   });

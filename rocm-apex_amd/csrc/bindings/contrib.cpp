@@ -8,9 +8,9 @@
 namespace apex_amd {
 
 void bias_dropout_add_fwd(const void* x, const void* bias, const void* res, void* out, int64_t n, int h, int dtype,
-                          float p, uint64_t seed, uint64_t offset, int cus, hipStream_t s);
+                          float p, uint64_t seed, uint64_t offset, int cus, hipStream_t s, const int64_t* step);
 void bias_dropout_add_bwd(const void* g, void* dx, int64_t n, int dtype, float p, uint64_t seed, uint64_t offset, int cus,
-                          hipStream_t s);
+                          hipStream_t s, const int64_t* step);
 
 void* peer_alloc(size_t bytes, int* kind);
 void peer_free(void* p);
@@ -49,8 +49,15 @@ void pm_allgather(const at::Tensor& local, const std::vector<int64_t>& bufs, int
 }
 
 // out = residual + dropout(x + bias) with a regenerable counter-hash mask (csrc/transformer/bias_dropout_add.hip)
+const int64_t* step_ptr(const c10::optional<at::Tensor>& step) {
+  if (!step.has_value() || !step->defined()) return nullptr;
+  TORCH_CHECK(step->is_cuda() && step->scalar_type() == at::kLong && step->numel() >= 1,
+              "rng_step must be an int64 GPU tensor");
+  return step->data_ptr<int64_t>();
+}
+
 at::Tensor bda_forward(const at::Tensor& x, const c10::optional<at::Tensor>& bias, const at::Tensor& residual, double p,
-                       int64_t seed, int64_t offset) {
+                       int64_t seed, int64_t offset, const c10::optional<at::Tensor>& rng_step) {
   TORCH_CHECK(x.is_cuda() && x.sizes() == residual.sizes() && x.scalar_type() == residual.scalar_type(),
               "bias_dropout_add: x and residual must be same-shape GPU tensors");
   const c10::hip::HIPGuard guard(x.get_device());
@@ -64,16 +71,17 @@ at::Tensor bda_forward(const at::Tensor& x, const c10::optional<at::Tensor>& bia
   at::Tensor out = at::empty_like(xc);
   bias_dropout_add_fwd(xc.data_ptr(), bc.defined() ? bc.data_ptr() : nullptr, rc.data_ptr(), out.data_ptr(), xc.numel(),
                        h, dtype_code(x.scalar_type()), (float)p, (uint64_t)seed, (uint64_t)offset,
-                       device_cus(x.get_device()), cur_stream());
+                       device_cus(x.get_device()), cur_stream(), step_ptr(rng_step));
   return out;
 }
 
-at::Tensor bda_backward(const at::Tensor& g, double p, int64_t seed, int64_t offset) {
+at::Tensor bda_backward(const at::Tensor& g, double p, int64_t seed, int64_t offset,
+                        const c10::optional<at::Tensor>& rng_step) {
   const c10::hip::HIPGuard guard(g.get_device());
   at::Tensor gc = g.contiguous();
   at::Tensor dx = at::empty_like(gc);
   bias_dropout_add_bwd(gc.data_ptr(), dx.data_ptr(), gc.numel(), dtype_code(g.scalar_type()), (float)p, (uint64_t)seed,
-                       (uint64_t)offset, device_cus(g.get_device()), cur_stream());
+                       (uint64_t)offset, device_cus(g.get_device()), cur_stream(), step_ptr(rng_step));
   return dx;
 }
 
@@ -287,9 +295,9 @@ void bind_contrib(pybind11::module_& root) {
   pm.def("allgather", &pm_allgather);
   auto t = root.def_submodule("fused_transformer", "transformer block elementwise fusions (gfx950)");
   t.def("bias_dropout_add_forward", &bda_forward, pybind11::arg("x"), pybind11::arg("bias"), pybind11::arg("residual"),
-        pybind11::arg("p"), pybind11::arg("seed"), pybind11::arg("offset"));
+        pybind11::arg("p"), pybind11::arg("seed"), pybind11::arg("offset"), pybind11::arg("rng_step") = c10::nullopt);
   t.def("bias_dropout_add_backward", &bda_backward, pybind11::arg("grad"), pybind11::arg("p"), pybind11::arg("seed"),
-        pybind11::arg("offset"));
+        pybind11::arg("offset"), pybind11::arg("rng_step") = c10::nullopt);
 }
 
 }  // namespace apex_amd

@@ -32,6 +32,10 @@ struct AttnArgs {
   int64_t bias_sb, bias_sh, bias_sq, bias_sk;
   float p_drop;     // attention-probability dropout
   uint64_t seed, offset;
+  // optional device-resident RNG step (int64[1], graph-safe dropout): the effective offset is
+  // offset + (step << 32), read by the kernel, so a hipGraph replay draws fresh masks once the
+  // step counter has been advanced on the device
+  const int64_t* rng_step;
   float* lse;       // [h][rows_q] natural-log sum-exp of the scaled scores (+inf: empty row)
   int dtype;        // kF16 / kBF16
 };

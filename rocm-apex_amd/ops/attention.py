@@ -16,6 +16,7 @@ import math
 import torch
 
 from .. import _native
+from . import dropout_rng
 
 _M32 = 0xFFFFFFFF
 
@@ -118,12 +119,16 @@ class FlashAttnFunc(torch.autograd.Function):
             if b is not None:
                 while b.dim() < 4:
                     b = b.unsqueeze(0)
-            out, lse = C.attn.fwd(q, k, v, cu_q, cu_k, max_q, max_k, scale, causal, b, p, seed, offset)
+            step = dropout_rng.step_tensor(q.device) if p > 0 else None
+            out, lse = C.attn.fwd(q, k, v, cu_q, cu_k, max_q, max_k, scale, causal, b, p, seed, offset,
+                                  rng_step=step)
             ctx.save_for_backward(q, k, v, out, lse, b, cu_q, cu_k)
+            ctx.rng_step = step
         else:
             with torch.enable_grad():
                 qq, kk, vv = (t.detach().requires_grad_(t.requires_grad) for t in (q, k, v))
-                out_g, lse = _ref_attention(qq, kk, vv, scale, causal, bias, p, seed, offset, cu_q, cu_k)
+                off = dropout_rng.effective_offset(offset, q.device) if p > 0 else offset
+                out_g, lse = _ref_attention(qq, kk, vv, scale, causal, bias, p, seed, off, cu_q, cu_k)
             ctx.ref_graph = (qq, kk, vv, out_g)
             out = out_g.detach()
         ctx.native = native
@@ -137,7 +142,7 @@ class FlashAttnFunc(torch.autograd.Function):
             q, k, v, out, lse, b, cu_q, cu_k = ctx.saved_tensors
             C = _native.require("flash attention backward")
             dq, dk, dv = C.attn.bwd(dout, q, k, v, out, lse, cu_q, cu_k, max_q, max_k, scale, causal, b, p, seed,
-                                    offset)
+                                    offset, rng_step=ctx.rng_step)
         else:
             qq, kk, vv, out_g = ctx.ref_graph
             need = [t for t in (qq, kk, vv) if t.requires_grad]
@@ -194,9 +199,12 @@ class _PackedQKVSelfAttention(torch.autograd.Function):
         if bias4 is not None:
             while bias4.dim() < 4:
                 bias4 = bias4.unsqueeze(0)
-        _, lse = C.attn.fwd(q, k, v, None, None, 0, 0, scale, causal, bias4, p, seed, offset, out.permute(1, 0, 2, 3))
+        step = dropout_rng.step_tensor(mixed.device) if p > 0 else None
+        _, lse = C.attn.fwd(q, k, v, None, None, 0, 0, scale, causal, bias4, p, seed, offset, out.permute(1, 0, 2, 3),
+                            rng_step=step)
         ctx.save_for_backward(mixed, out, lse, bias4)
         ctx.meta = (scale, causal, p, seed, offset)
+        ctx.rng_step = step
         return out.view(s, b, nh * d)
 
     @staticmethod
@@ -211,7 +219,7 @@ class _PackedQKVSelfAttention(torch.autograd.Function):
         dq, dk, dv = (dmixed[..., i * d:(i + 1) * d].permute(1, 0, 2, 3) for i in range(3))
         g = dout.contiguous().view(s, b, nh, d).permute(1, 0, 2, 3)
         C.attn.bwd(g, q, k, v, out.permute(1, 0, 2, 3), lse, None, None, 0, 0, scale, causal, bias4, p, seed, offset,
-                   dq, dk, dv)
+                   dq, dk, dv, rng_step=ctx.rng_step)
         return dmixed, None, None, None, None, None, None
 
 

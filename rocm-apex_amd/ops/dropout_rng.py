@@ -1,0 +1,53 @@
+"""Graph-safe dropout randomness for the native dropout kernels (flash attention, fused
+bias-dropout-add).
+
+Those kernels regenerate their keep masks from a counter-based hash of (seed, offset); seed and
+offset come from the host (the model's seed and the Megatron counter streams,
+``tensor_parallel.get_counter_rng_streams``).  Inside a captured hipGraph the host values are
+frozen at capture time, so every replay would redraw the SAME masks.  With device RNG steps
+enabled, each launch additionally gets a pointer to a per-device int64 step counter and uses
+``offset + (step << 32)``; ``advance()`` bumps that counter ON THE DEVICE (one tiny kernel, itself
+capturable), so a graph that starts with ``advance()`` draws fresh masks on every replay while the
+forward and the backward of one step still agree (the counter only moves between steps).
+
+Eager code that never calls ``enable()`` is unaffected (no pointer is passed)."""
+import torch
+
+_ENABLED = [False]
+_STEPS = {}
+
+
+def enable(flag=True):
+    _ENABLED[0] = bool(flag)
+
+
+def enabled():
+    return _ENABLED[0]
+
+
+def step_tensor(device):
+    """The device's int64[1] step counter when device steps are enabled (else None)."""
+    if not _ENABLED[0]:
+        return None
+    device = torch.device(device)
+    if device.type != "cuda":
+        return None
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    t = _STEPS.get(key)
+    if t is None:
+        t = torch.zeros(1, dtype=torch.int64, device=torch.device("cuda", key))
+        _STEPS[key] = t
+    return t
+
+
+def advance(device=None):
+    """Next step's masks: increments the device counter in stream order (capturable)."""
+    t = step_tensor(device if device is not None else torch.device("cuda", torch.cuda.current_device()))
+    if t is not None:
+        t.add_(1)
+
+
+def effective_offset(offset, device):
+    """Host-side equivalent of the kernels' offset (reference / CPU paths; reads the counter)."""
+    t = step_tensor(device)
+    return int(offset) + ((int(t.item()) << 32) if t is not None else 0)

@@ -78,7 +78,15 @@ def build(args, dev, distributed):
             lm_loss, binary_logits = model(tokens, mask, tokentype_ids=types, lm_labels=labels)
             return lm_loss.float().mean() + torch.nn.functional.cross_entropy(binary_logits.float(), nsp)
 
+    # graph-safe dropout: the native dropout kernels read a device step counter that each step
+    # advances on the device, so a hipGraph-captured step (bench.py --graph) draws fresh masks on
+    # every replay (apex.ops.dropout_rng)
+    from apex.ops import dropout_rng
+
+    dropout_rng.enable()
+
     def step():
+        dropout_rng.advance(dev)
         loss = loss_fn()
         opt.zero_grad()
         with amp.scale_loss(loss, opt) as scaled:
