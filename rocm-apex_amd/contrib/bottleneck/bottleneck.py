@@ -63,6 +63,81 @@ def _fold(w, bn, explicit_nhwc):
     return w * s.reshape(-1, 1, 1, 1).to(w.dtype), b.reshape(-1).to(w.dtype)
 
 
+class _FusedBottleneckFn(torch.autograd.Function):
+    """The whole frozen-BN bottleneck as one autograd node on the native kernels.
+
+    Forward: one implicit-GEMM launch per stage with the scale / bias (/ residual) / ReLU epilogue.
+    Backward, stage by stage from the block output: a single ReLU-mask pass on the incoming
+    gradient (the block output's own ReLU), then per stage ONE data-gradient launch that does
+    dconv + dReLU + dscale together — the frozen-BN scale is folded into the (tiny) weight
+    (``W * s``), and the previous stage's ReLU mask is applied in the dconv epilogue from that
+    stage's saved output (the 1x1 GEMM's DReLU epilogue / the tap kernel's mask epilogue) — the
+    capability of the reference's cudnn-frontend dconv + drelu + dscale graphs
+    (apex/contrib/csrc/bottleneck/bottleneck.cpp:760, :1287-1534).  Weight gradients: MIOpen on
+    the masked gradient, post-scaled per output channel."""
+
+    @staticmethod
+    def forward(ctx, x, w1, w2, w3, wd, s1, b1, s2, b2, s3, b3, sd, bd, stride):
+        if wd is not None:
+            identity = conv_bn_act(x, wd, sd, bd, None, False, stride, (0, 0))
+        else:
+            identity = x
+        y1 = conv_bn_act(x, w1, s1, b1, None, True, stride, (0, 0))
+        y2 = conv_bn_act(y1, w2, s2, b2, None, True, 1, (1, 1))
+        out = conv_bn_act(y2, w3, s3, b3, identity, True, 1, (0, 0))
+        ctx.save_for_backward(x, w1, w2, w3, wd, s1, s2, s3, sd, y1, y2, out)
+        ctx.stride = stride
+        return out
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w1, w2, w3, wd, s1, s2, s3, sd, y1, y2, out = ctx.saved_tensors
+        stride = ctx.stride
+        from ...ops.conv import conv_tap_dgrad
+        from ... import _native
+
+        gmm = _native.require("fused bottleneck backward").gemm
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        g3 = torch.where(out > 0, gy, torch.zeros((), dtype=gy.dtype, device=gy.device))
+
+        def wgrad(g, inp, w, s, st, pad):
+            dw = torch.ops.aten.convolution_backward(g, inp, w, None, [st, st], [pad, pad], [1, 1], False, [0, 0], 1,
+                                                     [False, True, False])[1]
+            return dw * s.to(dw.dtype).view(-1, 1, 1, 1)
+
+        def scaled(w, s):
+            return (w * s.to(w.dtype).view(-1, 1, 1, 1)).contiguous(memory_format=torch.channels_last)
+
+        def dgrad_1x1(g, w, s, mask):
+            n, k, h, wdt = g.shape
+            c = w.shape[1]
+            g2 = g.permute(0, 2, 3, 1).reshape(-1, k)
+            ws = scaled(w, s).view(k, c)
+            aux = None if mask is None else mask.permute(0, 2, 3, 1).reshape(-1, c)
+            epi = gmm.EPI_NONE if mask is None else gmm.EPI_DRELU
+            return gmm.linear_dgrad(g2, ws, epi, aux).view(n, h, wdt, c).permute(0, 3, 1, 2)
+
+        dw3 = wgrad(g3, y2, w3, s3, 1, 0)
+        g2 = dgrad_1x1(g3, w3, s3, y2)                      # dconv3 + dReLU(y2) + dscale3
+        dw2 = wgrad(g2, y1, w2, s2, 1, 1)
+        g1 = conv_tap_dgrad(g2, scaled(w2, s2), y1.shape, 1, 1, mask=y1)  # dconv2 + dReLU(y1) + dscale2
+        dw1 = wgrad(g1, x, w1, s1, stride, 0)
+        if stride == 1:
+            dx = dgrad_1x1(g1, w1, s1, None)
+        else:
+            dx = conv_tap_dgrad(g1, scaled(w1, s1), x.shape, stride, 0)
+        dwd = None
+        if wd is not None:
+            dwd = wgrad(g3, x, wd, sd, stride, 0)
+            if stride == 1:
+                dx = dx + dgrad_1x1(g3, wd, sd, None)
+            else:
+                dx = dx + conv_tap_dgrad(g3, scaled(wd, sd), x.shape, stride, 0)
+        else:
+            dx = dx + g3
+        return dx, dw1, dw2, dw3, dwd, None, None, None, None, None, None, None, None, None
+
+
 class Bottleneck(nn.Module):
     def __init__(self, in_channels, bottleneck_channels, out_channels, stride=1, groups=1, dilation=1,
                  norm_func=None, use_cudnn=False, explicit_nhwc=False):
@@ -134,11 +209,42 @@ class Bottleneck(nn.Module):
             y = y + residual
         return F.relu(y) if relu else y
 
+    def _weights(self):
+        ws = [c.weight.permute(0, 3, 1, 2) if self.explicit_nhwc else c.weight
+              for c in (self.conv1, self.conv2, self.conv3)]
+        wd = None
+        if self.downsample is not None:
+            wd = self.downsample[0].weight
+            wd = wd.permute(0, 3, 1, 2) if self.explicit_nhwc else wd
+        return ws, wd
+
+    def _single_node_ok(self, x):
+        """One fused autograd node (native forward stages + dconv/dReLU/dscale backward launches)
+        for the whole block: every stage on the native kernels, no spatial halo."""
+        if not self.use_native or getattr(self, "spatial_group_size", 1) > 1:
+            return False
+        (w1, w2, w3), wd = self._weights()
+        ws = (w1, w2, w3) + ((wd,) if wd is not None else ())
+        return (conv_bn_act_supported(x, w1) and (wd is None or conv_bn_act_supported(x, wd))
+                and all(t.dtype == x.dtype and t.is_contiguous(memory_format=torch.channels_last) for t in ws)
+                and all(t.shape[0] % 64 == 0 and t.shape[1] % 64 == 0 for t in ws))
+
     # ---- fused path: conv -> frozen-BN scale/bias -> (+ residual) -> ReLU per stage ----
     def _forward_fused(self, x):
         nhwc = self.explicit_nhwc
         if nhwc:
             x = x.permute(0, 3, 1, 2)  # [N, H, W, C] -> channels_last NCHW view
+        if self._single_node_ok(x) and torch.is_grad_enabled():
+            (w1, w2, w3), wd = self._weights()
+            sb = [bn.get_scale_bias(False) for bn in (self.bn1, self.bn2, self.bn3)]
+            sb = [(s.reshape(-1).float().contiguous(), b.reshape(-1).float().contiguous()) for s, b in sb]
+            sd = bd = None
+            if wd is not None:
+                s_, b_ = self.downsample[1].get_scale_bias(False)
+                sd, bd = s_.reshape(-1).float().contiguous(), b_.reshape(-1).float().contiguous()
+            out = _FusedBottleneckFn.apply(x, w1, w2, w3, wd, sb[0][0], sb[0][1], sb[1][0], sb[1][1], sb[2][0],
+                                           sb[2][1], sd, bd, self.stride)
+            return out.permute(0, 2, 3, 1) if nhwc else out
         if self.downsample is not None:
             identity = self._stage(x, self.downsample[0], self.downsample[1], relu=False, stride=self.stride)
         else:

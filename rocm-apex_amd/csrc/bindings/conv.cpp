@@ -58,7 +58,8 @@ ConvTapArgs make_args(const at::Tensor& in, const at::Tensor& w, const at::Tenso
 void tap_fprop(const at::Tensor& in, const at::Tensor& w, at::Tensor& out, int64_t oh, int64_t ow, int64_t ish,
                int64_t isw, int64_t osh, int64_t osw, int64_t oph, int64_t opw, std::vector<int64_t> dh,
                std::vector<int64_t> dw, const c10::optional<at::Tensor>& scale,
-               const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& residual, bool relu) {
+               const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& residual, bool relu,
+               const c10::optional<at::Tensor>& mask) {
   ConvTapArgs a = make_args(in, w, out, oh, ow, ish, isw, osh, osw, oph, opw, dh, dw);
   auto per_channel = [&](const c10::optional<at::Tensor>& t, const char* what) -> const float* {
     if (!t.has_value()) return nullptr;
@@ -76,6 +77,13 @@ void tap_fprop(const at::Tensor& in, const at::Tensor& w, at::Tensor& out, int64
     a.residual = residual->data_ptr();
   }
   a.relu = relu ? 1 : 0;
+  if (mask.has_value()) {
+    check_nhwc(*mask, "mask");
+    TORCH_CHECK(mask->sizes() == out.sizes() && mask->strides() == out.strides() &&
+                    mask->scalar_type() == out.scalar_type(),
+                "conv tap_fprop: mask must match the output's shape, layout and dtype");
+    a.mask = mask->data_ptr();
+  }
   const c10::hip::HIPGuard g(in.get_device());
   TORCH_CHECK(conv_tap_supported(a), "conv tap_fprop: unsupported (C and K must be multiples of 64, bf16/fp16)");
   conv_tap_fprop(a, device_cus(in.get_device()), cur_stream());
@@ -109,7 +117,8 @@ void bind_conv(pybind11::module_& root) {
         pybind11::arg("oh"), pybind11::arg("ow"), pybind11::arg("ish"), pybind11::arg("isw"), pybind11::arg("osh"),
         pybind11::arg("osw"), pybind11::arg("oph"), pybind11::arg("opw"), pybind11::arg("dh"), pybind11::arg("dw"),
         pybind11::arg("scale") = pybind11::none(), pybind11::arg("bias") = pybind11::none(),
-        pybind11::arg("residual") = pybind11::none(), pybind11::arg("relu") = false);
+        pybind11::arg("residual") = pybind11::none(), pybind11::arg("relu") = false,
+        pybind11::arg("mask") = pybind11::none());
   m.def("wgrad", &wgrad);
   m.def("force_fprop_cfg", &conv_force_fprop_cfg);
 }

@@ -182,8 +182,10 @@ std::vector<at::Tensor> lt_linear(at::Tensor x, at::Tensor w, c10::optional<at::
   return {y};
 }
 
-// dz[M, N1] = (g[M, N2] W2[N2, N1]) * gelu'(aux[M, N1]);  db[N1] = column sums of dz
-std::vector<at::Tensor> lt_dgelu_bgrad(at::Tensor g, at::Tensor w2, at::Tensor aux) {
+// dz[M, N1] = (g[M, N2] W2[N2, N1]) * gelu'(aux[M, N1]);  db[N1] = column sums of dz (DGELU_BGRAD),
+// or dz alone (DGELU: the bias gradient then rides on the next wgrad GEMM's BGRADB epilogue —
+// gfx950's bf16 kernels have DGELU at the transformer MLP shapes but DGELU_BGRAD only at a few)
+std::vector<at::Tensor> lt_dgelu_bgrad(at::Tensor g, at::Tensor w2, at::Tensor aux, bool with_bgrad) {
   check2d(g, "grad");
   check2d(w2, "weight");
   check2d(aux, "aux");
@@ -191,12 +193,15 @@ std::vector<at::Tensor> lt_dgelu_bgrad(at::Tensor g, at::Tensor w2, at::Tensor a
   const int64_t M = g.size(0), N2 = g.size(1), N1 = w2.size(1);
   TORCH_CHECK(w2.size(0) == N2 && aux.size(0) == M && aux.size(1) == N1, "lt_dgelu_bgrad: shape mismatch");
   auto dz = at::empty({M, N1}, g.options());
-  auto db = at::empty({N1}, g.options());
+  at::Tensor db = with_bgrad ? at::empty({N1}, g.options()) : at::Tensor();
   // col-major: dz^T[N1 x M] = W2^T (A = W2 stored col-major N1 x N2) * g^T (B = g stored N2 x M)
-  Problem p{N1, M, N2, N1, N2, N1, false, false, lt_type(g.scalar_type()), HIPBLASLT_EPILOGUE_DGELU_BGRAD,
-            g.get_device()};
-  if (!lt_run(p, w2.data_ptr(), g.data_ptr(), dz.data_ptr(), db.data_ptr(), p.type, aux.data_ptr(), N1)) return {};
-  return {dz, db};
+  Problem p{N1, M, N2, N1, N2, N1, false, false, lt_type(g.scalar_type()),
+            with_bgrad ? HIPBLASLT_EPILOGUE_DGELU_BGRAD : HIPBLASLT_EPILOGUE_DGELU, g.get_device()};
+  if (!lt_run(p, w2.data_ptr(), g.data_ptr(), dz.data_ptr(), with_bgrad ? db.data_ptr() : nullptr, p.type,
+              aux.data_ptr(), N1))
+    return {};
+  if (with_bgrad) return {dz, db};
+  return {dz};
 }
 
 // dW[N, K] = g[M, N]^T x[M, K];  db[N] = column sums of g (BGRADB)
@@ -228,7 +233,8 @@ void bind_lt(pybind11::module_& root) {
   auto m = root.def_submodule("lt_gemm", "hipBLASLt GEMMs with fused bias / GeLU-aux / dGeLU-bgrad / bgradb epilogues");
   m.def("linear", &lt_linear, pybind11::arg("x"), pybind11::arg("weight"), pybind11::arg("bias"),
         pybind11::arg("epilogue"));
-  m.def("dgelu_bgrad", &lt_dgelu_bgrad);
+  m.def("dgelu_bgrad", &lt_dgelu_bgrad, pybind11::arg("grad"), pybind11::arg("weight"), pybind11::arg("aux"),
+        pybind11::arg("with_bgrad") = true);
   m.def("wgrad_bgrad", &lt_wgrad_bgrad);
   m.def("clear_cache", &lt_clear_cache);
   m.attr("EPI_NONE") = 0;

@@ -50,6 +50,7 @@ struct Geo {
   const float* scale;
   const float* bias;
   const uint16_t* res;
+  const uint16_t* mask;
   int relu;
 };
 
@@ -62,6 +63,7 @@ inline Geo make_geo(const ConvTapArgs& a) {
   g.scale = a.scale;
   g.bias = a.bias;
   g.res = reinterpret_cast<const uint16_t*>(a.residual);
+  g.mask = reinterpret_cast<const uint16_t*>(a.mask);
   g.relu = a.relu;
   for (int t = 0; t < kConvMaxTaps; ++t) {
     g.dh[t] = t < a.ntaps ? a.dh[t] : 0;
@@ -298,6 +300,12 @@ fprop_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, ui
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
         }
+        if (g.mask) {
+          float mk[8];
+          Vec8<T>::load(mk, reinterpret_cast<const T*>(g.mask) + pix * g.kout + gc);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = mk[e] > 0.f ? v[e] : 0.f;
+        }
         Vec8<T>::store(reinterpret_cast<T*>(Y) + pix * g.kout + gc, v);
       }
     }
@@ -476,7 +484,8 @@ bool conv_tap_supported(const ConvTapArgs& a) {
   if (a.ntaps < 1 || a.ntaps > kConvMaxTaps) return false;
   if (a.n <= 0 || a.oh <= 0 || a.ow <= 0) return false;
   if ((int64_t)a.n * a.oh * a.ow >= (1ll << 31) || (int64_t)a.n * a.ih * a.iw >= (1ll << 31)) return false;
-  if ((a.scale && !aligned16(a.scale)) || (a.bias && !aligned16(a.bias)) || (a.residual && !aligned16(a.residual)))
+  if ((a.scale && !aligned16(a.scale)) || (a.bias && !aligned16(a.bias)) || (a.residual && !aligned16(a.residual)) ||
+      (a.mask && !aligned16(a.mask)))
     return false;
   return aligned16(a.in) && aligned16(a.wt) && aligned16(a.out);
 }

@@ -39,6 +39,10 @@ struct ConvTapArgs {
   const float* bias = nullptr;
   const void* residual = nullptr;
   int relu = 0;
+  // optional gradient mask (data-gradient launches of a ReLU chain): y *= (mask[pix, k] > 0), with
+  // `mask` the producing layer's ReLU output in the output tensor's layout and dtype — the dReLU
+  // of the previous stage applied in this dconv's epilogue
+  const void* mask = nullptr;
 };
 
 // shape constraints: c % 64 == 0, kout % 64 == 0, 16-byte aligned pointers

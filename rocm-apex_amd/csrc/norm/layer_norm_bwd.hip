@@ -56,20 +56,47 @@ ln_bwd_kernel(const TO* __restrict__ dy, const TI* __restrict__ x, const float* 
       ab[j][k] = 0.f;
     }
 
+  // software pipeline: the next row-group's x / dy (and statistics) are loaded raw while the
+  // current one is reduced and written, so every lane keeps two rows' bytes in flight
+  Raw8<TI> px[VPT];
+  Raw8<TO> pd[VPT];
+  float pmu = 0.f, piv = 0.f;
+  auto prefetch = [&](int64_t grp) {
+    const int64_t row = grp * RPB + row_in_block;
+    const bool ok = grp < ngroups && row < n1;
+    const int64_t rr = ok ? row : 0;
+    pmu = (rms || !ok) ? 0.f : mean[rr];
+    piv = ok ? invvar[rr] : 0.f;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int v = j * W * 64 + li;
+      if (ok && v < nv) {
+        px[j].load(x + rr * n2 + v * 8);
+        pd[j].load(dy + rr * n2 + v * 8);
+      } else {
+        px[j].zero();
+        pd[j].zero();
+      }
+    }
+  };
+  prefetch(blockIdx.x);
   for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int64_t row = grp * RPB + row_in_block;
     const bool valid = row < n1;
     const int64_t rr = valid ? row : 0;
-    const float mu = (rms || !valid) ? 0.f : mean[rr];
-    const float iv = valid ? invvar[rr] : 0.f;
+    const float mu = pmu, iv = piv;
     float xh[VPT][8], d[VPT][8];
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      px[j].unpack(xh[j]);
+      pd[j].unpack(d[j]);
+    }
+    prefetch(grp + gridDim.x);
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
       const int v = j * W * 64 + li;
       if (valid && v < nv) {
-        Vec8<TI>::load(xh[j], x + rr * n2 + v * 8);
-        Vec8<TO>::load(d[j], dy + rr * n2 + v * 8);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           xh[j][k] = (xh[j][k] - mu) * iv;
@@ -78,12 +105,6 @@ ln_bwd_kernel(const TO* __restrict__ dy, const TI* __restrict__ x, const float* 
           s2 += gd * xh[j][k];
           ag[j][k] += d[j][k] * xh[j][k];
           ab[j][k] += d[j][k];
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          xh[j][k] = 0.f;
-          d[j][k] = 0.f;
         }
       }
     }

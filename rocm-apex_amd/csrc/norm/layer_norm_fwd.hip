@@ -23,70 +23,82 @@ ln_fwd_kernel(const TI* __restrict__ x, const TW* __restrict__ gamma, const TW* 
   const int row_in_block = wave / W;
   const int wave_in_row = wave % W;
   const int li = wave_in_row * 64 + (threadIdx.x & 63);  // lane index within the row
-  const int64_t row = (int64_t)blockIdx.x * RPB + row_in_block;
-  const bool valid = row < n1;
   const int nv = n2 >> 3;
+  const int64_t ngroups = (n1 + RPB - 1) / RPB;
+  const float inv_n = 1.f / (float)n2;
 
-  float r[VPT][8];
-  const TI* xr = x + (valid ? row : 0) * (int64_t)n2;
-  float s = 0.f;
+  // gamma / beta are the same for every row this lane visits: loaded once
+  float g[VPT][8], b[VPT][8];
 #pragma unroll
   for (int j = 0; j < VPT; ++j) {
     const int v = j * W * 64 + li;
-    if (valid && v < nv) {
-      Vec8<TI>::load(r[j], xr + v * 8);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      g[j][k] = 1.f;
+      b[j][k] = 0.f;
+    }
+    if (v < nv) {
+      if (gamma != nullptr) Vec8<TW>::load(g[j], gamma + v * 8);
+      if (beta != nullptr) Vec8<TW>::load(b[j], beta + v * 8);
+    }
+  }
+  // persistent, software-pipelined: the next row-group's input is loaded raw while the current
+  // row is reduced and stored (two rows' bytes in flight per lane)
+  Raw8<TI> px[VPT];
+  auto prefetch = [&](int64_t grp) {
+    const int64_t row = grp * RPB + row_in_block;
+    const bool ok = grp < ngroups && row < n1;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int v = j * W * 64 + li;
+      if (ok && v < nv) px[j].load(x + row * (int64_t)n2 + v * 8);
+      else px[j].zero();
+    }
+  };
+  prefetch(blockIdx.x);
+  for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const int64_t row = grp * RPB + row_in_block;
+    const bool valid = row < n1;
+    float r[VPT][8];
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) px[j].unpack(r[j]);
+    prefetch(grp + gridDim.x);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j)
 #pragma unroll
       for (int k = 0; k < 8; ++k) s += r[j][k];
-    } else {
+    float mu = 0.f;
+    if (!rms) mu = row_sum<W>(s, red, row_in_block, wave_in_row) * inv_n;
+    float q = 0.f;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) r[j][k] = 0.f;
-    }
-  }
-  const float inv_n = 1.f / (float)n2;
-  float mu = 0.f;
-  if (!rms) mu = row_sum<W>(s, red, row_in_block, wave_in_row) * inv_n;
-  float q = 0.f;
+    for (int j = 0; j < VPT; ++j) {
+      const int v = j * W * 64 + li;
+      if (v < nv) {
 #pragma unroll
-  for (int j = 0; j < VPT; ++j) {
-    const int v = j * W * 64 + li;
-    if (v < nv) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float d = r[j][k] - mu;
-        q += d * d;
-      }
-    }
-  }
-  q = row_sum<W>(q, red + RPB * W, row_in_block, wave_in_row);
-  const float iv = rsqrtf(q * inv_n + eps);
-  if (valid && li == 0) {
-    if (!rms) mean_out[row] = mu;
-    invvar_out[row] = iv;
-  }
-  if (!valid) return;
-  TO* yr = y + row * (int64_t)n2;
-#pragma unroll
-  for (int j = 0; j < VPT; ++j) {
-    const int v = j * W * 64 + li;
-    if (v < nv) {
-      float o[8];
-      if (gamma != nullptr) {
-        float g[8];
-        Vec8<TW>::load(g, gamma + v * 8);
-        if (beta != nullptr) {
-          float b[8];
-          Vec8<TW>::load(b, beta + v * 8);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) o[k] = (r[j][k] - mu) * iv * g[k] + b[k];
-        } else {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) o[k] = (r[j][k] - mu) * iv * g[k];
+        for (int k = 0; k < 8; ++k) {
+          const float d = r[j][k] - mu;
+          q += d * d;
         }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] = (r[j][k] - mu) * iv;
       }
-      Vec8<TO>::store(yr + v * 8, o);
+    }
+    q = row_sum<W>(q, red + RPB * W, row_in_block, wave_in_row);
+    const float iv = rsqrtf(q * inv_n + eps);
+    if (!valid) continue;
+    if (li == 0) {
+      if (!rms) mean_out[row] = mu;
+      invvar_out[row] = iv;
+    }
+    TO* yr = y + row * (int64_t)n2;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int v = j * W * 64 + li;
+      if (v < nv) {
+        float o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = (r[j][k] - mu) * iv * g[j][k] + b[j][k];
+        Vec8<TO>::store(yr + v * 8, o);
+      }
     }
   }
 }
@@ -125,10 +137,12 @@ ln_fwd_generic_kernel(const TI* __restrict__ x, const TW* __restrict__ gamma, co
 }
 
 template <typename TI, typename TW, typename TO, int W, int VPT>
-static void launch_fwd(const NormFwdArgs& a, hipStream_t s) {
+static void launch_fwd(const NormFwdArgs& a, int cus, hipStream_t s) {
   constexpr int NT = block_threads<W>();
   constexpr int RPB = NT / 64 / W;
-  const int64_t grid = (a.n1 + RPB - 1) / RPB;
+  const int64_t ngroups = (a.n1 + RPB - 1) / RPB;
+  const int64_t cap = (int64_t)cus * (W == 8 ? 2 : 4);  // resident blocks per CU of the persistent grid
+  const int64_t grid = ngroups < cap ? ngroups : cap;
   hipLaunchKernelGGL((ln_fwd_kernel<TI, TW, TO, W, VPT>), dim3((unsigned)grid), dim3(NT), 0, s,
                      (const TI*)a.x, (const TW*)a.gamma, (const TW*)a.beta, (TO*)a.y, a.mean, a.invvar, a.n1,
                      a.n2, a.eps, a.rms);
@@ -136,7 +150,7 @@ static void launch_fwd(const NormFwdArgs& a, hipStream_t s) {
 
 static bool aligned16(const void* p) { return p == nullptr || ((uintptr_t)p & 15u) == 0; }
 
-void norm_fwd_impl(const NormFwdArgs& a, hipStream_t s) {
+void norm_fwd_impl(const NormFwdArgs& a, int cus, hipStream_t s) {
   if (a.n1 <= 0 || a.n2 <= 0) return;
   const Cfg c = pick_cfg(a.n2);
   const bool fast = c.W > 0 && (a.n2 % 8 == 0) && aligned16(a.x) && aligned16(a.y) && aligned16(a.gamma) &&
@@ -151,18 +165,18 @@ void norm_fwd_impl(const NormFwdArgs& a, hipStream_t s) {
                          a.n2, a.eps, a.rms);
       return;
     }
-    if (c.W == 1 && c.VPT == 1) launch_fwd<TI, TW, TO, 1, 1>(a, s);
-    else if (c.W == 1 && c.VPT == 2) launch_fwd<TI, TW, TO, 1, 2>(a, s);
-    else if (c.W == 1 && c.VPT == 4) launch_fwd<TI, TW, TO, 1, 4>(a, s);
-    else if (c.W == 4 && c.VPT == 2) launch_fwd<TI, TW, TO, 4, 2>(a, s);
-    else if (c.W == 4 && c.VPT == 4) launch_fwd<TI, TW, TO, 4, 4>(a, s);
-    else launch_fwd<TI, TW, TO, 8, 4>(a, s);
+    if (c.W == 1 && c.VPT == 1) launch_fwd<TI, TW, TO, 1, 1>(a, cus, s);
+    else if (c.W == 1 && c.VPT == 2) launch_fwd<TI, TW, TO, 1, 2>(a, cus, s);
+    else if (c.W == 1 && c.VPT == 4) launch_fwd<TI, TW, TO, 1, 4>(a, cus, s);
+    else if (c.W == 4 && c.VPT == 2) launch_fwd<TI, TW, TO, 4, 2>(a, cus, s);
+    else if (c.W == 4 && c.VPT == 4) launch_fwd<TI, TW, TO, 4, 4>(a, cus, s);
+    else launch_fwd<TI, TW, TO, 8, 4>(a, cus, s);
   });
   check_launch("layer_norm forward");
 }
 
 }  // namespace norm
 
-void norm_fwd(const NormFwdArgs& a, int /*cus*/, hipStream_t s) { norm::norm_fwd_impl(a, s); }
+void norm_fwd(const NormFwdArgs& a, int cus, hipStream_t s) { norm::norm_fwd_impl(a, cus, s); }
 
 }  // namespace apex_amd

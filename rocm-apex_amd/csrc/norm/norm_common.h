@@ -74,6 +74,41 @@ __device__ __forceinline__ void row_sum2(float& a, float& b, float* red, int row
   }
 }
 
+// 8 raw elements held in registers between a prefetch and their use (16-bit types: one 16-byte
+// load; fp32: two).  Keeping the NEXT row's data raw lets its loads stay in flight while the
+// current row is reduced (the software pipeline of the persistent kernels).
+template <typename T>
+struct Raw8 {
+  static constexpr int kWords = (int)sizeof(T) * 2;  // 32-bit words for 8 elements
+  uint32_t w[kWords];
+  __device__ __forceinline__ void load(const T* p) {
+#pragma unroll
+    for (int i = 0; i < kWords / 4; ++i) {
+      const uint4 u = reinterpret_cast<const uint4*>(p)[i];
+      w[4 * i] = u.x;
+      w[4 * i + 1] = u.y;
+      w[4 * i + 2] = u.z;
+      w[4 * i + 3] = u.w;
+    }
+  }
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < kWords; ++i) w[i] = 0u;
+  }
+  __device__ __forceinline__ void unpack(float (&r)[8]) const {
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r[i] = __uint_as_float(w[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        r[2 * i] = to_f(T{(uint16_t)(w[i] & 0xffffu)});
+        r[2 * i + 1] = to_f(T{(uint16_t)(w[i] >> 16)});
+      }
+    }
+  }
+};
+
 // typed dispatch over the (input, weight, output) triples the python layer can produce
 template <typename F>
 inline void dispatch_norm_types(int in_t, int w_t, int out_t, F&& f) {

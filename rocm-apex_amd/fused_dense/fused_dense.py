@@ -19,8 +19,11 @@ Routing (static, identical on every rank and every run; ``APEX_AMD_DENSE_ROUTE``
   dGeLU+bias-grad and weight-grad+bias-grad epilogues (the reference's cuBLASLt
   GELU_AUX_BIAS / DGELU_BGRAD / BGRADB, csrc/fused_dense_cuda.cu:220,471,843,977).  At the
   GPT-2 / BERT MLP shapes hipBLASLt's main loop is ahead of the native MFMA kernel
-  (profiles/gemm8p_shapes_ab_r02.jsonl), so the epilogue fusion rides on the faster GEMM; a shape
-  the library has no kernel for falls back to the unfused torch ops;
+  (profiles/gemm8p_shapes_ab_r02.jsonl), so the epilogue fusion rides on the faster GEMM.  Kernel
+  coverage differs by dtype (profiles/lt_probe_r03.jsonl, ROCm 7.2 on gfx950): fp16 has every
+  epilogue; bf16 has BIAS, DGELU and BGRADB but no GELU_AUX_BIAS and DGELU_BGRAD only at a few
+  shapes, so bf16 runs GEMM+bias then one GeLU pass forward, and dGeLU-dgrad + (wgrad+bgrad)
+  backward.  A shape the library has no kernel for at all falls back to the torch ops;
 * ``native``: every GEMM on the gfx950 MFMA kernels (``csrc/gemm/gemm_mfma.hip``) with their
   own fused epilogues;
 * ``library``: plain torch ops (addmm + GeLU + sum) — the A/B baseline;
@@ -187,12 +190,19 @@ def _lib_gelu_dense_fwd(x, w1, b1, w2, b2):
     x2 = x.reshape(-1, x.shape[-1])
     lt = _lt()
     if lt is not None and x2.is_cuda and x2.is_contiguous():
-        r1 = lt.linear(x2, w1.contiguous(), b1, lt.EPI_GELU_AUX_BIAS)
+        w1c, w2c = w1.contiguous(), w2.contiguous()
+        r1 = lt.linear(x2, w1c, b1, lt.EPI_GELU_AUX_BIAS)
         if r1:
             out1, gelu_in = r1
-            r2 = lt.linear(out1, w2.contiguous(), b2, lt.EPI_BIAS)
-            out2 = r2[0] if r2 else torch.addmm(b2, out1, w2.t())
-            return out1, out2.view(x.shape[:-1] + (w2.shape[0],)), gelu_in
+        else:
+            # no GELU_AUX_BIAS kernel (gfx950 bf16): GEMM + bias epilogue writes the
+            # pre-activation, one elementwise GeLU pass
+            r1 = lt.linear(x2, w1c, b1, lt.EPI_BIAS)
+            gelu_in = r1[0] if r1 else torch.addmm(b1, x2, w1.t())
+            out1 = _gelu_tanh(gelu_in)
+        r2 = lt.linear(out1, w2c, b2, lt.EPI_BIAS)
+        out2 = r2[0] if r2 else torch.addmm(b2, out1, w2.t())
+        return out1, out2.view(x.shape[:-1] + (w2.shape[0],)), gelu_in
     gelu_in = torch.addmm(b1, x2, w1.t())
     out1 = _gelu_tanh(gelu_in)
     out2 = torch.addmm(b2, out1, w2.t())
@@ -240,17 +250,23 @@ class FusedDenseGeluDenseFunc(torch.autograd.Function):
         x2 = input.reshape(-1, input.shape[-1])
         dw2, db2 = _lib_wgrad(g2, h, True)
         lt = _lt()
-        r = None
+        gz = db1 = None
         if lt is not None and g2.is_cuda:
-            r = lt.dgelu_bgrad(g2.contiguous(), weight2.contiguous(), gelu_in.reshape(h.shape).contiguous())
-        if r:
-            gz, db1 = r  # dGeLU and the bias gradient in the dgrad GEMM's epilogue
-            dw1, _ = _lib_wgrad(gz, x2, False)
-        else:
+            args = (g2.contiguous(), weight2.contiguous(), gelu_in.reshape(h.shape).contiguous())
+            r = lt.dgelu_bgrad(*args, True)  # dGeLU and the bias gradient in the dgrad epilogue
+            if r:
+                gz, db1 = r
+            else:
+                r = lt.dgelu_bgrad(*args, False)  # dGeLU epilogue; db1 from the wgrad's BGRADB
+                gz = r[0] if r else None
+        if gz is None:
             z = gelu_in.reshape(h.shape).detach().requires_grad_(True)
             with torch.enable_grad():
                 gz = torch.autograd.grad(_gelu_tanh(z), z, g2.matmul(weight2))[0]
+        if db1 is None:
             dw1, db1 = _lib_wgrad(gz, x2, True)
+        else:
+            dw1, _ = _lib_wgrad(gz, x2, False)
         dx = gz.matmul(weight1).view(input.shape)
         return dx, dw1, db1, dw2, db2
 

@@ -241,7 +241,10 @@ def conv_bn_act(x, w, scale, bias, residual=None, relu=True, stride=1, padding=0
         return _conv_bn_act_reference(x, w, scale.detach(), bias.detach(), residual, relu, stride, padding)
 
 
-def conv_tap_dgrad(gy, w, x_shape, stride, pad):
+def conv_tap_dgrad(gy, w, x_shape, stride, pad, mask=None):
+    """Data gradient through the native tap kernel.  ``mask`` (optional, the layer input's producer
+    ReLU output, same shape as dx): dx *= (mask > 0) in the kernel's epilogue — the previous
+    stage's dReLU fused into this dconv."""
     n, c, h, wd = x_shape
     kout, _, k, _ = w.shape
     ext = _conv_ext()
@@ -255,7 +258,7 @@ def conv_tap_dgrad(gy, w, x_shape, stride, pad):
             continue
         wt = torch.stack([wk[:, r, s_, :] for r, s_, _, _ in taps], 1).contiguous()  # [C, taps, K]
         ext.tap_fprop(_nhwc(gy), wt, _nhwc(dx), oh, ow, 1, 1, stride, stride, ph, pw,
-                      [t[2] for t in taps], [t[3] for t in taps])
+                      [t[2] for t in taps], [t[3] for t in taps], mask=None if mask is None else _nhwc(mask))
     return dx
 
 

