@@ -21,9 +21,9 @@ Routing (static, identical on every rank and every run; ``APEX_AMD_DENSE_ROUTE``
   GPT-2 / BERT MLP shapes hipBLASLt's main loop is ahead of the native MFMA kernel
   (profiles/gemm8p_shapes_ab_r02.jsonl), so the epilogue fusion rides on the faster GEMM.  Kernel
   coverage differs by dtype (profiles/lt_probe_r03.jsonl, ROCm 7.2 on gfx950): fp16 has every
-  epilogue; bf16 has BIAS, DGELU and BGRADB but no GELU_AUX_BIAS and DGELU_BGRAD only at a few
-  shapes, so bf16 runs GEMM+bias then one GeLU pass forward, and dGeLU-dgrad + (wgrad+bgrad)
-  backward.  A shape the library has no kernel for at all falls back to the torch ops;
+  epilogue; bf16 has BIAS and BGRADB but no GELU_AUX_BIAS, and its DGELU kernels give wrong
+  results (disabled in lt_epilogue.cpp), so bf16 runs GEMM+bias then one GeLU pass forward, and
+  dgrad + GeLU-backward + wgrad + column sum backward.  BGRADB is opt-in (see ``_lt_bgradb``);  A shape the library has no kernel for at all falls back to the torch ops;
 * ``native``: every GEMM on the gfx950 MFMA kernels (``csrc/gemm/gemm_mfma.hip``) with their
   own fused epilogues;
 * ``library``: plain torch ops (addmm + GeLU + sum) — the A/B baseline;
@@ -127,10 +127,18 @@ def _lib_dense_fwd(x, w, b):
     return out.view(x.shape[:-1] + (w.shape[0],))
 
 
+def _lt_bgradb():
+    # hipBLASLt's heuristic answers BGRADB at the transformer shapes with a 32x32-tile kernel that
+    # runs ~10x slower than the plain wgrad GEMM (1.1 ms vs ~0.1 ms at 16384 tokens,
+    # profiles/gpt2_medium_steady_r03a.md), so the bias-grad epilogue is opt-in
+    return os.environ.get("APEX_AMD_LT_BGRADB", "0") == "1"
+
+
 def _lib_wgrad(g2, x2, has_bias):
-    """(dW, db): one hipBLASLt launch with the BGRADB epilogue, else matmul + column sum."""
+    """(dW, db): matmul + column sum, or (APEX_AMD_LT_BGRADB=1) one hipBLASLt launch with the BGRADB
+    epilogue."""
     lt = _lt()
-    if lt is not None and g2.is_cuda:
+    if lt is not None and g2.is_cuda and has_bias and _lt_bgradb():
         r = lt.wgrad_bgrad(g2.contiguous(), x2.contiguous(), has_bias)
         if r:
             return r[0], (r[1] if has_bias else None)
