@@ -1,19 +1,23 @@
-"""1x1 stride-1 convolution on the gfx950 MFMA GEMM where it beats MIOpen.
+"""1x1 stride-1 convolution routed per operation to the fastest engine for its shape.
 
 On a channels_last activation a 1x1 stride-1 convolution IS a GEMM over the dense NHWC view:
 ``y[M, Cout] = x[M, Cin] W[Cout, Cin]^T`` with M = N*H*W, and its backward is the dgrad
 ``dx = dy W`` and the weight gradient ``dW = dy^T x`` (K = M, split-K in the native kernel).
 ``Conv1x1NHWC`` is a drop-in ``nn.Conv2d(cin, cout, 1, bias=False)`` (same parameter and
-state_dict) that routes each of forward / backward to the native GEMM (``csrc/gemm/gemm_mfma.hip``)
-or to MIOpen per shape, from the measurements in ``profiles/conv1x1_miopen_vs_gemm_r01f.jsonl``
-(1 x MI355X, ResNet-50 bs 256 shapes):
+state_dict) whose forward, data gradient and weight gradient each go to MIOpen, to hipBLASLt
+(``torch.matmul`` on the NHWC views) or to the native split-K MFMA GEMM (``csrc/gemm/gemm_mfma.hip``),
+from the per-op A/B of every ResNet-50 1x1 shape at bs 256 (``profiles/conv_routes_ab_r03.jsonl``,
+``tools/conv_bwd_ab.py``; 1 x MI355X, one process, interleaved):
 
-* backward: native 1.14-1.24x MIOpen at 14x14 / 7x7 (M <= 50k) and for Cin >= 512 at 28x28;
-  MIOpen ahead at 56x56 where Cout = 64 leaves the 256-wide MFMA tiles half empty;
-* forward: the Cin >= 1024 reductions at 14x14 / 7x7 run as NHWC GEMMs (hipBLASLt by default).
+* forward: hipBLASLt 1.1-4x MIOpen almost everywhere (e.g. 28x28 128->512: 64 vs 109 us,
+  14x14 256->1024: 49 vs 84 us); MIOpen keeps the 56x56 -> 64-channel ones (58 / 127 us vs
+  84 / 151), native the 7x7 512->2048 (46 vs 54 / 68 us);
+* data gradient: hipBLASLt 1.1-2.4x MIOpen except where dx has 64 channels (56x56);
+* weight gradient: native split-K at 14x14 / 7x7 and for 512->256 at 28x28 (1.2-1.5x MIOpen),
+  MIOpen elsewhere (hipBLASLt's plain K = N*H*W GEMM is 2-10x slower there).
 
 Everything else (CPU, autocast, other layouts / dtypes, odd channel counts) is plain
-``nn.Conv2d``.  ``APEX_AMD_CONV1X1=0`` disables the native routing (A/B switch).
+``nn.Conv2d``.  ``APEX_AMD_CONV1X1=0`` disables the routing (A/B switch).
 
 Reference capability: the fused 1x1 convolutions of apex/contrib/bottleneck (cudnn-frontend
 graphs, ``apex/contrib/csrc/bottleneck/bottleneck.cpp``) — here the GEMM is our own MFMA kernel.
@@ -29,61 +33,72 @@ from .. import _native
 _ENABLED = os.environ.get("APEX_AMD_CONV1X1", "1") != "0"
 _STEM_PAD = os.environ.get("APEX_AMD_STEM_PAD", "1") != "0"
 
-
-# forward of the Cin >= 1024 reductions at 14x14 / 7x7: "lib" = the NHWC GEMM on hipBLASLt
-# (torch.matmul on the [pixels, Cin] view), "native" = the gfx950 GEMM, "miopen" = F.conv2d.
-# Measured (profiles/conv1x1_miopen_vs_gemm_r01f.jsonl, profiles/gemm8p_shapes_ab_r02.jsonl):
-# 1024->256 @14: lib 29.9 us, native 37.4, MIOpen 42.9; 1024->512 @14: 53.8 / 67.7 / 77.2;
-# 2048->512 @7: lib 31.5, MIOpen 46.1.  APEX_AMD_CONV1X1_FWD selects (A/B).
-_FWD_BIG = os.environ.get("APEX_AMD_CONV1X1_FWD", "lib")
+MIOPEN, LIB, NATIVE = "miopen", "lib", "native"
+_ROUTES_R02 = os.environ.get("APEX_AMD_CONV1X1_ROUTES", "") == "r02"
 
 
 def route(m, cin, cout):
-    """(forward, backward_native) for a 1x1 stride-1 conv with M = N*H*W rows; forward is False
-    (MIOpen) or one of "lib" / "native"."""
-    bwd = m <= 65536 or (cin >= 512 and cout >= 256 and m <= 262144)
-    fwd = False
-    if cin >= 1024 and m <= 65536 and _FWD_BIG in ("lib", "native"):
-        fwd = _FWD_BIG if (_FWD_BIG == "lib" or m >= 32768) else False
-    return fwd, bwd
+    """(forward, dgrad, wgrad) engines for a 1x1 stride-1 conv with M = N*H*W rows, each one of
+    ``"miopen"`` / ``"lib"`` (hipBLASLt) / ``"native"`` (profiles/conv_routes_ab_r03.jsonl)."""
+    if _ROUTES_R02:  # the round-2 policy (A/B): MIOpen forward except the Cin >= 1024 reductions
+        fwd = LIB if (cin >= 1024 and m <= 65536) else MIOPEN
+        bwd = NATIVE if (m <= 65536 or (cin >= 512 and cout >= 256 and m <= 262144)) else MIOPEN
+        return fwd, bwd, bwd
+    if m >= 524288 and cout <= 64:
+        fwd = MIOPEN
+    elif m <= 16384 and cin <= 512:
+        fwd = NATIVE
+    else:
+        fwd = LIB
+    dgrad = MIOPEN if cin <= 64 else LIB
+    wgrad = NATIVE if (m <= 65536 or (cin >= 512 and cout >= 256 and m <= 262144)) else MIOPEN
+    return fwd, dgrad, wgrad
 
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, fwd_native, bwd_native):
+    def forward(ctx, x, w, routes):
+        fwd, dgrad, wgrad = routes
         n, c, h, wd = x.shape
         cout = w.size(0)
         x2 = x.permute(0, 2, 3, 1).reshape(-1, c)  # zero-copy: x is channels_last contiguous
         w2 = w.view(cout, c)
-        if fwd_native == "lib":
+        if fwd == LIB:
             y = torch.matmul(x2, w2.t()).view(n, h, wd, cout).permute(0, 3, 1, 2)
-        elif fwd_native:
+        elif fwd == NATIVE:
             g = _native.require("conv1x1").gemm
             y = g.linear(x2, w2, None, g.EPI_NONE, False)[0].view(n, h, wd, cout).permute(0, 3, 1, 2)
         else:
             y = F.conv2d(x, w)
         ctx.save_for_backward(x, w)
-        ctx.bwd_native = bwd_native
+        ctx.routes = routes
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
+        _, dgrad, wgrad = ctx.routes
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
-        if not ctx.bwd_native:
-            dx, dw, _ = torch.ops.aten.convolution_backward(gy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
-                                                            [need_x, need_w, False])
-            return dx, dw, None, None
-        g = _native.require("conv1x1").gemm
         n, c, h, wd = x.shape
         cout = w.size(0)
-        gy2 = gy.permute(0, 2, 3, 1).reshape(-1, cout)  # a view when gy is channels_last contiguous
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        mi_x, mi_w = need_x and dgrad == MIOPEN, need_w and wgrad == MIOPEN
         dx = dw = None
-        if need_x:
-            dx = g.linear_dgrad(gy2, w.view(cout, c), g.EPI_NONE, None).view(n, h, wd, c).permute(0, 3, 1, 2)
-        if need_w:
+        if mi_x or mi_w:
+            dx, dw, _ = torch.ops.aten.convolution_backward(gy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                                                            [mi_x, mi_w, False])
+        gy2 = gy.permute(0, 2, 3, 1).reshape(-1, cout)  # a view: gy is channels_last contiguous
+        if need_x and dgrad != MIOPEN:
+            if dgrad == LIB:
+                dx2 = torch.matmul(gy2, w.view(cout, c))
+            else:
+                g = _native.require("conv1x1").gemm
+                dx2 = g.linear_dgrad(gy2, w.view(cout, c), g.EPI_NONE, None)
+            dx = dx2.view(n, h, wd, c).permute(0, 3, 1, 2)
+        if need_w and wgrad != MIOPEN:
+            g = _native.require("conv1x1").gemm
             dw = g.linear_wgrad(gy2, x.permute(0, 2, 3, 1).reshape(-1, c)).view_as(w)
-        return dx, dw, None, None
+        return dx, dw, None
 
 
 class Conv1x1NHWC(nn.Conv2d):
@@ -102,9 +117,9 @@ class Conv1x1NHWC(nn.Conv2d):
     def forward(self, x):
         if self._native_ok(x):
             n, _, h, wd = x.shape
-            fwd, bwd = route(n * h * wd, self.in_channels, self.out_channels)
-            if fwd or bwd:
-                return _Conv1x1Fn.apply(x, self.weight, fwd, bwd)
+            routes = route(n * h * wd, self.in_channels, self.out_channels)
+            if routes != (MIOPEN, MIOPEN, MIOPEN):
+                return _Conv1x1Fn.apply(x, self.weight, routes)
         return super().forward(x)
 
 

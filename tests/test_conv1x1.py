@@ -17,13 +17,15 @@ def test_cpu_falls_back_and_matches_conv2d_state():
 
 
 def test_route_policy():
-    # ResNet-50 bs 256: native backward at 14x14 / 7x7 and for the 512->256 reduction at 28x28,
-    # MIOpen at 56x56; the Cin >= 1024 reductions at 14x14 / 7x7 forward as hipBLASLt NHWC GEMMs
-    assert route(256 * 7 * 7, 2048, 512) == ("lib", True)
-    assert route(256 * 14 * 14, 1024, 256) == ("lib", True)
-    assert route(256 * 28 * 28, 512, 256) == (False, True)
-    assert route(256 * 28 * 28, 512, 128) == (False, False)
-    assert route(256 * 56 * 56, 64, 256) == (False, False)
+    # ResNet-50 bs 256, per-op winners of profiles/conv_routes_ab_r03.jsonl
+    assert route(256 * 7 * 7, 2048, 512) == ("lib", "lib", "native")
+    assert route(256 * 7 * 7, 512, 2048) == ("native", "lib", "native")
+    assert route(256 * 14 * 14, 1024, 256) == ("lib", "lib", "native")
+    assert route(256 * 28 * 28, 512, 256) == ("lib", "lib", "native")
+    assert route(256 * 28 * 28, 512, 128) == ("lib", "lib", "miopen")
+    assert route(256 * 56 * 56, 64, 256) == ("lib", "miopen", "miopen")
+    assert route(256 * 56 * 56, 256, 64) == ("miopen", "lib", "miopen")
+    assert route(256 * 56 * 56, 64, 64) == ("miopen", "miopen", "miopen")
 
 
 def _ref(x, w, gy):
@@ -44,8 +46,10 @@ def _close(a, b, tol=2e-2):
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,cin,cout,hw", [(4, 1024, 256, 14), (2, 512, 2048, 7), (8, 2048, 512, 7),
                                            (2, 256, 64, 9)])
-@pytest.mark.parametrize("fwd_native", [True, "lib", False])
-def test_gpu_conv1x1_native(n, cin, cout, hw, fwd_native):
+@pytest.mark.parametrize("routes", [("native", "native", "native"), ("lib", "lib", "native"),
+                                    ("miopen", "miopen", "native"), ("lib", "native", "miopen"),
+                                    ("native", "miopen", "miopen")])
+def test_gpu_conv1x1_native(n, cin, cout, hw, routes):
     from apex import _native
 
     assert _native.available(), "native extension must be loaded on a GPU box"
@@ -56,7 +60,7 @@ def test_gpu_conv1x1_native(n, cin, cout, hw, fwd_native):
     gy = torch.randn(n, cout, hw, hw, device="cuda", dtype=dt).to(memory_format=torch.channels_last)
     xa = x.clone().requires_grad_(True)
     wa = w.clone().requires_grad_(True)
-    y = _Conv1x1Fn.apply(xa, wa, fwd_native, True)
+    y = _Conv1x1Fn.apply(xa, wa, routes)
     assert y.is_contiguous(memory_format=torch.channels_last)
     y.backward(gy)
     yr, dxr, dwr = _ref(x, w, gy)
