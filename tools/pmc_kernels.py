@@ -52,6 +52,13 @@ def main():
     gy = torch.randn_like(y)
     rep(lambda: ln(x))
     rep(lambda: torch.autograd.grad(y, [x] + list(ln.parameters()), gy, retain_graph=True))
+    x4 = torch.randn(16384, 4096, device="cuda", dtype=dt, requires_grad=True)
+    ln4 = FusedLayerNorm(4096).cuda().to(dt)
+    y4 = ln4(x4)
+    gy4 = torch.randn_like(y4)
+    rep(lambda: ln4(x4))
+    rep(lambda: torch.autograd.grad(y4, [x4] + list(ln4.parameters()), gy4, retain_graph=True))
+    del x4, y4, gy4
 
     from apex.contrib.groupbn import BatchNorm2d_NHWC
 
@@ -83,6 +90,11 @@ def main():
     rep(opt.step)
     flag = torch.zeros(1, dtype=torch.int, device="cuda")
     rep(lambda: amp_C.multi_tensor_l2norm(65536, flag, [[p.grad for p in ps]], False))
+    # unscale: bf16 model grads -> fp32 master grads, and fp32 -> fp32 in place
+    hs = [p.grad.to(dt) for p in ps]
+    outs = [torch.empty_like(p.grad) for p in ps]
+    rep(lambda: amp_C.multi_tensor_scale(65536, flag, [hs, outs], 0.5))
+    rep(lambda: amp_C.multi_tensor_scale(65536, flag, [outs, outs], 0.5))
     print("pmc_kernels done", flush=True)
 
 
