@@ -75,3 +75,15 @@ def use_native(*tensors) -> bool:
                 return False
             return True
     return False
+
+
+def column_sum(x, out_dtype):
+    """Sum of a [..., N] tensor over all leading dims (fp32 accumulation) in ``out_dtype``: the bias
+    gradient of a dense layer.  The gfx950 two-stage column reduction (deterministic, fixed order)
+    for contiguous fp16/bf16/fp32 GPU tensors with N % 8 == 0, torch otherwise."""
+    import torch
+
+    if (use_native(x) and submodule("gemm") is not None and x.dim() >= 2 and x.is_contiguous()
+            and x.shape[-1] % 8 == 0 and x.dtype in (torch.float16, torch.bfloat16, torch.float32)):
+        return _C.gemm.column_sum(x.reshape(-1, x.shape[-1]), out_dtype)
+    return x.reshape(-1, x.shape[-1]).sum(0, dtype=torch.float32).to(out_dtype)

@@ -138,6 +138,21 @@ void bind_gemm(pybind11::module_& root) {
     const c10::hip::HIPGuard guard(dy.get_device());
     return linear_wgrad(as2d(dy), as2d(x));
   });
+  g.def("dgelu_column_sum", [](at::Tensor dy, at::Tensor aux, c10::optional<at::ScalarType> out_dtype) {
+    // (dz, db): dz = dy * gelu_tanh'(aux), db = column sums of dz — one pass
+    const c10::hip::HIPGuard guard(dy.get_device());
+    at::Tensor d = as2d(dy), a = as2d(aux);
+    TORCH_CHECK(d.sizes() == a.sizes() && d.scalar_type() == a.scalar_type(), "dgelu_column_sum: shape mismatch");
+    const int64_t m = d.size(0), n = d.size(1);
+    auto dz = at::empty_like(d);
+    const at::ScalarType ot = out_dtype.value_or(d.scalar_type());
+    auto db = at::empty({n}, d.options().dtype(ot));
+    const int cus = device_cus(d.get_device());
+    auto ws = at::empty({column_sum_workspace_floats(m, n, cus)}, d.options().dtype(at::kFloat));
+    dgelu_column_sum(d.data_ptr(), a.data_ptr(), dz.data_ptr(), dtype_code(d.scalar_type()), m, (int)n, db.data_ptr(),
+                     dtype_code(ot), ws.data_ptr<float>(), cus, cur_stream());
+    return std::make_tuple(dz, db);
+  }, pybind11::arg("dy"), pybind11::arg("aux"), pybind11::arg("out_dtype") = c10::nullopt);
   g.def("column_sum", [](at::Tensor x, c10::optional<at::ScalarType> out_dtype) {
     return colsum(as2d(x), out_dtype.value_or(x.scalar_type()));
   }, py::arg("x"), py::arg("out_dtype") = c10::nullopt);

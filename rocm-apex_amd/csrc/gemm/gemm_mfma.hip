@@ -304,6 +304,61 @@ __global__ void __launch_bounds__(256) colsum_partial(const T* __restrict__ x, i
   }
 }
 
+// dz = dy * gelu'(aux) written out and its column sums in the same pass (the dGeLU + bias-grad
+// of a dense layer whose GEMM ran on the library: cuBLASLt's DGELU_BGRAD capability,
+// reference csrc/fused_dense_cuda.cu:977, for the bf16 case hipBLASLt has no working kernel for).
+// Block layout as colsum_partial; two rows in flight per lane.  The sums are of the ROUNDED dz
+// (what the unfused dz.sum(0) would add).
+template <typename T>
+__global__ void __launch_bounds__(256) dgelu_colsum_partial(const T* __restrict__ dy, const T* __restrict__ aux,
+                                                            T* __restrict__ dz, int64_t m, int n,
+                                                            float* __restrict__ part) {
+  const int cv = blockIdx.x * 32 + (threadIdx.x & 31);
+  const int rg = threadIdx.x >> 5;
+  const int c0 = cv * 8;
+  __shared__ float red[8][32 * 8];
+  float s[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s[e] = 0.f;
+  if (c0 < n) {
+    const int64_t step = (int64_t)gridDim.y * 8;
+    for (int64_t r = (int64_t)blockIdx.y * 8 + rg; r < m; r += 2 * step) {
+      const int64_t r1 = r + step;
+      const bool two = r1 < m;
+      float g0[8], a0[8], g1[8], a1[8];
+      Vec8<T>::load(g0, dy + r * n + c0);
+      Vec8<T>::load(a0, aux + r * n + c0);
+      if (two) {
+        Vec8<T>::load(g1, dy + r1 * n + c0);
+        Vec8<T>::load(a1, aux + r1 * n + c0);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g0[e] = to_f(from_f<T>(g0[e] * dgelu_tanh(a0[e])));
+      Vec8<T>::store(dz + r * n + c0, g0);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += g0[e];
+      if (two) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g1[e] = to_f(from_f<T>(g1[e] * dgelu_tanh(a1[e])));
+        Vec8<T>::store(dz + r1 * n + c0, g1);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s[e] += g1[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rg][(threadIdx.x & 31) * 8 + e] = s[e];
+  __syncthreads();
+  if (rg == 0 && c0 < n) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float t = 0.f;
+      for (int g = 0; g < 8; ++g) t += red[g][(threadIdx.x & 31) * 8 + e];
+      part[(int64_t)blockIdx.y * n + c0 + e] = t;
+    }
+  }
+}
+
 template <typename TO>
 __global__ void __launch_bounds__(256) colsum_finalize(const float* __restrict__ part, int p, int n,
                                                        TO* __restrict__ out) {
@@ -1001,6 +1056,24 @@ void column_sum(const void* x, int dtype, int64_t m, int n, int64_t ldx, void* o
     hipLaunchKernelGGL((gemm::colsum_finalize<TO>), dim3((n + 15) / 16), dim3(256), 0, s, ws, p, n, (TO*)out);
   }, "column_sum out");
   check_launch("column_sum");
+}
+
+void dgelu_column_sum(const void* dy, const void* aux, void* dz, int dtype, int64_t m, int n, void* out, int out_dtype,
+                      float* ws, int cus, hipStream_t s) {
+  if (n <= 0) return;
+  if (n % 8 || ((uintptr_t)dy & 15u) || ((uintptr_t)aux & 15u) || ((uintptr_t)dz & 15u))
+    throw std::runtime_error("dgelu_column_sum: n must be a multiple of 8, operands 16-byte aligned");
+  const int p = gemm::colsum_parts(m, n, cus);
+  dispatch_16(dtype, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    hipLaunchKernelGGL((gemm::dgelu_colsum_partial<T>), dim3((n / 8 + 31) / 32, p), dim3(256), 0, s, (const T*)dy,
+                       (const T*)aux, (T*)dz, m, n, ws);
+  }, "dgelu_column_sum");
+  dispatch_float(out_dtype, [&](auto tag) {
+    using TO = typename decltype(tag)::type;
+    hipLaunchKernelGGL((gemm::colsum_finalize<TO>), dim3((n + 15) / 16), dim3(256), 0, s, ws, p, n, (TO*)out);
+  }, "dgelu_column_sum out");
+  check_launch("dgelu_column_sum");
 }
 
 }  // namespace apex_amd

@@ -53,5 +53,8 @@ int64_t gemm_splitk_workspace_floats(const GemmArgs& g, int cus);
 void column_sum(const void* x, int dtype, int64_t m, int n, int64_t ldx, void* out, int out_dtype, float* ws, int cus,
                 hipStream_t s);
 int64_t column_sum_workspace_floats(int64_t m, int n, int cus);
+// dz = dy * gelu_tanh'(aux) and out = column sums of dz, one pass (workspace as column_sum)
+void dgelu_column_sum(const void* dy, const void* aux, void* dz, int dtype, int64_t m, int n, void* out, int out_dtype,
+                      float* ws, int cus, hipStream_t s);
 
 }  // namespace apex_amd

@@ -127,6 +127,21 @@ def _lib_dense_fwd(x, w, b):
     return out.view(x.shape[:-1] + (w.shape[0],))
 
 
+def native_wgrad_ok(g2, x2):
+    """The native split-K wgrad beats hipBLASLt's ``g.t() @ x`` when the N x K output is small
+    (<= 1M elements: too few output tiles for hipBLASLt to fill 256 CUs) and K = M is deep
+    (profiles/wgrad_shapes_ab_r03.jsonl: 1024 x 1024 at 8k / 16k tokens 1.06-1.64x); at
+    3072-4096 x 1024 the two tie or hipBLASLt leads."""
+    if not (g2.is_cuda and _native.use_native(g2) and _native.submodule("gemm") is not None):
+        return False
+    if g2.dtype not in (torch.float16, torch.bfloat16) or x2.dtype != g2.dtype or g2.dim() != 2 or x2.dim() != 2:
+        return False
+    m, n = g2.shape
+    k = x2.shape[1]
+    return (n * k <= (1 << 20) and m >= 4096 and n % 64 == 0 and k % 64 == 0 and g2.is_contiguous()
+            and x2.is_contiguous())
+
+
 def _lt_bgradb():
     # hipBLASLt's heuristic answers BGRADB at the transformer shapes with a 32x32-tile kernel that
     # runs ~10x slower than the plain wgrad GEMM (1.1 ms vs ~0.1 ms at 16384 tokens,
@@ -142,7 +157,8 @@ def _lib_wgrad(g2, x2, has_bias):
         r = lt.wgrad_bgrad(g2.contiguous(), x2.contiguous(), has_bias)
         if r:
             return r[0], (r[1] if has_bias else None)
-    return g2.t().matmul(x2), (g2.sum(0) if has_bias else None)
+    dw = _g().linear_wgrad(g2, x2) if native_wgrad_ok(g2, x2) else g2.t().matmul(x2)
+    return dw, (g2.sum(0) if has_bias else None)
 
 
 def _lib_dense_bwd(x, w, gy, has_bias):
@@ -268,9 +284,13 @@ class FusedDenseGeluDenseFunc(torch.autograd.Function):
                 r = lt.dgelu_bgrad(*args, False)  # dGeLU epilogue; db1 from the wgrad's BGRADB
                 gz = r[0] if r else None
         if gz is None:
-            z = gelu_in.reshape(h.shape).detach().requires_grad_(True)
-            with torch.enable_grad():
-                gz = torch.autograd.grad(_gelu_tanh(z), z, g2.matmul(weight2))[0]
+            dh = g2.matmul(weight2)
+            z = gelu_in.reshape(h.shape)
+            if _native.use_native(dh) and _native.submodule("gemm") is not None and dh.shape[1] % 8 == 0:
+                # dGeLU + bias gradient in one native pass over dh (no GeLU recompute)
+                gz, db1 = _g().dgelu_column_sum(dh, z.contiguous())
+            else:
+                gz = torch.ops.aten.gelu_backward(dh, z, approximate="tanh")
         if db1 is None:
             dw1, db1 = _lib_wgrad(gz, x2, True)
         else:

@@ -98,6 +98,22 @@ def _linear(x, weight, bias):
     return out + bias if bias is not None else out
 
 
+from ... import _native  # noqa: E402
+
+
+def _wgrad(go2, ti2):
+    """dW[N, K] = go2[M, N]^T ti2[M, K]: the native split-K MFMA kernel where it beats hipBLASLt
+    (small N x K outputs, e.g. the 1024 x 1024 attention projection at 16k tokens: 66 vs 108 us,
+    profiles/wgrad_shapes_ab_r03.jsonl), else ``torch.matmul``."""
+    from ...fused_dense.fused_dense import native_wgrad_ok
+
+    if native_wgrad_ok(go2, ti2):
+        from ... import _native
+
+        return _native.require("gemm").gemm.linear_wgrad(go2, ti2)
+    return go2.t().matmul(ti2)
+
+
 class VocabParallelEmbedding(torch.nn.Module):
     """Embedding parallelized in the vocabulary dimension."""
 
@@ -173,8 +189,8 @@ class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
             handle = torch.distributed.all_reduce(grad_input, group=group, async_op=True)
         go2 = grad_output.reshape(-1, grad_output.shape[-1])
         ti2 = total_input.reshape(-1, total_input.shape[-1])
-        grad_weight = go2.t().matmul(ti2)
-        grad_bias = go2.sum(dim=0) if ctx.use_bias else None
+        grad_weight = _wgrad(go2, ti2)
+        grad_bias = _native.column_sum(go2, go2.dtype) if ctx.use_bias else None
         if handle is not None:
             handle.wait()
         if ctx.sequence_parallel:

@@ -51,11 +51,9 @@ def post_language_model_processing(lm_output, pooled_output, lm_head, binary_hea
     if lm_labels is None:
         return lm_logits, binary_logits
     lm_labels = lm_labels.transpose(0, 1).contiguous()
-    if fp16_lm_cross_entropy:
-        assert lm_logits.dtype == torch.half
-        lm_loss = tensor_parallel.vocab_parallel_cross_entropy(lm_logits, lm_labels)
-    else:
-        lm_loss = tensor_parallel.vocab_parallel_cross_entropy(lm_logits, lm_labels)  # fp32 math inside
+    # fp32 loss math inside either way (see standalone_gpt.post_language_model_processing)
+    assert not fp16_lm_cross_entropy or lm_logits.dtype == torch.half
+    lm_loss = tensor_parallel.vocab_parallel_cross_entropy(lm_logits, lm_labels)
     return lm_loss.transpose(0, 1).contiguous(), binary_logits
 
 

@@ -16,12 +16,11 @@ def post_language_model_processing(lm_output, labels, logit_weights, parallel_ou
         return output
     # labels [b, s]; logits [s, b, v/tp]
     labels = labels.transpose(0, 1).contiguous()
-    # fp16_lm_cross_entropy: hand the half logits to the loss as they are (its reductions run in
-    # fp32 registers either way); otherwise upcast first, as the reference does
-    if fp16_lm_cross_entropy:
-        assert output.dtype == torch.half
-    else:
-        output = output.float()
+    # the loss math is fp32 either way: the fused kernel (unsharded vocabulary) upcasts the half
+    # logits in registers and the sharded path upcasts them itself, so an fp32 copy of the
+    # [tokens, vocab] logits (the reference's upcast) is never materialised;
+    # fp16_lm_cross_entropy only pins the logits dtype
+    assert not fp16_lm_cross_entropy or output.dtype == torch.half
     loss = tensor_parallel.vocab_parallel_cross_entropy(output, labels)
     return loss.transpose(0, 1).contiguous()  # [b, s]
 

@@ -376,3 +376,35 @@ def test_gpu_lt_epilogues_vs_fp32(m, k, n, dtype):
     assert len(rw) == 2, "no hipBLASLt BGRADB kernel for this shape"
     close(rw[0], g.float().t() @ x.float())
     close(rw[1], g.float().sum(0), tol=3e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("m,n", [(16384, 4096), (1000, 1024), (37, 8)])
+def test_gpu_dgelu_column_sum_vs_fp32(m, n, dtype):
+    """One-pass dGeLU + bias gradient (csrc/gemm/gemm_mfma.hip dgelu_colsum_partial) against fp32
+    torch autograd of the tanh GeLU; the bias gradient sums the rounded dz like dz.sum(0)."""
+    from apex import _native
+
+    g = _native.require("gemm").gemm
+    torch.manual_seed(0)
+    dy = torch.randn(m, n, device="cuda").to(dtype)
+    z = (torch.randn(m, n, device="cuda") * 2).to(dtype)
+    dz, db = g.dgelu_column_sum(dy, z)
+    zr = z.float().requires_grad_(True)
+    gz = torch.autograd.grad(torch.nn.functional.gelu(zr, approximate="tanh"), zr, dy.float())[0]
+    torch.testing.assert_close(dz.float(), gz, atol=2e-2, rtol=2e-2)
+    ref_db = dz.float().sum(0)
+    torch.testing.assert_close(db.float(), ref_db, atol=1e-2 * max(1.0, m ** 0.5), rtol=1e-2)
+    _, db32 = g.dgelu_column_sum(dy, z, torch.float32)
+    torch.testing.assert_close(db32, ref_db, atol=1e-3 * max(1.0, m ** 0.5), rtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_gpu_native_column_sum_helper():
+    from apex import _native
+
+    x = torch.randn(4, 1024, 1024, device="cuda", dtype=torch.bfloat16)
+    got = _native.column_sum(x, torch.bfloat16)
+    torch.testing.assert_close(got.float(), x.float().sum((0, 1)), atol=0.5, rtol=1e-2)
+    assert got.dtype == torch.bfloat16
