@@ -315,6 +315,56 @@ at::Tensor bwd_group_finish(at::Tensor dy_masked, at::Tensor x, at::Tensor sums,
   return dx;
 }
 
+// statistics only: (save_mean, save_invstd, coef[2, C]) of x, running stats updated in place
+std::vector<at::Tensor> stats(at::Tensor x, OT w, OT b, OT running_mean, OT running_var, double momentum, double eps) {
+  check2d(x, "input");
+  const c10::hip::HIPGuard g(x.get_device());
+  const int64_t m = x.size(0);
+  const int c = (int)x.size(1);
+  for (const OT* p : {&w, &b, &running_mean, &running_var}) check_param(*p, c);
+  const int cus = device_cus(x.get_device());
+  int64_t wsf = 0;
+  const int gy = bn_nhwc_plan(m, c, cus, &wsf);
+  auto fo = x.options().dtype(at::kFloat);
+  auto ws = at::empty({wsf}, fo);
+  auto sm = at::empty({c}, fo), si = at::empty({c}, fo), coef = at::empty({2, c}, fo);
+  bn_nhwc_stats(x.data_ptr(), dtype_code(x.scalar_type()), m, c, fptr(w), fptr(b), (float)eps, (float)momentum,
+                fptr_mut(running_mean), fptr_mut(running_var), sm.data_ptr<float>(), si.data_ptr<float>(),
+                coef.data_ptr<float>(), ws.data_ptr<float>(), gy, cus, cur_stream());
+  return {sm, si, coef};
+}
+
+// apply only, with precomputed coefficients: y = act(x * coef[0] + coef[1] (+ z)) (+ ReLU bit mask);
+// with z2 / coef_z the downsampling pair y = relu(bn(x) + bn_z(z))
+std::vector<at::Tensor> apply(at::Tensor x, OT z, at::Tensor coef, bool relu, bool want_mask, OT coef_z) {
+  check2d(x, "input");
+  TORCH_CHECK(!want_mask || relu, "bn_nhwc apply: the ReLU bit mask needs relu=True");
+  const c10::hip::HIPGuard g(x.get_device());
+  const int64_t m = x.size(0);
+  const int c = (int)x.size(1);
+  TORCH_CHECK(coef.scalar_type() == at::kFloat && coef.is_contiguous() && coef.numel() == 2 * (int64_t)c,
+              "bn_nhwc apply: coef must be contiguous fp32 [2C]");
+  if (has(z)) {
+    check2d(*z, "z");
+    TORCH_CHECK(z->sizes() == x.sizes() && z->scalar_type() == x.scalar_type(), "bn_nhwc apply: z must match x");
+  }
+  at::Tensor mask;
+  if (want_mask) mask = at::empty({m * c / 8}, x.options().dtype(at::kByte));
+  auto y = at::empty_like(x);
+  const int cus = device_cus(x.get_device());
+  if (has(coef_z)) {
+    TORCH_CHECK(has(z) && relu && coef_z->scalar_type() == at::kFloat && coef_z->numel() == 2 * (int64_t)c,
+                "bn_nhwc apply: the dual form needs z, relu and coef_z [2C]");
+    bn_nhwc_apply_dual(x.data_ptr(), z->data_ptr(), dtype_code(x.scalar_type()), coef.data_ptr<float>(),
+                       coef_z->data_ptr<float>(), y.data_ptr(), m, c, cus, cur_stream(),
+                       want_mask ? mask.data_ptr<uint8_t>() : nullptr);
+  } else {
+    bn_nhwc_apply(x.data_ptr(), dtype_code(x.scalar_type()), has(z) ? z->data_ptr() : nullptr, coef.data_ptr<float>(),
+                  relu, y.data_ptr(), m, c, cus, cur_stream(), want_mask ? mask.data_ptr<uint8_t>() : nullptr);
+  }
+  return {y, mask};
+}
+
 }  // namespace
 
 void bind_bn_nhwc(pybind11::module_& root) {
@@ -323,6 +373,9 @@ void bind_bn_nhwc(pybind11::module_& root) {
         pybind11::arg("running_mean"), pybind11::arg("running_var"), pybind11::arg("momentum"), pybind11::arg("eps"),
         pybind11::arg("relu"), pybind11::arg("want_mask") = false);
   m.def("fwd_eval", &fwd_eval);
+  m.def("stats", &stats);
+  m.def("apply", &apply, pybind11::arg("x"), pybind11::arg("z"), pybind11::arg("coef"), pybind11::arg("relu"),
+        pybind11::arg("want_mask") = false, pybind11::arg("coef_z") = c10::nullopt);
   m.def("fwd_train_dual", &fwd_train_dual);
   m.def("fwd_train_relu_maxpool", &fwd_train_relu_maxpool);
   m.def("bwd", &bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("z"), pybind11::arg("w"),

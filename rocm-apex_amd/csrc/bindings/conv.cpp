@@ -109,6 +109,86 @@ void wgrad(const at::Tensor& in, const at::Tensor& dy, at::Tensor& dw_out, int64
              cur_stream());
 }
 
+// y = pro(a) . W^T (+ BN statistics partials); see conv_api.h.  Returns (y, part or empty).
+std::vector<at::Tensor> bn1x1(const at::Tensor& a, const at::Tensor& w, bool w_kmajor_out,
+                              const c10::optional<at::Tensor>& pcoef, const c10::optional<at::Tensor>& shift,
+                              bool stats) {
+  TORCH_CHECK(a.is_cuda() && a.dim() == 2 && a.is_contiguous(), "bn1x1: a must be a contiguous [M, K] GPU tensor");
+  TORCH_CHECK(w.is_cuda() && w.dim() == 2 && w.is_contiguous() && w.scalar_type() == a.scalar_type(),
+              "bn1x1: w must be a contiguous 2-D tensor of a's dtype");
+  const int64_t m = a.size(0);
+  const int k = (int)a.size(1);
+  const int ncols = (int)(w_kmajor_out ? w.size(1) : w.size(0));
+  TORCH_CHECK((w_kmajor_out ? w.size(0) : w.size(1)) == k, "bn1x1: weight does not match the reduction dim");
+  TORCH_CHECK(conv1x1_bn_supported(m, k, ncols), "bn1x1: unsupported shape (k in 64/128/256/512, ncols % 64)");
+  auto f32 = [&](const c10::optional<at::Tensor>& t, int64_t n, const char* what) -> const float* {
+    if (!t.has_value()) return nullptr;
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == n, "bn1x1: ",
+                what, " must be a contiguous fp32 tensor of ", n, " elements");
+    return t->data_ptr<float>();
+  };
+  const float* pc = f32(pcoef, 2 * (int64_t)k, "pcoef");
+  const float* sh = f32(shift, ncols, "shift");
+  const c10::hip::HIPGuard g(a.get_device());
+  const int cus = device_cus(a.get_device());
+  auto y = at::empty({m, ncols}, a.options());
+  at::Tensor part;
+  if (stats)
+    part = at::empty({2, conv1x1_bn_partials(m, k, ncols, pc != nullptr, cus), ncols}, a.options().dtype(at::kFloat));
+  conv1x1_bn(a.data_ptr(), w.data_ptr(), y.data_ptr(), m, k, ncols, w_kmajor_out, dtype_code(a.scalar_type()), pc, sh,
+             stats ? part.data_ptr<float>() : nullptr, cus, cur_stream());
+  return {y, part};
+}
+
+// (save_mean, save_invstd, coef[2C]) from bn1x1 partials; running stats updated in place
+std::vector<at::Tensor> bn_finalize(const at::Tensor& part, double count, const c10::optional<at::Tensor>& shift,
+                                    const c10::optional<at::Tensor>& w, const c10::optional<at::Tensor>& b,
+                                    const c10::optional<at::Tensor>& running_mean,
+                                    const c10::optional<at::Tensor>& running_var, double eps, double momentum) {
+  TORCH_CHECK(part.is_cuda() && part.dim() == 3 && part.size(0) == 2 && part.is_contiguous() &&
+                  part.scalar_type() == at::kFloat,
+              "bn_finalize: part must be the [2, G, C] fp32 partials");
+  const int c = (int)part.size(2);
+  auto f = [&](const c10::optional<at::Tensor>& t) -> float* {
+    if (!t.has_value()) return nullptr;
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == c,
+                "bn_finalize: per-channel tensors must be contiguous fp32 [C]");
+    return t->data_ptr<float>();
+  };
+  const c10::hip::HIPGuard g(part.get_device());
+  auto opt = part.options();
+  auto sm = at::empty({c}, opt), si = at::empty({c}, opt), coef = at::empty({2 * c}, opt);
+  conv1x1_bn_finalize(part.data_ptr<float>(), (int)part.size(1), c, (float)count, f(shift), f(w), f(b), (float)eps,
+                      (float)momentum, f(running_mean), f(running_var), sm.data_ptr<float>(), si.data_ptr<float>(),
+                      coef.data_ptr<float>(), cur_stream());
+  return {sm, si, coef};
+}
+
+// dW [N, K] = g^T . pro(x) (pro = relu(x * xcoef[:K] + xcoef[K:]) when given), out_dtype per `like`
+at::Tensor wgrad1x1(const at::Tensor& g, const at::Tensor& x, const c10::optional<at::Tensor>& xcoef,
+                    c10::optional<at::ScalarType> out_dtype) {
+  TORCH_CHECK(g.is_cuda() && g.dim() == 2 && g.is_contiguous() && x.is_cuda() && x.dim() == 2 && x.is_contiguous() &&
+                  g.size(0) == x.size(0) && g.scalar_type() == x.scalar_type(),
+              "wgrad1x1: g [M, N] and x [M, K] must be contiguous GPU tensors of one dtype");
+  const int64_t m = g.size(0);
+  const int n = (int)g.size(1), k = (int)x.size(1);
+  TORCH_CHECK(conv1x1_wgrad_supported(m, n, k), "wgrad1x1: unsupported shape (N, K multiples of 64)");
+  const float* xc = nullptr;
+  if (xcoef.has_value()) {
+    TORCH_CHECK(xcoef->is_cuda() && xcoef->scalar_type() == at::kFloat && xcoef->is_contiguous() &&
+                    xcoef->numel() == 2 * (int64_t)k,
+                "wgrad1x1: xcoef must be contiguous fp32 [2K]");
+    xc = xcoef->data_ptr<float>();
+  }
+  const c10::hip::HIPGuard guard(g.get_device());
+  const int cus = device_cus(g.get_device());
+  auto dw = at::empty({n, k}, g.options().dtype(out_dtype.value_or(g.scalar_type())));
+  auto ws = at::empty({conv1x1_wgrad_workspace_floats(m, n, k, cus)}, g.options().dtype(at::kFloat));
+  conv1x1_wgrad(g.data_ptr(), x.data_ptr(), dw.data_ptr(), dtype_code(dw.scalar_type()), m, n, k,
+                dtype_code(g.scalar_type()), xc, ws.data_ptr<float>(), cus, cur_stream());
+  return dw;
+}
+
 }  // namespace
 
 void bind_conv(pybind11::module_& root) {
@@ -121,6 +201,12 @@ void bind_conv(pybind11::module_& root) {
         pybind11::arg("mask") = pybind11::none());
   m.def("wgrad", &wgrad);
   m.def("force_fprop_cfg", &conv_force_fprop_cfg);
+  m.def("bn1x1", &bn1x1, pybind11::arg("a"), pybind11::arg("w"), pybind11::arg("w_kmajor_out") = false,
+        pybind11::arg("pcoef") = pybind11::none(), pybind11::arg("shift") = pybind11::none(),
+        pybind11::arg("stats") = false);
+  m.def("bn_finalize", &bn_finalize);
+  m.def("wgrad1x1", &wgrad1x1, pybind11::arg("g"), pybind11::arg("x"), pybind11::arg("xcoef") = pybind11::none(),
+        pybind11::arg("out_dtype") = pybind11::none());
 }
 
 }  // namespace apex_amd

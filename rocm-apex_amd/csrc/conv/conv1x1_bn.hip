@@ -1,0 +1,608 @@
+// Memory-bound 1x1 convolutions of the ResNet bottleneck as NHWC GEMMs with the batch norm
+// fused in: Y[M, N] = pro(A[M, K]) . W^T, where
+//   * pro = the PRODUCING batch norm's apply + ReLU on the operand load (relu(a * s[k] + t[k])),
+//     so the normalized activation is never written;
+//   * the epilogue emits per-output-channel sum / sum-of-squares partials (about a per-channel
+//     shift) from the fp32 accumulators for the CONSUMING batch norm, so its statistics pass never
+//     re-reads Y.
+// Reference capability: the scale-bias-ReLU-conv-with-BN-statistics graphs of the fused
+// bottleneck (apex/contrib/csrc/bottleneck/bottleneck.cpp:1104-1287) and groupbn's separate
+// stats / apply kernels (apex/contrib/csrc/groupbn/nhwc_batch_norm_kernel.h) — here one gfx950
+// kernel per convolution.
+//
+// Why a dedicated kernel: at ResNet-50 bs 256 every 1x1 conv of stages 1-2 is ~26 GFLOP over
+// 0.25-0.5 GB of activations — 10 us of MFMA against 40-80 us of HBM.  The roofline is the
+// activation stream, so the design is built around reading A exactly once:
+//   * one wave owns 32 output rows x all NC columns of a tile (NC <= 256: CN = NC / 32
+//     v_mfma_f32_32x32x16 accumulator blocks), so A fragments are wave-private and go straight
+//     from HBM into registers (16-byte loads, the MFMA A-operand map) — no LDS round trip;
+//   * the weight tile [NC][K] (<= 133 KB) is loaded ONCE per persistent workgroup into LDS
+//     (rows padded by 16 B: the 32 rows a B-fragment read touches hit distinct 16-B slots);
+//   * A fragments are double-buffered in registers one K-chunk (<= 128 deep) ahead, across tiles;
+//   * epilogue: bf16 round, staged through a wave-private LDS slab 64 columns at a time and
+//     written as 16-byte row vectors; the statistics are per-lane running sums in registers
+//     (the C layout puts one column on each lane), reduced once at the end of the kernel.
+// dgrad (dX = dY . W) is the same kernel with the weight read transposed into the LDS image.
+#include "apex_amd/conv_api.h"
+#include "apex_amd/dispatch.h"
+#include "apex_amd/mfma.h"
+
+#include <stdexcept>
+
+namespace apex_amd {
+namespace c1bn {
+using namespace mfma;
+
+struct Args {
+  const uint16_t* a;    // [M][K]
+  const uint16_t* w;    // !WT: [ncols][K]  WT: [K][ncols]
+  uint16_t* y;          // [M][ncols]
+  int64_t m;
+  int ncols;            // total output columns (blockIdx.y selects NC of them)
+  int ntiles;           // ceil(M / 128)
+  const float* pcoef;   // PRO: [2][K] scale | shift of the producing batch norm (then ReLU)
+  const float* shift;   // STATS: per-output-channel shift [ncols] (nullable = 0)
+  float* part;          // STATS: [2][gridDim.x][ncols] partial sums (S1 slab, then S2 slab)
+};
+
+constexpr int kWaves = 4, kRowsB = kWaves * 32;
+constexpr int kSS = 64 + 8;  // staging row stride (elements): rows h and h+4 land 16 banks apart
+
+template <int NC, int KR, bool PRO>
+constexpr int lds_bytes() {
+  return NC * (KR + 8) * 2 + kWaves * 32 * kSS * 2 + (PRO ? 2 * KR * 4 : 0);
+}
+
+template <typename T, int NC, int KR, bool WT, bool PRO, bool STATS>
+__global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
+  constexpr int BS = KR + 8;                 // B image row stride (elements)
+  constexpr int CN = NC / 32;                // accumulator blocks per wave
+  constexpr int KCH = KR < (NC >= 256 ? 64 : 128) ? KR : (NC >= 256 ? 64 : 128);  // k depth per register chunk
+  constexpr int KC = KCH / 16;               // k-steps per chunk
+  constexpr int NCH = KR / KCH;              // chunks per tile
+  static_assert(NC % 64 == 0 && KR % 64 == 0, "tile shape");
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  uint16_t* bimg = lds;                       // [NC][BS]
+  uint16_t* stg = lds + NC * BS;              // [kWaves][32][kSS]
+  float* pc = reinterpret_cast<float*>(stg + kWaves * 32 * kSS);  // [2][KR]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, lr = lane & 31, lh = lane >> 5;
+  const int col0 = blockIdx.y * NC;
+
+  // ---- weight tile -> LDS, once per workgroup ----
+  if constexpr (!WT) {
+    for (int i = tid; i < NC * KR / 8; i += 256) {
+      const int n = i / (KR / 8), k8 = (i % (KR / 8)) * 8;
+      *reinterpret_cast<uint4*>(bimg + n * BS + k8) =
+          *reinterpret_cast<const uint4*>(p.w + (int64_t)(col0 + n) * KR + k8);
+    }
+  } else {
+    for (int i = tid; i < NC * KR / 8; i += 256) {
+      const int k = i / (NC / 8), n8 = (i % (NC / 8)) * 8;
+      const uint4 v = *reinterpret_cast<const uint4*>(p.w + (int64_t)k * p.ncols + col0 + n8);
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bimg[(n8 + 2 * j) * BS + k] = (uint16_t)(w4[j] & 0xffffu);
+        bimg[(n8 + 2 * j + 1) * BS + k] = (uint16_t)(w4[j] >> 16);
+      }
+    }
+  }
+  if constexpr (PRO)
+    for (int i = tid; i < 2 * KR; i += 256) pc[i] = p.pcoef[i];
+  float sh[CN], s1[CN], s2[CN];
+#pragma unroll
+  for (int cb = 0; cb < CN; ++cb) {
+    sh[cb] = (STATS && p.shift) ? p.shift[col0 + 32 * cb + lr] : 0.f;
+    s1[cb] = s2[cb] = 0.f;
+  }
+  __syncthreads();
+
+  f32x16 acc[CN];
+#pragma unroll
+  for (int cb = 0; cb < CN; ++cb) acc[cb] = zero16();
+
+  auto load = [&](s16x8(&f)[KC], int t, int ch) {
+    int64_t row = (int64_t)t * kRowsB + wid * 32 + lr;
+    if (row >= p.m) row = p.m - 1;  // tail rows: valid memory, masked in the epilogue
+    const uint16_t* src = p.a + row * KR + ch * KCH + 8 * lh;
+#pragma unroll
+    for (int s = 0; s < KC; ++s) f[s] = *reinterpret_cast<const s16x8*>(src + 16 * s);
+  };
+
+  auto compute = [&](const s16x8(&f)[KC], int ch) {
+#pragma unroll
+    for (int s = 0; s < KC; ++s) {
+      s16x8 a = f[s];
+      if constexpr (PRO) {
+        const int kb = ch * KCH + 16 * s + 8 * lh;
+        const float4 c0 = *reinterpret_cast<const float4*>(pc + kb);
+        const float4 c1 = *reinterpret_cast<const float4*>(pc + kb + 4);
+        const float4 d0 = *reinterpret_cast<const float4*>(pc + KR + kb);
+        const float4 d1 = *reinterpret_cast<const float4*>(pc + KR + kb + 4);
+        const float sc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        const float sf[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = fmaxf(fmaf(to_f(T{(uint16_t)a[j]}), sc[j], sf[j]), 0.f);
+          a[j] = (short)from_f<T>(v).x;
+        }
+      }
+#pragma unroll
+      for (int cb = 0; cb < CN; ++cb) {
+        const s16x8 b = *reinterpret_cast<const s16x8*>(bimg + (32 * cb + lr) * BS + ch * KCH + 16 * s + 8 * lh);
+        acc[cb] = mma<T>(a, b, acc[cb]);
+      }
+    }
+  };
+
+  auto epilogue = [&](int t) {
+    const int64_t row0 = (int64_t)t * kRowsB + wid * 32;
+    if constexpr (STATS) {
+#pragma unroll
+      for (int cb = 0; cb < CN; ++cb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          if (row0 + crow(r, lh) < p.m) {
+            const float d = acc[cb][r] - sh[cb];
+            s1[cb] += d;
+            s2[cb] = fmaf(d, d, s2[cb]);
+          }
+        }
+    }
+    uint16_t* st = stg + wid * 32 * kSS;
+#pragma unroll
+    for (int g = 0; g < CN / 2; ++g) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) st[crow(r, lh) * kSS + 32 * q + lr] = from_f<T>(acc[2 * g + q][r]).x;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int qid = lane + 64 * i, rr = qid >> 3, c8 = (qid & 7) * 8;
+        const uint4 v = *reinterpret_cast<const uint4*>(st + rr * kSS + c8);
+        if (row0 + rr < p.m)
+          *reinterpret_cast<uint4*>(p.y + (row0 + rr) * p.ncols + col0 + 64 * g + c8) = v;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+#pragma unroll
+    for (int cb = 0; cb < CN; ++cb) acc[cb] = zero16();
+  };
+
+  // flat (tile, chunk) stream, the next chunk's loads in flight under the current one's MFMAs
+  s16x8 fa[KC], fb[KC];
+  int t = blockIdx.x, ch = 0;
+  if (t < p.ntiles) load(fa, t, 0);
+  while (t < p.ntiles) {
+    {
+      int nt = t, nch = ch + 1;
+      if (nch == NCH) { nch = 0; nt += gridDim.x; }
+      if (nt < p.ntiles) load(fb, nt, nch);
+      compute(fa, ch);
+      if (ch == NCH - 1) epilogue(t);
+      t = nt;
+      ch = nch;
+    }
+    if (t >= p.ntiles) break;
+    {
+      int nt = t, nch = ch + 1;
+      if (nch == NCH) { nch = 0; nt += gridDim.x; }
+      if (nt < p.ntiles) load(fa, nt, nch);
+      compute(fb, ch);
+      if (ch == NCH - 1) epilogue(t);
+      t = nt;
+      ch = nch;
+    }
+  }
+
+  if constexpr (STATS) {
+    float* red = reinterpret_cast<float*>(stg);  // [kWaves][2][NC] (8 KB at NC = 256 <= staging slab)
+#pragma unroll
+    for (int cb = 0; cb < CN; ++cb) {
+      s1[cb] += __shfl_xor(s1[cb], 32, 64);
+      s2[cb] += __shfl_xor(s2[cb], 32, 64);
+    }
+    __syncthreads();
+    if (lh == 0) {
+#pragma unroll
+      for (int cb = 0; cb < CN; ++cb) {
+        red[(wid * 2 + 0) * NC + 32 * cb + lr] = s1[cb];
+        red[(wid * 2 + 1) * NC + 32 * cb + lr] = s2[cb];
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < 2 * NC; i += 256) {
+      const int which = i / NC, n = i % NC;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) v += red[(w * 2 + which) * NC + n];
+      p.part[((int64_t)which * gridDim.x + blockIdx.x) * p.ncols + col0 + n] = v;
+    }
+  }
+}
+
+// ---- statistics finalize: fixed-order sum of the per-workgroup partials -> batch mean /
+// inv_std, the running-stat EMA and the apply coefficients coef = [scale | shift] ----
+__global__ void __launch_bounds__(256) stats_finalize(const float* __restrict__ part, int g, int c, float n,
+                                                      const float* __restrict__ shift, const float* __restrict__ w,
+                                                      const float* __restrict__ b, float eps, float momentum,
+                                                      float* __restrict__ rmean, float* __restrict__ rvar,
+                                                      float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                                      float* __restrict__ coef) {
+  // 8 channels x 32 partial-row groups per block (the finalize is latency-bound)
+  __shared__ float red[2][32][9];
+  const int lc = threadIdx.x & 7, grp = threadIdx.x >> 3, ch = blockIdx.x * 8 + lc;
+  float a = 0.f, q = 0.f;
+  if (ch < c)
+    for (int j = grp; j < g; j += 32) {
+      a += part[(int64_t)j * c + ch];
+      q += part[(int64_t)(g + j) * c + ch];
+    }
+  red[0][grp][lc] = a;
+  red[1][grp][lc] = q;
+  __syncthreads();
+  if (grp != 0 || ch >= c) return;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll 8
+  for (int i = 0; i < 32; ++i) {
+    s1 += red[0][i][lc];
+    s2 += red[1][i][lc];
+  }
+  const float sft = shift ? shift[ch] : 0.f;
+  const float dm = s1 / n;
+  const float var_b = fmaxf(s2 / n - dm * dm, 0.f);
+  const float mm = sft + dm;
+  const float istd = rsqrtf(var_b + eps);
+  save_mean[ch] = mm;
+  save_invstd[ch] = istd;
+  const float sc = istd * (w ? w[ch] : 1.f);
+  coef[ch] = sc;
+  coef[c + ch] = (b ? b[ch] : 0.f) - mm * sc;
+  if (rmean) rmean[ch] = (1.f - momentum) * rmean[ch] + momentum * mm;
+  if (rvar) rvar[ch] = (1.f - momentum) * rvar[ch] + momentum * (n > 1.f ? var_b * n / (n - 1.f) : var_b);
+}
+
+template <typename T, int NC, int KR, bool WT, bool PRO, bool STATS>
+void launch_t(const Args& a, int cus, hipStream_t s) {
+  constexpr int lds = lds_bytes<NC, KR, PRO>();
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&fused1x1<T, NC, KR, WT, PRO, STATS>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  const int per_cu = (160 * 1024) / lds >= 2 ? 2 : 1;
+  int gx = cus * per_cu;
+  if (gx > a.ntiles) gx = a.ntiles;
+  hipLaunchKernelGGL((fused1x1<T, NC, KR, WT, PRO, STATS>), dim3(gx, a.ncols / NC), dim3(256), lds, s, a);
+}
+
+inline int grid_x(int64_t m, int nc, int kr, bool pro, int cus) {
+  const int lds = nc * (kr + 8) * 2 + kWaves * 32 * kSS * 2 + (pro ? 2 * kr * 4 : 0);
+  const int per_cu = (160 * 1024) / lds >= 2 ? 2 : 1;
+  const int ntiles = (int)((m + kRowsB - 1) / kRowsB);
+  const int gx = cus * per_cu;
+  return gx < ntiles ? gx : ntiles;
+}
+
+// column tile: the widest of 256 / 128 / 64 that divides ncols (256 needs the 128 accumulator
+// registers of 8 blocks; the register file holds it at 2 waves / SIMD)
+inline int col_tile(int ncols) { return ncols % 256 == 0 ? 256 : ncols % 128 == 0 ? 128 : 64; }
+
+template <typename T, bool WT, bool PRO, bool STATS>
+void dispatch_shape(const Args& a, int nc, int kr, int cus, hipStream_t s) {
+#define C1BN_CASE(NC_, KR_)                                 \
+  if (nc == NC_ && kr == KR_) {                             \
+    launch_t<T, NC_, KR_, WT, PRO, STATS>(a, cus, s);       \
+    return;                                                 \
+  }
+  C1BN_CASE(64, 64) C1BN_CASE(64, 128) C1BN_CASE(64, 256) C1BN_CASE(64, 512)
+  C1BN_CASE(128, 64) C1BN_CASE(128, 128) C1BN_CASE(128, 256) C1BN_CASE(128, 512)
+  C1BN_CASE(256, 64) C1BN_CASE(256, 128) C1BN_CASE(256, 256)
+#undef C1BN_CASE
+  throw std::runtime_error("conv1x1_bn: unsupported (columns, reduction) tile");
+}
+
+}  // namespace c1bn
+
+bool conv1x1_bn_supported(int64_t m, int k, int ncols) {
+  if (m <= 0 || ncols % 64 != 0 || ncols <= 0) return false;
+  if (!(k == 64 || k == 128 || k == 256 || k == 512)) return false;
+  const int nc = c1bn::col_tile(ncols);
+  return !(nc == 256 && k == 512);
+}
+
+int conv1x1_bn_partials(int64_t m, int k, int ncols, bool pro, int cus) {
+  return c1bn::grid_x(m, c1bn::col_tile(ncols), k, pro, cus);
+}
+
+void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int ncols, bool w_kmajor_out, int dtype,
+                const float* pcoef, const float* shift, float* part, int cus, hipStream_t s) {
+  if (!conv1x1_bn_supported(m, k, ncols)) throw std::runtime_error("conv1x1_bn: unsupported shape");
+  c1bn::Args args;
+  args.a = static_cast<const uint16_t*>(a);
+  args.w = static_cast<const uint16_t*>(w);
+  args.y = static_cast<uint16_t*>(y);
+  args.m = m;
+  args.ncols = ncols;
+  args.ntiles = (int)((m + c1bn::kRowsB - 1) / c1bn::kRowsB);
+  args.pcoef = pcoef;
+  args.shift = shift;
+  args.part = part;
+  const int nc = c1bn::col_tile(ncols);
+  const bool wt = w_kmajor_out;
+  const bool pro = pcoef != nullptr, stats = part != nullptr;
+  auto go = [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    if (wt) {
+      if (pro || stats) throw std::runtime_error("conv1x1_bn: the transposed-weight (dgrad) form has no BN fusion");
+      c1bn::dispatch_shape<T, true, false, false>(args, nc, k, cus, s);
+    } else if (pro) {
+      if (stats) c1bn::dispatch_shape<T, false, true, true>(args, nc, k, cus, s);
+      else c1bn::dispatch_shape<T, false, true, false>(args, nc, k, cus, s);
+    } else {
+      if (stats) c1bn::dispatch_shape<T, false, false, true>(args, nc, k, cus, s);
+      else c1bn::dispatch_shape<T, false, false, false>(args, nc, k, cus, s);
+    }
+  };
+  dispatch_16(dtype, go, "conv1x1_bn");
+  check_launch("conv1x1_bn");
+}
+
+void conv1x1_bn_finalize(const float* part, int g, int c, float n, const float* shift, const float* w, const float* b,
+                         float eps, float momentum, float* rmean, float* rvar, float* save_mean, float* save_invstd,
+                         float* coef, hipStream_t s) {
+  hipLaunchKernelGGL(c1bn::stats_finalize, dim3((c + 7) / 8), dim3(256), 0, s, part, g, c, n, shift, w, b, eps,
+                     momentum, rmean, rvar, save_mean, save_invstd, coef);
+  check_launch("conv1x1_bn_finalize");
+}
+
+// =============================================================================================
+// Weight gradient of a 1x1 convolution with the producing batch norm (+ReLU) applied to the
+// activation on load: dW[n][k] = sum_m G[m][n] . pro(X[m][k]), G = dY [M][N], X [M][K].
+// Split over M (the pixels): each workgroup owns a [NT][KT] block of dW for a contiguous row
+// range, streams 64-row chunks of G and X global -> registers (pro applied once per element
+// here) -> LDS (row-major images, rows padded so the 4 rows a 16-lane transposed read touches
+// start 64 B apart in the bank space), and feeds the MFMAs with ds_read_b64_tr_b16 fragments
+// (both operands are m-major).  The next chunk's loads are in flight under the current chunk's
+// MFMAs; one barrier per chunk.  fp32 partials [S][N][K] are summed in a fixed order by
+// wgrad_reduce (deterministic, no atomics).
+// =============================================================================================
+namespace c1w {
+using namespace mfma;
+
+struct Args {
+  const uint16_t* g;   // [M][N]
+  const uint16_t* x;   // [M][K]
+  float* ws;           // [S][N][K]
+  int64_t m;
+  int n, k;
+  int64_t rows;        // rows per split (multiple of 64)
+  const float* xcoef;  // PRO: [2][K] scale | shift, pro(x) = relu(x * scale + shift)
+};
+
+constexpr int MB = 64;
+
+template <int NT, int KT>
+constexpr int lds_bytes() {
+  return 2 * MB * ((NT + 32) + (KT + 32)) * 2;
+}
+
+template <typename T, int NT, int KT, bool PRO>
+__global__ void __launch_bounds__(256, 1) wgrad1x1(Args p) {
+  constexpr int GS = NT + 32, XS = KT + 32;   // LDS row strides (elements)
+  constexpr int GL = MB * NT / 8 / 256;       // 16-byte loads per thread per chunk
+  constexpr int XL = MB * KT / 8 / 256;
+  constexpr int WN = NT / 64, WK = KT / 64;   // 32x32 blocks per wave (2 x 2 waves)
+  static_assert(GL >= 1 && XL >= 1 && WN * WK <= 8, "wgrad tile");
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, lr = lane & 31, lh = lane >> 5;
+  const int wn = wid & 1, wk = wid >> 1;
+  const int n0 = blockIdx.y * NT, k0 = blockIdx.z * KT;
+  const int64_t r0 = (int64_t)blockIdx.x * p.rows;
+  const int64_t r1 = r0 + p.rows < p.m ? r0 + p.rows : p.m;
+
+  // this thread's X columns are the same for every load (256 is a multiple of KT / 8)
+  const int xc8 = (tid % (KT / 8)) * 8;
+  float xs[8], xb[8];
+  if constexpr (PRO) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      xs[j] = p.xcoef[k0 + xc8 + j];
+      xb[j] = p.xcoef[p.k + k0 + xc8 + j];
+    }
+  }
+
+  uint4 gr[GL], xr[XL];
+  auto gload = [&](int64_t base) {
+#pragma unroll
+    for (int i = 0; i < GL; ++i) {
+      const int idx = tid + 256 * i, row = idx / (NT / 8), c8 = (idx % (NT / 8)) * 8;
+      const int64_t rr = base + row;
+      gr[i] = rr < r1 ? *reinterpret_cast<const uint4*>(p.g + rr * p.n + n0 + c8) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < XL; ++i) {
+      const int idx = tid + 256 * i, row = idx / (KT / 8);
+      const int64_t rr = base + row;
+      xr[i] = rr < r1 ? *reinterpret_cast<const uint4*>(p.x + rr * p.k + k0 + xc8) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto lwrite = [&](int buf) {
+    uint16_t* gi = lds + buf * MB * (GS + XS);
+    uint16_t* xi = gi + MB * GS;
+#pragma unroll
+    for (int i = 0; i < GL; ++i) {
+      const int idx = tid + 256 * i, row = idx / (NT / 8), c8 = (idx % (NT / 8)) * 8;
+      *reinterpret_cast<uint4*>(gi + row * GS + c8) = gr[i];
+    }
+#pragma unroll
+    for (int i = 0; i < XL; ++i) {
+      const int idx = tid + 256 * i, row = idx / (KT / 8);
+      uint4 v = xr[i];
+      if constexpr (PRO) {
+        uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float lo = fmaxf(fmaf(to_f(T{(uint16_t)(w4[j] & 0xffffu)}), xs[2 * j], xb[2 * j]), 0.f);
+          const float hi = fmaxf(fmaf(to_f(T{(uint16_t)(w4[j] >> 16)}), xs[2 * j + 1], xb[2 * j + 1]), 0.f);
+          w4[j] = (uint32_t)from_f<T>(lo).x | ((uint32_t)from_f<T>(hi).x << 16);
+        }
+        v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      }
+      *reinterpret_cast<uint4*>(xi + row * XS + xc8) = v;
+    }
+  };
+
+  f32x16 acc[WN][WK];
+#pragma unroll
+  for (int i = 0; i < WN; ++i)
+#pragma unroll
+    for (int j = 0; j < WK; ++j) acc[i][j] = zero16();
+
+  auto compute = [&](int buf) {
+    const uint16_t* gi = lds + buf * MB * (GS + XS);
+    const uint16_t* xi = gi + MB * GS;
+#pragma unroll
+    for (int kk = 0; kk < MB / 16; ++kk) {
+      const int klo = 16 * kk + 8 * lh;
+      s16x8 a[WN], b[WK];
+#pragma unroll
+      for (int i = 0; i < WN; ++i) a[i] = frag_tr<GS>(gi, wn * (NT / 2) + 32 * i, klo, klo + 4, lane);
+#pragma unroll
+      for (int j = 0; j < WK; ++j) b[j] = frag_tr<XS>(xi, wk * (KT / 2) + 32 * j, klo, klo + 4, lane);
+#pragma unroll
+      for (int i = 0; i < WN; ++i)
+#pragma unroll
+        for (int j = 0; j < WK; ++j) acc[i][j] = mma<T>(a[i], b[j], acc[i][j]);
+    }
+  };
+
+  int buf = 0;
+  if (r0 < r1) {
+    gload(r0);
+    lwrite(0);
+  }
+  __syncthreads();
+  for (int64_t base = r0; base < r1; base += MB) {
+    const bool more = base + MB < r1;
+    if (more) gload(base + MB);
+    compute(buf);
+    if (more) lwrite(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  float* out = p.ws + (int64_t)blockIdx.x * p.n * p.k;
+#pragma unroll
+  for (int i = 0; i < WN; ++i)
+#pragma unroll
+    for (int j = 0; j < WK; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int nn = n0 + wn * (NT / 2) + 32 * i + crow(r, lh);
+        const int kc = k0 + wk * (KT / 2) + 32 * j + lr;
+        out[(int64_t)nn * p.k + kc] = acc[i][j][r];
+      }
+}
+
+// dW = sum over the S split partials in a fixed order, 8 consecutive elements per thread
+template <typename TO>
+__global__ void __launch_bounds__(256) wgrad_reduce(const float* __restrict__ ws, int s, int64_t nk,
+                                                    TO* __restrict__ out) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i >= nk) return;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int q = 0; q < s; ++q) {
+    float v[8];
+    Vec8<float>::load(v, ws + (int64_t)q * nk + i);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] += v[j];
+  }
+  Vec8<TO>::store(out + i, a);
+}
+
+// tile: 256 x 64, 64 x 256, 128 x 128 (16K accumulators / workgroup) or a 256 x 128 / 128 x 256
+// block (32K) when the other dimension is read once either way
+inline void tile(int n, int k, int& nt, int& kt) {
+  if (k == 64) { nt = n % 256 == 0 ? 256 : 128; kt = 64; }
+  else if (n == 64) { nt = 64; kt = k % 256 == 0 ? 256 : 128; }
+  else if (n % 256 == 0 && k % 128 == 0) { nt = 256; kt = 128; }
+  else if (k % 256 == 0 && n % 128 == 0) { nt = 128; kt = 256; }
+  else { nt = 128; kt = 128; }
+}
+
+inline int splits(int64_t m, int n, int k, int cus) {
+  int nt, kt;
+  tile(n, k, nt, kt);
+  const int tiles = (n / nt) * (k / kt);
+  int s = (cus + tiles - 1) / tiles;
+  const int64_t maxs = (m + MB - 1) / MB;
+  if (s > maxs) s = (int)maxs;
+  return s < 1 ? 1 : s;
+}
+
+template <typename T, bool PRO>
+void launch(const Args& a, int s, int cus, hipStream_t st) {
+  int nt, kt;
+  tile(a.n, a.k, nt, kt);
+  dim3 grid(s, a.n / nt, a.k / kt);
+#define C1W_CASE(NT_, KT_)                                                                                 \
+  if (nt == NT_ && kt == KT_) {                                                                            \
+    constexpr int lds = lds_bytes<NT_, KT_>();                                                             \
+    static bool attr = false;                                                                              \
+    if (!attr) {                                                                                           \
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad1x1<T, NT_, KT_, PRO>),                      \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, lds);                                \
+      attr = true;                                                                                         \
+    }                                                                                                      \
+    hipLaunchKernelGGL((wgrad1x1<T, NT_, KT_, PRO>), grid, dim3(256), lds, st, a);                         \
+    return;                                                                                                \
+  }
+  C1W_CASE(256, 64) C1W_CASE(128, 64) C1W_CASE(64, 256) C1W_CASE(64, 128) C1W_CASE(256, 128)
+  C1W_CASE(128, 256) C1W_CASE(128, 128)
+#undef C1W_CASE
+  (void)cus;
+  throw std::runtime_error("conv1x1 wgrad: no tile");
+}
+
+}  // namespace c1w
+
+bool conv1x1_wgrad_supported(int64_t m, int n, int k) {
+  return m > 0 && n % 64 == 0 && k % 64 == 0 && n >= 64 && k >= 64 && (n % 128 == 0 || k % 128 == 0 || n == 64);
+}
+
+int64_t conv1x1_wgrad_workspace_floats(int64_t m, int n, int k, int cus) {
+  return (int64_t)c1w::splits(m, n, k, cus) * n * k;
+}
+
+void conv1x1_wgrad(const void* g, const void* x, void* dw, int out_dtype, int64_t m, int n, int k, int dtype,
+                   const float* xcoef, float* ws, int cus, hipStream_t s) {
+  if (!conv1x1_wgrad_supported(m, n, k)) throw std::runtime_error("conv1x1 wgrad: unsupported shape");
+  c1w::Args a;
+  a.g = static_cast<const uint16_t*>(g);
+  a.x = static_cast<const uint16_t*>(x);
+  a.ws = ws;
+  a.m = m;
+  a.n = n;
+  a.k = k;
+  a.xcoef = xcoef;
+  const int sp = c1w::splits(m, n, k, cus);
+  a.rows = ((m + sp - 1) / sp + c1w::MB - 1) / c1w::MB * c1w::MB;
+  dispatch_16(dtype, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    if (xcoef) c1w::launch<T, true>(a, sp, cus, s);
+    else c1w::launch<T, false>(a, sp, cus, s);
+  }, "conv1x1 wgrad");
+  const int64_t nk = (int64_t)n * k;
+  const unsigned blocks = (unsigned)((nk / 8 + 255) / 256);
+  dispatch_float(out_dtype, [&](auto tag) {
+    using TO = typename decltype(tag)::type;
+    hipLaunchKernelGGL((c1w::wgrad_reduce<TO>), dim3(blocks), dim3(256), 0, s, ws, sp, nk, static_cast<TO*>(dw));
+  }, "conv1x1 wgrad reduce");
+  check_launch("conv1x1_wgrad");
+}
+
+}  // namespace apex_amd

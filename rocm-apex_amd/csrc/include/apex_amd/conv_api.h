@@ -59,4 +59,28 @@ int64_t conv_wgrad_workspace_floats(const ConvTapArgs& a, int cus);
 void conv_wgrad(const ConvTapArgs& a, const void* dy, void* dw_out, int out_dtype, float* ws, int cus,
                 hipStream_t s);
 
+// ---- memory-bound 1x1 convolutions with the batch norm fused in (csrc/conv/conv1x1_bn.hip) ----
+// y[M][ncols] = pro(a[M][k]) . W^T with W [ncols][k] (forward) or, w_kmajor_out, W [k][ncols]
+// (data gradient dX = dY . W of a [k-out][ncols-in] conv weight).  pcoef (nullable, [2][k]
+// scale | shift): pro(a) = relu(a * scale + shift), the producing batch norm applied on load.
+// part (nullable, [2][G][ncols] with G = conv1x1_bn_partials(...)): per-workgroup sums of
+// (y - shift) and (y - shift)^2 for the consuming batch norm, finalized by conv1x1_bn_finalize.
+// Shapes: k in {64, 128, 256, 512}, ncols % 64 == 0, bf16 / fp16, 16-byte aligned rows.
+bool conv1x1_bn_supported(int64_t m, int k, int ncols);
+int conv1x1_bn_partials(int64_t m, int k, int ncols, bool pro, int cus);
+void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int ncols, bool w_kmajor_out, int dtype,
+                const float* pcoef, const float* shift, float* part, int cus, hipStream_t s);
+// batch statistics from the partials: save_mean / save_invstd, running-stat EMA (nullable),
+// coef = [scale | shift] of the apply (w, b nullable = affine-free)
+void conv1x1_bn_finalize(const float* part, int g, int c, float n, const float* shift, const float* w, const float* b,
+                         float eps, float momentum, float* rmean, float* rvar, float* save_mean, float* save_invstd,
+                         float* coef, hipStream_t s);
+
+// dW [n][k] (out_dtype) = sum_m g[m][n] . pro(x[m][k]), pro = relu(x * xcoef[k] + xcoef[K + k]) when
+// xcoef is non-null; fp32 split partials in ws (conv1x1_wgrad_workspace_floats), fixed-order sum
+bool conv1x1_wgrad_supported(int64_t m, int n, int k);
+int64_t conv1x1_wgrad_workspace_floats(int64_t m, int n, int k, int cus);
+void conv1x1_wgrad(const void* g, const void* x, void* dw, int out_dtype, int64_t m, int n, int k, int dtype,
+                   const float* xcoef, float* ws, int cus, hipStream_t s);
+
 }  // namespace apex_amd

@@ -1,0 +1,127 @@
+"""BN-fused 1x1 convolution kernels (csrc/conv/conv1x1_bn.hip, ``apex._C.conv.bn1x1``):
+y = pro(a) . W^T with the producing batch norm's apply + ReLU on the operand load, the consuming
+batch norm's statistics partials in the epilogue, and the transposed-weight (data gradient) form —
+each against the fp32 PyTorch composition of the same bf16/fp16 operands."""
+import pytest
+import torch
+
+SHAPES = [
+    # m, k, ncols
+    (128, 64, 64),
+    (1000, 64, 256),      # tail tile (m % 128 != 0)
+    (4096, 256, 64),
+    (2048, 256, 128),
+    (3000, 128, 512),     # two 256-column groups
+    (1536, 512, 128),
+    (777, 128, 192),      # 64-column tile, odd row count
+]
+
+
+def _ext():
+    import apex
+
+    return apex._native.require("conv").conv
+
+
+def _close(a, b, tol):
+    scale = max(1.0, float(b.abs().max()))
+    err = float((a.float() - b.float()).abs().max())
+    assert err <= tol * scale, (err, scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("m,k,nc", SHAPES)
+@pytest.mark.parametrize("pro", [False, True])
+def test_gpu_bn1x1_forward_and_stats(dtype, m, k, nc, pro):
+    ext = _ext()
+    torch.manual_seed(0)
+    a = (torch.randn(m, k, device="cuda") * 2 + 0.5).to(dtype)
+    w = (torch.randn(nc, k, device="cuda") * 0.1).to(dtype)
+    pcoef = torch.cat([torch.rand(k, device="cuda") + 0.5, torch.randn(k, device="cuda") * 0.3]) if pro else None
+    shift = torch.randn(nc, device="cuda") * 0.1
+    y, part = ext.bn1x1(a, w, False, pcoef, shift, True)
+    af = a.float()
+    if pro:
+        af = torch.relu(af * pcoef[:k] + pcoef[k:]).to(dtype).float()
+    yr = af @ w.float().t()
+    assert y.shape == (m, nc) and y.dtype == dtype
+    _close(y, yr, 1e-2)
+    # statistics: partials of the fp32 accumulators about `shift`, then the finalize
+    rm = torch.zeros(nc, device="cuda")
+    rv = torch.ones(nc, device="cuda")
+    gam = torch.rand(nc, device="cuda") + 0.5
+    bet = torch.randn(nc, device="cuda")
+    sm, si, coef = ext.bn_finalize(part, float(m), shift, gam, bet, rm, rv, 1e-5, 0.1)
+    mean, var = yr.mean(0), yr.var(0, unbiased=False)
+    torch.testing.assert_close(sm, mean, atol=2e-3 * float(yr.std()), rtol=1e-3)
+    torch.testing.assert_close(si, torch.rsqrt(var + 1e-5), atol=0, rtol=3e-3)
+    torch.testing.assert_close(coef[:nc], gam * torch.rsqrt(var + 1e-5), atol=0, rtol=3e-3)
+    torch.testing.assert_close(rm, 0.1 * mean, atol=2e-4 * float(yr.std()), rtol=1e-3)
+    torch.testing.assert_close(rv, 0.9 + 0.1 * yr.var(0, unbiased=True), atol=0, rtol=3e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("m,k,nc", SHAPES)
+def test_gpu_bn1x1_dgrad_form(dtype, m, k, nc):
+    """w_kmajor_out: y = a . W with W [k, ncols] (the data gradient of a [k-out, ncols-in] conv)."""
+    ext = _ext()
+    torch.manual_seed(1)
+    a = torch.randn(m, k, device="cuda").to(dtype)
+    w = (torch.randn(k, nc, device="cuda") * 0.1).to(dtype)
+    y, part = ext.bn1x1(a, w, True)
+    assert part.numel() == 0
+    _close(y, a.float() @ w.float(), 1e-2)
+
+
+@pytest.mark.gpu
+def test_gpu_bn1x1_large_mean_shift():
+    """A channel mean far from zero: the running-mean shift keeps the variance accurate."""
+    ext = _ext()
+    torch.manual_seed(2)
+    m, k, nc = 65536, 64, 64
+    a = torch.randn(m, k, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(nc, k, device="cuda") * 0.02).to(torch.bfloat16)
+    w[:, 0] = 1.0
+    a[:, 0] = 300.0  # every output channel ~ 300 + small noise
+    yr = a.float() @ w.float().t()
+    shift = yr[:64].mean(0)  # a running-mean-like estimate
+    _, part = ext.bn1x1(a, w, False, None, shift, True)
+    sm, si, _ = ext.bn_finalize(part, float(m), shift, None, None, None, None, 1e-5, 0.1)
+    torch.testing.assert_close(si, torch.rsqrt(yr.var(0, unbiased=False) + 1e-5), atol=0, rtol=1e-2)
+
+
+WGRAD_SHAPES = [
+    # m, n (grad channels), k (activation channels)
+    (1000, 256, 64),
+    (4096, 64, 256),
+    (2048, 128, 128),
+    (3000, 512, 128),
+    (1536, 128, 512),
+    (640, 128, 64),
+    (5000, 64, 128),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("m,n,k", WGRAD_SHAPES)
+@pytest.mark.parametrize("pro", [False, True])
+def test_gpu_wgrad1x1(dtype, m, n, k, pro):
+    """dW = g^T . pro(x) against fp32 torch, pro = the producing BN's apply + ReLU."""
+    ext = _ext()
+    torch.manual_seed(3)
+    g = torch.randn(m, n, device="cuda").to(dtype)
+    x = (torch.randn(m, k, device="cuda") + 0.3).to(dtype)
+    xcoef = torch.cat([torch.rand(k, device="cuda") + 0.5, torch.randn(k, device="cuda") * 0.3]) if pro else None
+    xf = x.float()
+    if pro:
+        xf = torch.relu(xf * xcoef[:k] + xcoef[k:]).to(dtype).float()
+    ref = g.float().t() @ xf
+    dw = ext.wgrad1x1(g, x, xcoef, torch.float32)
+    assert dw.shape == (n, k)
+    _close(dw, ref, 2e-3)
+    dw16 = ext.wgrad1x1(g, x, xcoef)
+    assert dw16.dtype == dtype
+    _close(dw16, ref, 1e-2)
