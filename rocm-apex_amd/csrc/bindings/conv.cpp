@@ -112,7 +112,7 @@ void wgrad(const at::Tensor& in, const at::Tensor& dy, at::Tensor& dw_out, int64
 // y = pro(a) . W^T (+ BN statistics partials); see conv_api.h.  Returns (y, part or empty).
 std::vector<at::Tensor> bn1x1(const at::Tensor& a, const at::Tensor& w, bool w_kmajor_out,
                               const c10::optional<at::Tensor>& pcoef, const c10::optional<at::Tensor>& shift,
-                              bool stats) {
+                              bool stats, const c10::optional<at::Tensor>& res) {
   TORCH_CHECK(a.is_cuda() && a.dim() == 2 && a.is_contiguous(), "bn1x1: a must be a contiguous [M, K] GPU tensor");
   TORCH_CHECK(w.is_cuda() && w.dim() == 2 && w.is_contiguous() && w.scalar_type() == a.scalar_type(),
               "bn1x1: w must be a contiguous 2-D tensor of a's dtype");
@@ -135,8 +135,12 @@ std::vector<at::Tensor> bn1x1(const at::Tensor& a, const at::Tensor& w, bool w_k
   at::Tensor part;
   if (stats)
     part = at::empty({2, conv1x1_bn_partials(m, k, ncols, pc != nullptr, cus), ncols}, a.options().dtype(at::kFloat));
+  if (res.has_value())
+    TORCH_CHECK(res->is_cuda() && res->is_contiguous() && res->scalar_type() == a.scalar_type() &&
+                    res->numel() == m * ncols,
+                "bn1x1: res must be a contiguous [M, ncols] tensor of a's dtype");
   conv1x1_bn(a.data_ptr(), w.data_ptr(), y.data_ptr(), m, k, ncols, w_kmajor_out, dtype_code(a.scalar_type()), pc, sh,
-             stats ? part.data_ptr<float>() : nullptr, cus, cur_stream());
+             stats ? part.data_ptr<float>() : nullptr, cus, cur_stream(), res.has_value() ? res->data_ptr() : nullptr);
   return {y, part};
 }
 
@@ -203,7 +207,7 @@ void bind_conv(pybind11::module_& root) {
   m.def("force_fprop_cfg", &conv_force_fprop_cfg);
   m.def("bn1x1", &bn1x1, pybind11::arg("a"), pybind11::arg("w"), pybind11::arg("w_kmajor_out") = false,
         pybind11::arg("pcoef") = pybind11::none(), pybind11::arg("shift") = pybind11::none(),
-        pybind11::arg("stats") = false);
+        pybind11::arg("stats") = false, pybind11::arg("res") = pybind11::none());
   m.def("bn_finalize", &bn_finalize);
   m.def("wgrad1x1", &wgrad1x1, pybind11::arg("g"), pybind11::arg("x"), pybind11::arg("xcoef") = pybind11::none(),
         pybind11::arg("out_dtype") = pybind11::none());

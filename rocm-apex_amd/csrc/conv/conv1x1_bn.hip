@@ -43,6 +43,7 @@ struct Args {
   const float* pcoef;   // PRO: [2][K] scale | shift of the producing batch norm (then ReLU)
   const float* shift;   // STATS: per-output-channel shift [ncols] (nullable = 0)
   float* part;          // STATS: [2][gridDim.x][ncols] partial sums (S1 slab, then S2 slab)
+  const uint16_t* res;  // nullable [M][ncols]: y += res before the store (a residual gradient)
 };
 
 constexpr int kWaves = 4, kRowsB = kWaves * 32;
@@ -161,9 +162,19 @@ __global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int qid = lane + 64 * i, rr = qid >> 3, c8 = (qid & 7) * 8;
-        const uint4 v = *reinterpret_cast<const uint4*>(st + rr * kSS + c8);
-        if (row0 + rr < p.m)
-          *reinterpret_cast<uint4*>(p.y + (row0 + rr) * p.ncols + col0 + 64 * g + c8) = v;
+        uint4 v = *reinterpret_cast<const uint4*>(st + rr * kSS + c8);
+        const int64_t off = (row0 + rr) * p.ncols + col0 + 64 * g + c8;
+        if (row0 + rr < p.m) {
+          if (p.res) {  // wave-uniform branch
+            float a[8], b[8];
+            Vec8<T>::load(a, reinterpret_cast<const T*>(&v));
+            Vec8<T>::load(b, reinterpret_cast<const T*>(p.res + off));
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a[j] += b[j];
+            Vec8<T>::store(reinterpret_cast<T*>(&v), a);
+          }
+          *reinterpret_cast<uint4*>(p.y + off) = v;
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
@@ -269,7 +280,7 @@ void launch_t(const Args& a, int cus, hipStream_t s) {
   constexpr int lds = lds_bytes<NC, KR, PRO>();
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&fused1x1<T, NC, KR, WT, PRO, STATS>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fused1x1<T, NC, KR, WT, PRO, STATS>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
@@ -288,8 +299,12 @@ inline int grid_x(int64_t m, int nc, int kr, bool pro, int cus) {
 }
 
 // column tile: the widest of 256 / 128 / 64 that divides ncols (256 needs the 128 accumulator
-// registers of 8 blocks; the register file holds it at 2 waves / SIMD)
-inline int col_tile(int ncols) { return ncols % 256 == 0 ? 256 : ncols % 128 == 0 ? 128 : 64; }
+// registers of 8 blocks; the register file holds it at 2 waves / SIMD; at k = 512 its weight
+// image would not fit the LDS)
+inline int col_tile(int ncols, int kr) {
+  if (ncols % 256 == 0 && kr <= 256) return 256;
+  return ncols % 128 == 0 ? 128 : 64;
+}
 
 template <typename T, bool WT, bool PRO, bool STATS>
 void dispatch_shape(const Args& a, int nc, int kr, int cus, hipStream_t s) {
@@ -310,16 +325,15 @@ void dispatch_shape(const Args& a, int nc, int kr, int cus, hipStream_t s) {
 bool conv1x1_bn_supported(int64_t m, int k, int ncols) {
   if (m <= 0 || ncols % 64 != 0 || ncols <= 0) return false;
   if (!(k == 64 || k == 128 || k == 256 || k == 512)) return false;
-  const int nc = c1bn::col_tile(ncols);
-  return !(nc == 256 && k == 512);
+  return true;
 }
 
 int conv1x1_bn_partials(int64_t m, int k, int ncols, bool pro, int cus) {
-  return c1bn::grid_x(m, c1bn::col_tile(ncols), k, pro, cus);
+  return c1bn::grid_x(m, c1bn::col_tile(ncols, k), k, pro, cus);
 }
 
 void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int ncols, bool w_kmajor_out, int dtype,
-                const float* pcoef, const float* shift, float* part, int cus, hipStream_t s) {
+                const float* pcoef, const float* shift, float* part, int cus, hipStream_t s, const void* res) {
   if (!conv1x1_bn_supported(m, k, ncols)) throw std::runtime_error("conv1x1_bn: unsupported shape");
   c1bn::Args args;
   args.a = static_cast<const uint16_t*>(a);
@@ -331,7 +345,8 @@ void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int nco
   args.pcoef = pcoef;
   args.shift = shift;
   args.part = part;
-  const int nc = c1bn::col_tile(ncols);
+  args.res = static_cast<const uint16_t*>(res);
+  const int nc = c1bn::col_tile(ncols, k);
   const bool wt = w_kmajor_out;
   const bool pro = pcoef != nullptr, stats = part != nullptr;
   auto go = [&](auto tag) {
@@ -527,11 +542,21 @@ __global__ void __launch_bounds__(256) wgrad_reduce(const float* __restrict__ ws
 // tile: 256 x 64, 64 x 256, 128 x 128 (16K accumulators / workgroup) or a 256 x 128 / 128 x 256
 // block (32K) when the other dimension is read once either way
 inline void tile(int n, int k, int& nt, int& kt) {
-  if (k == 64) { nt = n % 256 == 0 ? 256 : 128; kt = 64; }
-  else if (n == 64) { nt = 64; kt = k % 256 == 0 ? 256 : 128; }
-  else if (n % 256 == 0 && k % 128 == 0) { nt = 256; kt = 128; }
-  else if (k % 256 == 0 && n % 128 == 0) { nt = 128; kt = 256; }
-  else { nt = 128; kt = 128; }
+  // first candidate that divides (n, k): full-K tiles when K is the small side (the gradient,
+  // the big operand, is then read once), full-N when N is
+  static const int cand[][2] = {{256, 64}, {128, 64}, {64, 256}, {64, 128}, {256, 128}, {128, 256},
+                                {128, 128}, {64, 64}};
+  const int* pick = nullptr;
+  for (const auto& c : cand) {
+    if (k == 64 && c[1] != 64) continue;
+    if (n == 64 && c[0] != 64) continue;
+    if (n % c[0] == 0 && k % c[1] == 0) {
+      pick = c;
+      break;
+    }
+  }
+  nt = pick ? pick[0] : 64;
+  kt = pick ? pick[1] : 64;
 }
 
 inline int splits(int64_t m, int n, int k, int cus) {
@@ -554,7 +579,7 @@ void launch(const Args& a, int s, int cus, hipStream_t st) {
     constexpr int lds = lds_bytes<NT_, KT_>();                                                             \
     static bool attr = false;                                                                              \
     if (!attr) {                                                                                           \
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad1x1<T, NT_, KT_, PRO>),                      \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad1x1<T, NT_, KT_, PRO>),                      \
                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);                                \
       attr = true;                                                                                         \
     }                                                                                                      \
@@ -562,7 +587,7 @@ void launch(const Args& a, int s, int cus, hipStream_t st) {
     return;                                                                                                \
   }
   C1W_CASE(256, 64) C1W_CASE(128, 64) C1W_CASE(64, 256) C1W_CASE(64, 128) C1W_CASE(256, 128)
-  C1W_CASE(128, 256) C1W_CASE(128, 128)
+  C1W_CASE(128, 256) C1W_CASE(128, 128) C1W_CASE(64, 64)
 #undef C1W_CASE
   (void)cus;
   throw std::runtime_error("conv1x1 wgrad: no tile");
@@ -571,7 +596,7 @@ void launch(const Args& a, int s, int cus, hipStream_t st) {
 }  // namespace c1w
 
 bool conv1x1_wgrad_supported(int64_t m, int n, int k) {
-  return m > 0 && n % 64 == 0 && k % 64 == 0 && n >= 64 && k >= 64 && (n % 128 == 0 || k % 128 == 0 || n == 64);
+  return m > 0 && n % 64 == 0 && k % 64 == 0 && n >= 64 && k >= 64;
 }
 
 int64_t conv1x1_wgrad_workspace_floats(int64_t m, int n, int k, int cus) {

@@ -111,6 +111,12 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         if self.fused_bn:
+            from ..ops import bottleneck_bn
+
+            if not isinstance(x, tuple) and self.training and bottleneck_bn.block_supported(self, x):
+                # the whole block as one node: BN statistics in the 1x1 conv epilogues, bn2's
+                # apply+ReLU as conv3's operand prologue (ops/bottleneck_bn.py)
+                return bottleneck_bn.bottleneck_forward(self, x)
             xm, xr = x if isinstance(x, tuple) else (x, x)
             # downsampling block: the shortcut's conv output goes straight into the fused
             # relu(bn3(.) + bn_ds(.)) pass (contrib.groupbn.bn_add_bn_relu) — its normalized

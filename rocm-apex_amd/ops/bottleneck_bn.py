@@ -1,0 +1,256 @@
+"""Training-mode ResNet bottleneck block as ONE autograd node with the batch norms fused into the
+convolutions (``models.resnet.Bottleneck`` with ``fused_bn=True`` runs this on the GPU path).
+
+Per block (M = N*H*W pixels, width w, output 4w) the forward is
+
+    y1 = X . W1^T                + BN1 statistics in the conv epilogue   (csrc/conv/conv1x1_bn.hip)
+    z1 = relu(bn1(y1))                                                   (one apply pass)
+    y2 = conv3x3(z1, W2)                                                 (native implicit GEMM / MIOpen)
+    BN2 statistics                                                        (one read of y2)
+    y3 = relu(bn2(y2)) . W3^T    + BN3 statistics: bn2's apply+ReLU is the conv's operand
+                                   prologue, so z2 is never written
+    out = relu(bn3(y3) + shortcut)  (+ the ReLU bit mask)                 (one apply pass)
+
+with shortcut = X (identity) or bn_ds(X . Wds^T) fused into the output pass (downsampling
+block).  That removes two full statistics re-reads (y1: w, y3: 4w channels) and the bn2
+apply pass (read + write of w channels) per block against the module-per-op path.
+
+Backward: the bn3 reduction (bit mask, masked gradient = the identity branch's gradient),
+conv3's data gradient on the native transposed-weight kernel, conv3's weight gradient on the
+split-M kernel with bn2's apply+ReLU recomputed on its operand load (z2 is neither stored nor
+re-materialized), bn2 / conv2 / bn1 as before, and conv1's data gradient with the shortcut's
+gradient summed in (hipBLASLt ``addmm`` beta = 1), so the block hands ONE gradient tensor to
+the block below — no fork.
+
+Reference capability: apex/contrib/bottleneck (``bottleneck.cpp:1104-1534`` — the fused
+scale-bias-ReLU-conv graphs with BN statistics) and groupbn's NHWC BN; the composition here is
+gfx950-specific: the 1x1 convs of stages 1-2 are HBM-bound (26 GFLOP vs 0.25-0.5 GB each), so
+every fused pass saved is time saved.
+
+``APEX_AMD_FUSED_BLOCK=0`` disables the block node (the per-module fused path runs instead).
+"""
+import os
+
+import torch
+import torch.nn.functional as F
+
+from .. import _native
+from . import conv as convops
+
+_ENABLED = os.environ.get("APEX_AMD_FUSED_BLOCK", "1") != "0"
+_NATIVE_K = (64, 128, 256, 512)
+
+
+def _conv():
+    return _native.require("conv").conv
+
+
+def _bn():
+    return _native.require("bn_nhwc").bn_nhwc
+
+
+def _m2(t):
+    """[M, C] zero-copy view of a channels_last [N, C, H, W] tensor."""
+    return t.permute(0, 2, 3, 1).reshape(-1, t.size(1))
+
+
+def _nchw(t2, n, h, w):
+    return t2.view(n, h, w, t2.size(1)).permute(0, 3, 1, 2)
+
+
+class _BN:
+    """Per-BN constants of one forward: fp32 affine params, running buffers, momentum / eps."""
+
+    __slots__ = ("w", "b", "rm", "rv", "mom", "eps")
+
+    def __init__(self, bn):
+        self.w, self.b, self.rm, self.rv = bn.weight, bn.bias, bn.running_mean, bn.running_var
+        self.mom, self.eps = float(bn.momentum), float(bn.eps)
+
+
+# ---- 1x1 stride-1 convolution pieces ---------------------------------------------------------
+# Engine per op from the per-shape A/B at ResNet-50 bs 256 (profiles/bn1x1_kernels_r03a.jsonl,
+# tools/bn1x1_bench.py): the native kernels run the HBM-bound stage-1/2 shapes at 4.6-6.4 TB/s
+# (1.25-1.8x MIOpen / hipBLASLt); at K >= 512 with >= 256 output columns (the weight image no
+# longer holds a 256-column tile) and at stage-3/4 sizes hipBLASLt is faster, so those run there
+# with the separate statistics / apply passes.
+def _fwd_native(m, k, n):
+    return k in _NATIVE_K and n % 64 == 0 and n <= 512 and not (k == 512 and n >= 256)
+
+
+def _dgrad_native(m, kout, cin):
+    return kout in _NATIVE_K and cin % 64 == 0 and cin <= 256 and m >= 100000
+
+
+def _wgrad_native(m, n, k, pro):
+    # MIOpen's split-K wgrad leads at the 56x56 shapes unless the operand needs the BN prologue
+    return pro or m < 500000
+
+
+def conv1x1_bn_fwd(a2, w2d, pcoef, bn):
+    """y = pro(a) . W^T and the consuming BN's (save_mean, save_invstd, coef).  pro = relu(a *
+    pcoef[:K] + pcoef[K:]) when ``pcoef`` is given (the producing BN's apply + ReLU)."""
+    m, k = a2.shape
+    n = w2d.size(0)
+    if _fwd_native(m, k, n):
+        y2, part = _conv().bn1x1(a2, w2d, False, pcoef, bn.rm, True)
+        sm, si, coef = _conv().bn_finalize(part, float(m), bn.rm, bn.w, bn.b, bn.rm, bn.rv, bn.eps, bn.mom)
+        return y2, sm, si, coef
+    if pcoef is not None:
+        a2 = _bn().apply(a2, None, pcoef, True)[0]
+    y2 = torch.matmul(a2, w2d.t())
+    sm, si, coef = _bn().stats(y2, bn.w, bn.b, bn.rm, bn.rv, bn.mom, bn.eps)
+    return y2, sm, si, coef.view(-1)
+
+
+def conv1x1_dgrad(g2, w2d, add2=None):
+    """dX = g . W (+ add2): W [Cout, Cin], g [M, Cout]."""
+    m, kout = g2.shape
+    if _dgrad_native(m, kout, w2d.size(1)):
+        return _conv().bn1x1(g2, w2d, True, None, None, False, add2)[0]
+    if add2 is not None:
+        return torch.addmm(add2, g2, w2d)
+    return torch.matmul(g2, w2d)
+
+
+def conv1x1_wgrad(g2, x2, xcoef, w, n_h_w):
+    """dW [Cout, Cin, 1, 1] = g^T . pro(x), pro = the producing BN's apply + ReLU when ``xcoef``."""
+    m = g2.size(0)
+    if _wgrad_native(m, g2.size(1), x2.size(1), xcoef is not None):
+        return _conv().wgrad1x1(g2, x2, xcoef, w.dtype).view_as(w)
+    n, h, wd = n_h_w
+    gy, x = _nchw(g2, n, h, wd), _nchw(x2, n, h, wd)
+    return torch.ops.aten.convolution_backward(gy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                                               [False, True, False])[1]
+
+
+# ---- 3x3 / strided convolutions (ops/conv.py routes) -----------------------------------------
+def _conv_fwd(x, w, stride, pad):
+    fwd, _, _ = convops.tap_route(x.size(1), w.size(0), w.size(2), stride, x.size(2))
+    return convops.conv_tap_forward(x, w, stride, pad) if fwd else F.conv2d(x, w, None, stride, pad)
+
+
+def _conv_bwd(gy, x, w, stride, pad, need_x=True):
+    _, dg, _ = convops.tap_route(x.size(1), w.size(0), w.size(2), stride, x.size(2))
+    dx = None
+    if need_x and dg:
+        dx = convops.conv_tap_dgrad(gy, w, x.shape, stride, pad)
+    dx_m, dw, _ = torch.ops.aten.convolution_backward(gy, x, w, None, [stride, stride], [pad, pad], [1, 1], False,
+                                                      [0, 0], 1, [need_x and not dg, True, False])
+    return (dx if dx is not None else dx_m), dw
+
+
+class _BottleneckFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, w2, w3, wds, g1, b1, g2, b2, g3, b3, gds, bds, cfg):
+        bn1, bn2, bn3, bnd, stride = cfg
+        n, cin, h, wd = x.shape
+        width = w1.size(0)
+        cout = w3.size(0)
+        x2 = _m2(x)
+        # conv1 (+ bn1 statistics) -> bn1 apply + ReLU
+        y1, sm1, si1, c1 = conv1x1_bn_fwd(x2, w1.view(width, cin), None, bn1)
+        z1 = _bn().apply(y1, None, c1, True)[0]
+        # conv2 (3x3, stride) -> bn2 statistics
+        y2 = _conv_fwd(_nchw(z1, n, h, wd), w2, stride, 1)
+        oh, ow = y2.shape[2], y2.shape[3]
+        y2m = _m2(y2)
+        sm2, si2, c2 = _bn().stats(y2m, bn2.w, bn2.b, bn2.rm, bn2.rv, bn2.mom, bn2.eps)
+        c2 = c2.view(-1)
+        # conv3 with bn2's apply + ReLU on its operand load (+ bn3 statistics)
+        y3, sm3, si3, c3 = conv1x1_bn_fwd(y2m, w3.view(cout, width), c2, bn3)
+        if wds is None:
+            out2, bits = _bn().apply(y3, x2, c3, True, True)
+            yd = smd = sid = cd = None
+        else:
+            if stride == 1:
+                yd, smd, sid, cd = conv1x1_bn_fwd(x2, wds.view(cout, cin), None, bnd)
+            else:
+                yd = _m2(_conv_fwd(x, wds, stride, 0))
+                smd, sid, cd = _bn().stats(yd, bnd.w, bnd.b, bnd.rm, bnd.rv, bnd.mom, bnd.eps)
+                cd = cd.view(-1)
+            out2, bits = _bn().apply(y3, yd, c3, True, True, cd)
+        ctx.save_for_backward(x, w1, w2, w3, wds, g1, g2, g3, gds, y1, z1, y2m, y3, yd, bits,
+                              sm1, si1, c1, sm2, si2, c2, sm3, si3, c3, smd, sid, cd)
+        ctx.geo = (n, h, wd, oh, ow, stride)
+        return _nchw(out2, n, oh, ow)
+
+    @staticmethod
+    def backward(ctx, gout):
+        (x, w1, w2, w3, wds, g1, g2, g3, gds, y1, z1, y2m, y3, yd, bits,
+         sm1, si1, c1, sm2, si2, c2, sm3, si3, c3, smd, sid, cd) = ctx.saved_tensors
+        n, h, wd, oh, ow, stride = ctx.geo
+        bn = _bn()
+        width, cin, cout = w1.size(0), w1.size(1), w3.size(0)
+        gout = gout.contiguous(memory_format=torch.channels_last)
+        go2 = _m2(gout)
+        x2 = _m2(x)
+        # bn3 (+ shortcut): masked gradient dm (= the identity branch's gradient) and dx3
+        dx3, dm, gg3, gb3 = bn.bwd(go2, y3, None, g3, sm3, si3, c3, True, True, None, bits)
+        # conv3: data gradient (native transposed-weight kernel) and weight gradient with bn2's
+        # apply + ReLU recomputed on the operand load
+        dz2 = conv1x1_dgrad(dx3, w3.view(cout, width))
+        dw3 = conv1x1_wgrad(dx3, y2m, c2, w3, (n, oh, ow))
+        # bn2 (ReLU mask recomputed from y2)
+        dy2, _, gg2, gb2 = bn.bwd(dz2, y2m, None, g2, sm2, si2, c2, True, False)
+        # conv2
+        dz1, dw2 = _conv_bwd(_nchw(dy2, n, oh, ow), _nchw(z1, n, h, wd), w2, stride, 1)
+        dz1 = _m2(dz1.contiguous(memory_format=torch.channels_last))
+        # bn1
+        dy1, _, gg1, gb1 = bn.bwd(dz1, y1, None, g1, sm1, si1, c1, True, False)
+        # shortcut gradient, then conv1's data gradient summed onto it
+        dwd = ggd = gbd = None
+        if wds is None:
+            short = dm
+        else:
+            dyd, _, ggd, gbd = bn.bwd(dm, yd, None, gds, smd, sid, cd, False, False)
+            if stride == 1:
+                short = conv1x1_dgrad(dyd, wds.view(cout, cin))
+                dwd = conv1x1_wgrad(dyd, x2, None, wds, (n, h, wd))
+            else:
+                dxd, dwd = _conv_bwd(_nchw(dyd, n, oh, ow), x, wds, stride, 0)
+                short = _m2(dxd.contiguous(memory_format=torch.channels_last))
+        dx = conv1x1_dgrad(dy1, w1.view(width, cin), short)
+        dw1 = conv1x1_wgrad(dy1, x2, None, w1, (n, h, wd))
+        return (_nchw(dx, n, h, wd), dw1, dw2, dw3, dwd, gg1, gb1, gg2, gb2, gg3, gb3, ggd, gbd, None)
+
+
+def _bn_ok(bn):
+    return (bn.training and bn.track_running_stats and bn.bn_group == 1 and bn.weight is not None
+            and bn.weight.dtype == torch.float32 and bn.momentum is not None and bn.running_mean is not None)
+
+
+def block_supported(block, x):
+    """True when ``block`` (a fused_bn Bottleneck) can run as one fused node on ``x``."""
+    if not (_ENABLED and torch.is_tensor(x) and x.is_cuda and x.dim() == 4 and _native.available()
+            and x.dtype in (torch.bfloat16, torch.float16) and x.is_contiguous(memory_format=torch.channels_last)
+            and not torch.is_autocast_enabled("cuda")):
+        return False
+    if _native.submodule("conv") is None or _native.submodule("bn_nhwc") is None:
+        return False
+    convs = [block.conv1, block.conv2, block.conv3]
+    bns = [block.bn1, block.bn2, block.bn3]
+    if block.downsample is not None:
+        convs.append(block.downsample[0])
+        bns.append(block.downsample[1])
+    if not all(_bn_ok(b) for b in bns):
+        return False
+    if not all(c.weight.dtype == x.dtype and c.bias is None and c.groups == 1 and c.dilation == (1, 1)
+               and c.weight.is_contiguous(memory_format=torch.channels_last) for c in convs):
+        return False
+    if block.conv2.kernel_size != (3, 3) or block.conv1.stride != (1, 1) or block.conv3.stride != (1, 1):
+        return False
+    chans = (block.conv1.in_channels, block.conv1.out_channels, block.conv3.out_channels)
+    return all(c % 64 == 0 for c in chans)
+
+
+def bottleneck_forward(block, x):
+    ds = block.downsample
+    stride = block.conv2.stride[0]
+    if ds is not None and ds[0].stride[0] != stride:
+        raise ValueError("fused bottleneck: downsample stride must match conv2's")
+    cfg = (_BN(block.bn1), _BN(block.bn2), _BN(block.bn3), _BN(ds[1]) if ds is not None else None, stride)
+    return _BottleneckFn.apply(
+        x, block.conv1.weight, block.conv2.weight, block.conv3.weight, ds[0].weight if ds is not None else None,
+        block.bn1.weight, block.bn1.bias, block.bn2.weight, block.bn2.bias, block.bn3.weight, block.bn3.bias,
+        ds[1].weight if ds is not None else None, ds[1].bias if ds is not None else None, cfg)

@@ -1,0 +1,170 @@
+"""The fused training bottleneck node (ops/bottleneck_bn.py: BN statistics in the 1x1 conv
+epilogues, bn2 apply+ReLU as conv3's operand prologue, one gradient out) against the fp32
+PyTorch bottleneck with the same weights: forward output, input gradient, every weight / BN
+parameter gradient and the running statistics."""
+import copy
+
+import pytest
+import torch
+
+CASES = [
+    # inplanes, planes, stride, downsample, h, batch
+    (256, 64, 1, False, 14, 3),    # identity block (stage-1 widths)
+    (64, 64, 1, True, 14, 2),      # first block of stage 1: stride-1 1x1 downsample
+    (256, 128, 2, True, 16, 2),    # first block of stage 2: stride-2 downsample
+    (512, 128, 1, False, 7, 4),    # identity, conv1 K = 512
+    (1024, 256, 1, False, 7, 2),   # identity, conv1 K = 1024 (library fallback forward)
+]
+
+
+def _make(inplanes, planes, stride, downsample, fused):
+    from apex.models.resnet import Bottleneck, conv1x1, _fused_bn
+    import torch.nn as nn
+
+    ds = None
+    if downsample:
+        bn = _fused_bn(planes * 4, False) if fused else nn.BatchNorm2d(planes * 4)
+        ds = nn.Sequential(conv1x1(inplanes, planes * 4, stride, native=fused), bn)
+    return Bottleneck(inplanes, planes, stride, ds, fused_bn=fused)
+
+
+def _rel(a, b):
+    a, b = a.detach().float(), b.detach().float()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inplanes,planes,stride,downsample,h,batch", CASES)
+@pytest.mark.parametrize("block_node", [True, False])
+def test_gpu_fused_bottleneck_matches_fp32(inplanes, planes, stride, downsample, h, batch, block_node):
+    import apex  # noqa: F401
+    from apex.ops import bottleneck_bn
+
+    torch.manual_seed(0)
+    ref = _make(inplanes, planes, stride, downsample, fused=False).cuda().float()
+    for m in ref.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.2, 0.2)
+            m.running_mean.uniform_(-0.1, 0.1)
+    blk = _make(inplanes, planes, stride, downsample, fused=True).cuda()
+    blk.load_state_dict(ref.state_dict())
+    # amp O2 layout: bf16 convs, fp32 BN params, channels_last
+    for mod in blk.modules():
+        if isinstance(mod, torch.nn.Conv2d):
+            mod.to(torch.bfloat16)
+    blk = blk.to(memory_format=torch.channels_last)
+    blk.train()
+    ref.train()
+
+    x = torch.randn(batch, inplanes, h, h, device="cuda")
+    xb = x.to(torch.bfloat16).to(memory_format=torch.channels_last).requires_grad_(True)
+    xr = xb.detach().float().requires_grad_(True)
+    assert bottleneck_bn.block_supported(blk, xb)
+    old_enabled = bottleneck_bn._ENABLED
+    bottleneck_bn._ENABLED = block_node
+    calls = {"n": 0}
+    orig = bottleneck_bn._BottleneckFn.forward
+
+    def counted(*a, **k):
+        calls["n"] += 1
+        return orig(*a, **k)
+
+    bottleneck_bn._BottleneckFn.forward = staticmethod(counted)
+    try:
+        y = blk(xb)
+    finally:
+        bottleneck_bn._BottleneckFn.forward = staticmethod(orig)
+        bottleneck_bn._ENABLED = old_enabled
+    assert calls["n"] == int(block_node) and not isinstance(y, tuple)
+    yr = ref(xr)
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
+    assert _rel(y, yr) < 2e-2, _rel(y, yr)
+
+    gy = torch.randn_like(yr)
+    y.backward(gy.to(torch.bfloat16).to(memory_format=torch.channels_last))
+    yr.backward(gy)
+    pairs = dict(ref.named_parameters())
+    errs = {"x": _rel(xb.grad, xr.grad)}
+    for name, p in blk.named_parameters():
+        assert p.grad is not None, name
+        errs[name] = _rel(p.grad, pairs[name].grad)
+    print("rel errors", {k: round(v, 4) for k, v in errs.items()})
+    # bf16 activations / gradients through three batch norms at a few thousand pixels: ~5-10 %
+    # relative error against fp32 for BOTH fused paths (the per-module path measures the same)
+    assert max(errs.values()) < 0.15, errs
+    bufs = dict(ref.named_buffers())
+    for name, b in blk.named_buffers():
+        if name.endswith("running_mean") or name.endswith("running_var"):
+            torch.testing.assert_close(b, bufs[name], atol=2e-3, rtol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inplanes,planes,stride,downsample,h,batch", CASES)
+def test_gpu_fused_bottleneck_node_vs_module_path(inplanes, planes, stride, downsample, h, batch):
+    """The block node against the per-module fused path on identical bf16 inputs: the two
+    differ only in rounding order, so they agree far more closely than either does with fp32."""
+    import apex  # noqa: F401
+    from apex.ops import bottleneck_bn
+
+    torch.manual_seed(1)
+    a = _make(inplanes, planes, stride, downsample, fused=True).cuda()
+    for mod in a.modules():
+        if isinstance(mod, torch.nn.Conv2d):
+            mod.to(torch.bfloat16)
+    a = a.to(memory_format=torch.channels_last).train()
+    b = copy.deepcopy(a)
+    x = torch.randn(batch, inplanes, h, h, device="cuda").to(torch.bfloat16).to(memory_format=torch.channels_last)
+    gy = None
+    outs = []
+    for mod, node in ((a, True), (b, False)):
+        xi = x.clone().requires_grad_(True)
+        old = bottleneck_bn._ENABLED
+        bottleneck_bn._ENABLED = node
+        try:
+            y = mod(xi)
+            if gy is None:
+                gy = torch.randn_like(y)
+            y.backward(gy)
+        finally:
+            bottleneck_bn._ENABLED = old
+        outs.append((y.detach(), xi.grad, {n: p.grad for n, p in mod.named_parameters()}))
+    (ya, ga, pa), (yb, gb, pb) = outs
+    assert _rel(ya, yb) < 1e-2
+    assert _rel(ga, gb) < 3e-2, _rel(ga, gb)
+    for n in pa:
+        assert _rel(pa[n], pb[n]) < 5e-2, (n, _rel(pa[n], pb[n]))
+
+
+@pytest.mark.gpu
+def test_gpu_fused_bottleneck_resnet50_step_matches_module_path():
+    """A full fused-BN ResNet-50 training step: the block nodes vs the per-module fused path
+    (APEX_AMD_FUSED_BLOCK off) — same loss, close gradients."""
+    import apex  # noqa: F401
+    from apex.models import resnet50
+    from apex.ops import bottleneck_bn
+
+    torch.manual_seed(0)
+    m1 = resnet50(fused_bn=True).cuda().to(memory_format=torch.channels_last)
+    for mod in m1.modules():
+        if isinstance(mod, (torch.nn.Conv2d, torch.nn.Linear)):
+            mod.to(torch.bfloat16)
+    m2 = copy.deepcopy(m1)
+    x = torch.randn(8, 3, 64, 64, device="cuda").to(torch.bfloat16).to(memory_format=torch.channels_last)
+    tgt = torch.randint(0, 1000, (8,), device="cuda")
+
+    def step(model, enabled):
+        old = bottleneck_bn._ENABLED
+        bottleneck_bn._ENABLED = enabled
+        try:
+            loss = torch.nn.functional.cross_entropy(model(x).float(), tgt)
+            loss.backward()
+        finally:
+            bottleneck_bn._ENABLED = old
+        return loss.detach()
+
+    l1, l2 = step(m1, True), step(m2, False)
+    torch.testing.assert_close(l1, l2, atol=2e-2, rtol=2e-2)
+    g2 = dict(m2.named_parameters())
+    worst = max(_rel(p.grad, g2[n].grad) for n, p in m1.named_parameters())
+    assert worst < 0.1, worst
