@@ -365,6 +365,47 @@ std::vector<at::Tensor> apply(at::Tensor x, OT z, at::Tensor coef, bool relu, bo
   return {y, mask};
 }
 
+// backward reduction only: (dy_masked, coef_bwd[3, C], grad_w, grad_b).  The dx pass is left to
+// the consumer (bwd_apply below, or a convolution whose operand prologue computes
+// dx = coef_bwd[0] * dy_masked + coef_bwd[1] * x + coef_bwd[2] on load).
+std::vector<at::Tensor> bwd_reduce(at::Tensor dy_, at::Tensor x, OT w, at::Tensor save_mean, at::Tensor save_invstd,
+                                   at::Tensor coef_fwd, bool relu, OT mask_) {
+  check2d(x, "input");
+  const c10::hip::HIPGuard g(x.get_device());
+  at::Tensor dy = dy_.contiguous();
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "bn_nhwc: grad must match input");
+  const int64_t m = x.size(0);
+  const int c = (int)x.size(1);
+  const int cus = device_cus(x.get_device());
+  int64_t wsf = 0;
+  const int gy = bn_nhwc_plan(m, c, cus, &wsf);
+  auto fo = x.options().dtype(at::kFloat);
+  auto ws = at::empty({wsf}, fo);
+  auto gw = at::empty({c}, fo), gb = at::empty({c}, fo), coef_bwd = at::empty({3, c}, fo);
+  const bool bits = has(mask_);
+  if (bits)
+    TORCH_CHECK(relu && mask_->scalar_type() == at::kByte && mask_->numel() * 8 == m * c && mask_->is_contiguous(),
+                "bn_nhwc: mask must be a contiguous uint8 [M*C/8] tensor of a relu forward");
+  at::Tensor dm = relu ? at::empty_like(x) : dy;
+  bn_nhwc_bwd_reduce(dy.data_ptr(), x.data_ptr(), dtype_code(x.scalar_type()), nullptr, coef_fwd.data_ptr<float>(), relu,
+                     save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(), fptr(w), gw.data_ptr<float>(),
+                     gb.data_ptr<float>(), coef_bwd.data_ptr<float>(), relu ? dm.data_ptr() : nullptr, m, c,
+                     ws.data_ptr<float>(), gy, cus, cur_stream(), nullptr, bits ? mask_->data_ptr<uint8_t>() : nullptr);
+  return {dm, coef_bwd, gw, gb};
+}
+
+// dx = coef_bwd[0] * dy_masked + coef_bwd[1] * x + coef_bwd[2]
+at::Tensor bwd_apply(at::Tensor dy_masked, at::Tensor x, at::Tensor coef_fwd, at::Tensor coef_bwd) {
+  check2d(x, "input");
+  check2d(dy_masked, "grad");
+  const c10::hip::HIPGuard g(x.get_device());
+  auto dx = at::empty_like(x);
+  bn_nhwc_bwd_apply(dy_masked.data_ptr(), true, x.data_ptr(), dtype_code(x.scalar_type()), nullptr,
+                    coef_fwd.data_ptr<float>(), false, coef_bwd.data_ptr<float>(), dx.data_ptr(), x.size(0),
+                    (int)x.size(1), device_cus(x.get_device()), cur_stream());
+  return dx;
+}
+
 }  // namespace
 
 void bind_bn_nhwc(pybind11::module_& root) {
@@ -374,6 +415,8 @@ void bind_bn_nhwc(pybind11::module_& root) {
         pybind11::arg("relu"), pybind11::arg("want_mask") = false);
   m.def("fwd_eval", &fwd_eval);
   m.def("stats", &stats);
+  m.def("bwd_reduce", &bwd_reduce);
+  m.def("bwd_apply", &bwd_apply);
   m.def("apply", &apply, pybind11::arg("x"), pybind11::arg("z"), pybind11::arg("coef"), pybind11::arg("relu"),
         pybind11::arg("want_mask") = false, pybind11::arg("coef_z") = c10::nullopt);
   m.def("fwd_train_dual", &fwd_train_dual);

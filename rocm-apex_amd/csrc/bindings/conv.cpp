@@ -112,7 +112,8 @@ void wgrad(const at::Tensor& in, const at::Tensor& dy, at::Tensor& dw_out, int64
 // y = pro(a) . W^T (+ BN statistics partials); see conv_api.h.  Returns (y, part or empty).
 std::vector<at::Tensor> bn1x1(const at::Tensor& a, const at::Tensor& w, bool w_kmajor_out,
                               const c10::optional<at::Tensor>& pcoef, const c10::optional<at::Tensor>& shift,
-                              bool stats, const c10::optional<at::Tensor>& res) {
+                              bool stats, const c10::optional<at::Tensor>& res,
+                              const c10::optional<at::Tensor>& py, bool want_aout) {
   TORCH_CHECK(a.is_cuda() && a.dim() == 2 && a.is_contiguous(), "bn1x1: a must be a contiguous [M, K] GPU tensor");
   TORCH_CHECK(w.is_cuda() && w.dim() == 2 && w.is_contiguous() && w.scalar_type() == a.scalar_type(),
               "bn1x1: w must be a contiguous 2-D tensor of a's dtype");
@@ -127,12 +128,18 @@ std::vector<at::Tensor> bn1x1(const at::Tensor& a, const at::Tensor& w, bool w_k
                 what, " must be a contiguous fp32 tensor of ", n, " elements");
     return t->data_ptr<float>();
   };
-  const float* pc = f32(pcoef, 2 * (int64_t)k, "pcoef");
+  const bool bnbwd = py.has_value();
+  const float* pc = f32(pcoef, (bnbwd ? 3 : 2) * (int64_t)k, "pcoef");
+  TORCH_CHECK(!bnbwd || (pc && w_kmajor_out && py->is_cuda() && py->is_contiguous() &&
+                         py->scalar_type() == a.scalar_type() && py->sizes() == a.sizes()),
+              "bn1x1: py (BN-backward prologue) needs the dgrad form, pcoef [3K] and a tensor shaped like a");
+  TORCH_CHECK(!want_aout || bnbwd, "bn1x1: want_aout needs the BN-backward prologue");
   const float* sh = f32(shift, ncols, "shift");
   const c10::hip::HIPGuard g(a.get_device());
   const int cus = device_cus(a.get_device());
   auto y = at::empty({m, ncols}, a.options());
-  at::Tensor part;
+  at::Tensor part, aout;
+  if (want_aout) aout = at::empty_like(a);
   if (stats)
     part = at::empty({2, conv1x1_bn_partials(m, k, ncols, pc != nullptr, cus), ncols}, a.options().dtype(at::kFloat));
   if (res.has_value())
@@ -140,8 +147,9 @@ std::vector<at::Tensor> bn1x1(const at::Tensor& a, const at::Tensor& w, bool w_k
                     res->numel() == m * ncols,
                 "bn1x1: res must be a contiguous [M, ncols] tensor of a's dtype");
   conv1x1_bn(a.data_ptr(), w.data_ptr(), y.data_ptr(), m, k, ncols, w_kmajor_out, dtype_code(a.scalar_type()), pc, sh,
-             stats ? part.data_ptr<float>() : nullptr, cus, cur_stream(), res.has_value() ? res->data_ptr() : nullptr);
-  return {y, part};
+             stats ? part.data_ptr<float>() : nullptr, cus, cur_stream(), res.has_value() ? res->data_ptr() : nullptr,
+             bnbwd ? py->data_ptr() : nullptr, want_aout ? aout.data_ptr() : nullptr);
+  return {y, part, aout};
 }
 
 // (save_mean, save_invstd, coef[2C]) from bn1x1 partials; running stats updated in place
@@ -207,7 +215,8 @@ void bind_conv(pybind11::module_& root) {
   m.def("force_fprop_cfg", &conv_force_fprop_cfg);
   m.def("bn1x1", &bn1x1, pybind11::arg("a"), pybind11::arg("w"), pybind11::arg("w_kmajor_out") = false,
         pybind11::arg("pcoef") = pybind11::none(), pybind11::arg("shift") = pybind11::none(),
-        pybind11::arg("stats") = false, pybind11::arg("res") = pybind11::none());
+        pybind11::arg("stats") = false, pybind11::arg("res") = pybind11::none(),
+        pybind11::arg("py") = pybind11::none(), pybind11::arg("want_aout") = false);
   m.def("bn_finalize", &bn_finalize);
   m.def("wgrad1x1", &wgrad1x1, pybind11::arg("g"), pybind11::arg("x"), pybind11::arg("xcoef") = pybind11::none(),
         pybind11::arg("out_dtype") = pybind11::none());

@@ -27,6 +27,7 @@
 #include "apex_amd/dispatch.h"
 #include "apex_amd/mfma.h"
 
+#include <cstdlib>
 #include <stdexcept>
 
 namespace apex_amd {
@@ -44,17 +45,25 @@ struct Args {
   const float* shift;   // STATS: per-output-channel shift [ncols] (nullable = 0)
   float* part;          // STATS: [2][gridDim.x][ncols] partial sums (S1 slab, then S2 slab)
   const uint16_t* res;  // nullable [M][ncols]: y += res before the store (a residual gradient)
+  const uint16_t* py;   // PRO == kProBnBwd: second operand tensor [M][K] (the BN's input)
+  uint16_t* aout;       // PRO == kProBnBwd, nullable: the transformed operand written out [M][K]
 };
+
+// operand prologues
+constexpr int kProNone = 0;
+constexpr int kProBnRelu = 1;  // a' = relu(a * c[k] + c[K + k])            (BN apply + ReLU)
+constexpr int kProBnBwd = 2;   // a' = c[k] * a + c[K + k] * y + c[2K + k]  (BN backward dx from the
+                               //       masked gradient a and the BN input y: bwd_apply fused)
 
 constexpr int kWaves = 4, kRowsB = kWaves * 32;
 constexpr int kSS = 64 + 8;  // staging row stride (elements): rows h and h+4 land 16 banks apart
 
-template <int NC, int KR, bool PRO>
+template <int NC, int KR, int PRO>
 constexpr int lds_bytes() {
-  return NC * (KR + 8) * 2 + kWaves * 32 * kSS * 2 + (PRO ? 2 * KR * 4 : 0);
+  return NC * (KR + 8) * 2 + kWaves * 32 * kSS * 2 + (PRO == kProBnRelu ? 2 : PRO == kProBnBwd ? 3 : 0) * KR * 4;
 }
 
-template <typename T, int NC, int KR, bool WT, bool PRO, bool STATS>
+template <typename T, int NC, int KR, bool WT, int PRO, bool STATS>
 __global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
   constexpr int BS = KR + 8;                 // B image row stride (elements)
   constexpr int CN = NC / 32;                // accumulator blocks per wave
@@ -65,7 +74,7 @@ __global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   uint16_t* bimg = lds;                       // [NC][BS]
   uint16_t* stg = lds + NC * BS;              // [kWaves][32][kSS]
-  float* pc = reinterpret_cast<float*>(stg + kWaves * 32 * kSS);  // [2][KR]
+  float* pc = reinterpret_cast<float*>(stg + kWaves * 32 * kSS);  // [2 or 3][KR]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, lr = lane & 31, lh = lane >> 5;
   const int col0 = blockIdx.y * NC;
@@ -89,8 +98,8 @@ __global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
       }
     }
   }
-  if constexpr (PRO)
-    for (int i = tid; i < 2 * KR; i += 256) pc[i] = p.pcoef[i];
+  if constexpr (PRO != kProNone)
+    for (int i = tid; i < (PRO == kProBnBwd ? 3 : 2) * KR; i += 256) pc[i] = p.pcoef[i];
   float sh[CN], s1[CN], s2[CN];
 #pragma unroll
   for (int cb = 0; cb < CN; ++cb) {
@@ -103,19 +112,48 @@ __global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
 #pragma unroll
   for (int cb = 0; cb < CN; ++cb) acc[cb] = zero16();
 
-  auto load = [&](s16x8(&f)[KC], int t, int ch) {
+  constexpr int KY = PRO == kProBnBwd ? KC : 1;
+  struct Frags {
+    s16x8 a[KC];
+    s16x8 y[KY];
+  };
+  auto load = [&](Frags& f, int t, int ch) {
     int64_t row = (int64_t)t * kRowsB + wid * 32 + lr;
     if (row >= p.m) row = p.m - 1;  // tail rows: valid memory, masked in the epilogue
-    const uint16_t* src = p.a + row * KR + ch * KCH + 8 * lh;
+    const int64_t off = row * KR + ch * KCH + 8 * lh;
 #pragma unroll
-    for (int s = 0; s < KC; ++s) f[s] = *reinterpret_cast<const s16x8*>(src + 16 * s);
+    for (int s = 0; s < KC; ++s) f.a[s] = *reinterpret_cast<const s16x8*>(p.a + off + 16 * s);
+    if constexpr (PRO == kProBnBwd) {
+#pragma unroll
+      for (int s = 0; s < KC; ++s) f.y[s] = *reinterpret_cast<const s16x8*>(p.py + off + 16 * s);
+    }
   };
 
-  auto compute = [&](const s16x8(&f)[KC], int ch) {
+  auto compute = [&](const Frags& f, int t, int ch) {
 #pragma unroll
     for (int s = 0; s < KC; ++s) {
-      s16x8 a = f[s];
-      if constexpr (PRO) {
+      s16x8 a = f.a[s];
+      if constexpr (PRO == kProBnBwd) {
+        const int kb = ch * KCH + 16 * s + 8 * lh;
+        float c[3][8];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const float4 u0 = *reinterpret_cast<const float4*>(pc + q * KR + kb);
+          const float4 u1 = *reinterpret_cast<const float4*>(pc + q * KR + kb + 4);
+          c[q][0] = u0.x; c[q][1] = u0.y; c[q][2] = u0.z; c[q][3] = u0.w;
+          c[q][4] = u1.x; c[q][5] = u1.y; c[q][6] = u1.z; c[q][7] = u1.w;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = fmaf(c[0][j], to_f(T{(uint16_t)a[j]}), fmaf(c[1][j], to_f(T{(uint16_t)f.y[s][j]}), c[2][j]));
+          a[j] = (short)from_f<T>(v).x;
+        }
+        if (p.aout) {  // dx of the BN, for the weight gradient that also needs it
+          const int64_t row = (int64_t)t * kRowsB + wid * 32 + lr;
+          if (row < p.m) *reinterpret_cast<s16x8*>(p.aout + row * KR + kb) = a;
+        }
+      }
+      if constexpr (PRO == kProBnRelu) {
         const int kb = ch * KCH + 16 * s + 8 * lh;
         const float4 c0 = *reinterpret_cast<const float4*>(pc + kb);
         const float4 c1 = *reinterpret_cast<const float4*>(pc + kb + 4);
@@ -183,7 +221,7 @@ __global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
   };
 
   // flat (tile, chunk) stream, the next chunk's loads in flight under the current one's MFMAs
-  s16x8 fa[KC], fb[KC];
+  Frags fa, fb;
   int t = blockIdx.x, ch = 0;
   if (t < p.ntiles) load(fa, t, 0);
   while (t < p.ntiles) {
@@ -191,7 +229,7 @@ __global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
       int nt = t, nch = ch + 1;
       if (nch == NCH) { nch = 0; nt += gridDim.x; }
       if (nt < p.ntiles) load(fb, nt, nch);
-      compute(fa, ch);
+      compute(fa, t, ch);
       if (ch == NCH - 1) epilogue(t);
       t = nt;
       ch = nch;
@@ -201,7 +239,7 @@ __global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
       int nt = t, nch = ch + 1;
       if (nch == NCH) { nch = 0; nt += gridDim.x; }
       if (nt < p.ntiles) load(fa, nt, nch);
-      compute(fb, ch);
+      compute(fb, t, ch);
       if (ch == NCH - 1) epilogue(t);
       t = nt;
       ch = nch;
@@ -275,7 +313,7 @@ __global__ void __launch_bounds__(256) stats_finalize(const float* __restrict__ 
   if (rvar) rvar[ch] = (1.f - momentum) * rvar[ch] + momentum * (n > 1.f ? var_b * n / (n - 1.f) : var_b);
 }
 
-template <typename T, int NC, int KR, bool WT, bool PRO, bool STATS>
+template <typename T, int NC, int KR, bool WT, int PRO, bool STATS>
 void launch_t(const Args& a, int cus, hipStream_t s) {
   constexpr int lds = lds_bytes<NC, KR, PRO>();
   static bool attr = false;
@@ -290,8 +328,8 @@ void launch_t(const Args& a, int cus, hipStream_t s) {
   hipLaunchKernelGGL((fused1x1<T, NC, KR, WT, PRO, STATS>), dim3(gx, a.ncols / NC), dim3(256), lds, s, a);
 }
 
-inline int grid_x(int64_t m, int nc, int kr, bool pro, int cus) {
-  const int lds = nc * (kr + 8) * 2 + kWaves * 32 * kSS * 2 + (pro ? 2 * kr * 4 : 0);
+inline int grid_x(int64_t m, int nc, int kr, int pro, int cus) {
+  const int lds = nc * (kr + 8) * 2 + kWaves * 32 * kSS * 2 + pro * kr * 4;
   const int per_cu = (160 * 1024) / lds >= 2 ? 2 : 1;
   const int ntiles = (int)((m + kRowsB - 1) / kRowsB);
   const int gx = cus * per_cu;
@@ -306,7 +344,7 @@ inline int col_tile(int ncols, int kr) {
   return ncols % 128 == 0 ? 128 : 64;
 }
 
-template <typename T, bool WT, bool PRO, bool STATS>
+template <typename T, bool WT, int PRO, bool STATS>
 void dispatch_shape(const Args& a, int nc, int kr, int cus, hipStream_t s) {
 #define C1BN_CASE(NC_, KR_)                                 \
   if (nc == NC_ && kr == KR_) {                             \
@@ -329,11 +367,12 @@ bool conv1x1_bn_supported(int64_t m, int k, int ncols) {
 }
 
 int conv1x1_bn_partials(int64_t m, int k, int ncols, bool pro, int cus) {
-  return c1bn::grid_x(m, c1bn::col_tile(ncols, k), k, pro, cus);
+  return c1bn::grid_x(m, c1bn::col_tile(ncols, k), k, pro ? 2 : 0, cus);
 }
 
 void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int ncols, bool w_kmajor_out, int dtype,
-                const float* pcoef, const float* shift, float* part, int cus, hipStream_t s, const void* res) {
+                const float* pcoef, const float* shift, float* part, int cus, hipStream_t s, const void* res,
+                const void* py, void* aout) {
   if (!conv1x1_bn_supported(m, k, ncols)) throw std::runtime_error("conv1x1_bn: unsupported shape");
   c1bn::Args args;
   args.a = static_cast<const uint16_t*>(a);
@@ -346,20 +385,30 @@ void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int nco
   args.shift = shift;
   args.part = part;
   args.res = static_cast<const uint16_t*>(res);
+  args.py = static_cast<const uint16_t*>(py);
+  args.aout = static_cast<uint16_t*>(aout);
   const int nc = c1bn::col_tile(ncols, k);
   const bool wt = w_kmajor_out;
-  const bool pro = pcoef != nullptr, stats = part != nullptr;
+  const bool stats = part != nullptr;
+  // py given: the BN-backward prologue (pcoef = [3][k]); else pcoef = the BN apply + ReLU [2][k]
+  const int pro = pcoef == nullptr ? c1bn::kProNone : py ? c1bn::kProBnBwd : c1bn::kProBnRelu;
+  if (aout && pro != c1bn::kProBnBwd) throw std::runtime_error("conv1x1_bn: aout needs the BN-backward prologue");
   auto go = [&](auto tag) {
     using T = typename decltype(tag)::type;
     if (wt) {
-      if (pro || stats) throw std::runtime_error("conv1x1_bn: the transposed-weight (dgrad) form has no BN fusion");
-      c1bn::dispatch_shape<T, true, false, false>(args, nc, k, cus, s);
-    } else if (pro) {
-      if (stats) c1bn::dispatch_shape<T, false, true, true>(args, nc, k, cus, s);
-      else c1bn::dispatch_shape<T, false, true, false>(args, nc, k, cus, s);
+      if (stats || pro == c1bn::kProBnRelu)
+        throw std::runtime_error("conv1x1_bn: the transposed-weight (dgrad) form takes the BN-backward prologue only");
+      if (pro == c1bn::kProBnBwd) c1bn::dispatch_shape<T, true, c1bn::kProBnBwd, false>(args, nc, k, cus, s);
+      else c1bn::dispatch_shape<T, true, c1bn::kProNone, false>(args, nc, k, cus, s);
     } else {
-      if (stats) c1bn::dispatch_shape<T, false, false, true>(args, nc, k, cus, s);
-      else c1bn::dispatch_shape<T, false, false, false>(args, nc, k, cus, s);
+      if (pro == c1bn::kProBnBwd) throw std::runtime_error("conv1x1_bn: BN-backward prologue is a dgrad-form option");
+      if (pro == c1bn::kProBnRelu) {
+        if (stats) c1bn::dispatch_shape<T, false, c1bn::kProBnRelu, true>(args, nc, k, cus, s);
+        else c1bn::dispatch_shape<T, false, c1bn::kProBnRelu, false>(args, nc, k, cus, s);
+      } else {
+        if (stats) c1bn::dispatch_shape<T, false, c1bn::kProNone, true>(args, nc, k, cus, s);
+        else c1bn::dispatch_shape<T, false, c1bn::kProNone, false>(args, nc, k, cus, s);
+      }
     }
   };
   dispatch_16(dtype, go, "conv1x1_bn");
@@ -523,6 +572,164 @@ __global__ void __launch_bounds__(256, 1) wgrad1x1(Args p) {
       }
 }
 
+// Ring variant: the same tile loop with the operands moved global -> LDS by LDS-DMA
+// (global_load_lds_dwordx4, no staging registers) into a 3-slot ring, two chunks (80 KB / CU at
+// 256 x 64) in flight under the MFMAs of the current one — the register-staged loop above keeps
+// only one chunk in flight and reads HBM at 2-3 TB/s on the 56x56 shapes.  The DMA image is
+// lane-linear per 1-KB instruction, so the bank swizzle goes on the source address: logical
+// 16-byte chunk c of pixel row r sits at c ^ ((r & 3) << 1), which puts the 4 rows x 2 chunks a
+// 16-lane ds_read_b64_tr_b16 touches on 8 distinct bank chunks.  The BN prologue moves to the
+// fragment: an X^T fragment is one channel per lane, so its scale / shift are two registers.
+constexpr int kRing = 3;
+
+__device__ __forceinline__ void dma16(const uint16_t* src, uint16_t* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+
+// wait until at most N of this wave's DMA instructions are in flight (N = one chunk's worth)
+template <int N>
+__device__ __forceinline__ void vm_wait_ring() {
+  static_assert(N == 0 || N == 4 || N == 6 || N == 8 || N == 10 || N == 12, "ring vmcnt");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+}
+
+template <int COLS>
+__device__ __forceinline__ void issue_img(const uint16_t* __restrict__ src, int64_t ld, int col0, int64_t base,
+                                          int64_t mlast, uint16_t* img, int wave, int lane) {
+  constexpr int CPR = COLS / 8;               // 16-byte chunks per row
+  constexpr int RPI = 64 / CPR;               // rows per 1-KB instruction
+  constexpr int NI = MB * COLS / 512;         // instructions per image
+  static_assert(NI % 4 == 0, "image instructions split over 4 waves");
+#pragma unroll
+  for (int i = 0; i < NI / 4; ++i) {
+    const int j = i * 4 + wave;
+    const int row = RPI * j + lane / CPR;
+    const int c = (lane % CPR) ^ ((row & 3) << 1);
+    int64_t rr = base + row;
+    rr = rr <= mlast ? rr : mlast;  // past-the-end rows: valid memory, zeroed in the fragment
+    dma16(src + rr * ld + col0 + 8 * c, img + j * 512);
+  }
+}
+
+template <int STR>
+__device__ __forceinline__ s16x8 frag_ring(const uint16_t* img, int colbase, int klo, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int col = colbase + 16 * (g & 1) + 4 * p;
+  const int ck = col >> 3, off = col & 7;
+  const int r0 = klo + q, r1 = klo + 4 + q;
+  const s16x4 lo = tr_read(img + r0 * STR + ((ck ^ ((r0 & 3) << 1)) << 3) + off);
+  const s16x4 hi = tr_read(img + r1 * STR + ((ck ^ ((r1 & 3) << 1)) << 3) + off);
+  return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int NT, int KT>
+constexpr int ring_lds_bytes() {
+  return kRing * MB * (NT + KT) * 2;
+}
+
+template <typename T, int NT, int KT, bool PRO>
+__global__ void __launch_bounds__(256, 1) wgrad1x1_ring(Args p) {
+  constexpr int WN = NT / 64, WK = KT / 64;
+  constexpr int GI = MB * NT / 512 / 4, XI = MB * KT / 512 / 4;  // DMA instructions per wave per chunk
+  constexpr int PER = GI + XI;
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, lr = lane & 31, lh = lane >> 5;
+  const int wn = wid & 1, wk = wid >> 1;
+  const int n0 = blockIdx.y * NT, k0 = blockIdx.z * KT;
+  const int64_t r0 = (int64_t)blockIdx.x * p.rows;
+  const int64_t r1 = r0 + p.rows < p.m ? r0 + p.rows : p.m;
+  const int nch = r1 > r0 ? (int)((r1 - r0 + MB - 1) / MB) : 0;
+  const int64_t mlast = p.m - 1;
+
+  float xs[WK], xb[WK];
+  if constexpr (PRO) {
+#pragma unroll
+    for (int j = 0; j < WK; ++j) {
+      const int kc = k0 + wk * (KT / 2) + 32 * j + lr;
+      xs[j] = p.xcoef[kc];
+      xb[j] = p.xcoef[p.k + kc];
+    }
+  }
+
+  auto slot_g = [&](int c) { return lds + (c % kRing) * MB * (NT + KT); };
+  auto issue = [&](int c) {
+    uint16_t* gi = slot_g(c);
+    const int64_t base = r0 + (int64_t)c * MB;
+    issue_img<NT>(p.g, p.n, n0, base, mlast, gi, wid, lane);
+    issue_img<KT>(p.x, p.k, k0, base, mlast, gi + MB * NT, wid, lane);
+  };
+
+  f32x16 acc[WN][WK];
+#pragma unroll
+  for (int i = 0; i < WN; ++i)
+#pragma unroll
+    for (int j = 0; j < WK; ++j) acc[i][j] = zero16();
+
+  if (nch > 0) issue(0);
+  if (nch > 1) issue(1);
+  for (int c = 0; c < nch; ++c) {
+    // this wave's part of chunk c has landed (chunk c+1 may still be in flight); its reads of
+    // chunk c-1 are complete; the barrier makes both true for every wave
+    if (c + 1 < nch) vm_wait_ring<PER>();
+    else vm_wait_ring<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (c + 2 < nch) issue(c + 2);        // into chunk c-1's slot
+    const uint16_t* gi = slot_g(c);
+    const uint16_t* xi = gi + MB * NT;
+    const int64_t base = r0 + (int64_t)c * MB;
+    const bool tail = base + MB > r1;
+#pragma unroll
+    for (int kk = 0; kk < MB / 16; ++kk) {
+      const int klo = 16 * kk + 8 * lh;
+      s16x8 a[WN], b[WK];
+#pragma unroll
+      for (int i = 0; i < WN; ++i) {
+        a[i] = frag_ring<NT>(gi, wn * (NT / 2) + 32 * i, klo, lane);
+        if (tail) {  // rows past this split's end contribute nothing
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (base + klo + (e & 3) + 4 * (e >> 2) >= r1) a[i][e] = 0;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < WK; ++j) {
+        b[j] = frag_ring<KT>(xi, wk * (KT / 2) + 32 * j, klo, lane);
+        if constexpr (PRO) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float v = fmaxf(fmaf(to_f(T{(uint16_t)b[j][e]}), xs[j], xb[j]), 0.f);
+            b[j][e] = (short)from_f<T>(v).x;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < WN; ++i)
+#pragma unroll
+        for (int j = 0; j < WK; ++j) acc[i][j] = mma<T>(a[i], b[j], acc[i][j]);
+    }
+  }
+
+  float* out = p.ws + (int64_t)blockIdx.x * p.n * p.k;
+#pragma unroll
+  for (int i = 0; i < WN; ++i)
+#pragma unroll
+    for (int j = 0; j < WK; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int nn = n0 + wn * (NT / 2) + 32 * i + crow(r, lh);
+        const int kc = k0 + wk * (KT / 2) + 32 * j + lr;
+        out[(int64_t)nn * p.k + kc] = acc[i][j][r];
+      }
+}
+
 // dW = sum over the S split partials in a fixed order, 8 consecutive elements per thread
 template <typename TO>
 __global__ void __launch_bounds__(256) wgrad_reduce(const float* __restrict__ ws, int s, int64_t nk,
@@ -569,6 +776,15 @@ inline int splits(int64_t m, int n, int k, int cus) {
   return s < 1 ? 1 : s;
 }
 
+// APEX_AMD_WGRAD_RING=0: the register-staged loop (A/B)
+inline bool ring_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("APEX_AMD_WGRAD_RING");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <typename T, bool PRO>
 void launch(const Args& a, int s, int cus, hipStream_t st) {
   int nt, kt;
@@ -582,6 +798,17 @@ void launch(const Args& a, int s, int cus, hipStream_t st) {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad1x1<T, NT_, KT_, PRO>),                      \
                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);                                \
       attr = true;                                                                                         \
+    }                                                                                                      \
+    if (ring_on()) {                                                                                       \
+      constexpr int rl = ring_lds_bytes<NT_, KT_>();                                                       \
+      static bool rattr = false;                                                                           \
+      if (!rattr) {                                                                                        \
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad1x1_ring<T, NT_, KT_, PRO>),         \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, rl);                         \
+        rattr = true;                                                                                      \
+      }                                                                                                    \
+      hipLaunchKernelGGL((wgrad1x1_ring<T, NT_, KT_, PRO>), grid, dim3(256), rl, st, a);                   \
+      return;                                                                                              \
     }                                                                                                      \
     hipLaunchKernelGGL((wgrad1x1<T, NT_, KT_, PRO>), grid, dim3(256), lds, st, a);                         \
     return;                                                                                                \

@@ -185,11 +185,17 @@ class _BottleneckFn(torch.autograd.Function):
         gout = gout.contiguous(memory_format=torch.channels_last)
         go2 = _m2(gout)
         x2 = _m2(x)
-        # bn3 (+ shortcut): masked gradient dm (= the identity branch's gradient) and dx3
-        dx3, dm, gg3, gb3 = bn.bwd(go2, y3, None, g3, sm3, si3, c3, True, True, None, bits)
-        # conv3: data gradient (native transposed-weight kernel) and weight gradient with bn2's
-        # apply + ReLU recomputed on the operand load
-        dz2 = conv1x1_dgrad(dx3, w3.view(cout, width))
+        # bn3 (+ shortcut): masked gradient dm (= the identity branch's gradient) + coefficients;
+        # its dx pass runs as conv3's dgrad operand prologue (dx3 written as a by-product for
+        # the weight gradient) where that kernel takes the shape
+        dm, cb3, gg3, gb3 = bn.bwd_reduce(go2, y3, g3, sm3, si3, c3, True, bits)
+        w3m = w3.view(cout, width)
+        if _dgrad_native(dm.size(0), cout, width):
+            dz2, _, dx3 = _conv().bn1x1(dm, w3m, True, cb3.view(-1), None, False, None, y3, True)
+        else:
+            dx3 = bn.bwd_apply(dm, y3, c3, cb3)
+            dz2 = conv1x1_dgrad(dx3, w3m)
+        # conv3 weight gradient with bn2's apply + ReLU recomputed on the operand load
         dw3 = conv1x1_wgrad(dx3, y2m, c2, w3, (n, oh, ow))
         # bn2 (ReLU mask recomputed from y2)
         dy2, _, gg2, gb2 = bn.bwd(dz2, y2m, None, g2, sm2, si2, c2, True, False)

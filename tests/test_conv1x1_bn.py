@@ -130,3 +130,21 @@ def test_gpu_wgrad1x1(dtype, m, n, k, pro):
     dw16 = ext.wgrad1x1(g, x, xcoef)
     assert dw16.dtype == dtype
     _close(dw16, ref, 1e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("m,k,nc", SHAPES)
+def test_gpu_bn1x1_dgrad_bn_backward_prologue(dtype, m, k, nc):
+    """dgrad form with the BN-backward prologue: a' = c0 * dm + c1 * y + c2 per reduction
+    channel, the product a' . W, and a' itself written out (aout)."""
+    ext = _ext()
+    torch.manual_seed(4)
+    dm = torch.randn(m, k, device="cuda").to(dtype)
+    y = (torch.randn(m, k, device="cuda") + 0.2).to(dtype)
+    w = (torch.randn(k, nc, device="cuda") * 0.1).to(dtype)
+    cb = torch.randn(3 * k, device="cuda") * 0.5
+    out, _, aout = ext.bn1x1(dm, w, True, cb, None, False, None, y, True)
+    ap = (cb[:k] * dm.float() + cb[k:2 * k] * y.float() + cb[2 * k:]).to(dtype)
+    _close(aout, ap, 1e-2)
+    _close(out, ap.float() @ w.float(), 1e-2)

@@ -70,6 +70,8 @@ def main():
             gy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [False, True, False]),
             "native": lambda: ext.wgrad1x1(gy2, x2),
             "native_pro": lambda: ext.wgrad1x1(gy2, x2, pcoef)}
+        if os.environ.get("BN1X1_BENCH_ONLY_WGRAD"):
+            arms = {"wgrad": arms["wgrad"]}
         res = {op: {k: [] for k in a} for op, a in arms.items()}
         for _ in range(args.rounds):
             for op, a in arms.items():
