@@ -201,6 +201,50 @@ at::Tensor wgrad1x1(const at::Tensor& g, const at::Tensor& x, const c10::optiona
   return dw;
 }
 
+// conv dgrad (dgrad form W [k, ncols]) + residual, masked by the block-below BN's ReLU bits, with
+// that BN's backward reduction partials; returns (out, part)
+std::vector<at::Tensor> dgrad_bnred(const at::Tensor& g, const at::Tensor& w, const c10::optional<at::Tensor>& res,
+                                    const at::Tensor& bits, const at::Tensor& x, const at::Tensor& mean) {
+  TORCH_CHECK(g.is_cuda() && g.dim() == 2 && g.is_contiguous() && w.dim() == 2 && w.is_contiguous() &&
+                  w.scalar_type() == g.scalar_type() && w.size(0) == g.size(1),
+              "dgrad_bnred: g [M, k] and w [k, ncols] expected");
+  const int64_t m = g.size(0);
+  const int k = (int)g.size(1), ncols = (int)w.size(1);
+  TORCH_CHECK(x.is_contiguous() && x.scalar_type() == g.scalar_type() && x.numel() == m * ncols,
+              "dgrad_bnred: x must be the contiguous [M, ncols] BN input");
+  TORCH_CHECK(bits.is_contiguous() && bits.scalar_type() == at::kByte && bits.numel() * 8 == m * ncols,
+              "dgrad_bnred: bits must be the [M * ncols / 8] ReLU mask");
+  TORCH_CHECK(mean.is_contiguous() && mean.scalar_type() == at::kFloat && mean.numel() == ncols,
+              "dgrad_bnred: mean must be fp32 [ncols]");
+  if (res.has_value())
+    TORCH_CHECK(res->is_contiguous() && res->scalar_type() == g.scalar_type() && res->numel() == m * ncols,
+                "dgrad_bnred: res must be a contiguous [M, ncols] tensor");
+  TORCH_CHECK(conv1x1_bn_supported(m, k, ncols), "dgrad_bnred: unsupported shape");
+  const c10::hip::HIPGuard guard(g.get_device());
+  const int cus = device_cus(g.get_device());
+  auto out = at::empty({m, ncols}, g.options());
+  auto part = at::empty({2, conv1x1_dgrad_bnred_partials(m, k, ncols, cus), ncols}, g.options().dtype(at::kFloat));
+  conv1x1_dgrad_bnred(g.data_ptr(), w.data_ptr(), out.data_ptr(), m, k, ncols, dtype_code(g.scalar_type()),
+                      res.has_value() ? res->data_ptr() : nullptr, bits.data_ptr<uint8_t>(), x.data_ptr(),
+                      mean.data_ptr<float>(), part.data_ptr<float>(), cus, cur_stream());
+  return {out, part};
+}
+
+// (coef_bwd [3C], grad_w, grad_b) from dgrad_bnred partials
+std::vector<at::Tensor> bnbwd_finalize(const at::Tensor& part, double count, const at::Tensor& mean,
+                                       const at::Tensor& invstd, const c10::optional<at::Tensor>& w) {
+  TORCH_CHECK(part.is_cuda() && part.dim() == 3 && part.size(0) == 2 && part.scalar_type() == at::kFloat,
+              "bnbwd_finalize: part must be [2, G, C] fp32");
+  const int c = (int)part.size(2);
+  const c10::hip::HIPGuard guard(part.get_device());
+  auto opt = part.options();
+  auto coef = at::empty({3 * c}, opt), gw = at::empty({c}, opt), gb = at::empty({c}, opt);
+  conv1x1_bnbwd_finalize(part.data_ptr<float>(), (int)part.size(1), c, (float)(1.0 / count), mean.data_ptr<float>(),
+                         invstd.data_ptr<float>(), w.has_value() ? w->data_ptr<float>() : nullptr,
+                         gw.data_ptr<float>(), gb.data_ptr<float>(), coef.data_ptr<float>(), cur_stream());
+  return {coef, gw, gb};
+}
+
 }  // namespace
 
 void bind_conv(pybind11::module_& root) {
@@ -218,6 +262,8 @@ void bind_conv(pybind11::module_& root) {
         pybind11::arg("stats") = false, pybind11::arg("res") = pybind11::none(),
         pybind11::arg("py") = pybind11::none(), pybind11::arg("want_aout") = false);
   m.def("bn_finalize", &bn_finalize);
+  m.def("dgrad_bnred", &dgrad_bnred);
+  m.def("bnbwd_finalize", &bnbwd_finalize);
   m.def("wgrad1x1", &wgrad1x1, pybind11::arg("g"), pybind11::arg("x"), pybind11::arg("xcoef") = pybind11::none(),
         pybind11::arg("out_dtype") = pybind11::none());
 }

@@ -47,6 +47,12 @@ struct Args {
   const uint16_t* res;  // nullable [M][ncols]: y += res before the store (a residual gradient)
   const uint16_t* py;   // PRO == kProBnBwd: second operand tensor [M][K] (the BN's input)
   uint16_t* aout;       // PRO == kProBnBwd, nullable: the transformed operand written out [M][K]
+  // RED (dgrad form): the output is the gradient of a ReLU'd batch-norm output (the block
+  // below's) — masked with that BN's forward ReLU bits, and its backward reduction
+  // sum(g), sum(g * (x - mean)) accumulated per column into part [2][G][ncols]
+  const uint8_t* rbits;  // [M * ncols / 8]
+  const uint16_t* rx;    // the BN's input [M][ncols]
+  const float* rmean;    // the BN's batch mean [ncols]
 };
 
 // operand prologues
@@ -58,12 +64,13 @@ constexpr int kProBnBwd = 2;   // a' = c[k] * a + c[K + k] * y + c[2K + k]  (BN 
 constexpr int kWaves = 4, kRowsB = kWaves * 32;
 constexpr int kSS = 64 + 8;  // staging row stride (elements): rows h and h+4 land 16 banks apart
 
-template <int NC, int KR, int PRO>
+template <int NC, int KR, int PRO, bool RED = false>
 constexpr int lds_bytes() {
-  return NC * (KR + 8) * 2 + kWaves * 32 * kSS * 2 + (PRO == kProBnRelu ? 2 : PRO == kProBnBwd ? 3 : 0) * KR * 4;
+  return NC * (KR + 8) * 2 + kWaves * 32 * kSS * 2 + (PRO == kProBnRelu ? 2 : PRO == kProBnBwd ? 3 : 0) * KR * 4 +
+         (RED ? kWaves * 2 * NC * 4 : 0);
 }
 
-template <typename T, int NC, int KR, bool WT, int PRO, bool STATS>
+template <typename T, int NC, int KR, bool WT, int PRO, bool STATS, bool RED = false>
 __global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
   constexpr int BS = KR + 8;                 // B image row stride (elements)
   constexpr int CN = NC / 32;                // accumulator blocks per wave
@@ -75,6 +82,7 @@ __global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
   uint16_t* bimg = lds;                       // [NC][BS]
   uint16_t* stg = lds + NC * BS;              // [kWaves][32][kSS]
   float* pc = reinterpret_cast<float*>(stg + kWaves * 32 * kSS);  // [2 or 3][KR]
+  float* rsum = pc + (PRO == kProBnRelu ? 2 : PRO == kProBnBwd ? 3 : 0) * KR;  // RED: [kWaves][2][NC]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, lr = lane & 31, lh = lane >> 5;
   const int col0 = blockIdx.y * NC;
@@ -106,6 +114,8 @@ __global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
     sh[cb] = (STATS && p.shift) ? p.shift[col0 + 32 * cb + lr] : 0.f;
     s1[cb] = s2[cb] = 0.f;
   }
+  if constexpr (RED)
+    for (int i = tid; i < kWaves * 2 * NC; i += 256) rsum[i] = 0.f;
   __syncthreads();
 
   f32x16 acc[CN];
@@ -197,21 +207,64 @@ __global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) st[crow(r, lh) * kSS + 32 * q + lr] = from_f<T>(acc[2 * g + q][r]).x;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      float rs[8], rq[8], mu[8];
+      if constexpr (RED) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) rs[j] = rq[j] = 0.f;
+        Vec8<float>::load(mu, p.rmean + col0 + 64 * g + (lane & 7) * 8);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int qid = lane + 64 * i, rr = qid >> 3, c8 = (qid & 7) * 8;
         uint4 v = *reinterpret_cast<const uint4*>(st + rr * kSS + c8);
         const int64_t off = (row0 + rr) * p.ncols + col0 + 64 * g + c8;
         if (row0 + rr < p.m) {
-          if (p.res) {  // wave-uniform branch
-            float a[8], b[8];
+          if (RED || p.res) {  // wave-uniform branch
+            float a[8];
             Vec8<T>::load(a, reinterpret_cast<const T*>(&v));
-            Vec8<T>::load(b, reinterpret_cast<const T*>(p.res + off));
+            if (p.res) {
+              float b[8];
+              Vec8<T>::load(b, reinterpret_cast<const T*>(p.res + off));
 #pragma unroll
-            for (int j = 0; j < 8; ++j) a[j] += b[j];
+              for (int j = 0; j < 8; ++j) a[j] += b[j];
+            }
+            if constexpr (RED) {
+              const unsigned mb = p.rbits[off >> 3];
+              float xv[8];
+              Vec8<T>::load(xv, reinterpret_cast<const T*>(p.rx + off));
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                // the stored (rounded) gradient is what the rest of the backward sees
+                const float gq = ((mb >> j) & 1u) ? to_f(from_f<T>(a[j])) : 0.f;
+                a[j] = gq;
+                rs[j] += gq;
+                rq[j] = fmaf(gq, xv[j] - mu[j], rq[j]);
+              }
+            }
             Vec8<T>::store(reinterpret_cast<T*>(&v), a);
           }
           *reinterpret_cast<uint4*>(p.y + off) = v;
+        }
+      }
+      if constexpr (RED) {
+        // lanes l, l ^ 8, l ^ 16, ... hold the same 8 columns: fold them, then lanes 0-7 add
+        // into this wave's LDS accumulators (wave-private: no atomics)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+#pragma unroll
+          for (int o = 8; o < 64; o <<= 1) {
+            rs[j] += __shfl_xor(rs[j], o, 64);
+            rq[j] += __shfl_xor(rq[j], o, 64);
+          }
+        }
+        if (lane < 8) {
+          float* r0p = rsum + (wid * 2) * NC + 64 * g + lane * 8;
+          float* r1p = r0p + NC;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            r0p[j] += rs[j];
+            r1p[j] += rq[j];
+          }
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -246,6 +299,16 @@ __global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
     }
   }
 
+  if constexpr (RED) {
+    __syncthreads();
+    for (int i = tid; i < 2 * NC; i += 256) {
+      const int which = i / NC, n = i % NC;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) v += rsum[(w * 2 + which) * NC + n];
+      p.part[((int64_t)which * gridDim.x + blockIdx.x) * p.ncols + col0 + n] = v;
+    }
+  }
   if constexpr (STATS) {
     float* red = reinterpret_cast<float*>(stg);  // [kWaves][2][NC] (8 KB at NC = 256 <= staging slab)
 #pragma unroll
@@ -313,23 +376,57 @@ __global__ void __launch_bounds__(256) stats_finalize(const float* __restrict__ 
   if (rvar) rvar[ch] = (1.f - momentum) * rvar[ch] + momentum * (n > 1.f ? var_b * n / (n - 1.f) : var_b);
 }
 
-template <typename T, int NC, int KR, bool WT, int PRO, bool STATS>
+// backward reduction finalize (the RED partials): grad_w, grad_b and the dx coefficients
+// coef_bwd = [A | B | K] with dx = A * g + B * x + K (the BN backward of a training-mode norm)
+__global__ void __launch_bounds__(256) bwd_finalize(const float* __restrict__ part, int g, int c, float inv_n,
+                                                    const float* __restrict__ mean, const float* __restrict__ istd,
+                                                    const float* __restrict__ w, float* __restrict__ gw,
+                                                    float* __restrict__ gb, float* __restrict__ coef) {
+  __shared__ float red[2][32][9];
+  const int lc = threadIdx.x & 7, grp = threadIdx.x >> 3, ch = blockIdx.x * 8 + lc;
+  float a = 0.f, q = 0.f;
+  if (ch < c)
+    for (int j = grp; j < g; j += 32) {
+      a += part[(int64_t)j * c + ch];
+      q += part[(int64_t)(g + j) * c + ch];
+    }
+  red[0][grp][lc] = a;
+  red[1][grp][lc] = q;
+  __syncthreads();
+  if (grp != 0 || ch >= c) return;
+  float sdy = 0.f, sdyx = 0.f;
+#pragma unroll 8
+  for (int i = 0; i < 32; ++i) {
+    sdy += red[0][i][lc];
+    sdyx += red[1][i][lc];
+  }
+  const float is = istd[ch];
+  if (gw) gw[ch] = sdyx * is;
+  if (gb) gb[ch] = sdy;
+  const float A = is * (w ? w[ch] : 1.f);
+  const float B = -A * is * is * (sdyx * inv_n);
+  coef[ch] = A;
+  coef[c + ch] = B;
+  coef[2 * c + ch] = -A * (sdy * inv_n) - B * mean[ch];
+}
+
+template <typename T, int NC, int KR, bool WT, int PRO, bool STATS, bool RED = false>
 void launch_t(const Args& a, int cus, hipStream_t s) {
-  constexpr int lds = lds_bytes<NC, KR, PRO>();
+  constexpr int lds = lds_bytes<NC, KR, PRO, RED>();
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fused1x1<T, NC, KR, WT, PRO, STATS>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fused1x1<T, NC, KR, WT, PRO, STATS, RED>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
   const int per_cu = (160 * 1024) / lds >= 2 ? 2 : 1;
   int gx = cus * per_cu;
   if (gx > a.ntiles) gx = a.ntiles;
-  hipLaunchKernelGGL((fused1x1<T, NC, KR, WT, PRO, STATS>), dim3(gx, a.ncols / NC), dim3(256), lds, s, a);
+  hipLaunchKernelGGL((fused1x1<T, NC, KR, WT, PRO, STATS, RED>), dim3(gx, a.ncols / NC), dim3(256), lds, s, a);
 }
 
-inline int grid_x(int64_t m, int nc, int kr, int pro, int cus) {
-  const int lds = nc * (kr + 8) * 2 + kWaves * 32 * kSS * 2 + pro * kr * 4;
+inline int grid_x(int64_t m, int nc, int kr, int pro, int cus, bool red = false) {
+  const int lds = nc * (kr + 8) * 2 + kWaves * 32 * kSS * 2 + pro * kr * 4 + (red ? kWaves * 2 * nc * 4 : 0);
   const int per_cu = (160 * 1024) / lds >= 2 ? 2 : 1;
   const int ntiles = (int)((m + kRowsB - 1) / kRowsB);
   const int gx = cus * per_cu;
@@ -344,11 +441,11 @@ inline int col_tile(int ncols, int kr) {
   return ncols % 128 == 0 ? 128 : 64;
 }
 
-template <typename T, bool WT, int PRO, bool STATS>
+template <typename T, bool WT, int PRO, bool STATS, bool RED = false>
 void dispatch_shape(const Args& a, int nc, int kr, int cus, hipStream_t s) {
 #define C1BN_CASE(NC_, KR_)                                 \
   if (nc == NC_ && kr == KR_) {                             \
-    launch_t<T, NC_, KR_, WT, PRO, STATS>(a, cus, s);       \
+    launch_t<T, NC_, KR_, WT, PRO, STATS, RED>(a, cus, s);  \
     return;                                                 \
   }
   C1BN_CASE(64, 64) C1BN_CASE(64, 128) C1BN_CASE(64, 256) C1BN_CASE(64, 512)
@@ -413,6 +510,35 @@ void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int nco
   };
   dispatch_16(dtype, go, "conv1x1_bn");
   check_launch("conv1x1_bn");
+}
+
+int conv1x1_dgrad_bnred_partials(int64_t m, int k, int ncols, int cus) {
+  return c1bn::grid_x(m, c1bn::col_tile(ncols, k), k, 0, cus, true);
+}
+
+void conv1x1_dgrad_bnred(const void* g, const void* w, void* out, int64_t m, int k, int ncols, int dtype,
+                         const void* res, const uint8_t* bits, const void* x, const float* mean, float* part, int cus,
+                         hipStream_t s) {
+  if (!conv1x1_bn_supported(m, k, ncols)) throw std::runtime_error("conv1x1_dgrad_bnred: unsupported shape");
+  if (!bits || !x || !mean || !part) throw std::runtime_error("conv1x1_dgrad_bnred: bits, x, mean and part required");
+  c1bn::Args args{};
+  args.a = static_cast<const uint16_t*>(g);
+  args.w = static_cast<const uint16_t*>(w);
+  args.y = static_cast<uint16_t*>(out);
+  args.m = m;
+  args.ncols = ncols;
+  args.ntiles = (int)((m + c1bn::kRowsB - 1) / c1bn::kRowsB);
+  args.part = part;
+  args.res = static_cast<const uint16_t*>(res);
+  args.rbits = bits;
+  args.rx = static_cast<const uint16_t*>(x);
+  args.rmean = mean;
+  const int nc = c1bn::col_tile(ncols, k);
+  dispatch_16(dtype, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    c1bn::dispatch_shape<T, true, c1bn::kProNone, false, true>(args, nc, k, cus, s);
+  }, "conv1x1_dgrad_bnred");
+  check_launch("conv1x1_dgrad_bnred");
 }
 
 void conv1x1_bn_finalize(const float* part, int g, int c, float n, const float* shift, const float* w, const float* b,
@@ -590,21 +716,25 @@ __device__ __forceinline__ void dma16(const uint16_t* src, uint16_t* lds_dst) {
 // wait until at most N of this wave's DMA instructions are in flight (N = one chunk's worth)
 template <int N>
 __device__ __forceinline__ void vm_wait_ring() {
-  static_assert(N == 0 || N == 4 || N == 6 || N == 8 || N == 10 || N == 12, "ring vmcnt");
+  static_assert(N >= 0 && N <= 6 || N == 8 || N == 10 || N == 12, "ring vmcnt");
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
 }
 
-template <int COLS>
+template <int COLS, int RMB>
 __device__ __forceinline__ void issue_img(const uint16_t* __restrict__ src, int64_t ld, int col0, int64_t base,
                                           int64_t mlast, uint16_t* img, int wave, int lane) {
   constexpr int CPR = COLS / 8;               // 16-byte chunks per row
   constexpr int RPI = 64 / CPR;               // rows per 1-KB instruction
-  constexpr int NI = MB * COLS / 512;         // instructions per image
+  constexpr int NI = RMB * COLS / 512;        // instructions per image
   static_assert(NI % 4 == 0, "image instructions split over 4 waves");
 #pragma unroll
   for (int i = 0; i < NI / 4; ++i) {
@@ -628,13 +758,18 @@ __device__ __forceinline__ s16x8 frag_ring(const uint16_t* img, int colbase, int
   return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
+// 32-row chunks: 60 KB of ring at 256 x 64, so two workgroups (8 waves) share a CU and one's
+// barrier stalls overlap the other's loads
+constexpr int RMB = 32;
+
 template <int NT, int KT>
 constexpr int ring_lds_bytes() {
-  return kRing * MB * (NT + KT) * 2;
+  return kRing * RMB * (NT + KT) * 2;
 }
 
 template <typename T, int NT, int KT, bool PRO>
-__global__ void __launch_bounds__(256, 1) wgrad1x1_ring(Args p) {
+__global__ void __launch_bounds__(256, 2) wgrad1x1_ring(Args p) {
+  constexpr int MB = RMB;
   constexpr int WN = NT / 64, WK = KT / 64;
   constexpr int GI = MB * NT / 512 / 4, XI = MB * KT / 512 / 4;  // DMA instructions per wave per chunk
   constexpr int PER = GI + XI;
@@ -661,8 +796,8 @@ __global__ void __launch_bounds__(256, 1) wgrad1x1_ring(Args p) {
   auto issue = [&](int c) {
     uint16_t* gi = slot_g(c);
     const int64_t base = r0 + (int64_t)c * MB;
-    issue_img<NT>(p.g, p.n, n0, base, mlast, gi, wid, lane);
-    issue_img<KT>(p.x, p.k, k0, base, mlast, gi + MB * NT, wid, lane);
+    issue_img<NT, MB>(p.g, p.n, n0, base, mlast, gi, wid, lane);
+    issue_img<KT, MB>(p.x, p.k, k0, base, mlast, gi + MB * NT, wid, lane);
   };
 
   f32x16 acc[WN][WK];
@@ -770,7 +905,7 @@ inline int splits(int64_t m, int n, int k, int cus) {
   int nt, kt;
   tile(n, k, nt, kt);
   const int tiles = (n / nt) * (k / kt);
-  int s = (cus + tiles - 1) / tiles;
+  int s = (2 * cus + tiles - 1) / tiles;  // two workgroups per CU (ring kernel)
   const int64_t maxs = (m + MB - 1) / MB;
   if (s > maxs) s = (int)maxs;
   return s < 1 ? 1 : s;
@@ -855,6 +990,13 @@ void conv1x1_wgrad(const void* g, const void* x, void* dw, int out_dtype, int64_
     hipLaunchKernelGGL((c1w::wgrad_reduce<TO>), dim3(blocks), dim3(256), 0, s, ws, sp, nk, static_cast<TO*>(dw));
   }, "conv1x1 wgrad reduce");
   check_launch("conv1x1_wgrad");
+}
+
+void conv1x1_bnbwd_finalize(const float* part, int g, int c, float inv_n, const float* mean, const float* istd,
+                            const float* w, float* gw, float* gb, float* coef, hipStream_t s) {
+  hipLaunchKernelGGL(c1bn::bwd_finalize, dim3((c + 7) / 8), dim3(256), 0, s, part, g, c, inv_n, mean, istd, w, gw, gb,
+                     coef);
+  check_launch("conv1x1_bnbwd_finalize");
 }
 
 }  // namespace apex_amd

@@ -86,4 +86,15 @@ int64_t conv1x1_wgrad_workspace_floats(int64_t m, int n, int k, int cus);
 void conv1x1_wgrad(const void* g, const void* x, void* dw, int out_dtype, int64_t m, int n, int k, int dtype,
                    const float* xcoef, float* ws, int cus, hipStream_t s);
 
+// dgrad form with the BN-backward reduction of the block below in the epilogue:
+// out = mask(g . W + res) (mask = bits, that BN's forward ReLU bit mask) and per-column partial
+// sums [2][G][ncols] of out and out * (x - mean); G = conv1x1_dgrad_bnred_partials(...).
+// conv1x1_bnbwd_finalize turns them into grad_w, grad_b and coef_bwd [3][C].
+int conv1x1_dgrad_bnred_partials(int64_t m, int k, int ncols, int cus);
+void conv1x1_dgrad_bnred(const void* g, const void* w, void* out, int64_t m, int k, int ncols, int dtype,
+                         const void* res, const uint8_t* bits, const void* x, const float* mean, float* part, int cus,
+                         hipStream_t s);
+void conv1x1_bnbwd_finalize(const float* part, int g, int c, float inv_n, const float* mean, const float* istd,
+                            const float* w, float* gw, float* gb, float* coef, hipStream_t s);
+
 }  // namespace apex_amd

@@ -109,6 +109,16 @@ class Bottleneck(nn.Module):
         self.stride = stride
         self.fork_out = False
 
+    def forward_linked(self, x, link_in):
+        """Fused-node forward that chains with its neighbours (``ops.bottleneck_bn.BlockLink``):
+        returns ``(out, link_out)``; falls back to ``forward`` (and no link) off the node path."""
+        from ..ops import bottleneck_bn
+
+        if self.fused_bn and not isinstance(x, tuple) and self.training and bottleneck_bn.block_supported(self, x):
+            link_out = bottleneck_bn.BlockLink()
+            return bottleneck_bn.bottleneck_forward(self, x, link_in, link_out), link_out
+        return self.forward(x), None
+
     def forward(self, x):
         if self.fused_bn:
             from ..ops import bottleneck_bn
@@ -200,9 +210,20 @@ class ResNet(nn.Module):
             from ..contrib.groupbn import bn_relu_maxpool
 
             x = bn_relu_maxpool(self.conv1(x), self.bn1, self.maxpool)
+            # bottleneck nodes hand each other their output BN's state (ops/bottleneck_bn.py
+            # BlockLink): block i+1's conv1 dgrad does block i's bn3 backward reduction
+            link = None
+            for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+                for blk in layer:
+                    if isinstance(blk, Bottleneck):
+                        x, link = blk.forward_linked(x, link)
+                    else:
+                        x, link = blk(x), None
         else:
             x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
-        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+            x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        if isinstance(x, tuple):
+            x = x[0]
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)
 

@@ -38,6 +38,9 @@ from .. import _native
 from . import conv as convops
 
 _ENABLED = os.environ.get("APEX_AMD_FUSED_BLOCK", "1") != "0"
+# tests: take every native 1x1 route the kernels support, whatever the size (small test shapes
+# would otherwise route to the library)
+FORCE_NATIVE = os.environ.get("APEX_AMD_FUSED_BLOCK_FORCE_NATIVE", "0") == "1"
 _NATIVE_K = (64, 128, 256, 512)
 
 
@@ -58,6 +61,22 @@ def _nchw(t2, n, h, w):
     return t2.view(n, h, w, t2.size(1)).permute(0, 3, 1, 2)
 
 
+class BlockLink:
+    """Hand-off between two consecutive block nodes (block i's output feeds only block i+1).
+
+    Forward: block i stores its output batch norm's input y3, ReLU bit mask and batch
+    statistics here.  Backward: block i+1's conv1 data gradient masks its result with those bits
+    and accumulates bn3_i's backward reduction in the same kernel (``dgrad_bnred``), returning
+    the masked gradient and leaving the partial sums in ``part``; block i then finalizes them
+    instead of re-reading its output gradient — one full read + write of the block output saved
+    per block boundary."""
+
+    __slots__ = ("y3", "bits", "mean", "invstd", "part")
+
+    def __init__(self):
+        self.y3 = self.bits = self.mean = self.invstd = self.part = None
+
+
 class _BN:
     """Per-BN constants of one forward: fp32 affine params, running buffers, momentum / eps."""
 
@@ -75,16 +94,28 @@ class _BN:
 # longer holds a 256-column tile) and at stage-3/4 sizes hipBLASLt is faster, so those run there
 # with the separate statistics / apply passes.
 def _fwd_native(m, k, n):
+    if FORCE_NATIVE:
+        return k in _NATIVE_K and n % 64 == 0
     return k in _NATIVE_K and n % 64 == 0 and n <= 512 and not (k == 512 and n >= 256)
 
 
 def _dgrad_native(m, kout, cin):
+    if FORCE_NATIVE:
+        return kout in _NATIVE_K and cin % 64 == 0
     return kout in _NATIVE_K and cin % 64 == 0 and cin <= 256 and m >= 100000
+
+
+def _red_native(m, kout, cin):
+    # the masked dgrad + reduction replaces a 4-tensor-pass reduction of the block output, which
+    # outweighs hipBLASLt's lead on the plain dgrad up to 512 output channels (stages 1-2)
+    if FORCE_NATIVE:
+        return kout in _NATIVE_K and cin % 64 == 0
+    return kout in _NATIVE_K and cin % 64 == 0 and cin <= 512 and m >= 100000
 
 
 def _wgrad_native(m, n, k, pro):
     # MIOpen's split-K wgrad leads at the 56x56 shapes unless the operand needs the BN prologue
-    return pro or m < 500000
+    return FORCE_NATIVE or pro or m < 500000
 
 
 def conv1x1_bn_fwd(a2, w2d, pcoef, bn):
@@ -93,7 +124,7 @@ def conv1x1_bn_fwd(a2, w2d, pcoef, bn):
     m, k = a2.shape
     n = w2d.size(0)
     if _fwd_native(m, k, n):
-        y2, part = _conv().bn1x1(a2, w2d, False, pcoef, bn.rm, True)
+        y2, part, _ = _conv().bn1x1(a2, w2d, False, pcoef, bn.rm, True)
         sm, si, coef = _conv().bn_finalize(part, float(m), bn.rm, bn.w, bn.b, bn.rm, bn.rv, bn.eps, bn.mom)
         return y2, sm, si, coef
     if pcoef is not None:
@@ -143,7 +174,7 @@ def _conv_bwd(gy, x, w, stride, pad, need_x=True):
 class _BottleneckFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, w2, w3, wds, g1, b1, g2, b2, g3, b3, gds, bds, cfg):
-        bn1, bn2, bn3, bnd, stride = cfg
+        bn1, bn2, bn3, bnd, stride, link_in, link_out = cfg
         n, cin, h, wd = x.shape
         width = w1.size(0)
         cout = w3.size(0)
@@ -173,6 +204,9 @@ class _BottleneckFn(torch.autograd.Function):
         ctx.save_for_backward(x, w1, w2, w3, wds, g1, g2, g3, gds, y1, z1, y2m, y3, yd, bits,
                               sm1, si1, c1, sm2, si2, c2, sm3, si3, c3, smd, sid, cd)
         ctx.geo = (n, h, wd, oh, ow, stride)
+        ctx.links = (link_in, link_out)
+        if link_out is not None:
+            link_out.y3, link_out.bits, link_out.mean, link_out.invstd = y3, bits, sm3, si3
         return _nchw(out2, n, oh, ow)
 
     @staticmethod
@@ -185,10 +219,17 @@ class _BottleneckFn(torch.autograd.Function):
         gout = gout.contiguous(memory_format=torch.channels_last)
         go2 = _m2(gout)
         x2 = _m2(x)
-        # bn3 (+ shortcut): masked gradient dm (= the identity branch's gradient) + coefficients;
-        # its dx pass runs as conv3's dgrad operand prologue (dx3 written as a by-product for
-        # the weight gradient) where that kernel takes the shape
-        dm, cb3, gg3, gb3 = bn.bwd_reduce(go2, y3, g3, sm3, si3, c3, True, bits)
+        link_in, link_out = ctx.links
+        # bn3 (+ shortcut): masked gradient dm (= the identity branch's gradient) + coefficients
+        # (the block above already masked the gradient and reduced it when linked); bn3's dx
+        # pass runs as conv3's dgrad operand prologue (dx3 written as a by-product for the
+        # weight gradient) where that kernel takes the shape
+        if link_out is not None and link_out.part is not None:
+            dm = go2
+            cb3, gg3, gb3 = _conv().bnbwd_finalize(link_out.part, float(go2.size(0)), sm3, si3, g3)
+            link_out.part = None
+        else:
+            dm, cb3, gg3, gb3 = bn.bwd_reduce(go2, y3, g3, sm3, si3, c3, True, bits)
         w3m = w3.view(cout, width)
         if _dgrad_native(dm.size(0), cout, width):
             dz2, _, dx3 = _conv().bn1x1(dm, w3m, True, cb3.view(-1), None, False, None, y3, True)
@@ -216,7 +257,12 @@ class _BottleneckFn(torch.autograd.Function):
             else:
                 dxd, dwd = _conv_bwd(_nchw(dyd, n, oh, ow), x, wds, stride, 0)
                 short = _m2(dxd.contiguous(memory_format=torch.channels_last))
-        dx = conv1x1_dgrad(dy1, w1.view(width, cin), short)
+        if link_in is not None and link_in.bits is not None and _red_native(dy1.size(0), width, cin):
+            # mask with the block below's ReLU bits + its bn3 backward reduction, in this kernel
+            dx, link_in.part = _conv().dgrad_bnred(dy1, w1.view(width, cin), short, link_in.bits, link_in.y3,
+                                                   link_in.mean)
+        else:
+            dx = conv1x1_dgrad(dy1, w1.view(width, cin), short)
         dw1 = conv1x1_wgrad(dy1, x2, None, w1, (n, h, wd))
         return (_nchw(dx, n, h, wd), dw1, dw2, dw3, dwd, gg1, gb1, gg2, gb2, gg3, gb3, ggd, gbd, None)
 
@@ -250,12 +296,15 @@ def block_supported(block, x):
     return all(c % 64 == 0 for c in chans)
 
 
-def bottleneck_forward(block, x):
+def bottleneck_forward(block, x, link_in=None, link_out=None):
+    """Run ``block`` as one node.  ``link_in``: the BlockLink the block below filled (its output
+    is ``x`` and feeds nothing else); ``link_out``: a fresh BlockLink for the block above."""
     ds = block.downsample
     stride = block.conv2.stride[0]
     if ds is not None and ds[0].stride[0] != stride:
         raise ValueError("fused bottleneck: downsample stride must match conv2's")
-    cfg = (_BN(block.bn1), _BN(block.bn2), _BN(block.bn3), _BN(ds[1]) if ds is not None else None, stride)
+    cfg = (_BN(block.bn1), _BN(block.bn2), _BN(block.bn3), _BN(ds[1]) if ds is not None else None, stride,
+           link_in, link_out)
     return _BottleneckFn.apply(
         x, block.conv1.weight, block.conv2.weight, block.conv3.weight, ds[0].weight if ds is not None else None,
         block.bn1.weight, block.bn1.bias, block.bn2.weight, block.bn2.bias, block.bn3.weight, block.bn3.bias,

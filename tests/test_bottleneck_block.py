@@ -137,12 +137,31 @@ def test_gpu_fused_bottleneck_node_vs_module_path(inplanes, planes, stride, down
 
 
 @pytest.mark.gpu
-def test_gpu_fused_bottleneck_resnet50_step_matches_module_path():
-    """A full fused-BN ResNet-50 training step: the block nodes vs the per-module fused path
-    (APEX_AMD_FUSED_BLOCK off) — same loss, close gradients."""
+@pytest.mark.parametrize("force_native", [False, True])
+def test_gpu_fused_bottleneck_resnet50_step_matches_module_path(force_native, monkeypatch):
+    """A full fused-BN ResNet-50 training step: the chained block nodes (BlockLink hand-offs)
+    vs the per-module fused path (APEX_AMD_FUSED_BLOCK off) — same loss, close gradients.
+    force_native: every native 1x1 route (incl. the masked dgrad + reduction across blocks)
+    even at this small size."""
     import apex  # noqa: F401
     from apex.models import resnet50
     from apex.ops import bottleneck_bn
+
+    monkeypatch.setattr(bottleneck_bn, "FORCE_NATIVE", force_native)
+    calls = {"red": 0}
+    conv = apex._native.require("conv").conv
+    orig = conv.dgrad_bnred
+
+    class _Spy:
+        def __getattr__(self, name):
+            if name == "dgrad_bnred":
+                def f(*a):
+                    calls["red"] += 1
+                    return orig(*a)
+                return f
+            return getattr(conv, name)
+
+    monkeypatch.setattr(bottleneck_bn, "_conv", lambda: _Spy())
 
     torch.manual_seed(0)
     m1 = resnet50(fused_bn=True).cuda().to(memory_format=torch.channels_last)
@@ -165,6 +184,8 @@ def test_gpu_fused_bottleneck_resnet50_step_matches_module_path():
 
     l1, l2 = step(m1, True), step(m2, False)
     torch.testing.assert_close(l1, l2, atol=2e-2, rtol=2e-2)
+    # 16 bottlenecks, 15 boundaries; the masked-dgrad hand-off where the route takes it
+    assert calls["red"] == (15 if force_native else 0), calls
     g2 = dict(m2.named_parameters())
     worst = max(_rel(p.grad, g2[n].grad) for n, p in m1.named_parameters())
     assert worst < 0.1, worst

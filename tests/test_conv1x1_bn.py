@@ -40,7 +40,7 @@ def test_gpu_bn1x1_forward_and_stats(dtype, m, k, nc, pro):
     w = (torch.randn(nc, k, device="cuda") * 0.1).to(dtype)
     pcoef = torch.cat([torch.rand(k, device="cuda") + 0.5, torch.randn(k, device="cuda") * 0.3]) if pro else None
     shift = torch.randn(nc, device="cuda") * 0.1
-    y, part = ext.bn1x1(a, w, False, pcoef, shift, True)
+    y, part, _ = ext.bn1x1(a, w, False, pcoef, shift, True)
     af = a.float()
     if pro:
         af = torch.relu(af * pcoef[:k] + pcoef[k:]).to(dtype).float()
@@ -70,11 +70,11 @@ def test_gpu_bn1x1_dgrad_form(dtype, m, k, nc):
     torch.manual_seed(1)
     a = torch.randn(m, k, device="cuda").to(dtype)
     w = (torch.randn(k, nc, device="cuda") * 0.1).to(dtype)
-    y, part = ext.bn1x1(a, w, True)
+    y, part, _ = ext.bn1x1(a, w, True)
     assert part is None or part.numel() == 0
     _close(y, a.float() @ w.float(), 1e-2)
     res = torch.randn(m, nc, device="cuda").to(dtype)
-    y2, _ = ext.bn1x1(a, w, True, None, None, False, res)
+    y2, _, _ = ext.bn1x1(a, w, True, None, None, False, res)
     _close(y2, a.float() @ w.float() + res.float(), 1e-2)
 
 
@@ -90,7 +90,7 @@ def test_gpu_bn1x1_large_mean_shift():
     a[:, 0] = 300.0  # every output channel ~ 300 + small noise
     yr = a.float() @ w.float().t()
     shift = yr[:64].mean(0)  # a running-mean-like estimate
-    _, part = ext.bn1x1(a, w, False, None, shift, True)
+    _, part, _ = ext.bn1x1(a, w, False, None, shift, True)
     sm, si, _ = ext.bn_finalize(part, float(m), shift, None, None, None, None, 1e-5, 0.1)
     torch.testing.assert_close(si, torch.rsqrt(yr.var(0, unbiased=False) + 1e-5), atol=0, rtol=1e-2)
 
