@@ -61,17 +61,24 @@ constexpr int kProBnRelu = 1;  // a' = relu(a * c[k] + c[K + k])            (BN 
 constexpr int kProBnBwd = 2;   // a' = c[k] * a + c[K + k] * y + c[2K + k]  (BN backward dx from the
                                //       masked gradient a and the BN input y: bwd_apply fused)
 
-constexpr int kWaves = 4, kRowsB = kWaves * 32;
 constexpr int kSS = 64 + 8;  // staging row stride (elements): rows h and h+4 land 16 banks apart
 
-template <int NC, int KR, int PRO, bool RED = false>
-constexpr int lds_bytes() {
-  return NC * (KR + 8) * 2 + kWaves * 32 * kSS * 2 + (PRO == kProBnRelu ? 2 : PRO == kProBnBwd ? 3 : 0) * KR * 4 +
-         (RED ? kWaves * 2 * NC * 4 : 0);
+constexpr int lds_bytes_nw(int nc, int kr, int pro, bool red, int nw) {
+  return nc * (kr + 8) * 2 + nw * 32 * kSS * 2 + (pro == kProBnRelu ? 2 : pro == kProBnBwd ? 3 : 0) * kr * 4 +
+         (red ? nw * 2 * nc * 4 : 0);
 }
 
-template <typename T, int NC, int KR, bool WT, int PRO, bool STATS, bool RED = false>
-__global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
+// waves per workgroup: 4 (two workgroups per CU) while the weight image is small; 8 sharing one
+// image when a 4-wave workgroup would hold the CU's LDS alone anyway (8 waves either way — a
+// 4-wave CU streams at half the rate, profiles/resnet50_node_r03a.md)
+constexpr int pick_nw(int nc, int kr, int pro, bool red) {
+  return lds_bytes_nw(nc, kr, pro, red, 4) <= 80 * 1024 ? 4
+         : lds_bytes_nw(nc, kr, pro, red, 8) <= 160 * 1024 ? 8 : 4;
+}
+
+template <typename T, int NC, int KR, bool WT, int PRO, bool STATS, bool RED, int NW>
+__global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
+  constexpr int kWaves = NW, kRowsB = NW * 32, NT = NW * 64;
   constexpr int BS = KR + 8;                 // B image row stride (elements)
   constexpr int CN = NC / 32;                // accumulator blocks per wave
   constexpr int KCH = KR < (NC >= 256 ? 64 : 128) ? KR : (NC >= 256 ? 64 : 128);  // k depth per register chunk
@@ -89,13 +96,13 @@ __global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
 
   // ---- weight tile -> LDS, once per workgroup ----
   if constexpr (!WT) {
-    for (int i = tid; i < NC * KR / 8; i += 256) {
+    for (int i = tid; i < NC * KR / 8; i += NT) {
       const int n = i / (KR / 8), k8 = (i % (KR / 8)) * 8;
       *reinterpret_cast<uint4*>(bimg + n * BS + k8) =
           *reinterpret_cast<const uint4*>(p.w + (int64_t)(col0 + n) * KR + k8);
     }
   } else {
-    for (int i = tid; i < NC * KR / 8; i += 256) {
+    for (int i = tid; i < NC * KR / 8; i += NT) {
       const int k = i / (NC / 8), n8 = (i % (NC / 8)) * 8;
       const uint4 v = *reinterpret_cast<const uint4*>(p.w + (int64_t)k * p.ncols + col0 + n8);
       const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
@@ -107,7 +114,7 @@ __global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
     }
   }
   if constexpr (PRO != kProNone)
-    for (int i = tid; i < (PRO == kProBnBwd ? 3 : 2) * KR; i += 256) pc[i] = p.pcoef[i];
+    for (int i = tid; i < (PRO == kProBnBwd ? 3 : 2) * KR; i += NT) pc[i] = p.pcoef[i];
   float sh[CN], s1[CN], s2[CN];
 #pragma unroll
   for (int cb = 0; cb < CN; ++cb) {
@@ -115,7 +122,7 @@ __global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
     s1[cb] = s2[cb] = 0.f;
   }
   if constexpr (RED)
-    for (int i = tid; i < kWaves * 2 * NC; i += 256) rsum[i] = 0.f;
+    for (int i = tid; i < kWaves * 2 * NC; i += NT) rsum[i] = 0.f;
   __syncthreads();
 
   f32x16 acc[CN];
@@ -247,25 +254,28 @@ __global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
         }
       }
       if constexpr (RED) {
-        // lanes l, l ^ 8, l ^ 16, ... hold the same 8 columns: fold them, then lanes 0-7 add
-        // into this wave's LDS accumulators (wave-private: no atomics)
+        // lanes l, l ^ 8, ..., l ^ 56 hold the same 8 columns: a reduce-scatter over lane bits
+        // 5, 4, 3 (4 + 2 + 1 exchanges per sum instead of 3 x 8) leaves lane l the total of
+        // column 4 b5 + 2 b4 + b3 of its 8; the 64 lanes then own 64 distinct columns and add
+        // them into this wave's LDS accumulators (wave-private: no atomics)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int st = 0; st < 3; ++st) {
+          const int msk = 32 >> st, half = 4 >> st;
+          const bool up = (lane & msk) != 0;
 #pragma unroll
-          for (int o = 8; o < 64; o <<= 1) {
-            rs[j] += __shfl_xor(rs[j], o, 64);
-            rq[j] += __shfl_xor(rq[j], o, 64);
+          for (int j = 0; j < half; ++j) {
+            const float ss = up ? rs[j] : rs[j + half];
+            const float sq = up ? rq[j] : rq[j + half];
+            const float gs = __shfl_xor(ss, msk, 64);
+            const float gq = __shfl_xor(sq, msk, 64);
+            rs[j] = (up ? rs[j + half] : rs[j]) + gs;
+            rq[j] = (up ? rq[j + half] : rq[j]) + gq;
           }
         }
-        if (lane < 8) {
-          float* r0p = rsum + (wid * 2) * NC + 64 * g + lane * 8;
-          float* r1p = r0p + NC;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            r0p[j] += rs[j];
-            r1p[j] += rq[j];
-          }
-        }
+        const int jc = ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1);
+        float* r0p = rsum + (wid * 2) * NC + 64 * g + (lane & 7) * 8 + jc;
+        r0p[0] += rs[0];
+        r0p[NC] += rq[0];
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
@@ -301,7 +311,7 @@ __global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
 
   if constexpr (RED) {
     __syncthreads();
-    for (int i = tid; i < 2 * NC; i += 256) {
+    for (int i = tid; i < 2 * NC; i += NT) {
       const int which = i / NC, n = i % NC;
       float v = 0.f;
 #pragma unroll
@@ -325,7 +335,7 @@ __global__ void __launch_bounds__(256, 2) fused1x1(Args p) {
       }
     }
     __syncthreads();
-    for (int i = tid; i < 2 * NC; i += 256) {
+    for (int i = tid; i < 2 * NC; i += NT) {
       const int which = i / NC, n = i % NC;
       float v = 0.f;
 #pragma unroll
@@ -411,24 +421,29 @@ __global__ void __launch_bounds__(256) bwd_finalize(const float* __restrict__ pa
 }
 
 template <typename T, int NC, int KR, bool WT, int PRO, bool STATS, bool RED = false>
-void launch_t(const Args& a, int cus, hipStream_t s) {
-  constexpr int lds = lds_bytes<NC, KR, PRO, RED>();
+void launch_t(const Args& a0, int cus, hipStream_t s) {
+  constexpr int NW = pick_nw(NC, KR, PRO, RED);
+  constexpr int lds = lds_bytes_nw(NC, KR, PRO, RED, NW);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fused1x1<T, NC, KR, WT, PRO, STATS, RED>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fused1x1<T, NC, KR, WT, PRO, STATS, RED, NW>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
+  Args a = a0;
+  a.ntiles = (int)((a.m + NW * 32 - 1) / (NW * 32));
   const int per_cu = (160 * 1024) / lds >= 2 ? 2 : 1;
   int gx = cus * per_cu;
   if (gx > a.ntiles) gx = a.ntiles;
-  hipLaunchKernelGGL((fused1x1<T, NC, KR, WT, PRO, STATS, RED>), dim3(gx, a.ncols / NC), dim3(256), lds, s, a);
+  hipLaunchKernelGGL((fused1x1<T, NC, KR, WT, PRO, STATS, RED, NW>), dim3(gx, a.ncols / NC), dim3(NW * 64), lds, s,
+                     a);
 }
 
 inline int grid_x(int64_t m, int nc, int kr, int pro, int cus, bool red = false) {
-  const int lds = nc * (kr + 8) * 2 + kWaves * 32 * kSS * 2 + pro * kr * 4 + (red ? kWaves * 2 * nc * 4 : 0);
+  const int nw = pick_nw(nc, kr, pro, red);
+  const int lds = lds_bytes_nw(nc, kr, pro, red, nw);
   const int per_cu = (160 * 1024) / lds >= 2 ? 2 : 1;
-  const int ntiles = (int)((m + kRowsB - 1) / kRowsB);
+  const int ntiles = (int)((m + nw * 32 - 1) / (nw * 32));
   const int gx = cus * per_cu;
   return gx < ntiles ? gx : ntiles;
 }
@@ -464,7 +479,7 @@ bool conv1x1_bn_supported(int64_t m, int k, int ncols) {
 }
 
 int conv1x1_bn_partials(int64_t m, int k, int ncols, bool pro, int cus) {
-  return c1bn::grid_x(m, c1bn::col_tile(ncols, k), k, pro ? 2 : 0, cus);
+  return c1bn::grid_x(m, c1bn::col_tile(ncols, k), k, pro ? c1bn::kProBnRelu : c1bn::kProNone, cus);
 }
 
 void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int ncols, bool w_kmajor_out, int dtype,
@@ -477,7 +492,7 @@ void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int nco
   args.y = static_cast<uint16_t*>(y);
   args.m = m;
   args.ncols = ncols;
-  args.ntiles = (int)((m + c1bn::kRowsB - 1) / c1bn::kRowsB);
+  args.ntiles = 0;  // set per wave count by launch_t
   args.pcoef = pcoef;
   args.shift = shift;
   args.part = part;
@@ -527,7 +542,7 @@ void conv1x1_dgrad_bnred(const void* g, const void* w, void* out, int64_t m, int
   args.y = static_cast<uint16_t*>(out);
   args.m = m;
   args.ncols = ncols;
-  args.ntiles = (int)((m + c1bn::kRowsB - 1) / c1bn::kRowsB);
+  args.ntiles = 0;  // set per wave count by launch_t
   args.part = part;
   args.res = static_cast<const uint16_t*>(res);
   args.rbits = bits;
@@ -865,19 +880,34 @@ __global__ void __launch_bounds__(256, 2) wgrad1x1_ring(Args p) {
       }
 }
 
-// dW = sum over the S split partials in a fixed order, 8 consecutive elements per thread
+// dW = sum over the S split partials in a fixed order.  A block owns 16 consecutive 8-element
+// vectors; its 16 thread groups each sum every 16th split (splits g, g+16, ...), then one fixed-
+// order LDS pass adds the 16 group sums — S / 16 loads per thread instead of S, and nk / 128
+// blocks (a [256][64] weight: 128 blocks, not 8).
 template <typename TO>
 __global__ void __launch_bounds__(256) wgrad_reduce(const float* __restrict__ ws, int s, int64_t nk,
                                                     TO* __restrict__ out) {
-  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
-  if (i >= nk) return;
+  __shared__ float red[16][16 * 8 + 4];
+  const int v = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int64_t i = ((int64_t)blockIdx.x * 16 + v) * 8;
   float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int q = 0; q < s; ++q) {
-    float v[8];
-    Vec8<float>::load(v, ws + (int64_t)q * nk + i);
+  if (i < nk) {
+    for (int q = grp; q < s; q += 16) {
+      float t[8];
+      Vec8<float>::load(t, ws + (int64_t)q * nk + i);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) a[j] += v[j];
+      for (int j = 0; j < 8; ++j) a[j] += t[j];
+    }
   }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[grp][v * 8 + j] = a[j];
+  __syncthreads();
+  if (grp != 0 || i >= nk) return;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = 0.f;
+  for (int g2 = 0; g2 < 16; ++g2)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] += red[g2][v * 8 + j];
   Vec8<TO>::store(out + i, a);
 }
 
@@ -901,23 +931,25 @@ inline void tile(int n, int k, int& nt, int& kt) {
   kt = pick ? pick[1] : 64;
 }
 
+// APEX_AMD_WGRAD_RING=1: the LDS-DMA ring variant (A/B; the register-staged loop measured
+// faster on every ResNet-50 shape, profiles/bn1x1_kernels_r03a.jsonl vs the ring run)
+inline bool ring_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("APEX_AMD_WGRAD_RING");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 inline int splits(int64_t m, int n, int k, int cus) {
   int nt, kt;
   tile(n, k, nt, kt);
   const int tiles = (n / nt) * (k / kt);
-  int s = (2 * cus + tiles - 1) / tiles;  // two workgroups per CU (ring kernel)
+  // one workgroup per CU (register-staged loop) or two (ring kernel)
+  int s = ((ring_on() ? 2 : 1) * cus + tiles - 1) / tiles;
   const int64_t maxs = (m + MB - 1) / MB;
   if (s > maxs) s = (int)maxs;
   return s < 1 ? 1 : s;
-}
-
-// APEX_AMD_WGRAD_RING=0: the register-staged loop (A/B)
-inline bool ring_on() {
-  static const bool on = [] {
-    const char* e = std::getenv("APEX_AMD_WGRAD_RING");
-    return !(e && e[0] == '0');
-  }();
-  return on;
 }
 
 template <typename T, bool PRO>
@@ -984,7 +1016,7 @@ void conv1x1_wgrad(const void* g, const void* x, void* dw, int out_dtype, int64_
     else c1w::launch<T, false>(a, sp, cus, s);
   }, "conv1x1 wgrad");
   const int64_t nk = (int64_t)n * k;
-  const unsigned blocks = (unsigned)((nk / 8 + 255) / 256);
+  const unsigned blocks = (unsigned)((nk / 8 + 15) / 16);
   dispatch_float(out_dtype, [&](auto tag) {
     using TO = typename decltype(tag)::type;
     hipLaunchKernelGGL((c1w::wgrad_reduce<TO>), dim3(blocks), dim3(256), 0, s, ws, sp, nk, static_cast<TO*>(dw));

@@ -134,13 +134,15 @@ def conv1x1_bn_fwd(a2, w2d, pcoef, bn):
     return y2, sm, si, coef.view(-1)
 
 
-def conv1x1_dgrad(g2, w2d, add2=None):
-    """dX = g . W (+ add2): W [Cout, Cin], g [M, Cout]."""
+def conv1x1_dgrad(g2, w2d, add2=None, add_inplace=False):
+    """dX = g . W (+ add2): W [Cout, Cin], g [M, Cout].  ``add_inplace``: add2 is a temporary
+    the caller no longer needs, so the library GEMM accumulates into it (beta = 1) instead of
+    first copying it to a fresh output (a full D2D copy per call)."""
     m, kout = g2.shape
     if _dgrad_native(m, kout, w2d.size(1)):
         return _conv().bn1x1(g2, w2d, True, None, None, False, add2)[0]
     if add2 is not None:
-        return torch.addmm(add2, g2, w2d)
+        return add2.addmm_(g2, w2d) if add_inplace else torch.addmm(add2, g2, w2d)
     return torch.matmul(g2, w2d)
 
 
@@ -248,8 +250,12 @@ class _BottleneckFn(torch.autograd.Function):
         # shortcut gradient, then conv1's data gradient summed onto it
         dwd = ggd = gbd = None
         if wds is None:
+            # dm is this node's own temporary unless the block above handed it in (then it is
+            # autograd's incoming gradient, which must not be written)
             short = dm
+            short_tmp = dm is not go2
         else:
+            short_tmp = True
             dyd, _, ggd, gbd = bn.bwd(dm, yd, None, gds, smd, sid, cd, False, False)
             if stride == 1:
                 short = conv1x1_dgrad(dyd, wds.view(cout, cin))
@@ -262,7 +268,7 @@ class _BottleneckFn(torch.autograd.Function):
             dx, link_in.part = _conv().dgrad_bnred(dy1, w1.view(width, cin), short, link_in.bits, link_in.y3,
                                                    link_in.mean)
         else:
-            dx = conv1x1_dgrad(dy1, w1.view(width, cin), short)
+            dx = conv1x1_dgrad(dy1, w1.view(width, cin), short, short_tmp)
         dw1 = conv1x1_wgrad(dy1, x2, None, w1, (n, h, wd))
         return (_nchw(dx, n, h, wd), dw1, dw2, dw3, dwd, gg1, gb1, gg2, gb2, gg3, gb3, ggd, gbd, None)
 
