@@ -209,6 +209,24 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
     uint16_t* st = stg + wid * 32 * kSS;
 #pragma unroll
     for (int g = 0; g < CN / 2; ++g) {
+      // this group's residual / reduction operands first: their HBM latency runs under the
+      // LDS staging below instead of after it (the compiler barrier keeps loads from being
+      // hoisted across the staging otherwise)
+      const bool has_res = WT && p.res != nullptr;  // residual add: a dgrad-form option
+      uint4 rv[4], xq[4];
+      unsigned mbv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int qid = lane + 64 * i, rr = qid >> 3, c8 = (qid & 7) * 8;
+        const int64_t off = (row0 + rr) * p.ncols + col0 + 64 * g + c8;
+        const bool ok = row0 + rr < p.m;
+        rv[i] = make_uint4(0, 0, 0, 0);
+        if (has_res && ok) rv[i] = *reinterpret_cast<const uint4*>(p.res + off);
+        if constexpr (RED) {
+          xq[i] = ok ? *reinterpret_cast<const uint4*>(p.rx + off) : make_uint4(0, 0, 0, 0);
+          mbv[i] = ok ? p.rbits[off >> 3] : 0u;
+        }
+      }
 #pragma unroll
       for (int q = 0; q < 2; ++q)
 #pragma unroll
@@ -226,19 +244,19 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
         uint4 v = *reinterpret_cast<const uint4*>(st + rr * kSS + c8);
         const int64_t off = (row0 + rr) * p.ncols + col0 + 64 * g + c8;
         if (row0 + rr < p.m) {
-          if (RED || p.res) {  // wave-uniform branch
+          if (RED || has_res) {  // wave-uniform branch
             float a[8];
             Vec8<T>::load(a, reinterpret_cast<const T*>(&v));
-            if (p.res) {
+            if (has_res) {
               float b[8];
-              Vec8<T>::load(b, reinterpret_cast<const T*>(p.res + off));
+              Vec8<T>::load(b, reinterpret_cast<const T*>(&rv[i]));
 #pragma unroll
               for (int j = 0; j < 8; ++j) a[j] += b[j];
             }
             if constexpr (RED) {
-              const unsigned mb = p.rbits[off >> 3];
+              const unsigned mb = mbv[i];
               float xv[8];
-              Vec8<T>::load(xv, reinterpret_cast<const T*>(p.rx + off));
+              Vec8<T>::load(xv, reinterpret_cast<const T*>(&xq[i]));
 #pragma unroll
               for (int j = 0; j < 8; ++j) {
                 // the stored (rounded) gradient is what the rest of the backward sees
@@ -433,18 +451,22 @@ void launch_t(const Args& a0, int cus, hipStream_t s) {
   Args a = a0;
   a.ntiles = (int)((a.m + NW * 32 - 1) / (NW * 32));
   const int per_cu = (160 * 1024) / lds >= 2 ? 2 : 1;
-  int gx = cus * per_cu;
+  // one resident round over the whole grid (column groups included): every workgroup loads the
+  // weight image once and then streams ~ntiles / gx tiles
+  const int gy = a.ncols / NC;
+  int gx = (cus * per_cu + gy - 1) / gy;
   if (gx > a.ntiles) gx = a.ntiles;
   hipLaunchKernelGGL((fused1x1<T, NC, KR, WT, PRO, STATS, RED, NW>), dim3(gx, a.ncols / NC), dim3(NW * 64), lds, s,
                      a);
 }
 
-inline int grid_x(int64_t m, int nc, int kr, int pro, int cus, bool red = false) {
+inline int grid_x(int64_t m, int nc, int kr, int pro, int cus, int ncols, bool red = false) {
   const int nw = pick_nw(nc, kr, pro, red);
   const int lds = lds_bytes_nw(nc, kr, pro, red, nw);
   const int per_cu = (160 * 1024) / lds >= 2 ? 2 : 1;
   const int ntiles = (int)((m + nw * 32 - 1) / (nw * 32));
-  const int gx = cus * per_cu;
+  const int gy = ncols / nc;
+  const int gx = (cus * per_cu + gy - 1) / gy;
   return gx < ntiles ? gx : ntiles;
 }
 
@@ -479,7 +501,7 @@ bool conv1x1_bn_supported(int64_t m, int k, int ncols) {
 }
 
 int conv1x1_bn_partials(int64_t m, int k, int ncols, bool pro, int cus) {
-  return c1bn::grid_x(m, c1bn::col_tile(ncols, k), k, pro ? c1bn::kProBnRelu : c1bn::kProNone, cus);
+  return c1bn::grid_x(m, c1bn::col_tile(ncols, k), k, pro ? c1bn::kProBnRelu : c1bn::kProNone, cus, ncols);
 }
 
 void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int ncols, bool w_kmajor_out, int dtype,
@@ -528,7 +550,7 @@ void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int nco
 }
 
 int conv1x1_dgrad_bnred_partials(int64_t m, int k, int ncols, int cus) {
-  return c1bn::grid_x(m, c1bn::col_tile(ncols, k), k, 0, cus, true);
+  return c1bn::grid_x(m, c1bn::col_tile(ncols, k), k, 0, cus, ncols, true);
 }
 
 void conv1x1_dgrad_bnred(const void* g, const void* w, void* out, int64_t m, int k, int ncols, int dtype,
@@ -914,21 +936,22 @@ __global__ void __launch_bounds__(256) wgrad_reduce(const float* __restrict__ ws
 // tile: 256 x 64, 64 x 256, 128 x 128 (16K accumulators / workgroup) or a 256 x 128 / 128 x 256
 // block (32K) when the other dimension is read once either way
 inline void tile(int n, int k, int& nt, int& kt) {
-  // first candidate that divides (n, k): full-K tiles when K is the small side (the gradient,
-  // the big operand, is then read once), full-N when N is
-  static const int cand[][2] = {{256, 64}, {128, 64}, {64, 256}, {64, 128}, {256, 128}, {128, 256},
-                                {128, 128}, {64, 64}};
-  const int* pick = nullptr;
+  // every N-tile re-reads X and every K-tile re-reads G, so the operand traffic goes as
+  // n k (1 / KT + 1 / NT): take the dividing tile with the smallest 1/KT + 1/NT (ties: the
+  // order below), up to 32K accumulators per workgroup
+  static const int cand[][2] = {{256, 128}, {128, 256}, {128, 128}, {256, 64}, {64, 256},
+                                {128, 64}, {64, 128}, {64, 64}};
+  double best = 1e30;
+  nt = kt = 64;
   for (const auto& c : cand) {
-    if (k == 64 && c[1] != 64) continue;
-    if (n == 64 && c[0] != 64) continue;
-    if (n % c[0] == 0 && k % c[1] == 0) {
-      pick = c;
-      break;
+    if (n % c[0] || k % c[1]) continue;
+    const double cost = 1.0 / c[1] + 1.0 / c[0];
+    if (cost < best - 1e-12) {
+      best = cost;
+      nt = c[0];
+      kt = c[1];
     }
   }
-  nt = pick ? pick[0] : 64;
-  kt = pick ? pick[1] : 64;
 }
 
 // APEX_AMD_WGRAD_RING=1: the LDS-DMA ring variant (A/B; the register-staged loop measured

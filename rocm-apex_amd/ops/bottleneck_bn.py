@@ -114,8 +114,9 @@ def _red_native(m, kout, cin):
 
 
 def _wgrad_native(m, n, k, pro):
-    # MIOpen's split-K wgrad leads at the 56x56 shapes unless the operand needs the BN prologue
-    return FORCE_NATIVE or pro or m < 500000
+    # the split-M kernel with cost-based tiles runs 4.4-5.1 TB/s at the 56x56 shapes and leads
+    # MIOpen's wgrad at every ResNet-50 1x1 shape (1.2-1.8x, profiles/bn1x1_wgrad_r03b.jsonl)
+    return True
 
 
 def conv1x1_bn_fwd(a2, w2d, pcoef, bn):
