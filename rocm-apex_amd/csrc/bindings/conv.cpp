@@ -59,7 +59,8 @@ void tap_fprop(const at::Tensor& in, const at::Tensor& w, at::Tensor& out, int64
                int64_t isw, int64_t osh, int64_t osw, int64_t oph, int64_t opw, std::vector<int64_t> dh,
                std::vector<int64_t> dw, const c10::optional<at::Tensor>& scale,
                const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& residual, bool relu,
-               const c10::optional<at::Tensor>& mask) {
+               const c10::optional<at::Tensor>& mask, const c10::optional<at::Tensor>& stats,
+               const c10::optional<at::Tensor>& stats_shift) {
   ConvTapArgs a = make_args(in, w, out, oh, ow, ish, isw, osh, osw, oph, opw, dh, dw);
   auto per_channel = [&](const c10::optional<at::Tensor>& t, const char* what) -> const float* {
     if (!t.has_value()) return nullptr;
@@ -83,6 +84,13 @@ void tap_fprop(const at::Tensor& in, const at::Tensor& w, at::Tensor& out, int64
                     mask->scalar_type() == out.scalar_type(),
                 "conv tap_fprop: mask must match the output's shape, layout and dtype");
     a.mask = mask->data_ptr();
+  }
+  if (stats.has_value()) {
+    TORCH_CHECK(stats->is_cuda() && stats->scalar_type() == at::kFloat && stats->is_contiguous() &&
+                    stats->numel() == 2 * (int64_t)conv_tap_stats_tiles(a) * out.size(3),
+                "conv tap_fprop: stats must be contiguous fp32 [2, stats_tiles, K]");
+    a.stats = stats->data_ptr<float>();
+    a.stats_shift = per_channel(stats_shift, "stats_shift");
   }
   const c10::hip::HIPGuard g(in.get_device());
   TORCH_CHECK(conv_tap_supported(a), "conv tap_fprop: unsupported (C and K must be multiples of 64, bf16/fp16)");
@@ -254,7 +262,15 @@ void bind_conv(pybind11::module_& root) {
         pybind11::arg("osw"), pybind11::arg("oph"), pybind11::arg("opw"), pybind11::arg("dh"), pybind11::arg("dw"),
         pybind11::arg("scale") = pybind11::none(), pybind11::arg("bias") = pybind11::none(),
         pybind11::arg("residual") = pybind11::none(), pybind11::arg("relu") = false,
-        pybind11::arg("mask") = pybind11::none());
+        pybind11::arg("mask") = pybind11::none(), pybind11::arg("stats") = pybind11::none(),
+        pybind11::arg("stats_shift") = pybind11::none());
+  m.def("tap_stats_tiles", [](int64_t n, int64_t oh, int64_t ow) {
+    ConvTapArgs a{};
+    a.n = (int)n;
+    a.oh = (int)oh;
+    a.ow = (int)ow;
+    return conv_tap_stats_tiles(a);
+  });
   m.def("wgrad", &wgrad);
   m.def("force_fprop_cfg", &conv_force_fprop_cfg);
   m.def("bn1x1", &bn1x1, pybind11::arg("a"), pybind11::arg("w"), pybind11::arg("w_kmajor_out") = false,

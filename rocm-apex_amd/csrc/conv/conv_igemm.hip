@@ -52,6 +52,8 @@ struct Geo {
   const uint16_t* res;
   const uint16_t* mask;
   int relu;
+  float* stats;         // nullable: BN statistics partials [2][tiles_m][kout] of the stored output
+  const float* shift;   //   about this per-channel shift (nullable = 0)
 };
 
 inline Geo make_geo(const ConvTapArgs& a) {
@@ -63,6 +65,8 @@ inline Geo make_geo(const ConvTapArgs& a) {
   g.scale = a.scale;
   g.bias = a.bias;
   g.res = reinterpret_cast<const uint16_t*>(a.residual);
+  g.stats = a.stats;
+  g.shift = a.stats_shift;
   g.mask = reinterpret_cast<const uint16_t*>(a.mask);
   g.relu = a.relu;
   for (int t = 0; t < kConvMaxTaps; ++t) {
@@ -257,6 +261,11 @@ fprop_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, ui
   if (g.scale) Vec8<float>::load(sc, g.scale + gc);
   if (g.bias) Vec8<float>::load(bi, g.bias + gc);
   const bool affine = g.scale || g.bias;
+  // BN statistics of the stored values (the consuming batch norm's pass over Y, done here)
+  float st1[8], st2[8], sft[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) st1[e] = st2[e] = sft[e] = 0.f;
+  if (g.stats && g.shift) Vec8<float>::load(sft, g.shift + gc);
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     const int wr0 = wm * (BM / WM);
@@ -307,9 +316,33 @@ fprop_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, ui
           for (int e = 0; e < 8; ++e) v[e] = mk[e] > 0.f ? v[e] : 0.f;
         }
         Vec8<T>::store(reinterpret_cast<T*>(Y) + pix * g.kout + gc, v);
+        if (g.stats) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = v[e] - sft[e];
+            st1[e] += d;
+            st2[e] = fmaf(d, d, st2[e]);
+          }
+        }
       }
     }
     __syncthreads();
+  }
+  if (g.stats) {
+    // fixed-order fold of the RP row-groups sharing each column chunk (LDS is free again)
+    float* red = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(rsub * 2 + 0) * BN + ch * 8 + e] = st1[e];
+      red[(rsub * 2 + 1) * BN + ch * 8 + e] = st2[e];
+    }
+    __syncthreads();
+    for (int i = tid; i < 2 * BN; i += C::THREADS) {
+      const int which = i / BN, col = i % BN;
+      float acc2 = 0.f;
+      for (int r = 0; r < RP; ++r) acc2 += red[(r * 2 + which) * BN + col];
+      g.stats[((int64_t)which * tiles_m + bm) * g.kout + col0 + col] = acc2;
+    }
   }
 }
 
@@ -511,6 +544,10 @@ static int g_forced_cfg = [] {
 void conv_force_fprop_cfg(int cfg) { g_forced_cfg = cfg; }
 
 static int fprop_cfg(const ConvTapArgs& a, int cus) { return plan::conv_fprop_cfg(a, cus, g_forced_cfg); }
+
+int conv_tap_stats_tiles(const ConvTapArgs& a) {
+  return (int)(((int64_t)a.n * a.oh * a.ow + conv::BM - 1) / conv::BM);
+}
 
 void conv_tap_fprop(const ConvTapArgs& a, int cus, hipStream_t s) {
   if (!conv_tap_supported(a)) throw std::runtime_error("conv_tap_fprop: unsupported shape / dtype / alignment");

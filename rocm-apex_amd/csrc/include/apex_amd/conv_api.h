@@ -43,6 +43,11 @@ struct ConvTapArgs {
   // `mask` the producing layer's ReLU output in the output tensor's layout and dtype — the dReLU
   // of the previous stage applied in this dconv's epilogue
   const void* mask = nullptr;
+  // optional BN statistics of the fprop output (the consuming training-mode batch norm):
+  // per-M-tile partial sums of (y - shift) and (y - shift)^2, [2][conv_tap_stats_tiles][kout]
+  // fp32, finalized by conv1x1_bn_finalize (no separate statistics pass over y)
+  float* stats = nullptr;
+  const float* stats_shift = nullptr;
 };
 
 // shape constraints: c % 64 == 0, kout % 64 == 0, 16-byte aligned pointers
@@ -50,6 +55,8 @@ bool conv_tap_supported(const ConvTapArgs& a);
 // A/B hook: force one fprop tile configuration (-1 = per-shape choice); see conv_igemm.hip
 void conv_force_fprop_cfg(int cfg);
 void conv_tap_fprop(const ConvTapArgs& a, int cus, hipStream_t s);
+// number of M tiles of a tap fprop launch (the stats partial rows)
+int conv_tap_stats_tiles(const ConvTapArgs& a);
 
 // weight gradient: dw[k][t][c] = sum_{n,oh,ow} dy[n,oh,ow,k] * x[n, oh*ish + dh[t], ow*isw + dw[t], c]
 // (dy = `out` geometry with osh = osw = 1, oph = opw = 0; x = `in`).  fp32 result [kout][ntaps][c]

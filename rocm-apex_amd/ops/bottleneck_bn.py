@@ -185,12 +185,20 @@ class _BottleneckFn(torch.autograd.Function):
         # conv1 (+ bn1 statistics) -> bn1 apply + ReLU
         y1, sm1, si1, c1 = conv1x1_bn_fwd(x2, w1.view(width, cin), None, bn1)
         z1 = _bn().apply(y1, None, c1, True)[0]
-        # conv2 (3x3, stride) -> bn2 statistics
-        y2 = _conv_fwd(_nchw(z1, n, h, wd), w2, stride, 1)
-        oh, ow = y2.shape[2], y2.shape[3]
-        y2m = _m2(y2)
-        sm2, si2, c2 = _bn().stats(y2m, bn2.w, bn2.b, bn2.rm, bn2.rv, bn2.mom, bn2.eps)
-        c2 = c2.view(-1)
+        # conv2 (3x3, stride) -> bn2 statistics (in the native conv's epilogue where it runs)
+        z1v = _nchw(z1, n, h, wd)
+        if convops.tap_route(z1v.size(1), w2.size(0), 3, stride, h)[0]:
+            y2, part2 = convops.conv_tap_forward(z1v, w2, stride, 1, stats_shift=bn2.rm)
+            oh, ow = y2.shape[2], y2.shape[3]
+            y2m = _m2(y2)
+            sm2, si2, c2 = _conv().bn_finalize(part2, float(y2m.size(0)), bn2.rm, bn2.w, bn2.b, bn2.rm, bn2.rv,
+                                               bn2.eps, bn2.mom)
+        else:
+            y2 = F.conv2d(z1v, w2, None, stride, 1)
+            oh, ow = y2.shape[2], y2.shape[3]
+            y2m = _m2(y2)
+            sm2, si2, c2 = _bn().stats(y2m, bn2.w, bn2.b, bn2.rm, bn2.rv, bn2.mom, bn2.eps)
+            c2 = c2.view(-1)
         # conv3 with bn2's apply + ReLU on its operand load (+ bn3 statistics)
         y3, sm3, si3, c3 = conv1x1_bn_fwd(y2m, w3.view(cout, width), c2, bn3)
         if wds is None:

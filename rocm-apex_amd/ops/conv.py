@@ -163,16 +163,22 @@ def _dgrad_phases(k, stride, pad, h, w):
     return out
 
 
-def conv_tap_forward(x, w, stride, pad):
-    """NHWC conv through the native tap kernel: x [N,C,H,W] channels_last, w [K,C,R,S]."""
+def conv_tap_forward(x, w, stride, pad, stats_shift=None):
+    """NHWC conv through the native tap kernel: x [N,C,H,W] channels_last, w [K,C,R,S].
+    ``stats_shift`` (fp32 [K], e.g. the consuming BN's running mean): also return the BN
+    statistics partials [2, tiles, K] of the output from the kernel's epilogue, ``(y, part)``."""
     n, c, h, wd = x.shape
     kout, _, k, _ = w.shape
     oh, ow = (h + 2 * pad - k) // stride + 1, (wd + 2 * pad - k) // stride + 1
     y = torch.empty((n, kout, oh, ow), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
     taps = _fwd_taps(k, pad)
-    _conv_ext().tap_fprop(_nhwc(x), _w_krc(w).contiguous(), _nhwc(y), oh, ow, stride, stride, 1, 1, 0, 0,
-                          [t[0] for t in taps], [t[1] for t in taps])
-    return y
+    ext = _conv_ext()
+    part = None
+    if stats_shift is not None:
+        part = torch.empty((2, ext.tap_stats_tiles(n, oh, ow), kout), dtype=torch.float32, device=x.device)
+    ext.tap_fprop(_nhwc(x), _w_krc(w).contiguous(), _nhwc(y), oh, ow, stride, stride, 1, 1, 0, 0,
+                  [t[0] for t in taps], [t[1] for t in taps], stats=part, stats_shift=stats_shift)
+    return y if stats_shift is None else (y, part)
 
 
 # ------------------------------------------------------------------------------------------------

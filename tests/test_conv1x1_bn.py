@@ -148,3 +148,25 @@ def test_gpu_bn1x1_dgrad_bn_backward_prologue(dtype, m, k, nc):
     ap = (cb[:k] * dm.float() + cb[k:2 * k] * y.float() + cb[2 * k:]).to(dtype)
     _close(aout, ap, 1e-2)
     _close(out, ap.float() @ w.float(), 1e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,stride,h", [(64, 64, 1, 14), (128, 256, 2, 16), (256, 256, 1, 7)])
+def test_gpu_tap_conv_bn_statistics_epilogue(cin, cout, stride, h):
+    """3x3 implicit-GEMM forward with the consuming BN's statistics in the epilogue
+    (ops.conv.conv_tap_forward(stats_shift=...)) -> finalize == torch batch mean / var."""
+    import torch.nn.functional as F
+    from apex.ops import conv as C
+
+    ext = _ext()
+    torch.manual_seed(5)
+    x = (torch.randn(3, cin, h, h, device="cuda") + 0.3).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    w = (torch.randn(cout, cin, 3, 3, device="cuda") * 0.05).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    shift = torch.randn(cout, device="cuda") * 0.1
+    y, part = C.conv_tap_forward(x, w, stride, 1, stats_shift=shift)
+    yr = F.conv2d(x.float(), w.float(), None, stride, 1)
+    assert float((y.float() - yr).abs().max()) <= 1e-2 * max(1.0, float(yr.abs().max()))
+    y2 = yr.permute(0, 2, 3, 1).reshape(-1, cout)
+    sm, si, _ = ext.bn_finalize(part, float(y2.size(0)), shift, None, None, None, None, 1e-5, 0.1)
+    torch.testing.assert_close(sm, y2.mean(0), atol=3e-3 * float(y2.std()), rtol=2e-3)
+    torch.testing.assert_close(si, torch.rsqrt(y2.var(0, unbiased=False) + 1e-5), atol=0, rtol=5e-3)
