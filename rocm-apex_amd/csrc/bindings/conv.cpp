@@ -209,10 +209,14 @@ at::Tensor wgrad1x1(const at::Tensor& g, const at::Tensor& x, const c10::optiona
   return dw;
 }
 
-// conv dgrad (dgrad form W [k, ncols]) + residual, masked by the block-below BN's ReLU bits, with
-// that BN's backward reduction partials; returns (out, part)
+// conv dgrad (dgrad form W [k, ncols]) + residual, masked with the BN below's ReLU (its forward
+// bit mask, or recomputed from x and its apply coefficients `coef`) and that BN's backward
+// reduction partials.  Optional BN-backward prologue (py, pcoef [3k]) with the transformed
+// operand written out (want_aout).  Returns (out, part, aout)
 std::vector<at::Tensor> dgrad_bnred(const at::Tensor& g, const at::Tensor& w, const c10::optional<at::Tensor>& res,
-                                    const at::Tensor& bits, const at::Tensor& x, const at::Tensor& mean) {
+                                    const c10::optional<at::Tensor>& bits, const at::Tensor& x, const at::Tensor& mean,
+                                    const c10::optional<at::Tensor>& coef, const c10::optional<at::Tensor>& py,
+                                    const c10::optional<at::Tensor>& pcoef, bool want_aout) {
   TORCH_CHECK(g.is_cuda() && g.dim() == 2 && g.is_contiguous() && w.dim() == 2 && w.is_contiguous() &&
                   w.scalar_type() == g.scalar_type() && w.size(0) == g.size(1),
               "dgrad_bnred: g [M, k] and w [k, ncols] expected");
@@ -220,22 +224,38 @@ std::vector<at::Tensor> dgrad_bnred(const at::Tensor& g, const at::Tensor& w, co
   const int k = (int)g.size(1), ncols = (int)w.size(1);
   TORCH_CHECK(x.is_contiguous() && x.scalar_type() == g.scalar_type() && x.numel() == m * ncols,
               "dgrad_bnred: x must be the contiguous [M, ncols] BN input");
-  TORCH_CHECK(bits.is_contiguous() && bits.scalar_type() == at::kByte && bits.numel() * 8 == m * ncols,
-              "dgrad_bnred: bits must be the [M * ncols / 8] ReLU mask");
+  TORCH_CHECK(bits.has_value() != coef.has_value(), "dgrad_bnred: exactly one of bits / coef");
+  if (bits.has_value())
+    TORCH_CHECK(bits->is_contiguous() && bits->scalar_type() == at::kByte && bits->numel() * 8 == m * ncols,
+                "dgrad_bnred: bits must be the [M * ncols / 8] ReLU mask");
+  if (coef.has_value())
+    TORCH_CHECK(coef->is_contiguous() && coef->scalar_type() == at::kFloat && coef->numel() == 2 * (int64_t)ncols,
+                "dgrad_bnred: coef must be fp32 [2 * ncols]");
   TORCH_CHECK(mean.is_contiguous() && mean.scalar_type() == at::kFloat && mean.numel() == ncols,
               "dgrad_bnred: mean must be fp32 [ncols]");
   if (res.has_value())
     TORCH_CHECK(res->is_contiguous() && res->scalar_type() == g.scalar_type() && res->numel() == m * ncols,
                 "dgrad_bnred: res must be a contiguous [M, ncols] tensor");
+  const bool pro = py.has_value();
+  TORCH_CHECK(pro == pcoef.has_value(), "dgrad_bnred: py and pcoef go together");
+  if (pro)
+    TORCH_CHECK(py->is_contiguous() && py->sizes() == g.sizes() && py->scalar_type() == g.scalar_type() &&
+                    pcoef->scalar_type() == at::kFloat && pcoef->is_contiguous() && pcoef->numel() == 3 * (int64_t)k,
+                "dgrad_bnred: py must match g, pcoef fp32 [3k]");
+  TORCH_CHECK(!want_aout || pro, "dgrad_bnred: want_aout needs the prologue");
   TORCH_CHECK(conv1x1_bn_supported(m, k, ncols), "dgrad_bnred: unsupported shape");
   const c10::hip::HIPGuard guard(g.get_device());
   const int cus = device_cus(g.get_device());
   auto out = at::empty({m, ncols}, g.options());
-  auto part = at::empty({2, conv1x1_dgrad_bnred_partials(m, k, ncols, cus), ncols}, g.options().dtype(at::kFloat));
+  auto part = at::empty({2, conv1x1_dgrad_bnred_partials(m, k, ncols, cus, pro), ncols}, g.options().dtype(at::kFloat));
+  at::Tensor aout;
+  if (want_aout) aout = at::empty_like(g);
   conv1x1_dgrad_bnred(g.data_ptr(), w.data_ptr(), out.data_ptr(), m, k, ncols, dtype_code(g.scalar_type()),
-                      res.has_value() ? res->data_ptr() : nullptr, bits.data_ptr<uint8_t>(), x.data_ptr(),
-                      mean.data_ptr<float>(), part.data_ptr<float>(), cus, cur_stream());
-  return {out, part};
+                      res.has_value() ? res->data_ptr() : nullptr, bits.has_value() ? bits->data_ptr<uint8_t>() : nullptr,
+                      x.data_ptr(), mean.data_ptr<float>(), part.data_ptr<float>(), cus, cur_stream(),
+                      coef.has_value() ? coef->data_ptr<float>() : nullptr, pro ? py->data_ptr() : nullptr,
+                      pro ? pcoef->data_ptr<float>() : nullptr, want_aout ? aout.data_ptr() : nullptr);
+  return {out, part, aout};
 }
 
 // (coef_bwd [3C], grad_w, grad_b) from dgrad_bnred partials
@@ -278,7 +298,10 @@ void bind_conv(pybind11::module_& root) {
         pybind11::arg("stats") = false, pybind11::arg("res") = pybind11::none(),
         pybind11::arg("py") = pybind11::none(), pybind11::arg("want_aout") = false);
   m.def("bn_finalize", &bn_finalize);
-  m.def("dgrad_bnred", &dgrad_bnred);
+  m.def("dgrad_bnred", &dgrad_bnred, pybind11::arg("g"), pybind11::arg("w"), pybind11::arg("res"),
+        pybind11::arg("bits"), pybind11::arg("x"), pybind11::arg("mean"), pybind11::arg("coef") = pybind11::none(),
+        pybind11::arg("py") = pybind11::none(), pybind11::arg("pcoef") = pybind11::none(),
+        pybind11::arg("want_aout") = false);
   m.def("bnbwd_finalize", &bnbwd_finalize);
   m.def("wgrad1x1", &wgrad1x1, pybind11::arg("g"), pybind11::arg("x"), pybind11::arg("xcoef") = pybind11::none(),
         pybind11::arg("out_dtype") = pybind11::none());

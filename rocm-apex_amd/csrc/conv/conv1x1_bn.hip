@@ -50,7 +50,8 @@ struct Args {
   // RED (dgrad form): the output is the gradient of a ReLU'd batch-norm output (the block
   // below's) — masked with that BN's forward ReLU bits, and its backward reduction
   // sum(g), sum(g * (x - mean)) accumulated per column into part [2][G][ncols]
-  const uint8_t* rbits;  // [M * ncols / 8]
+  const uint8_t* rbits;  // [M * ncols / 8]; null: the mask is recomputed as rx * rcoef[c] + rcoef[C + c] > 0
+  const float* rcoef;    // the BN's forward apply coefficients [2][ncols] (recomputed-mask mode)
   const uint16_t* rx;    // the BN's input [M][ncols]
   const float* rmean;    // the BN's batch mean [ncols]
 };
@@ -81,7 +82,11 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
   constexpr int kWaves = NW, kRowsB = NW * 32, NT = NW * 64;
   constexpr int BS = KR + 8;                 // B image row stride (elements)
   constexpr int CN = NC / 32;                // accumulator blocks per wave
-  constexpr int KCH = KR < (NC >= 256 ? 64 : 128) ? KR : (NC >= 256 ? 64 : 128);  // k depth per register chunk
+  // k depth per register chunk: 128, 64 at 256 columns (128 accumulator registers); the two-
+  // tensor BN-backward prologue halves it again (it holds a second operand's fragments)
+  constexpr int KCH0 = NC >= 256 ? 64 : 128;
+  constexpr int KCH1 = PRO == kProBnBwd ? KCH0 / 2 : KCH0;
+  constexpr int KCH = KR < KCH1 ? KR : KCH1;
   constexpr int KC = KCH / 16;               // k-steps per chunk
   constexpr int NCH = KR / KCH;              // chunks per tile
   static_assert(NC % 64 == 0 && KR % 64 == 0, "tile shape");
@@ -224,7 +229,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
         if (has_res && ok) rv[i] = *reinterpret_cast<const uint4*>(p.res + off);
         if constexpr (RED) {
           xq[i] = ok ? *reinterpret_cast<const uint4*>(p.rx + off) : make_uint4(0, 0, 0, 0);
-          mbv[i] = ok ? p.rbits[off >> 3] : 0u;
+          mbv[i] = (ok && p.rbits) ? p.rbits[off >> 3] : 0u;
         }
       }
 #pragma unroll
@@ -232,11 +237,16 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) st[crow(r, lh) * kSS + 32 * q + lr] = from_f<T>(acc[2 * g + q][r]).x;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      float rs[8], rq[8], mu[8];
+      float rs[8], rq[8], mu[8], rsc[8], rsh[8];
       if constexpr (RED) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) rs[j] = rq[j] = 0.f;
-        Vec8<float>::load(mu, p.rmean + col0 + 64 * g + (lane & 7) * 8);
+        const int cc = col0 + 64 * g + (lane & 7) * 8;
+        Vec8<float>::load(mu, p.rmean + cc);
+        if (!p.rbits) {  // wave-uniform: the mask of a plain BN + ReLU, recomputed from its input
+          Vec8<float>::load(rsc, p.rcoef + cc);
+          Vec8<float>::load(rsh, p.rcoef + p.ncols + cc);
+        }
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -254,9 +264,14 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
               for (int j = 0; j < 8; ++j) a[j] += b[j];
             }
             if constexpr (RED) {
-              const unsigned mb = mbv[i];
               float xv[8];
               Vec8<T>::load(xv, reinterpret_cast<const T*>(&xq[i]));
+              unsigned mb = mbv[i];
+              if (!p.rbits) {
+                mb = 0u;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) mb |= (fmaf(xv[j], rsc[j], rsh[j]) > 0.f ? 1u : 0u) << j;
+              }
 #pragma unroll
               for (int j = 0; j < 8; ++j) {
                 // the stored (rounded) gradient is what the rest of the backward sees
@@ -549,31 +564,37 @@ void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int nco
   check_launch("conv1x1_bn");
 }
 
-int conv1x1_dgrad_bnred_partials(int64_t m, int k, int ncols, int cus) {
-  return c1bn::grid_x(m, c1bn::col_tile(ncols, k), k, 0, cus, ncols, true);
+int conv1x1_dgrad_bnred_partials(int64_t m, int k, int ncols, int cus, bool pro) {
+  return c1bn::grid_x(m, c1bn::col_tile(ncols, k), k, pro ? c1bn::kProBnBwd : c1bn::kProNone, cus, ncols, true);
 }
 
 void conv1x1_dgrad_bnred(const void* g, const void* w, void* out, int64_t m, int k, int ncols, int dtype,
                          const void* res, const uint8_t* bits, const void* x, const float* mean, float* part, int cus,
-                         hipStream_t s) {
+                         hipStream_t s, const float* rcoef, const void* py, const float* pcoef, void* aout) {
   if (!conv1x1_bn_supported(m, k, ncols)) throw std::runtime_error("conv1x1_dgrad_bnred: unsupported shape");
-  if (!bits || !x || !mean || !part) throw std::runtime_error("conv1x1_dgrad_bnred: bits, x, mean and part required");
+  if ((!bits && !rcoef) || !x || !mean || !part)
+    throw std::runtime_error("conv1x1_dgrad_bnred: a mask source (bits or coef), x, mean and part are required");
+  if ((py == nullptr) != (pcoef == nullptr)) throw std::runtime_error("conv1x1_dgrad_bnred: prologue needs py and pcoef");
   c1bn::Args args{};
   args.a = static_cast<const uint16_t*>(g);
   args.w = static_cast<const uint16_t*>(w);
   args.y = static_cast<uint16_t*>(out);
   args.m = m;
   args.ncols = ncols;
-  args.ntiles = 0;  // set per wave count by launch_t
   args.part = part;
   args.res = static_cast<const uint16_t*>(res);
   args.rbits = bits;
+  args.rcoef = rcoef;
   args.rx = static_cast<const uint16_t*>(x);
   args.rmean = mean;
+  args.pcoef = pcoef;
+  args.py = static_cast<const uint16_t*>(py);
+  args.aout = static_cast<uint16_t*>(aout);
   const int nc = c1bn::col_tile(ncols, k);
   dispatch_16(dtype, [&](auto tag) {
     using T = typename decltype(tag)::type;
-    c1bn::dispatch_shape<T, true, c1bn::kProNone, false, true>(args, nc, k, cus, s);
+    if (py) c1bn::dispatch_shape<T, true, c1bn::kProBnBwd, false, true>(args, nc, k, cus, s);
+    else c1bn::dispatch_shape<T, true, c1bn::kProNone, false, true>(args, nc, k, cus, s);
   }, "conv1x1_dgrad_bnred");
   check_launch("conv1x1_dgrad_bnred");
 }

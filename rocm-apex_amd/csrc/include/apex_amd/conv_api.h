@@ -97,10 +97,14 @@ void conv1x1_wgrad(const void* g, const void* x, void* dw, int out_dtype, int64_
 // out = mask(g . W + res) (mask = bits, that BN's forward ReLU bit mask) and per-column partial
 // sums [2][G][ncols] of out and out * (x - mean); G = conv1x1_dgrad_bnred_partials(...).
 // conv1x1_bnbwd_finalize turns them into grad_w, grad_b and coef_bwd [3][C].
-int conv1x1_dgrad_bnred_partials(int64_t m, int k, int ncols, int cus);
+int conv1x1_dgrad_bnred_partials(int64_t m, int k, int ncols, int cus, bool pro = false);
+// bits null: mask = x * rcoef[c] + rcoef[ncols + c] > 0 (a plain BN + ReLU, recomputed);
+// py / pcoef (optional): the BN-backward operand prologue a' = pcoef0 g + pcoef1 py + pcoef2 of
+// the BN below this conv, with a' written to aout (nullable) for the weight gradient
 void conv1x1_dgrad_bnred(const void* g, const void* w, void* out, int64_t m, int k, int ncols, int dtype,
                          const void* res, const uint8_t* bits, const void* x, const float* mean, float* part, int cus,
-                         hipStream_t s);
+                         hipStream_t s, const float* rcoef = nullptr, const void* py = nullptr,
+                         const float* pcoef = nullptr, void* aout = nullptr);
 void conv1x1_bnbwd_finalize(const float* part, int g, int c, float inv_n, const float* mean, const float* istd,
                             const float* w, float* gw, float* gb, float* coef, hipStream_t s);
 

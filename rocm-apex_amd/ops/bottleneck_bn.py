@@ -242,20 +242,37 @@ class _BottleneckFn(torch.autograd.Function):
         else:
             dm, cb3, gg3, gb3 = bn.bwd_reduce(go2, y3, g3, sm3, si3, c3, True, bits)
         w3m = w3.view(cout, width)
-        if _dgrad_native(dm.size(0), cout, width):
+        if _dgrad_native(dm.size(0), cout, width) and width == 64:
+            # conv3 dgrad with bn3's dx as the operand prologue (dx3 written for the wgrad) AND
+            # bn2's ReLU mask + backward reduction in the epilogue: bn2's reduction pass is gone
+            # (stage 1 only: at 128+ channels the longer epilogue costs more than the pass,
+            # profiles/resnet50_node_r03e.md)
+            dz2, part2, dx3 = _conv().dgrad_bnred(dm, w3m, None, None, y2m, sm2, coef=c2, py=y3,
+                                                  pcoef=cb3.view(-1), want_aout=True)
+            cb2, gg2, gb2 = _conv().bnbwd_finalize(part2, float(dm.size(0)), sm2, si2, g2)
+            dy2 = bn.bwd_apply(dz2, y2m, c2, cb2)
+        elif _dgrad_native(dm.size(0), cout, width):
             dz2, _, dx3 = _conv().bn1x1(dm, w3m, True, cb3.view(-1), None, False, None, y3, True)
+            dy2, _, gg2, gb2 = bn.bwd(dz2, y2m, None, g2, sm2, si2, c2, True, False)
         else:
             dx3 = bn.bwd_apply(dm, y3, c3, cb3)
             dz2 = conv1x1_dgrad(dx3, w3m)
+            dy2, _, gg2, gb2 = bn.bwd(dz2, y2m, None, g2, sm2, si2, c2, True, False)
         # conv3 weight gradient with bn2's apply + ReLU recomputed on the operand load
         dw3 = conv1x1_wgrad(dx3, y2m, c2, w3, (n, oh, ow))
-        # bn2 (ReLU mask recomputed from y2)
-        dy2, _, gg2, gb2 = bn.bwd(dz2, y2m, None, g2, sm2, si2, c2, True, False)
         # conv2
         dz1, dw2 = _conv_bwd(_nchw(dy2, n, oh, ow), _nchw(z1, n, h, wd), w2, stride, 1)
         dz1 = _m2(dz1.contiguous(memory_format=torch.channels_last))
-        # bn1
-        dy1, _, gg1, gb1 = bn.bwd(dz1, y1, None, g1, sm1, si1, c1, True, False)
+        # bn1: the reduction here; its dx pass runs as conv1's dgrad operand prologue where that
+        # kernel takes it (stage 1), else as a pass of its own
+        linked = link_in is not None and link_in.bits is not None and _red_native(dz1.size(0), width, cin)
+        # (bn1's dx as conv1's dgrad prologue moves the same bytes — the reduction then has to
+        # write the masked gradient — and measured slower: off)
+        pro1 = False
+        if pro1:
+            dz1m, cb1, gg1, gb1 = bn.bwd_reduce(dz1, y1, g1, sm1, si1, c1, True, None)
+        else:
+            dy1, _, gg1, gb1 = bn.bwd(dz1, y1, None, g1, sm1, si1, c1, True, False)
         # shortcut gradient, then conv1's data gradient summed onto it
         dwd = ggd = gbd = None
         if wds is None:
@@ -272,10 +289,16 @@ class _BottleneckFn(torch.autograd.Function):
             else:
                 dxd, dwd = _conv_bwd(_nchw(dyd, n, oh, ow), x, wds, stride, 0)
                 short = _m2(dxd.contiguous(memory_format=torch.channels_last))
-        if link_in is not None and link_in.bits is not None and _red_native(dy1.size(0), width, cin):
+        if pro1:
+            # bn1's dx as the operand prologue (dy1 written for the wgrad) + the block below's
+            # ReLU mask and bn3 backward reduction in the epilogue
+            dx, link_in.part, dy1 = _conv().dgrad_bnred(dz1m, w1.view(width, cin), short, link_in.bits,
+                                                        link_in.y3, link_in.mean, py=y1, pcoef=cb1.view(-1),
+                                                        want_aout=True)
+        elif linked:
             # mask with the block below's ReLU bits + its bn3 backward reduction, in this kernel
-            dx, link_in.part = _conv().dgrad_bnred(dy1, w1.view(width, cin), short, link_in.bits, link_in.y3,
-                                                   link_in.mean)
+            dx, link_in.part, _ = _conv().dgrad_bnred(dy1, w1.view(width, cin), short, link_in.bits, link_in.y3,
+                                                      link_in.mean)
         else:
             dx = conv1x1_dgrad(dy1, w1.view(width, cin), short, short_tmp)
         dw1 = conv1x1_wgrad(dy1, x2, None, w1, (n, h, wd))

@@ -170,3 +170,45 @@ def test_gpu_tap_conv_bn_statistics_epilogue(cin, cout, stride, h):
     sm, si, _ = ext.bn_finalize(part, float(y2.size(0)), shift, None, None, None, None, 1e-5, 0.1)
     torch.testing.assert_close(sm, y2.mean(0), atol=3e-3 * float(y2.std()), rtol=2e-3)
     torch.testing.assert_close(si, torch.rsqrt(y2.var(0, unbiased=False) + 1e-5), atol=0, rtol=5e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,k,nc", [(1000, 256, 64), (2048, 64, 256), (777, 512, 128)])
+@pytest.mark.parametrize("mode", ["bits", "coef", "coef+pro"])
+def test_gpu_dgrad_bnred(m, k, nc, mode):
+    """dgrad form with the BN-backward reduction epilogue: out = mask(g' . W + res), partial
+    sums of out and out * (x - mean); the mask from ReLU bits or recomputed from x and the BN's
+    apply coefficients; optionally the BN-backward prologue g' = c0 g + c1 py + c2 (aout = g')."""
+    ext = _ext()
+    torch.manual_seed(6)
+    dt = torch.bfloat16
+    g = torch.randn(m, k, device="cuda").to(dt)
+    w = (torch.randn(k, nc, device="cuda") * 0.1).to(dt)
+    res = torch.randn(m, nc, device="cuda").to(dt)
+    x = torch.randn(m, nc, device="cuda").to(dt)
+    mean = torch.randn(nc, device="cuda") * 0.1
+    coef = torch.cat([torch.rand(nc, device="cuda") + 0.5, torch.randn(nc, device="cuda") * 0.3])
+    if mode == "bits":
+        maskb = torch.rand(m, nc, device="cuda") > 0.4
+        wts = (2 ** torch.arange(8, device="cuda")).view(1, 8)
+        bits = (maskb.view(-1, 8).long() * wts).sum(1).to(torch.uint8)
+        kw = dict(bits=bits)
+    else:
+        maskb = (x.float() * coef[:nc] + coef[nc:]) > 0
+        kw = dict(bits=None, coef=coef)
+    gp = g
+    if mode == "coef+pro":
+        py = torch.randn(m, k, device="cuda").to(dt)
+        pc = torch.randn(3 * k, device="cuda") * 0.5
+        gp = (pc[:k] * g.float() + pc[k:2 * k] * py.float() + pc[2 * k:]).to(dt)
+        kw.update(py=py, pcoef=pc, want_aout=True)
+    out, part, aout = ext.dgrad_bnred(g, w, res, kw.pop("bits"), x, mean, **kw)
+    ref = torch.where(maskb, (gp.float() @ w.float() + res.float()).to(dt).float(), torch.zeros(()).cuda())
+    _close(out, ref, 2e-2)
+    if mode == "coef+pro":
+        _close(aout, gp, 1e-2)
+    s1 = part[0].sum(0)
+    s2 = part[1].sum(0)
+    of = out.float()
+    torch.testing.assert_close(s1, of.sum(0), atol=0.05 * float(of.abs().sum(0).max()) / 100 + 0.5, rtol=2e-2)
+    torch.testing.assert_close(s2, (of * (x.float() - mean)).sum(0), atol=1.0, rtol=2e-2)
