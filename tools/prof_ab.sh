@@ -13,6 +13,7 @@ for arm in "$A|$EA" "$B|$EB"; do
       > $R/gpurun_out/prof_$name.log 2>&1 ) || { echo "arm $name failed"; tail -5 $R/gpurun_out/prof_$name.log; exit 1; }
   db=$(find $R/gpurun_out/prof_$name -name '*results.db' | head -1)
   python3 $R/tools/prof_summary.py "$db" --after spin_kernel --top 45 --md $R/gpurun_out/prof_$name.md > /dev/null || exit 1
+  python3 $R/tools/prof_gaps.py "$db" --after spin_kernel > $R/gpurun_out/prof_${name}_gaps.md || exit 1
   rm -rf $R/gpurun_out/prof_$name
   head -14 $R/gpurun_out/prof_$name.md
 done
