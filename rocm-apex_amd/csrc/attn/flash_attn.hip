@@ -625,6 +625,46 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
 // (7 instead of 5) but removes every atomic, the fp32 dQ buffer, its memset and the convert pass.
 // ---------------------------------------------------------------------------------------------
 
+// XOR-swizzled Q / dO slice images of the dK/dV kernel (head dim 64 / 128): rows are D elements
+// long with no padding, and 16-byte chunk c of row r is stored at chunk c ^ swz(r).  The padded
+// (D + 8) layout kept the 32-row fragment reads conflict-free but put two of the four rows a
+// 16-lane ds_read_b64_tr_b16 touches on the same banks (22 % LDS bank-conflict cycles,
+// profiles/pmc_kernels_r03.md); the swizzle gives both the row reads (16 rows, one chunk) and the
+// transposed reads (4 rows x 4 chunks per 32 lanes) 16 distinct 16-byte bank slots.
+//   D = 128 (one row per 256-B bank line): swz(r) = ((r & 3) << 2) | ((r >> 2) & 3)
+//   D =  64 (two rows per line):           swz(r) = f((r >> 1) & 7), f(j) = ((j & 1) << 2) | (j >> 1)
+template <int D>
+__device__ __forceinline__ int qswz(int r) {
+  if constexpr (D == 128) return ((r & 3) << 2) | ((r >> 2) & 3);
+  else {
+    const int j = (r >> 1) & 7;
+    return ((j & 1) << 2) | (j >> 1);
+  }
+}
+
+template <int D>
+__device__ __forceinline__ s16x8 frag_rows_sw(const uint16_t* lds, int kk, int lane) {
+  const int row = lane & 31;
+  const int c = (2 * kk + (lane >> 5)) ^ qswz<D>(row);
+  return *reinterpret_cast<const s16x8*>(lds + row * D + 8 * c);
+}
+
+template <int D>
+__device__ __forceinline__ s16x8 frag_tr_sw(const uint16_t* lds, int colbase, int klo, int khi, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int col = colbase + 16 * (g & 1) + 4 * p;
+  const int ck = col >> 3, off = col & 7;
+  const int r0 = klo + q, r1 = khi + q;
+  const s16x4 lo = tr_read(lds + r0 * D + ((ck ^ qswz<D>(r0)) << 3) + off);
+  const s16x4 hi = tr_read(lds + r1 * D + ((ck ^ qswz<D>(r1)) << 3) + off);
+  return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int D>
+constexpr bool dkdv_swz() {
+  return D == 64 || D == 128;
+}
+
 // dK, dV: one workgroup = 4 waves = 128 keys (K, V of the wave's 32 keys in registers); 32-query
 // slices of Q / dO (+ lse, delta) double-buffered in LDS, one barrier per slice.
 template <typename T, int D, int MODE, int QS>
@@ -634,7 +674,8 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
   const AttnArgs& a = ba.f;
   using G = Geo<D>;
   constexpr int BK = 128, QB = QS, NKK = G::NKK, NDT = G::NDT;  // QB queries per LDS slice
-  constexpr int QSTR = G::KSTR;  // row reads (S, dP) and transposed reads (dK, dV)
+  constexpr bool SW = dkdv_swz<D>();
+  constexpr int QSTR = SW ? D : G::KSTR;  // row reads (S, dP) and transposed reads (dK, dV)
   constexpr int CPR = D / 8;
   // Q, dO images + lse, delta (fp32) + per-row dropout hash prefix (u32), in 16-bit units
   constexpr int SLICE = 2 * QB * QSTR + 6 * QB;
@@ -721,7 +762,9 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
         for (int i = 0; i < QCPT; ++i) {
           const int ch = tid + 256 * i;
           if (ch < QCH) {
-            const int row = ch / CPR, col = (ch % CPR) * 8;
+            const int row = ch / CPR;
+            // 32-row sub-slices restart the swizzle pattern: row index within the sub-slice
+            const int col = SW ? ((ch % CPR) ^ qswz<D>(row & 31)) * 8 : (ch % CPR) * 8;
             *reinterpret_cast<uint4*>(Ql(buf) + row * QSTR + col) = pq[i];
             *reinterpret_cast<uint4*>(dOl(buf) + row * QSTR + col) = pg[i];
           }
@@ -753,8 +796,13 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
         f32x16 sacc = zero16(), dpacc = zero16();
         #pragma unroll
         for (int kk = 0; kk < NKK; ++kk) {
-          sacc = mma<T>(frag_rows<QSTR>(Qb, 0, kk, lane), kf[kk], sacc);
-          dpacc = mma<T>(frag_rows<QSTR>(Gb, 0, kk, lane), vf[kk], dpacc);
+          if constexpr (SW) {
+            sacc = mma<T>(frag_rows_sw<D>(Qb, kk, lane), kf[kk], sacc);
+            dpacc = mma<T>(frag_rows_sw<D>(Gb, kk, lane), vf[kk], dpacc);
+          } else {
+            sacc = mma<T>(frag_rows<QSTR>(Qb, 0, kk, lane), kf[kk], sacc);
+            dpacc = mma<T>(frag_rows<QSTR>(Gb, 0, kk, lane), vf[kk], dpacc);
+          }
         }
         float p[16], ds[16];
         const bool edge = !kvalid || q0s + 32 > sq.lq || (a.causal && q0s < k_start + wave * 32 + 32) ||
@@ -793,8 +841,13 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
           const int klo = 16 * s2 + 4 * h2;
           #pragma unroll
           for (int dt = 0; dt < NDT; ++dt) {
-            dv[dt] = mma<T>(frag_tr<QSTR>(Gb, 32 * dt, klo, klo + 8, lane), pf, dv[dt]);
-            dk[dt] = mma<T>(frag_tr<QSTR>(Qb, 32 * dt, klo, klo + 8, lane), dsf, dk[dt]);
+            if constexpr (SW) {
+              dv[dt] = mma<T>(frag_tr_sw<D>(Gb, 32 * dt, klo, klo + 8, lane), pf, dv[dt]);
+              dk[dt] = mma<T>(frag_tr_sw<D>(Qb, 32 * dt, klo, klo + 8, lane), dsf, dk[dt]);
+            } else {
+              dv[dt] = mma<T>(frag_tr<QSTR>(Gb, 32 * dt, klo, klo + 8, lane), pf, dv[dt]);
+              dk[dt] = mma<T>(frag_tr<QSTR>(Qb, 32 * dt, klo, klo + 8, lane), dsf, dk[dt]);
+            }
           }
         }
         }
@@ -1055,7 +1108,7 @@ void launch_fwd(const AttnArgs& a, hipStream_t s) {
 
 template <int D, int QS>
 constexpr size_t dkdv_lds() {
-  return (size_t)2 * (2 * QS * Geo<D>::KSTR + 6 * QS) * 2;
+  return (size_t)2 * (2 * QS * (dkdv_swz<D>() ? D : Geo<D>::KSTR) + 6 * QS) * 2;
 }
 
 // dK/dV LDS slice depth in queries (APEX_ATTN_DKDV_QS=32|64 overrides, A/B).  Measured on MI355X
