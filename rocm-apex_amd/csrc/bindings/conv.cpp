@@ -273,6 +273,34 @@ std::vector<at::Tensor> bnbwd_finalize(const at::Tensor& part, double count, con
   return {coef, gw, gb};
 }
 
+// dW [K, 3, 3, C] (channels_last memory [K][3][3][C]) of a pad-1 3x3 conv: dy [N, OH, OW, K]
+// (NHWC), x [N, H, W, C] (NHWC), optional BN-apply+ReLU prologue on x (xcoef [2C])
+at::Tensor wgrad3x3(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const c10::optional<at::Tensor>& xcoef,
+                    c10::optional<at::ScalarType> out_dtype) {
+  check_nhwc(dy, "dy");
+  check_nhwc(x, "x");
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type() && dy.size(0) == x.size(0), "wgrad3x3: dtype / batch mismatch");
+  const int nimg = (int)x.size(0), h = (int)x.size(1), w = (int)x.size(2), c = (int)x.size(3);
+  const int oh = (int)dy.size(1), ow = (int)dy.size(2), kout = (int)dy.size(3);
+  TORCH_CHECK(oh == (h + 2 - 3) / stride + 1 && ow == (w + 2 - 3) / stride + 1, "wgrad3x3: geometry mismatch");
+  TORCH_CHECK(conv3x3_wgrad_supported(c, kout), "wgrad3x3: C and K must be multiples of 64");
+  const float* xc = nullptr;
+  if (xcoef.has_value()) {
+    TORCH_CHECK(xcoef->is_cuda() && xcoef->scalar_type() == at::kFloat && xcoef->is_contiguous() &&
+                    xcoef->numel() == 2 * (int64_t)c,
+                "wgrad3x3: xcoef must be contiguous fp32 [2C]");
+    xc = xcoef->data_ptr<float>();
+  }
+  const c10::hip::HIPGuard guard(dy.get_device());
+  const int cus = device_cus(dy.get_device());
+  const int64_t m = (int64_t)nimg * oh * ow;
+  auto dw = at::empty({kout, 3, 3, c}, dy.options().dtype(out_dtype.value_or(dy.scalar_type())));
+  auto ws = at::empty({conv3x3_wgrad_workspace_floats(m, kout, c, cus)}, dy.options().dtype(at::kFloat));
+  conv3x3_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), dtype_code(dw.scalar_type()), nimg, h, w, c, oh, ow,
+                (int)stride, kout, dtype_code(dy.scalar_type()), xc, ws.data_ptr<float>(), cus, cur_stream());
+  return dw.permute({0, 3, 1, 2});  // [K, C, 3, 3] in channels_last memory
+}
+
 }  // namespace
 
 void bind_conv(pybind11::module_& root) {
@@ -298,6 +326,8 @@ void bind_conv(pybind11::module_& root) {
         pybind11::arg("stats") = false, pybind11::arg("res") = pybind11::none(),
         pybind11::arg("py") = pybind11::none(), pybind11::arg("want_aout") = false);
   m.def("bn_finalize", &bn_finalize);
+  m.def("wgrad3x3", &wgrad3x3, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("stride"),
+        pybind11::arg("xcoef") = pybind11::none(), pybind11::arg("out_dtype") = pybind11::none());
   m.def("dgrad_bnred", &dgrad_bnred, pybind11::arg("g"), pybind11::arg("w"), pybind11::arg("res"),
         pybind11::arg("bits"), pybind11::arg("x"), pybind11::arg("mean"), pybind11::arg("coef") = pybind11::none(),
         pybind11::arg("py") = pybind11::none(), pybind11::arg("pcoef") = pybind11::none(),

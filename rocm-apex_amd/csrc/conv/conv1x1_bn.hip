@@ -629,6 +629,10 @@ struct Args {
   int n, k;
   int64_t rows;        // rows per split (multiple of 64)
   const float* xcoef;  // PRO: [2][K] scale | shift, pro(x) = relu(x * scale + shift)
+  // GATHER (3x3, pad 1): x is the [N][H][W][C] input, K = 9 C with column (tap t, channel c) at
+  // t * C + c, and row m = (n, oh, ow) of G reads input pixel (oh * st + t / 3 - 1, ow * st + t % 3 - 1)
+  // (zero outside the image); xcoef is then per channel [2][C]
+  int h, w, c, oh, ow, st;
 };
 
 constexpr int MB = 64;
@@ -638,7 +642,7 @@ constexpr int lds_bytes() {
   return 2 * MB * ((NT + 32) + (KT + 32)) * 2;
 }
 
-template <typename T, int NT, int KT, bool PRO>
+template <typename T, int NT, int KT, bool PRO, bool GATHER = false>
 __global__ void __launch_bounds__(256, 1) wgrad1x1(Args p) {
   constexpr int GS = NT + 32, XS = KT + 32;   // LDS row strides (elements)
   constexpr int GL = MB * NT / 8 / 256;       // 16-byte loads per thread per chunk
@@ -655,13 +659,14 @@ __global__ void __launch_bounds__(256, 1) wgrad1x1(Args p) {
   // this thread's X columns are the same for every load (256 is a multiple of KT / 8)
   const int xc8 = (tid % (KT / 8)) * 8;
   float xs[8], xb[8];
-  if constexpr (PRO) {
+  if constexpr (PRO && !GATHER) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       xs[j] = p.xcoef[k0 + xc8 + j];
       xb[j] = p.xcoef[p.k + k0 + xc8 + j];
     }
   }
+  unsigned xvalid = 0;  // GATHER: bit i = load i read a real pixel (padding stays exactly 0)
 
   uint4 gr[GL], xr[XL];
   auto gload = [&](int64_t base) {
@@ -671,11 +676,31 @@ __global__ void __launch_bounds__(256, 1) wgrad1x1(Args p) {
       const int64_t rr = base + row;
       gr[i] = rr < r1 ? *reinterpret_cast<const uint4*>(p.g + rr * p.n + n0 + c8) : make_uint4(0, 0, 0, 0);
     }
+    if constexpr (GATHER) xvalid = 0;
 #pragma unroll
     for (int i = 0; i < XL; ++i) {
       const int idx = tid + 256 * i, row = idx / (KT / 8);
       const int64_t rr = base + row;
-      xr[i] = rr < r1 ? *reinterpret_cast<const uint4*>(p.x + rr * p.k + k0 + xc8) : make_uint4(0, 0, 0, 0);
+      if constexpr (GATHER) {
+        // 192-wide tiles: 256 is not a multiple of KT / 8, so the column is per load
+        const int gcol = k0 + (idx % (KT / 8)) * 8;
+        const int gtap = gcol / p.c, gch = gcol - gtap * p.c;
+        const int tdh = gtap / 3 - 1, tdw = gtap % 3 - 1;
+        bool ok = rr < r1;
+        int64_t src = 0;
+        if (ok) {
+          const int ohw = p.oh * p.ow;
+          const int nimg = (int)(rr / ohw), rem = (int)(rr - (int64_t)nimg * ohw);
+          const int oy = rem / p.ow, ox = rem - oy * p.ow;
+          const int iy = oy * p.st + tdh, ix = ox * p.st + tdw;
+          ok = (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
+          src = (((int64_t)nimg * p.h + iy) * p.w + ix) * p.c + gch;
+        }
+        xr[i] = ok ? *reinterpret_cast<const uint4*>(p.x + src) : make_uint4(0, 0, 0, 0);
+        xvalid |= (ok ? 1u : 0u) << i;
+      } else {
+        xr[i] = rr < r1 ? *reinterpret_cast<const uint4*>(p.x + rr * p.k + k0 + xc8) : make_uint4(0, 0, 0, 0);
+      }
     }
   };
   auto lwrite = [&](int buf) {
@@ -689,7 +714,16 @@ __global__ void __launch_bounds__(256, 1) wgrad1x1(Args p) {
 #pragma unroll
     for (int i = 0; i < XL; ++i) {
       const int idx = tid + 256 * i, row = idx / (KT / 8);
+      const int lcol = GATHER ? (idx % (KT / 8)) * 8 : xc8;
       uint4 v = xr[i];
+      if constexpr (PRO && GATHER) {
+        const int gcol = k0 + lcol, gch = gcol % p.c;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xs[j] = p.xcoef[gch + j];
+          xb[j] = p.xcoef[p.c + gch + j];
+        }
+      }
       if constexpr (PRO) {
         uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -699,8 +733,9 @@ __global__ void __launch_bounds__(256, 1) wgrad1x1(Args p) {
           w4[j] = (uint32_t)from_f<T>(lo).x | ((uint32_t)from_f<T>(hi).x << 16);
         }
         v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        if (GATHER && !((xvalid >> i) & 1u)) v = make_uint4(0, 0, 0, 0);
       }
-      *reinterpret_cast<uint4*>(xi + row * XS + xc8) = v;
+      *reinterpret_cast<uint4*>(xi + row * XS + lcol) = v;
     }
   };
 
@@ -956,6 +991,23 @@ __global__ void __launch_bounds__(256) wgrad_reduce(const float* __restrict__ ws
 
 // tile: 256 x 64, 64 x 256, 128 x 128 (16K accumulators / workgroup) or a 256 x 128 / 128 x 256
 // block (32K) when the other dimension is read once either way
+inline void tile_gather(int n, int k, int& nt, int& kt) {
+  // 3x3: K = 9 C; the 192-wide tiles (3 taps at C = 64) keep G re-reads at 3 instead of 9
+  static const int cand[][2] = {{256, 128}, {128, 192}, {128, 256}, {128, 128}, {64, 192}, {256, 64},
+                                {64, 256}, {128, 64}, {64, 128}, {64, 64}};
+  double best = 1e30;
+  nt = kt = 64;
+  for (const auto& c : cand) {
+    if (n % c[0] || k % c[1]) continue;
+    const double cost = 1.0 / c[1] + 1.0 / c[0];
+    if (cost < best - 1e-12) {
+      best = cost;
+      nt = c[0];
+      kt = c[1];
+    }
+  }
+}
+
 inline void tile(int n, int k, int& nt, int& kt) {
   // every N-tile re-reads X and every K-tile re-reads G, so the operand traffic goes as
   // n k (1 / KT + 1 / NT): take the dividing tile with the smallest 1/KT + 1/NT (ties: the
@@ -985,9 +1037,10 @@ inline bool ring_on() {
   return on;
 }
 
-inline int splits(int64_t m, int n, int k, int cus) {
+inline int splits(int64_t m, int n, int k, int cus, bool gather = false) {
   int nt, kt;
-  tile(n, k, nt, kt);
+  if (gather) tile_gather(n, k, nt, kt);
+  else tile(n, k, nt, kt);
   const int tiles = (n / nt) * (k / kt);
   // one workgroup per CU (register-staged loop) or two (ring kernel)
   int s = ((ring_on() ? 2 : 1) * cus + tiles - 1) / tiles;
@@ -1031,7 +1084,69 @@ void launch(const Args& a, int s, int cus, hipStream_t st) {
   throw std::runtime_error("conv1x1 wgrad: no tile");
 }
 
+template <typename T, bool PRO>
+void launch_gather(const Args& a, int s, hipStream_t st) {
+  int nt, kt;
+  tile_gather(a.n, a.k, nt, kt);
+  dim3 grid(s, a.n / nt, a.k / kt);
+#define C3W_CASE(NT_, KT_)                                                                                \
+  if (nt == NT_ && kt == KT_) {                                                                           \
+    constexpr int lds = lds_bytes<NT_, KT_>();                                                            \
+    static bool attr = false;                                                                             \
+    if (!attr) {                                                                                          \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad1x1<T, NT_, KT_, PRO, true>),         \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);                         \
+      attr = true;                                                                                        \
+    }                                                                                                     \
+    hipLaunchKernelGGL((wgrad1x1<T, NT_, KT_, PRO, true>), grid, dim3(256), lds, st, a);                  \
+    return;                                                                                               \
+  }
+  C3W_CASE(256, 128) C3W_CASE(128, 192) C3W_CASE(128, 256) C3W_CASE(128, 128) C3W_CASE(64, 192)
+  C3W_CASE(256, 64) C3W_CASE(64, 256) C3W_CASE(128, 64) C3W_CASE(64, 128) C3W_CASE(64, 64)
+#undef C3W_CASE
+  throw std::runtime_error("conv3x3 wgrad: no tile");
+}
+
 }  // namespace c1w
+
+bool conv3x3_wgrad_supported(int c, int kout) { return c % 64 == 0 && kout % 64 == 0 && c > 0 && kout > 0; }
+
+int64_t conv3x3_wgrad_workspace_floats(int64_t m, int kout, int c, int cus) {
+  return (int64_t)c1w::splits(m, kout, 9 * c, cus, true) * kout * 9 * c;
+}
+
+void conv3x3_wgrad(const void* g, const void* x, void* dw, int out_dtype, int nimg, int h, int w, int c, int oh,
+                   int ow, int stride, int kout, int dtype, const float* xcoef, float* ws, int cus, hipStream_t s) {
+  if (!conv3x3_wgrad_supported(c, kout)) throw std::runtime_error("conv3x3 wgrad: C, K must be multiples of 64");
+  c1w::Args a{};
+  a.g = static_cast<const uint16_t*>(g);
+  a.x = static_cast<const uint16_t*>(x);
+  a.ws = ws;
+  a.m = (int64_t)nimg * oh * ow;
+  a.n = kout;
+  a.k = 9 * c;
+  a.xcoef = xcoef;
+  a.h = h;
+  a.w = w;
+  a.c = c;
+  a.oh = oh;
+  a.ow = ow;
+  a.st = stride;
+  const int sp = c1w::splits(a.m, kout, 9 * c, cus, true);
+  a.rows = ((a.m + sp - 1) / sp + c1w::MB - 1) / c1w::MB * c1w::MB;
+  dispatch_16(dtype, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    if (xcoef) c1w::launch_gather<T, true>(a, sp, s);
+    else c1w::launch_gather<T, false>(a, sp, s);
+  }, "conv3x3 wgrad");
+  const int64_t nk = (int64_t)kout * 9 * c;
+  const unsigned blocks = (unsigned)((nk / 8 + 15) / 16);
+  dispatch_float(out_dtype, [&](auto tag) {
+    using TO = typename decltype(tag)::type;
+    hipLaunchKernelGGL((c1w::wgrad_reduce<TO>), dim3(blocks), dim3(256), 0, s, ws, sp, nk, static_cast<TO*>(dw));
+  }, "conv3x3 wgrad reduce");
+  check_launch("conv3x3_wgrad");
+}
 
 bool conv1x1_wgrad_supported(int64_t m, int n, int k) {
   return m > 0 && n % 64 == 0 && k % 64 == 0 && n >= 64 && k >= 64;

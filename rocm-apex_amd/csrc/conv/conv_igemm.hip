@@ -489,19 +489,33 @@ wgrad_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ DY, fl
       }
 }
 
+// fixed-order sum of the split partials: a block owns 16 consecutive 8-element vectors and its 16
+// thread groups each sum every 16th split, folded in LDS in a fixed order (S / 16 loads per
+// thread and n / 128 blocks — one thread per vector over all S splits left the chip idle)
 template <typename TO>
 __global__ void __launch_bounds__(256) wgrad_reduce(const float* __restrict__ part, int splits, int64_t n,
                                                     TO* __restrict__ out) {
-  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8; i < n; i += (int64_t)gridDim.x * 256 * 8) {
-    float v[8], t8[8];
-    Vec8<float>::load(v, part + i);
-    for (int s = 1; s < splits; ++s) {
-      Vec8<float>::load(t8, part + (int64_t)s * n + i);
+  __shared__ float red[16][16 * 8 + 4];
+  const int v = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int64_t i = ((int64_t)blockIdx.x * 16 + v) * 8;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (i < n)
+    for (int q = grp; q < splits; q += 16) {
+      float t8[8];
+      Vec8<float>::load(t8, part + (int64_t)q * n + i);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] += t8[k];
+      for (int k = 0; k < 8; ++k) a[k] += t8[k];
     }
-    Vec8<TO>::store(out + i, v);
-  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[grp][v * 8 + k] = a[k];
+  __syncthreads();
+  if (grp != 0 || i >= n) return;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a[k] = 0.f;
+  for (int g2 = 0; g2 < 16; ++g2)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] += red[g2][v * 8 + k];
+  Vec8<TO>::store(out + i, a);
 }
 
 using plan::WgPlan;
@@ -602,8 +616,7 @@ void conv_wgrad(const ConvTapArgs& a, const void* dy, void* dw_out, int out_dtyp
     else go(conv::wgrad_kernel<T, 64, 64>, 64, 64);
   }, "conv_wgrad");
   const int64_t n = (int64_t)a.kout * a.ntaps * a.c;
-  int64_t grid = (n / 8 + 255) / 256;
-  if (grid > (int64_t)cus * 4) grid = (int64_t)cus * 4;
+  const int64_t grid = (n / 8 + 15) / 16;
   dispatch_float(out_dtype, [&](auto tag) {
     using TO = typename decltype(tag)::type;
     hipLaunchKernelGGL((conv::wgrad_reduce<TO>), dim3((unsigned)grid), dim3(256), 0, s, (const float*)ws, p.splits, n,

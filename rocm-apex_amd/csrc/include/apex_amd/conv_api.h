@@ -108,4 +108,12 @@ void conv1x1_dgrad_bnred(const void* g, const void* w, void* out, int64_t m, int
 void conv1x1_bnbwd_finalize(const float* part, int g, int c, float inv_n, const float* mean, const float* istd,
                             const float* w, float* gw, float* gb, float* coef, hipStream_t s);
 
+// 3x3 (pad 1, stride 1 / 2) weight gradient on the split-M kernel with the input gathered per
+// tap: dw [kout][9][c] = sum over output pixels dy[p][k] * pro(x[tap-shifted p][c]), zero padding;
+// pro = relu(x * xcoef[c] + xcoef[C + c]) when xcoef (the producing BN + ReLU), padding stays 0
+bool conv3x3_wgrad_supported(int c, int kout);
+int64_t conv3x3_wgrad_workspace_floats(int64_t m, int kout, int c, int cus);
+void conv3x3_wgrad(const void* g, const void* x, void* dw, int out_dtype, int nimg, int h, int w, int c, int oh,
+                   int ow, int stride, int kout, int dtype, const float* xcoef, float* ws, int cus, hipStream_t s);
+
 }  // namespace apex_amd

@@ -212,3 +212,28 @@ def test_gpu_dgrad_bnred(m, k, nc, mode):
     of = out.float()
     torch.testing.assert_close(s1, of.sum(0), atol=0.05 * float(of.abs().sum(0).max()) / 100 + 0.5, rtol=2e-2)
     torch.testing.assert_close(s2, (of * (x.float() - mean)).sum(0), atol=1.0, rtol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,stride,h,batch", [(64, 64, 1, 14, 3), (128, 128, 2, 16, 2), (64, 128, 1, 9, 2),
+                                                     (256, 256, 2, 14, 2), (128, 192, 1, 7, 5)])
+@pytest.mark.parametrize("pro", [False, True])
+def test_gpu_wgrad3x3_gather(cin, cout, stride, h, batch, pro):
+    """3x3 weight gradient on the split-M kernel with the per-tap input gather (zero padding) and
+    the optional BN-apply + ReLU prologue, against fp32 torch's convolution weight gradient."""
+    ext = _ext()
+    torch.manual_seed(7)
+    dt = torch.bfloat16
+    x = (torch.randn(batch, cin, h, h, device="cuda") + 0.2).to(dt).to(memory_format=torch.channels_last)
+    oh = (h + 2 - 3) // stride + 1
+    gy = torch.randn(batch, cout, oh, oh, device="cuda").to(dt).to(memory_format=torch.channels_last)
+    xcoef = torch.cat([torch.rand(cin, device="cuda") + 0.5, torch.randn(cin, device="cuda") * 0.3]) if pro else None
+    xf = x.float()
+    if pro:
+        xf = torch.relu(xf * xcoef[:cin].view(1, -1, 1, 1) + xcoef[cin:].view(1, -1, 1, 1)).to(dt).float()
+    w = torch.zeros(cout, cin, 3, 3, device="cuda")
+    ref = torch.ops.aten.convolution_backward(gy.float(), xf, w, None, [stride, stride], [1, 1], [1, 1], False,
+                                              [0, 0], 1, [False, True, False])[1]
+    dw = ext.wgrad3x3(gy.permute(0, 2, 3, 1), x.permute(0, 2, 3, 1), stride, xcoef, torch.float32)
+    assert dw.shape == ref.shape
+    _close(dw, ref, 2e-3)

@@ -50,9 +50,10 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     args = ap.parse_args()
     g = apex._native.require("conv1x1").gemm
+    ext = apex._native.require("conv").conv
     dev = torch.device("cuda")
     cl = torch.channels_last
-    for h, cin, cout in ONE:
+    for h, cin, cout in ([] if os.environ.get("CONV_AB_ONLY_3X3") else ONE):
         x = torch.randn(N, cin, h, h, device=dev, dtype=torch.bfloat16).to(memory_format=cl)
         gy = torch.randn(N, cout, h, h, device=dev, dtype=torch.bfloat16).to(memory_format=cl)
         w = (torch.randn(cout, cin, 1, 1, device=dev, dtype=torch.bfloat16) * 0.05).to(memory_format=cl)
@@ -98,6 +99,7 @@ def main():
             "miopen": lambda: torch.ops.aten.convolution_backward(gy, x, w, None, [st, st], [1, 1], [1, 1], False,
                                                                   [0, 0], 1, [False, True, False]),
             "native": lambda: conv_ops.conv_tap_wgrad(gy, x, w.shape, st, 1, w.dtype),
+            "native_gather": lambda: ext.wgrad3x3(gy.permute(0, 2, 3, 1), x.permute(0, 2, 3, 1), st),
         }
         res = {kk: [] for kk in fns}
         for _ in range(args.rounds):
