@@ -85,6 +85,18 @@ __device__ __forceinline__ uint64_t drop_offset(const AttnArgs& a) {
 // v_exp_f32 directly (inputs here are <= 0 or -inf; no denormal range reduction needed)
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// reductions over the lane pair (l, l ^ 32) of a 32x32 accumulator column: v_permlane32_swap
+// exchanges the two wave halves in the VALU (no LDS round trip as with ds_bpermute); both lanes of
+// a pair combine the same two values in the same order, so they agree bitwise
+__device__ __forceinline__ float swap32_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float swap32_add(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 struct Seq {
   int64_t qrow0, krow0;  // token-space base row (side buffers)
   int64_t qoff, koff;    // element offset of the sequence start for the batch stride / varlen row
@@ -237,6 +249,7 @@ __global__ void __launch_bounds__(256, (fwd_occupancy<D, MODE, QF, LO>())) fwd_k
       for (int i = 0; i < NDT; ++i) o[f][i] = zero16();
     }
     const float c = a.scale * kLog2e;
+    const float inv_scale = 1.f / a.scale;
     const bool dropout = MODE >= 1 && a.p_drop > 0.f;  // MODE 0: no dropout (compiled out)
     const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
     const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
@@ -276,11 +289,14 @@ __global__ void __launch_bounds__(256, (fwd_occupancy<D, MODE, QF, LO>())) fwd_k
       s16x8 pf[QF][2][2];
       #pragma unroll
       for (int f = 0; f < QF; ++f) {
+        // scores stay in raw Q.K units until the exponent: max over the raw values (c > 0, so
+        // fl(c * max) == max(fl(c * s))) and p = exp2(fma(s, c, -m)) — one VALU op per score
+        // less than scaling first; the bias is added in raw units (bias / scale)
         float x[1][2][16];
         #pragma unroll
         for (int t = 0; t < 2; ++t)
           #pragma unroll
-          for (int r = 0; r < 16; ++r) x[0][t][r] = sacc[f][t][r] * c;
+          for (int r = 0; r < 16; ++r) x[0][t][r] = sacc[f][t][r];
         if (need_mask) {
           #pragma unroll
           for (int t = 0; t < 2; ++t)
@@ -290,7 +306,7 @@ __global__ void __launch_bounds__(256, (fwd_occupancy<D, MODE, QF, LO>())) fwd_k
               const bool ok = key < sq.lk && (!a.causal || key <= myq[f]);
               float v = x[0][t][r];
               if (biasb != nullptr && ok && qvalid[f])
-                v += biasb[(int64_t)myq[f] * a.bias_sq + (int64_t)key * a.bias_sk] * kLog2e;
+                v += biasb[(int64_t)myq[f] * a.bias_sq + (int64_t)key * a.bias_sk] * inv_scale;
               x[0][t][r] = ok ? v : -INFINITY;
             }
         }
@@ -299,7 +315,7 @@ __global__ void __launch_bounds__(256, (fwd_occupancy<D, MODE, QF, LO>())) fwd_k
         for (int t = 0; t < 2; ++t)
           #pragma unroll
           for (int r = 0; r < 16; ++r) mx = fmaxf(mx, x[0][t][r]);
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        mx = swap32_max(mx) * c;
         const float m_new = fmaxf(m_i[f], mx);
         const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
         const float alpha = fast_exp2(m_i[f] - m_use);
@@ -308,11 +324,11 @@ __global__ void __launch_bounds__(256, (fwd_occupancy<D, MODE, QF, LO>())) fwd_k
         for (int t = 0; t < 2; ++t)
           #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const float pr = fast_exp2(x[0][t][r] - m_use);
+            const float pr = fast_exp2(__builtin_fmaf(x[0][t][r], c, -m_use));
             ls += pr;
             x[0][t][r] = pr;
           }
-        ls += __shfl_xor(ls, 32, 64);
+        ls = swap32_add(ls);
         l_i[f] = l_i[f] * alpha + ls;
         m_i[f] = m_new;
         // skip the O rescale when no lane's running max moved (after the first tiles it rarely does;
