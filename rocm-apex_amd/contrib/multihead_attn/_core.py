@@ -70,3 +70,58 @@ def dropout_add(x, residual, p, is_training):
     if is_training and p > 0:
         x = F.dropout(x, p=p, training=True)
     return x + residual
+
+
+def _masks(use_time_mask, mask):
+    """The reference's single ``mask`` argument -> (key_padding_mask, attn_mask)."""
+    return (None, mask) if use_time_mask else (mask, None)
+
+
+def self_attn(use_time_mask, is_training, heads, scale, inputs, input_weights, output_weights, input_biases,
+              output_biases, mask, mask_additive, dropout_prob, impl, norm=None):
+    """Self attention as the reference's ``*self_attn*_func`` API: inputs [seq, batch, E],
+    input_weights [3E, E] interleaved per head as [q|k|v]; ``norm`` = (gamma, beta) runs the
+    fused LayerNorm on the input first and adds the dropped-out result to ``inputs`` (norm_add)."""
+    from ...normalization.fused_layer_norm import fused_layer_norm_affine
+
+    seq, batch, e = inputs.shape
+    x = inputs if norm is None else fused_layer_norm_affine(inputs, norm[0], norm[1], (e,), 1e-5)
+    lin = F.linear(x, input_weights, input_biases)
+    q4, k4, v4 = split_heads_interleaved(lin, seq, batch, heads, 3)
+    kpm, am = _masks(use_time_mask, mask)
+    bias = mask_to_bias(kpm, am, mask_additive, batch, seq, seq, inputs.device)
+    ctx = attention(q4, k4, v4, bias, scale, dropout_prob, is_training, impl)
+    out = F.linear(ctx, output_weights, output_biases)
+    return out if norm is None else dropout_add(out, inputs, dropout_prob, is_training)
+
+
+def encdec_attn(use_time_mask, is_training, heads, scale, inputs_q, inputs_kv, input_weights_q, input_weights_kv,
+                output_weights, input_biases_q, input_biases_kv, output_biases, mask, dropout_prob, impl,
+                norm=None):
+    """Encoder-decoder attention as the reference's ``*encdec_attn*_func`` API: queries from
+    ``inputs_q`` [sq, batch, E], keys / values from ``inputs_kv`` [sk, batch, E] through one [2E, E]
+    projection interleaved per head as [k|v]."""
+    from ...normalization.fused_layer_norm import fused_layer_norm_affine
+
+    sq, batch, e = inputs_q.shape
+    sk = inputs_kv.size(0)
+    x = inputs_q if norm is None else fused_layer_norm_affine(inputs_q, norm[0], norm[1], (e,), 1e-5)
+    lq = F.linear(x, input_weights_q, input_biases_q)
+    lkv = F.linear(inputs_kv, input_weights_kv, input_biases_kv)
+    (q4,) = split_heads_interleaved(lq, sq, batch, heads, 1)
+    k4, v4 = split_heads_interleaved(lkv, sk, batch, heads, 2)
+    kpm, am = _masks(use_time_mask, mask)
+    bias = mask_to_bias(kpm, am, False, batch, sq, sk, inputs_q.device)
+    ctx = attention(q4, k4, v4, bias, scale, dropout_prob, is_training, impl)
+    out = F.linear(ctx, output_weights, output_biases)
+    return out if norm is None else dropout_add(out, inputs_q, dropout_prob, is_training)
+
+
+class FuncNamespace:
+    """Reference modules expose ``XxxFunc`` autograd classes next to ``xxx_func = XxxFunc.apply``;
+    here the functions are compositions of autograd-capable ops (the flash-attention Function,
+    fused LayerNorm, linear), so the class only carries ``apply``."""
+
+    def __init_subclass__(cls, fn=None, **kw):
+        super().__init_subclass__(**kw)
+        cls.apply = staticmethod(fn)

@@ -6,10 +6,9 @@ import math
 import torch
 from torch import nn
 from torch.nn import Parameter
-import torch.nn.functional as F
 
-from ...normalization.fused_layer_norm import FusedLayerNorm, fused_layer_norm_affine
-from ._core import attention, dropout_add, mask_to_bias, split_heads_interleaved
+from ...normalization.fused_layer_norm import FusedLayerNorm
+from ._core import dropout_add, encdec_attn
 
 
 class EncdecMultiheadAttn(nn.Module):
@@ -68,22 +67,19 @@ class EncdecMultiheadAttn(nn.Module):
         """query [sq, batch, embed]; key [sk, batch, embed] (value ignored: kv share one projection)."""
         if key_padding_mask is not None:
             assert attn_mask is None, "ERROR attn_mask and key_padding_mask should not be both defined!"
-        sq, batch, e = query.shape
-        sk = key.size(0)
-        x = query
-        if self.include_norm_add:
-            if self.impl == "fast":
-                x = fused_layer_norm_affine(query, self.lyr_nrm_gamma_weights, self.lyr_nrm_beta_weights, (e,),
-                                            1e-5)
-            else:
-                x = self.lyr_nrm(query)
-        lq = F.linear(x, self.in_proj_weight_q, self.in_proj_bias_q)
-        lkv = F.linear(key, self.in_proj_weight_kv, self.in_proj_bias_kv)
-        (q4,) = split_heads_interleaved(lq, sq, batch, self.num_heads, 1)
-        k4, v4 = split_heads_interleaved(lkv, sk, batch, self.num_heads, 2)
-        bias = mask_to_bias(key_padding_mask, attn_mask, False, batch, sq, sk, query.device)
-        ctx = attention(q4, k4, v4, bias, self.scaling, self.dropout, is_training, self.impl)
-        out = F.linear(ctx, self.out_proj_weight, self.out_proj_bias)
+        mask = key_padding_mask if key_padding_mask is not None else attn_mask
+        use_time_mask = attn_mask is not None
+        weights = (self.in_proj_weight_q, self.in_proj_weight_kv, self.out_proj_weight, self.in_proj_bias_q,
+                   self.in_proj_bias_kv, self.out_proj_bias)
+        if self.include_norm_add and self.impl == "fast":
+            # the reference's fast_encdec_attn_norm_add_func
+            out = encdec_attn(use_time_mask, is_training, self.num_heads, self.scaling, query, key, *weights, mask,
+                              self.dropout, "fast", norm=(self.lyr_nrm_gamma_weights, self.lyr_nrm_beta_weights))
+            return out, None
+        x = self.lyr_nrm(query) if self.include_norm_add else query
+        # the reference's encdec_attn_func / fast_encdec_attn_func
+        out = encdec_attn(use_time_mask, is_training, self.num_heads, self.scaling, x, key, *weights, mask,
+                          self.dropout, self.impl)
         if self.include_norm_add:
             out = dropout_add(out, query, self.dropout, is_training)
         return out, None

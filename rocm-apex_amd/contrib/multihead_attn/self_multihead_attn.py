@@ -9,10 +9,9 @@ import math
 import torch
 from torch import nn
 from torch.nn import Parameter
-import torch.nn.functional as F
 
-from ...normalization.fused_layer_norm import FusedLayerNorm, fused_layer_norm_affine
-from ._core import attention, dropout_add, mask_to_bias, split_heads_interleaved
+from ...normalization.fused_layer_norm import FusedLayerNorm
+from ._core import dropout_add, self_attn
 
 
 class SelfMultiheadAttn(nn.Module):
@@ -109,20 +108,19 @@ class SelfMultiheadAttn(nn.Module):
             assert attn_mask is None, "ERROR attn_mask and key_padding_mask should not be both defined!"
         elif attn_mask is not None:
             assert not self.mask_additive, "additive mask not supported for time mask"
-        seq, batch, e = query.shape
-        x = query
-        if self.include_norm_add:
-            if self.impl == "fast":
-                x = fused_layer_norm_affine(query, self.lyr_nrm_gamma_weights, self.lyr_nrm_beta_weights, (e,),
-                                            1e-5)
-            else:
-                x = self.lyr_nrm(query)
         w, b = self._input_weights()
-        lin = F.linear(x, w, b)  # [seq, batch, 3E] interleaved per head as [q|k|v]
-        q4, k4, v4 = split_heads_interleaved(lin, seq, batch, self.num_heads, 3)
-        bias = mask_to_bias(key_padding_mask, attn_mask, self.mask_additive, batch, seq, seq, query.device)
-        ctx = attention(q4, k4, v4, bias, self.scaling, self.dropout, is_training, self.impl)
-        out = F.linear(ctx, self.out_proj_weight, self.out_proj_bias)
+        mask = key_padding_mask if key_padding_mask is not None else attn_mask
+        use_time_mask = attn_mask is not None
+        if self.include_norm_add and self.impl == "fast":
+            # the reference's fast_self_attn_norm_add_func: LN -> attention -> dropout + residual
+            out = self_attn(use_time_mask, is_training, self.num_heads, self.scaling, query, w,
+                            self.out_proj_weight, b, self.out_proj_bias, mask, self.mask_additive, self.dropout,
+                            "fast", norm=(self.lyr_nrm_gamma_weights, self.lyr_nrm_beta_weights))
+            return out, None
+        x = self.lyr_nrm(query) if self.include_norm_add else query
+        # the reference's self_attn_func / fast_self_attn_func
+        out = self_attn(use_time_mask, is_training, self.num_heads, self.scaling, x, w, self.out_proj_weight, b,
+                        self.out_proj_bias, mask, self.mask_additive, self.dropout, self.impl)
         if self.include_norm_add:
             out = dropout_add(out, query, self.dropout, is_training)
         return out, None

@@ -2,6 +2,8 @@
 //   _C.attn.fwd / _C.attn.bwd      generic strided / varlen flash attention (apex.ops.attention)
 //   _C.fmhalib.fwd / bwd (+ _nl)   the reference contrib FMHA module (apex/contrib/fmha/fmha.py:33-55):
 //                                  packed qkv [total, 3, h, d] with cu_seqlens
+#include <cmath>
+
 #include "common.h"
 #include "apex_amd/attn_api.h"
 
@@ -45,6 +47,9 @@ void fill_common(Common& c, const at::Tensor& q, const at::Tensor& k, const at::
   const bool varlen = has(cu_q);
   TORCH_CHECK(varlen == has(cu_k), "attn: cu_seqlens_q and cu_seqlens_k go together");
   TORCH_CHECK(q.scalar_type() == k.scalar_type() && q.scalar_type() == v.scalar_type(), "attn: dtype mismatch");
+  // the forward's softmax takes the row max of the RAW scores and scales afterwards (valid for a
+  // positive scale only), and folds the bias in as bias / scale
+  TORCH_CHECK(scale > 0.0 && std::isfinite(scale), "attn: softmax scale must be positive and finite, got ", scale);
   AttnArgs& a = c.a;
   a.q = view_of(q, varlen, "q");
   a.k = view_of(k, varlen, "k");

@@ -380,10 +380,12 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
 
 // ---- statistics finalize: fixed-order sum of the per-workgroup partials -> batch mean /
 // inv_std, the running-stat EMA and the apply coefficients coef = [scale | shift] ----
+// ``shift`` (the statistics' centring shift) is usually the running mean itself, so shift, rmean
+// and rvar are NOT restrict: shift[ch] is read into a register before rmean[ch] is written.
 __global__ void __launch_bounds__(256) stats_finalize(const float* __restrict__ part, int g, int c, float n,
-                                                      const float* __restrict__ shift, const float* __restrict__ w,
+                                                      const float* shift, const float* __restrict__ w,
                                                       const float* __restrict__ b, float eps, float momentum,
-                                                      float* __restrict__ rmean, float* __restrict__ rvar,
+                                                      float* rmean, float* rvar,
                                                       float* __restrict__ save_mean, float* __restrict__ save_invstd,
                                                       float* __restrict__ coef) {
   // 8 channels x 32 partial-row groups per block (the finalize is latency-bound)

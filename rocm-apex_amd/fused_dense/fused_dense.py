@@ -75,9 +75,16 @@ def route_mode():
     return os.environ.get("APEX_AMD_DENSE_ROUTE", "lt")
 
 
-def _lt():
-    """hipBLASLt epilogue GEMMs (None when the route is not lt / the extension lacks them)."""
+def _lt(*tensors):
+    """hipBLASLt epilogue GEMMs, or None when the route is not lt, the extension lacks them, or
+    the operands are not all CUDA fp16 / all CUDA bf16 (the wrapper's kernels take those only:
+    fp32 and mixed-dtype calls run the torch ops instead)."""
     if route_mode() not in ("lt", "auto"):
+        return None
+    ts = [t for t in tensors if t is not None]
+    if not ts or ts[0].dtype not in (torch.float16, torch.bfloat16):
+        return None
+    if any(not t.is_cuda or t.dtype != ts[0].dtype for t in ts):
         return None
     return _native.submodule("lt_gemm")
 
@@ -118,8 +125,8 @@ def _use_native(key, native_fn, library_fn):
 
 def _lib_dense_fwd(x, w, b):
     x2 = x.reshape(-1, x.shape[-1])
-    lt = _lt()
-    if lt is not None and x2.is_cuda and x2.is_contiguous():
+    lt = _lt(x2, w, b)
+    if lt is not None and x2.is_contiguous():
         r = lt.linear(x2, w.contiguous(), b, lt.EPI_BIAS if b is not None else lt.EPI_NONE)
         if r:
             return r[0].view(x.shape[:-1] + (w.shape[0],))
@@ -152,8 +159,8 @@ def _lt_bgradb():
 def _lib_wgrad(g2, x2, has_bias):
     """(dW, db): matmul + column sum, or (APEX_AMD_LT_BGRADB=1) one hipBLASLt launch with the BGRADB
     epilogue."""
-    lt = _lt()
-    if lt is not None and g2.is_cuda and has_bias and _lt_bgradb():
+    lt = _lt(g2, x2)
+    if lt is not None and has_bias and _lt_bgradb():
         r = lt.wgrad_bgrad(g2.contiguous(), x2.contiguous(), has_bias)
         if r:
             return r[0], (r[1] if has_bias else None)
@@ -212,8 +219,8 @@ class DenseNoBiasFunc(torch.autograd.Function):
 
 def _lib_gelu_dense_fwd(x, w1, b1, w2, b2):
     x2 = x.reshape(-1, x.shape[-1])
-    lt = _lt()
-    if lt is not None and x2.is_cuda and x2.is_contiguous():
+    lt = _lt(x2, w1, b1, w2, b2)
+    if lt is not None and x2.is_contiguous():
         w1c, w2c = w1.contiguous(), w2.contiguous()
         r1 = lt.linear(x2, w1c, b1, lt.EPI_GELU_AUX_BIAS)
         if r1:
@@ -273,9 +280,9 @@ class FusedDenseGeluDenseFunc(torch.autograd.Function):
         h = output1.reshape(-1, output1.shape[-1])
         x2 = input.reshape(-1, input.shape[-1])
         dw2, db2 = _lib_wgrad(g2, h, True)
-        lt = _lt()
+        lt = _lt(g2, weight2, gelu_in)
         gz = db1 = None
-        if lt is not None and g2.is_cuda:
+        if lt is not None:
             args = (g2.contiguous(), weight2.contiguous(), gelu_in.reshape(h.shape).contiguous())
             r = lt.dgelu_bgrad(*args, True)  # dGeLU and the bias gradient in the dgrad epilogue
             if r:
@@ -286,7 +293,8 @@ class FusedDenseGeluDenseFunc(torch.autograd.Function):
         if gz is None:
             dh = g2.matmul(weight2)
             z = gelu_in.reshape(h.shape)
-            if _native.use_native(dh) and _native.submodule("gemm") is not None and dh.shape[1] % 8 == 0:
+            if (_native.use_native(dh) and _native.submodule("gemm") is not None and dh.shape[1] % 8 == 0
+                    and dh.dtype in (torch.float16, torch.bfloat16) and z.dtype == dh.dtype):
                 # dGeLU + bias gradient in one native pass over dh (no GeLU recompute)
                 gz, db1 = _g().dgelu_column_sum(dh, z.contiguous())
             else:

@@ -144,6 +144,20 @@ class Bottleneck(nn.Module):
         return self.relu(out + identity)
 
 
+def _has_hooks(layers):
+    from torch.nn.modules import module as _m
+
+    if any(getattr(_m, n, None) for n in ("_global_forward_hooks", "_global_forward_pre_hooks",
+                                         "_global_backward_hooks", "_global_backward_pre_hooks")):
+        return True
+    for layer in layers:
+        for mod in (layer, *layer):
+            if (mod._forward_hooks or mod._forward_pre_hooks or mod._backward_hooks
+                    or getattr(mod, "_backward_pre_hooks", None)):
+                return True
+    return False
+
+
 class ResNet(nn.Module):
     def __init__(self, block, layers, num_classes=1000, zero_init_residual=False, groups=1, width_per_group=64,
                  norm_layer=None, fused_bn=False, bn_group=1):
@@ -211,14 +225,22 @@ class ResNet(nn.Module):
 
             x = bn_relu_maxpool(self.conv1(x), self.bn1, self.maxpool)
             # bottleneck nodes hand each other their output BN's state (ops/bottleneck_bn.py
-            # BlockLink): block i+1's conv1 dgrad does block i's bn3 backward reduction
-            link = None
-            for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
-                for blk in layer:
-                    if isinstance(blk, Bottleneck):
-                        x, link = blk.forward_linked(x, link)
-                    else:
-                        x, link = blk(x), None
+            # BlockLink): block i+1's conv1 dgrad does block i's bn3 backward reduction.  The
+            # linked walk calls the blocks directly and hands block i the ReLU-MASKED gradient of
+            # its output, so with any module hook on the layers / blocks (forward or backward,
+            # global ones included) the model runs each layer through ``__call__`` unlinked.
+            layers = (self.layer1, self.layer2, self.layer3, self.layer4)
+            if _has_hooks(layers):
+                for layer in layers:
+                    x = layer(x)
+            else:
+                link = None
+                for layer in layers:
+                    for blk in layer:
+                        if isinstance(blk, Bottleneck):
+                            x, link = blk.forward_linked(x, link)
+                        else:
+                            x, link = blk(x), None
         else:
             x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
             x = self.layer4(self.layer3(self.layer2(self.layer1(x))))

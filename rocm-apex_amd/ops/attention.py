@@ -119,7 +119,7 @@ class FlashAttnFunc(torch.autograd.Function):
             if b is not None:
                 while b.dim() < 4:
                     b = b.unsqueeze(0)
-            step = dropout_rng.step_tensor(q.device) if p > 0 else None
+            step = dropout_rng.snapshot(q.device) if p > 0 else None
             out, lse = C.attn.fwd(q, k, v, cu_q, cu_k, max_q, max_k, scale, causal, b, p, seed, offset,
                                   rng_step=step)
             ctx.save_for_backward(q, k, v, out, lse, b, cu_q, cu_k)
@@ -199,7 +199,7 @@ class _PackedQKVSelfAttention(torch.autograd.Function):
         if bias4 is not None:
             while bias4.dim() < 4:
                 bias4 = bias4.unsqueeze(0)
-        step = dropout_rng.step_tensor(mixed.device) if p > 0 else None
+        step = dropout_rng.snapshot(mixed.device) if p > 0 else None
         _, lse = C.attn.fwd(q, k, v, None, None, 0, 0, scale, causal, bias4, p, seed, offset, out.permute(1, 0, 2, 3),
                             rng_step=step)
         ctx.save_for_backward(mixed, out, lse, bias4)

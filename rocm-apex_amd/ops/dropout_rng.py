@@ -8,7 +8,8 @@ frozen at capture time, so every replay would redraw the SAME masks.  With devic
 enabled, each launch additionally gets a pointer to a per-device int64 step counter and uses
 ``offset + (step << 32)``; ``advance()`` bumps that counter ON THE DEVICE (one tiny kernel, itself
 capturable), so a graph that starts with ``advance()`` draws fresh masks on every replay while the
-forward and the backward of one step still agree (the counter only moves between steps).
+forward and the backward of one call always agree: each forward launches with a snapshot of the
+counter (``snapshot()``) and saves that snapshot for its backward.
 
 Eager code that never calls ``enable()`` is unaffected (no pointer is passed)."""
 import torch
@@ -38,6 +39,16 @@ def step_tensor(device):
         t = torch.zeros(1, dtype=torch.int64, device=torch.device("cuda", key))
         _STEPS[key] = t
     return t
+
+
+def snapshot(device):
+    """A private copy of the step counter for ONE dropout call (None when device steps are off).
+
+    The forward launches with the copy and saves it for the backward, so the backward rebuilds
+    exactly the forward's mask even when ``advance()`` runs in between (gradient accumulation,
+    pipeline 1F1B with several forwards in flight, recompute).  A D2D copy: capturable."""
+    t = step_tensor(device)
+    return None if t is None else t.clone()
 
 
 def advance(device=None):

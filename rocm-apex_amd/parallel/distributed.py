@@ -26,7 +26,6 @@ MI355X design (not a port of the reference's flatten / side-stream / unflatten p
   from rank 0's observed gradient-arrival order, broadcast to all ranks (reference behaviour,
   :284-317).
 """
-import os
 import warnings
 import weakref
 

@@ -30,6 +30,12 @@ def annotate(rec):
     return rec
 
 
+def foo(mod, op, d):
+    """The op model pricing ``op`` of module ``mod`` for the kernel record ``d`` (a ``Data``);
+    the reference's dispatch entry point (apex/pyprof/prof/prof.py:27-169)."""
+    return model(d.record(mod, op))
+
+
 def attribute_to_main_kernel(records):
     """An op launches several kernels (fills, transposes, the GEMM, a reduction); its modelled
     FLOPs / bytes are charged once, to the longest kernel of the op instance (same thread,

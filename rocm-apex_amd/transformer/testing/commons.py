@@ -9,6 +9,9 @@ import torch.nn as nn
 from .. import parallel_state, tensor_parallel
 
 
+TEST_SUCCESS_MESSAGE = ">> passed the test :-)"  # reference commons.py:27 (test harness banner)
+
+
 class MyLayer(nn.Module):
     def __init__(self, hidden_size, pre_process, post_process):
         super().__init__()

@@ -387,3 +387,41 @@ def test_gpu_fused_bias_dropout_add(with_bias):
     torch.testing.assert_close(r.grad.float(), r2.grad, atol=1e-2, rtol=1e-2)
     if with_bias:
         torch.testing.assert_close(b.grad.float(), b2.grad, atol=0.5, rtol=2e-2)
+
+
+def test_cpu_reference_functional_api_matches_modules():
+    """The reference's functional module paths (``*_multihead_attn_func``) give the modules' results."""
+    from apex.contrib.multihead_attn import EncdecMultiheadAttn, SelfMultiheadAttn
+    from apex.contrib.multihead_attn.encdec_multihead_attn_func import encdec_attn_func
+    from apex.contrib.multihead_attn.fast_encdec_multihead_attn_func import fast_encdec_attn_func
+    from apex.contrib.multihead_attn.fast_self_multihead_attn_func import fast_self_attn_func
+    from apex.contrib.multihead_attn.fast_self_multihead_attn_norm_add_func import fast_self_attn_norm_add_func
+    from apex.contrib.multihead_attn.self_multihead_attn_func import SelfAttnFunc, self_attn_func
+
+    torch.manual_seed(5)
+    m = SelfMultiheadAttn(64, 4, bias=True, impl="default")
+    x = torch.randn(10, 3, 64)
+    kpm = torch.zeros(3, 10, dtype=torch.bool)
+    kpm[2, 6:] = True
+    ref, _ = m(x, x, x, key_padding_mask=kpm, is_training=False)
+    got = self_attn_func(False, False, 4, m.scaling, x, m.in_proj_weight, m.out_proj_weight, m.in_proj_bias,
+                         m.out_proj_bias, kpm, False, 0.0)
+    torch.testing.assert_close(got, ref)
+    assert SelfAttnFunc.apply is self_attn_func
+    got = fast_self_attn_func(False, False, 4, x, m.in_proj_weight, m.out_proj_weight, m.in_proj_bias,
+                              m.out_proj_bias, kpm, False, 0.0)
+    torch.testing.assert_close(got, ref, atol=1e-5, rtol=1e-4)
+    n = SelfMultiheadAttn(64, 4, include_norm_add=True, impl="fast")
+    ref, _ = n(x, x, x, is_training=False)
+    got = fast_self_attn_norm_add_func(False, False, 4, x, n.lyr_nrm_gamma_weights, n.lyr_nrm_beta_weights,
+                                       n.in_proj_weight, n.out_proj_weight, None, 0.0)
+    torch.testing.assert_close(got, ref)
+    e = EncdecMultiheadAttn(64, 8, impl="default")
+    q, kv = torch.randn(6, 2, 64), torch.randn(9, 2, 64)
+    ref, _ = e(q, kv, kv, is_training=False)
+    got = encdec_attn_func(False, False, 8, e.scaling, q, kv, e.in_proj_weight_q, e.in_proj_weight_kv,
+                           e.out_proj_weight, None, None, None, None, 0.0)
+    torch.testing.assert_close(got, ref)
+    got = fast_encdec_attn_func(False, False, 8, q, kv, e.in_proj_weight_q, e.in_proj_weight_kv, e.out_proj_weight,
+                                None, 0.0)
+    torch.testing.assert_close(got, ref, atol=1e-5, rtol=1e-4)

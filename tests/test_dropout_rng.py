@@ -104,3 +104,29 @@ def test_gpu_flash_attention_dropout_uses_step(device_rng):
     for a, b in ((o3, o3r), (dq, dqr), (dk, dkr), (dv, dvr)):
         s = max(1.0, float(b.abs().max()))
         torch.testing.assert_close(a.float() / s, b.float() / s, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.gpu
+def test_gpu_advance_between_forward_and_backward(device_rng):
+    """each forward snapshots the step counter, so an advance() between a forward and
+    its backward (gradient accumulation, 1F1B, recompute) cannot change the backward's mask."""
+    from apex.ops.attention import flash_attn_func
+    from apex.transformer.functional.fused_bias_dropout_add import fused_bias_dropout_add
+
+    torch.manual_seed(4)
+    x = torch.randn(64, 256, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    r = torch.zeros(64, 256, device="cuda", dtype=torch.bfloat16)
+    y = fused_bias_dropout_add(x, None, r, 0.3, True, 7, 2)
+    dropout_rng.advance()
+    (dx,) = torch.autograd.grad(y, x, torch.ones_like(y))
+    assert torch.equal(y != 0, dx != 0), "backward must reuse the forward's mask"
+    q, k, v = (torch.randn(2, 128, 4, 64, device="cuda", dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
+    go = torch.randn(2, 128, 4, 64, device="cuda", dtype=torch.bfloat16)
+    o = flash_attn_func(q, k, v, dropout_p=0.2, seed=5, offset=1)
+    ref = torch.autograd.grad(o, (q, k, v), go, retain_graph=True)
+    dropout_rng.advance()
+    dropout_rng.advance()
+    got = torch.autograd.grad(o, (q, k, v), go)
+    for a, b in zip(got, ref):
+        # (dQ is summed with float atomics: equal up to summation order, far below a mask change)
+        torch.testing.assert_close(a.float(), b.float(), atol=2e-3, rtol=1e-2)

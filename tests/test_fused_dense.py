@@ -155,6 +155,28 @@ def test_gpu_fused_dense_gelu_dense(dtype, route, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("route", ["native", "lt", "library"])
+def test_gpu_fused_dense_fp32(route, monkeypatch):
+    """fp32 GPU tensors take the torch ops on every route: the hipBLASLt wrapper only takes fp16 /
+    bf16 operands of one dtype and must not be called with fp32 ones."""
+    monkeypatch.setenv("APEX_AMD_DENSE_ROUTE", route)
+    torch.manual_seed(3)
+    x = torch.randn(64, 128, device="cuda", requires_grad=True)
+    dense = FusedDense(128, 96).cuda()
+    y = dense(x)
+    y.backward(torch.ones_like(y))
+    torch.testing.assert_close(y, x.detach() @ dense.weight.t() + dense.bias, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(dense.bias.grad, torch.full((96,), 64.0, device="cuda"))
+    mod = FusedDenseGeluDense(128, 256, 64).cuda()
+    x2 = torch.randn(2, 32, 128, device="cuda", requires_grad=True)
+    out = mod(x2)
+    ref = torch.nn.functional.gelu(x2.detach() @ mod.weight1.t() + mod.bias1, approximate="tanh") @ mod.weight2.t()
+    torch.testing.assert_close(out, ref + mod.bias2, atol=1e-4, rtol=1e-4)
+    out.sum().backward()
+    assert x2.grad is not None and torch.isfinite(x2.grad).all() and mod.bias1.grad is not None
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("activation", ["none", "relu", "sigmoid"])
 @pytest.mark.parametrize("bias", [True, False])
 def test_gpu_mlp_vs_sequential(activation, bias):

@@ -25,20 +25,32 @@ def short(name):
     return name[:90]
 
 
-def load(d):
+def _grid(r):
+    g = r.get("Grid_Size")
+    if g:
+        return int(g)
+    try:
+        return int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+    except (KeyError, ValueError):
+        return 0
+
+
+def load(d, by_grid=False):
     counters = collections.defaultdict(lambda: collections.defaultdict(list))
     durations = collections.defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         per = collections.defaultdict(dict)
         for r in csv.DictReader(open(f)):
-            key = (r.get("Dispatch_Id") or r.get("Correlation_Id"), short(r["Kernel_Name"]))
+            nm = short(r["Kernel_Name"]) + (f" @grid{_grid(r)}" if by_grid else "")
+            key = (r.get("Dispatch_Id") or r.get("Correlation_Id"), nm)
             per[key][r["Counter_Name"]] = per[key].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
         for (_, k), vals in per.items():
             for c, v in vals.items():
                 counters[k][c].append(v)
     for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            durations[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+            nm = short(r["Kernel_Name"]) + (f" @grid{_grid(r)}" if by_grid else "")
+            durations[nm].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     return counters, durations
 
 
@@ -47,8 +59,9 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--md")
     ap.add_argument("--filter", default="apex_amd::")
+    ap.add_argument("--by-grid", action="store_true", help="one row per (kernel, grid size): per-shape rows")
     a = ap.parse_args()
-    counters, durations = load(a.dir)
+    counters, durations = load(a.dir, a.by_grid)
     rows = []
     for k in sorted(set(counters) | set(durations)):
         if a.filter not in k:
