@@ -247,6 +247,9 @@ def timed(args, step, dev, world, rank, distributed, B, impl, desc=None):
         # in a rocprofv3 trace; tools/prof_summary.py --after spin_kernel keeps what follows it
         torch.cuda._sleep(100)
         torch.cuda.synchronize()
+    from apex.ops import bottleneck_bn
+
+    nodes0 = bottleneck_bn.NODE_CALLS[0]
     start = time.perf_counter()
     for i in range(args.steps):
         loss = step()
@@ -259,6 +262,9 @@ def timed(args, step, dev, world, rank, distributed, B, impl, desc=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     ms_per_step = elapsed * 1000.0 / args.steps
+    # fused bottleneck nodes run per timed step (16 on ResNet-50's fused path; graph replays do
+    # not re-enter Python, so the count is taken from the eager / capture steps)
+    nodes = (bottleneck_bn.NODE_CALLS[0] - nodes0) / args.steps
     value = world * B * args.steps / elapsed
     if rank == 0 and desc is not None:
         value = world * desc["items_per_gpu_step"] * args.steps / elapsed
@@ -303,6 +309,8 @@ def timed(args, step, dev, world, rank, distributed, B, impl, desc=None):
                 "parallelism": f"dp{world}",
                 "timing": "hipgraph-replay" if getattr(args, "graph", False) else "eager",
                 "bn_exchange": getattr(args, "bn_exchange", None),
+                "block_nodes_per_step": None if getattr(args, "graph", False) else nodes,
+                "block_node": bool(nodes > 0) if not getattr(args, "graph", False) else None,
                 "final_loss": round(float(loss.item()), 4),
             },
         }

@@ -315,6 +315,58 @@ at::Tensor bwd_group_finish(at::Tensor dy_masked, at::Tensor x, at::Tensor sums,
   return dx;
 }
 
+// group statistics without the apply: merge the [world, 2C+1] payloads -> (save_mean,
+// save_invstd, coef [2C], inv_count [1]), running stats updated (the fused bottleneck node
+// applies the coefficients inside its convolutions)
+std::vector<at::Tensor> stats_group_merge(at::Tensor gathered, OT w, OT b, OT running_mean, OT running_var,
+                                          double momentum, double eps) {
+  TORCH_CHECK(gathered.is_cuda() && gathered.scalar_type() == at::kFloat && gathered.is_contiguous() &&
+                  gathered.dim() == 2 && gathered.size(1) % 2 == 1,
+              "bn_nhwc: gathered statistics must be a contiguous fp32 [world, 2C+1] GPU tensor");
+  const int c = (int)(gathered.size(1) / 2);
+  for (const OT* p : {&w, &b, &running_mean, &running_var}) check_param(*p, c);
+  const c10::hip::HIPGuard g(gathered.get_device());
+  auto fo = gathered.options();
+  auto save_mean = at::empty({c}, fo), save_invstd = at::empty({c}, fo), coef = at::empty({2 * c}, fo);
+  auto inv_count = at::empty({1}, fo);
+  bn_nhwc_stats_merge(gathered.data_ptr<float>(), (int)gathered.size(0), c, fptr(w), fptr(b), (float)eps,
+                      (float)momentum, fptr_mut(running_mean), fptr_mut(running_var), save_mean.data_ptr<float>(),
+                      save_invstd.data_ptr<float>(), coef.data_ptr<float>(), inv_count.data_ptr<float>(),
+                      cur_stream());
+  return {save_mean, save_invstd, coef, inv_count};
+}
+
+// group backward from [2, G, C] reduction partials (sum_dy | sum_dy_xmu, e.g. a conv epilogue's):
+// (payload [2C], local grad_w, local grad_b)
+std::vector<at::Tensor> bwd_part_local(at::Tensor part, at::Tensor save_invstd) {
+  TORCH_CHECK(part.is_cuda() && part.dim() == 3 && part.size(0) == 2 && part.is_contiguous() &&
+                  part.scalar_type() == at::kFloat,
+              "bn_nhwc bwd_part_local: part must be the [2, G, C] fp32 partials");
+  const int c = (int)part.size(2);
+  check_param(save_invstd, c);
+  const c10::hip::HIPGuard g(part.get_device());
+  auto fo = part.options();
+  auto payload = at::empty({2 * (int64_t)c}, fo), gw = at::empty({c}, fo), gb = at::empty({c}, fo);
+  bn_nhwc_bwd_local(part.data_ptr<float>(), (int)part.size(1), c, save_invstd.data_ptr<float>(), gw.data_ptr<float>(),
+                    gb.data_ptr<float>(), payload.data_ptr<float>(), cur_stream());
+  return {payload, gw, gb};
+}
+
+// group backward: coef_bwd [3C] from the group's exchanged sums ([rows, 2C], summed in row order)
+at::Tensor bwd_group_coef(at::Tensor sums, at::Tensor inv_count, at::Tensor save_mean, at::Tensor save_invstd, OT w) {
+  const int c = (int)save_mean.numel();
+  TORCH_CHECK(sums.is_cuda() && sums.scalar_type() == at::kFloat && sums.is_contiguous() &&
+                  sums.numel() % (2 * (int64_t)c) == 0 && sums.numel() > 0,
+              "bn_nhwc: group sums must be a contiguous fp32 [rows, 2C] GPU tensor");
+  check_param(w, c);
+  const c10::hip::HIPGuard g(sums.get_device());
+  auto coef = at::empty({3 * (int64_t)c}, sums.options());
+  bn_nhwc_bwd_coef_group(sums.data_ptr<float>(), (int)(sums.numel() / (2 * (int64_t)c)), c, inv_count.data_ptr<float>(),
+                         save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(), fptr(w), coef.data_ptr<float>(),
+                         cur_stream());
+  return coef;
+}
+
 // statistics only: (save_mean, save_invstd, coef[2, C]) of x, running stats updated in place
 std::vector<at::Tensor> stats(at::Tensor x, OT w, OT b, OT running_mean, OT running_var, double momentum, double eps) {
   check2d(x, "input");
@@ -430,6 +482,9 @@ void bind_bn_nhwc(pybind11::module_& root) {
         pybind11::arg("w"), pybind11::arg("save_mean"), pybind11::arg("save_invstd"), pybind11::arg("coef_fwd"),
         pybind11::arg("relu"), pybind11::arg("dy2") = c10::nullopt, pybind11::arg("mask") = c10::nullopt);
   m.def("bwd_group_finish", &bwd_group_finish);
+  m.def("stats_group_merge", &stats_group_merge);
+  m.def("bwd_part_local", &bwd_part_local);
+  m.def("bwd_group_coef", &bwd_group_coef);
 }
 
 }  // namespace apex_amd

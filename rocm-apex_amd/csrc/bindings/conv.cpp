@@ -184,6 +184,23 @@ std::vector<at::Tensor> bn_finalize(const at::Tensor& part, double count, const 
   return {sm, si, coef};
 }
 
+// bn_group > 1: this rank's Welford payload [mean | M2 | count] (2C + 1) from the partials
+at::Tensor part_payload(const at::Tensor& part, double count, const c10::optional<at::Tensor>& shift) {
+  TORCH_CHECK(part.is_cuda() && part.dim() == 3 && part.size(0) == 2 && part.is_contiguous() &&
+                  part.scalar_type() == at::kFloat,
+              "part_payload: part must be the [2, G, C] fp32 partials");
+  const int c = (int)part.size(2);
+  if (shift.has_value())
+    TORCH_CHECK(shift->is_cuda() && shift->scalar_type() == at::kFloat && shift->is_contiguous() && shift->numel() == c,
+                "part_payload: shift must be contiguous fp32 [C]");
+  const c10::hip::HIPGuard g(part.get_device());
+  auto payload = at::empty({2 * (int64_t)c + 1}, part.options());
+  conv1x1_bn_part_payload(part.data_ptr<float>(), (int)part.size(1), c, (float)count,
+                          shift.has_value() ? shift->data_ptr<float>() : nullptr, payload.data_ptr<float>(),
+                          cur_stream());
+  return payload;
+}
+
 // dW [N, K] = g^T . pro(x) (pro = relu(x * xcoef[:K] + xcoef[K:]) when given), out_dtype per `like`
 at::Tensor wgrad1x1(const at::Tensor& g, const at::Tensor& x, const c10::optional<at::Tensor>& xcoef,
                     c10::optional<at::ScalarType> out_dtype) {
@@ -321,6 +338,7 @@ void bind_conv(pybind11::module_& root) {
   });
   m.def("wgrad", &wgrad);
   m.def("force_fprop_cfg", &conv_force_fprop_cfg);
+  m.def("force_wgrad_variant", &conv_force_wgrad_variant);
   m.def("bn1x1", &bn1x1, pybind11::arg("a"), pybind11::arg("w"), pybind11::arg("w_kmajor_out") = false,
         pybind11::arg("pcoef") = pybind11::none(), pybind11::arg("shift") = pybind11::none(),
         pybind11::arg("stats") = false, pybind11::arg("res") = pybind11::none(),
@@ -333,6 +351,8 @@ void bind_conv(pybind11::module_& root) {
         pybind11::arg("py") = pybind11::none(), pybind11::arg("pcoef") = pybind11::none(),
         pybind11::arg("want_aout") = false);
   m.def("bnbwd_finalize", &bnbwd_finalize);
+  m.def("part_payload", &part_payload, pybind11::arg("part"), pybind11::arg("count"),
+        pybind11::arg("shift") = pybind11::none());
   m.def("wgrad1x1", &wgrad1x1, pybind11::arg("g"), pybind11::arg("x"), pybind11::arg("xcoef") = pybind11::none(),
         pybind11::arg("out_dtype") = pybind11::none());
 }

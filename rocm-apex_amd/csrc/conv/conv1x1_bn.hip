@@ -423,6 +423,35 @@ __global__ void __launch_bounds__(256) stats_finalize(const float* __restrict__ 
 
 // backward reduction finalize (the RED partials): grad_w, grad_b and the dx coefficients
 // coef_bwd = [A | B | K] with dx = A * g + B * x + K (the BN backward of a training-mode norm)
+// ---- group (cross-rank) statistics from the epilogue partials: the Welford payload
+// [mean(C) | M2(C) | count] of this rank, M2 = sum of squared deviations from the local mean,
+// for the group exchange + merge of csrc/groupbn (bn_nhwc_stats_merge) ----
+__global__ void __launch_bounds__(256) part_payload(const float* __restrict__ part, int g, int c, float n,
+                                                    const float* shift, float* __restrict__ payload) {
+  __shared__ float red[2][32][9];
+  const int lc = threadIdx.x & 7, grp = threadIdx.x >> 3, ch = blockIdx.x * 8 + lc;
+  float a = 0.f, q = 0.f;
+  if (ch < c)
+    for (int j = grp; j < g; j += 32) {
+      a += part[(int64_t)j * c + ch];
+      q += part[(int64_t)(g + j) * c + ch];
+    }
+  red[0][grp][lc] = a;
+  red[1][grp][lc] = q;
+  __syncthreads();
+  if (grp != 0 || ch >= c) return;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll 8
+  for (int i = 0; i < 32; ++i) {
+    s1 += red[0][i][lc];
+    s2 += red[1][i][lc];
+  }
+  const float dm = s1 / n;
+  payload[ch] = (shift ? shift[ch] : 0.f) + dm;
+  payload[c + ch] = fmaxf(s2 - s1 * dm, 0.f);
+  if (ch == 0) payload[2 * c] = n;
+}
+
 __global__ void __launch_bounds__(256) bwd_finalize(const float* __restrict__ part, int g, int c, float inv_n,
                                                     const float* __restrict__ mean, const float* __restrict__ istd,
                                                     const float* __restrict__ w, float* __restrict__ gw,
@@ -1183,6 +1212,12 @@ void conv1x1_wgrad(const void* g, const void* x, void* dw, int out_dtype, int64_
     hipLaunchKernelGGL((c1w::wgrad_reduce<TO>), dim3(blocks), dim3(256), 0, s, ws, sp, nk, static_cast<TO*>(dw));
   }, "conv1x1 wgrad reduce");
   check_launch("conv1x1_wgrad");
+}
+
+void conv1x1_bn_part_payload(const float* part, int g, int c, float n, const float* shift, float* payload,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(c1bn::part_payload, dim3((c + 7) / 8), dim3(256), 0, s, part, g, c, n, shift, payload);
+  check_launch("conv1x1_bn_part_payload");
 }
 
 void conv1x1_bnbwd_finalize(const float* part, int g, int c, float inv_n, const float* mean, const float* istd,

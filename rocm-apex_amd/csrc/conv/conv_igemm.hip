@@ -29,6 +29,7 @@
 #include "apex_amd/dispatch.h"
 #include "apex_amd/launch_plan.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
 
@@ -44,9 +45,36 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // 128 bytes of zeros: the DMA source for padding taps and rows past the end
 __device__ __attribute__((aligned(16))) uint16_t g_zero[64];
 
+// exact unsigned 32-bit division by a runtime-constant divisor (Granlund-Montgomery, round-up
+// multiplier with the "add" fix-up): q = (t + ((n - t) >> s1)) >> s2, t = umulhi(n, mul).  Four
+// VALU ops instead of the ~30 of a v_rcp-based integer divide.
+struct FastDiv {
+  uint32_t d, mul, s1, s2;
+};
+
+inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  f.mul = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+  f.s1 = l > 0 ? 1 : 0;
+  f.s2 = l > 0 ? l - 1 : 0;
+  return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  const uint32_t t = __umulhi(n, f.mul);
+  return (t + ((n - t) >> f.s1)) >> f.s2;
+}
+
 struct Geo {
   int n, h, w, c, oh, ow, oht, owt, kout, ish, isw, osh, osw, oph, opw, ntaps, m;
   int dh[kConvMaxTaps], dw[kConvMaxTaps];
+  int tapoff[kConvMaxTaps];  // byte offset of tap t in the input image: (dh * w + dw) * c * 2
+  FastDiv div_ohw, div_ow;
+  int ident;                 // output pixel == M row (stride-1 placement over the whole tensor)
+  int xbytes, wbytes;        // buffer-descriptor ranges (< 2^31: fprop2 only)
   const float* scale;
   const float* bias;
   const uint16_t* res;
@@ -72,7 +100,14 @@ inline Geo make_geo(const ConvTapArgs& a) {
   for (int t = 0; t < kConvMaxTaps; ++t) {
     g.dh[t] = t < a.ntaps ? a.dh[t] : 0;
     g.dw[t] = t < a.ntaps ? a.dw[t] : 0;
+    g.tapoff[t] = (g.dh[t] * a.iw + g.dw[t]) * a.c * 2;
   }
+  g.div_ohw = make_fastdiv((uint32_t)(a.oh * a.ow));
+  g.div_ow = make_fastdiv((uint32_t)a.ow);
+  g.ident = a.osh == 1 && a.osw == 1 && a.oph == 0 && a.opw == 0 && a.oht == a.oh && a.owt == a.ow;
+  const int64_t xb = (int64_t)a.n * a.ih * a.iw * a.c * 2, wb = (int64_t)a.kout * a.ntaps * a.c * 2;
+  g.xbytes = xb < (1ll << 31) ? (int)xb : -1;
+  g.wbytes = wb < (1ll << 31) ? (int)wb : -1;
   return g;
 }
 
@@ -104,7 +139,7 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 // =============================================================================================
 // fprop
 // =============================================================================================
-constexpr int BM = plan::kConvBM, BK = 64;
+constexpr int BM = 256, BK = 64;  // fprop_kernel output-pixel tile, K step
 constexpr int STAGES = 3;  // wgrad LDS ring depth
 
 // Tile configuration: BN output channels per workgroup, WM x WN waves, S-deep LDS ring.
@@ -119,6 +154,108 @@ struct FCfg {
   static constexpr size_t LDS = OPS > EPI ? OPS : EPI;
   static_assert(PA >= 1 && PB >= 1 && TM >= 1 && TN >= 1, "bad tile configuration");
 };
+
+// Epilogue of one EH-row chunk of an fprop tile whose fp32 accumulators are staged in ``cs``
+// ([EH][BN + 4] floats): fused scale / bias / residual / ReLU / mask, 16-byte row stores, and the
+// consuming BN's statistics partials of the chunk ([2][ceil(M / 128)][kout], one row per 128
+// output rows; EH = 128 or 64 — two 64-row chunks of one 128-row stats tile sum there in the
+// finalize).  Ends with LDS reused for the statistics fold: the caller barriers before reusing cs.
+template <int EH>
+__device__ __forceinline__ int stats_row_of(int row0c) { return row0c / 128 * (128 / EH) + (row0c % 128) / EH; }
+
+template <typename T, int BN, int THREADS, int EH>
+__device__ __forceinline__ void epi_chunk(const Geo& g, uint16_t* __restrict__ Y, float* cs, int row0c, int col0,
+                                          int tid) {
+  constexpr int CST = BN + 4;
+  constexpr int CPR = BN / 8;               // 8-column chunks per row
+  constexpr int RP = THREADS / CPR;         // rows per pass
+  static_assert(EH % RP == 0 || RP > EH, "epilogue row passes");
+  const int ch = tid % CPR, rsub = tid / CPR;
+  const int gc = col0 + ch * 8;
+  float sc[8], bi[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = 1.f;
+    bi[e] = 0.f;
+  }
+  if (g.scale) Vec8<float>::load(sc, g.scale + gc);
+  if (g.bias) Vec8<float>::load(bi, g.bias + gc);
+  const bool affine = g.scale || g.bias;
+  float st1[8], st2[8], sft[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) st1[e] = st2[e] = sft[e] = 0.f;
+  if (g.stats && g.shift) Vec8<float>::load(sft, g.shift + gc);
+  const int ohw = g.oh * g.ow;
+#pragma unroll
+  for (int it = 0; it < (EH + RP - 1) / RP; ++it) {
+    const int rl = rsub + RP * it;
+    const int m = row0c + rl;
+    if (rl < EH && m < g.m) {
+      int64_t pix = m;
+      if (!g.ident) {
+        const int nimg = (int)fdiv((uint32_t)m, g.div_ohw), rem = m - nimg * ohw;
+        const int oy = (int)fdiv((uint32_t)rem, g.div_ow), ox = rem - oy * g.ow;
+        pix = ((int64_t)nimg * g.oht + oy * g.osh + g.oph) * g.owt + ox * g.osw + g.opw;
+      }
+      float v[8];
+      const float4 lo = *reinterpret_cast<const float4*>(cs + rl * CST + ch * 8);
+      const float4 hi = *reinterpret_cast<const float4*>(cs + rl * CST + ch * 8 + 4);
+      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+      v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+      if (affine) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaf(v[e], sc[e], bi[e]);
+      }
+      if (g.res) {
+        float r[8];
+        Vec8<T>::load(r, reinterpret_cast<const T*>(g.res) + pix * g.kout + gc);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += r[e];
+      }
+      if (g.relu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if (g.mask) {
+        float mk[8];
+        Vec8<T>::load(mk, reinterpret_cast<const T*>(g.mask) + pix * g.kout + gc);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = mk[e] > 0.f ? v[e] : 0.f;
+      }
+      Vec8<T>::store(reinterpret_cast<T*>(Y) + pix * g.kout + gc, v);
+      if (g.stats) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = v[e] - sft[e];
+          st1[e] += d;
+          st2[e] = fmaf(d, d, st2[e]);
+        }
+      }
+    }
+  }
+  if (g.stats && row0c < g.m) {  // (uniform: a chunk wholly past M has no statistics row)
+    // fixed-order fold of the row groups sharing each column chunk (cs is dead: reuse it)
+    constexpr int NG = RP < EH ? RP : EH;
+    __syncthreads();
+    float* red = cs;
+    if (rsub < NG) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(rsub * 2 + 0) * BN + ch * 8 + e] = st1[e];
+        red[(rsub * 2 + 1) * BN + ch * 8 + e] = st2[e];
+      }
+    }
+    __syncthreads();
+    const int tiles = (g.m + 127) / 128 * (128 / EH);
+    const int srow = stats_row_of<EH>(row0c);
+    for (int i = tid; i < 2 * BN; i += THREADS) {
+      const int which = i / BN, col = i % BN;
+      float acc2 = 0.f;
+      for (int r = 0; r < NG; ++r) acc2 += red[(r * 2 + which) * BN + col];
+      g.stats[((int64_t)which * tiles + srow) * g.kout + col0 + col] = acc2;
+    }
+  }
+}
 
 // k-major fragment of a 32-row subtile at k-step kk from a swizzled [rows][64] image
 __device__ __forceinline__ s16x8 frag_k(const uint16_t* tile, int rowbase, int kk, int lane) {
@@ -244,30 +381,10 @@ fprop_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, ui
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // ---- epilogue: two 128-row halves staged as fp32 through LDS, 16-byte row stores ----
-  constexpr int CST = BN + 4;
-  constexpr int CPR = BN / 8;               // 8-column chunks per row
-  constexpr int RP = C::THREADS / CPR;      // rows per pass
+  // ---- epilogue: 128-row chunks staged as fp32 through LDS, 16-byte row stores ----
   float* cs = reinterpret_cast<float*>(lds);
-  const int ch = tid % CPR, rsub = tid / CPR;
-  const int gc = col0 + ch * 8;
-  // fused epilogue operands of this thread's 8 columns (folded-BN scale/bias: per channel)
-  float sc[8], bi[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    sc[e] = 1.f;
-    bi[e] = 0.f;
-  }
-  if (g.scale) Vec8<float>::load(sc, g.scale + gc);
-  if (g.bias) Vec8<float>::load(bi, g.bias + gc);
-  const bool affine = g.scale || g.bias;
-  // BN statistics of the stored values (the consuming batch norm's pass over Y, done here)
-  float st1[8], st2[8], sft[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) st1[e] = st2[e] = sft[e] = 0.f;
-  if (g.stats && g.shift) Vec8<float>::load(sft, g.shift + gc);
-#pragma unroll
-  for (int half = 0; half < 2; ++half) {
+  for (int half = 0; half < BM / 128; ++half) {
     const int wr0 = wm * (BM / WM);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -278,71 +395,175 @@ fprop_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, ui
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int rl = rb - 128 * half + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          cs[rl * CST + wn * (BN / WN) + 32 * j + (lane & 31)] = acc[i][j][r];
+          cs[rl * (BN + 4) + wn * (BN / WN) + 32 * j + (lane & 31)] = acc[i][j][r];
         }
     }
     __syncthreads();
-#pragma unroll
-    for (int it = 0; it < 128 / RP; ++it) {
-      const int rl = rsub + RP * it;
-      const int m = row0 + half * 128 + rl;
-      if (m < g.m) {
-        const int nimg = m / ohw, rem = m - nimg * ohw;
-        const int oy = rem / g.ow, ox = rem - oy * g.ow;
-        const int64_t pix = ((int64_t)nimg * g.oht + oy * g.osh + g.oph) * g.owt + ox * g.osw + g.opw;
-        float v[8];
-        const float4 lo = *reinterpret_cast<const float4*>(cs + rl * CST + ch * 8);
-        const float4 hi = *reinterpret_cast<const float4*>(cs + rl * CST + ch * 8 + 4);
-        v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
-        v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
-        if (affine) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = fmaf(v[e], sc[e], bi[e]);
-        }
-        if (g.res) {
-          float r[8];
-          Vec8<T>::load(r, reinterpret_cast<const T*>(g.res) + pix * g.kout + gc);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += r[e];
-        }
-        if (g.relu) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-        }
-        if (g.mask) {
-          float mk[8];
-          Vec8<T>::load(mk, reinterpret_cast<const T*>(g.mask) + pix * g.kout + gc);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = mk[e] > 0.f ? v[e] : 0.f;
-        }
-        Vec8<T>::store(reinterpret_cast<T*>(Y) + pix * g.kout + gc, v);
-        if (g.stats) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float d = v[e] - sft[e];
-            st1[e] += d;
-            st2[e] = fmaf(d, d, st2[e]);
-          }
-        }
-      }
-    }
+    epi_chunk<T, BN, C::THREADS, 128>(g, Y, cs, row0 + 128 * half, col0, tid);
     __syncthreads();
   }
-  if (g.stats) {
-    // fixed-order fold of the RP row-groups sharing each column chunk (LDS is free again)
-    float* red = reinterpret_cast<float*>(lds);
+}
+
+// ---------------------------------------------------------------------------------------------
+// fprop2: the same tap GEMM with the operand staging rebuilt for a low VALU count per MFMA.
+//   * A rows are fetched with buffer_load ... lds through a range-checked descriptor: a padding
+//     tap or a row past M gets an out-of-range offset and the hardware writes zeros (no zero
+//     page, no 64-bit address math).  Each lane precomputes, once, its rows' byte offsets and a
+//     ntaps-bit validity mask, so a K-step costs ~4 VALU per 1-KiB piece (bit test, add, select)
+//     instead of ~20 (64-bit address, two range compares, select).
+//   * B (weights) offsets are a per-lane constant plus the step's scalar k offset.
+//   * Pixel decomposition (setup and epilogue) by multiply-high (FastDiv), the epilogue skips
+//     it entirely for the identity output placement.
+//   * BM x BN tiles with 64 x 64 (or 128 x 64) per wave: every A fragment feeds TN MFMAs and every
+//     B fragment TM (the 32 x 64 per-wave tiles of fprop_kernel re-read B for every 2 MFMAs).
+// Requires the input and weight tensors to be < 2 GiB (buffer ranges); fprop_kernel otherwise.
+// ---------------------------------------------------------------------------------------------
+template <int BM_, int BN_, int WM_, int WN_, int S_>
+struct F2Cfg {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, S = S_;
+  static constexpr int NW = WM * WN, THREADS = NW * 64;
+  static constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  static constexpr int PA = BM / 8 / NW, PB = BN / 8 / NW;
+  static constexpr size_t OPS = (size_t)S * (BM * BK + BN * BK) * 2;
+  static constexpr size_t EPI = (size_t)128 * (BN + 4) * 4;
+  static constexpr size_t LDS = OPS > EPI ? OPS : EPI;
+  static_assert(PA >= 1 && PB >= 1 && TM >= 1 && TN >= 1 && BM % 128 == 0, "bad fprop2 tile configuration");
+};
+
+__device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint16_t* lds_dst) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_dst, 16, (int)voff, 0, 0,
+                                           0);
+}
+
+template <typename T, typename C>
+__global__ void __launch_bounds__(C::THREADS, 1)
+fprop2_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y, Geo g) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  constexpr int BM2 = C::BM, BN = C::BN, WM = C::WM, WN = C::WN, NW = C::NW, TM = C::TM, TN = C::TN;
+  constexpr int PA = C::PA, PB = C::PB, S = C::S;
+  constexpr int TA = BM2 * BK, TB = BN * BK;
+  auto a_buf = [&](int b) { return lds + b * (TA + TB); };
+  auto b_buf = [&](int b) { return lds + b * (TA + TB) + TA; };
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_m = (g.m + BM2 - 1) / BM2, tiles_n = g.kout / BN;
+  const int wg = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int bm = wg / tiles_n, bn = wg % tiles_n;
+  const int row0 = bm * BM2, col0 = bn * BN;
+  const int ohw = g.oh * g.ow;
+  const int kw = g.ntaps * g.c;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)X, 0, __builtin_amdgcn_readfirstlane(g.xbytes), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)Wt, 0, __builtin_amdgcn_readfirstlane(g.wbytes), 0x00020000);
+
+  // this lane's A rows: byte offset of (pixel origin, its 16-byte chunk) + tap validity bits
+  uint32_t aoff[PA], amask[PA];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      red[(rsub * 2 + 0) * BN + ch * 8 + e] = st1[e];
-      red[(rsub * 2 + 1) * BN + ch * 8 + e] = st2[e];
+  for (int i = 0; i < PA; ++i) {
+    const int row = 8 * (i * NW + wave) + (lane >> 3);
+    const int m = row0 + row;
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    aoff[i] = 0;
+    amask[i] = 0;
+    if (m < g.m) {
+      const int nimg = (int)fdiv((uint32_t)m, g.div_ohw), rem = m - nimg * ohw;
+      const int oy = (int)fdiv((uint32_t)rem, g.div_ow), ox = rem - oy * g.ow;
+      const int ih0 = oy * g.ish, iw0 = ox * g.isw;
+      aoff[i] = (uint32_t)((((nimg * g.h + ih0) * g.w + iw0) * g.c + 8 * chunk) * 2);
+      uint32_t mk = 0;
+      for (int t = 0; t < g.ntaps; ++t) {
+        const int ih = ih0 + g.dh[t], iw = iw0 + g.dw[t];
+        mk |= ((unsigned)ih < (unsigned)g.h && (unsigned)iw < (unsigned)g.w) ? (1u << t) : 0u;
+      }
+      amask[i] = mk;
+    }
+  }
+  uint32_t boff[PB];
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {
+    const int row = 8 * (i * NW + wave) + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    boff[i] = (uint32_t)(((col0 + row) * kw + 8 * chunk) * 2);
+  }
+  const int cblocks = g.c / BK;
+  const int nk = g.ntaps * cblocks;
+
+  auto issue = [&](int kt, int buf) {
+    const int t = kt / cblocks, c0 = (kt - t * cblocks) * BK;
+    const uint32_t toff = (uint32_t)(g.tapoff[t] + c0 * 2);
+    uint16_t* adst = a_buf(buf);
+#pragma unroll
+    for (int i = 0; i < PA; ++i) {
+      const uint32_t voff = ((amask[i] >> t) & 1u) ? aoff[i] + toff : 0x80000000u;  // OOB -> zeros
+      bdma16(xr, voff, adst + (i * NW + wave) * 512);
+    }
+    uint16_t* bdst = b_buf(buf);
+    const uint32_t k0b = (uint32_t)((t * g.c + c0) * 2);
+#pragma unroll
+    for (int i = 0; i < PB; ++i) bdma16(wr, boff[i] + k0b, bdst + (i * NW + wave) * 512);
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  constexpr int PER_STEP = PA + PB;
+#pragma unroll
+  for (int p = 0; p < S - 1; ++p)
+    if (p < nk) issue(p, p);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = nk - 1 - kt < S - 2 ? nk - 1 - kt : S - 2;
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER_STEP) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_STEP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + S - 1 < nk) issue(kt + S - 1, (kt + S - 1) % S);
+    const int cur = kt % S;
+    const uint16_t* at = a_buf(cur);
+    const uint16_t* bt = b_buf(cur);
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      s16x8 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = frag_k(at, wm * (BM2 / WM) + 32 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bf[j] = frag_k(bt, wn * (BN / WN) + 32 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma<T>(af[i], bf[j], acc[i][j]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  float* cs = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int half = 0; half < BM2 / 128; ++half) {
+    const int wr0 = wm * (BM2 / WM);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int rb = wr0 + 32 * i;
+      if (rb / 128 != half) continue;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = rb - 128 * half + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          cs[rl * (BN + 4) + wn * (BN / WN) + 32 * j + (lane & 31)] = acc[i][j][r];
+        }
     }
     __syncthreads();
-    for (int i = tid; i < 2 * BN; i += C::THREADS) {
-      const int which = i / BN, col = i % BN;
-      float acc2 = 0.f;
-      for (int r = 0; r < RP; ++r) acc2 += red[(r * 2 + which) * BN + col];
-      g.stats[((int64_t)which * tiles_m + bm) * g.kout + col0 + col] = acc2;
-    }
+    epi_chunk<T, BN, C::THREADS, 128>(g, Y, cs, row0 + 128 * half, col0, tid);
+    __syncthreads();
   }
 }
 
@@ -489,6 +710,131 @@ wgrad_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ DY, fl
       }
 }
 
+// wgrad2: the same split-pixel weight gradient with cheap operand addressing — buffer_load ...
+// lds through range-checked descriptors (out-of-range offsets zero-fill), DY offsets advanced by a
+// uniform stride per K-step, the pixel -> (image, row, col) decomposition of the X rows by
+// FastDiv (4 VALU per divide instead of ~30) — and W x W tiles per wave that feed 2 x 2 MFMAs
+// per fragment pair.  BMW x BNW output tile, 4 waves in WMW x WNW.
+template <typename T, int BMW, int BNW, int WMW, int WNW>
+__global__ void __launch_bounds__(WG_THREADS, 1)
+wgrad2_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ DY, float* __restrict__ part, Geo g,
+              int chunk, int dybytes) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  static_assert(WMW * WNW == 4, "wgrad2 runs 4 waves");
+  constexpr int TA = WG_BK * BMW, TB = WG_BK * BNW;
+  constexpr int TM = BMW / WMW / 32, TN = BNW / WNW / 32;
+  constexpr int PA = TA / 512 / 4, PB = TB / 512 / 4;  // 1-KiB DMA pieces per wave per step
+  auto a_buf = [&](int b) { return lds + b * (TA + TB); };
+  auto b_buf = [&](int b) { return lds + b * (TA + TB) + TA; };
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WNW, wn = wave % WNW;
+  const int tiles_m = g.kout / BMW, tiles_n = g.ntaps * g.c / BNW;
+  const int tile = xcd_remap(blockIdx.x, tiles_m * tiles_n), split = blockIdx.y;
+  const int bm = tile / tiles_n, bn = tile % tiles_n;
+  const int k0 = bm * BMW;
+  const int j0 = bn * BNW;
+  const int t = j0 / g.c, c0 = j0 - t * g.c;
+  const int dh = g.dh[t], dw = g.dw[t];
+  const int ohw = g.oh * g.ow;
+  const int p_begin = split * chunk;
+  const int p_end = min(g.m, p_begin + chunk);
+  const int nk = (p_end - p_begin + WG_BK - 1) / WG_BK;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)X, 0, __builtin_amdgcn_readfirstlane(g.xbytes), 0x00020000);
+  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)DY, 0, __builtin_amdgcn_readfirstlane(dybytes), 0x00020000);
+
+  constexpr int RA = 512 / BMW, RB = 512 / BNW;  // pixel rows per piece
+  // A (DY) pieces: fixed column chunk per lane, pixel row advanced by WG_BK per step
+  int arow[PA];
+  uint32_t aoff[PA];
+#pragma unroll
+  for (int i = 0; i < PA; ++i) {
+    const int piece = i * 4 + wave;
+    const int row = piece * RA + lane / (BMW / 8);
+    const int cc = (lane % (BMW / 8)) ^ (tr_swz<BMW>(row) << 2);
+    arow[i] = row;
+    aoff[i] = (uint32_t)(((p_begin + row) * g.kout + k0 + 8 * cc) * 2);
+  }
+  const uint32_t astep = (uint32_t)(WG_BK * g.kout * 2);
+  int brow[PB], bcol[PB];
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {
+    const int piece = i * 4 + wave;
+    brow[i] = piece * RB + lane / (BNW / 8);
+    bcol[i] = 8 * ((lane % (BNW / 8)) ^ (tr_swz<BNW>(brow[i]) << 2));
+  }
+
+  auto issue = [&](int kt, int buf) {
+    const int pbase = p_begin + kt * WG_BK;
+    uint16_t* adst = a_buf(buf);
+#pragma unroll
+    for (int i = 0; i < PA; ++i) {
+      const uint32_t voff = pbase + arow[i] < p_end ? aoff[i] + (uint32_t)kt * astep : 0x80000000u;
+      bdma16(dr, voff, adst + (i * 4 + wave) * 512);
+    }
+    uint16_t* bdst = b_buf(buf);
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      const int p = pbase + brow[i];
+      const int nimg = (int)fdiv((uint32_t)p, g.div_ohw), rem = p - nimg * ohw;
+      const int oy = (int)fdiv((uint32_t)rem, g.div_ow), ox = rem - oy * g.ow;
+      const int ih = oy * g.ish + dh, iw = ox * g.isw + dw;
+      const bool ok = p < p_end && (unsigned)ih < (unsigned)g.h && (unsigned)iw < (unsigned)g.w;
+      const uint32_t voff = ok ? (uint32_t)((((nimg * g.h + ih) * g.w + iw) * g.c + c0 + bcol[i]) * 2) : 0x80000000u;
+      bdma16(xr, voff, bdst + (i * 4 + wave) * 512);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  constexpr int PER_STEP = PA + PB;
+  if (nk > 0) issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_STEP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < nk) issue(kt + 2, (kt + 2) % STAGES);
+    const int cur = kt % STAGES;
+    const uint16_t* at = a_buf(cur);
+    const uint16_t* bt = b_buf(cur);
+#pragma unroll
+    for (int kk = 0; kk < WG_BK / 16; ++kk) {
+      s16x8 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = frag_t<BMW>(at, wm * (BMW / WMW) + 32 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bf[j] = frag_t<BNW>(bt, wn * (BNW / WNW) + 32 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma<T>(af[i], bf[j], acc[i][j]);
+    }
+  }
+
+  const int64_t ldp = (int64_t)g.ntaps * g.c;
+  float* dst = part + (int64_t)split * g.kout * ldp;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = k0 + wm * (BMW / WMW) + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int col = j0 + wn * (BNW / WNW) + 32 * j + (lane & 31);
+        dst[(int64_t)row * ldp + col] = acc[i][j][r];
+      }
+}
+
 // fixed-order sum of the split partials: a block owns 16 consecutive 8-element vectors and its 16
 // thread groups each sum every 16th split, folded in LDS in a fixed order (S / 16 loads per
 // thread and n / 128 blocks — one thread per vector over all S splits left the chip idle)
@@ -519,7 +865,6 @@ __global__ void __launch_bounds__(256) wgrad_reduce(const float* __restrict__ pa
 }
 
 using plan::WgPlan;
-inline WgPlan wgrad_plan(const ConvTapArgs& a, int cus) { return plan::conv_wgrad(a, cus); }
 
 }  // namespace conv
 
@@ -549,6 +894,14 @@ using FC3 = conv::FCfg<64, 4, 1, 3>;
 using FC4 = conv::FCfg<128, 4, 2, 2>;
 using FC5 = conv::FCfg<64, 8, 1, 2>;
 using FC6 = conv::FCfg<256, 2, 4, 2>;
+// fprop2 (BM, BN, WM x WN waves, stages)
+using F7 = conv::F2Cfg<256, 64, 4, 1, 3>;
+using F8 = conv::F2Cfg<256, 64, 4, 1, 2>;
+using F9 = conv::F2Cfg<256, 128, 4, 2, 2>;
+using F10 = conv::F2Cfg<128, 128, 2, 2, 3>;
+using F11 = conv::F2Cfg<128, 128, 2, 2, 2>;
+using F12 = conv::F2Cfg<256, 256, 2, 4, 2>;
+using F13 = conv::F2Cfg<128, 256, 2, 4, 2>;
 
 static int g_forced_cfg = [] {
   const char* e = std::getenv("APEX_AMD_CONV_CFG");
@@ -560,21 +913,28 @@ void conv_force_fprop_cfg(int cfg) { g_forced_cfg = cfg; }
 static int fprop_cfg(const ConvTapArgs& a, int cus) { return plan::conv_fprop_cfg(a, cus, g_forced_cfg); }
 
 int conv_tap_stats_tiles(const ConvTapArgs& a) {
-  return (int)(((int64_t)a.n * a.oh * a.ow + conv::BM - 1) / conv::BM);
+  return (int)(((int64_t)a.n * a.oh * a.ow + plan::kConvStatsRows - 1) / plan::kConvStatsRows);
 }
 
 void conv_tap_fprop(const ConvTapArgs& a, int cus, hipStream_t s) {
   if (!conv_tap_supported(a)) throw std::runtime_error("conv_tap_fprop: unsupported shape / dtype / alignment");
   const conv::Geo g = conv::make_geo(a);
-  const int64_t tiles_m = (g.m + conv::BM - 1) / conv::BM;
   const int cfg = fprop_cfg(a, cus);
   dispatch_16(a.dtype, [&](auto tag) {
     using T = typename decltype(tag)::type;
     auto go = [&](auto cfg_tag) {
       using C = decltype(cfg_tag);
+      const int64_t tiles_m = (g.m + conv::BM - 1) / conv::BM;
       const unsigned grid = (unsigned)(tiles_m * (a.kout / C::BN));
       hipLaunchKernelGGL((conv::fprop_kernel<T, C>), dim3(grid), dim3(C::THREADS), C::LDS, s, (const uint16_t*)a.in,
                          (const uint16_t*)a.wt, (uint16_t*)a.out, g);
+    };
+    auto go2 = [&](auto cfg_tag) {
+      using C = decltype(cfg_tag);
+      const int64_t tiles_m = (g.m + C::BM - 1) / C::BM;
+      const unsigned grid = (unsigned)(tiles_m * (a.kout / C::BN));
+      hipLaunchKernelGGL((conv::fprop2_kernel<T, C>), dim3(grid), dim3(C::THREADS), C::LDS, s,
+                         (const uint16_t*)a.in, (const uint16_t*)a.wt, (uint16_t*)a.out, g);
     };
     switch (cfg) {
       case 0: go(FC0{}); break;
@@ -583,7 +943,14 @@ void conv_tap_fprop(const ConvTapArgs& a, int cus, hipStream_t s) {
       case 3: go(FC3{}); break;
       case 4: go(FC4{}); break;
       case 5: go(FC5{}); break;
-      default: go(FC6{}); break;
+      case 6: go(FC6{}); break;
+      case 7: go2(F7{}); break;
+      case 8: go2(F8{}); break;
+      case 9: go2(F9{}); break;
+      case 10: go2(F10{}); break;
+      case 11: go2(F11{}); break;
+      case 12: go2(F12{}); break;
+      default: go2(F13{}); break;
     }
   }, "conv_tap_fprop");
   check_launch("conv_tap_fprop");
@@ -594,8 +961,21 @@ bool conv_wgrad_supported(const ConvTapArgs& a) {
   return a.osh == 1 && a.osw == 1 && a.oph == 0 && a.opw == 0 && a.oht == a.oh && a.owt == a.ow;
 }
 
+static int g_wgrad_variant = [] {
+  const char* e = std::getenv("APEX_AMD_WGRAD_VARIANT");
+  return e ? std::atoi(e) : -1;
+}();
+
+void conv_force_wgrad_variant(int v) { g_wgrad_variant = v; }
+
+// variant for this shape: forced (A/B) or the measured default (plan: 0 = wgrad_kernel)
+static int wgrad_variant(const ConvTapArgs& a) {
+  if (g_wgrad_variant >= 0) return plan::conv_wgrad_variant_ok(a, g_wgrad_variant) ? g_wgrad_variant : 0;
+  return 0;
+}
+
 int64_t conv_wgrad_workspace_floats(const ConvTapArgs& a, int cus) {
-  const conv::WgPlan p = conv::wgrad_plan(a, cus);
+  const conv::WgPlan p = plan::conv_wgrad(a, cus, wgrad_variant(a));
   return (int64_t)p.splits * a.kout * a.ntaps * a.c;
 }
 
@@ -604,7 +984,9 @@ void conv_wgrad(const ConvTapArgs& a, const void* dy, void* dw_out, int out_dtyp
   if (!conv_wgrad_supported(a) || !aligned16(dy) || !aligned16(dw_out) || !aligned16(ws))
     throw std::runtime_error("conv_wgrad: unsupported shape / dtype / alignment");
   const conv::Geo g = conv::make_geo(a);
-  const conv::WgPlan p = conv::wgrad_plan(a, cus);
+  const int v = wgrad_variant(a);
+  const conv::WgPlan p = plan::conv_wgrad(a, cus, v);
+  const int dybytes = (int)std::min<int64_t>((int64_t)g.m * a.kout * 2, (1ll << 31) - 1);
   dispatch_16(a.dtype, [&](auto tag) {
     using T = typename decltype(tag)::type;
     auto go = [&](auto kern, int bm, int bn) {
@@ -612,8 +994,20 @@ void conv_wgrad(const ConvTapArgs& a, const void* dy, void* dw_out, int out_dtyp
       hipLaunchKernelGGL(kern, dim3(p.tiles, p.splits), dim3(conv::WG_THREADS), lds, s, (const uint16_t*)a.in,
                          (const uint16_t*)dy, ws, g, p.chunk);
     };
-    if (p.bm == 128) go(conv::wgrad_kernel<T, 128, 128>, 128, 128);
-    else go(conv::wgrad_kernel<T, 64, 64>, 64, 64);
+    auto go2 = [&](auto kern, int bm, int bn) {
+      const size_t lds = (size_t)conv::STAGES * conv::WG_BK * (bm + bn) * 2;
+      hipLaunchKernelGGL(kern, dim3(p.tiles, p.splits), dim3(conv::WG_THREADS), lds, s, (const uint16_t*)a.in,
+                         (const uint16_t*)dy, ws, g, p.chunk, dybytes);
+    };
+    switch (v) {
+      case 1: go2(conv::wgrad2_kernel<T, 64, 64, 2, 2>, 64, 64); break;
+      case 2: go2(conv::wgrad2_kernel<T, 128, 128, 2, 2>, 128, 128); break;
+      case 3: go2(conv::wgrad2_kernel<T, 128, 64, 2, 2>, 128, 64); break;
+      case 4: go2(conv::wgrad2_kernel<T, 64, 128, 2, 2>, 64, 128); break;
+      default:
+        if (p.bm == 128) go(conv::wgrad_kernel<T, 128, 128>, 128, 128);
+        else go(conv::wgrad_kernel<T, 64, 64>, 64, 64);
+    }
   }, "conv_wgrad");
   const int64_t n = (int64_t)a.kout * a.ntaps * a.c;
   const int64_t grid = (n / 8 + 15) / 16;

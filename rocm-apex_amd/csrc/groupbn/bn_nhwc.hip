@@ -617,6 +617,14 @@ void bn_nhwc_bwd_coef_group(const float* sums, int rows, int c, const float* inv
   check_launch("bn_nhwc_bwd_coef_group");
 }
 
+void bn_nhwc_bwd_local(const float* part, int gy, int c, const float* save_invstd, float* grad_w, float* grad_b,
+                       float* payload, hipStream_t s) {
+  if (gy < 1 || c <= 0) throw std::runtime_error("bn_nhwc bwd local: bad partial rows / channels");
+  hipLaunchKernelGGL(bnh::bwd_local, dim3((c + bnh::kFinC - 1) / bnh::kFinC), dim3(256), 0, s, part, gy, c, save_invstd,
+                     grad_w, grad_b, payload);
+  check_launch("bn_nhwc_bwd_local");
+}
+
 void bn_nhwc_coef_from_stats(const float* mean, const float* v, bool is_var, const float* w, const float* b, float eps,
                              int c, float* coef_fwd, hipStream_t s) {
   hipLaunchKernelGGL(bnh::coef_from_stats, dim3((c + 255) / 256), dim3(256), 0, s, mean, v, is_var ? 1 : 0, w, b, eps,

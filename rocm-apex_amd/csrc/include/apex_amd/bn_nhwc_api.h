@@ -70,6 +70,10 @@ void bn_nhwc_stats_merge(const float* gathered, int world, int c, const float* w
 // payload rows summed in order: world after a peer all-gather, 1 after an all-reduce)
 void bn_nhwc_bwd_coef_group(const float* sums, int rows, int c, const float* inv_count, const float* save_mean,
                             const float* save_invstd, const float* w, float* coef_bwd, hipStream_t s);
+// group backward from externally computed partials [2][gy][C] (sum_dy | sum_dy_xmu rows, e.g. a
+// convolution epilogue's): the exchange payload [2C] and the LOCAL grad_w / grad_b
+void bn_nhwc_bwd_local(const float* part, int gy, int c, const float* save_invstd, float* grad_w, float* grad_b,
+                       float* payload, hipStream_t s);
 
 // dx = A * dy' + B * x + K   (dy' masked in registers when relu && !dy_is_masked)
 void bn_nhwc_bwd_apply(const void* dy, bool dy_is_masked, const void* x, int x_t, const void* z,

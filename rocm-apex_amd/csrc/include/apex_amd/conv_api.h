@@ -62,6 +62,8 @@ int conv_tap_stats_tiles(const ConvTapArgs& a);
 // (dy = `out` geometry with osh = osw = 1, oph = opw = 0; x = `in`).  fp32 result [kout][ntaps][c]
 // through split-K partials in `ws` (conv_wgrad_workspace_floats), summed in a fixed order.
 bool conv_wgrad_supported(const ConvTapArgs& a);
+// A/B hook: force one weight-gradient variant (launch_plan.h conv_wgrad; -1 = per-shape default)
+void conv_force_wgrad_variant(int v);
 int64_t conv_wgrad_workspace_floats(const ConvTapArgs& a, int cus);
 void conv_wgrad(const ConvTapArgs& a, const void* dy, void* dw_out, int out_dtype, float* ws, int cus,
                 hipStream_t s);
@@ -85,6 +87,11 @@ void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int nco
 void conv1x1_bn_finalize(const float* part, int g, int c, float n, const float* shift, const float* w, const float* b,
                          float eps, float momentum, float* rmean, float* rvar, float* save_mean, float* save_invstd,
                          float* coef, hipStream_t s);
+
+// bn_group > 1: this rank's Welford payload [mean(C) | M2(C) | n] from the partials (the group
+// exchange + csrc/groupbn stats merge replace conv1x1_bn_finalize)
+void conv1x1_bn_part_payload(const float* part, int g, int c, float n, const float* shift, float* payload,
+                             hipStream_t s);
 
 // dW [n][k] (out_dtype) = sum_m g[m][n] . pro(x[m][k]), pro = relu(x * xcoef[k] + xcoef[K + k]) when
 // xcoef is non-null; fp32 split partials in ws (conv1x1_wgrad_workspace_floats), fixed-order sum

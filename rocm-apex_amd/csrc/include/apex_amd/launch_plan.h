@@ -13,22 +13,37 @@ namespace apex_amd {
 namespace plan {
 
 // ---- implicit-GEMM convolutions (csrc/conv/conv_igemm.hip) ----
-constexpr int kConvBM = 256;   // fprop output-pixel tile
+constexpr int kConvStatsRows = 128;  // fprop output rows per BN-statistics partial row
 constexpr int kWgradBK = 64;   // wgrad pixels per K-step
 
 struct WgPlan {
   int bm, bn, tiles, splits, chunk;
 };
 
-// wgrad: (kout x ntaps*c) output tiles x pixel splits (fp32 partial per split, fixed-order reduce)
-inline WgPlan conv_wgrad(const ConvTapArgs& a, int cus) {
+// wgrad: (kout x ntaps*c) output tiles x pixel splits (fp32 partial per split, fixed-order reduce).
+// variant 0: wgrad_kernel, 128 x 128 tiles when kout and c allow, else 64 x 64; variants 1-4:
+// wgrad2_kernel (buffer-load staging) with (bm, bn) = (64, 64), (128, 128), (128, 64), (64, 128)
+constexpr int kWgradVariants = 5;
+inline bool conv_wgrad_variant_ok(const ConvTapArgs& a, int v) {
+  static const int bm[kWgradVariants] = {64, 64, 128, 128, 64}, bn[kWgradVariants] = {64, 64, 128, 64, 128};
+  if (v < 0 || v >= kWgradVariants) return false;
+  if (v == 0) return true;
+  const int64_t xb = (int64_t)a.n * a.ih * a.iw * a.c * 2, db = (int64_t)a.n * a.oh * a.ow * a.kout * 2;
+  return a.kout % bm[v] == 0 && (a.ntaps * a.c) % bn[v] == 0 && a.c % bn[v] == 0 && xb < (1ll << 31) &&
+         db < (1ll << 31);
+}
+inline WgPlan conv_wgrad(const ConvTapArgs& a, int cus, int variant = 0) {
   WgPlan p;
+  static const int vbm[kWgradVariants] = {0, 64, 128, 128, 64}, vbn[kWgradVariants] = {0, 64, 128, 64, 128};
+  if (!conv_wgrad_variant_ok(a, variant)) variant = 0;
   const bool big = a.kout % 128 == 0 && a.c % 128 == 0;
-  p.bm = big ? 128 : 64;
-  p.bn = big ? 128 : 64;
+  p.bm = variant ? vbm[variant] : (big ? 128 : 64);
+  p.bn = variant ? vbn[variant] : (big ? 128 : 64);
   p.tiles = (a.kout / p.bm) * (a.ntaps * a.c / p.bn);
   const int64_t m = (int64_t)a.n * a.oh * a.ow;
-  const int target = cus * (big ? 2 : 4);  // resident workgroups per CU (LDS ring) x two rounds
+  // resident workgroups per CU (LDS ring: 3 stages x 64 pixels x (bm + bn) x 2 B) x two rounds
+  const int per_cu = variant ? (int)(160 * 1024 / (3 * 64 * (p.bm + p.bn) * 2)) : (big ? 1 : 2);
+  const int target = cus * 2 * (per_cu < 1 ? 1 : per_cu);
   int64_t s = (target + p.tiles - 1) / p.tiles;
   const int64_t max_s = (m + 16 * kWgradBK - 1) / (16 * kWgradBK);  // >= 16 K-steps per workgroup
   if (s > max_s) s = max_s;
@@ -40,18 +55,42 @@ inline WgPlan conv_wgrad(const ConvTapArgs& a, int cus) {
   return p;
 }
 
-// fprop tile configuration index (conv_igemm.hip FC0..FC6); forced >= 0 overrides when legal.
-// Measured on MI355X (profiles/conv_cfg_sweep_r02.jsonl, ResNet-50 3x3 shapes, bs 256): the
-// 2-stage rings win; BN 256 where it still gives >= half a wave of tiles, BN 64 for <= 128
-// output channels (two workgroups per CU), BN 128 otherwise
-inline int conv_fprop_bn(int cfg) { return cfg == 6 ? 256 : (cfg % 2 == 0 ? 128 : 64); }
+// fprop tile configurations (conv_igemm.hip): 0-6 = fprop_kernel (BM 256; the < 2 GiB-or-larger
+// fallback), 7-13 = fprop2_kernel (buffer-load staging, 64 x 64+ per wave).  (BM, BN) per index:
+constexpr int kConvCfgs = 14;
+inline int conv_fprop_bm(int cfg) {
+  static const int bm[kConvCfgs] = {256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 128, 128, 256, 128};
+  return cfg >= 0 && cfg < kConvCfgs ? bm[cfg] : 256;
+}
+inline int conv_fprop_bn(int cfg) {
+  static const int bn[kConvCfgs] = {128, 64, 128, 64, 128, 64, 256, 64, 64, 128, 128, 128, 256, 256};
+  return cfg >= 0 && cfg < kConvCfgs ? bn[cfg] : 64;
+}
+// fprop2 needs the input / weight byte ranges to fit a buffer descriptor (< 2 GiB)
+inline bool conv_fprop2_ok(const ConvTapArgs& a) {
+  const int64_t xb = (int64_t)a.n * a.ih * a.iw * a.c * 2, wb = (int64_t)a.kout * a.ntaps * a.c * 2;
+  return xb < (1ll << 31) && wb < (1ll << 31);
+}
+// forced >= 0 overrides when legal.  Defaults: fprop2 per output width (r04 sweep,
+// profiles/conv_cfg_sweep_r04.jsonl); fprop_kernel for > 2 GiB operands (r02 sweep choice)
 inline int conv_fprop_cfg(const ConvTapArgs& a, int cus, int forced) {
-  const int64_t tiles_m = ((int64_t)a.n * a.oh * a.ow + kConvBM - 1) / kConvBM;
-  auto ok = [&](int bn) { return a.kout % bn == 0; };
-  if (forced >= 0 && forced <= 6 && ok(conv_fprop_bn(forced))) return forced;
+  auto ok = [&](int cfg) {
+    return a.kout % conv_fprop_bn(cfg) == 0 && (cfg < 7 || conv_fprop2_ok(a));
+  };
+  if (forced >= 0 && forced < kConvCfgs && ok(forced)) return forced;
+  const int64_t m = (int64_t)a.n * a.oh * a.ow;
+  auto tiles = [&](int cfg) {
+    return (m + conv_fprop_bm(cfg) - 1) / conv_fprop_bm(cfg) * (a.kout / conv_fprop_bn(cfg));
+  };
+  if (conv_fprop2_ok(a)) {
+    if (a.kout % 128) return 8;
+    if (a.kout % 256 == 0 && tiles(13) >= 2 * cus) return 13;
+    return 11;
+  }
+  const int64_t tiles_m = (m + 255) / 256;
   if (a.kout <= 128) return 5;
-  if (ok(256) && tiles_m * (a.kout / 256) >= cus / 2) return 6;
-  return ok(128) ? 4 : 5;
+  if (a.kout % 256 == 0 && tiles_m * (a.kout / 256) >= cus / 2) return 6;
+  return a.kout % 128 == 0 ? 4 : 5;
 }
 
 // ---- GEMM (csrc/gemm/gemm_mfma.hip, 256 x 256 x 64 tiles) ----

@@ -144,6 +144,19 @@ class Bottleneck(nn.Module):
         return self.relu(out + identity)
 
 
+def run_linked(blocks, x):
+    """Run consecutive fused-BN blocks as chained bottleneck nodes: block i hands block i+1 its
+    output BN's state (ops/bottleneck_bn.py BlockLink), so block i+1's conv1 data gradient does
+    block i's bn3 backward reduction.  Blocks off the node path run unlinked."""
+    link = None
+    for blk in blocks:
+        if isinstance(blk, Bottleneck):
+            x, link = blk.forward_linked(x, link)
+        else:
+            x, link = blk(x), None
+    return x
+
+
 def _has_hooks(layers):
     from torch.nn.modules import module as _m
 
@@ -234,13 +247,7 @@ class ResNet(nn.Module):
                 for layer in layers:
                     x = layer(x)
             else:
-                link = None
-                for layer in layers:
-                    for blk in layer:
-                        if isinstance(blk, Bottleneck):
-                            x, link = blk.forward_linked(x, link)
-                        else:
-                            x, link = blk(x), None
+                x = run_linked([blk for layer in layers for blk in layer], x)
         else:
             x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
             x = self.layer4(self.layer3(self.layer2(self.layer1(x))))

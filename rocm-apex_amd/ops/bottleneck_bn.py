@@ -27,6 +27,10 @@ scale-bias-ReLU-conv graphs with BN statistics) and groupbn's NHWC BN; the compo
 gfx950-specific: the 1x1 convs of stages 1-2 are HBM-bound (26 GFLOP vs 0.25-0.5 GB each), so
 every fused pass saved is time saved.
 
+SyncBatchNorm (``bn_group > 1``, e.g. ``bench.py --sync-bn``): every BN of the node reduces its
+statistics and backward sums over its group — one exchange per BN and direction, xGMI peer
+memory or RCCL (``finalize_part`` / ``stats_pass`` / ``bwd_*``), so the fusions stay on.
+
 ``APEX_AMD_FUSED_BLOCK=0`` disables the block node (the per-module fused path runs instead).
 """
 import os
@@ -78,13 +82,89 @@ class BlockLink:
 
 
 class _BN:
-    """Per-BN constants of one forward: fp32 affine params, running buffers, momentum / eps."""
+    """Per-BN constants of one forward: fp32 affine params, running buffers, momentum / eps, and
+    the process group its statistics are reduced over (None: this rank's batch only)."""
 
-    __slots__ = ("w", "b", "rm", "rv", "mom", "eps")
+    __slots__ = ("w", "b", "rm", "rv", "mom", "eps", "group")
 
     def __init__(self, bn):
         self.w, self.b, self.rm, self.rv = bn.weight, bn.bias, bn.running_mean, bn.running_var
         self.mom, self.eps = float(bn.momentum), float(bn.eps)
+        self.group = _Group(bn.process_group) if getattr(bn, "bn_group", 1) > 1 else None
+
+
+class _Group:
+    """Marks a synchronized BN: ``pg`` is the process group its statistics reduce over (None =
+    the default group, as for torch SyncBatchNorm)."""
+
+    __slots__ = ("pg",)
+
+    def __init__(self, pg):
+        self.pg = pg
+
+
+# ---- batch statistics, local or synchronized over the BN's group (SyncBatchNorm, bn_group > 1) --
+# Synchronized: each rank turns its partial sums into a Welford payload [mean | M2 | count], ONE
+# exchange per BN gathers the group's payloads (xGMI peer memory, else an RCCL all-gather:
+# contrib.groupbn._exchange_gather) and every member merges the same block in rank order, so all
+# ranks hold bit-identical statistics (reference: optimized_sync_batchnorm_kernel.py:39 all_gather
+# of [mean, var, count]).  Backward: [sum_dy | sum_dy_xmu] of every BN summed over the group
+# (:104 all_reduce) before the dx coefficients; weight / bias gradients stay local (DDP averages).
+def _exchange_gather(payload, group):
+    from ..contrib.groupbn.batch_norm import _exchange_gather as ex
+
+    return ex(payload, group)
+
+
+def _exchange_sum(payload, group):
+    from ..contrib.groupbn.batch_norm import _exchange_sum as ex
+
+    return ex(payload, group)
+
+
+def finalize_part(part, n, bn):
+    """(save_mean, save_invstd, coef [2C], inv_count or None) from [2, G, C] partials about bn.rm."""
+    if bn.group is None:
+        sm, si, coef = _conv().bn_finalize(part, n, bn.rm, bn.w, bn.b, bn.rm, bn.rv, bn.eps, bn.mom)
+        return sm, si, coef, None
+    gathered = _exchange_gather(_conv().part_payload(part, n, bn.rm), bn.group.pg)
+    sm, si, coef, inv_n = _bn().stats_group_merge(gathered, bn.w, bn.b, bn.rm, bn.rv, bn.mom, bn.eps)
+    return sm, si, coef, inv_n
+
+
+def stats_pass(y2, bn):
+    """Statistics of y2 [M, C] in a pass of their own (off the epilogue-statistics conv routes)."""
+    if bn.group is None:
+        sm, si, coef = _bn().stats(y2, bn.w, bn.b, bn.rm, bn.rv, bn.mom, bn.eps)
+        return sm, si, coef.view(-1), None
+    gathered = _exchange_gather(_bn().fwd_group_local(y2), bn.group.pg)
+    sm, si, coef, inv_n = _bn().stats_group_merge(gathered, bn.w, bn.b, bn.rm, bn.rv, bn.mom, bn.eps)
+    return sm, si, coef, inv_n
+
+
+def bwd_from_part(part, n, sm, si, w, group, inv_n):
+    """(coef_bwd [3C], grad_w, grad_b) from [2, G, C] backward-reduction partials."""
+    if group is None:
+        return _conv().bnbwd_finalize(part, n, sm, si, w)
+    payload, gw, gb = _bn().bwd_part_local(part, si)
+    return _bn().bwd_group_coef(_exchange_sum(payload, group.pg), inv_n, sm, si, w), gw, gb
+
+
+def bwd_reduce(dy, x, w, sm, si, coef, relu, bits, group, inv_n):
+    """(dy_masked, coef_bwd, grad_w, grad_b): the reduction half of the BN backward."""
+    if group is None:
+        return _bn().bwd_reduce(dy, x, w, sm, si, coef, relu, bits)
+    payload, gw, gb, dym = _bn().bwd_group_local(dy, x, None, w, sm, si, coef, relu, None, bits)
+    return dym, _bn().bwd_group_coef(_exchange_sum(payload, group.pg), inv_n, sm, si, w), gw, gb
+
+
+def bwd_full(dy, x, w, sm, si, coef, relu, group, inv_n):
+    """(dx, grad_w, grad_b): reduction + dx pass."""
+    if group is None:
+        dx, _, gw, gb = _bn().bwd(dy, x, None, w, sm, si, coef, relu, False)
+        return dx, gw, gb
+    payload, gw, gb, dym = _bn().bwd_group_local(dy, x, None, w, sm, si, coef, relu)
+    return _bn().bwd_group_finish(dym, x, _exchange_sum(payload, group.pg), inv_n, w, sm, si, coef), gw, gb
 
 
 # ---- 1x1 stride-1 convolution pieces ---------------------------------------------------------
@@ -113,26 +193,18 @@ def _red_native(m, kout, cin):
     return kout in _NATIVE_K and cin % 64 == 0 and cin <= 512 and m >= 100000
 
 
-def _wgrad_native(m, n, k, pro):
-    # the split-M kernel with cost-based tiles runs 4.4-5.1 TB/s at the 56x56 shapes and leads
-    # MIOpen's wgrad at every ResNet-50 1x1 shape (1.2-1.8x, profiles/bn1x1_wgrad_r03b.jsonl)
-    return True
-
-
 def conv1x1_bn_fwd(a2, w2d, pcoef, bn):
-    """y = pro(a) . W^T and the consuming BN's (save_mean, save_invstd, coef).  pro = relu(a *
-    pcoef[:K] + pcoef[K:]) when ``pcoef`` is given (the producing BN's apply + ReLU)."""
+    """y = pro(a) . W^T and the consuming BN's (save_mean, save_invstd, coef, inv_count).  pro =
+    relu(a * pcoef[:K] + pcoef[K:]) when ``pcoef`` is given (the producing BN's apply + ReLU)."""
     m, k = a2.shape
     n = w2d.size(0)
     if _fwd_native(m, k, n):
         y2, part, _ = _conv().bn1x1(a2, w2d, False, pcoef, bn.rm, True)
-        sm, si, coef = _conv().bn_finalize(part, float(m), bn.rm, bn.w, bn.b, bn.rm, bn.rv, bn.eps, bn.mom)
-        return y2, sm, si, coef
+        return (y2,) + finalize_part(part, float(m), bn)
     if pcoef is not None:
         a2 = _bn().apply(a2, None, pcoef, True)[0]
     y2 = torch.matmul(a2, w2d.t())
-    sm, si, coef = _bn().stats(y2, bn.w, bn.b, bn.rm, bn.rv, bn.mom, bn.eps)
-    return y2, sm, si, coef.view(-1)
+    return (y2,) + stats_pass(y2, bn)
 
 
 def conv1x1_dgrad(g2, w2d, add2=None, add_inplace=False):
@@ -147,15 +219,11 @@ def conv1x1_dgrad(g2, w2d, add2=None, add_inplace=False):
     return torch.matmul(g2, w2d)
 
 
-def conv1x1_wgrad(g2, x2, xcoef, w, n_h_w):
+def conv1x1_wgrad(g2, x2, xcoef, w):
     """dW [Cout, Cin, 1, 1] = g^T . pro(x), pro = the producing BN's apply + ReLU when ``xcoef``."""
-    m = g2.size(0)
-    if _wgrad_native(m, g2.size(1), x2.size(1), xcoef is not None):
-        return _conv().wgrad1x1(g2, x2, xcoef, w.dtype).view_as(w)
-    n, h, wd = n_h_w
-    gy, x = _nchw(g2, n, h, wd), _nchw(x2, n, h, wd)
-    return torch.ops.aten.convolution_backward(gy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
-                                               [False, True, False])[1]
+    # the split-M kernel with cost-based tiles runs 4.4-5.1 TB/s at the 56x56 shapes and leads
+    # MIOpen's wgrad at every ResNet-50 1x1 shape (1.2-1.8x, profiles/bn1x1_wgrad_r03b.jsonl)
+    return _conv().wgrad1x1(g2, x2, xcoef, w.dtype).view_as(w)
 
 
 # ---- 3x3 / strided convolutions (ops/conv.py routes) -----------------------------------------
@@ -183,7 +251,7 @@ class _BottleneckFn(torch.autograd.Function):
         cout = w3.size(0)
         x2 = _m2(x)
         # conv1 (+ bn1 statistics) -> bn1 apply + ReLU
-        y1, sm1, si1, c1 = conv1x1_bn_fwd(x2, w1.view(width, cin), None, bn1)
+        y1, sm1, si1, c1, in1 = conv1x1_bn_fwd(x2, w1.view(width, cin), None, bn1)
         z1 = _bn().apply(y1, None, c1, True)[0]
         # conv2 (3x3, stride) -> bn2 statistics (in the native conv's epilogue where it runs)
         z1v = _nchw(z1, n, h, wd)
@@ -191,31 +259,29 @@ class _BottleneckFn(torch.autograd.Function):
             y2, part2 = convops.conv_tap_forward(z1v, w2, stride, 1, stats_shift=bn2.rm)
             oh, ow = y2.shape[2], y2.shape[3]
             y2m = _m2(y2)
-            sm2, si2, c2 = _conv().bn_finalize(part2, float(y2m.size(0)), bn2.rm, bn2.w, bn2.b, bn2.rm, bn2.rv,
-                                               bn2.eps, bn2.mom)
+            sm2, si2, c2, in2 = finalize_part(part2, float(y2m.size(0)), bn2)
         else:
             y2 = F.conv2d(z1v, w2, None, stride, 1)
             oh, ow = y2.shape[2], y2.shape[3]
             y2m = _m2(y2)
-            sm2, si2, c2 = _bn().stats(y2m, bn2.w, bn2.b, bn2.rm, bn2.rv, bn2.mom, bn2.eps)
-            c2 = c2.view(-1)
+            sm2, si2, c2, in2 = stats_pass(y2m, bn2)
         # conv3 with bn2's apply + ReLU on its operand load (+ bn3 statistics)
-        y3, sm3, si3, c3 = conv1x1_bn_fwd(y2m, w3.view(cout, width), c2, bn3)
+        y3, sm3, si3, c3, in3 = conv1x1_bn_fwd(y2m, w3.view(cout, width), c2, bn3)
         if wds is None:
             out2, bits = _bn().apply(y3, x2, c3, True, True)
-            yd = smd = sid = cd = None
+            yd = smd = sid = cd = ind = None
         else:
             if stride == 1:
-                yd, smd, sid, cd = conv1x1_bn_fwd(x2, wds.view(cout, cin), None, bnd)
+                yd, smd, sid, cd, ind = conv1x1_bn_fwd(x2, wds.view(cout, cin), None, bnd)
             else:
                 yd = _m2(_conv_fwd(x, wds, stride, 0))
-                smd, sid, cd = _bn().stats(yd, bnd.w, bnd.b, bnd.rm, bnd.rv, bnd.mom, bnd.eps)
-                cd = cd.view(-1)
+                smd, sid, cd, ind = stats_pass(yd, bnd)
             out2, bits = _bn().apply(y3, yd, c3, True, True, cd)
         ctx.save_for_backward(x, w1, w2, w3, wds, g1, g2, g3, gds, y1, z1, y2m, y3, yd, bits,
-                              sm1, si1, c1, sm2, si2, c2, sm3, si3, c3, smd, sid, cd)
+                              sm1, si1, c1, sm2, si2, c2, sm3, si3, c3, smd, sid, cd, in1, in2, in3, ind)
         ctx.geo = (n, h, wd, oh, ow, stride)
         ctx.links = (link_in, link_out)
+        ctx.groups = (bn1.group, bn2.group, bn3.group, bnd.group if bnd is not None else None)
         if link_out is not None:
             link_out.y3, link_out.bits, link_out.mean, link_out.invstd = y3, bits, sm3, si3
         return _nchw(out2, n, oh, ow)
@@ -223,8 +289,9 @@ class _BottleneckFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         (x, w1, w2, w3, wds, g1, g2, g3, gds, y1, z1, y2m, y3, yd, bits,
-         sm1, si1, c1, sm2, si2, c2, sm3, si3, c3, smd, sid, cd) = ctx.saved_tensors
+         sm1, si1, c1, sm2, si2, c2, sm3, si3, c3, smd, sid, cd, in1, in2, in3, ind) = ctx.saved_tensors
         n, h, wd, oh, ow, stride = ctx.geo
+        gr1, gr2, gr3, grd = ctx.groups
         bn = _bn()
         width, cin, cout = w1.size(0), w1.size(1), w3.size(0)
         gout = gout.contiguous(memory_format=torch.channels_last)
@@ -237,10 +304,10 @@ class _BottleneckFn(torch.autograd.Function):
         # weight gradient) where that kernel takes the shape
         if link_out is not None and link_out.part is not None:
             dm = go2
-            cb3, gg3, gb3 = _conv().bnbwd_finalize(link_out.part, float(go2.size(0)), sm3, si3, g3)
+            cb3, gg3, gb3 = bwd_from_part(link_out.part, float(go2.size(0)), sm3, si3, g3, gr3, in3)
             link_out.part = None
         else:
-            dm, cb3, gg3, gb3 = bn.bwd_reduce(go2, y3, g3, sm3, si3, c3, True, bits)
+            dm, cb3, gg3, gb3 = bwd_reduce(go2, y3, g3, sm3, si3, c3, True, bits, gr3, in3)
         w3m = w3.view(cout, width)
         if _dgrad_native(dm.size(0), cout, width) and width == 64:
             # conv3 dgrad with bn3's dx as the operand prologue (dx3 written for the wgrad) AND
@@ -249,30 +316,23 @@ class _BottleneckFn(torch.autograd.Function):
             # profiles/resnet50_node_r03e.md)
             dz2, part2, dx3 = _conv().dgrad_bnred(dm, w3m, None, None, y2m, sm2, coef=c2, py=y3,
                                                   pcoef=cb3.view(-1), want_aout=True)
-            cb2, gg2, gb2 = _conv().bnbwd_finalize(part2, float(dm.size(0)), sm2, si2, g2)
+            cb2, gg2, gb2 = bwd_from_part(part2, float(dm.size(0)), sm2, si2, g2, gr2, in2)
             dy2 = bn.bwd_apply(dz2, y2m, c2, cb2)
         elif _dgrad_native(dm.size(0), cout, width):
             dz2, _, dx3 = _conv().bn1x1(dm, w3m, True, cb3.view(-1), None, False, None, y3, True)
-            dy2, _, gg2, gb2 = bn.bwd(dz2, y2m, None, g2, sm2, si2, c2, True, False)
+            dy2, gg2, gb2 = bwd_full(dz2, y2m, g2, sm2, si2, c2, True, gr2, in2)
         else:
             dx3 = bn.bwd_apply(dm, y3, c3, cb3)
             dz2 = conv1x1_dgrad(dx3, w3m)
-            dy2, _, gg2, gb2 = bn.bwd(dz2, y2m, None, g2, sm2, si2, c2, True, False)
+            dy2, gg2, gb2 = bwd_full(dz2, y2m, g2, sm2, si2, c2, True, gr2, in2)
         # conv3 weight gradient with bn2's apply + ReLU recomputed on the operand load
-        dw3 = conv1x1_wgrad(dx3, y2m, c2, w3, (n, oh, ow))
+        dw3 = conv1x1_wgrad(dx3, y2m, c2, w3)
         # conv2
         dz1, dw2 = _conv_bwd(_nchw(dy2, n, oh, ow), _nchw(z1, n, h, wd), w2, stride, 1)
         dz1 = _m2(dz1.contiguous(memory_format=torch.channels_last))
-        # bn1: the reduction here; its dx pass runs as conv1's dgrad operand prologue where that
-        # kernel takes it (stage 1), else as a pass of its own
-        linked = link_in is not None and link_in.bits is not None and _red_native(dz1.size(0), width, cin)
-        # (bn1's dx as conv1's dgrad prologue moves the same bytes — the reduction then has to
-        # write the masked gradient — and measured slower: off)
-        pro1 = False
-        if pro1:
-            dz1m, cb1, gg1, gb1 = bn.bwd_reduce(dz1, y1, g1, sm1, si1, c1, True, None)
-        else:
-            dy1, _, gg1, gb1 = bn.bwd(dz1, y1, None, g1, sm1, si1, c1, True, False)
+        # bn1: reduction + dx pass (as conv1's dgrad operand prologue it moved the same bytes —
+        # the reduction then has to write the masked gradient — and measured slower)
+        dy1, gg1, gb1 = bwd_full(dz1, y1, g1, sm1, si1, c1, True, gr1, in1)
         # shortcut gradient, then conv1's data gradient summed onto it
         dwd = ggd = gbd = None
         if wds is None:
@@ -282,31 +342,27 @@ class _BottleneckFn(torch.autograd.Function):
             short_tmp = dm is not go2
         else:
             short_tmp = True
-            dyd, _, ggd, gbd = bn.bwd(dm, yd, None, gds, smd, sid, cd, False, False)
+            dyd, ggd, gbd = bwd_full(dm, yd, gds, smd, sid, cd, False, grd, ind)
             if stride == 1:
                 short = conv1x1_dgrad(dyd, wds.view(cout, cin))
-                dwd = conv1x1_wgrad(dyd, x2, None, wds, (n, h, wd))
+                dwd = conv1x1_wgrad(dyd, x2, None, wds)
             else:
                 dxd, dwd = _conv_bwd(_nchw(dyd, n, oh, ow), x, wds, stride, 0)
                 short = _m2(dxd.contiguous(memory_format=torch.channels_last))
-        if pro1:
-            # bn1's dx as the operand prologue (dy1 written for the wgrad) + the block below's
-            # ReLU mask and bn3 backward reduction in the epilogue
-            dx, link_in.part, dy1 = _conv().dgrad_bnred(dz1m, w1.view(width, cin), short, link_in.bits,
-                                                        link_in.y3, link_in.mean, py=y1, pcoef=cb1.view(-1),
-                                                        want_aout=True)
-        elif linked:
+        if link_in is not None and link_in.bits is not None and _red_native(dz1.size(0), width, cin):
             # mask with the block below's ReLU bits + its bn3 backward reduction, in this kernel
             dx, link_in.part, _ = _conv().dgrad_bnred(dy1, w1.view(width, cin), short, link_in.bits, link_in.y3,
                                                       link_in.mean)
         else:
             dx = conv1x1_dgrad(dy1, w1.view(width, cin), short, short_tmp)
-        dw1 = conv1x1_wgrad(dy1, x2, None, w1, (n, h, wd))
+        dw1 = conv1x1_wgrad(dy1, x2, None, w1)
         return (_nchw(dx, n, h, wd), dw1, dw2, dw3, dwd, gg1, gb1, gg2, gb2, gg3, gb3, ggd, gbd, None)
 
 
 def _bn_ok(bn):
-    return (bn.training and bn.track_running_stats and bn.bn_group == 1 and bn.weight is not None
+    # any bn_group: with bn_group > 1 (SyncBatchNorm over bn.process_group) the statistics and
+    # backward sums are exchanged per BN (finalize_part / stats_pass / bwd_* above)
+    return (bn.training and bn.track_running_stats and bn.weight is not None
             and bn.weight.dtype == torch.float32 and bn.momentum is not None and bn.running_mean is not None)
 
 
@@ -334,9 +390,14 @@ def block_supported(block, x):
     return all(c % 64 == 0 for c in chans)
 
 
+# forward calls of the node since import (bench.py reports nodes per step)
+NODE_CALLS = [0]
+
+
 def bottleneck_forward(block, x, link_in=None, link_out=None):
     """Run ``block`` as one node.  ``link_in``: the BlockLink the block below filled (its output
     is ``x`` and feeds nothing else); ``link_out``: a fresh BlockLink for the block above."""
+    NODE_CALLS[0] += 1
     ds = block.downsample
     stride = block.conv2.stride[0]
     if ds is not None and ds[0].stride[0] != stride:

@@ -86,3 +86,86 @@ def test_gpu_conv2d_nhwc_module_autograd():
     _close(y, yr, 2e-2)
     _close(x.grad, xr.grad, 2e-2)
     _close(m.weight.grad, ref.weight.grad, 2e-2)
+
+
+CFG_SHAPES = [
+    # cin, cout, stride, h, batch: ragged M (not a multiple of 128 / 256), both strides, every
+    # output width the configurations tile (64 / 128 / 256 / 512)
+    (64, 64, 1, 11, 3),
+    (64, 128, 2, 13, 2),
+    (128, 256, 1, 9, 3),
+    (256, 512, 2, 10, 2),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", list(range(14)))
+@pytest.mark.parametrize("cin,cout,stride,h,batch", CFG_SHAPES)
+def test_gpu_conv_tap_every_tile_config(cfg, cin, cout, stride, h, batch):
+    """Every fprop tile configuration (0-6 fprop_kernel, 7-13 fprop2_kernel: buffer-load staging
+    with out-of-range zero fill) forced on ragged shapes: forward + BN statistics epilogue, the
+    stride-1 / per-phase stride-2 data gradient (phase-shifted output placement), and the fused
+    scale / bias / residual / ReLU epilogue, against fp32 torch."""
+    from apex import _native
+    from apex.ops import conv as C
+
+    ext = _native.require("conv").conv
+    bn = [128, 64, 128, 64, 128, 64, 256, 64, 64, 128, 128, 128, 256, 256][cfg]
+    if cout % bn:
+        pytest.skip("tile wider than the output")
+    torch.manual_seed(cfg * 7 + cin)
+    x = (torch.randn(batch, cin, h, h, device="cuda") + 0.2).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    w = (torch.randn(cout, cin, 3, 3, device="cuda") * 0.05).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    shift = torch.randn(cout, device="cuda") * 0.1
+    C._conv_ext().force_fprop_cfg(cfg)
+    try:
+        y, part = C.conv_tap_forward(x, w, stride, 1, stats_shift=shift)
+        yr = F.conv2d(x.float(), w.float(), None, stride, 1)
+        _close(y, yr, 1e-2)
+        y2 = yr.permute(0, 2, 3, 1).reshape(-1, cout)
+        sm, si, _ = ext.bn_finalize(part, float(y2.size(0)), shift, None, None, None, None, 1e-5, 0.1)
+        torch.testing.assert_close(sm, y2.mean(0), atol=3e-3 * float(y2.std()), rtol=2e-3)
+        torch.testing.assert_close(si, torch.rsqrt(y2.var(0, unbiased=False) + 1e-5), atol=0, rtol=5e-3)
+        # data gradient (its launches run the same fprop kernels with the flipped weight; the
+        # stride-2 one places each phase's output with osh = osw = 2)
+        if cin % bn == 0:
+            gy = torch.randn_like(yr).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            xr = x.float().requires_grad_(True)
+            torch.autograd.backward(F.conv2d(xr, w.float(), None, stride, 1), gy.float())
+            dx = C.conv_tap_dgrad(gy, w, x.shape, stride, 1)
+            _close(dx, xr.grad, 2e-2)
+        # fused frozen-BN epilogue: relu(conv * scale + bias + residual)
+        if stride == 1:
+            sc = torch.rand(cout, device="cuda") + 0.5
+            bi = torch.randn(cout, device="cuda") * 0.2
+            res = torch.randn_like(yr).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            out = C.conv_bn_act(x, w, sc, bi, res, True, 1, 1)
+            ref = torch.relu(yr * sc.view(1, -1, 1, 1) + bi.view(1, -1, 1, 1) + res.float())
+            _close(out, ref, 2e-2)
+    finally:
+        C._conv_ext().force_fprop_cfg(-1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", list(range(5)))
+@pytest.mark.parametrize("cin,cout,stride,h,batch", CFG_SHAPES + [(128, 128, 1, 7, 5)])
+def test_gpu_conv_wgrad_every_variant(variant, cin, cout, stride, h, batch):
+    """Every weight-gradient variant (0 wgrad_kernel, 1-4 wgrad2_kernel tiles) forced on ragged
+    pixel counts (partial K-steps, zero-filled padding taps) against the fp32 torch gradient."""
+    from apex.ops import conv as C
+
+    torch.manual_seed(variant * 11 + cin)
+    x = torch.randn(batch, cin, h, h, device="cuda").to(torch.bfloat16).to(memory_format=torch.channels_last)
+    w = torch.randn(cout, cin, 3, 3, device="cuda").to(torch.bfloat16).to(memory_format=torch.channels_last)
+    ho = (h + 2 - 3) // stride + 1
+    gy = torch.randn(batch, cout, ho, ho, device="cuda").to(torch.bfloat16).to(memory_format=torch.channels_last)
+    wr = w.float().requires_grad_(True)
+    torch.autograd.backward(F.conv2d(x.float(), wr, None, stride, 1), gy.float())
+    C._conv_ext().force_wgrad_variant(variant)
+    try:
+        dw = C.conv_tap_wgrad(gy, x, w.shape, stride, 1, torch.float32)
+        dwb = C.conv_tap_wgrad(gy, x, w.shape, stride, 1, torch.bfloat16)
+    finally:
+        C._conv_ext().force_wgrad_variant(-1)
+    _close(dw, wr.grad, 5e-3)
+    _close(dwb, wr.grad, 2e-2)

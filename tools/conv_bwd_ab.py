@@ -98,9 +98,20 @@ def main():
         fns = {
             "miopen": lambda: torch.ops.aten.convolution_backward(gy, x, w, None, [st, st], [1, 1], [1, 1], False,
                                                                   [0, 0], 1, [False, True, False]),
-            "native": lambda: conv_ops.conv_tap_wgrad(gy, x, w.shape, st, 1, w.dtype),
             "native_gather": lambda: ext.wgrad3x3(gy.permute(0, 2, 3, 1), x.permute(0, 2, 3, 1), st),
         }
+
+        def variant(v):
+            def f():
+                ext.force_wgrad_variant(v)
+                try:
+                    return conv_ops.conv_tap_wgrad(gy, x, w.shape, st, 1, w.dtype)
+                finally:
+                    ext.force_wgrad_variant(-1)
+            return f
+
+        for v in range(5):  # 0 wgrad_kernel, 1-4 wgrad2_kernel tiles (launch_plan.h conv_wgrad)
+            fns[f"native_v{v}"] = variant(v)
         res = {kk: [] for kk in fns}
         for _ in range(args.rounds):
             for kk, fn in fns.items():

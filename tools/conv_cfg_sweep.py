@@ -23,12 +23,12 @@ def main():
     ext = C._conv_ext()
     B = int(os.environ.get("BATCH", "256"))
     for cin, cout, k, st, h, cnt in SHAPES:
-        if k != 3 or cin % 64:
+        if not (k == 3 or (k == 1 and st == 2)) or cin % 64:
             continue
-        pad = 1
-        ho = (h + 2 - 3) // st + 1
+        pad = k // 2
+        ho = (h + 2 * pad - k) // st + 1
         x = torch.randn(B, cin, h, h, device="cuda", dtype=torch.bfloat16).to(memory_format=torch.channels_last)
-        w = (torch.randn(cout, cin, 3, 3, device="cuda", dtype=torch.bfloat16) * 0.05).to(
+        w = (torch.randn(cout, cin, k, k, device="cuda", dtype=torch.bfloat16) * 0.05).to(
             memory_format=torch.channels_last)
         gy = torch.randn(B, cout, ho, ho, device="cuda", dtype=torch.bfloat16).to(memory_format=torch.channels_last)
         args = ([st, st], [pad, pad], [1, 1], False, [0, 0], 1)
@@ -37,7 +37,10 @@ def main():
              "miopen_fwd_us": round(timeit(lambda: F.conv2d(x, w, None, st, pad)) * 1e6, 1),
              "miopen_dgrad_us": round(timeit(lambda: torch.ops.aten.convolution_backward(
                  gy, x, w, None, *args, [True, False, False])) * 1e6, 1)}
-        for cfg in range(7):
+        for cfg in range(14):
+            bn = [128, 64, 128, 64, 128, 64, 256, 64, 64, 128, 128, 128, 256, 256][cfg]
+            if cout % bn:
+                continue
             ext.force_fprop_cfg(cfg)
             y = C.conv_tap_forward(x, w, st, pad).float()
             err = float((y - ref_f).abs().max()) / max(1.0, float(ref_f.abs().max()))

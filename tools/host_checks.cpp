@@ -53,22 +53,26 @@ void check_conv() {
       const apex_amd::ConvTapArgs a = conv_args(n, s.h, s.h, s.c, s.kout, s.k, s.stride);
       const int64_t m = (int64_t)a.n * a.oh * a.ow;
       // fprop: every forced or chosen tile width divides kout, the grid fits the launch's unsigned x
-      for (int forced = -1; forced <= 7; ++forced) {
+      for (int forced = -1; forced <= plan::kConvCfgs; ++forced) {
         const int cfg = plan::conv_fprop_cfg(a, cus, forced);
-        const int bn = plan::conv_fprop_bn(cfg);
-        CHECK(cfg >= 0 && cfg <= 6 && a.kout % bn == 0, "cfg %d kout %d", cfg, a.kout);
-        const int64_t grid = (m + plan::kConvBM - 1) / plan::kConvBM * (a.kout / bn);
+        const int bn = plan::conv_fprop_bn(cfg), bm = plan::conv_fprop_bm(cfg);
+        CHECK(cfg >= 0 && cfg < plan::kConvCfgs && a.kout % bn == 0, "cfg %d kout %d", cfg, a.kout);
+        CHECK(cfg < 7 || plan::conv_fprop2_ok(a), "fprop2 cfg %d with > 2 GiB operands", cfg);
+        const int64_t grid = (m + bm - 1) / bm * (a.kout / bn);
         CHECK(grid > 0 && grid < (1ll << 32), "grid %lld", (long long)grid);
       }
       // wgrad: the pixel splits cover [0, m) exactly once, chunks are whole K-steps, every split
       // has work, the output tiling covers kout x ntaps*c
-      const plan::WgPlan p = plan::conv_wgrad(a, cus);
-      CHECK(p.chunk % plan::kWgradBK == 0 && p.chunk > 0, "chunk %d", p.chunk);
-      CHECK((int64_t)p.splits * p.chunk >= m && (int64_t)(p.splits - 1) * p.chunk < m,
-            "splits %d chunk %d m %lld", p.splits, p.chunk, (long long)m);
-      CHECK(a.kout % p.bm == 0 && (a.ntaps * a.c) % p.bn == 0, "tile %dx%d", p.bm, p.bn);
-      CHECK(p.tiles == (a.kout / p.bm) * (a.ntaps * a.c / p.bn), "tiles %d", p.tiles);
-      CHECK((int64_t)p.splits * a.kout * a.ntaps * a.c < (1ll << 40), "workspace");
+      for (int v = 0; v < plan::kWgradVariants; ++v) {
+        const plan::WgPlan p = plan::conv_wgrad(a, cus, v);
+        CHECK(p.chunk % plan::kWgradBK == 0 && p.chunk > 0, "chunk %d", p.chunk);
+        CHECK((int64_t)p.splits * p.chunk >= m && (int64_t)(p.splits - 1) * p.chunk < m,
+              "splits %d chunk %d m %lld", p.splits, p.chunk, (long long)m);
+        CHECK(a.kout % p.bm == 0 && (a.ntaps * a.c) % p.bn == 0, "tile %dx%d", p.bm, p.bn);
+        CHECK(p.tiles == (a.kout / p.bm) * (a.ntaps * a.c / p.bn), "tiles %d", p.tiles);
+        CHECK(!plan::conv_wgrad_variant_ok(a, v) || v == 0 || a.c % p.bn == 0, "tile crosses a tap");
+        CHECK((int64_t)p.splits * a.kout * a.ntaps * a.c < (1ll << 40), "workspace");
+      }
     }
   }
 }
