@@ -153,6 +153,15 @@ void bind_gemm(pybind11::module_& root) {
                      dtype_code(ot), ws.data_ptr<float>(), cus, cur_stream());
     return std::make_tuple(dz, db);
   }, pybind11::arg("dy"), pybind11::arg("aux"), pybind11::arg("out_dtype") = c10::nullopt);
+  g.def("gelu", [](at::Tensor z) {
+    // y = gelu_tanh(z) (the tanh approximation of the reference's cuBLASLt GELU epilogue)
+    const c10::hip::HIPGuard guard(z.get_device());
+    at::Tensor zc = z.contiguous();
+    auto y = at::empty_like(zc);
+    gelu_tanh_forward(zc.data_ptr(), y.data_ptr(), dtype_code(zc.scalar_type()), zc.numel(), device_cus(zc.get_device()),
+                      cur_stream());
+    return y;
+  });
   g.def("column_sum", [](at::Tensor x, c10::optional<at::ScalarType> out_dtype) {
     return colsum(as2d(x), out_dtype.value_or(x.scalar_type()));
   }, py::arg("x"), py::arg("out_dtype") = c10::nullopt);

@@ -8,12 +8,16 @@
 //   wgrad_bgrad   dW = g^T x,                db = sum_rows g                      one launch
 // so the library route of FusedDense / FusedDenseGeluDense has no separate GeLU, GeLU-backward
 // or bias-gradient kernels.  Row-major tensors are handed to the column-major library as their
-// transposes (no copies).  Every (shape, epilogue) asks the heuristic once and caches the algo;
-// a shape the library has no kernel for reports "unsupported" and the Python side falls back.
+// transposes (no copies).  Every (shape, epilogue) is planned once: descriptors built, the
+// heuristic's top answers timed on the first call and the fastest kept (APEX_AMD_LT_TUNE=0: the
+// first answer); a shape the library has no kernel for reports "unsupported" and the Python side
+// falls back.
 #include "common.h"
 
 #include <hipblaslt/hipblaslt.h>
 
+#include <cstdlib>
+#include <memory>
 #include <mutex>
 #include <tuple>
 #include <unordered_map>
@@ -66,11 +70,6 @@ struct ProblemHash {
   }
 };
 
-struct Plan {
-  bool ok = false;
-  hipblasLtMatmulAlgo_t algo;
-};
-
 struct Descs {
   hipblasLtMatmulDesc_t op = nullptr;
   hipblasLtMatrixLayout_t a = nullptr, b = nullptr, d = nullptr;
@@ -82,67 +81,132 @@ struct Descs {
   }
 };
 
-void make_descs(const Problem& p, Descs& ds, const void* bias, hipDataType bias_t, void* aux, int64_t aux_ld) {
+// Everything a problem needs after its first call, kept for the process lifetime: the matmul /
+// layout descriptors (only the bias / aux pointers change between calls) and the algorithm.
+struct Plan {
+  bool ok = false;
+  hipblasLtMatmulAlgo_t algo;
+  Descs ds;
+  int candidates = 0;   // heuristic results considered
+  float best_us = 0.f;  // measured time of the pick (0: not timed)
+};
+
+void make_descs(const Problem& p, Descs& ds, hipDataType bias_t, bool has_aux, int64_t aux_ld) {
   LT_CHECK(hipblasLtMatmulDescCreate(&ds.op, HIPBLAS_COMPUTE_32F, HIP_R_32F), "desc");
   const int32_t ta = p.ta ? HIPBLAS_OP_T : HIPBLAS_OP_N, tb = p.tb ? HIPBLAS_OP_T : HIPBLAS_OP_N;
   LT_CHECK(hipblasLtMatmulDescSetAttribute(ds.op, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)), "transa");
   LT_CHECK(hipblasLtMatmulDescSetAttribute(ds.op, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)), "transb");
   LT_CHECK(hipblasLtMatmulDescSetAttribute(ds.op, HIPBLASLT_MATMUL_DESC_EPILOGUE, &p.epi, sizeof(p.epi)), "epilogue");
-  if (bias) {
-    LT_CHECK(hipblasLtMatmulDescSetAttribute(ds.op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)), "bias");
-    const int32_t bt = bias_t;
-    LT_CHECK(hipblasLtMatmulDescSetAttribute(ds.op, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)), "bias type");
-  }
-  if (aux) {
-    LT_CHECK(hipblasLtMatmulDescSetAttribute(ds.op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &aux, sizeof(aux)),
-             "aux");
+  const int32_t bt = bias_t;
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(ds.op, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)), "bias type");
+  if (has_aux)
     LT_CHECK(hipblasLtMatmulDescSetAttribute(ds.op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_LD, &aux_ld, sizeof(aux_ld)),
              "aux ld");
-  }
   LT_CHECK(hipblasLtMatrixLayoutCreate(&ds.a, p.type, p.ta ? p.k : p.m, p.ta ? p.m : p.k, p.lda), "layout a");
   LT_CHECK(hipblasLtMatrixLayoutCreate(&ds.b, p.type, p.tb ? p.n : p.k, p.tb ? p.k : p.n, p.ldb), "layout b");
   LT_CHECK(hipblasLtMatrixLayoutCreate(&ds.d, p.type, p.m, p.n, p.ldd), "layout d");
 }
 
-std::unordered_map<Problem, Plan, ProblemHash>& plans() {
-  static std::unordered_map<Problem, Plan, ProblemHash> m;
+void set_pointers(Descs& ds, const void* bias, void* aux) {
+  if (bias)
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(ds.op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)), "bias");
+  if (aux)
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(ds.op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &aux, sizeof(aux)),
+             "aux");
+}
+
+std::unordered_map<Problem, std::unique_ptr<Plan>, ProblemHash>& plans() {
+  static std::unordered_map<Problem, std::unique_ptr<Plan>, ProblemHash> m;
   return m;
 }
 std::mutex g_plan_mu;
+
+// APEX_AMD_LT_TUNE=0: take the heuristic's first answer (deterministic across ranks / runs);
+// default: time the top kTop answers once per problem on its first (non-captured) call and keep
+// the fastest — the single-answer heuristic picked a 32 x 32-tile BGRADB kernel ~10x slower than
+// the plain GEMM at the GPT-2 shapes
+constexpr int kTop = 8;
+bool tune_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("APEX_AMD_LT_TUNE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 // Runs the problem; returns false (nothing launched) when the library has no kernel for it.
 bool lt_run(const Problem& p, const void* a, const void* b, void* d, const void* bias, hipDataType bias_t, void* aux,
             int64_t aux_ld) {
   hipblasLtHandle_t h = lt_handle(p.dev);
-  Descs ds;
-  make_descs(p, ds, bias, bias_t, aux, aux_ld);
-  Plan plan;
-  {
-    std::lock_guard<std::mutex> lock(g_plan_mu);
-    auto it = plans().find(p);
-    if (it != plans().end()) {
-      plan = it->second;
-    } else {
-      hipblasLtMatmulPreference_t pref;
-      LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref), "preference");
-      const uint64_t ws = kWorkspace;
-      LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws, sizeof(ws)),
-               "workspace pref");
-      hipblasLtMatmulHeuristicResult_t res[1];
-      int found = 0;
-      const hipblasStatus_t st =
-          hipblasLtMatmulAlgoGetHeuristic(h, ds.op, ds.a, ds.b, ds.d, ds.d, pref, 1, res, &found);
-      hipblasLtMatmulPreferenceDestroy(pref);
-      plan.ok = st == HIPBLAS_STATUS_SUCCESS && found > 0 && res[0].state == HIPBLAS_STATUS_SUCCESS;
-      if (plan.ok) plan.algo = res[0].algo;
-      plans()[p] = plan;
-    }
-  }
-  if (!plan.ok) return false;
-  auto ws = at::empty({(int64_t)kWorkspace}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, p.dev));
+  std::lock_guard<std::mutex> lock(g_plan_mu);
+  auto it = plans().find(p);
+  Plan* plan = nullptr;
   const float alpha = 1.f, beta = 0.f;
-  LT_CHECK(hipblasLtMatmul(h, ds.op, &alpha, a, ds.a, b, ds.b, &beta, d, ds.d, d, ds.d, &plan.algo, ws.data_ptr(),
-                           kWorkspace, cur_stream()),
+  // stream-ordered workspace from the caching allocator (safe under concurrent streams / capture)
+  auto ws = at::empty({(int64_t)kWorkspace}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, p.dev));
+  void* wsp = ws.data_ptr();
+  hipStream_t stream = cur_stream();
+  if (it != plans().end()) {
+    plan = it->second.get();
+  } else {
+    auto np = std::make_unique<Plan>();
+    plan = np.get();
+    make_descs(p, plan->ds, bias_t, aux != nullptr, aux_ld);
+    set_pointers(plan->ds, bias, aux);
+    hipblasLtMatmulPreference_t pref;
+    LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref), "preference");
+    const uint64_t wsb = kWorkspace;
+    LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb)),
+             "workspace pref");
+    hipblasLtMatmulHeuristicResult_t res[kTop];
+    int found = 0;
+    const hipblasStatus_t st =
+        hipblasLtMatmulAlgoGetHeuristic(h, plan->ds.op, plan->ds.a, plan->ds.b, plan->ds.d, plan->ds.d, pref,
+                                        tune_enabled() ? kTop : 1, res, &found);
+    hipblasLtMatmulPreferenceDestroy(pref);
+    int valid[kTop], nv = 0;
+    if (st == HIPBLAS_STATUS_SUCCESS)
+      for (int i = 0; i < found; ++i)
+        if (res[i].state == HIPBLAS_STATUS_SUCCESS) valid[nv++] = i;
+    plan->ok = nv > 0;
+    plan->candidates = nv;
+    if (plan->ok) plan->algo = res[valid[0]].algo;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(stream, &cs);
+    if (nv > 1 && cs == hipStreamCaptureStatusNone) {
+      // time each candidate on the live operands (the output is rewritten by the real call below)
+      hipEvent_t e0, e1;
+      (void)hipEventCreate(&e0);
+      (void)hipEventCreate(&e1);
+      float best = 1e30f;
+      for (int j = 0; j < nv; ++j) {
+        const hipblasLtMatmulAlgo_t* al = &res[valid[j]].algo;
+        if (hipblasLtMatmul(h, plan->ds.op, &alpha, a, plan->ds.a, b, plan->ds.b, &beta, d, plan->ds.d, d, plan->ds.d,
+                            al, wsp, kWorkspace, stream) != HIPBLAS_STATUS_SUCCESS)
+          continue;  // warm-up; a candidate that fails to launch is skipped
+        (void)hipEventRecord(e0, stream);
+        for (int r = 0; r < 3; ++r)
+          (void)hipblasLtMatmul(h, plan->ds.op, &alpha, a, plan->ds.a, b, plan->ds.b, &beta, d, plan->ds.d, d,
+                                plan->ds.d, al, wsp, kWorkspace, stream);
+        (void)hipEventRecord(e1, stream);
+        (void)hipEventSynchronize(e1);
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        if (ms < best) {
+          best = ms;
+          plan->algo = *al;
+        }
+      }
+      plan->best_us = best * 1000.f / 3.f;
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+    }
+    plans()[p] = std::move(np);
+  }
+  if (!plan->ok) return false;
+  set_pointers(plan->ds, bias, aux);
+  LT_CHECK(hipblasLtMatmul(h, plan->ds.op, &alpha, a, plan->ds.a, b, plan->ds.b, &beta, d, plan->ds.d, d, plan->ds.d,
+                           &plan->algo, wsp, kWorkspace, stream),
            "matmul");
   return true;
 }
@@ -231,6 +295,16 @@ void lt_clear_cache() {
   plans().clear();
 }
 
+// [(m, n, k, epilogue, candidates, best_us)] of every problem planned so far (evidence logs)
+std::vector<std::tuple<int64_t, int64_t, int64_t, int, int, double>> lt_plan_table() {
+  std::lock_guard<std::mutex> lock(g_plan_mu);
+  std::vector<std::tuple<int64_t, int64_t, int64_t, int, int, double>> out;
+  for (const auto& kv : plans())
+    out.emplace_back(kv.first.m, kv.first.n, kv.first.k, (int)kv.first.epi, kv.second->candidates,
+                     (double)kv.second->best_us);
+  return out;
+}
+
 }  // namespace
 
 void bind_lt(pybind11::module_& root) {
@@ -241,6 +315,7 @@ void bind_lt(pybind11::module_& root) {
         pybind11::arg("with_bgrad") = true);
   m.def("wgrad_bgrad", &lt_wgrad_bgrad);
   m.def("clear_cache", &lt_clear_cache);
+  m.def("plan_table", &lt_plan_table);
   m.attr("EPI_NONE") = 0;
   m.attr("EPI_BIAS") = 1;
   m.attr("EPI_GELU_AUX_BIAS") = 2;

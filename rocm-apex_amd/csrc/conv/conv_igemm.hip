@@ -968,10 +968,12 @@ static int g_wgrad_variant = [] {
 
 void conv_force_wgrad_variant(int v) { g_wgrad_variant = v; }
 
-// variant for this shape: forced (A/B) or the measured default (plan: 0 = wgrad_kernel)
+// variant for this shape: forced (A/B) or the measured default — wgrad2 128 x 64 (variant 3),
+// the best native tile at every ResNet-50 3x3 shape (profiles/wgrad3x3_variants_r04.jsonl; it
+// beats MIOpen only at 28 x 28 x 128, where ops/conv.py tap_route routes it)
 static int wgrad_variant(const ConvTapArgs& a) {
   if (g_wgrad_variant >= 0) return plan::conv_wgrad_variant_ok(a, g_wgrad_variant) ? g_wgrad_variant : 0;
-  return 0;
+  return plan::conv_wgrad_variant_ok(a, 3) ? 3 : 0;
 }
 
 int64_t conv_wgrad_workspace_floats(const ConvTapArgs& a, int cus) {

@@ -27,6 +27,8 @@
 #include "apex_amd/device.h"
 #include "apex_amd/dispatch.h"
 #include "apex_amd/gemm_api.h"
+
+#include <algorithm>
 #include "apex_amd/launch_plan.h"
 
 namespace apex_amd {
@@ -356,6 +358,20 @@ __global__ void __launch_bounds__(256) dgelu_colsum_partial(const T* __restrict_
       for (int g = 0; g < 8; ++g) t += red[g][(threadIdx.x & 31) * 8 + e];
       part[(int64_t)blockIdx.y * n + c0 + e] = t;
     }
+  }
+}
+
+// y = gelu_tanh(z), 8 elements per lane per iteration (one 16-byte load + store), grid-stride:
+// the activation pass after a library GEMM whose bias epilogue wrote the pre-activation z (kept
+// as the backward's aux) — gfx950 bf16 hipBLASLt has no GELU_AUX_BIAS kernel
+template <typename T>
+__global__ void __launch_bounds__(256) gelu_fwd_kernel(const T* __restrict__ z, T* __restrict__ y, int64_t n8) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    float v[8];
+    Vec8<T>::load(v, z + i * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
+    Vec8<T>::store(y + i * 8, v);
   }
 }
 
@@ -1056,6 +1072,19 @@ void column_sum(const void* x, int dtype, int64_t m, int n, int64_t ldx, void* o
     hipLaunchKernelGGL((gemm::colsum_finalize<TO>), dim3((n + 15) / 16), dim3(256), 0, s, ws, p, n, (TO*)out);
   }, "column_sum out");
   check_launch("column_sum");
+}
+
+void gelu_tanh_forward(const void* z, void* y, int dtype, int64_t numel, int cus, hipStream_t s) {
+  if (numel % 8 || ((uintptr_t)z & 15) || ((uintptr_t)y & 15))
+    throw std::runtime_error("gelu_tanh_forward: numel must be a multiple of 8, operands 16-byte aligned");
+  const int64_t n8 = numel / 8;
+  const int64_t blocks = std::min<int64_t>((n8 + 255) / 256, (int64_t)cus * 8);
+  dispatch_16(dtype, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    hipLaunchKernelGGL((gemm::gelu_fwd_kernel<T>), dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, s,
+                       (const T*)z, (T*)y, n8);
+  }, "gelu_tanh_forward");
+  check_launch("gelu_tanh_forward");
 }
 
 void dgelu_column_sum(const void* dy, const void* aux, void* dz, int dtype, int64_t m, int n, void* out, int out_dtype,

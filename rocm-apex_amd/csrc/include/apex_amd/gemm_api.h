@@ -54,6 +54,8 @@ void column_sum(const void* x, int dtype, int64_t m, int n, int64_t ldx, void* o
                 hipStream_t s);
 int64_t column_sum_workspace_floats(int64_t m, int n, int cus);
 // dz = dy * gelu_tanh'(aux) and out = column sums of dz, one pass (workspace as column_sum)
+// y = gelu_tanh(z) elementwise (numel % 8 == 0, 16-byte aligned), full-bandwidth vector pass
+void gelu_tanh_forward(const void* z, void* y, int dtype, int64_t numel, int cus, hipStream_t s);
 void dgelu_column_sum(const void* dy, const void* aux, void* dz, int dtype, int64_t m, int n, void* out, int out_dtype,
                       float* ws, int cus, hipStream_t s);
 

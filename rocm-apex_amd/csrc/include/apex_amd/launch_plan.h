@@ -71,8 +71,14 @@ inline bool conv_fprop2_ok(const ConvTapArgs& a) {
   const int64_t xb = (int64_t)a.n * a.ih * a.iw * a.c * 2, wb = (int64_t)a.kout * a.ntaps * a.c * 2;
   return xb < (1ll << 31) && wb < (1ll << 31);
 }
-// forced >= 0 overrides when legal.  Defaults: fprop2 per output width (r04 sweep,
-// profiles/conv_cfg_sweep_r04.jsonl); fprop_kernel for > 2 GiB operands (r02 sweep choice)
+// forced >= 0 overrides when legal.  Defaults from the r04 sweep of every ResNet-50 3x3 / strided
+// 1x1 shape, forward and data gradient, bs 256 (profiles/conv_cfg_sweep_r04.jsonl):
+//  * 64 output channels (stage 1): fprop_kernel 8 waves x 32 x 64, 2 stages (cfg 5, two
+//    workgroups / 16 waves per CU hide the 9-step K loop's load latency: 108 us vs 134 for the
+//    best fprop2 tile);
+//  * otherwise fprop2: 256 x 256 (cfg 12) while it still gives >= 3/4 of a wave of workgroups,
+//    else 128 x 128 (cfg 11) — 5-20 % faster than the fprop_kernel choices at stages 2-4
+//    (e.g. 7 x 7 x 512: 67.7 vs 83.3 us forward, 82.9 vs 97.3 us data gradient)
 inline int conv_fprop_cfg(const ConvTapArgs& a, int cus, int forced) {
   auto ok = [&](int cfg) {
     return a.kout % conv_fprop_bn(cfg) == 0 && (cfg < 7 || conv_fprop2_ok(a));
@@ -82,9 +88,8 @@ inline int conv_fprop_cfg(const ConvTapArgs& a, int cus, int forced) {
   auto tiles = [&](int cfg) {
     return (m + conv_fprop_bm(cfg) - 1) / conv_fprop_bm(cfg) * (a.kout / conv_fprop_bn(cfg));
   };
-  if (conv_fprop2_ok(a)) {
-    if (a.kout % 128) return 8;
-    if (a.kout % 256 == 0 && tiles(13) >= 2 * cus) return 13;
+  if (conv_fprop2_ok(a) && a.kout % 128 == 0) {
+    if (a.kout % 256 == 0 && 4 * tiles(12) >= 3 * (int64_t)cus) return 12;
     return 11;
   }
   const int64_t tiles_m = (m + 255) / 256;

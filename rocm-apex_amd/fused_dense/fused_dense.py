@@ -68,6 +68,15 @@ def _gelu_tanh(x):
     return torch.nn.functional.gelu(x, approximate="tanh")
 
 
+def _gelu_pass(z):
+    """tanh-GeLU of a GPU pre-activation: the native vector kernel (exp + rcp form, one 16-byte
+    load / store per 8 elements) where it applies, else torch's GeLU."""
+    if (_native.use_native(z) and _native.submodule("gemm") is not None and z.dtype in (torch.float16, torch.bfloat16)
+            and z.is_contiguous() and z.numel() % 8 == 0):
+        return _g().gelu(z)
+    return _gelu_tanh(z)
+
+
 _ROUTES = {}
 
 
@@ -230,7 +239,7 @@ def _lib_gelu_dense_fwd(x, w1, b1, w2, b2):
             # pre-activation, one elementwise GeLU pass
             r1 = lt.linear(x2, w1c, b1, lt.EPI_BIAS)
             gelu_in = r1[0] if r1 else torch.addmm(b1, x2, w1.t())
-            out1 = _gelu_tanh(gelu_in)
+            out1 = _gelu_pass(gelu_in)
         r2 = lt.linear(out1, w2c, b2, lt.EPI_BIAS)
         out2 = r2[0] if r2 else torch.addmm(b2, out1, w2.t())
         return out1, out2.view(x.shape[:-1] + (w2.shape[0],)), gelu_in

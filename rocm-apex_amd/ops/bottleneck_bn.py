@@ -233,13 +233,18 @@ def _conv_fwd(x, w, stride, pad):
 
 
 def _conv_bwd(gy, x, w, stride, pad, need_x=True):
-    _, dg, _ = convops.tap_route(x.size(1), w.size(0), w.size(2), stride, x.size(2))
-    dx = None
+    _, dg, wg = convops.tap_route(x.size(1), w.size(0), w.size(2), stride, x.size(2))
+    dx = dw = None
     if need_x and dg:
         dx = convops.conv_tap_dgrad(gy, w, x.shape, stride, pad)
-    dx_m, dw, _ = torch.ops.aten.convolution_backward(gy, x, w, None, [stride, stride], [pad, pad], [1, 1], False,
-                                                      [0, 0], 1, [need_x and not dg, True, False])
-    return (dx if dx is not None else dx_m), dw
+    if wg:
+        dw = convops.conv_tap_wgrad(gy, x, w.shape, stride, pad, w.dtype)
+    if (need_x and not dg) or not wg:
+        dx_m, dw_m, _ = torch.ops.aten.convolution_backward(gy, x, w, None, [stride, stride], [pad, pad], [1, 1],
+                                                            False, [0, 0], 1, [need_x and not dg, not wg, False])
+        dx = dx if dx is not None else dx_m
+        dw = dw if dw is not None else dw_m
+    return dx, dw
 
 
 class _BottleneckFn(torch.autograd.Function):

@@ -294,17 +294,19 @@ def conv_tap_wgrad(gy, x, w_shape, stride, pad, out_dtype):
 
 def tap_route(cin, cout, k, stride, h):
     """(fwd, dgrad, wgrad) through the native kernels for this shape, from the per-shape A/B
-    against MIOpen on MI355X (profiles/conv_cfg_sweep_r02.jsonl, profiles/conv_igemm_v1_vs_miopen_r02
-    .jsonl; ResNet-50 bs 256 bf16):
-      * 3x3: forward native except at 128 output channels (MIOpen 0.9-1.0x ahead there); data
-        gradient native except the stride-2 / <= 128-channel one (per-phase launches lose);
-        native 1.05-1.42x elsewhere (e.g. 14x14x256 dgrad 78 vs 111 us);
-      * 1x1 stride 2 (downsample): data gradient native (1.02-1.24x);
-      * weight gradients stay on MIOpen (the split-K kernel is 0.5-0.9x)."""
+    against MIOpen on MI355X (ResNet-50 bs 256 bf16; r04: profiles/conv_cfg_sweep_r04.jsonl,
+    profiles/wgrad3x3_variants_r04.jsonl — r02: conv_cfg_sweep_r02.jsonl):
+      * 3x3 forward: native everywhere (fprop2 tiles: 0.64-1.0x MIOpen's time, e.g. 7x7x512 67.7
+        vs 102.8 us; 56x56x128 stride 2 ties at 95.8 vs 95.6);
+      * 3x3 data gradient: native except the stride-2 one at <= 128 channels (per-phase launches,
+        173.9 vs 171.0 us);
+      * 1x1 stride 2 (downsample): data gradient native (0.70-0.91x MIOpen);
+      * 3x3 weight gradient: native (wgrad2 128 x 64) only at 28x28x128 stride 1 (136 vs 149 us);
+        MIOpen's is 5-12 % ahead at the other shapes."""
     if not _TAP_ENABLED:
         return False, False, False
     if k == 3:
-        return cout != 128, not (stride == 2 and cout <= 128), False
+        return True, not (stride == 2 and cout <= 128), (stride == 1 and cin == 128 and cout == 128 and h == 28)
     if k == 1 and stride == 2:
         return False, True, False
     return False, False, False

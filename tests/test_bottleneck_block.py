@@ -231,7 +231,7 @@ def _chain(bn_group=1, peer=True):
     return chain
 
 
-def _run_chain(chain, x, gy, node, bn_group=1, group=None, peer=True):
+def _run_chain(chain, x, gy, node, bn_group=1, group=None, peer=True, linked=True):
     import apex  # noqa: F401
     from apex.contrib.groupbn import BatchNorm2d_NHWC
     from apex.models.resnet import run_linked
@@ -264,7 +264,12 @@ def _run_chain(chain, x, gy, node, bn_group=1, group=None, peer=True):
     bottleneck_bn._BottleneckFn.forward = staticmethod(counted)
     try:
         xi = x.clone().requires_grad_(True)
-        y = run_linked(list(chain), xi)
+        if linked:
+            y = run_linked(list(chain), xi)
+        else:
+            y = xi
+            for blk in chain:
+                y = blk(y)
         if isinstance(y, tuple):
             y = y[0]
         y.backward(gy)
@@ -275,24 +280,34 @@ def _run_chain(chain, x, gy, node, bn_group=1, group=None, peer=True):
 
 
 @pytest.mark.gpu
-def test_gpu_bottleneck_chain_node_vs_module_path():
-    """a 3-block chain with every native route forced (the BlockLink
-    hand-offs active: block i+1's conv1 dgrad masks with block i's ReLU bits and does its bn3
-    backward reduction) against the per-module fused path at the SINGLE-block tolerances."""
+def test_gpu_bottleneck_chain_linked_vs_unlinked():
+    """a 3-block chain with every native route forced.  The linked walk
+    (BlockLink: block i+1's conv1 dgrad masks with block i's ReLU bits and does its bn3 backward
+    reduction) against the same nodes called one by one (no hand-off): the forward is identical
+    and the backward differs only in the order of one reduction's sums, so a wrong hand-off
+    (mask, reduction, coefficients) shows as an O(1) difference while the correct one agrees to
+    rounding.  Against fp32 all three bf16 arms (linked, unlinked, per-module) sit at the same
+    ~18 % dx / ~17 % median parameter-gradient distance through 3 blocks (tools/dbg_chain_link.py,
+    profiles/chain_link_r04.jsonl), so the per-module path is checked at that noise level only."""
     torch.manual_seed(3)
     a = _chain().cuda().to(memory_format=torch.channels_last).train()
-    b = copy.deepcopy(a)
+    b, c = copy.deepcopy(a), copy.deepcopy(a)
     x = torch.randn(4, 64, 14, 14, device="cuda").to(torch.bfloat16).to(memory_format=torch.channels_last)
     gy = torch.randn(4, 256, 14, 14, device="cuda").to(torch.bfloat16).to(memory_format=torch.channels_last)
     ya, ga, pa, ca = _run_chain(a, x, gy, True)
-    yb, gb, pb, cb = _run_chain(b, x, gy, False)
-    assert ca["n"] == 3 and cb["n"] == 0, (ca, cb)
-    assert ca["red"] == 2, ca  # both block boundaries took the masked-dgrad + reduction hand-off
-    assert _rel(ya, yb) < 1e-2
-    assert _rel(ga, gb) < 6e-2, _rel(ga, gb)
+    yb, gb, pb, cb = _run_chain(b, x, gy, True, linked=False)
+    yc, gc, pc, cc = _run_chain(c, x, gy, False)
+    assert ca["n"] == 3 and cb["n"] == 3 and cc["n"] == 0, (ca, cb, cc)
+    assert ca["red"] == 2 and cb["red"] == 0, (ca, cb)  # both boundaries took the hand-off when linked
+    assert torch.equal(ya, yb)
+    assert _rel(ga, gb) < 2e-2, _rel(ga, gb)
     for n in pa:
-        assert _rel(pa[n], pb[n]) < 8e-2, (n, _rel(pa[n], pb[n]))
-    for (n, ba), bb in zip(a.named_buffers(), b.buffers()):
+        assert _rel(pa[n], pb[n]) < 2e-2, (n, _rel(pa[n], pb[n]))
+    assert _rel(ya, yc) < 1e-2
+    assert _rel(ga, gc) < 0.3, _rel(ga, gc)
+    for n in pa:
+        assert _rel(pa[n], pc[n]) < 0.35, (n, _rel(pa[n], pc[n]))
+    for (n, ba), bb in zip(a.named_buffers(), c.buffers()):
         if n.endswith("running_mean") or n.endswith("running_var"):
             torch.testing.assert_close(ba, bb, atol=2e-3, rtol=2e-2)
 
@@ -314,12 +329,16 @@ def _sync_chain_worker(rank, world, peer):
     ys, gs, ps, calls = _run_chain(mine, x[sl].contiguous(memory_format=torch.channels_last),
                                    gy[sl].contiguous(memory_format=torch.channels_last), True, world, None, peer)
     assert calls["n"] == 3, calls
+    # the statistics are the full batch's up to summation order (merged Welford payloads vs one
+    # shifted sum), which flips bf16 roundings and grows to a few % through 3 blocks' BN backward
+    # (measured 6-7 % dx; all bf16 arms are ~18 % from fp32, profiles/chain_link_r04.jsonl); a
+    # wrong exchange (local count, missing sums) is an O(1) error
     assert _rel(ys, yf[sl]) < 1e-2, _rel(ys, yf[sl])
-    assert _rel(gs, gf[sl]) < 6e-2, _rel(gs, gf[sl])
+    assert _rel(gs, gf[sl]) < 0.15, _rel(gs, gf[sl])
     for n, g in ps.items():
         tot = g.detach().float().cpu()
         dist.all_reduce(tot)  # local parameter gradients: the group sum is the full-batch gradient
-        assert _rel(tot, pf[n].cpu()) < 8e-2, (n, _rel(tot, pf[n].cpu()))
+        assert _rel(tot, pf[n].cpu()) < 0.15, (n, _rel(tot, pf[n].cpu()))
     for (n, bs), bf in zip(mine.named_buffers(), full.buffers()):
         if n.endswith("running_mean") or n.endswith("running_var"):
             torch.testing.assert_close(bs, bf, atol=2e-3, rtol=2e-2)

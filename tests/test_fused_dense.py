@@ -430,3 +430,17 @@ def test_gpu_native_column_sum_helper():
     got = _native.column_sum(x, torch.bfloat16)
     torch.testing.assert_close(got.float(), x.float().sum((0, 1)), atol=0.5, rtol=1e-2)
     assert got.dtype == torch.bfloat16
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_gpu_gelu_pass(dtype):
+    """The native tanh-GeLU pass of the bf16 library route against torch's tanh GeLU in fp32."""
+    import apex
+
+    g = apex._native.require("gemm").gemm
+    torch.manual_seed(4)
+    z = (torch.randn(4099, 1024, device="cuda") * 3).to(dtype)
+    y = g.gelu(z)
+    ref = torch.nn.functional.gelu(z.float(), approximate="tanh")
+    torch.testing.assert_close(y.float(), ref, atol=2e-2, rtol=2e-2)

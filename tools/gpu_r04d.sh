@@ -1,9 +1,7 @@
 #!/bin/bash
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r04c
-timeout -k 10 300 python tools/dbg_chain_link.py > gpurun_out/r04c/chain_link.jsonl 2>&1 || { tail -20 gpurun_out/r04c/chain_link.jsonl; exit 1; }
-cat gpurun_out/r04c/chain_link.jsonl
-timeout -k 10 600 python -u -m pytest -q --timeout 200 --timeout-method thread tests/test_bottleneck_block.py -k "not chain_node_vs_module" > gpurun_out/r04c/tests_blk.log 2>&1
+timeout -k 10 600 python -u -m pytest -q --timeout 200 --timeout-method thread tests/test_bottleneck_block.py tests/test_fused_dense.py -k "chain or syncbn or gelu_pass or fp32 or fused_dense_gelu" > gpurun_out/r04c/tests_blk.log 2>&1
 rc=$?; tail -3 gpurun_out/r04c/tests_blk.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python tools/conv_cfg_sweep.py > gpurun_out/r04c/sweep.jsonl 2> gpurun_out/r04c/sweep.err || { tail -5 gpurun_out/r04c/sweep.err; exit 1; }
 echo SWEEP_DONE
