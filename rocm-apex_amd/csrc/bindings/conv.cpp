@@ -55,7 +55,9 @@ ConvTapArgs make_args(const at::Tensor& in, const at::Tensor& w, const at::Tenso
 }
 
 // out[n, oh*osh+oph, ow*osw+opw, k] = sum_t,c in[n, oh*ish+dh[t], ow*isw+dw[t], c] * w[k, t, c]
-void tap_fprop(const at::Tensor& in, const at::Tensor& w, at::Tensor& out, int64_t oh, int64_t ow, int64_t ish,
+// Returns the BN-statistics partials [2, rows, K] (rows = the chosen tile configuration's M
+// tiles) when ``stats_shift`` is given without a ``stats`` buffer, else None.
+c10::optional<at::Tensor> tap_fprop(const at::Tensor& in, const at::Tensor& w, at::Tensor& out, int64_t oh, int64_t ow, int64_t ish,
                int64_t isw, int64_t osh, int64_t osw, int64_t oph, int64_t opw, std::vector<int64_t> dh,
                std::vector<int64_t> dw, const c10::optional<at::Tensor>& scale,
                const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& residual, bool relu,
@@ -85,16 +87,22 @@ void tap_fprop(const at::Tensor& in, const at::Tensor& w, at::Tensor& out, int64
                 "conv tap_fprop: mask must match the output's shape, layout and dtype");
     a.mask = mask->data_ptr();
   }
-  if (stats.has_value()) {
-    TORCH_CHECK(stats->is_cuda() && stats->scalar_type() == at::kFloat && stats->is_contiguous() &&
-                    stats->numel() == 2 * (int64_t)conv_tap_stats_tiles(a) * out.size(3),
-                "conv tap_fprop: stats must be contiguous fp32 [2, stats_tiles, K]");
-    a.stats = stats->data_ptr<float>();
-    a.stats_shift = per_channel(stats_shift, "stats_shift");
-  }
   const c10::hip::HIPGuard g(in.get_device());
+  const int cus = device_cus(in.get_device());
+  c10::optional<at::Tensor> made;
+  if (stats.has_value() || stats_shift.has_value()) {
+    const int64_t rows = conv_tap_stats_tiles(a, cus);
+    at::Tensor st = stats.has_value() ? *stats : at::empty({2, rows, out.size(3)}, out.options().dtype(at::kFloat));
+    TORCH_CHECK(st.is_cuda() && st.scalar_type() == at::kFloat && st.is_contiguous() &&
+                    st.numel() == 2 * rows * out.size(3),
+                "conv tap_fprop: stats must be contiguous fp32 [2, stats_tiles, K]");
+    a.stats = st.data_ptr<float>();
+    a.stats_shift = per_channel(stats_shift, "stats_shift");
+    if (!stats.has_value()) made = st;
+  }
   TORCH_CHECK(conv_tap_supported(a), "conv tap_fprop: unsupported (C and K must be multiples of 64, bf16/fp16)");
-  conv_tap_fprop(a, device_cus(in.get_device()), cur_stream());
+  conv_tap_fprop(a, cus, cur_stream());
+  return made;
 }
 
 // dw[k, t, c] (fp32-accumulated, written in dw's dtype) for the forward `in` -> dy geometry
@@ -329,13 +337,6 @@ void bind_conv(pybind11::module_& root) {
         pybind11::arg("residual") = pybind11::none(), pybind11::arg("relu") = false,
         pybind11::arg("mask") = pybind11::none(), pybind11::arg("stats") = pybind11::none(),
         pybind11::arg("stats_shift") = pybind11::none());
-  m.def("tap_stats_tiles", [](int64_t n, int64_t oh, int64_t ow) {
-    ConvTapArgs a{};
-    a.n = (int)n;
-    a.oh = (int)oh;
-    a.ow = (int)ow;
-    return conv_tap_stats_tiles(a);
-  });
   m.def("wgrad", &wgrad);
   m.def("force_fprop_cfg", &conv_force_fprop_cfg);
   m.def("force_wgrad_variant", &conv_force_wgrad_variant);

@@ -378,22 +378,26 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
   }
 }
 
+// finalize kernels: 8 channels x kFinG row groups per block (the partial rows of a 3x3 conv's
+// 256-row tiles number ~3k at ResNet stage 1: 128 groups keep ~25 independent loads per thread)
+constexpr int kFinG = 128;
+
 // ---- statistics finalize: fixed-order sum of the per-workgroup partials -> batch mean /
 // inv_std, the running-stat EMA and the apply coefficients coef = [scale | shift] ----
 // ``shift`` (the statistics' centring shift) is usually the running mean itself, so shift, rmean
 // and rvar are NOT restrict: shift[ch] is read into a register before rmean[ch] is written.
-__global__ void __launch_bounds__(256) stats_finalize(const float* __restrict__ part, int g, int c, float n,
+__global__ void __launch_bounds__(8 * kFinG) stats_finalize(const float* __restrict__ part, int g, int c, float n,
                                                       const float* shift, const float* __restrict__ w,
                                                       const float* __restrict__ b, float eps, float momentum,
                                                       float* rmean, float* rvar,
                                                       float* __restrict__ save_mean, float* __restrict__ save_invstd,
                                                       float* __restrict__ coef) {
   // 8 channels x 32 partial-row groups per block (the finalize is latency-bound)
-  __shared__ float red[2][32][9];
+  __shared__ float red[2][kFinG][9];
   const int lc = threadIdx.x & 7, grp = threadIdx.x >> 3, ch = blockIdx.x * 8 + lc;
   float a = 0.f, q = 0.f;
   if (ch < c)
-    for (int j = grp; j < g; j += 32) {
+    for (int j = grp; j < g; j += kFinG) {
       a += part[(int64_t)j * c + ch];
       q += part[(int64_t)(g + j) * c + ch];
     }
@@ -403,7 +407,7 @@ __global__ void __launch_bounds__(256) stats_finalize(const float* __restrict__ 
   if (grp != 0 || ch >= c) return;
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll 8
-  for (int i = 0; i < 32; ++i) {
+  for (int i = 0; i < kFinG; ++i) {
     s1 += red[0][i][lc];
     s2 += red[1][i][lc];
   }
@@ -426,13 +430,13 @@ __global__ void __launch_bounds__(256) stats_finalize(const float* __restrict__ 
 // ---- group (cross-rank) statistics from the epilogue partials: the Welford payload
 // [mean(C) | M2(C) | count] of this rank, M2 = sum of squared deviations from the local mean,
 // for the group exchange + merge of csrc/groupbn (bn_nhwc_stats_merge) ----
-__global__ void __launch_bounds__(256) part_payload(const float* __restrict__ part, int g, int c, float n,
+__global__ void __launch_bounds__(8 * kFinG) part_payload(const float* __restrict__ part, int g, int c, float n,
                                                     const float* shift, float* __restrict__ payload) {
-  __shared__ float red[2][32][9];
+  __shared__ float red[2][kFinG][9];
   const int lc = threadIdx.x & 7, grp = threadIdx.x >> 3, ch = blockIdx.x * 8 + lc;
   float a = 0.f, q = 0.f;
   if (ch < c)
-    for (int j = grp; j < g; j += 32) {
+    for (int j = grp; j < g; j += kFinG) {
       a += part[(int64_t)j * c + ch];
       q += part[(int64_t)(g + j) * c + ch];
     }
@@ -442,7 +446,7 @@ __global__ void __launch_bounds__(256) part_payload(const float* __restrict__ pa
   if (grp != 0 || ch >= c) return;
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll 8
-  for (int i = 0; i < 32; ++i) {
+  for (int i = 0; i < kFinG; ++i) {
     s1 += red[0][i][lc];
     s2 += red[1][i][lc];
   }
@@ -452,15 +456,15 @@ __global__ void __launch_bounds__(256) part_payload(const float* __restrict__ pa
   if (ch == 0) payload[2 * c] = n;
 }
 
-__global__ void __launch_bounds__(256) bwd_finalize(const float* __restrict__ part, int g, int c, float inv_n,
+__global__ void __launch_bounds__(8 * kFinG) bwd_finalize(const float* __restrict__ part, int g, int c, float inv_n,
                                                     const float* __restrict__ mean, const float* __restrict__ istd,
                                                     const float* __restrict__ w, float* __restrict__ gw,
                                                     float* __restrict__ gb, float* __restrict__ coef) {
-  __shared__ float red[2][32][9];
+  __shared__ float red[2][kFinG][9];
   const int lc = threadIdx.x & 7, grp = threadIdx.x >> 3, ch = blockIdx.x * 8 + lc;
   float a = 0.f, q = 0.f;
   if (ch < c)
-    for (int j = grp; j < g; j += 32) {
+    for (int j = grp; j < g; j += kFinG) {
       a += part[(int64_t)j * c + ch];
       q += part[(int64_t)(g + j) * c + ch];
     }
@@ -470,7 +474,7 @@ __global__ void __launch_bounds__(256) bwd_finalize(const float* __restrict__ pa
   if (grp != 0 || ch >= c) return;
   float sdy = 0.f, sdyx = 0.f;
 #pragma unroll 8
-  for (int i = 0; i < 32; ++i) {
+  for (int i = 0; i < kFinG; ++i) {
     sdy += red[0][i][lc];
     sdyx += red[1][i][lc];
   }
@@ -633,7 +637,7 @@ void conv1x1_dgrad_bnred(const void* g, const void* w, void* out, int64_t m, int
 void conv1x1_bn_finalize(const float* part, int g, int c, float n, const float* shift, const float* w, const float* b,
                          float eps, float momentum, float* rmean, float* rvar, float* save_mean, float* save_invstd,
                          float* coef, hipStream_t s) {
-  hipLaunchKernelGGL(c1bn::stats_finalize, dim3((c + 7) / 8), dim3(256), 0, s, part, g, c, n, shift, w, b, eps,
+  hipLaunchKernelGGL(c1bn::stats_finalize, dim3((c + 7) / 8), dim3(8 * c1bn::kFinG), 0, s, part, g, c, n, shift, w, b, eps,
                      momentum, rmean, rvar, save_mean, save_invstd, coef);
   check_launch("conv1x1_bn_finalize");
 }
@@ -1216,13 +1220,13 @@ void conv1x1_wgrad(const void* g, const void* x, void* dw, int out_dtype, int64_
 
 void conv1x1_bn_part_payload(const float* part, int g, int c, float n, const float* shift, float* payload,
                              hipStream_t s) {
-  hipLaunchKernelGGL(c1bn::part_payload, dim3((c + 7) / 8), dim3(256), 0, s, part, g, c, n, shift, payload);
+  hipLaunchKernelGGL(c1bn::part_payload, dim3((c + 7) / 8), dim3(8 * c1bn::kFinG), 0, s, part, g, c, n, shift, payload);
   check_launch("conv1x1_bn_part_payload");
 }
 
 void conv1x1_bnbwd_finalize(const float* part, int g, int c, float inv_n, const float* mean, const float* istd,
                             const float* w, float* gw, float* gb, float* coef, hipStream_t s) {
-  hipLaunchKernelGGL(c1bn::bwd_finalize, dim3((c + 7) / 8), dim3(256), 0, s, part, g, c, inv_n, mean, istd, w, gw, gb,
+  hipLaunchKernelGGL(c1bn::bwd_finalize, dim3((c + 7) / 8), dim3(8 * c1bn::kFinG), 0, s, part, g, c, inv_n, mean, istd, w, gw, gb,
                      coef);
   check_launch("conv1x1_bnbwd_finalize");
 }

@@ -156,16 +156,12 @@ struct FCfg {
 };
 
 // Epilogue of one EH-row chunk of an fprop tile whose fp32 accumulators are staged in ``cs``
-// ([EH][BN + 4] floats): fused scale / bias / residual / ReLU / mask, 16-byte row stores, and the
-// consuming BN's statistics partials of the chunk ([2][ceil(M / 128)][kout], one row per 128
-// output rows; EH = 128 or 64 — two 64-row chunks of one 128-row stats tile sum there in the
-// finalize).  Ends with LDS reused for the statistics fold: the caller barriers before reusing cs.
-template <int EH>
-__device__ __forceinline__ int stats_row_of(int row0c) { return row0c / 128 * (128 / EH) + (row0c % 128) / EH; }
-
+// ([EH][BN + 4] floats): fused scale / bias / residual / ReLU / mask, 16-byte row stores.  The
+// consuming BN's statistics of the stored values accumulate in the caller's st1 / st2 (8
+// columns per thread) over all chunks of the tile; stats_fold writes the tile's row.
 template <typename T, int BN, int THREADS, int EH>
-__device__ __forceinline__ void epi_chunk(const Geo& g, uint16_t* __restrict__ Y, float* cs, int row0c, int col0,
-                                          int tid) {
+__device__ __forceinline__ void epi_chunk(const Geo& g, uint16_t* __restrict__ Y, const float* cs, int row0c,
+                                          int col0, int tid, float (&st1)[8], float (&st2)[8]) {
   constexpr int CST = BN + 4;
   constexpr int CPR = BN / 8;               // 8-column chunks per row
   constexpr int RP = THREADS / CPR;         // rows per pass
@@ -181,9 +177,9 @@ __device__ __forceinline__ void epi_chunk(const Geo& g, uint16_t* __restrict__ Y
   if (g.scale) Vec8<float>::load(sc, g.scale + gc);
   if (g.bias) Vec8<float>::load(bi, g.bias + gc);
   const bool affine = g.scale || g.bias;
-  float st1[8], st2[8], sft[8];
+  float sft[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) st1[e] = st2[e] = sft[e] = 0.f;
+  for (int e = 0; e < 8; ++e) sft[e] = 0.f;
   if (g.stats && g.shift) Vec8<float>::load(sft, g.shift + gc);
   const int ohw = g.oh * g.ow;
 #pragma unroll
@@ -233,27 +229,27 @@ __device__ __forceinline__ void epi_chunk(const Geo& g, uint16_t* __restrict__ Y
       }
     }
   }
-  if (g.stats && row0c < g.m) {  // (uniform: a chunk wholly past M has no statistics row)
-    // fixed-order fold of the row groups sharing each column chunk (cs is dead: reuse it)
-    constexpr int NG = RP < EH ? RP : EH;
-    __syncthreads();
-    float* red = cs;
-    if (rsub < NG) {
+}
+
+// fixed-order fold of the thread groups sharing each 8-column chunk -> statistics row ``srow``
+// of [2][rows][kout] (rows = the launch's M tiles: conv_tap_stats_tiles).  Uses ``red`` (LDS,
+// 2 x min(RP, rows_per_tile) x BN floats) — the caller has barriered after its last read of it.
+template <int BN, int THREADS>
+__device__ __forceinline__ void stats_fold(const Geo& g, float* red, int srow, int rows, int col0, int tid,
+                                           const float (&st1)[8], const float (&st2)[8]) {
+  constexpr int CPR = BN / 8, RP = THREADS / CPR;
+  const int ch = tid % CPR, rsub = tid / CPR;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        red[(rsub * 2 + 0) * BN + ch * 8 + e] = st1[e];
-        red[(rsub * 2 + 1) * BN + ch * 8 + e] = st2[e];
-      }
-    }
-    __syncthreads();
-    const int tiles = (g.m + 127) / 128 * (128 / EH);
-    const int srow = stats_row_of<EH>(row0c);
-    for (int i = tid; i < 2 * BN; i += THREADS) {
-      const int which = i / BN, col = i % BN;
-      float acc2 = 0.f;
-      for (int r = 0; r < NG; ++r) acc2 += red[(r * 2 + which) * BN + col];
-      g.stats[((int64_t)which * tiles + srow) * g.kout + col0 + col] = acc2;
-    }
+  for (int e = 0; e < 8; ++e) {
+    red[(rsub * 2 + 0) * BN + ch * 8 + e] = st1[e];
+    red[(rsub * 2 + 1) * BN + ch * 8 + e] = st2[e];
+  }
+  __syncthreads();
+  for (int i = tid; i < 2 * BN; i += THREADS) {
+    const int which = i / BN, col = i % BN;
+    float acc2 = 0.f;
+    for (int r = 0; r < RP; ++r) acc2 += red[(r * 2 + which) * BN + col];
+    g.stats[((int64_t)which * rows + srow) * g.kout + col0 + col] = acc2;
   }
 }
 
@@ -383,6 +379,8 @@ fprop_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, ui
 
   // ---- epilogue: 128-row chunks staged as fp32 through LDS, 16-byte row stores ----
   float* cs = reinterpret_cast<float*>(lds);
+  constexpr int BMT = BM;
+  float st1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, st2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int half = 0; half < BM / 128; ++half) {
     const int wr0 = wm * (BM / WM);
@@ -399,9 +397,10 @@ fprop_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, ui
         }
     }
     __syncthreads();
-    epi_chunk<T, BN, C::THREADS, 128>(g, Y, cs, row0 + 128 * half, col0, tid);
+    epi_chunk<T, BN, C::THREADS, 128>(g, Y, cs, row0 + 128 * half, col0, tid, st1, st2);
     __syncthreads();
   }
+  if (g.stats) stats_fold<BN, C::THREADS>(g, cs, bm, (g.m + BMT - 1) / BMT, col0, tid, st1, st2);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -546,6 +545,8 @@ fprop2_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, u
   __syncthreads();
 
   float* cs = reinterpret_cast<float*>(lds);
+  constexpr int BMT = BM2;
+  float st1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, st2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int half = 0; half < BM2 / 128; ++half) {
     const int wr0 = wm * (BM2 / WM);
@@ -562,8 +563,276 @@ fprop2_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, u
         }
     }
     __syncthreads();
-    epi_chunk<T, BN, C::THREADS, 128>(g, Y, cs, row0 + 128 * half, col0, tid);
+    epi_chunk<T, BN, C::THREADS, 128>(g, Y, cs, row0 + 128 * half, col0, tid, st1, st2);
     __syncthreads();
+  }
+  if (g.stats) stats_fold<BN, C::THREADS>(g, cs, bm, (g.m + BMT - 1) / BMT, col0, tid, st1, st2);
+}
+
+// ---------------------------------------------------------------------------------------------
+// fprop3: persistent tap GEMM with the accumulators transposed (D[channel][pixel]) and the
+// epilogue straight from registers.
+//   * Workgroup (n, p) of a P x tiles_n grid owns output-channel block n and the contiguous
+//     pixel-tile range [p T / P, (p+1) T / P): the LDS-DMA ring (fprop2's buffer-load staging) runs
+//     across tile boundaries, so the next tile's operands stream in while the current tile's
+//     last K-steps and its epilogue run — no per-tile pipeline fill / drain (the 9-step K loop
+//     of a 64-channel 3x3 conv spends most of its time there otherwise).
+//   * MFMA operands swapped (a = weight fragment, b = activation fragment): lane l holds, for
+//     pixel (l & 31) of a 32-pixel subtile, 4 consecutive channels per register group, so the
+//     epilogue writes 8-byte channel runs per pixel directly from the accumulators (no LDS
+//     staging, no barrier) and the LDS ring is never repurposed.
+//   * BN statistics of the output accumulate per lane over all the workgroup's tiles; one
+//     cross-lane + cross-wave fold per workgroup writes statistics row p ([2][rows][kout];
+//     rows >= P are zero-filled).
+// ---------------------------------------------------------------------------------------------
+template <int BM_, int BN_, int WM_, int WN_, int S_>
+struct F3Cfg {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, S = S_;
+  static constexpr int NW = WM * WN, THREADS = NW * 64;
+  static constexpr int TPX = BM / WM / 32, TCH = BN / WN / 32;  // 32-pixel / 32-channel subtiles per wave
+  static constexpr int PA = BM / 8 / NW, PB = BN / 8 / NW;
+  static constexpr size_t LDS = (size_t)S * (BM * BK + BN * BK) * 2;
+  static_assert(PA >= 1 && PB >= 1 && TPX >= 1 && TCH >= 1, "bad fprop3 tile configuration");
+  static_assert(LDS >= (size_t)2 * WM * BN * 4, "statistics fold needs 2 x WM x BN floats of LDS");
+};
+
+struct F3Sched {
+  int P, rows;  // workgroups per channel block (balanced split of the pixel tiles), stats rows
+};
+
+template <typename T, typename C, bool STATS>
+__global__ void __launch_bounds__(C::THREADS, 1)
+fprop3_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y, Geo g,
+              F3Sched sc) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  constexpr int BMX = C::BM, BN = C::BN, WM = C::WM, WN = C::WN, NW = C::NW, TPX = C::TPX, TCH = C::TCH;
+  constexpr int PA = C::PA, PB = C::PB, S = C::S;
+  constexpr int TA = BMX * BK, TB = BN * BK;
+  auto a_buf = [&](int b) { return lds + b * (TA + TB); };
+  auto b_buf = [&](int b) { return lds + b * (TA + TB) + TA; };
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_m = (g.m + BMX - 1) / BMX, tiles_n = g.kout / BN;
+  const int wg = xcd_remap(blockIdx.x, sc.P * tiles_n);
+  const int bn = wg % tiles_n, p = wg / tiles_n;
+  const int t_begin = (int)((int64_t)p * tiles_m / sc.P), t_end = (int)((int64_t)(p + 1) * tiles_m / sc.P);
+  const int ntile = max(0, t_end - t_begin);
+  const int col0 = bn * BN;
+  const int ohw = g.oh * g.ow;
+  const int kw = g.ntaps * g.c;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)X, 0, __builtin_amdgcn_readfirstlane(g.xbytes), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)Wt, 0, __builtin_amdgcn_readfirstlane(g.wbytes), 0x00020000);
+  const int cblocks = g.c / BK;
+  const int nk = g.ntaps * cblocks;
+  const int nsteps = ntile * nk;
+
+  // issue-side state: this lane's A rows of the tile being ISSUED (recomputed at its first step)
+  uint32_t aoff[PA], amask[PA];
+  auto set_rows = [&](int tile) {
+    const int row0 = tile * BMX;
+#pragma unroll
+    for (int i = 0; i < PA; ++i) {
+      const int row = 8 * (i * NW + wave) + (lane >> 3);
+      const int m = row0 + row;
+      const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+      aoff[i] = 0;
+      amask[i] = 0;
+      if (m < g.m) {
+        const int nimg = (int)fdiv((uint32_t)m, g.div_ohw), rem = m - nimg * ohw;
+        const int oy = (int)fdiv((uint32_t)rem, g.div_ow), ox = rem - oy * g.ow;
+        const int ih0 = oy * g.ish, iw0 = ox * g.isw;
+        aoff[i] = (uint32_t)((((nimg * g.h + ih0) * g.w + iw0) * g.c + 8 * chunk) * 2);
+        uint32_t mk = 0;
+        for (int t = 0; t < g.ntaps; ++t) {
+          const int ih = ih0 + g.dh[t], iw = iw0 + g.dw[t];
+          mk |= ((unsigned)ih < (unsigned)g.h && (unsigned)iw < (unsigned)g.w) ? (1u << t) : 0u;
+        }
+        amask[i] = mk;
+      }
+    }
+  };
+  uint32_t boff[PB];
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {
+    const int row = 8 * (i * NW + wave) + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    boff[i] = (uint32_t)(((col0 + row) * kw + 8 * chunk) * 2);
+  }
+  int issue_tile = -1;
+  auto issue = [&](int gs, int buf) {
+    const int tl = gs / nk, kt = gs - tl * nk;
+    if (tl != issue_tile) {
+      issue_tile = tl;
+      set_rows(t_begin + tl);
+    }
+    const int t = kt / cblocks, c0 = (kt - t * cblocks) * BK;
+    const uint32_t toff = (uint32_t)(g.tapoff[t] + c0 * 2);
+    uint16_t* adst = a_buf(buf);
+#pragma unroll
+    for (int i = 0; i < PA; ++i) {
+      const uint32_t voff = ((amask[i] >> t) & 1u) ? aoff[i] + toff : 0x80000000u;
+      bdma16(xr, voff, adst + (i * NW + wave) * 512);
+    }
+    uint16_t* bdst = b_buf(buf);
+    const uint32_t k0b = (uint32_t)((t * g.c + c0) * 2);
+#pragma unroll
+    for (int i = 0; i < PB; ++i) bdma16(wr, boff[i] + k0b, bdst + (i * NW + wave) * 512);
+  };
+
+  // epilogue constants of this lane's channels: channel of register r of subtile ci =
+  // chw + 32 ci + 8 (r >> 2) + 4 (lane >> 5) + (r & 3)
+  const int chw = col0 + wn * (BN / WN);
+  // (statistics registers only in the STATS instantiation: the others keep the occupancy)
+  constexpr int SR = STATS ? 16 : 1;
+  float st1[TCH][SR], st2[TCH][SR], sft[TCH][SR];
+#pragma unroll
+  for (int ci = 0; ci < TCH; ++ci)
+#pragma unroll
+    for (int r = 0; r < SR; ++r) {
+      st1[ci][r] = st2[ci][r] = 0.f;
+      sft[ci][r] = (STATS && g.shift) ? g.shift[chw + 32 * ci + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3)] : 0.f;
+    }
+
+  f32x16 acc[TCH][TPX];
+#pragma unroll
+  for (int i = 0; i < TCH; ++i)
+#pragma unroll
+    for (int j = 0; j < TPX; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  constexpr int PER_STEP = PA + PB;
+#pragma unroll
+  for (int q = 0; q < S - 1; ++q)
+    if (q < nsteps) issue(q, q);
+  int gs = 0;
+  for (int tl = 0; tl < ntile; ++tl) {
+  for (int kt = 0; kt < nk; ++kt, ++gs) {
+    const int ahead = nsteps - 1 - gs < S - 2 ? nsteps - 1 - gs : S - 2;
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER_STEP) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_STEP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (gs + S - 1 < nsteps) issue(gs + S - 1, (gs + S - 1) % S);
+    const int cur = gs % S;
+    const uint16_t* at = a_buf(cur);
+    const uint16_t* bt = b_buf(cur);
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      s16x8 wf[TCH], xf[TPX];
+#pragma unroll
+      for (int i = 0; i < TCH; ++i) wf[i] = frag_k(bt, wn * (BN / WN) + 32 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TPX; ++j) xf[j] = frag_k(at, wm * (BMX / WM) + 32 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TCH; ++i)
+#pragma unroll
+        for (int j = 0; j < TPX; ++j) acc[i][j] = mfma<T>(wf[i], xf[j], acc[i][j]);
+    }
+  }
+    // ---- tile epilogue from registers (no LDS): 8-byte channel runs per pixel ----
+    const int tile = t_begin + tl;
+#pragma unroll
+    for (int j = 0; j < TPX; ++j) {
+      const int m = tile * BMX + wm * (BMX / WM) + 32 * j + (lane & 31);
+      if (m >= g.m) continue;
+      int64_t pix = m;
+      if (!g.ident) {
+        const int nimg = (int)fdiv((uint32_t)m, g.div_ohw), rem = m - nimg * ohw;
+        const int oy = (int)fdiv((uint32_t)rem, g.div_ow), ox = rem - oy * g.ow;
+        pix = ((int64_t)nimg * g.oht + oy * g.osh + g.oph) * g.owt + ox * g.osw + g.opw;
+      }
+#pragma unroll
+      for (int i = 0; i < TCH; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int ch = chw + 32 * i + 8 * q + 4 * (lane >> 5);
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+          if (g.scale || g.bias) {
+            const float4 s4 = g.scale ? *reinterpret_cast<const float4*>(g.scale + ch) : make_float4(1.f, 1.f, 1.f, 1.f);
+            const float4 b4 = g.bias ? *reinterpret_cast<const float4*>(g.bias + ch) : make_float4(0.f, 0.f, 0.f, 0.f);
+            v[0] = fmaf(v[0], s4.x, b4.x); v[1] = fmaf(v[1], s4.y, b4.y);
+            v[2] = fmaf(v[2], s4.z, b4.z); v[3] = fmaf(v[3], s4.w, b4.w);
+          }
+          const int64_t off = pix * g.kout + ch;
+          if (g.res) {
+            const uint2 rr = *reinterpret_cast<const uint2*>(g.res + off);
+            v[0] += to_f(T{(uint16_t)(rr.x & 0xffffu)}); v[1] += to_f(T{(uint16_t)(rr.x >> 16)});
+            v[2] += to_f(T{(uint16_t)(rr.y & 0xffffu)}); v[3] += to_f(T{(uint16_t)(rr.y >> 16)});
+          }
+          if (g.relu) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+          }
+          if (g.mask) {
+            const uint2 mm = *reinterpret_cast<const uint2*>(g.mask + off);
+            const uint16_t mk[4] = {(uint16_t)(mm.x & 0xffffu), (uint16_t)(mm.x >> 16), (uint16_t)(mm.y & 0xffffu),
+                                    (uint16_t)(mm.y >> 16)};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = to_f(T{mk[e]}) > 0.f ? v[e] : 0.f;
+          }
+          uint2 o;
+          o.x = (uint32_t)from_f<T>(v[0]).x | ((uint32_t)from_f<T>(v[1]).x << 16);
+          o.y = (uint32_t)from_f<T>(v[2]).x | ((uint32_t)from_f<T>(v[3]).x << 16);
+          *reinterpret_cast<uint2*>(Y + off) = o;
+          if constexpr (STATS) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float d = v[e] - sft[i][4 * q + e];
+              st1[i][4 * q + e] += d;
+              st2[i][4 * q + e] = fmaf(d, d, st2[i][4 * q + e]);
+            }
+          }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < TCH; ++i)
+#pragma unroll
+      for (int j = 0; j < TPX; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  }
+  if constexpr (!STATS) return;
+  // ---- statistics: fold the 32 pixels of each half-wave (xor shuffles), then the WM wave rows
+  // sharing a channel range through LDS in a fixed order, one row per workgroup ----
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < TCH; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+#pragma unroll
+      for (int sh = 1; sh < 32; sh <<= 1) {
+        st1[i][r] += __shfl_xor(st1[i][r], sh);
+        st2[i][r] += __shfl_xor(st2[i][r], sh);
+      }
+    }
+  float* red = reinterpret_cast<float*>(lds);  // [2][WM][BN]
+  if ((lane & 31) == 0) {
+#pragma unroll
+    for (int i = 0; i < TCH; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int c = wn * (BN / WN) + 32 * i + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3);
+        red[(0 * WM + wm) * BN + c] = st1[i][r];
+        red[(1 * WM + wm) * BN + c] = st2[i][r];
+      }
+  }
+  __syncthreads();
+  for (int i = tid; i < 2 * BN; i += C::THREADS) {
+    const int which = i / BN, c = i % BN;
+    float v = 0.f;
+    for (int w = 0; w < WM; ++w) v += red[(which * WM + w) * BN + c];
+    g.stats[((int64_t)which * sc.rows + p) * g.kout + col0 + c] = v;
+    // rows past the schedule's P are zero (the finalize sums every row)
+    for (int r2 = p + sc.P; r2 < sc.rows; r2 += sc.P) g.stats[((int64_t)which * sc.rows + r2) * g.kout + col0 + c] = 0.f;
   }
 }
 
@@ -895,13 +1164,21 @@ using FC4 = conv::FCfg<128, 4, 2, 2>;
 using FC5 = conv::FCfg<64, 8, 1, 2>;
 using FC6 = conv::FCfg<256, 2, 4, 2>;
 // fprop2 (BM, BN, WM x WN waves, stages)
-using F7 = conv::F2Cfg<256, 64, 4, 1, 3>;
+using F7 = conv::F2Cfg<256, 64, 8, 1, 2>;
 using F8 = conv::F2Cfg<256, 64, 4, 1, 2>;
 using F9 = conv::F2Cfg<256, 128, 4, 2, 2>;
 using F10 = conv::F2Cfg<128, 128, 2, 2, 3>;
 using F11 = conv::F2Cfg<128, 128, 2, 2, 2>;
 using F12 = conv::F2Cfg<256, 256, 2, 4, 2>;
 using F13 = conv::F2Cfg<128, 256, 2, 4, 2>;
+// fprop3 (persistent, transposed accumulators): BM pixels, BN channels, WM x WN waves, stages
+using F14 = conv::F3Cfg<256, 64, 8, 1, 2>;
+using F15 = conv::F3Cfg<128, 64, 4, 1, 2>;
+using F16 = conv::F3Cfg<128, 128, 4, 2, 2>;
+using F17 = conv::F3Cfg<128, 128, 2, 2, 2>;
+using F18 = conv::F3Cfg<256, 128, 4, 2, 2>;
+using F19 = conv::F3Cfg<128, 256, 2, 4, 2>;
+using F20 = conv::F3Cfg<256, 64, 4, 1, 2>;
 
 static int g_forced_cfg = [] {
   const char* e = std::getenv("APEX_AMD_CONV_CFG");
@@ -912,8 +1189,9 @@ void conv_force_fprop_cfg(int cfg) { g_forced_cfg = cfg; }
 
 static int fprop_cfg(const ConvTapArgs& a, int cus) { return plan::conv_fprop_cfg(a, cus, g_forced_cfg); }
 
-int conv_tap_stats_tiles(const ConvTapArgs& a) {
-  return (int)(((int64_t)a.n * a.oh * a.ow + plan::kConvStatsRows - 1) / plan::kConvStatsRows);
+int conv_tap_stats_tiles(const ConvTapArgs& a, int cus) {
+  const int bm = plan::conv_fprop_bm(fprop_cfg(a, cus));
+  return (int)(((int64_t)a.n * a.oh * a.ow + bm - 1) / bm);
 }
 
 void conv_tap_fprop(const ConvTapArgs& a, int cus, hipStream_t s) {
@@ -936,6 +1214,20 @@ void conv_tap_fprop(const ConvTapArgs& a, int cus, hipStream_t s) {
       hipLaunchKernelGGL((conv::fprop2_kernel<T, C>), dim3(grid), dim3(C::THREADS), C::LDS, s,
                          (const uint16_t*)a.in, (const uint16_t*)a.wt, (uint16_t*)a.out, g);
     };
+    auto go3 = [&](auto cfg_tag) {
+      using C = decltype(cfg_tag);
+      const int64_t tiles_m = (g.m + C::BM - 1) / C::BM, tiles_n = a.kout / C::BN;
+      const int per_cu = std::max(1, (int)((160 * 1024) / C::LDS));
+      int64_t P = std::max<int64_t>(1, (int64_t)cus * per_cu / tiles_n);
+      P = std::min(P, tiles_m);
+      conv::F3Sched sc{(int)P, (int)tiles_m};
+      if (g.stats)
+        hipLaunchKernelGGL((conv::fprop3_kernel<T, C, true>), dim3((unsigned)(P * tiles_n)), dim3(C::THREADS), C::LDS,
+                           s, (const uint16_t*)a.in, (const uint16_t*)a.wt, (uint16_t*)a.out, g, sc);
+      else
+        hipLaunchKernelGGL((conv::fprop3_kernel<T, C, false>), dim3((unsigned)(P * tiles_n)), dim3(C::THREADS), C::LDS,
+                           s, (const uint16_t*)a.in, (const uint16_t*)a.wt, (uint16_t*)a.out, g, sc);
+    };
     switch (cfg) {
       case 0: go(FC0{}); break;
       case 1: go(FC1{}); break;
@@ -950,7 +1242,14 @@ void conv_tap_fprop(const ConvTapArgs& a, int cus, hipStream_t s) {
       case 10: go2(F10{}); break;
       case 11: go2(F11{}); break;
       case 12: go2(F12{}); break;
-      default: go2(F13{}); break;
+      case 13: go2(F13{}); break;
+      case 14: go3(F14{}); break;
+      case 15: go3(F15{}); break;
+      case 16: go3(F16{}); break;
+      case 17: go3(F17{}); break;
+      case 18: go3(F18{}); break;
+      case 19: go3(F19{}); break;
+      default: go3(F20{}); break;
     }
   }, "conv_tap_fprop");
   check_launch("conv_tap_fprop");

@@ -45,6 +45,7 @@ struct ConvTapArgs {
   const void* mask = nullptr;
   // optional BN statistics of the fprop output (the consuming training-mode batch norm):
   // per-M-tile partial sums of (y - shift) and (y - shift)^2, [2][conv_tap_stats_tiles][kout]
+  // (rows = the chosen tile configuration's M tiles)
   // fp32, finalized by conv1x1_bn_finalize (no separate statistics pass over y)
   float* stats = nullptr;
   const float* stats_shift = nullptr;
@@ -56,7 +57,7 @@ bool conv_tap_supported(const ConvTapArgs& a);
 void conv_force_fprop_cfg(int cfg);
 void conv_tap_fprop(const ConvTapArgs& a, int cus, hipStream_t s);
 // number of M tiles of a tap fprop launch (the stats partial rows)
-int conv_tap_stats_tiles(const ConvTapArgs& a);
+int conv_tap_stats_tiles(const ConvTapArgs& a, int cus);
 
 // weight gradient: dw[k][t][c] = sum_{n,oh,ow} dy[n,oh,ow,k] * x[n, oh*ish + dh[t], ow*isw + dw[t], c]
 // (dy = `out` geometry with osh = osw = 1, oph = opw = 0; x = `in`).  fp32 result [kout][ntaps][c]

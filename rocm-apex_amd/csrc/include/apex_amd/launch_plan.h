@@ -13,7 +13,6 @@ namespace apex_amd {
 namespace plan {
 
 // ---- implicit-GEMM convolutions (csrc/conv/conv_igemm.hip) ----
-constexpr int kConvStatsRows = 128;  // fprop output rows per BN-statistics partial row
 constexpr int kWgradBK = 64;   // wgrad pixels per K-step
 
 struct WgPlan {
@@ -56,14 +55,17 @@ inline WgPlan conv_wgrad(const ConvTapArgs& a, int cus, int variant = 0) {
 }
 
 // fprop tile configurations (conv_igemm.hip): 0-6 = fprop_kernel (BM 256; the < 2 GiB-or-larger
-// fallback), 7-13 = fprop2_kernel (buffer-load staging, 64 x 64+ per wave).  (BM, BN) per index:
-constexpr int kConvCfgs = 14;
+// fallback), 7-13 = fprop2_kernel (buffer-load staging, 64 x 64+ per wave), 14-20 = fprop3_kernel
+// (persistent, transposed accumulators, register epilogue).  (BM, BN) per index:
+constexpr int kConvCfgs = 21;
 inline int conv_fprop_bm(int cfg) {
-  static const int bm[kConvCfgs] = {256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 128, 128, 256, 128};
+  static const int bm[kConvCfgs] = {256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 128,
+                                    128, 256, 128, 256, 128, 128, 128, 256, 128, 256};
   return cfg >= 0 && cfg < kConvCfgs ? bm[cfg] : 256;
 }
 inline int conv_fprop_bn(int cfg) {
-  static const int bn[kConvCfgs] = {128, 64, 128, 64, 128, 64, 256, 64, 64, 128, 128, 128, 256, 256};
+  static const int bn[kConvCfgs] = {128, 64, 128, 64, 128, 64, 256, 64, 64, 128, 128,
+                                    128, 256, 256, 64, 64, 128, 128, 128, 256, 64};
   return cfg >= 0 && cfg < kConvCfgs ? bn[cfg] : 64;
 }
 // fprop2 needs the input / weight byte ranges to fit a buffer descriptor (< 2 GiB)
@@ -71,14 +73,15 @@ inline bool conv_fprop2_ok(const ConvTapArgs& a) {
   const int64_t xb = (int64_t)a.n * a.ih * a.iw * a.c * 2, wb = (int64_t)a.kout * a.ntaps * a.c * 2;
   return xb < (1ll << 31) && wb < (1ll << 31);
 }
-// forced >= 0 overrides when legal.  Defaults from the r04 sweep of every ResNet-50 3x3 / strided
-// 1x1 shape, forward and data gradient, bs 256 (profiles/conv_cfg_sweep_r04.jsonl):
-//  * 64 output channels (stage 1): fprop_kernel 8 waves x 32 x 64, 2 stages (cfg 5, two
-//    workgroups / 16 waves per CU hide the 9-step K loop's load latency: 108 us vs 134 for the
-//    best fprop2 tile);
-//  * otherwise fprop2: 256 x 256 (cfg 12) while it still gives >= 3/4 of a wave of workgroups,
-//    else 128 x 128 (cfg 11) — 5-20 % faster than the fprop_kernel choices at stages 2-4
-//    (e.g. 7 x 7 x 512: 67.7 vs 83.3 us forward, 82.9 vs 97.3 us data gradient)
+// forced >= 0 overrides when legal.  Defaults from the r04 sweeps of every ResNet-50 3x3 / strided
+// 1x1 shape, forward and data gradient, bs 256 (profiles/conv_cfg_sweep_r04{,b}.jsonl):
+//  * <= 128 output channels: fprop2 8 waves x (32 px x 64 ch), 2 stages (cfg 7, two workgroups /
+//    16 waves per CU: 109 us at 56x56x64 vs 111 for fprop_kernel's cfg 5, 88.7 vs 90.8 at
+//    28x28x128);
+//  * wider: fprop2 256 x 256 (cfg 12) while it still gives >= 3/4 of a wave of workgroups, else
+//    128 x 128 (cfg 11) — 5-20 % faster than the fprop_kernel choices at stages 2-4.
+// The persistent fprop3 tiles (cfg 14-20) measured within +-5 % of these (no fill / drain to
+// win at 16 waves per CU) and stay opt-in.  > 2 GiB operands: fprop_kernel (r02 choices).
 inline int conv_fprop_cfg(const ConvTapArgs& a, int cus, int forced) {
   auto ok = [&](int cfg) {
     return a.kout % conv_fprop_bn(cfg) == 0 && (cfg < 7 || conv_fprop2_ok(a));
@@ -88,9 +91,11 @@ inline int conv_fprop_cfg(const ConvTapArgs& a, int cus, int forced) {
   auto tiles = [&](int cfg) {
     return (m + conv_fprop_bm(cfg) - 1) / conv_fprop_bm(cfg) * (a.kout / conv_fprop_bn(cfg));
   };
-  if (conv_fprop2_ok(a) && a.kout % 128 == 0) {
+  if (conv_fprop2_ok(a)) {
+    if (a.kout <= 128) return 7;
     if (a.kout % 256 == 0 && 4 * tiles(12) >= 3 * (int64_t)cus) return 12;
-    return 11;
+    if (a.kout % 128 == 0) return 11;
+    return 7;
   }
   const int64_t tiles_m = (m + 255) / 256;
   if (a.kout <= 128) return 5;

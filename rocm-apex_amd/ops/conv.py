@@ -173,11 +173,8 @@ def conv_tap_forward(x, w, stride, pad, stats_shift=None):
     y = torch.empty((n, kout, oh, ow), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
     taps = _fwd_taps(k, pad)
     ext = _conv_ext()
-    part = None
-    if stats_shift is not None:
-        part = torch.empty((2, ext.tap_stats_tiles(n, oh, ow), kout), dtype=torch.float32, device=x.device)
-    ext.tap_fprop(_nhwc(x), _w_krc(w).contiguous(), _nhwc(y), oh, ow, stride, stride, 1, 1, 0, 0,
-                  [t[0] for t in taps], [t[1] for t in taps], stats=part, stats_shift=stats_shift)
+    part = ext.tap_fprop(_nhwc(x), _w_krc(w).contiguous(), _nhwc(y), oh, ow, stride, stride, 1, 1, 0, 0,
+                         [t[0] for t in taps], [t[1] for t in taps], stats_shift=stats_shift)
     return y if stats_shift is None else (y, part)
 
 

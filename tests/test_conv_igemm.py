@@ -99,7 +99,7 @@ CFG_SHAPES = [
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", list(range(14)))
+@pytest.mark.parametrize("cfg", list(range(21)))
 @pytest.mark.parametrize("cin,cout,stride,h,batch", CFG_SHAPES)
 def test_gpu_conv_tap_every_tile_config(cfg, cin, cout, stride, h, batch):
     """Every fprop tile configuration (0-6 fprop_kernel, 7-13 fprop2_kernel: buffer-load staging
@@ -110,7 +110,7 @@ def test_gpu_conv_tap_every_tile_config(cfg, cin, cout, stride, h, batch):
     from apex.ops import conv as C
 
     ext = _native.require("conv").conv
-    bn = [128, 64, 128, 64, 128, 64, 256, 64, 64, 128, 128, 128, 256, 256][cfg]
+    bn = [128, 64, 128, 64, 128, 64, 256, 64, 64, 128, 128, 128, 256, 256, 64, 64, 128, 128, 128, 256, 64][cfg]
     if cout % bn:
         pytest.skip("tile wider than the output")
     torch.manual_seed(cfg * 7 + cin)

@@ -37,8 +37,8 @@ def main():
              "miopen_fwd_us": round(timeit(lambda: F.conv2d(x, w, None, st, pad)) * 1e6, 1),
              "miopen_dgrad_us": round(timeit(lambda: torch.ops.aten.convolution_backward(
                  gy, x, w, None, *args, [True, False, False])) * 1e6, 1)}
-        for cfg in range(14):
-            bn = [128, 64, 128, 64, 128, 64, 256, 64, 64, 128, 128, 128, 256, 256][cfg]
+        for cfg in range(21):
+            bn = [128, 64, 128, 64, 128, 64, 256, 64, 64, 128, 128, 128, 256, 256, 64, 64, 128, 128, 128, 256, 64][cfg]
             if cout % bn:
                 continue
             ext.force_fprop_cfg(cfg)
