@@ -326,6 +326,113 @@ at::Tensor wgrad3x3(const at::Tensor& dy, const at::Tensor& x, int64_t stride, c
   return dw.permute({0, 3, 1, 2});  // [K, C, 3, 3] in channels_last memory
 }
 
+// ---- ResNet stem (csrc/conv/stem.hip): activations are torch channels_last tensors ----
+void check_cl(const at::Tensor& t, int64_t c, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 4 && t.size(1) == c && t.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem: ", what, " must be a channels_last [N, ", c, ", H, W] GPU tensor");
+}
+
+// x [N, cin <= 4, H, W] image (any strides, fp32 / fp16 / bf16), w [64, cin, 7, 7] (compute dtype),
+// shift [64] fp32 (statistics shift, the running mean) -> (y [N, 64, OH, OW] channels_last,
+// statistics partials [2, G, 64], the halo'd NHWC4 image for the weight gradient)
+std::vector<at::Tensor> stem_fprop_b(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& shift) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.size(1) >= 1 && x.size(1) <= 4, "stem: x must be [N, 1-4, H, W] on the GPU");
+  TORCH_CHECK(w.is_cuda() && w.dim() == 4 && w.size(0) == 64 && w.size(1) == x.size(1) && w.size(2) == 7 && w.size(3) == 7,
+              "stem: w must be [64, cin, 7, 7]");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 || w.scalar_type() == at::kHalf, "stem: bf16 / fp16 weights");
+  if (shift.has_value())
+    TORCH_CHECK(shift->is_cuda() && shift->scalar_type() == at::kFloat && shift->is_contiguous() && shift->numel() == 64,
+                "stem: shift must be contiguous fp32 [64]");
+  const c10::hip::HIPGuard guard(x.get_device());
+  const int n = (int)x.size(0), cin = (int)x.size(1), h = (int)x.size(2), wd = (int)x.size(3);
+  int oh, ow, hp, wp, ph, pw;
+  stem_geometry(n, h, wd, &oh, &ow, &hp, &wp, &ph, &pw);
+  const int cus = device_cus(x.get_device());
+  const int t = dtype_code(w.scalar_type());
+  auto opt = w.options();
+  auto xp = at::empty({n, hp, wp, 4}, opt);
+  auto wpk = at::empty({64, 224}, opt);
+  auto y = at::empty({n, 64, oh, ow}, opt.memory_format(at::MemoryFormat::ChannelsLast));
+  auto part = at::empty({2, stem_fprop_rows(cus), 64}, opt.dtype(at::kFloat));
+  const int64_t xs[4] = {x.stride(0), x.stride(1), x.stride(2), x.stride(3)};
+  const int64_t wsd[4] = {w.stride(0), w.stride(1), w.stride(2), w.stride(3)};
+  stem_pad(x.data_ptr(), dtype_code(x.scalar_type()), n, cin, h, wd, xs, xp.data_ptr(), t, cus, cur_stream());
+  stem_wpack(w.data_ptr(), t, cin, wsd, wpk.data_ptr(), t, cur_stream());
+  stem_fprop(xp.data_ptr(), wpk.data_ptr(), shift.has_value() ? shift->data_ptr<float>() : nullptr, y.data_ptr(),
+             part.data_ptr<float>(), n, h, wd, t, cus, cur_stream());
+  return {y, part, xp};
+}
+
+void check_coef(const at::Tensor& c, int64_t n, const char* what) {
+  TORCH_CHECK(c.is_cuda() && c.scalar_type() == at::kFloat && c.is_contiguous() && c.numel() == n, "stem: ", what,
+              " must be contiguous fp32 [", n, "]");
+}
+
+// y [N, 64, OH, OW] channels_last, coef [128] scale | shift -> (pooled [N, 64, PH, PW] channels_last,
+// window indices [N, PH, PW, 64] uint8)
+std::vector<at::Tensor> stem_pool_b(const at::Tensor& y, const at::Tensor& coef) {
+  check_cl(y, 64, "y");
+  check_coef(coef, 128, "coef");
+  const c10::hip::HIPGuard guard(y.get_device());
+  const int n = (int)y.size(0), oh = (int)y.size(2), ow = (int)y.size(3);
+  const int ph = (oh - 1) / 2 + 1, pw = (ow - 1) / 2 + 1;
+  auto p = at::empty({n, 64, ph, pw}, y.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto idx = at::empty({n, ph, pw, 64}, y.options().dtype(at::kByte));
+  stem_pool_fwd(y.data_ptr(), coef.data_ptr<float>(), p.data_ptr(), idx.data_ptr<uint8_t>(), n, 2 * oh, 2 * ow,
+                dtype_code(y.scalar_type()), device_cus(y.get_device()), cur_stream());
+  return {p, idx};
+}
+
+void check_bwd(const at::Tensor& dp, const at::Tensor& idx, const at::Tensor& y) {
+  check_cl(y, 64, "y");
+  check_cl(dp, 64, "dp");
+  const int64_t oh = y.size(2), ow = y.size(3);
+  TORCH_CHECK(dp.scalar_type() == y.scalar_type() && dp.size(0) == y.size(0) && dp.size(2) == (oh - 1) / 2 + 1 &&
+                  dp.size(3) == (ow - 1) / 2 + 1,
+              "stem: pooled gradient does not match y");
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kByte && idx.is_contiguous() && idx.dim() == 4 &&
+                  idx.size(0) == dp.size(0) && idx.size(1) == dp.size(2) && idx.size(2) == dp.size(3) && idx.size(3) == 64,
+              "stem: idx must be the forward's [N, PH, PW, 64] uint8 indices");
+}
+
+// [2, G, 64] partials of sum(g), sum(g * (y - mean)); g = ReLU-masked pool backward of dp
+at::Tensor stem_reduce_b(const at::Tensor& dp, const at::Tensor& idx, const at::Tensor& y, const at::Tensor& coef,
+                         const at::Tensor& mean) {
+  check_bwd(dp, idx, y);
+  check_coef(coef, 128, "coef");
+  check_coef(mean, 64, "mean");
+  const c10::hip::HIPGuard guard(y.get_device());
+  const int cus = device_cus(y.get_device());
+  auto part = at::empty({2, stem_reduce_rows(cus), 64}, y.options().dtype(at::kFloat));
+  stem_bwd_reduce(dp.data_ptr(), idx.data_ptr<uint8_t>(), y.data_ptr(), coef.data_ptr<float>(), mean.data_ptr<float>(),
+                  part.data_ptr<float>(), (int)y.size(0), 2 * (int)y.size(2), 2 * (int)y.size(3),
+                  dtype_code(y.scalar_type()), cus, cur_stream());
+  return part;
+}
+
+// weight gradient [64, cin, 7, 7] (w's strides and dtype); cb [192] = the BN backward's A | B | K
+at::Tensor stem_wgrad_b(const at::Tensor& dp, const at::Tensor& idx, const at::Tensor& y, const at::Tensor& coef,
+                        const at::Tensor& cb, const at::Tensor& xp, const at::Tensor& w) {
+  check_bwd(dp, idx, y);
+  check_coef(coef, 128, "coef");
+  check_coef(cb, 192, "cb");
+  const int n = (int)y.size(0), oh = (int)y.size(2), ow = (int)y.size(3);
+  TORCH_CHECK(xp.is_cuda() && xp.is_contiguous() && xp.dim() == 4 && xp.size(0) == n && xp.size(1) == 2 * (oh - 1) + 7 &&
+                  xp.size(2) == 2 * (ow - 1) + 8 && xp.size(3) == 4 && xp.scalar_type() == y.scalar_type(),
+              "stem: xp must be the forward's halo'd image");
+  TORCH_CHECK(w.dim() == 4 && w.size(0) == 64 && w.size(1) >= 1 && w.size(1) <= 4 && w.size(2) == 7 && w.size(3) == 7,
+              "stem: w must be [64, cin, 7, 7]");
+  const c10::hip::HIPGuard guard(y.get_device());
+  const int cus = device_cus(y.get_device());
+  auto dw = at::empty_like(w);
+  auto ws = at::empty({(int64_t)stem_wgrad_parts(cus) * 64 * 224}, y.options().dtype(at::kFloat));
+  const int64_t st[4] = {dw.stride(0), dw.stride(1), dw.stride(2), dw.stride(3)};
+  stem_wgrad(dp.data_ptr(), idx.data_ptr<uint8_t>(), y.data_ptr(), coef.data_ptr<float>(), cb.data_ptr<float>(),
+             xp.data_ptr(), ws.data_ptr<float>(), dw.data_ptr(), dtype_code(dw.scalar_type()), (int)w.size(1), st, n,
+             2 * oh, 2 * ow, dtype_code(y.scalar_type()), cus, cur_stream());
+  return dw;
+}
+
 }  // namespace
 
 void bind_conv(pybind11::module_& root) {
@@ -354,6 +461,10 @@ void bind_conv(pybind11::module_& root) {
   m.def("bnbwd_finalize", &bnbwd_finalize);
   m.def("part_payload", &part_payload, pybind11::arg("part"), pybind11::arg("count"),
         pybind11::arg("shift") = pybind11::none());
+  m.def("stem_fprop", &stem_fprop_b, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("shift") = pybind11::none());
+  m.def("stem_pool", &stem_pool_b);
+  m.def("stem_reduce", &stem_reduce_b);
+  m.def("stem_wgrad", &stem_wgrad_b);
   m.def("wgrad1x1", &wgrad1x1, pybind11::arg("g"), pybind11::arg("x"), pybind11::arg("xcoef") = pybind11::none(),
         pybind11::arg("out_dtype") = pybind11::none());
 }

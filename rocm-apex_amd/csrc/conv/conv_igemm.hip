@@ -27,6 +27,7 @@
 #include "apex_amd/conv_api.h"
 #include "apex_amd/device.h"
 #include "apex_amd/dispatch.h"
+#include "apex_amd/fastdiv.h"
 #include "apex_amd/launch_plan.h"
 
 #include <algorithm>
@@ -44,29 +45,6 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // 128 bytes of zeros: the DMA source for padding taps and rows past the end
 __device__ __attribute__((aligned(16))) uint16_t g_zero[64];
-
-// exact unsigned 32-bit division by a runtime-constant divisor (Granlund-Montgomery, round-up
-// multiplier with the "add" fix-up): q = (t + ((n - t) >> s1)) >> s2, t = umulhi(n, mul).  Four
-// VALU ops instead of the ~30 of a v_rcp-based integer divide.
-struct FastDiv {
-  uint32_t d, mul, s1, s2;
-};
-
-inline FastDiv make_fastdiv(uint32_t d) {
-  FastDiv f;
-  f.d = d;
-  uint32_t l = 0;
-  while ((1ull << l) < d) ++l;
-  f.mul = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
-  f.s1 = l > 0 ? 1 : 0;
-  f.s2 = l > 0 ? l - 1 : 0;
-  return f;
-}
-
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
-  const uint32_t t = __umulhi(n, f.mul);
-  return (t + ((n - t) >> f.s1)) >> f.s2;
-}
 
 struct Geo {
   int n, h, w, c, oh, ow, oht, owt, kout, ish, isw, osh, osw, oph, opw, ntaps, m;

@@ -1,0 +1,706 @@
+// ResNet stem for gfx950: 7x7/2 convolution (<= 4 input channels -> 64) + training batch norm +
+// ReLU + 3x3/2 max pool, forward and backward, in five native kernels.
+//
+// Reference capability: the stem of the reference's ResNet-50 examples (torchvision conv1 /
+// bn1 / relu / maxpool run as four library ops: examples/imagenet/main_amp.py), with the BN on
+// apex's NHWC kernels (apex/contrib/csrc/groupbn).  Composition here (MI355X-first):
+//
+//  forward   pad_kernel    image [N, C<=4, H, W] (any strides) -> halo'd NHWC4 image
+//                          XP [N][HP][WP][4] (zero halo of 3): the convolution then needs no
+//                          bounds checks and every k-chunk is a 16-byte aligned load
+//            fprop_kernel  implicit GEMM with K = 7 kernel rows x 32 (8 columns x 4 channels; the
+//                          8th column carries zero weights): for an output pixel and kernel row r
+//                          the 32 k-values are 64 CONTIGUOUS bytes of XP.  Swapped product
+//                          Y^T = W . A^T: the weights are the MFMA A operand, resident in
+//                          registers for the whole kernel (28 fragments); each lane's B fragment
+//                          is one 16-byte load of its pixel's row chunk; 32 pixels x 64 channels
+//                          per wave-tile = 28 MFMAs.  Channel rows are permuted so every lane holds
+//                          16 consecutive channels of its pixel (two 16-byte stores); BN statistics
+//                          (shift-centred sums) accumulate in registers and are folded once per
+//                          workgroup (one partial row per workgroup).
+//            pool_fwd      BN apply + ReLU + 3x3/2 max pool with the window separable: each lane
+//                          walks a strip of pooled rows, keeping the horizontal max of the shared
+//                          input row (6 loads per output instead of 9); 1-byte window indices.
+//  backward  bwd_reduce    pool-backward gather + ReLU mask + BN backward sums in ONE pass over y
+//                          (the full-resolution gradient is never written)
+//            wgrad_kernel  dW = dX^T . im2col(XP) with dX = A g + B y + K recomputed from the
+//                          pooled gradient, the window indices and y as the operand prologue; both
+//                          operands staged pixel-major in LDS and fed with ds_read_b64_tr_b16;
+//                          split over pixels, fp32 partials reduced in a fixed order.
+// Against the library path (CK / MIOpen convolution on a channel-padded copy, BN statistics pass,
+// apply+pool, pool backward writing the full-resolution gradient, BN reduction + dx passes, MIOpen
+// weight gradient) this drops three full-resolution (N x 112 x 112 x 64) passes and moves both
+// convolutions onto hand-written MFMA kernels.
+#include "apex_amd/conv_api.h"
+#include "apex_amd/device.h"
+#include "apex_amd/dispatch.h"
+#include "apex_amd/fastdiv.h"
+#include "apex_amd/mfma.h"
+
+#include <stdexcept>
+
+namespace apex_amd {
+namespace stem {
+using namespace mfma;
+
+constexpr int CO = 64;          // output channels
+constexpr int KROW = 32;        // k per kernel row: 8 columns x 4 channels
+constexpr int KT = 7 * KROW;    // 224
+constexpr int NKS = KT / 16;    // 14 MFMA k-steps
+
+struct Geo {
+  int n, h, w, cin;
+  int oh, ow, hp, wp, ph, pw;
+  uint32_t m;  // n * oh * ow
+};
+
+inline Geo geo_of(int n, int h, int w, int cin) {
+  Geo g;
+  g.n = n;
+  g.h = h;
+  g.w = w;
+  g.cin = cin;
+  g.oh = (h - 1) / 2 + 1;
+  g.ow = (w - 1) / 2 + 1;
+  g.hp = 2 * (g.oh - 1) + 7;
+  g.wp = 2 * (g.ow - 1) + 8;
+  g.ph = (g.oh - 1) / 2 + 1;
+  g.pw = (g.ow - 1) / 2 + 1;
+  g.m = (uint32_t)((int64_t)n * g.oh * g.ow);
+  return g;
+}
+
+// ---- image -> halo'd NHWC4 ---------------------------------------------------------------
+template <typename TI, typename T>
+__global__ void __launch_bounds__(256) pad_kernel(const TI* __restrict__ x, int64_t sn, int64_t sc, int64_t sh,
+                                                  int64_t sw, const Geo g, T* __restrict__ xp) {
+  const uint32_t total = (uint32_t)g.n * g.hp * g.wp;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const int j = (int)(i % (uint32_t)g.wp);
+    const uint32_t r = i / (uint32_t)g.wp;
+    const int ii = (int)(r % (uint32_t)g.hp), nn = (int)(r / (uint32_t)g.hp);
+    const int ih = ii - 3, iw = j - 3;
+    uint16_t v[4] = {0, 0, 0, 0};
+    if (ih >= 0 && ih < g.h && iw >= 0 && iw < g.w) {
+      const TI* src = x + nn * sn + ih * sh + iw * sw;
+      for (int c = 0; c < g.cin; ++c) v[c] = from_f<T>(to_f(src[c * sc])).x;
+    }
+    *reinterpret_cast<uint2*>(xp + (size_t)i * 4) =
+        make_uint2(v[0] | ((uint32_t)v[1] << 16), v[2] | ((uint32_t)v[3] << 16));
+  }
+}
+
+// ---- weights [64, cin, 7, 7] (any strides) -> [64][224] with k = r * 32 + s * 4 + c -------
+template <typename TW, typename T>
+__global__ void __launch_bounds__(256) wpack_kernel(const TW* __restrict__ w, int cin, int64_t s0, int64_t s1,
+                                                    int64_t s2, int64_t s3, T* __restrict__ wp) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= CO * KT) return;
+  const int co = i / KT, k = i % KT, r = k / KROW, s = (k % KROW) / 4, c = k % 4;
+  const float v = (s < 7 && c < cin) ? to_f(w[co * s0 + c * s1 + r * s2 + s * s3]) : 0.f;
+  wp[i] = from_f<T>(v);
+}
+
+// ---- forward convolution + BN statistics ------------------------------------------------------
+struct FpArgs {
+  const uint16_t* xp;
+  const uint16_t* wp;     // [64][224]
+  const float* shift;     // [64] statistics shift (the running mean)
+  uint16_t* y;            // [M][64]
+  float* part;            // [2][G][64]
+  Geo g;
+  FastDiv div_ohw, div_ow;
+  int tiles;              // ceil(M / 32)
+};
+
+// MFMA row m of channel tile t holds channel 32 t + perm(m): lane half h then owns channels
+// 16 h .. 16 h + 15 of the tile in accumulator registers r = 0..15 (crow(r, h) -> 16 h + r)
+__device__ __forceinline__ int chan_of_row(int m) { return 16 * ((m >> 2) & 1) + (m & 3) + 4 * (m >> 3); }
+
+template <typename T>
+__global__ void __launch_bounds__(256, 1) fprop_kernel(const FpArgs a) {
+  __shared__ float red[4 * 64 * 33];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, pl = lane & 31;
+  const Geo& g = a.g;
+  s16x8 wa[2][NKS];
+  const int chm = chan_of_row(pl);
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+      wa[t][ks] = *reinterpret_cast<const s16x8*>(a.wp + (32 * t + chm) * KT + 16 * ks + 8 * h);
+  float sft[2][16], s1[2][16], s2[2][16];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sft[t][r] = a.shift ? a.shift[32 * t + 16 * h + r] : 0.f;
+      s1[t][r] = s2[t][r] = 0.f;
+    }
+  const int nw = gridDim.x * 4, gw = blockIdx.x * 4 + wave;
+  const int t0 = (int)((int64_t)gw * a.tiles / nw), t1 = (int)((int64_t)(gw + 1) * a.tiles / nw);
+  const size_t rowstep = (size_t)g.wp * 4;
+
+  auto src_of = [&](int tile, uint32_t& p) -> const uint16_t* {
+    p = (uint32_t)tile * 32 + pl;
+    const uint32_t pc = p < g.m ? p : g.m - 1;
+    const uint32_t nn = fdiv(pc, a.div_ohw), rem = pc - nn * a.div_ohw.d;
+    const uint32_t oh = fdiv(rem, a.div_ow), ow = rem - oh * a.div_ow.d;
+    return a.xp + ((size_t)(nn * g.hp + 2 * oh) * g.wp + 2 * ow) * 4 + 8 * h;
+  };
+  auto load = [&](s16x8 (&b)[NKS], const uint16_t* src) {
+#pragma unroll
+    for (int r = 0; r < 7; ++r)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) b[2 * r + q] = *reinterpret_cast<const s16x8*>(src + r * rowstep + 16 * q);
+  };
+  auto step = [&](const s16x8 (&b)[NKS], uint32_t p) {
+    f32x16 acc[2] = {zero16(), zero16()};
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      acc[0] = mma<T>(wa[0][ks], b[ks], acc[0]);
+      acc[1] = mma<T>(wa[1][ks], b[ks], acc[1]);
+    }
+    if (p >= g.m) return;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      uint32_t wv[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const T lo = from_f<T>(acc[t][2 * i]), hi = from_f<T>(acc[t][2 * i + 1]);
+        wv[i] = (uint32_t)lo.x | ((uint32_t)hi.x << 16);
+        const float vl = to_f(lo) - sft[t][2 * i], vh = to_f(hi) - sft[t][2 * i + 1];
+        s1[t][2 * i] += vl;
+        s2[t][2 * i] = fmaf(vl, vl, s2[t][2 * i]);
+        s1[t][2 * i + 1] += vh;
+        s2[t][2 * i + 1] = fmaf(vh, vh, s2[t][2 * i + 1]);
+      }
+      uint4* dst = reinterpret_cast<uint4*>(a.y + (size_t)p * CO + 32 * t + 16 * h);
+      dst[0] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+      dst[1] = make_uint4(wv[4], wv[5], wv[6], wv[7]);
+    }
+  };
+
+  // double-buffered: the next tile's 14 loads are in flight under this tile's 28 MFMAs
+  s16x8 b0[NKS], b1[NKS];
+  uint32_t p0 = 0, p1 = 0;
+  if (t0 < t1) load(b0, src_of(t0, p0));
+  if (t0 + 1 < t1) load(b1, src_of(t0 + 1, p1));
+  for (int tile = t0; tile < t1; tile += 2) {
+    step(b0, p0);
+    if (tile + 2 < t1) load(b0, src_of(tile + 2, p0));
+    if (tile + 1 < t1) {
+      step(b1, p1);
+      if (tile + 3 < t1) load(b1, src_of(tile + 3, p1));
+    }
+  }
+
+  // fold the statistics: per-lane sums -> LDS -> one row per workgroup (fixed order)
+  const int ch = threadIdx.x & 63, which = threadIdx.x >> 6;  // which: 0 = s1, 1 = s2 (threads < 128)
+  for (int pass = 0; pass < 2; ++pass) {
+    float* row = red + (wave * 64 + lane) * 33;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) row[16 * t + r] = pass == 0 ? s1[t][r] : s2[t][r];
+    __syncthreads();
+    if (which == pass) {
+      const int t = ch >> 5, hh = (ch >> 4) & 1, r = ch & 15;
+      float acc = 0.f;
+      for (int w = 0; w < 4; ++w)
+        for (int l = 0; l < 32; ++l) acc += red[(w * 64 + 32 * hh + l) * 33 + 16 * t + r];
+      a.part[((size_t)pass * gridDim.x + blockIdx.x) * CO + ch] = acc;
+    }
+    __syncthreads();
+  }
+}
+
+// ---- BN apply + ReLU + 3x3/2 max pool (pad 1) -------------------------------------------------
+constexpr int PR = 4;  // pooled rows per lane
+
+struct PoolArgs {
+  const uint16_t* y;   // [N][OH][OW][64]
+  const float* coef;   // [2][64] scale | shift
+  uint16_t* p;         // [N][PH][PW][64]
+  uint8_t* idx;        // [N][PH][PW][64] window index kh * 3 + kw
+  Geo g;
+  int strips;
+};
+
+template <typename T>
+__device__ __forceinline__ void hbest(const PoolArgs& a, int nn, int yr, int pw, int c8, const float (&sc)[8],
+                                      const float (&sh)[8], float (&hv)[8], int (&hk)[8]) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    hv[e] = -INFINITY;
+    hk[e] = 0;
+  }
+  if (yr < 0 || yr >= a.g.oh) return;
+  const uint16_t* row = a.y + ((size_t)(nn * a.g.oh + yr) * a.g.ow) * CO + c8 * 8;
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    const int col = 2 * pw - 1 + b;
+    if (col < 0 || col >= a.g.ow) continue;
+    float v[8];
+    Vec8<T>::load(v, reinterpret_cast<const T*>(row + (size_t)col * CO));
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      // the value the unfused apply pass would store, so argmax ties resolve identically
+      const float o = to_f(from_f<T>(fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f)));
+      if (o > hv[e]) {
+        hv[e] = o;
+        hk[e] = b;
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) pool_fwd_kernel(const PoolArgs a) {
+  const Geo& g = a.g;
+  const uint32_t total = (uint32_t)g.n * a.strips * g.pw * 8;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const int c8 = (int)(i & 7);
+    uint32_t r = i >> 3;
+    const int pw = (int)(r % (uint32_t)g.pw);
+    r /= (uint32_t)g.pw;
+    const int strip = (int)(r % (uint32_t)a.strips), nn = (int)(r / (uint32_t)a.strips);
+    float sc[8], sh[8];
+    Vec8<float>::load(sc, a.coef + c8 * 8);
+    Vec8<float>::load(sh, a.coef + CO + c8 * 8);
+    const int ph0 = strip * PR;
+    float cv[8];
+    int ck[8];
+    hbest<T>(a, nn, 2 * ph0 - 1, pw, c8, sc, sh, cv, ck);
+#pragma unroll 1
+    for (int j = 0; j < PR; ++j) {
+      const int ph = ph0 + j;
+      if (ph >= g.ph) break;
+      float v1[8], v2[8];
+      int k1[8], k2[8];
+      hbest<T>(a, nn, 2 * ph, pw, c8, sc, sh, v1, k1);
+      hbest<T>(a, nn, 2 * ph + 1, pw, c8, sc, sh, v2, k2);
+      float best[8];
+      uint32_t bi[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        // row-major first maximum: rows in order, strict > (same as the window scan)
+        best[e] = cv[e];
+        bi[e] = (uint32_t)ck[e];
+        if (v1[e] > best[e]) {
+          best[e] = v1[e];
+          bi[e] = 3u + (uint32_t)k1[e];
+        }
+        if (v2[e] > best[e]) {
+          best[e] = v2[e];
+          bi[e] = 6u + (uint32_t)k2[e];
+        }
+        cv[e] = v2[e];
+        ck[e] = k2[e];
+      }
+      const size_t o = ((size_t)(nn * g.ph + ph) * g.pw + pw) * CO + c8 * 8;
+      Vec8<T>::store(reinterpret_cast<T*>(a.p + o), best);
+      *reinterpret_cast<uint2*>(a.idx + o) = make_uint2(bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24),
+                                                        bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24));
+    }
+  }
+}
+
+// ---- backward: pool gather + ReLU mask (+ BN backward) ----------------------------------------
+struct BwdArgs {
+  const uint16_t* dp;     // [N][PH][PW][64] pooled gradient
+  const uint8_t* idx;     // [N][PH][PW][64]
+  const uint16_t* y;      // [M][64] convolution output (BN input)
+  const float* coef;      // [2][64] forward scale | shift (ReLU mask recompute)
+  const float* mean;      // [64] batch mean
+  const float* cb;        // [3][64] dx = A g + B y + K
+  const uint16_t* xp;     // halo'd image
+  float* part;            // bwd_reduce: [2][G][64]
+  float* ws;              // wgrad: [G][64][224]
+  Geo g;
+  FastDiv div_ohw, div_ow;
+  uint32_t chunk;         // wgrad: pixels per workgroup (multiple of 64)
+};
+
+// raw loads of one (pixel, 8-channel) item's pooled-gradient windows: <= 2 x 2 windows contain a
+// stride-2 / size-3 / pad-1 pool input pixel
+struct Gather {
+  uint2 ix[4];
+  uint4 gv[4];
+  uint32_t kk[4];  // window index the pixel has in each window (255: no window)
+};
+
+__device__ __forceinline__ void gather_issue(const BwdArgs& a, uint32_t nn, int yh, int yw, int c8, Gather& G) {
+  const int hh = yh + 1, ww = yw + 1;
+  const int ph_lo = hh >= 3 ? ((hh - 3) >> 1) + 1 : 0, ph_hi = min(a.g.ph - 1, hh >> 1);
+  const int pw_lo = ww >= 3 ? ((ww - 3) >> 1) + 1 : 0, pw_hi = min(a.g.pw - 1, ww >> 1);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int ph = ph_lo + (s >> 1), pw = pw_lo + (s & 1);
+    if (ph <= ph_hi && pw <= pw_hi) {
+      G.kk[s] = (uint32_t)((hh - 2 * ph) * 3 + (ww - 2 * pw));
+      const size_t o = ((size_t)(nn * a.g.ph + ph) * a.g.pw + pw) * CO + c8 * 8;
+      G.ix[s] = *reinterpret_cast<const uint2*>(a.idx + o);
+      G.gv[s] = *reinterpret_cast<const uint4*>(a.dp + o);
+    } else {
+      G.kk[s] = 255u;  // never matches a stored index (0..8)
+      G.ix[s] = make_uint2(0, 0);
+      G.gv[s] = make_uint4(0, 0, 0, 0);
+    }
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void gather_sum(const Gather& G, float (&gs)[8]) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) gs[e] = 0.f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const uint32_t w[2] = {G.ix[s].x, G.ix[s].y};
+    const uint32_t gw[4] = {G.gv[s].x, G.gv[s].y, G.gv[s].z, G.gv[s].w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const uint32_t k = (w[e >> 2] >> (8 * (e & 3))) & 0xffu;
+      const float v = to_f(T{(uint16_t)((gw[e >> 1] >> (16 * (e & 1))) & 0xffffu)});
+      gs[e] += k == G.kk[s] ? v : 0.f;
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bwd_reduce_kernel(const BwdArgs a) {
+  __shared__ float red[2][32][CO + 1];
+  const int tid = threadIdx.x, c8 = tid & 7;
+  float sc[8], sh[8], mu[8], a1[8], a2[8];
+  Vec8<float>::load(sc, a.coef + c8 * 8);
+  Vec8<float>::load(sh, a.coef + CO + c8 * 8);
+  Vec8<float>::load(mu, a.mean + c8 * 8);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a1[e] = a2[e] = 0.f;
+  const uint32_t total = a.g.m * 8u;
+  for (uint32_t i = blockIdx.x * 256u + tid; i < total; i += gridDim.x * 256u) {
+    const uint32_t pix = i >> 3;
+    const uint32_t nn = fdiv(pix, a.div_ohw), rem = pix - nn * a.div_ohw.d;
+    const uint32_t yh = fdiv(rem, a.div_ow), yw = rem - yh * a.div_ow.d;
+    Gather G;
+    gather_issue(a, nn, (int)yh, (int)yw, c8, G);
+    float v[8], gs[8];
+    Vec8<T>::load(v, reinterpret_cast<const T*>(a.y + (size_t)pix * CO + c8 * 8));
+    gather_sum<T>(G, gs);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float gm = fmaf(v[e], sc[e], sh[e]) > 0.f ? gs[e] : 0.f;
+      a1[e] += gm;
+      a2[e] = fmaf(gm, v[e] - mu[e], a2[e]);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[0][tid >> 3][c8 * 8 + e] = a1[e];
+    red[1][tid >> 3][c8 * 8 + e] = a2[e];
+  }
+  __syncthreads();
+  if (tid < 2 * CO) {
+    const int which = tid >> 6, ch = tid & 63;
+    float acc = 0.f;
+    for (int r = 0; r < 32; ++r) acc += red[which][r][ch];
+    a.part[((size_t)which * gridDim.x + blockIdx.x) * CO + ch] = acc;
+  }
+}
+
+// ---- backward: weight gradient with the BN-backward prologue ---------------------------------
+constexpr int WPX = 64;           // pixels per step
+constexpr int DSTR = CO + 32;     // dX image row stride (elements): rows 192 B apart in bank space
+constexpr int ISTR = KT + 64;     // im2col image row stride: rows 64 B apart in bank space
+constexpr int WG_LDS = 2 * WPX * (DSTR + ISTR) * 2;
+
+template <typename T>
+__global__ void __launch_bounds__(256, 1) wgrad_kernel(const BwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  auto dbuf = [&](int b) { return lds + b * WPX * (DSTR + ISTR); };
+  auto ibuf = [&](int b) { return lds + b * WPX * (DSTR + ISTR) + WPX * DSTR; };
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, pl = lane & 31;
+  const Geo& g = a.g;
+  const uint32_t p_begin = blockIdx.x * a.chunk;
+  const uint32_t p_end = min(p_begin + a.chunk, g.m);
+  const int steps = p_begin < p_end ? (int)((p_end - p_begin + WPX - 1) / WPX) : 0;
+  const size_t rowstep = (size_t)g.wp * 4;
+
+  // dX items: (pixel, 8 channels) = tid + 256 i; im2col: (pixel, kernel row) pairs tid, tid + 256 (< 448)
+  const int c8 = tid & 7;
+  float sc[8], sh[8], A[8], B[8], K[8];
+  Vec8<float>::load(sc, a.coef + c8 * 8);
+  Vec8<float>::load(sh, a.coef + CO + c8 * 8);
+  Vec8<float>::load(A, a.cb + c8 * 8);
+  Vec8<float>::load(B, a.cb + CO + c8 * 8);
+  Vec8<float>::load(K, a.cb + 2 * CO + c8 * 8);
+
+  Gather G[2];
+  uint4 yv[2];
+  bool live[2];
+  uint4 im[2][4];
+
+  auto issue = [&](int st) {
+    const uint32_t base = p_begin + (uint32_t)st * WPX;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint32_t pix = base + (uint32_t)((tid + 256 * i) >> 3);
+      live[i] = pix < p_end;
+      const uint32_t pc = live[i] ? pix : p_end - 1;
+      const uint32_t nn = fdiv(pc, a.div_ohw), rem = pc - nn * a.div_ohw.d;
+      const uint32_t yh = fdiv(rem, a.div_ow), yw = rem - yh * a.div_ow.d;
+      gather_issue(a, nn, (int)yh, (int)yw, c8, G[i]);
+      yv[i] = *reinterpret_cast<const uint4*>(a.y + (size_t)pc * CO + c8 * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int pr = tid + 256 * i;
+      if (pr >= WPX * 7) continue;
+      const uint32_t pix = base + (uint32_t)(pr / 7);
+      const int r = pr % 7;
+      const uint32_t pc = pix < p_end ? pix : p_end - 1;
+      const uint32_t nn = fdiv(pc, a.div_ohw), rem = pc - nn * a.div_ohw.d;
+      const uint32_t oh = fdiv(rem, a.div_ow), ow = rem - oh * a.div_ow.d;
+      const uint4* src = reinterpret_cast<const uint4*>(a.xp + ((size_t)(nn * g.hp + 2 * oh) * g.wp + 2 * ow) * 4 +
+                                                         r * rowstep);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) im[i][q] = src[q];
+    }
+  };
+  auto commit = [&](int b) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float gs[8], v[8], dx[8];
+      gather_sum<T>(G[i], gs);
+      const uint32_t yw4[4] = {yv[i].x, yv[i].y, yv[i].z, yv[i].w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[e] = to_f(T{(uint16_t)((yw4[e >> 1] >> (16 * (e & 1))) & 0xffffu)});
+        const float gm = fmaf(v[e], sc[e], sh[e]) > 0.f ? gs[e] : 0.f;
+        // dX rounded to the storage type, as the unfused path's dx tensor
+        dx[e] = live[i] ? fmaf(A[e], gm, fmaf(B[e], v[e], K[e])) : 0.f;
+      }
+      Vec8<T>::store(reinterpret_cast<T*>(dbuf(b) + ((tid + 256 * i) >> 3) * DSTR + c8 * 8), dx);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int pr = tid + 256 * i;
+      if (pr >= WPX * 7) continue;
+      uint4* dst = reinterpret_cast<uint4*>(ibuf(b) + (pr / 7) * ISTR + (pr % 7) * KROW);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dst[q] = im[i][q];
+    }
+  };
+
+  // wave w owns k-tiles u = w and w + 4 (< 7) for both 32-channel tiles
+  const int nu = wave + 4 < 7 ? 2 : 1;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) acc[t][0] = acc[t][1] = zero16();
+
+  if (steps > 0) {
+    issue(0);
+    commit(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < steps; ++st) {
+    const int cur = st & 1;
+    const bool more = st + 1 < steps;
+    if (more) issue(st + 1);
+    const uint16_t* dl = dbuf(cur);
+    const uint16_t* il = ibuf(cur);
+#pragma unroll
+    for (int ks = 0; ks < WPX / 16; ++ks) {
+      const int klo = 16 * ks + 8 * h;
+      const s16x8 a0 = frag_tr<DSTR>(dl, 0, klo, klo + 4, lane);
+      const s16x8 a1 = frag_tr<DSTR>(dl, 32, klo, klo + 4, lane);
+#pragma unroll
+      for (int ui = 0; ui < 2; ++ui) {
+        if (ui >= nu) break;
+        const s16x8 bf = frag_tr<ISTR>(il, 32 * (wave + 4 * ui), klo, klo + 4, lane);
+        acc[0][ui] = mma<T>(a0, bf, acc[0][ui]);
+        acc[1][ui] = mma<T>(a1, bf, acc[1][ui]);
+      }
+    }
+    if (more) commit(cur ^ 1);
+    __syncthreads();
+  }
+  float* ws = a.ws + (size_t)blockIdx.x * CO * KT;
+#pragma unroll
+  for (int ui = 0; ui < 2; ++ui) {
+    if (ui >= nu) break;
+    const int col = 32 * (wave + 4 * ui) + pl;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ws[(size_t)(32 * t + crow(r, h)) * KT + col] = acc[t][ui][r];
+  }
+}
+
+// dW[co][c][r][s] (strided, weight dtype) = sum over the G partials of k = r * 32 + s * 4 + c
+template <typename TW>
+__global__ void __launch_bounds__(256) wgrad_reduce(const float* __restrict__ ws, int G, int cin, int64_t s0,
+                                                    int64_t s1, int64_t s2, int64_t s3, TW* __restrict__ dw) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= CO * cin * 49) return;
+  const int s = i % 7, r = (i / 7) % 7, c = (i / 49) % cin, co = i / (49 * cin);
+  const size_t off = (size_t)co * KT + r * KROW + s * 4 + c;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  int j = 0;
+  for (; j + 3 < G; j += 4)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] += ws[(size_t)(j + u) * CO * KT + off];
+  for (; j < G; ++j) acc[0] += ws[(size_t)j * CO * KT + off];
+  dw[co * s0 + c * s1 + r * s2 + s * s3] = from_f<TW>((acc[0] + acc[1]) + (acc[2] + acc[3]));
+}
+
+inline void check_geo(const Geo& g) {
+  if (g.n <= 0 || g.h <= 0 || g.w <= 0 || g.cin < 1 || g.cin > 4)
+    throw std::runtime_error("stem: needs a non-empty image with 1-4 channels");
+  if ((int64_t)g.n * g.hp * g.wp * 4 >= (1ll << 31) || (int64_t)g.m * CO >= (1ll << 31))
+    throw std::runtime_error("stem: tensors past 2^31 elements (32-bit indexing)");
+}
+
+}  // namespace stem
+
+void stem_geometry(int n, int h, int w, int* oh, int* ow, int* hp, int* wp, int* ph, int* pw) {
+  const stem::Geo g = stem::geo_of(n, h, w, 1);
+  *oh = g.oh;
+  *ow = g.ow;
+  *hp = g.hp;
+  *wp = g.wp;
+  *ph = g.ph;
+  *pw = g.pw;
+}
+
+int stem_fprop_rows(int cus) { return cus; }
+int stem_reduce_rows(int cus) { return cus * 4; }
+int stem_wgrad_parts(int cus) { return cus; }
+
+void stem_pad(const void* x, int x_t, int n, int cin, int h, int w, const int64_t* strides, void* xp, int t,
+              int cus, hipStream_t s) {
+  const stem::Geo g = stem::geo_of(n, h, w, cin);
+  stem::check_geo(g);
+  const int64_t total = (int64_t)n * g.hp * g.wp;
+  int64_t grid = (total + 255) / 256;
+  if (grid > (int64_t)cus * 16) grid = (int64_t)cus * 16;
+  dispatch_float(x_t, [&](auto ti) {
+    using TI = typename decltype(ti)::type;
+    dispatch_16(t, [&](auto to) {
+      using T = typename decltype(to)::type;
+      hipLaunchKernelGGL((stem::pad_kernel<TI, T>), dim3((unsigned)grid), dim3(256), 0, s, (const TI*)x, strides[0],
+                         strides[1], strides[2], strides[3], g, (T*)xp);
+    }, "stem pad (out)");
+  }, "stem pad (in)");
+  check_launch("stem_pad");
+}
+
+void stem_wpack(const void* w, int w_t, int cin, const int64_t* strides, void* wp, int t, hipStream_t s) {
+  if (cin < 1 || cin > 4) throw std::runtime_error("stem: 1-4 input channels");
+  dispatch_float(w_t, [&](auto tw) {
+    using TW = typename decltype(tw)::type;
+    dispatch_16(t, [&](auto to) {
+      using T = typename decltype(to)::type;
+      hipLaunchKernelGGL((stem::wpack_kernel<TW, T>), dim3((stem::CO * stem::KT + 255) / 256), dim3(256), 0, s,
+                         (const TW*)w, cin, strides[0], strides[1], strides[2], strides[3], (T*)wp);
+    }, "stem wpack (out)");
+  }, "stem wpack (in)");
+  check_launch("stem_wpack");
+}
+
+void stem_fprop(const void* xp, const void* wp, const float* shift, void* y, float* part, int n, int h, int w,
+                int t, int cus, hipStream_t s) {
+  stem::FpArgs a;
+  a.g = stem::geo_of(n, h, w, 4);
+  stem::check_geo(a.g);
+  a.xp = (const uint16_t*)xp;
+  a.wp = (const uint16_t*)wp;
+  a.shift = shift;
+  a.y = (uint16_t*)y;
+  a.part = part;
+  a.div_ohw = make_fastdiv((uint32_t)(a.g.oh * a.g.ow));
+  a.div_ow = make_fastdiv((uint32_t)a.g.ow);
+  a.tiles = (int)((a.g.m + 31) / 32);
+  dispatch_16(t, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    hipLaunchKernelGGL((stem::fprop_kernel<T>), dim3(stem_fprop_rows(cus)), dim3(256), 0, s, a);
+  }, "stem fprop");
+  check_launch("stem_fprop");
+}
+
+void stem_pool_fwd(const void* y, const float* coef, void* p, uint8_t* idx, int n, int h, int w, int t, int cus,
+                   hipStream_t s) {
+  stem::PoolArgs a;
+  a.g = stem::geo_of(n, h, w, 4);
+  stem::check_geo(a.g);
+  a.y = (const uint16_t*)y;
+  a.coef = coef;
+  a.p = (uint16_t*)p;
+  a.idx = idx;
+  a.strips = (a.g.ph + stem::PR - 1) / stem::PR;
+  const int64_t total = (int64_t)n * a.strips * a.g.pw * 8;
+  int64_t grid = (total + 255) / 256;
+  if (grid > (int64_t)cus * 16) grid = (int64_t)cus * 16;
+  dispatch_16(t, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    hipLaunchKernelGGL((stem::pool_fwd_kernel<T>), dim3((unsigned)grid), dim3(256), 0, s, a);
+  }, "stem pool fwd");
+  check_launch("stem_pool_fwd");
+}
+
+static stem::BwdArgs bwd_args(const void* dp, const uint8_t* idx, const void* y, const float* coef, int n, int h,
+                              int w) {
+  stem::BwdArgs a{};
+  a.g = stem::geo_of(n, h, w, 4);
+  stem::check_geo(a.g);
+  a.dp = (const uint16_t*)dp;
+  a.idx = idx;
+  a.y = (const uint16_t*)y;
+  a.coef = coef;
+  a.div_ohw = make_fastdiv((uint32_t)(a.g.oh * a.g.ow));
+  a.div_ow = make_fastdiv((uint32_t)a.g.ow);
+  return a;
+}
+
+void stem_bwd_reduce(const void* dp, const uint8_t* idx, const void* y, const float* coef, const float* mean,
+                     float* part, int n, int h, int w, int t, int cus, hipStream_t s) {
+  stem::BwdArgs a = bwd_args(dp, idx, y, coef, n, h, w);
+  a.mean = mean;
+  a.part = part;
+  dispatch_16(t, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    hipLaunchKernelGGL((stem::bwd_reduce_kernel<T>), dim3(stem_reduce_rows(cus)), dim3(256), 0, s, a);
+  }, "stem bwd reduce");
+  check_launch("stem_bwd_reduce");
+}
+
+void stem_wgrad(const void* dp, const uint8_t* idx, const void* y, const float* coef, const float* cb,
+                const void* xp, float* ws, void* dw, int dw_t, int cin, const int64_t* dw_strides, int n, int h, int w,
+                int t, int cus, hipStream_t s) {
+  stem::BwdArgs a = bwd_args(dp, idx, y, coef, n, h, w);
+  a.cb = cb;
+  a.xp = (const uint16_t*)xp;
+  a.ws = ws;
+  const int G = stem_wgrad_parts(cus);
+  a.chunk = (uint32_t)(((int64_t)a.g.m + G - 1) / G);
+  a.chunk = (a.chunk + stem::WPX - 1) / stem::WPX * stem::WPX;
+  if (cin < 1 || cin > 4) throw std::runtime_error("stem wgrad: 1-4 input channels");
+  dispatch_16(t, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem::wgrad_kernel<T>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, stem::WG_LDS);
+      attr = true;
+    }
+    hipLaunchKernelGGL((stem::wgrad_kernel<T>), dim3(G), dim3(256), stem::WG_LDS, s, a);
+  }, "stem wgrad");
+  dispatch_float(dw_t, [&](auto tag) {
+    using TW = typename decltype(tag)::type;
+    hipLaunchKernelGGL((stem::wgrad_reduce<TW>), dim3((stem::CO * cin * 49 + 255) / 256), dim3(256), 0, s, ws, G, cin,
+                       dw_strides[0], dw_strides[1], dw_strides[2], dw_strides[3], (TW*)dw);
+  }, "stem wgrad reduce");
+  check_launch("stem_wgrad");
+}
+
+}  // namespace apex_amd

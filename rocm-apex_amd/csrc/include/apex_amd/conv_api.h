@@ -124,4 +124,29 @@ int64_t conv3x3_wgrad_workspace_floats(int64_t m, int kout, int c, int cus);
 void conv3x3_wgrad(const void* g, const void* x, void* dw, int out_dtype, int nimg, int h, int w, int c, int oh,
                    int ow, int stride, int kout, int dtype, const float* xcoef, float* ws, int cus, hipStream_t s);
 
+// ---- ResNet stem (csrc/conv/stem.hip): 7x7/2 conv (1-4 -> 64 channels, pad 3) + BN + ReLU +
+// 3x3/2 max pool (pad 1).  Compute dtype t = bf16 / fp16; activations NHWC.
+// image -> halo'd NHWC4 xp [n][hp][wp][4]; strides of the [n, cin, h, w] image in elements
+void stem_geometry(int n, int h, int w, int* oh, int* ow, int* hp, int* wp, int* ph, int* pw);
+int stem_fprop_rows(int cus);   // partial rows G of stem_fprop's statistics [2][G][64]
+int stem_reduce_rows(int cus);  // partial rows G of stem_bwd_reduce's sums [2][G][64]
+int stem_wgrad_parts(int cus);  // fp32 partial slabs [G][64][224] of stem_wgrad's workspace
+void stem_pad(const void* x, int x_t, int n, int cin, int h, int w, const int64_t* strides, void* xp, int t,
+              int cus, hipStream_t s);
+// weight [64, cin, 7, 7] (strided, dtype w_t) -> packed [64][224], k = r * 32 + s * 4 + c
+void stem_wpack(const void* w, int w_t, int cin, const int64_t* strides, void* wp, int t, hipStream_t s);
+// y [n*oh*ow][64] = conv(xp, wp) + statistics partials of (y - shift)
+void stem_fprop(const void* xp, const void* wp, const float* shift, void* y, float* part, int n, int h, int w,
+                int t, int cus, hipStream_t s);
+// p / idx [n][ph][pw][64] = maxpool(relu(y * coef[c] + coef[64 + c])), idx = window position
+void stem_pool_fwd(const void* y, const float* coef, void* p, uint8_t* idx, int n, int h, int w, int t, int cus,
+                   hipStream_t s);
+// [2][G][64] partials of sum(g) and sum(g * (y - mean)), g = ReLU-masked pool-backward of dp
+void stem_bwd_reduce(const void* dp, const uint8_t* idx, const void* y, const float* coef, const float* mean,
+                     float* part, int n, int h, int w, int t, int cus, hipStream_t s);
+// dw (strided [64, cin, 7, 7], dtype dw_t) = sum_p dx[p] (x) im2col(xp)[p], dx = cb0 g + cb1 y + cb2
+void stem_wgrad(const void* dp, const uint8_t* idx, const void* y, const float* coef, const float* cb,
+                const void* xp, float* ws, void* dw, int dw_t, int cin, const int64_t* dw_strides, int n, int h, int w,
+                int t, int cus, hipStream_t s);
+
 }  // namespace apex_amd

@@ -235,8 +235,13 @@ class ResNet(nn.Module):
         if self.fused_bn:
             # stem: BN statistics, then normalize + ReLU + 3x3/2 max pool in one pass
             from ..contrib.groupbn import bn_relu_maxpool
+            from ..ops import stem
 
-            x = bn_relu_maxpool(self.conv1(x), self.bn1, self.maxpool)
+            if stem.stem_supported(self.conv1, self.bn1, self.maxpool, x) and not _has_hooks(()):
+                # conv + BN statistics, BN + ReLU + pool, and the fused backward (ops/stem.py)
+                x = stem.stem_forward(self.conv1, self.bn1, self.maxpool, x)
+            else:
+                x = bn_relu_maxpool(self.conv1(x), self.bn1, self.maxpool)
             # bottleneck nodes hand each other their output BN's state (ops/bottleneck_bn.py
             # BlockLink): block i+1's conv1 dgrad does block i's bn3 backward reduction.  The
             # linked walk calls the blocks directly and hands block i the ReLU-MASKED gradient of
