@@ -3,7 +3,10 @@
 ``impl="fast"``: projections are plain library GEMMs (hipBLASLt through ``F.linear``); the
 attention itself is ONE fused flash kernel launch per direction reading Q/K/V straight out of the
 interleaved projection output (strided views, no permute copies) and writing the context in the
-``[seq, batch, embed]`` layout the output projection consumes.  The reference's fast path
+``[seq, batch, embed]`` layout the output projection consumes.  Self-attention hands the
+projection output to the packed-QKV kernel pair as ``[seq, batch, heads, 3*head_dim]``: the
+backward writes dQ / dK / dV into ONE gradient buffer of the projection, so autograd never forms
+the three zero-filled slice gradients and their sum (host launches and device passes per layer).  The reference's fast path
 (apex/contrib/csrc/multihead_attn/self_multihead_attn_cuda.cu) instead runs two strided-batched
 GEMMs around a materialised [b*h, sq, sk] softmax + dropout-mask tensor.
 
@@ -16,7 +19,7 @@ additive float mask when ``mask_additive``), ``attn_mask`` ("time mask") [sq, sk
 import torch
 import torch.nn.functional as F
 
-from ...ops.attention import flash_attn_func
+from ...ops.attention import flash_attn_func, next_dropout_seed, packed_qkv_self_attention
 
 
 def mask_to_bias(key_padding_mask, attn_mask, mask_additive, batch, sq, sk, device):
@@ -87,10 +90,15 @@ def self_attn(use_time_mask, is_training, heads, scale, inputs, input_weights, o
     seq, batch, e = inputs.shape
     x = inputs if norm is None else fused_layer_norm_affine(inputs, norm[0], norm[1], (e,), 1e-5)
     lin = F.linear(x, input_weights, input_biases)
-    q4, k4, v4 = split_heads_interleaved(lin, seq, batch, heads, 3)
     kpm, am = _masks(use_time_mask, mask)
     bias = mask_to_bias(kpm, am, mask_additive, batch, seq, seq, inputs.device)
-    ctx = attention(q4, k4, v4, bias, scale, dropout_prob, is_training, impl)
+    if impl == "fast":
+        p = dropout_prob if is_training else 0.0
+        seed, offset = next_dropout_seed() if p > 0 else (0, 0)
+        ctx = packed_qkv_self_attention(lin.view(seq, batch, heads, -1), scale, False, bias, p, seed, offset)
+    else:
+        q4, k4, v4 = split_heads_interleaved(lin, seq, batch, heads, 3)
+        ctx = attention(q4, k4, v4, bias, scale, dropout_prob, is_training, impl)
     out = F.linear(ctx, output_weights, output_biases)
     return out if norm is None else dropout_add(out, inputs, dropout_prob, is_training)
 
