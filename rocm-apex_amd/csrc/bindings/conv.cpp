@@ -433,6 +433,46 @@ at::Tensor stem_wgrad_b(const at::Tensor& dp, const at::Tensor& idx, const at::T
   return dw;
 }
 
+// bottleneck conv3 backward, both BNs fused: dm / y3 [M, C4], y2 [M, W] (dense NHWC views), w3
+// [C4, W] (any 2-D view of the [C4, W, 1, 1] weight, contiguous), cb3 [3 C4], c2 [2 W], mean2 [W]
+// -> (dz2 [M, W], bn2 partials [2, G, W], dW3 [C4, W] in w3's dtype)
+std::vector<at::Tensor> conv3_bwd_b(const at::Tensor& dm, const at::Tensor& y3, const at::Tensor& y2,
+                                    const at::Tensor& w3, const at::Tensor& cb3, const at::Tensor& c2,
+                                    const at::Tensor& mean2) {
+  auto chk2 = [](const at::Tensor& t, const char* what) {
+    TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.is_contiguous(), "conv3_bwd: ", what, " must be a contiguous 2-D GPU tensor");
+  };
+  chk2(dm, "dm");
+  chk2(y3, "y3");
+  chk2(y2, "y2");
+  chk2(w3, "w3");
+  const int64_t m = dm.size(0), c4 = dm.size(1), w = y2.size(1);
+  TORCH_CHECK(y3.sizes() == dm.sizes() && y2.size(0) == m && w3.size(0) == c4 && w3.size(1) == w,
+              "conv3_bwd: shape mismatch");
+  TORCH_CHECK(dm.scalar_type() == y3.scalar_type() && dm.scalar_type() == y2.scalar_type() &&
+                  dm.scalar_type() == w3.scalar_type(),
+              "conv3_bwd: one dtype");
+  TORCH_CHECK(conv3_bwd_fused_supported((int)c4, (int)w), "conv3_bwd: unsupported channel counts");
+  auto f32 = [](const at::Tensor& t, int64_t n, const char* what) {
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == n, "conv3_bwd: ",
+                what, " must be contiguous fp32 [", n, "]");
+  };
+  f32(cb3, 3 * c4, "cb3");
+  f32(c2, 2 * w, "c2");
+  f32(mean2, w, "mean2");
+  const c10::hip::HIPGuard guard(dm.get_device());
+  const int cus = device_cus(dm.get_device());
+  const int g = conv3_bwd_fused_parts(cus);
+  auto dz2 = at::empty({m, w}, y2.options());
+  auto part2 = at::empty({2, g, w}, y2.options().dtype(at::kFloat));
+  auto ws = at::empty({(int64_t)g * c4 * w}, y2.options().dtype(at::kFloat));
+  auto dw3 = at::empty({c4, w}, w3.options());
+  conv3_bwd_fused(dm.data_ptr(), y3.data_ptr(), y2.data_ptr(), w3.data_ptr(), cb3.data_ptr<float>(), c2.data_ptr<float>(),
+                  mean2.data_ptr<float>(), dz2.data_ptr(), part2.data_ptr<float>(), ws.data_ptr<float>(), dw3.data_ptr(),
+                  dtype_code(dw3.scalar_type()), m, (int)c4, (int)w, dtype_code(dm.scalar_type()), cus, cur_stream());
+  return {dz2, part2, dw3};
+}
+
 }  // namespace
 
 void bind_conv(pybind11::module_& root) {
@@ -461,6 +501,8 @@ void bind_conv(pybind11::module_& root) {
   m.def("bnbwd_finalize", &bnbwd_finalize);
   m.def("part_payload", &part_payload, pybind11::arg("part"), pybind11::arg("count"),
         pybind11::arg("shift") = pybind11::none());
+  m.def("conv3_bwd", &conv3_bwd_b);
+  m.def("supports_conv3_bwd", &conv3_bwd_fused_supported);
   m.def("stem_fprop", &stem_fprop_b, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("shift") = pybind11::none());
   m.def("stem_pool", &stem_pool_b);
   m.def("stem_reduce", &stem_reduce_b);

@@ -149,4 +149,14 @@ void stem_wgrad(const void* dp, const uint8_t* idx, const void* y, const float* 
                 const void* xp, float* ws, void* dw, int dw_t, int cin, const int64_t* dw_strides, int n, int h, int w,
                 int t, int cus, hipStream_t s);
 
+// ---- bottleneck conv3 backward with both batch norms fused (csrc/conv/conv3_bwd.hip) ----
+// dx3 = cb3[0] dm + cb3[1] y3 + cb3[2] (bn3's dx, never stored); dz2 = relu2-mask(dx3 . W3) written
+// with bn2's backward partial sums part2 [2][G][W] (sum g, sum g (y2 - mean2)); dW3 [C4][W] (dtype
+// dw_t) = dx3^T relu(y2 c2[0] + c2[1]) through fp32 slabs ws [G][C4][W]; G = conv3_bwd_fused_parts
+bool conv3_bwd_fused_supported(int c4, int w);
+int conv3_bwd_fused_parts(int cus);
+void conv3_bwd_fused(const void* dm, const void* y3, const void* y2, const void* w3, const float* cb3, const float* c2,
+                     const float* mean2, void* dz2, float* part2, float* ws, void* dw3, int dw_t, int64_t m, int c4,
+                     int w, int t, int cus, hipStream_t s);
+
 }  // namespace apex_amd

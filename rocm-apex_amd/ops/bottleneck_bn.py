@@ -46,6 +46,8 @@ _ENABLED = os.environ.get("APEX_AMD_FUSED_BLOCK", "1") != "0"
 # would otherwise route to the library)
 FORCE_NATIVE = os.environ.get("APEX_AMD_FUSED_BLOCK_FORCE_NATIVE", "0") == "1"
 _NATIVE_K = (64, 128, 256, 512)
+# conv3's fused data + weight gradient (csrc/conv/conv3_bwd.hip); 0 = the two-kernel path (A/B)
+_C3B = os.environ.get("APEX_AMD_CONV3_BWD", "1") != "0"
 
 
 def _conv():
@@ -314,7 +316,16 @@ class _BottleneckFn(torch.autograd.Function):
         else:
             dm, cb3, gg3, gb3 = bwd_reduce(go2, y3, g3, sm3, si3, c3, True, bits, gr3, in3)
         w3m = w3.view(cout, width)
-        if _dgrad_native(dm.size(0), cout, width) and width == 64:
+        dw3 = None
+        if _C3B and _conv().supports_conv3_bwd(cout, width):
+            # conv3's data AND weight gradients in one pass (csrc/conv/conv3_bwd.hip): bn3's dx
+            # computed on the operand load and kept in LDS, bn2's ReLU mask + backward sums in the
+            # dgrad epilogue, bn2's apply+ReLU on the weight gradient's operand
+            dz2, part2, dw3 = _conv().conv3_bwd(dm, y3, y2m, w3m, cb3.view(-1), c2, sm2)
+            dw3 = dw3.view_as(w3)
+            cb2, gg2, gb2 = bwd_from_part(part2, float(dm.size(0)), sm2, si2, g2, gr2, in2)
+            dy2 = bn.bwd_apply(dz2, y2m, c2, cb2)
+        elif _dgrad_native(dm.size(0), cout, width) and width == 64:
             # conv3 dgrad with bn3's dx as the operand prologue (dx3 written for the wgrad) AND
             # bn2's ReLU mask + backward reduction in the epilogue: bn2's reduction pass is gone
             # (stage 1 only: at 128+ channels the longer epilogue costs more than the pass,
@@ -331,7 +342,8 @@ class _BottleneckFn(torch.autograd.Function):
             dz2 = conv1x1_dgrad(dx3, w3m)
             dy2, gg2, gb2 = bwd_full(dz2, y2m, g2, sm2, si2, c2, True, gr2, in2)
         # conv3 weight gradient with bn2's apply + ReLU recomputed on the operand load
-        dw3 = conv1x1_wgrad(dx3, y2m, c2, w3)
+        if dw3 is None:
+            dw3 = conv1x1_wgrad(dx3, y2m, c2, w3)
         # conv2
         dz1, dw2 = _conv_bwd(_nchw(dy2, n, oh, ow), _nchw(z1, n, h, wd), w2, stride, 1)
         dz1 = _m2(dz1.contiguous(memory_format=torch.channels_last))

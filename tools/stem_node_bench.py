@@ -6,8 +6,14 @@ Run on the GPU box: python tools/stem_node_bench.py [--batch 256]"""
 import argparse
 import copy
 import json
+import os
+import sys
 
-import torch
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
 
 
 def timeit(fn, iters=20, warmup=5):
