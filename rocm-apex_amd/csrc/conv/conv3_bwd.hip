@@ -12,10 +12,12 @@
 // in LDS: per 64-pixel tile the workgroup reads dm, y3 [64][C4] and y2 [64][W], writes dz2 [64][W].
 // At ResNet-50 stage 1 (C4 = 256, W = 64, 802,816 pixels) that is 1.03 GB instead of 1.95 GB.
 //
-// gfx950 layout (one persistent workgroup per CU, 4 waves, 64-pixel tiles, LDS double-buffered):
-//  * staging: 16-byte global loads of dm / y3 / y2 into registers one tile ahead; dx3 computed
-//    in registers (fp32 FMA, rounded to the storage type like the unfused path's dx3 tensor) and
-//    written with y2 into the next LDS buffer; one barrier per tile;
+// gfx950 layout (one persistent workgroup per CU, 64-pixel tiles, LDS double-buffered), 8 waves in
+// two roles so the matrix work never waits on HBM:
+//  * 4 loader waves: 16-byte global loads of dm / y3 / y2 into registers TWO tiles ahead; dx3
+//    computed in registers (fp32 FMA, rounded to the storage type like the unfused path's dx3
+//    tensor) and written with y2 into the free LDS stage; one barrier per tile;
+//  * 4 math waves, as follows:
 //  * GEMM 1, swapped (dz2^T = W3^T dx3^T): the W3^T fragments are the A operand, resident in
 //    registers for the whole kernel; B fragments are 16-byte row reads of the dx3 image; rows of
 //    W3^T permuted so each lane ends with 16 consecutive channels of one pixel (16-byte y2 reads
@@ -57,29 +59,103 @@ template <int C4, int W>
 struct Cfg {
   static constexpr int DS = C4 + 16;  // dx3 row stride: 2 DS bytes = 32 mod 256
   static constexpr int YS = W + 32;   // y2 row stride: rows 64 B apart in bank space (transposed reads)
-  static constexpr int BUF = TM * DS + TM * YS;  // elements per LDS buffer
+  static constexpr int BUF = TM * DS + TM * YS;  // elements per LDS stage
   static constexpr int LDS = 2 * BUF * 2;
   static constexpr int KS1 = C4 / 16;  // GEMM 1 k-steps
   static constexpr int CPR = C4 / 8;   // 16-byte chunks per dm / y3 row
-  static constexpr int NQ = TM * CPR / 256;      // dm / y3 chunks per thread per tile
-  static constexpr int NY = TM * (W / 8) / 256;  // y2 chunks per thread per tile
-  static_assert(C4 == 256 && W == 64, "register plan: 4 waves = 2 channel tiles x 2 pixel halves");
+  static constexpr int NQ = TM * CPR / 256;      // dm / y3 chunks per loader thread per tile
+  static constexpr int NY = TM * (W / 8) / 256;  // y2 chunks per loader thread per tile
+  static_assert(C4 == 256 && W == 64, "register plan: 4 math waves = 2 channel tiles x 2 pixel halves");
   static_assert(NQ * 256 == TM * CPR && NY * 256 == TM * (W / 8), "staging split");
+  static_assert(4 * 64 * 17 * 4 <= LDS, "statistics fold aliases the stages");
 };
 
 __device__ __forceinline__ int chan_of_row(int r) { return 16 * ((r >> 2) & 1) + (r & 3) + 4 * (r >> 3); }
 
+// 8 waves: waves 0-3 are the math waves (both GEMMs, epilogue, accumulators), waves 4-7 the
+// loader waves (global -> registers two tiles ahead, dx3 -> LDS).  Iteration j: loaders commit
+// tile j into stage j % 2 and issue tile j + 2; math waves compute tile j - 1 from stage
+// (j - 1) % 2; one barrier.  The math waves never wait on HBM, the loaders keep two tiles
+// (144 KB per CU) of loads in flight.
 template <typename T, int C4, int W>
-__global__ void __launch_bounds__(256, 1) fused_kernel(const Args p) {
+__global__ void __launch_bounds__(512, 1) fused_kernel(const Args p) {
   using C = Cfg<C4, W>;
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
-  __shared__ float red[4 * 64 * 17];
+  __shared__ __attribute__((aligned(16))) float ec[3 * W];  // bn2 scale | shift | mean (math waves)
   auto dxb = [&](int b) { return lds + b * C::BUF; };
   auto y2b = [&](int b) { return lds + b * C::BUF + TM * C::DS; };
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, pl = lane & 31;
-  const int ct = wave & 1, mh = wave >> 1;  // GEMM 1: channel tile, pixel half
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, pl = lane & 31;
+  const bool loader = wave >= 4;
+  // this workgroup's tiles: blockIdx.x, + gridDim.x, ...
+  const int nmine = p.ntiles > (int)blockIdx.x ? (p.ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
+  auto tile_of = [&](int i) { return (int)blockIdx.x + i * (int)gridDim.x; };
 
-  // W3^T fragments (A operand of GEMM 1): MFMA row pl -> channel 32 ct + perm(pl), k = k4
+  if (loader) {
+    const int tid = threadIdx.x - 256;
+    const int qc = (tid % C::CPR) * 8, qr = tid / C::CPR;  // dm / y3: rows qr + (256 / CPR) i
+    const int yc = (tid % (W / 8)) * 8, yr = tid / (W / 8);
+    float cA[8], cB[8], cK[8];
+    Vec8<float>::load(cA, p.cb3 + qc);
+    Vec8<float>::load(cB, p.cb3 + C4 + qc);
+    Vec8<float>::load(cK, p.cb3 + 2 * C4 + qc);
+    uint4 rdm[2][C::NQ], ry3[2][C::NQ], ry2[2][C::NY];
+    auto issue = [&](int set, int t) {
+#pragma unroll
+      for (int i = 0; i < C::NQ; ++i) {
+        int64_t row = (int64_t)t * TM + qr + (256 / C::CPR) * i;
+        if (row >= p.m) row = p.m - 1;  // tail: valid memory, zeroed at commit
+        rdm[set][i] = *reinterpret_cast<const uint4*>(p.dm + row * C4 + qc);
+        ry3[set][i] = *reinterpret_cast<const uint4*>(p.y3 + row * C4 + qc);
+      }
+#pragma unroll
+      for (int i = 0; i < C::NY; ++i) {
+        int64_t row = (int64_t)t * TM + yr + (256 / (W / 8)) * i;
+        if (row >= p.m) row = p.m - 1;
+        ry2[set][i] = *reinterpret_cast<const uint4*>(p.y2 + row * W + yc);
+      }
+    };
+    auto commit = [&](int set, int t, int b) {
+#pragma unroll
+      for (int i = 0; i < C::NQ; ++i) {
+        const int lr = qr + (256 / C::CPR) * i;
+        const bool ok = (int64_t)t * TM + lr < p.m;
+        float g[8], y[8], d[8];
+        Vec8<T>::load(g, reinterpret_cast<const T*>(&rdm[set][i]));
+        Vec8<T>::load(y, reinterpret_cast<const T*>(&ry3[set][i]));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = ok ? fmaf(cA[j], g[j], fmaf(cB[j], y[j], cK[j])) : 0.f;
+        Vec8<T>::store(reinterpret_cast<T*>(dxb(b) + lr * C::DS + qc), d);
+      }
+#pragma unroll
+      for (int i = 0; i < C::NY; ++i) {
+        const int lr = yr + (256 / (W / 8)) * i;
+        *reinterpret_cast<uint4*>(y2b(b) + lr * C::YS + yc) = ry2[set][i];
+      }
+    };
+    if (nmine > 0) issue(0, tile_of(0));
+    if (nmine > 1) issue(1, tile_of(1));
+    for (int j = 0; j <= nmine; ++j) {
+      if (j < nmine) {
+        // register sets alternate with j; constant indices keep them in registers
+        if (j & 1) {
+          commit(1, tile_of(j), 1);
+          if (j + 2 < nmine) issue(1, tile_of(j + 2));
+        } else {
+          commit(0, tile_of(j), 0);
+          if (j + 2 < nmine) issue(0, tile_of(j + 2));
+        }
+      }
+      __syncthreads();
+    }
+    __syncthreads();  // statistics fold (math waves)
+    __syncthreads();
+    __syncthreads();
+    __syncthreads();
+    return;
+  }
+
+  // ---------------- math waves ----------------
+  const int ct = wave & 1, mh = wave >> 1;  // GEMM 1: channel tile, pixel half
   s16x8 wa[C::KS1];
   {
     const int c = 32 * ct + chan_of_row(pl);
@@ -88,106 +164,48 @@ __global__ void __launch_bounds__(256, 1) fused_kernel(const Args p) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) wa[ks][j] = (short)p.w3[(size_t)(16 * ks + 8 * h + j) * W + c];
   }
-  // GEMM 1 epilogue: this lane's 16 channels c0 .. c0 + 15
   const int c0 = 32 * ct + 16 * h;
-  float e_sc[16], e_sh[16], e_mu[16], s1[16], s2[16];
+  // bn2 coefficients of the epilogue's channels: an LDS table (registers go to the accumulators)
+  for (int i = threadIdx.x; i < 3 * W; i += 256) ec[i] = i < 2 * W ? p.c2[i] : p.mean2[i - 2 * W];
+  float s1[16], s2[16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    e_sc[r] = p.c2[c0 + r];
-    e_sh[r] = p.c2[W + c0 + r];
-    e_mu[r] = p.mean2[c0 + r];
-    s1[r] = s2[r] = 0.f;
-  }
-  // GEMM 2 B transform: channel pl of each 32-channel tile
+  for (int r = 0; r < 16; ++r) s1[r] = s2[r] = 0.f;
   const float b_sc0 = p.c2[pl], b_sh0 = p.c2[W + pl], b_sc1 = p.c2[32 + pl], b_sh1 = p.c2[W + 32 + pl];
-  // staging: fixed 16-byte column chunk per thread
-  const int qc = (tid % C::CPR) * 8, qr = tid / C::CPR;  // dm / y3: rows qr + (256 / CPR) i
-  const int yc = (tid % (W / 8)) * 8, yr = tid / (W / 8);
-  float cA[8], cB[8], cK[8];
-  Vec8<float>::load(cA, p.cb3 + qc);
-  Vec8<float>::load(cB, p.cb3 + C4 + qc);
-  Vec8<float>::load(cK, p.cb3 + 2 * C4 + qc);
-
-  uint4 rdm[C::NQ], ry3[C::NQ], ry2[C::NY];
-  auto issue = [&](int t) {
-#pragma unroll
-    for (int i = 0; i < C::NQ; ++i) {
-      int64_t row = (int64_t)t * TM + qr + (256 / C::CPR) * i;
-      if (row >= p.m) row = p.m - 1;  // tail: valid memory, zeroed at commit
-      rdm[i] = *reinterpret_cast<const uint4*>(p.dm + row * C4 + qc);
-      ry3[i] = *reinterpret_cast<const uint4*>(p.y3 + row * C4 + qc);
-    }
-#pragma unroll
-    for (int i = 0; i < C::NY; ++i) {
-      int64_t row = (int64_t)t * TM + yr + (256 / (W / 8)) * i;
-      if (row >= p.m) row = p.m - 1;
-      ry2[i] = *reinterpret_cast<const uint4*>(p.y2 + row * W + yc);
-    }
-  };
-  auto commit = [&](int t, int b) {
-#pragma unroll
-    for (int i = 0; i < C::NQ; ++i) {
-      const int lr = qr + (256 / C::CPR) * i;
-      const bool ok = (int64_t)t * TM + lr < p.m;
-      float g[8], y[8], d[8];
-      Vec8<T>::load(g, reinterpret_cast<const T*>(&rdm[i]));
-      Vec8<T>::load(y, reinterpret_cast<const T*>(&ry3[i]));
-#pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = ok ? fmaf(cA[j], g[j], fmaf(cB[j], y[j], cK[j])) : 0.f;
-      Vec8<T>::store(reinterpret_cast<T*>(dxb(b) + lr * C::DS + qc), d);
-    }
-#pragma unroll
-    for (int i = 0; i < C::NY; ++i) {
-      const int lr = yr + (256 / (W / 8)) * i;
-      *reinterpret_cast<uint4*>(y2b(b) + lr * C::YS + yc) = ry2[i];
-    }
-  };
-
   f32x16 dw[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) dw[i][0] = dw[i][1] = zero16();
 
-  int t = blockIdx.x;
-  if (t < p.ntiles) {
-    issue(t);
-    commit(t, 0);
-  }
-  __syncthreads();
-  for (int it = 0; t < p.ntiles; ++it, t += gridDim.x) {
-    const int cur = it & 1;
-    const int tn = t + gridDim.x;
-    const bool more = tn < p.ntiles;
-    if (more) issue(tn);
-    const uint16_t* dx = dxb(cur);
-    const uint16_t* yy = y2b(cur);
-
-    // GEMM 1: dz2^T tile [32 channels][32 pixels of half mh]
-    f32x16 acc = zero16();
+  for (int j = 0; j <= nmine; ++j) {
+    if (j >= 1) {
+      const int t = tile_of(j - 1), cur = (j - 1) & 1;
+      const uint16_t* dx = dxb(cur);
+      const uint16_t* yy = y2b(cur);
+      // GEMM 1: dz2^T tile [32 channels][32 pixels of half mh]
+      f32x16 acc = zero16();
 #pragma unroll
-    for (int ks = 0; ks < C::KS1; ++ks) {
-      const s16x8 bf = *reinterpret_cast<const s16x8*>(dx + (32 * mh + pl) * C::DS + 16 * ks + 8 * h);
-      acc = mma<T>(wa[ks], bf, acc);
-    }
-    // GEMM 2: dW3 [k4 tiles 2 wave, 2 wave + 1][c tiles 0, 1] over the tile's 64 pixels
-#pragma unroll
-    for (int s = 0; s < TM / 16; ++s) {
-      const int klo = 16 * s + 8 * h;
-      const s16x8 a0 = frag_tr<C::DS>(dx, 64 * wave, klo, klo + 4, lane);
-      const s16x8 a1 = frag_tr<C::DS>(dx, 64 * wave + 32, klo, klo + 4, lane);
-      s16x8 b0 = frag_tr<C::YS>(yy, 0, klo, klo + 4, lane);
-      s16x8 b1 = frag_tr<C::YS>(yy, 32, klo, klo + 4, lane);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        b0[j] = (short)from_f<T>(fmaxf(fmaf(to_f(T{(uint16_t)b0[j]}), b_sc0, b_sh0), 0.f)).x;
-        b1[j] = (short)from_f<T>(fmaxf(fmaf(to_f(T{(uint16_t)b1[j]}), b_sc1, b_sh1), 0.f)).x;
+      for (int ks = 0; ks < C::KS1; ++ks) {
+        const s16x8 bf = *reinterpret_cast<const s16x8*>(dx + (32 * mh + pl) * C::DS + 16 * ks + 8 * h);
+        acc = mma<T>(wa[ks], bf, acc);
       }
-      dw[0][0] = mma<T>(a0, b0, dw[0][0]);
-      dw[0][1] = mma<T>(a0, b1, dw[0][1]);
-      dw[1][0] = mma<T>(a1, b0, dw[1][0]);
-      dw[1][1] = mma<T>(a1, b1, dw[1][1]);
-    }
-    // GEMM 1 epilogue: bn2's ReLU mask, rounded gradient out, bn2 backward sums
-    {
+      // GEMM 2: dW3 [k4 tiles 2 wave, 2 wave + 1][c tiles 0, 1] over the tile's 64 pixels
+#pragma unroll
+      for (int s = 0; s < TM / 16; ++s) {
+        const int klo = 16 * s + 8 * h;
+        const s16x8 a0 = frag_tr<C::DS>(dx, 64 * wave, klo, klo + 4, lane);
+        const s16x8 a1 = frag_tr<C::DS>(dx, 64 * wave + 32, klo, klo + 4, lane);
+        s16x8 b0 = frag_tr<C::YS>(yy, 0, klo, klo + 4, lane);
+        s16x8 b1 = frag_tr<C::YS>(yy, 32, klo, klo + 4, lane);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          b0[e] = (short)from_f<T>(fmaxf(fmaf(to_f(T{(uint16_t)b0[e]}), b_sc0, b_sh0), 0.f)).x;
+          b1[e] = (short)from_f<T>(fmaxf(fmaf(to_f(T{(uint16_t)b1[e]}), b_sc1, b_sh1), 0.f)).x;
+        }
+        dw[0][0] = mma<T>(a0, b0, dw[0][0]);
+        dw[0][1] = mma<T>(a0, b1, dw[0][1]);
+        dw[1][0] = mma<T>(a1, b0, dw[1][0]);
+        dw[1][1] = mma<T>(a1, b1, dw[1][1]);
+      }
+      // GEMM 1 epilogue: bn2's ReLU mask, rounded gradient out, bn2 backward sums
       const int lm = 32 * mh + pl;
       const int64_t row = (int64_t)t * TM + lm;
       if (row < p.m) {
@@ -197,25 +215,27 @@ __global__ void __launch_bounds__(256, 1) fused_kernel(const Args p) {
         float g[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float gq = fmaf(y[r], e_sc[r], e_sh[r]) > 0.f ? to_f(from_f<T>(acc[r])) : 0.f;
+          const float gq = fmaf(y[r], ec[c0 + r], ec[W + c0 + r]) > 0.f ? to_f(from_f<T>(acc[r])) : 0.f;
           g[r] = gq;
           s1[r] += gq;
-          s2[r] = fmaf(gq, y[r] - e_mu[r], s2[r]);
+          s2[r] = fmaf(gq, y[r] - ec[2 * W + c0 + r], s2[r]);
         }
         T* dst = reinterpret_cast<T*>(p.dz2 + row * W + c0);
         Vec8<T>::store(dst, *reinterpret_cast<float(*)[8]>(&g[0]));
         Vec8<T>::store(dst + 8, *reinterpret_cast<float(*)[8]>(&g[8]));
       }
     }
-    if (more) commit(tn, cur ^ 1);
     __syncthreads();
   }
 
   // bn2 partial row: lanes (wave, h) own channels 32 (wave & 1) + 16 h + r; sum over pixels
+  // (the stages are free now: the fold reuses them)
+  float* red = reinterpret_cast<float*>(lds);
+  const int tid = threadIdx.x;
   for (int pass = 0; pass < 2; ++pass) {
-    float* row = red + (wave * 64 + lane) * 17;
+    float* rrow = red + (wave * 64 + lane) * 17;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) row[r] = pass == 0 ? s1[r] : s2[r];
+    for (int r = 0; r < 16; ++r) rrow[r] = pass == 0 ? s1[r] : s2[r];
     __syncthreads();
     if (tid < W) {
       const int c = tid, t2 = c >> 5, hh = (c >> 4) & 1, r = c & 15;
@@ -231,24 +251,36 @@ __global__ void __launch_bounds__(256, 1) fused_kernel(const Args p) {
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) ws[(size_t)(64 * wave + 32 * i + crow(r, h)) * W + 32 * j + pl] = dw[i][j][r];
+      for (int r = 0; r < 16; ++r) ws[(size_t)(64 * wave + 32 * i + crow(r, h)) * W + 32 * jj + pl] = dw[i][jj][r];
 }
 
-// dW [n] = sum over the G slabs (fixed order), 8 outputs per thread
+// out[n] = sum over the G slabs (fixed order): 8 consecutive outputs per lane, the slabs split
+// over 16 lane groups of the block (G / 16 loads each), then a fixed-order LDS sum of the groups
 template <typename TO>
 __global__ void __launch_bounds__(256) reduce_kernel(const float* __restrict__ ws, int g, int64_t n,
                                                      TO* __restrict__ out) {
-  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
-  if (i >= n) return;
+  __shared__ float red[16][16 * 8 + 4];
+  const int v = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int64_t i = ((int64_t)blockIdx.x * 16 + v) * 8;
   float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int q = 0; q < g; ++q) {
-    float v[8];
-    Vec8<float>::load(v, ws + (int64_t)q * n + i);
+  if (i < n)
+    for (int q = grp; q < g; q += 16) {
+      float t[8];
+      Vec8<float>::load(t, ws + (int64_t)q * n + i);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) a[j] += v[j];
-  }
+      for (int j = 0; j < 8; ++j) a[j] += t[j];
+    }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[grp][v * 8 + j] = a[j];
+  __syncthreads();
+  if (grp != 0 || i >= n) return;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = 0.f;
+  for (int g2 = 0; g2 < 16; ++g2)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] += red[g2][v * 8 + j];
   Vec8<TO>::store(out + i, a);
 }
 
@@ -285,12 +317,12 @@ void conv3_bwd_fused(const void* dm, const void* y3, const void* y2, const void*
                                 hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
       attr = true;
     }
-    hipLaunchKernelGGL((c3b::fused_kernel<T, 256, 64>), dim3(G), dim3(256), C::LDS, s, a);
+    hipLaunchKernelGGL((c3b::fused_kernel<T, 256, 64>), dim3(G), dim3(512), C::LDS, s, a);
   }, "conv3_bwd_fused");
   const int64_t n = (int64_t)c4 * w;
   dispatch_float(dw_t, [&](auto tag) {
     using TO = typename decltype(tag)::type;
-    hipLaunchKernelGGL((c3b::reduce_kernel<TO>), dim3((unsigned)((n / 8 + 255) / 256)), dim3(256), 0, s, ws, G, n,
+    hipLaunchKernelGGL((c3b::reduce_kernel<TO>), dim3((unsigned)((n / 8 + 15) / 16)), dim3(256), 0, s, ws, G, n,
                        (TO*)dw3);
   }, "conv3_bwd_fused reduce");
   check_launch("conv3_bwd_fused");

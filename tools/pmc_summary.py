@@ -76,14 +76,19 @@ def main():
         fetch, write = c.get("FETCH_SIZE"), c.get("WRITE_SIZE")
         gbs = (fetch + write) * 1024 / (dur * 1e3) if fetch is not None and write is not None and dur else None
         rows.append((k, dur, util, conf, fetch, write, gbs, c))
-    lines = ["| kernel | us (median) | MFMA % of 2.5 PF peak | LDS bank-conflict cycles % | FETCH KiB | WRITE KiB | HBM GB/s (lower bound) | MFMA insts | VALU insts | waves |",
-             "|---|---|---|---|---|---|---|---|---|---|"]
+    extra = any("SQ_WAVE_CYCLES" in r[7] for r in rows)
+    lines = ["| kernel | us (median) | MFMA % of 2.5 PF peak | LDS bank-conflict cycles % | FETCH KiB | WRITE KiB | HBM GB/s (lower bound) | MFMA insts | VALU insts | waves |"
+             + (" wait-any % of wave cycles | wait-inst-any % | wait-inst-LDS % | VALU/MFMA co-exec cycles |" if extra else ""),
+             "|---|---|---|---|---|---|---|---|---|---|" + ("---|---|---|---|" if extra else "")]
     fmt = lambda v, f="{:.1f}": "-" if v is None else f.format(v)  # noqa: E731
     for k, dur, util, conf, fetch, write, gbs, c in rows:
         lines.append("| `{}` | {} | {} | {} | {} | {} | {} | {} | {} | {} |".format(
             k, fmt(dur), fmt(util), fmt(conf), fmt(fetch, "{:.0f}"), fmt(write, "{:.0f}"), fmt(gbs, "{:.0f}"),
             fmt(c.get("SQ_INSTS_MFMA"), "{:.0f}"), fmt(c.get("SQ_INSTS_VALU"), "{:.0f}"),
-            fmt(c.get("SQ_WAVES"), "{:.0f}")))
+            fmt(c.get("SQ_WAVES"), "{:.0f}")) + ("" if not extra else " {} | {} | {} | {} |".format(
+                *[fmt(100.0 * c[n] / c["SQ_WAVE_CYCLES"] if c.get(n) is not None and c.get("SQ_WAVE_CYCLES") else None)
+                  for n in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_INST_LDS")],
+                fmt(c.get("SQ_VALU_MFMA_COEXEC_CYCLES"), "{:.0f}"))))
     out = "\n".join(lines)
     print(out)
     if a.md:
