@@ -316,15 +316,18 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
     for (int cb = 0; cb < CN; ++cb) acc[cb] = zero16();
   };
 
-  // flat (tile, chunk) stream, the next chunk's loads in flight under the current one's MFMAs
+  // flat (tile, chunk) stream, the next chunk's loads in flight under the current one's MFMAs.
+  // The prefetch is unconditional (past the end: the last tile again, discarded): a branch around
+  // the loads makes the compiler's vmcnt waits conservative.
   Frags fa, fb;
   int t = blockIdx.x, ch = 0;
-  if (t < p.ntiles) load(fa, t, 0);
+  const int tlast = p.ntiles - 1;
+  load(fa, min(t, tlast), 0);
   while (t < p.ntiles) {
     {
       int nt = t, nch = ch + 1;
       if (nch == NCH) { nch = 0; nt += gridDim.x; }
-      if (nt < p.ntiles) load(fb, nt, nch);
+      load(fb, min(nt, tlast), nch);
       compute(fa, t, ch);
       if (ch == NCH - 1) epilogue(t);
       t = nt;
@@ -334,7 +337,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
     {
       int nt = t, nch = ch + 1;
       if (nch == NCH) { nch = 0; nt += gridDim.x; }
-      if (nt < p.ntiles) load(fa, nt, nch);
+      load(fa, min(nt, tlast), nch);
       compute(fb, t, ch);
       if (ch == NCH - 1) epilogue(t);
       t = nt;

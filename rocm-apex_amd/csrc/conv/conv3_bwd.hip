@@ -40,6 +40,15 @@ using namespace mfma;
 
 constexpr int TM = 64;  // pixels per tile
 
+// LDS-only barrier: this wave's LDS accesses complete, then a raw s_barrier.  __syncthreads()
+// also drains every outstanding GLOBAL load (its workgroup fence waits vmcnt), which would
+// serialize the register prefetch that is meant to stay in flight across the barrier.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 struct Args {
   const uint16_t* dm;    // [M][C4]
   const uint16_t* y3;    // [M][C4]
@@ -89,6 +98,7 @@ __global__ void __launch_bounds__(512, 1) fused_kernel(const Args p) {
   // this workgroup's tiles: blockIdx.x, + gridDim.x, ...
   const int nmine = p.ntiles > (int)blockIdx.x ? (p.ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
   auto tile_of = [&](int i) { return (int)blockIdx.x + i * (int)gridDim.x; };
+  const int nsync = (nmine + 2) & ~1;  // barriers per role: >= nmine + 1, even (loader unroll)
 
   if (loader) {
     const int tid = threadIdx.x - 256;
@@ -132,21 +142,22 @@ __global__ void __launch_bounds__(512, 1) fused_kernel(const Args p) {
         *reinterpret_cast<uint4*>(y2b(b) + lr * C::YS + yc) = ry2[set][i];
       }
     };
-    if (nmine > 0) issue(0, tile_of(0));
-    if (nmine > 1) issue(1, tile_of(1));
-    for (int j = 0; j <= nmine; ++j) {
-      if (j < nmine) {
-        // register sets alternate with j; constant indices keep them in registers
-        if (j & 1) {
-          commit(1, tile_of(j), 1);
-          if (j + 2 < nmine) issue(1, tile_of(j + 2));
-        } else {
-          commit(0, tile_of(j), 0);
-          if (j + 2 < nmine) issue(0, tile_of(j + 2));
-        }
-      }
-      __syncthreads();
+    // loads are issued unconditionally (past the end: the last tile again, discarded) and the
+    // loop is unrolled by the two register sets, so every trip issues the same loads in the same
+    // order and the compiler's vmcnt waits stay counted (a conditional issue makes it wait for
+    // everything, which serializes the two tiles in flight)
+    const int last = nmine > 0 ? nmine - 1 : 0;
+    issue(0, tile_of(0));
+    issue(1, tile_of(min(1, last)));
+    for (int j = 0; j < nsync; j += 2) {
+      if (j < nmine) commit(0, tile_of(j), 0);
+      issue(0, tile_of(min(j + 2, last)));
+      lds_barrier();
+      if (j + 1 < nmine) commit(1, tile_of(j + 1), 1);
+      issue(1, tile_of(min(j + 3, last)));
+      lds_barrier();
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the discarded tail prefetch
     __syncthreads();  // statistics fold (math waves)
     __syncthreads();
     __syncthreads();
@@ -175,8 +186,8 @@ __global__ void __launch_bounds__(512, 1) fused_kernel(const Args p) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) dw[i][0] = dw[i][1] = zero16();
 
-  for (int j = 0; j <= nmine; ++j) {
-    if (j >= 1) {
+  for (int j = 0; j < nsync; ++j) {
+    if (j >= 1 && j <= nmine) {
       const int t = tile_of(j - 1), cur = (j - 1) & 1;
       const uint16_t* dx = dxb(cur);
       const uint16_t* yy = y2b(cur);
@@ -225,7 +236,7 @@ __global__ void __launch_bounds__(512, 1) fused_kernel(const Args p) {
         Vec8<T>::store(dst + 8, *reinterpret_cast<float(*)[8]>(&g[8]));
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
 
   // bn2 partial row: lanes (wave, h) own channels 32 (wave & 1) + 16 h + r; sum over pixels

@@ -37,6 +37,7 @@
 #include "apex_amd/fastdiv.h"
 #include "apex_amd/mfma.h"
 
+#include <cstdlib>
 #include <stdexcept>
 
 namespace apex_amd {
@@ -47,6 +48,15 @@ constexpr int CO = 64;          // output channels
 constexpr int KROW = 32;        // k per kernel row: 8 columns x 4 channels
 constexpr int KT = 7 * KROW;    // 224
 constexpr int NKS = KT / 16;    // 14 MFMA k-steps
+
+// LDS-only barrier: this wave's LDS accesses complete, then a raw s_barrier.  __syncthreads()
+// also drains every outstanding GLOBAL load (its workgroup fence waits vmcnt), which would
+// serialize the register prefetch that is meant to stay in flight across the barrier.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 
 struct Geo {
   int n, h, w, cin;
@@ -184,15 +194,15 @@ __global__ void __launch_bounds__(256, 1) fprop_kernel(const FpArgs a) {
   // double-buffered: the next tile's 14 loads are in flight under this tile's 28 MFMAs
   s16x8 b0[NKS], b1[NKS];
   uint32_t p0 = 0, p1 = 0;
-  if (t0 < t1) load(b0, src_of(t0, p0));
-  if (t0 + 1 < t1) load(b1, src_of(t0 + 1, p1));
+  // unconditional loads (past the end: a clamped tile, discarded) so the waits stay counted
+  const int tl = t1 > t0 ? t1 - 1 : t0;
+  load(b0, src_of(t0, p0));
+  load(b1, src_of(min(t0 + 1, tl), p1));
   for (int tile = t0; tile < t1; tile += 2) {
     step(b0, p0);
-    if (tile + 2 < t1) load(b0, src_of(tile + 2, p0));
-    if (tile + 1 < t1) {
-      step(b1, p1);
-      if (tile + 3 < t1) load(b1, src_of(tile + 3, p1));
-    }
+    load(b0, src_of(min(tile + 2, tl), p0));
+    if (tile + 1 < t1) step(b1, p1);
+    load(b1, src_of(min(tile + 3, tl), p1));
   }
 
   // fold the statistics: per-lane sums -> LDS -> one row per workgroup (fixed order)
@@ -216,7 +226,7 @@ __global__ void __launch_bounds__(256, 1) fprop_kernel(const FpArgs a) {
 }
 
 // ---- BN apply + ReLU + 3x3/2 max pool (pad 1) -------------------------------------------------
-constexpr int PR = 4;  // pooled rows per lane
+constexpr int PR = 2;  // pooled rows per lane: 5 input rows x 3 columns, all loads issued first
 
 struct PoolArgs {
   const uint16_t* y;   // [N][OH][OW][64]
@@ -227,25 +237,23 @@ struct PoolArgs {
   int strips;
 };
 
+// horizontal best (value, column) of one loaded input row: the value the unfused apply pass
+// would store, so argmax ties resolve identically; strict > keeps the first maximum
 template <typename T>
-__device__ __forceinline__ void hbest(const PoolArgs& a, int nn, int yr, int pw, int c8, const float (&sc)[8],
+__device__ __forceinline__ void hbest(const uint4 (&raw)[3], const bool (&ok)[3], const float (&sc)[8],
                                       const float (&sh)[8], float (&hv)[8], int (&hk)[8]) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     hv[e] = -INFINITY;
     hk[e] = 0;
   }
-  if (yr < 0 || yr >= a.g.oh) return;
-  const uint16_t* row = a.y + ((size_t)(nn * a.g.oh + yr) * a.g.ow) * CO + c8 * 8;
 #pragma unroll
   for (int b = 0; b < 3; ++b) {
-    const int col = 2 * pw - 1 + b;
-    if (col < 0 || col >= a.g.ow) continue;
+    if (!ok[b]) continue;
     float v[8];
-    Vec8<T>::load(v, reinterpret_cast<const T*>(row + (size_t)col * CO));
+    Vec8<T>::load(v, reinterpret_cast<const T*>(&raw[b]));
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      // the value the unfused apply pass would store, so argmax ties resolve identically
       const float o = to_f(from_f<T>(fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f)));
       if (o > hv[e]) {
         hv[e] = o;
@@ -265,21 +273,36 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(const PoolArgs a) {
     const int pw = (int)(r % (uint32_t)g.pw);
     r /= (uint32_t)g.pw;
     const int strip = (int)(r % (uint32_t)a.strips), nn = (int)(r / (uint32_t)a.strips);
+    const int ph0 = strip * PR;
+    // input rows 2 ph0 - 1 .. 2 ph0 + 3, columns 2 pw - 1 .. 2 pw + 1
+    uint4 raw[2 * PR + 1][3];
+    bool ok[2 * PR + 1][3];
+#pragma unroll
+    for (int rr = 0; rr < 2 * PR + 1; ++rr) {
+      const int yr = 2 * ph0 - 1 + rr;
+#pragma unroll
+      for (int b = 0; b < 3; ++b) {
+        const int col = 2 * pw - 1 + b;
+        ok[rr][b] = yr >= 0 && yr < g.oh && col >= 0 && col < g.ow;
+        // clamped address, unconditional load (no branch around loads: counted vmcnt waits)
+        const int yc = min(max(yr, 0), g.oh - 1), cc = min(max(col, 0), g.ow - 1);
+        raw[rr][b] = *reinterpret_cast<const uint4*>(a.y + ((size_t)(nn * g.oh + yc) * g.ow + cc) * CO + c8 * 8);
+      }
+    }
     float sc[8], sh[8];
     Vec8<float>::load(sc, a.coef + c8 * 8);
     Vec8<float>::load(sh, a.coef + CO + c8 * 8);
-    const int ph0 = strip * PR;
     float cv[8];
     int ck[8];
-    hbest<T>(a, nn, 2 * ph0 - 1, pw, c8, sc, sh, cv, ck);
-#pragma unroll 1
+    hbest<T>(raw[0], ok[0], sc, sh, cv, ck);
+#pragma unroll
     for (int j = 0; j < PR; ++j) {
       const int ph = ph0 + j;
       if (ph >= g.ph) break;
       float v1[8], v2[8];
       int k1[8], k2[8];
-      hbest<T>(a, nn, 2 * ph, pw, c8, sc, sh, v1, k1);
-      hbest<T>(a, nn, 2 * ph + 1, pw, c8, sc, sh, v2, k2);
+      hbest<T>(raw[2 * j + 1], ok[2 * j + 1], sc, sh, v1, k1);
+      hbest<T>(raw[2 * j + 2], ok[2 * j + 2], sc, sh, v2, k2);
       float best[8];
       uint32_t bi[8];
 #pragma unroll
@@ -327,26 +350,25 @@ struct BwdArgs {
 struct Gather {
   uint2 ix[4];
   uint4 gv[4];
-  uint32_t kk[4];  // window index the pixel has in each window (255: no window)
+  uint32_t kk;  // byte s: the window index the pixel has in window s (255: no window)
 };
 
 __device__ __forceinline__ void gather_issue(const BwdArgs& a, uint32_t nn, int yh, int yw, int c8, Gather& G) {
   const int hh = yh + 1, ww = yw + 1;
   const int ph_lo = hh >= 3 ? ((hh - 3) >> 1) + 1 : 0, ph_hi = min(a.g.ph - 1, hh >> 1);
   const int pw_lo = ww >= 3 ? ((ww - 3) >> 1) + 1 : 0, pw_hi = min(a.g.pw - 1, ww >> 1);
+  G.kk = 0;
+  // every slot loads (a missing window re-reads a valid one and can never match): no branch
+  // around a load, so the compiler's vmcnt waits stay counted
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int ph = ph_lo + (s >> 1), pw = pw_lo + (s & 1);
-    if (ph <= ph_hi && pw <= pw_hi) {
-      G.kk[s] = (uint32_t)((hh - 2 * ph) * 3 + (ww - 2 * pw));
-      const size_t o = ((size_t)(nn * a.g.ph + ph) * a.g.pw + pw) * CO + c8 * 8;
-      G.ix[s] = *reinterpret_cast<const uint2*>(a.idx + o);
-      G.gv[s] = *reinterpret_cast<const uint4*>(a.dp + o);
-    } else {
-      G.kk[s] = 255u;  // never matches a stored index (0..8)
-      G.ix[s] = make_uint2(0, 0);
-      G.gv[s] = make_uint4(0, 0, 0, 0);
-    }
+    const bool valid = ph <= ph_hi && pw <= pw_hi;
+    const int phc = min(ph, ph_hi), pwc = min(pw, pw_hi);
+    G.kk |= (valid ? (uint32_t)((hh - 2 * ph) * 3 + (ww - 2 * pw)) : 255u) << (8 * s);
+    const size_t o = ((size_t)(nn * a.g.ph + phc) * a.g.pw + pwc) * CO + c8 * 8;
+    G.ix[s] = *reinterpret_cast<const uint2*>(a.idx + o);
+    G.gv[s] = *reinterpret_cast<const uint4*>(a.dp + o);
   }
 }
 
@@ -362,7 +384,7 @@ __device__ __forceinline__ void gather_sum(const Gather& G, float (&gs)[8]) {
     for (int e = 0; e < 8; ++e) {
       const uint32_t k = (w[e >> 2] >> (8 * (e & 3))) & 0xffu;
       const float v = to_f(T{(uint16_t)((gw[e >> 1] >> (16 * (e & 1))) & 0xffffu)});
-      gs[e] += k == G.kk[s] ? v : 0.f;
+      gs[e] += k == ((G.kk >> (8 * s)) & 0xffu) ? v : 0.f;
     }
   }
 }
@@ -377,21 +399,34 @@ __global__ void __launch_bounds__(256) bwd_reduce_kernel(const BwdArgs a) {
   Vec8<float>::load(mu, a.mean + c8 * 8);
 #pragma unroll
   for (int e = 0; e < 8; ++e) a1[e] = a2[e] = 0.f;
-  const uint32_t total = a.g.m * 8u;
-  for (uint32_t i = blockIdx.x * 256u + tid; i < total; i += gridDim.x * 256u) {
-    const uint32_t pix = i >> 3;
-    const uint32_t nn = fdiv(pix, a.div_ohw), rem = pix - nn * a.div_ohw.d;
-    const uint32_t yh = fdiv(rem, a.div_ow), yw = rem - yh * a.div_ow.d;
-    Gather G;
-    gather_issue(a, nn, (int)yh, (int)yw, c8, G);
-    float v[8], gs[8];
-    Vec8<T>::load(v, reinterpret_cast<const T*>(a.y + (size_t)pix * CO + c8 * 8));
-    gather_sum<T>(G, gs);
+  const uint32_t total = a.g.m * 8u, stride = gridDim.x * 256u;
+  // two items per trip, every load of both issued before either is consumed
+  for (uint32_t i0 = blockIdx.x * 256u + tid; i0 < total; i0 += 2 * stride) {
+    Gather G[2];
+    uint4 yv[2];
+    bool live[2];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float gm = fmaf(v[e], sc[e], sh[e]) > 0.f ? gs[e] : 0.f;
-      a1[e] += gm;
-      a2[e] = fmaf(gm, v[e] - mu[e], a2[e]);
+    for (int u = 0; u < 2; ++u) {
+      const uint32_t i = i0 + u * stride;
+      live[u] = i < total;
+      const uint32_t pix = (live[u] ? i : i0) >> 3;
+      const uint32_t nn = fdiv(pix, a.div_ohw), rem = pix - nn * a.div_ohw.d;
+      const uint32_t yh = fdiv(rem, a.div_ow), yw = rem - yh * a.div_ow.d;
+      gather_issue(a, nn, (int)yh, (int)yw, c8, G[u]);
+      yv[u] = *reinterpret_cast<const uint4*>(a.y + (size_t)pix * CO + c8 * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (!live[u]) continue;
+      float v[8], gs[8];
+      Vec8<T>::load(v, reinterpret_cast<const T*>(&yv[u]));
+      gather_sum<T>(G[u], gs);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float gm = fmaf(v[e], sc[e], sh[e]) > 0.f ? gs[e] : 0.f;
+        a1[e] += gm;
+        a2[e] = fmaf(gm, v[e] - mu[e], a2[e]);
+      }
     }
   }
 #pragma unroll
@@ -409,53 +444,53 @@ __global__ void __launch_bounds__(256) bwd_reduce_kernel(const BwdArgs a) {
 }
 
 // ---- backward: weight gradient with the BN-backward prologue ---------------------------------
-constexpr int WPX = 64;           // pixels per step
+constexpr int WPX = 128;          // pixels per step
 constexpr int DSTR = CO + 32;     // dX image row stride (elements): rows 192 B apart in bank space
 constexpr int ISTR = KT + 64;     // im2col image row stride: rows 64 B apart in bank space
-constexpr int WG_LDS = 2 * WPX * (DSTR + ISTR) * 2;
+constexpr int WG_LDS = WPX * (DSTR + ISTR) * 2;
+constexpr int WG_NI = WPX * 8 / 512;          // dX items (pixel, 8 channels) per thread per step
+constexpr int WG_NP = (WPX * 7 + 511) / 512;  // im2col (pixel, kernel row) pairs per thread per step
 
-template <typename T>
-__global__ void __launch_bounds__(256, 1) wgrad_kernel(const BwdArgs a) {
+// All 8 waves stage and all run MFMAs.  A step is 128 pixels: its loads are issued BEFORE the
+// previous step's MFMAs (they land under them), committed to the single LDS stage after an
+// LDS-only barrier, and consumed after a second one.  One memory latency per 128 pixels instead of
+// one per 32: the prefetch that a register double-buffer is meant to provide does not survive the
+// compiler's loop rotation here (it copies in-flight load destinations and waits on them).
+// MODE (diagnostics, APEX_AMD_STEM_WG_MODE; 0 in production): bit 0 skips the pooled-gradient
+// gather, bit 1 the MFMAs, bit 2 the im2col loads
+template <typename T, int MODE>
+__global__ void __launch_bounds__(512, 1) wgrad_kernel(const BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
-  auto dbuf = [&](int b) { return lds + b * WPX * (DSTR + ISTR); };
-  auto ibuf = [&](int b) { return lds + b * WPX * (DSTR + ISTR) + WPX * DSTR; };
+  __shared__ __attribute__((aligned(16))) float cf[5 * CO];  // forward scale | shift, backward A | B | K
+  uint16_t* dl = lds;
+  uint16_t* il = lds + WPX * DSTR;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, pl = lane & 31;
   const Geo& g = a.g;
   const uint32_t p_begin = blockIdx.x * a.chunk;
   const uint32_t p_end = min(p_begin + a.chunk, g.m);
   const int steps = p_begin < p_end ? (int)((p_end - p_begin + WPX - 1) / WPX) : 0;
+  for (int i = tid; i < 5 * CO; i += 512) cf[i] = i < 2 * CO ? a.coef[i] : a.cb[i - 2 * CO];
+  const int c8 = tid & 7;
   const size_t rowstep = (size_t)g.wp * 4;
 
-  // dX items: (pixel, 8 channels) = tid + 256 i; im2col: (pixel, kernel row) pairs tid, tid + 256 (< 448)
-  const int c8 = tid & 7;
-  float sc[8], sh[8], A[8], B[8], K[8];
-  Vec8<float>::load(sc, a.coef + c8 * 8);
-  Vec8<float>::load(sh, a.coef + CO + c8 * 8);
-  Vec8<float>::load(A, a.cb + c8 * 8);
-  Vec8<float>::load(B, a.cb + CO + c8 * 8);
-  Vec8<float>::load(K, a.cb + 2 * CO + c8 * 8);
-
-  Gather G[2];
-  uint4 yv[2];
-  bool live[2];
-  uint4 im[2][4];
-
+  Gather G[WG_NI];
+  uint4 yv[WG_NI], im[WG_NP][4];
   auto issue = [&](int st) {
     const uint32_t base = p_begin + (uint32_t)st * WPX;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const uint32_t pix = base + (uint32_t)((tid + 256 * i) >> 3);
-      live[i] = pix < p_end;
-      const uint32_t pc = live[i] ? pix : p_end - 1;
+    for (int i = 0; i < WG_NI; ++i) {
+      const uint32_t pix = base + (uint32_t)((tid + 512 * i) >> 3);
+      const uint32_t pc = pix < p_end ? pix : p_end - 1;
       const uint32_t nn = fdiv(pc, a.div_ohw), rem = pc - nn * a.div_ohw.d;
       const uint32_t yh = fdiv(rem, a.div_ow), yw = rem - yh * a.div_ow.d;
-      gather_issue(a, nn, (int)yh, (int)yw, c8, G[i]);
+      if constexpr (MODE & 1) G[i] = Gather{};
+      else gather_issue(a, nn, (int)yh, (int)yw, c8, G[i]);
       yv[i] = *reinterpret_cast<const uint4*>(a.y + (size_t)pc * CO + c8 * 8);
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int pr = tid + 256 * i;
-      if (pr >= WPX * 7) continue;
+    for (int i = 0; i < WG_NP; ++i) {
+      // every lane loads (lanes past the last pair re-read pair 0; commit skips their store)
+      const int pr = (tid + 512 * i) < WPX * 7 ? tid + 512 * i : 0;
       const uint32_t pix = base + (uint32_t)(pr / 7);
       const int r = pr % 7;
       const uint32_t pc = pix < p_end ? pix : p_end - 1;
@@ -464,12 +499,20 @@ __global__ void __launch_bounds__(256, 1) wgrad_kernel(const BwdArgs a) {
       const uint4* src = reinterpret_cast<const uint4*>(a.xp + ((size_t)(nn * g.hp + 2 * oh) * g.wp + 2 * ow) * 4 +
                                                          r * rowstep);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) im[i][q] = src[q];
+      for (int q = 0; q < 4; ++q) im[i][q] = (MODE & 4) ? make_uint4(0, 0, 0, 0) : src[q];
     }
   };
-  auto commit = [&](int b) {
+  auto commit = [&](int st) {
+    const uint32_t base = p_begin + (uint32_t)st * WPX;
+    float sc[8], sh[8], A[8], B[8], K[8];
+    Vec8<float>::load(sc, cf + c8 * 8);
+    Vec8<float>::load(sh, cf + CO + c8 * 8);
+    Vec8<float>::load(A, cf + 2 * CO + c8 * 8);
+    Vec8<float>::load(B, cf + 3 * CO + c8 * 8);
+    Vec8<float>::load(K, cf + 4 * CO + c8 * 8);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < WG_NI; ++i) {
+      const bool live = base + (uint32_t)((tid + 512 * i) >> 3) < p_end;
       float gs[8], v[8], dx[8];
       gather_sum<T>(G[i], gs);
       const uint32_t yw4[4] = {yv[i].x, yv[i].y, yv[i].z, yv[i].w};
@@ -478,62 +521,48 @@ __global__ void __launch_bounds__(256, 1) wgrad_kernel(const BwdArgs a) {
         v[e] = to_f(T{(uint16_t)((yw4[e >> 1] >> (16 * (e & 1))) & 0xffffu)});
         const float gm = fmaf(v[e], sc[e], sh[e]) > 0.f ? gs[e] : 0.f;
         // dX rounded to the storage type, as the unfused path's dx tensor
-        dx[e] = live[i] ? fmaf(A[e], gm, fmaf(B[e], v[e], K[e])) : 0.f;
+        dx[e] = live ? fmaf(A[e], gm, fmaf(B[e], v[e], K[e])) : 0.f;
       }
-      Vec8<T>::store(reinterpret_cast<T*>(dbuf(b) + ((tid + 256 * i) >> 3) * DSTR + c8 * 8), dx);
+      Vec8<T>::store(reinterpret_cast<T*>(dl + ((tid + 512 * i) >> 3) * DSTR + c8 * 8), dx);
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int pr = tid + 256 * i;
+    for (int i = 0; i < WG_NP; ++i) {
+      const int pr = tid + 512 * i;
       if (pr >= WPX * 7) continue;
-      uint4* dst = reinterpret_cast<uint4*>(ibuf(b) + (pr / 7) * ISTR + (pr % 7) * KROW);
+      uint4* dst = reinterpret_cast<uint4*>(il + (pr / 7) * ISTR + (pr % 7) * KROW);
 #pragma unroll
       for (int q = 0; q < 4; ++q) dst[q] = im[i][q];
     }
   };
 
-  // wave w owns k-tiles u = w and w + 4 (< 7) for both 32-channel tiles
-  const int nu = wave + 4 < 7 ? 2 : 1;
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) acc[t][0] = acc[t][1] = zero16();
-
-  if (steps > 0) {
-    issue(0);
-    commit(0);
-  }
-  __syncthreads();
+  // waves 0-6 own k-tile u = wave (both 32-channel tiles); wave 7 only stages
+  f32x16 acc[2] = {zero16(), zero16()};
+  __syncthreads();  // cf
+  if (steps > 0) issue(0);
   for (int st = 0; st < steps; ++st) {
-    const int cur = st & 1;
-    const bool more = st + 1 < steps;
-    if (more) issue(st + 1);
-    const uint16_t* dl = dbuf(cur);
-    const uint16_t* il = ibuf(cur);
+    commit(st);
+    lds_barrier();
+    if (st + 1 < steps) issue(st + 1);  // lands under this step's MFMAs
+    if (wave < 7 && !(MODE & 2)) {
 #pragma unroll
-    for (int ks = 0; ks < WPX / 16; ++ks) {
-      const int klo = 16 * ks + 8 * h;
-      const s16x8 a0 = frag_tr<DSTR>(dl, 0, klo, klo + 4, lane);
-      const s16x8 a1 = frag_tr<DSTR>(dl, 32, klo, klo + 4, lane);
-#pragma unroll
-      for (int ui = 0; ui < 2; ++ui) {
-        if (ui >= nu) break;
-        const s16x8 bf = frag_tr<ISTR>(il, 32 * (wave + 4 * ui), klo, klo + 4, lane);
-        acc[0][ui] = mma<T>(a0, bf, acc[0][ui]);
-        acc[1][ui] = mma<T>(a1, bf, acc[1][ui]);
+      for (int ks = 0; ks < WPX / 16; ++ks) {
+        const int klo = 16 * ks + 8 * h;
+        const s16x8 a0 = frag_tr<DSTR>(dl, 0, klo, klo + 4, lane);
+        const s16x8 a1 = frag_tr<DSTR>(dl, 32, klo, klo + 4, lane);
+        const s16x8 bf = frag_tr<ISTR>(il, 32 * wave, klo, klo + 4, lane);
+        acc[0] = mma<T>(a0, bf, acc[0]);
+        acc[1] = mma<T>(a1, bf, acc[1]);
       }
     }
-    if (more) commit(cur ^ 1);
-    __syncthreads();
+    lds_barrier();
   }
-  float* ws = a.ws + (size_t)blockIdx.x * CO * KT;
-#pragma unroll
-  for (int ui = 0; ui < 2; ++ui) {
-    if (ui >= nu) break;
-    const int col = 32 * (wave + 4 * ui) + pl;
+  if (wave < 7) {
+    float* ws = a.ws + (size_t)blockIdx.x * CO * KT;
+    const int col = 32 * wave + pl;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) ws[(size_t)(32 * t + crow(r, h)) * KT + col] = acc[t][ui][r];
+      for (int r = 0; r < 16; ++r) ws[(size_t)(32 * t + crow(r, h)) * KT + col] = acc[t][r];
   }
 }
 
@@ -684,16 +713,26 @@ void stem_wgrad(const void* dp, const uint8_t* idx, const void* y, const float* 
   const int G = stem_wgrad_parts(cus);
   a.chunk = (uint32_t)(((int64_t)a.g.m + G - 1) / G);
   a.chunk = (a.chunk + stem::WPX - 1) / stem::WPX * stem::WPX;
+
   if (cin < 1 || cin > 4) throw std::runtime_error("stem wgrad: 1-4 input channels");
   dispatch_16(t, [&](auto tag) {
     using T = typename decltype(tag)::type;
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem::wgrad_kernel<T>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, stem::WG_LDS);
-      attr = true;
+    static const int mode = [] {
+      const char* e = std::getenv("APEX_AMD_STEM_WG_MODE");
+      return e ? std::atoi(e) : 0;
+    }();
+    auto go = [&](auto kern) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                stem::WG_LDS);
+      hipLaunchKernelGGL(kern, dim3(G), dim3(512), stem::WG_LDS, s, a);
+    };
+    switch (mode) {
+      case 1: go(stem::wgrad_kernel<T, 1>); break;
+      case 2: go(stem::wgrad_kernel<T, 2>); break;
+      case 4: go(stem::wgrad_kernel<T, 4>); break;
+      case 7: go(stem::wgrad_kernel<T, 7>); break;
+      default: go(stem::wgrad_kernel<T, 0>); break;
     }
-    hipLaunchKernelGGL((stem::wgrad_kernel<T>), dim3(G), dim3(256), stem::WG_LDS, s, a);
   }, "stem wgrad");
   dispatch_float(dw_t, [&](auto tag) {
     using TW = typename decltype(tag)::type;
