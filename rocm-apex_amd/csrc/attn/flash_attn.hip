@@ -60,11 +60,24 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x ^= x >> 16;
   return x;
 }
-// Counter-based dropout decision; mirrored in python (apex.contrib.multihead_attn / tests).
-__device__ __forceinline__ uint32_t drop_hash(uint32_t seed_mix, uint32_t bh, uint32_t q, uint32_t k) {
-  const uint32_t a = mix32(seed_mix ^ (bh * 0x9E3779B9u));
-  const uint32_t b = mix32(a ^ (q * 0x85EBCA6Bu));
-  return mix32(b ^ (k * 0xC2B2AE35u));
+// Counter-based dropout decision; mirrored in python (apex.ops.attention.dropout_keep_mask).
+// One 32-bit hash per (batch*head, query, key pair k >> 1): the even key of the pair tests the low
+// 16 bits against t16 = p * 65536, the odd key the high 16 bits.  A hash per pair instead of per
+// element halves the integer work (two quarter-rate v_mul_lo_u32 per mix32), which set the cost
+// of dropout in every attention kernel: the (bh, q) prefix is per row, and the two keys of a pair
+// sit in one lane (forward, dQ: key across the accumulator registers) or in lanes l, l ^ 1 (dK/dV:
+// key on the lane; each lane hashes half the rows and swaps them with its neighbour by DPP).
+__device__ __forceinline__ uint32_t drop_row(uint32_t seed_mix, uint32_t bh, uint32_t q) {
+  return mix32(mix32(seed_mix ^ (bh * 0x9E3779B9u)) ^ (q * 0x85EBCA6Bu));
+}
+__device__ __forceinline__ uint32_t drop_pair(uint32_t row, uint32_t k) {
+  return mix32(row ^ ((k >> 1) * 0xC2B2AE35u));
+}
+__device__ __forceinline__ uint32_t drop_bits(uint32_t h, uint32_t k) { return (k & 1u) ? (h >> 16) : (h & 0xFFFFu); }
+__device__ __forceinline__ uint32_t drop_t16(float p) { return (uint32_t)fminf(p * 65536.f, 65536.f); }
+// neighbour lane's value (lanes l, l ^ 1: DPP quad_perm [1, 0, 3, 2])
+__device__ __forceinline__ uint32_t swap_pair_lane(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
 }
 __host__ __device__ inline uint32_t seed_mix_of(uint64_t seed, uint64_t offset) {
   uint32_t x = (uint32_t)seed ^ ((uint32_t)(seed >> 32) * 0x27d4eb2du) ^ ((uint32_t)offset * 0x165667b1u) ^
@@ -251,10 +264,13 @@ __global__ void __launch_bounds__(256, (fwd_occupancy<D, MODE, QF, LO>())) fwd_k
     const float c = a.scale * kLog2e;
     const float inv_scale = 1.f / a.scale;
     const bool dropout = MODE >= 1 && a.p_drop > 0.f;  // MODE 0: no dropout (compiled out)
-    const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
+    const uint32_t thresh = drop_t16(a.p_drop);
     const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
     const uint32_t smix = seed_mix_of(a.seed, drop_offset(a));
     const uint32_t bh = (uint32_t)(b * a.h + hq);
+    uint32_t drow[QF];
+    #pragma unroll
+    for (int f = 0; f < QF; ++f) drow[f] = dropout ? drop_row(smix, bh, (uint32_t)myq[f]) : 0u;
     const float* biasb = (MODE == 2 && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh : nullptr;
 
     if (nkb > 0) {
@@ -340,12 +356,14 @@ __global__ void __launch_bounds__(256, (fwd_occupancy<D, MODE, QF, LO>())) fwd_k
             for (int r = 0; r < 16; ++r) o[f][i][r] *= alpha;
         }
         if (dropout) {
+          // registers r, r + 1 (r even) hold keys k, k + 1 of one pair: one hash for both
           #pragma unroll
           for (int t = 0; t < 2; ++t)
             #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const uint32_t key = (uint32_t)(kb0 + 32 * t + crow(r, h2));
-              x[0][t][r] *= drop_hash(smix, bh, (uint32_t)myq[f], key) >= thresh ? inv_keep : 0.f;
+            for (int r = 0; r < 16; r += 2) {
+              const uint32_t hp = drop_pair(drow[f], (uint32_t)(kb0 + 32 * t + crow(r, h2)));
+              x[0][t][r] *= (hp & 0xFFFFu) >= thresh ? inv_keep : 0.f;
+              x[0][t][r + 1] *= (hp >> 16) >= thresh ? inv_keep : 0.f;
             }
         }
         #pragma unroll
@@ -475,7 +493,7 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
   for (int i = 0; i < NDT; ++i) dk[i] = dv[i] = zero16();
   const float c = a.scale * kLog2e;
   const bool dropout = !PLAIN && a.p_drop > 0.f;  // PLAIN: no bias, no dropout (compiled out)
-  const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
+  const uint32_t thresh = drop_t16(a.p_drop);
   const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
   const uint32_t smix = seed_mix_of(a.seed, drop_offset(a));
   const int group = a.h / a.h_k;
@@ -568,7 +586,9 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
         float dpv = dpacc[r];
         float pd = pv;
         if (dropout) {
-          const float mk = drop_hash(smix, bh, (uint32_t)q, (uint32_t)mykey) >= thresh ? inv_keep : 0.f;
+          const float mk =
+              drop_bits(drop_pair(drop_row(smix, bh, (uint32_t)q), (uint32_t)mykey), (uint32_t)mykey) >= thresh
+                  ? inv_keep : 0.f;
           pd = pv * mk;
           dpv *= mk;
         }
@@ -735,7 +755,7 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
     for (int i = 0; i < NDT; ++i) dk[i] = dv[i] = zero16();
     const float c = a.scale * kLog2e;
     const bool dropout = MODE >= 1 && a.p_drop > 0.f;  // MODE 0: no dropout (compiled out)
-    const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
+    const uint32_t thresh = drop_t16(a.p_drop);
     const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
     const uint32_t smix = seed_mix_of(a.seed, drop_offset(a));
     const int group = a.h / a.h_k;
@@ -835,20 +855,26 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
             p[r] = ok ? xv : -INFINITY;
           }
         }
+        // dropout: lanes l, l ^ 1 hold keys k, k ^ 1 of one pair and need the same 16 row hashes;
+        // each hashes the rows of its own parity (the (bh, q) prefix read from LDS) and takes the
+        // other half from its neighbour
+        const uint32_t par = (uint32_t)ql & 1u;
         #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int qr = crow(r, h2), q = q0s + qr;
-          const float pv = fast_exp2(p[r]);
-          float dpv = dpacc[r];
-          float pd = pv;
+        for (int r = 0; r < 16; r += 2) {
+          float pv[2], dpv[2], mk[2] = {1.f, 1.f};
           if (dropout) {
-            // == drop_hash(smix, bh, q, mykey), the (bh, q) prefix read from LDS
-            const float mk = mix32(hb[qr] ^ ((uint32_t)mykey * 0xC2B2AE35u)) >= thresh ? inv_keep : 0.f;
-            pd = pv * mk;
-            dpv *= mk;
+            const uint32_t mine = drop_pair(hb[crow(r, h2) + par], (uint32_t)mykey);
+            const uint32_t other = swap_pair_lane(mine);
+            mk[0] = drop_bits(par ? other : mine, (uint32_t)mykey) >= thresh ? inv_keep : 0.f;
+            mk[1] = drop_bits(par ? mine : other, (uint32_t)mykey) >= thresh ? inv_keep : 0.f;
           }
-          p[r] = pd;
-          ds[r] = pv * (dpv - db[qr]);
+          #pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            pv[j] = fast_exp2(p[r + j]);
+            dpv[j] = dpacc[r + j] * mk[j];
+            p[r + j] = pv[j] * mk[j];
+            ds[r + j] = pv[j] * (dpv[j] - db[crow(r + j, h2)]);
+          }
         }
         #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
@@ -978,10 +1004,11 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dq_kernel(const A
     for (int i = 0; i < NDT; ++i) dq[i] = zero16();
     const float c = a.scale * kLog2e;
     const bool dropout = MODE >= 1 && a.p_drop > 0.f;  // MODE 0: no dropout (compiled out)
-    const uint32_t thresh = (uint32_t)fminf(a.p_drop * 4294967296.f, 4294967295.f);
+    const uint32_t thresh = drop_t16(a.p_drop);
     const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
     const uint32_t smix = seed_mix_of(a.seed, drop_offset(a));
     const uint32_t bh = (uint32_t)(b * a.h + hq);
+    const uint32_t drow = dropout ? drop_row(smix, bh, (uint32_t)myq) : 0u;
     const float* biasp = (MODE == 2 && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh + (int64_t)myq * a.bias_sq
                                 : nullptr;
 
@@ -1028,14 +1055,15 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dq_kernel(const A
       #pragma unroll
       for (int t = 0; t < 2; ++t)
         #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float pv = fast_exp2(ds[t][r]);
-          float dpv = dp[t][r];
-          if (dropout) {
-            const int key = kb0 + 32 * t + crow(r, h2);
-            dpv *= drop_hash(smix, bh, (uint32_t)myq, (uint32_t)key) >= thresh ? inv_keep : 0.f;
+        for (int r = 0; r < 16; r += 2) {
+          float dpv0 = dp[t][r], dpv1 = dp[t][r + 1];
+          if (dropout) {  // registers r, r + 1 hold the two keys of one pair
+            const uint32_t hp = drop_pair(drow, (uint32_t)(kb0 + 32 * t + crow(r, h2)));
+            dpv0 *= (hp & 0xFFFFu) >= thresh ? inv_keep : 0.f;
+            dpv1 *= (hp >> 16) >= thresh ? inv_keep : 0.f;
           }
-          ds[t][r] = pv * (dpv - dlt);
+          ds[t][r] = fast_exp2(ds[t][r]) * (dpv0 - dlt);
+          ds[t][r + 1] = fast_exp2(ds[t][r + 1]) * (dpv1 - dlt);
         }
       // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
       #pragma unroll

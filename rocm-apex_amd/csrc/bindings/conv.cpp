@@ -168,6 +168,47 @@ std::vector<at::Tensor> bn1x1(const at::Tensor& a, const at::Tensor& w, bool w_k
   return {y, part, aout};
 }
 
+// Forward 1x1 conv whose operand is the block below's output computed on load:
+// out = relu(pcoef[0] a + pcoef[1] res + pcoef[2]) (a = that block's output-BN input y3, res = its
+// shortcut: the identity input, or the downsample BN's input with the two BNs folded into pcoef).
+// Returns (y = out . W^T, statistics partials about shift, out [M, K], ReLU bits [M K / 8]).
+std::vector<at::Tensor> bn1x1_addrelu(const at::Tensor& a, const at::Tensor& res, const at::Tensor& pcoef,
+                                      const at::Tensor& w, const c10::optional<at::Tensor>& shift,
+                                      const c10::optional<at::Tensor>& out_opt) {
+  TORCH_CHECK(a.is_cuda() && a.dim() == 2 && a.is_contiguous(), "bn1x1_addrelu: a must be a contiguous [M, K] GPU tensor");
+  TORCH_CHECK(res.is_cuda() && res.is_contiguous() && res.sizes() == a.sizes() && res.scalar_type() == a.scalar_type(),
+              "bn1x1_addrelu: res must be shaped like a");
+  TORCH_CHECK(w.is_cuda() && w.dim() == 2 && w.is_contiguous() && w.scalar_type() == a.scalar_type() &&
+                  w.size(1) == a.size(1),
+              "bn1x1_addrelu: w must be [ncols, K] of a's dtype");
+  const int64_t m = a.size(0);
+  const int k = (int)a.size(1), ncols = (int)w.size(0);
+  TORCH_CHECK(conv1x1_bn_supported(m, k, ncols) && (m * k) % 8 == 0, "bn1x1_addrelu: unsupported shape");
+  TORCH_CHECK(pcoef.is_cuda() && pcoef.scalar_type() == at::kFloat && pcoef.is_contiguous() && pcoef.numel() == 3 * (int64_t)k,
+              "bn1x1_addrelu: pcoef must be contiguous fp32 [3K]");
+  if (shift.has_value())
+    TORCH_CHECK(shift->is_cuda() && shift->scalar_type() == at::kFloat && shift->is_contiguous() && shift->numel() == ncols,
+                "bn1x1_addrelu: shift must be contiguous fp32 [ncols]");
+  const c10::hip::HIPGuard g(a.get_device());
+  const int cus = device_cus(a.get_device());
+  auto y = at::empty({m, ncols}, a.options());
+  at::Tensor out;
+  if (out_opt.has_value()) {
+    TORCH_CHECK(out_opt->is_cuda() && out_opt->is_contiguous() && out_opt->sizes() == a.sizes() &&
+                    out_opt->scalar_type() == a.scalar_type(),
+                "bn1x1_addrelu: out must be a contiguous tensor shaped like a");
+    out = *out_opt;
+  } else {
+    out = at::empty_like(a);
+  }
+  auto bits = at::empty({m * k / 8}, a.options().dtype(at::kByte));
+  auto part = at::empty({2, conv1x1_bn_partials(m, k, ncols, true, cus, true), ncols}, a.options().dtype(at::kFloat));
+  conv1x1_bn(a.data_ptr(), w.data_ptr(), y.data_ptr(), m, k, ncols, false, dtype_code(a.scalar_type()),
+             pcoef.data_ptr<float>(), shift.has_value() ? shift->data_ptr<float>() : nullptr, part.data_ptr<float>(), cus,
+             cur_stream(), nullptr, res.data_ptr(), out.data_ptr(), true, bits.data_ptr<uint8_t>());
+  return {y, part, out, bits};
+}
+
 // (save_mean, save_invstd, coef[2C]) from bn1x1 partials; running stats updated in place
 std::vector<at::Tensor> bn_finalize(const at::Tensor& part, double count, const c10::optional<at::Tensor>& shift,
                                     const c10::optional<at::Tensor>& w, const c10::optional<at::Tensor>& b,
@@ -492,6 +533,8 @@ void bind_conv(pybind11::module_& root) {
         pybind11::arg("stats") = false, pybind11::arg("res") = pybind11::none(),
         pybind11::arg("py") = pybind11::none(), pybind11::arg("want_aout") = false);
   m.def("bn_finalize", &bn_finalize);
+  m.def("bn1x1_addrelu", &bn1x1_addrelu, pybind11::arg("a"), pybind11::arg("res"), pybind11::arg("pcoef"),
+        pybind11::arg("w"), pybind11::arg("shift") = pybind11::none(), pybind11::arg("out") = pybind11::none());
   m.def("wgrad3x3", &wgrad3x3, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("stride"),
         pybind11::arg("xcoef") = pybind11::none(), pybind11::arg("out_dtype") = pybind11::none());
   m.def("dgrad_bnred", &dgrad_bnred, pybind11::arg("g"), pybind11::arg("w"), pybind11::arg("res"),

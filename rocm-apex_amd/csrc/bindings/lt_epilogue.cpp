@@ -290,6 +290,26 @@ std::vector<at::Tensor> lt_wgrad_bgrad(at::Tensor g, at::Tensor x, bool with_bia
   return {dw};
 }
 
+// Row-major C[M, N] = op(a) op(b) with op(a) [M, K], op(b) [K, N] (a stored [K, M] when trans_a,
+// b stored [N, K] when trans_b); no epilogue.  The plain dgrad / wgrad GEMMs of the dense layers go
+// through here so they get the same per-shape top-k timing as the epilogue GEMMs (torch.matmul
+// takes the heuristic's first answer).  Empty list when the library has no kernel.
+std::vector<at::Tensor> lt_mm(at::Tensor a, at::Tensor b, bool trans_a, bool trans_b) {
+  check2d(a, "a");
+  check2d(b, "b");
+  const c10::hip::HIPGuard guard(a.get_device());
+  TORCH_CHECK(a.scalar_type() == b.scalar_type(), "lt_mm: dtype mismatch");
+  const int64_t M = trans_a ? a.size(1) : a.size(0), K = trans_a ? a.size(0) : a.size(1);
+  const int64_t N = trans_b ? b.size(0) : b.size(1), Kb = trans_b ? b.size(1) : b.size(0);
+  TORCH_CHECK(K == Kb, "lt_mm: inner dimensions differ (", K, " vs ", Kb, ")");
+  auto c = at::empty({M, N}, a.options());
+  // col-major: C^T[N x M] = op(b)^T op(a)^T; b is the library's A, a its B
+  Problem p{N, M, K, trans_b ? K : N, trans_a ? M : K, N, trans_b, trans_a, lt_type(a.scalar_type()),
+            HIPBLASLT_EPILOGUE_DEFAULT, a.get_device()};
+  if (!lt_run(p, b.data_ptr(), a.data_ptr(), c.data_ptr(), nullptr, p.type, nullptr, 0)) return {};
+  return {c};
+}
+
 void lt_clear_cache() {
   std::lock_guard<std::mutex> lock(g_plan_mu);
   plans().clear();
@@ -314,6 +334,8 @@ void bind_lt(pybind11::module_& root) {
   m.def("dgelu_bgrad", &lt_dgelu_bgrad, pybind11::arg("grad"), pybind11::arg("weight"), pybind11::arg("aux"),
         pybind11::arg("with_bgrad") = true);
   m.def("wgrad_bgrad", &lt_wgrad_bgrad);
+  m.def("mm", &lt_mm, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("trans_a") = false,
+        pybind11::arg("trans_b") = false);
   m.def("clear_cache", &lt_clear_cache);
   m.def("plan_table", &lt_plan_table);
   m.attr("EPI_NONE") = 0;

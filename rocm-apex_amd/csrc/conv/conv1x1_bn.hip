@@ -46,7 +46,8 @@ struct Args {
   float* part;          // STATS: [2][gridDim.x][ncols] partial sums (S1 slab, then S2 slab)
   const uint16_t* res;  // nullable [M][ncols]: y += res before the store (a residual gradient)
   const uint16_t* py;   // PRO == kProBnBwd: second operand tensor [M][K] (the BN's input)
-  uint16_t* aout;       // PRO == kProBnBwd, nullable: the transformed operand written out [M][K]
+  uint16_t* aout;       // PRO == kProBnBwd / kProBnAddRelu, nullable: the transformed operand written out [M][K]
+  uint8_t* bout;        // PRO == kProBnAddRelu, nullable: its ReLU bits [M * K / 8] (bit j of byte i = element 8 i + j)
   // RED (dgrad form): the output is the gradient of a ReLU'd batch-norm output (the block
   // below's) — masked with that BN's forward ReLU bits, and its backward reduction
   // sum(g), sum(g * (x - mean)) accumulated per column into part [2][G][ncols]
@@ -61,11 +62,17 @@ constexpr int kProNone = 0;
 constexpr int kProBnRelu = 1;  // a' = relu(a * c[k] + c[K + k])            (BN apply + ReLU)
 constexpr int kProBnBwd = 2;   // a' = c[k] * a + c[K + k] * y + c[2K + k]  (BN backward dx from the
                                //       masked gradient a and the BN input y: bwd_apply fused)
+constexpr int kProBnAddRelu = 3;  // a' = relu(c[k] * a + c[K + k] * y + c[2K + k]): the block below's
+                                  //   output BN + residual (y) + ReLU, so its apply pass is gone; a'
+                                  //   and its ReLU bits are written out for the block's other uses
+// per-k coefficient rows of a prologue
+constexpr int pro_rows(int pro) { return pro == kProBnRelu ? 2 : (pro == kProBnBwd || pro == kProBnAddRelu) ? 3 : 0; }
+constexpr bool pro_two(int pro) { return pro == kProBnBwd || pro == kProBnAddRelu; }  // a second operand
 
 constexpr int kSS = 64 + 8;  // staging row stride (elements): rows h and h+4 land 16 banks apart
 
 constexpr int lds_bytes_nw(int nc, int kr, int pro, bool red, int nw) {
-  return nc * (kr + 8) * 2 + nw * 32 * kSS * 2 + (pro == kProBnRelu ? 2 : pro == kProBnBwd ? 3 : 0) * kr * 4 +
+  return nc * (kr + 8) * 2 + nw * 32 * kSS * 2 + pro_rows(pro) * kr * 4 +
          (red ? nw * 2 * nc * 4 : 0);
 }
 
@@ -85,7 +92,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
   // k depth per register chunk: 128, 64 at 256 columns (128 accumulator registers); the two-
   // tensor BN-backward prologue halves it again (it holds a second operand's fragments)
   constexpr int KCH0 = NC >= 256 ? 64 : 128;
-  constexpr int KCH1 = PRO == kProBnBwd ? KCH0 / 2 : KCH0;
+  constexpr int KCH1 = pro_two(PRO) ? KCH0 / 2 : KCH0;
   constexpr int KCH = KR < KCH1 ? KR : KCH1;
   constexpr int KC = KCH / 16;               // k-steps per chunk
   constexpr int NCH = KR / KCH;              // chunks per tile
@@ -94,7 +101,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
   uint16_t* bimg = lds;                       // [NC][BS]
   uint16_t* stg = lds + NC * BS;              // [kWaves][32][kSS]
   float* pc = reinterpret_cast<float*>(stg + kWaves * 32 * kSS);  // [2 or 3][KR]
-  float* rsum = pc + (PRO == kProBnRelu ? 2 : PRO == kProBnBwd ? 3 : 0) * KR;  // RED: [kWaves][2][NC]
+  float* rsum = pc + pro_rows(PRO) * KR;  // RED: [kWaves][2][NC]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, lr = lane & 31, lh = lane >> 5;
   const int col0 = blockIdx.y * NC;
@@ -119,7 +126,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
     }
   }
   if constexpr (PRO != kProNone)
-    for (int i = tid; i < (PRO == kProBnBwd ? 3 : 2) * KR; i += NT) pc[i] = p.pcoef[i];
+    for (int i = tid; i < pro_rows(PRO) * KR; i += NT) pc[i] = p.pcoef[i];
   float sh[CN], s1[CN], s2[CN];
 #pragma unroll
   for (int cb = 0; cb < CN; ++cb) {
@@ -134,7 +141,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
 #pragma unroll
   for (int cb = 0; cb < CN; ++cb) acc[cb] = zero16();
 
-  constexpr int KY = PRO == kProBnBwd ? KC : 1;
+  constexpr int KY = pro_two(PRO) ? KC : 1;
   struct Frags {
     s16x8 a[KC];
     s16x8 y[KY];
@@ -145,7 +152,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
     const int64_t off = row * KR + ch * KCH + 8 * lh;
 #pragma unroll
     for (int s = 0; s < KC; ++s) f.a[s] = *reinterpret_cast<const s16x8*>(p.a + off + 16 * s);
-    if constexpr (PRO == kProBnBwd) {
+    if constexpr (pro_two(PRO)) {
 #pragma unroll
       for (int s = 0; s < KC; ++s) f.y[s] = *reinterpret_cast<const s16x8*>(p.py + off + 16 * s);
     }
@@ -155,7 +162,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
 #pragma unroll
     for (int s = 0; s < KC; ++s) {
       s16x8 a = f.a[s];
-      if constexpr (PRO == kProBnBwd) {
+      if constexpr (pro_two(PRO)) {
         const int kb = ch * KCH + 16 * s + 8 * lh;
         float c[3][8];
 #pragma unroll
@@ -165,15 +172,22 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
           c[q][0] = u0.x; c[q][1] = u0.y; c[q][2] = u0.z; c[q][3] = u0.w;
           c[q][4] = u1.x; c[q][5] = u1.y; c[q][6] = u1.z; c[q][7] = u1.w;
         }
+        unsigned mb = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float v = fmaf(c[0][j], to_f(T{(uint16_t)a[j]}), fmaf(c[1][j], to_f(T{(uint16_t)f.y[s][j]}), c[2][j]));
+          float v = fmaf(c[0][j], to_f(T{(uint16_t)a[j]}), fmaf(c[1][j], to_f(T{(uint16_t)f.y[s][j]}), c[2][j]));
+          if constexpr (PRO == kProBnAddRelu) {
+            v = fmaxf(v, 0.f);
+            mb |= (v > 0.f ? 1u : 0u) << j;
+          }
           a[j] = (short)from_f<T>(v).x;
         }
-        if (p.aout) {  // dx of the BN, for the weight gradient that also needs it
-          const int64_t row = (int64_t)t * kRowsB + wid * 32 + lr;
-          if (row < p.m) *reinterpret_cast<s16x8*>(p.aout + row * KR + kb) = a;
-        }
+        // BN dx (kProBnBwd: for the weight gradient) / the block output (kProBnAddRelu: the
+        // residual and weight-gradient operand of this block); one column group writes it
+        const int64_t row = (int64_t)t * kRowsB + wid * 32 + lr;
+        if (p.aout && blockIdx.y == 0 && row < p.m) *reinterpret_cast<s16x8*>(p.aout + row * KR + kb) = a;
+        if constexpr (PRO == kProBnAddRelu)
+          if (p.bout && blockIdx.y == 0 && row < p.m) p.bout[(row * KR + kb) >> 3] = (uint8_t)mb;
       }
       if constexpr (PRO == kProBnRelu) {
         const int kb = ch * KCH + 16 * s + 8 * lh;
@@ -553,13 +567,14 @@ bool conv1x1_bn_supported(int64_t m, int k, int ncols) {
   return true;
 }
 
-int conv1x1_bn_partials(int64_t m, int k, int ncols, bool pro, int cus) {
-  return c1bn::grid_x(m, c1bn::col_tile(ncols, k), k, pro ? c1bn::kProBnRelu : c1bn::kProNone, cus, ncols);
+int conv1x1_bn_partials(int64_t m, int k, int ncols, bool pro, int cus, bool pro_addrelu) {
+  return c1bn::grid_x(m, c1bn::col_tile(ncols, k), k,
+                      pro_addrelu ? c1bn::kProBnAddRelu : pro ? c1bn::kProBnRelu : c1bn::kProNone, cus, ncols);
 }
 
 void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int ncols, bool w_kmajor_out, int dtype,
                 const float* pcoef, const float* shift, float* part, int cus, hipStream_t s, const void* res,
-                const void* py, void* aout) {
+                const void* py, void* aout, bool pro_relu, uint8_t* bout) {
   if (!conv1x1_bn_supported(m, k, ncols)) throw std::runtime_error("conv1x1_bn: unsupported shape");
   c1bn::Args args;
   args.a = static_cast<const uint16_t*>(a);
@@ -574,21 +589,32 @@ void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int nco
   args.res = static_cast<const uint16_t*>(res);
   args.py = static_cast<const uint16_t*>(py);
   args.aout = static_cast<uint16_t*>(aout);
+  args.bout = bout;
   const int nc = c1bn::col_tile(ncols, k);
   const bool wt = w_kmajor_out;
   const bool stats = part != nullptr;
-  // py given: the BN-backward prologue (pcoef = [3][k]); else pcoef = the BN apply + ReLU [2][k]
-  const int pro = pcoef == nullptr ? c1bn::kProNone : py ? c1bn::kProBnBwd : c1bn::kProBnRelu;
-  if (aout && pro != c1bn::kProBnBwd) throw std::runtime_error("conv1x1_bn: aout needs the BN-backward prologue");
+  // py given: the two-operand prologue (pcoef = [3][k]) — BN backward, or with pro_relu the block
+  // below's output BN + residual + ReLU; else pcoef = the BN apply + ReLU [2][k]
+  const int pro = pcoef == nullptr ? c1bn::kProNone
+                  : py            ? (pro_relu ? c1bn::kProBnAddRelu : c1bn::kProBnBwd)
+                                  : c1bn::kProBnRelu;
+  if (aout && !c1bn::pro_two(pro)) throw std::runtime_error("conv1x1_bn: aout needs a two-operand prologue");
+  if (bout && pro != c1bn::kProBnAddRelu) throw std::runtime_error("conv1x1_bn: bout needs the add + ReLU prologue");
   auto go = [&](auto tag) {
     using T = typename decltype(tag)::type;
     if (wt) {
       if (stats || pro == c1bn::kProBnRelu)
         throw std::runtime_error("conv1x1_bn: the transposed-weight (dgrad) form takes the BN-backward prologue only");
+      if (pro == c1bn::kProBnAddRelu) throw std::runtime_error("conv1x1_bn: the add + ReLU prologue is a forward option");
       if (pro == c1bn::kProBnBwd) c1bn::dispatch_shape<T, true, c1bn::kProBnBwd, false>(args, nc, k, cus, s);
       else c1bn::dispatch_shape<T, true, c1bn::kProNone, false>(args, nc, k, cus, s);
     } else {
       if (pro == c1bn::kProBnBwd) throw std::runtime_error("conv1x1_bn: BN-backward prologue is a dgrad-form option");
+      if (pro == c1bn::kProBnAddRelu) {
+        if (stats) c1bn::dispatch_shape<T, false, c1bn::kProBnAddRelu, true>(args, nc, k, cus, s);
+        else c1bn::dispatch_shape<T, false, c1bn::kProBnAddRelu, false>(args, nc, k, cus, s);
+        return;
+      }
       if (pro == c1bn::kProBnRelu) {
         if (stats) c1bn::dispatch_shape<T, false, c1bn::kProBnRelu, true>(args, nc, k, cus, s);
         else c1bn::dispatch_shape<T, false, c1bn::kProBnRelu, false>(args, nc, k, cus, s);

@@ -77,12 +77,14 @@ void conv_wgrad(const ConvTapArgs& a, const void* dy, void* dw_out, int out_dtyp
 // (y - shift) and (y - shift)^2 for the consuming batch norm, finalized by conv1x1_bn_finalize.
 // Shapes: k in {64, 128, 256, 512}, ncols % 64 == 0, bf16 / fp16, 16-byte aligned rows.
 bool conv1x1_bn_supported(int64_t m, int k, int ncols);
-int conv1x1_bn_partials(int64_t m, int k, int ncols, bool pro, int cus);
+int conv1x1_bn_partials(int64_t m, int k, int ncols, bool pro, int cus, bool pro_addrelu = false);
 void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int ncols, bool w_kmajor_out, int dtype,
                 const float* pcoef, const float* shift, float* part, int cus, hipStream_t s,
                 const void* res = nullptr,    // nullable [M][ncols]: y += res (same dtype)
                 const void* py = nullptr,     // dgrad form: BN-backward prologue a' = c0 a + c1 py + c2,
-                void* aout = nullptr);        //   pcoef [3][k]; aout (nullable) receives a' [M][k]
+                void* aout = nullptr,         //   pcoef [3][k]; aout (nullable) receives a' [M][k]
+                bool pro_relu = false,        // forward form with py: a' = relu(c0 a + c1 py + c2) (the
+                uint8_t* bout = nullptr);     //   block output: BN + residual + ReLU), bits to bout
 // batch statistics from the partials: save_mean / save_invstd, running-stat EMA (nullable),
 // coef = [scale | shift] of the apply (w, b nullable = affine-free)
 void conv1x1_bn_finalize(const float* part, int g, int c, float n, const float* shift, const float* w, const float* b,

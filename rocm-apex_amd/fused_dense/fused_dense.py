@@ -158,6 +158,21 @@ def native_wgrad_ok(g2, x2):
             and x2.is_contiguous())
 
 
+def wgrad_gemm(g2, x2):
+    """dW[N, K] = g2[M, N]^T x2[M, K] for the dense layers: the native split-K kernel for small
+    outputs (``native_wgrad_ok``), else hipBLASLt through the wrapper's per-shape top-8 timing
+    (``lt_gemm.mm``: 149 vs 176 us for torch.matmul's first-heuristic kernel at the GPT-2 QKV
+    shape 16384 x 3072 x 1024, ties elsewhere; profiles/gemm_routes_r04t.jsonl), else torch."""
+    if native_wgrad_ok(g2, x2):
+        return _g().linear_wgrad(g2, x2)
+    lt = _lt(g2, x2)
+    if lt is not None and hasattr(lt, "mm") and g2.dim() == 2 and x2.dim() == 2:
+        r = lt.mm(g2.contiguous(), x2.contiguous(), True, False)
+        if r:
+            return r[0]
+    return g2.t().matmul(x2)
+
+
 def _lt_bgradb():
     # hipBLASLt's heuristic answers BGRADB at the transformer shapes with a 32x32-tile kernel that
     # runs ~10x slower than the plain wgrad GEMM (1.1 ms vs ~0.1 ms at 16384 tokens,
@@ -173,8 +188,7 @@ def _lib_wgrad(g2, x2, has_bias):
         r = lt.wgrad_bgrad(g2.contiguous(), x2.contiguous(), has_bias)
         if r:
             return r[0], (r[1] if has_bias else None)
-    dw = _g().linear_wgrad(g2, x2) if native_wgrad_ok(g2, x2) else g2.t().matmul(x2)
-    return dw, (g2.sum(0) if has_bias else None)
+    return wgrad_gemm(g2, x2), (_native.column_sum(g2, g2.dtype) if has_bias else None)
 
 
 def _lib_dense_bwd(x, w, gy, has_bias):

@@ -109,14 +109,22 @@ class Bottleneck(nn.Module):
         self.stride = stride
         self.fork_out = False
 
-    def forward_linked(self, x, link_in):
+    def forward_linked(self, x, link_in, nxt=None):
         """Fused-node forward that chains with its neighbours (``ops.bottleneck_bn.BlockLink``):
-        returns ``(out, link_out)``; falls back to ``forward`` (and no link) off the node path."""
+        returns ``(out, link_out)``; falls back to ``forward`` (and no link) off the node path.
+        ``nxt``: the block that consumes the output (it may take over the output pass)."""
         from ..ops import bottleneck_bn
 
         if self.fused_bn and not isinstance(x, tuple) and self.training and bottleneck_bn.block_supported(self, x):
-            link_out = bottleneck_bn.BlockLink()
+            n, _, h, w = x.shape
+            s = self.conv2.stride[0]
+            oh, ow = (h - 1) // s + 1, (w - 1) // s + 1
+            defer = nxt is not None and bottleneck_bn.takes_deferred_input(
+                nxt, (n, self.conv3.out_channels, oh, ow), x.dtype)
+            link_out = bottleneck_bn.BlockLink(defer)
             return bottleneck_bn.bottleneck_forward(self, x, link_in, link_out), link_out
+        if link_in is not None:
+            link_in.materialize()
         return self.forward(x), None
 
     def forward(self, x):
@@ -149,11 +157,16 @@ def run_linked(blocks, x):
     output BN's state (ops/bottleneck_bn.py BlockLink), so block i+1's conv1 data gradient does
     block i's bn3 backward reduction.  Blocks off the node path run unlinked."""
     link = None
-    for blk in blocks:
+    for i, blk in enumerate(blocks):
+        nxt = blocks[i + 1] if i + 1 < len(blocks) and isinstance(blocks[i + 1], Bottleneck) else None
         if isinstance(blk, Bottleneck):
-            x, link = blk.forward_linked(x, link)
+            x, link = blk.forward_linked(x, link, nxt)
         else:
+            if link is not None:
+                link.materialize()
             x, link = blk(x), None
+    if link is not None:
+        link.materialize()
     return x
 
 

@@ -48,10 +48,11 @@ def dropout_keep_mask(seed, offset, bh, sq, sk, p, device="cpu"):
     q = torch.arange(sq, dtype=torch.int64, device=device).view(1, -1, 1)
     k = torch.arange(sk, dtype=torch.int64, device=device).view(1, 1, -1)
     a = _mix32(sm ^ ((bh * 0x9E3779B9) & _M32))
-    b = _mix32(a ^ ((q * 0x85EBCA6B) & _M32))
-    h = _mix32(b ^ ((k * 0xC2B2AE35) & _M32))
-    thresh = min(int(p * 4294967296.0), _M32)
-    return h >= thresh
+    row = _mix32(a ^ ((q * 0x85EBCA6B) & _M32))
+    # one hash per key pair (k >> 1): the even key tests the low 16 bits, the odd key the high
+    h = _mix32(row ^ (((k >> 1) * 0xC2B2AE35) & _M32))
+    bits = torch.where((k & 1) == 1, h >> 16, h & 0xFFFF)
+    return bits >= min(int(p * 65536.0), 65536)
 
 
 def _native_ok(q, k, v, bias):

@@ -48,6 +48,8 @@ FORCE_NATIVE = os.environ.get("APEX_AMD_FUSED_BLOCK_FORCE_NATIVE", "0") == "1"
 _NATIVE_K = (64, 128, 256, 512)
 # conv3's fused data + weight gradient (csrc/conv/conv3_bwd.hip); 0 = the two-kernel path (A/B)
 _C3B = os.environ.get("APEX_AMD_CONV3_BWD", "1") != "0"
+# block output pass deferred into the next block's conv1 (BlockLink.defer); 0 = A/B off
+_DEFER = os.environ.get("APEX_AMD_DEFER_OUTPUT", "1") != "0"
 
 
 def _conv():
@@ -75,12 +77,29 @@ class BlockLink:
     and accumulates bn3_i's backward reduction in the same kernel (``dgrad_bnred``), returning
     the masked gradient and leaving the partial sums in ``part``; block i then finalizes them
     instead of re-reading its output gradient — one full read + write of the block output saved
-    per block boundary."""
+    per block boundary.
 
-    __slots__ = ("y3", "bits", "mean", "invstd", "part")
+    Forward, when the block above runs its conv1 on the native kernel (``defer``): block i does
+    not run its output pass; it leaves (y3, shortcut, folded coefficients, an empty output
+    tensor) in ``pend`` and block i+1's conv1 computes relu(bn3(y3) + shortcut) on its operand
+    load, writing the output and its ReLU bits as by-products (``bn1x1_addrelu``) — one full read
+    of the block output saved per boundary.  ``materialize`` runs the plain output pass instead
+    for a consumer that does not take it."""
 
-    def __init__(self):
-        self.y3 = self.bits = self.mean = self.invstd = self.part = None
+    __slots__ = ("y3", "bits", "mean", "invstd", "part", "defer", "pend")
+
+    def __init__(self, defer=False):
+        self.y3 = self.bits = self.mean = self.invstd = self.part = self.pend = None
+        self.defer = defer
+
+    def materialize(self):
+        if self.pend is None:
+            return
+        y3, res, _, out2, c3, cd = self.pend
+        self.pend = None
+        o, self.bits = (_bn().apply(y3, res, c3, True, True) if cd is None
+                        else _bn().apply(y3, res, c3, True, True, cd))
+        out2.copy_(o)
 
 
 class _BN:
@@ -257,8 +276,16 @@ class _BottleneckFn(torch.autograd.Function):
         width = w1.size(0)
         cout = w3.size(0)
         x2 = _m2(x)
-        # conv1 (+ bn1 statistics) -> bn1 apply + ReLU
-        y1, sm1, si1, c1, in1 = conv1x1_bn_fwd(x2, w1.view(width, cin), None, bn1)
+        # conv1 (+ bn1 statistics) -> bn1 apply + ReLU; with a deferred block below, conv1 computes
+        # that block's output (BN + shortcut + ReLU) on its operand load and writes it into x
+        if link_in is not None and link_in.pend is not None:
+            y3p, resp, pc3, outp, _, _ = link_in.pend
+            link_in.pend = None
+            DEFERRED_TAKEN[0] += 1
+            y1, part1, _, link_in.bits = _conv().bn1x1_addrelu(y3p, resp, pc3, w1.view(width, cin), bn1.rm, out=outp)
+            sm1, si1, c1, in1 = finalize_part(part1, float(x2.size(0)), bn1)
+        else:
+            y1, sm1, si1, c1, in1 = conv1x1_bn_fwd(x2, w1.view(width, cin), None, bn1)
         z1 = _bn().apply(y1, None, c1, True)[0]
         # conv2 (3x3, stride) -> bn2 statistics (in the native conv's epilogue where it runs)
         z1v = _nchw(z1, n, h, wd)
@@ -274,15 +301,24 @@ class _BottleneckFn(torch.autograd.Function):
             sm2, si2, c2, in2 = stats_pass(y2m, bn2)
         # conv3 with bn2's apply + ReLU on its operand load (+ bn3 statistics)
         y3, sm3, si3, c3, in3 = conv1x1_bn_fwd(y2m, w3.view(cout, width), c2, bn3)
-        if wds is None:
-            out2, bits = _bn().apply(y3, x2, c3, True, True)
-            yd = smd = sid = cd = ind = None
-        else:
+        yd = smd = sid = cd = ind = None
+        if wds is not None:
             if stride == 1:
                 yd, smd, sid, cd, ind = conv1x1_bn_fwd(x2, wds.view(cout, cin), None, bnd)
             else:
                 yd = _m2(_conv_fwd(x, wds, stride, 0))
                 smd, sid, cd, ind = stats_pass(yd, bnd)
+        if link_out is not None and link_out.defer:
+            # the block above computes this output in its conv1 (BlockLink docstring)
+            res = x2 if wds is None else yd
+            sc, sh = c3[:cout], c3[cout:]
+            pc3 = (torch.cat([sc, torch.ones_like(sc), sh]) if wds is None
+                   else torch.cat([sc, cd[:cout], sh + cd[cout:]]))
+            out2, bits = torch.empty_like(y3), None
+            link_out.pend = (y3, res, pc3, out2, c3, cd)
+        elif wds is None:
+            out2, bits = _bn().apply(y3, x2, c3, True, True)
+        else:
             out2, bits = _bn().apply(y3, yd, c3, True, True, cd)
         ctx.save_for_backward(x, w1, w2, w3, wds, g1, g2, g3, gds, y1, z1, y2m, y3, yd, bits,
                               sm1, si1, c1, sm2, si2, c2, sm3, si3, c3, smd, sid, cd, in1, in2, in3, ind)
@@ -314,6 +350,8 @@ class _BottleneckFn(torch.autograd.Function):
             cb3, gg3, gb3 = bwd_from_part(link_out.part, float(go2.size(0)), sm3, si3, g3, gr3, in3)
             link_out.part = None
         else:
+            if bits is None:  # deferred output: its ReLU bits came from the block above's conv1
+                bits = link_out.bits
             dm, cb3, gg3, gb3 = bwd_reduce(go2, y3, g3, sm3, si3, c3, True, bits, gr3, in3)
         w3m = w3.view(cout, width)
         dw3 = None
@@ -406,6 +444,21 @@ def block_supported(block, x):
     chans = (block.conv1.in_channels, block.conv1.out_channels, block.conv3.out_channels)
     return all(c % 64 == 0 for c in chans)
 
+
+def takes_deferred_input(block, x_shape, dtype):
+    """True when ``block`` (the next fused node) will run its conv1 on the native kernel, so the
+    block below may defer its output pass to it (``BlockLink.defer``)."""
+    if not (_DEFER and _ENABLED and getattr(block, "fused_bn", False) and block.training):
+        return False
+    if dtype not in (torch.bfloat16, torch.float16) or block.conv1.weight.dtype != dtype:
+        return False
+    n, c, h, w = x_shape
+    width = block.conv1.out_channels
+    return block.conv1.in_channels == c and _fwd_native(n * h * w, c, width) and _bn_ok(block.bn1)
+
+
+# block outputs computed by the next block's conv1 (BlockLink.defer) since import
+DEFERRED_TAKEN = [0]
 
 # forward calls of the node since import (bench.py reports nodes per step)
 NODE_CALLS = [0]

@@ -102,15 +102,14 @@ from ... import _native  # noqa: E402
 
 
 def _wgrad(go2, ti2):
-    """dW[N, K] = go2[M, N]^T ti2[M, K]: the native split-K MFMA kernel where it beats hipBLASLt
-    (small N x K outputs, e.g. the 1024 x 1024 attention projection at 16k tokens: 66 vs 108 us,
-    profiles/wgrad_shapes_ab_r03.jsonl), else ``torch.matmul``."""
-    from ...fused_dense.fused_dense import native_wgrad_ok
+    """dW[N, K] = go2[M, N]^T ti2[M, K]: fused_dense.wgrad_gemm (the native split-K MFMA kernel for
+    small N x K outputs, e.g. the 1024 x 1024 attention projection at 16k tokens: 64 vs 108 us;
+    hipBLASLt with per-shape top-8 timing otherwise, e.g. the QKV 3072 x 1024: 149 vs 176 us;
+    profiles/gemm_routes_r04t.jsonl)."""
+    if go2.is_cuda:
+        from ...fused_dense.fused_dense import wgrad_gemm
 
-    if native_wgrad_ok(go2, ti2):
-        from ... import _native
-
-        return _native.require("gemm").gemm.linear_wgrad(go2, ti2)
+        return wgrad_gemm(go2, ti2)
     return go2.t().matmul(ti2)
 
 

@@ -262,6 +262,7 @@ def _run_chain(chain, x, gy, node, bn_group=1, group=None, peer=True, linked=Tru
     bottleneck_bn._ENABLED, bottleneck_bn.FORCE_NATIVE = node, True
     bottleneck_bn._conv = lambda: _Spy()
     bottleneck_bn._BottleneckFn.forward = staticmethod(counted)
+    d0 = bottleneck_bn.DEFERRED_TAKEN[0]
     try:
         xi = x.clone().requires_grad_(True)
         if linked:
@@ -276,6 +277,7 @@ def _run_chain(chain, x, gy, node, bn_group=1, group=None, peer=True, linked=Tru
     finally:
         bottleneck_bn._BottleneckFn.forward = staticmethod(orig)
         bottleneck_bn._ENABLED, bottleneck_bn.FORCE_NATIVE, bottleneck_bn._conv = old
+    calls["deferred"] = bottleneck_bn.DEFERRED_TAKEN[0] - d0
     return y.detach(), xi.grad, {n: p.grad for n, p in chain.named_parameters()}, calls
 
 
@@ -298,6 +300,9 @@ def test_gpu_bottleneck_chain_linked_vs_unlinked():
     yb, gb, pb, cb = _run_chain(b, x, gy, True, linked=False)
     yc, gc, pc, cc = _run_chain(c, x, gy, False)
     assert ca["n"] == 3 and cb["n"] == 3 and cc["n"] == 0, (ca, cb, cc)
+    # the linked walk computes blocks 1 and 2's outputs in the next block's conv1 (deferred output
+    # pass); the unlinked arm runs every output pass itself
+    assert ca["deferred"] == 2 and cb["deferred"] == 0, (ca, cb)
     assert ca["red"] == 2 and cb["red"] == 0, (ca, cb)  # both boundaries took the hand-off when linked
     assert torch.equal(ya, yb)
     assert _rel(ga, gb) < 2e-2, _rel(ga, gb)

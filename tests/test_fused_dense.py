@@ -444,3 +444,29 @@ def test_gpu_gelu_pass(dtype):
     y = g.gelu(z)
     ref = torch.nn.functional.gelu(z.float(), approximate="tanh")
     torch.testing.assert_close(y.float(), ref, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("trans_a,trans_b", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_gpu_lt_mm_layouts(trans_a, trans_b, dtype):
+    """lt_gemm.mm (hipBLASLt, per-shape top-8 timing) against an fp32 torch product for every
+    operand layout, and the dense-layer wgrad helper built on it against g^T x."""
+    import apex  # noqa: F401
+    from apex import _native
+    from apex.fused_dense.fused_dense import wgrad_gemm
+
+    lt = _native.require("lt_gemm").lt_gemm
+    torch.manual_seed(0)
+    m, n, k = 192, 320, 256
+    a = torch.randn((k, m) if trans_a else (m, k), device="cuda").to(dtype)
+    b = torch.randn((n, k) if trans_b else (k, n), device="cuda").to(dtype)
+    r = lt.mm(a, b, trans_a, trans_b)
+    assert r, "hipBLASLt has no kernel for this layout"
+    ref = (a.float().t() if trans_a else a.float()) @ (b.float().t() if trans_b else b.float())
+    assert r[0].shape == (m, n)
+    assert float((r[0].float() - ref).norm() / ref.norm()) < 1e-2
+    g = torch.randn(4096, 3072, device="cuda").to(dtype)
+    x = torch.randn(4096, 1024, device="cuda").to(dtype)
+    want = g.float().t() @ x.float()
+    assert float((wgrad_gemm(g, x).float() - want).norm() / want.norm()) < 1e-2
