@@ -84,7 +84,7 @@ constexpr int pick_nw(int nc, int kr, int pro, bool red) {
          : lds_bytes_nw(nc, kr, pro, red, 8) <= 160 * 1024 ? 8 : 4;
 }
 
-template <typename T, int NC, int KR, bool WT, int PRO, bool STATS, bool RED, int NW>
+template <typename T, int NC, int KR, bool WT, int PRO, bool STATS, bool RED, int NW, int DEPTH>
 __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
   constexpr int kWaves = NW, kRowsB = NW * 32, NT = NW * 64;
   constexpr int BS = KR + 8;                 // B image row stride (elements)
@@ -183,11 +183,12 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
           a[j] = (short)from_f<T>(v).x;
         }
         // BN dx (kProBnBwd: for the weight gradient) / the block output (kProBnAddRelu: the
-        // residual and weight-gradient operand of this block); one column group writes it
-        const int64_t row = (int64_t)t * kRowsB + wid * 32 + lr;
-        if (p.aout && blockIdx.y == 0 && row < p.m) *reinterpret_cast<s16x8*>(p.aout + row * KR + kb) = a;
-        if constexpr (PRO == kProBnAddRelu)
-          if (p.bout && blockIdx.y == 0 && row < p.m) p.bout[(row * KR + kb) >> 3] = (uint8_t)mb;
+        // residual and weight-gradient operand of this block): staged in the wave's slab and
+        // written out as whole-row runs after the chunk (below) — a fragment puts one row on
+        // each lane, so direct stores would touch 32 partial cache lines per instruction
+        (void)mb;
+        if (p.aout && blockIdx.y == 0)
+          *reinterpret_cast<s16x8*>(stg + wid * 32 * kSS + lr * kSS + 16 * s + 8 * lh) = a;
       }
       if constexpr (PRO == kProBnRelu) {
         const int kb = ch * KCH + 16 * s + 8 * lh;
@@ -207,6 +208,34 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
       for (int cb = 0; cb < CN; ++cb) {
         const s16x8 b = *reinterpret_cast<const s16x8*>(bimg + (32 * cb + lr) * BS + ch * KCH + 16 * s + 8 * lh);
         acc[cb] = mma<T>(a, b, acc[cb]);
+      }
+    }
+    if constexpr (pro_two(PRO)) {
+      // the chunk's transformed operand [32 rows][KCH] from the slab: KCH / 8 lanes per row, each
+      // 16 B (and, for the add + ReLU prologue, its 8 ReLU bits: one byte)
+      if (p.aout && blockIdx.y == 0) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint16_t* sl = stg + wid * 32 * kSS;
+        constexpr int LPR = KCH / 8;
+        const int64_t row0 = (int64_t)t * kRowsB + wid * 32;
+#pragma unroll
+        for (int i = 0; i < 32 * LPR / 64; ++i) {
+          const int qid = lane + 64 * i, rr = qid / LPR, c8 = (qid % LPR) * 8;
+          const s16x8 v = *reinterpret_cast<const s16x8*>(sl + rr * kSS + c8);
+          if (row0 + rr < p.m) {
+            const int64_t off = (row0 + rr) * KR + ch * KCH + c8;
+            *reinterpret_cast<s16x8*>(p.aout + off) = v;
+            if constexpr (PRO == kProBnAddRelu) {
+              if (p.bout) {
+                unsigned mb = 0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) mb |= (v[j] > 0 ? 1u : 0u) << j;  // relu output: > 0 <=> bits > 0
+                p.bout[off >> 3] = (uint8_t)mb;
+              }
+            }
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
     }
   };
@@ -330,32 +359,69 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
     for (int cb = 0; cb < CN; ++cb) acc[cb] = zero16();
   };
 
-  // flat (tile, chunk) stream, the next chunk's loads in flight under the current one's MFMAs.
-  // The prefetch is unconditional (past the end: the last tile again, discarded): a branch around
-  // the loads makes the compiler's vmcnt waits conservative.
-  Frags fa, fb;
-  int t = blockIdx.x, ch = 0;
+  // flat (tile, chunk) stream with DEPTH - 1 chunks' loads in flight under the current chunk's
+  // math: a ring of DEPTH register sets (2: the next chunk only; 3: two ahead — one chunk's math
+  // is shorter than the HBM latency under full load, so a single chunk in flight leaves every
+  // wave waiting at the top of each chunk).  The prefetch is unconditional (past the end: the last
+  // tile again, discarded): a branch around the loads makes the compiler's vmcnt waits
+  // conservative.
   const int tlast = p.ntiles - 1;
-  load(fa, min(t, tlast), 0);
-  while (t < p.ntiles) {
-    {
-      int nt = t, nch = ch + 1;
-      if (nch == NCH) { nch = 0; nt += gridDim.x; }
-      load(fb, min(nt, tlast), nch);
-      compute(fa, t, ch);
-      if (ch == NCH - 1) epilogue(t);
-      t = nt;
-      ch = nch;
+  auto adv = [&](int& tt, int& cc) {
+    if (++cc == NCH) {
+      cc = 0;
+      tt += gridDim.x;
     }
-    if (t >= p.ntiles) break;
-    {
-      int nt = t, nch = ch + 1;
-      if (nch == NCH) { nch = 0; nt += gridDim.x; }
-      load(fa, min(nt, tlast), nch);
-      compute(fb, t, ch);
+  };
+  int t = blockIdx.x, ch = 0;
+  if constexpr (DEPTH == 2) {
+    Frags fa, fb;
+    load(fa, min(t, tlast), 0);
+    while (t < p.ntiles) {
+      {
+        int nt = t, nch = ch;
+        adv(nt, nch);
+        load(fb, min(nt, tlast), nch);
+        compute(fa, t, ch);
+        if (ch == NCH - 1) epilogue(t);
+        t = nt;
+        ch = nch;
+      }
+      if (t >= p.ntiles) break;
+      {
+        int nt = t, nch = ch;
+        adv(nt, nch);
+        load(fa, min(nt, tlast), nch);
+        compute(fb, t, ch);
+        if (ch == NCH - 1) epilogue(t);
+        t = nt;
+        ch = nch;
+      }
+    }
+  } else {
+    Frags f0, f1, f2;
+    int t1 = t, c1 = ch;
+    adv(t1, c1);
+    int t2 = t1, c2 = c1;
+    adv(t2, c2);
+    load(f0, min(t, tlast), ch);
+    load(f1, min(t1, tlast), c1);
+    // one ring step: prefetch position 2 into `nxt`, run position 0 from `cur`, shift positions
+    auto step = [&](Frags& nxt, const Frags& cur) {
+      load(nxt, min(t2, tlast), c2);
+      compute(cur, t, ch);
       if (ch == NCH - 1) epilogue(t);
-      t = nt;
-      ch = nch;
+      t = t1;
+      ch = c1;
+      t1 = t2;
+      c1 = c2;
+      adv(t2, c2);
+    };
+    while (t < p.ntiles) {
+      step(f2, f0);
+      if (t >= p.ntiles) break;
+      step(f0, f1);
+      if (t >= p.ntiles) break;
+      step(f1, f2);
     }
   }
 
@@ -505,13 +571,21 @@ __global__ void __launch_bounds__(8 * kFinG) bwd_finalize(const float* __restric
   coef[2 * c + ch] = -A * (sdy * inv_n) - B * mean[ch];
 }
 
-template <typename T, int NC, int KR, bool WT, int PRO, bool STATS, bool RED = false>
-void launch_t(const Args& a0, int cus, hipStream_t s) {
+// prefetch ring depth (APEX_AMD_C1BN_DEPTH=2|3 overrides, for A/B): 3 where the third register
+// set fits beside the accumulators without spills (<= 128 columns but 128 x 128), else 2
+static int g_c1bn_depth = [] {
+  const char* e = std::getenv("APEX_AMD_C1BN_DEPTH");
+  return e ? std::atoi(e) : 0;
+}();
+constexpr int default_depth(int nc, int kr) { return nc <= 128 && !(nc == 128 && kr == 128) ? 3 : 2; }
+
+template <typename T, int NC, int KR, bool WT, int PRO, bool STATS, bool RED, int DEPTH>
+void launch_d(const Args& a0, int cus, hipStream_t s) {
   constexpr int NW = pick_nw(NC, KR, PRO, RED);
   constexpr int lds = lds_bytes_nw(NC, KR, PRO, RED, NW);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fused1x1<T, NC, KR, WT, PRO, STATS, RED, NW>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fused1x1<T, NC, KR, WT, PRO, STATS, RED, NW, DEPTH>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
@@ -523,8 +597,15 @@ void launch_t(const Args& a0, int cus, hipStream_t s) {
   const int gy = a.ncols / NC;
   int gx = (cus * per_cu + gy - 1) / gy;
   if (gx > a.ntiles) gx = a.ntiles;
-  hipLaunchKernelGGL((fused1x1<T, NC, KR, WT, PRO, STATS, RED, NW>), dim3(gx, a.ncols / NC), dim3(NW * 64), lds, s,
-                     a);
+  hipLaunchKernelGGL((fused1x1<T, NC, KR, WT, PRO, STATS, RED, NW, DEPTH>), dim3(gx, a.ncols / NC), dim3(NW * 64),
+                     lds, s, a);
+}
+
+template <typename T, int NC, int KR, bool WT, int PRO, bool STATS, bool RED = false>
+void launch_t(const Args& a, int cus, hipStream_t s) {
+  const int d = g_c1bn_depth == 2 || g_c1bn_depth == 3 ? g_c1bn_depth : default_depth(NC, KR);
+  if (d == 3) launch_d<T, NC, KR, WT, PRO, STATS, RED, 3>(a, cus, s);
+  else launch_d<T, NC, KR, WT, PRO, STATS, RED, 2>(a, cus, s);
 }
 
 inline int grid_x(int64_t m, int nc, int kr, int pro, int cus, int ncols, bool red = false) {
