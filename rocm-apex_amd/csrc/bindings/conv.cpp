@@ -169,8 +169,10 @@ std::vector<at::Tensor> bn1x1(const at::Tensor& a, const at::Tensor& w, bool w_k
 }
 
 // Forward 1x1 conv whose operand is the block below's output computed on load:
-// out = relu(pcoef[0] a + pcoef[1] res + pcoef[2]) (a = that block's output-BN input y3, res = its
-// shortcut: the identity input, or the downsample BN's input with the two BNs folded into pcoef).
+// out = relu(fma(a, pcoef[0], pcoef[2]) + fma(res, pcoef[1], pcoef[3])) (a = that block's output-BN
+// input y3, res = its shortcut: the identity input with pcoef[1] = 1, pcoef[3] = 0, or the
+// downsample BN's input with that BN's scale / shift) — the same arithmetic as the standalone
+// apply / dual-apply passes, so the deferred output is bitwise the one they would write.
 // Returns (y = out . W^T, statistics partials about shift, out [M, K], ReLU bits [M K / 8]).
 std::vector<at::Tensor> bn1x1_addrelu(const at::Tensor& a, const at::Tensor& res, const at::Tensor& pcoef,
                                       const at::Tensor& w, const c10::optional<at::Tensor>& shift,
@@ -184,8 +186,8 @@ std::vector<at::Tensor> bn1x1_addrelu(const at::Tensor& a, const at::Tensor& res
   const int64_t m = a.size(0);
   const int k = (int)a.size(1), ncols = (int)w.size(0);
   TORCH_CHECK(conv1x1_bn_supported(m, k, ncols) && (m * k) % 8 == 0, "bn1x1_addrelu: unsupported shape");
-  TORCH_CHECK(pcoef.is_cuda() && pcoef.scalar_type() == at::kFloat && pcoef.is_contiguous() && pcoef.numel() == 3 * (int64_t)k,
-              "bn1x1_addrelu: pcoef must be contiguous fp32 [3K]");
+  TORCH_CHECK(pcoef.is_cuda() && pcoef.scalar_type() == at::kFloat && pcoef.is_contiguous() && pcoef.numel() == 4 * (int64_t)k,
+              "bn1x1_addrelu: pcoef must be contiguous fp32 [4K]");
   if (shift.has_value())
     TORCH_CHECK(shift->is_cuda() && shift->scalar_type() == at::kFloat && shift->is_contiguous() && shift->numel() == ncols,
                 "bn1x1_addrelu: shift must be contiguous fp32 [ncols]");

@@ -62,11 +62,14 @@ constexpr int kProNone = 0;
 constexpr int kProBnRelu = 1;  // a' = relu(a * c[k] + c[K + k])            (BN apply + ReLU)
 constexpr int kProBnBwd = 2;   // a' = c[k] * a + c[K + k] * y + c[2K + k]  (BN backward dx from the
                                //       masked gradient a and the BN input y: bwd_apply fused)
-constexpr int kProBnAddRelu = 3;  // a' = relu(c[k] * a + c[K + k] * y + c[2K + k]): the block below's
-                                  //   output BN + residual (y) + ReLU, so its apply pass is gone; a'
+constexpr int kProBnAddRelu = 3;  // a' = relu(fma(a, c[k], c[2K + k]) + fma(y, c[K + k], c[3K + k])): the
+                                  //   block below's output BN + residual / downsample BN (y) + ReLU with
+                                  //   the apply passes' exact arithmetic, so its apply pass is gone; a'
                                   //   and its ReLU bits are written out for the block's other uses
 // per-k coefficient rows of a prologue
-constexpr int pro_rows(int pro) { return pro == kProBnRelu ? 2 : (pro == kProBnBwd || pro == kProBnAddRelu) ? 3 : 0; }
+constexpr int pro_rows(int pro) {
+  return pro == kProBnRelu ? 2 : pro == kProBnBwd ? 3 : pro == kProBnAddRelu ? 4 : 0;
+}
 constexpr bool pro_two(int pro) { return pro == kProBnBwd || pro == kProBnAddRelu; }  // a second operand
 
 constexpr int kSS = 64 + 8;  // staging row stride (elements): rows h and h+4 land 16 banks apart
@@ -164,9 +167,10 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
       s16x8 a = f.a[s];
       if constexpr (pro_two(PRO)) {
         const int kb = ch * KCH + 16 * s + 8 * lh;
-        float c[3][8];
+        constexpr int NQ = pro_rows(PRO);
+        float c[NQ][8];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
+        for (int q = 0; q < NQ; ++q) {
           const float4 u0 = *reinterpret_cast<const float4*>(pc + q * KR + kb);
           const float4 u1 = *reinterpret_cast<const float4*>(pc + q * KR + kb + 4);
           c[q][0] = u0.x; c[q][1] = u0.y; c[q][2] = u0.z; c[q][3] = u0.w;
@@ -175,10 +179,13 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
         unsigned mb = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          float v = fmaf(c[0][j], to_f(T{(uint16_t)a[j]}), fmaf(c[1][j], to_f(T{(uint16_t)f.y[s][j]}), c[2][j]));
+          float v;
           if constexpr (PRO == kProBnAddRelu) {
+            v = fmaf(to_f(T{(uint16_t)a[j]}), c[0][j], c[2][j]) + fmaf(to_f(T{(uint16_t)f.y[s][j]}), c[1][j], c[3][j]);
             v = fmaxf(v, 0.f);
             mb |= (v > 0.f ? 1u : 0u) << j;
+          } else {
+            v = fmaf(c[0][j], to_f(T{(uint16_t)a[j]}), fmaf(c[1][j], to_f(T{(uint16_t)f.y[s][j]}), c[2][j]));
           }
           a[j] = (short)from_f<T>(v).x;
         }

@@ -1167,13 +1167,26 @@ void conv_force_fprop_cfg(int cfg) { g_forced_cfg = cfg; }
 
 static int fprop_cfg(const ConvTapArgs& a, int cus) { return plan::conv_fprop_cfg(a, cus, g_forced_cfg); }
 
+// the spatial-tile 64-channel kernel (conv3x3_sp.hip): forced as configuration 21, else taken
+// wherever it applies unless another configuration is forced
+constexpr int kSpCfg = 21;
+static bool use_sp(const ConvTapArgs& a) {
+  if (g_forced_cfg == kSpCfg) return conv_sp_supported(a);
+  return g_forced_cfg < 0 && conv_sp_default(a);
+}
+
 int conv_tap_stats_tiles(const ConvTapArgs& a, int cus) {
+  if (use_sp(a)) return conv_sp_grid(a, cus);
   const int bm = plan::conv_fprop_bm(fprop_cfg(a, cus));
   return (int)(((int64_t)a.n * a.oh * a.ow + bm - 1) / bm);
 }
 
 void conv_tap_fprop(const ConvTapArgs& a, int cus, hipStream_t s) {
   if (!conv_tap_supported(a)) throw std::runtime_error("conv_tap_fprop: unsupported shape / dtype / alignment");
+  if (use_sp(a)) {
+    conv_sp_fprop(a, cus, s);
+    return;
+  }
   const conv::Geo g = conv::make_geo(a);
   const int cfg = fprop_cfg(a, cus);
   dispatch_16(a.dtype, [&](auto tag) {

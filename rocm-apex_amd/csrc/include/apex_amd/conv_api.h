@@ -58,6 +58,13 @@ void conv_force_fprop_cfg(int cfg);
 void conv_tap_fprop(const ConvTapArgs& a, int cus, hipStream_t s);
 // number of M tiles of a tap fprop launch (the stats partial rows)
 int conv_tap_stats_tiles(const ConvTapArgs& a, int cus);
+// spatial-tile 3x3 kernel (csrc/conv/conv3x3_sp.hip): 64 -> 64 channels, stride 1, identity
+// placement, no fused epilogue but the BN statistics; conv_tap_fprop routes supported launches to
+// it by default (APEX_AMD_CONV_SP=0 disables; forced tile configuration 21 selects it)
+bool conv_sp_supported(const ConvTapArgs& a);
+bool conv_sp_default(const ConvTapArgs& a);
+int conv_sp_grid(const ConvTapArgs& a, int cus);
+void conv_sp_fprop(const ConvTapArgs& a, int cus, hipStream_t s);
 
 // weight gradient: dw[k][t][c] = sum_{n,oh,ow} dy[n,oh,ow,k] * x[n, oh*ish + dh[t], ow*isw + dw[t], c]
 // (dy = `out` geometry with osh = osw = 1, oph = opw = 0; x = `in`).  fp32 result [kout][ntaps][c]

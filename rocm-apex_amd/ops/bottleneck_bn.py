@@ -312,8 +312,9 @@ class _BottleneckFn(torch.autograd.Function):
             # the block above computes this output in its conv1 (BlockLink docstring)
             res = x2 if wds is None else yd
             sc, sh = c3[:cout], c3[cout:]
-            pc3 = (torch.cat([sc, torch.ones_like(sc), sh]) if wds is None
-                   else torch.cat([sc, cd[:cout], sh + cd[cout:]]))
+            # [a scale | res scale | a shift | res shift]: the apply passes' arithmetic exactly
+            pc3 = (torch.cat([sc, torch.ones_like(sc), sh, torch.zeros_like(sh)]) if wds is None
+                   else torch.cat([sc, cd[:cout], sh, cd[cout:]]))
             out2, bits = torch.empty_like(y3), None
             link_out.pend = (y3, res, pc3, out2, c3, cd)
         elif wds is None:

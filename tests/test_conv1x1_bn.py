@@ -237,3 +237,39 @@ def test_gpu_wgrad3x3_gather(cin, cout, stride, h, batch, pro):
     dw = ext.wgrad3x3(gy.permute(0, 2, 3, 1), x.permute(0, 2, 3, 1), stride, xcoef, torch.float32)
     assert dw.shape == ref.shape
     _close(dw, ref, 2e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,k,ncols", [(777, 256, 64), (1000, 512, 128), (300, 256, 128), (64, 64, 64)])
+@pytest.mark.parametrize("dual", [False, True])
+def test_gpu_bn1x1_addrelu_matches_apply_pass(m, k, ncols, dual):
+    """The deferred block output (conv1x1_bn kProBnAddRelu: the block below's output BN + shortcut
+    + ReLU computed on the conv's operand load, written out with its ReLU bits) is BITWISE the
+    output and bit mask of the standalone apply / dual-apply pass it replaces, and the conv output
+    and its statistics match fp32 torch on that operand."""
+    import apex
+    from apex import _native
+
+    bn = _native.require("bn_nhwc").bn_nhwc
+    ext = _ext()
+    torch.manual_seed(m + k)
+    dt = torch.bfloat16
+    y3 = torch.randn(m, k, device="cuda").to(dt)
+    res = torch.randn(m, k, device="cuda").to(dt)
+    c3 = torch.cat([torch.rand(k, device="cuda") + 0.5, torch.randn(k, device="cuda") * 0.3])
+    cd = torch.cat([torch.rand(k, device="cuda") + 0.5, torch.randn(k, device="cuda") * 0.3])
+    w = (torch.randn(ncols, k, device="cuda") * 0.05).to(dt)
+    shift = torch.randn(ncols, device="cuda") * 0.1
+    if dual:
+        want, want_bits = bn.apply(y3, res, c3, True, True, cd)
+        pc = torch.cat([c3[:k], cd[:k], c3[k:], cd[k:]])
+    else:
+        want, want_bits = bn.apply(y3, res, c3, True, True)
+        pc = torch.cat([c3[:k], torch.ones(k, device="cuda"), c3[k:], torch.zeros(k, device="cuda")])
+    y, part, out, bits = ext.bn1x1_addrelu(y3, res, pc, w, shift)
+    assert torch.equal(out, want.view_as(out))
+    assert torch.equal(bits.view(-1), want_bits.view(-1))
+    ref = out.float() @ w.float().t()
+    _close(y, ref, 1e-2)
+    d = y.float() - shift
+    torch.testing.assert_close(part[0].sum(0), d.sum(0), atol=0.05 + 1e-3 * float(d.abs().sum(0).max()), rtol=1e-3)

@@ -99,20 +99,23 @@ CFG_SHAPES = [
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", list(range(21)))
+@pytest.mark.parametrize("cfg", list(range(22)))
 @pytest.mark.parametrize("cin,cout,stride,h,batch", CFG_SHAPES)
 def test_gpu_conv_tap_every_tile_config(cfg, cin, cout, stride, h, batch):
     """Every fprop tile configuration (0-6 fprop_kernel, 7-13 fprop2_kernel: buffer-load staging
-    with out-of-range zero fill) forced on ragged shapes: forward + BN statistics epilogue, the
-    stride-1 / per-phase stride-2 data gradient (phase-shifted output placement), and the fused
-    scale / bias / residual / ReLU epilogue, against fp32 torch."""
+    with out-of-range zero fill, 14-20 fprop3, 21 the spatial-tile 64-channel kernel) forced on
+    ragged shapes: forward + BN statistics epilogue, the stride-1 / per-phase stride-2 data
+    gradient (phase-shifted output placement), and the fused scale / bias / residual / ReLU
+    epilogue, against fp32 torch."""
     from apex import _native
     from apex.ops import conv as C
 
     ext = _native.require("conv").conv
-    bn = [128, 64, 128, 64, 128, 64, 256, 64, 64, 128, 128, 128, 256, 256, 64, 64, 128, 128, 128, 256, 64][cfg]
+    bn = [128, 64, 128, 64, 128, 64, 256, 64, 64, 128, 128, 128, 256, 256, 64, 64, 128, 128, 128, 256, 64, 64][cfg]
     if cout % bn:
         pytest.skip("tile wider than the output")
+    if cfg == 21 and not (cin == 64 and cout == 64 and stride == 1):
+        pytest.skip("the spatial-tile kernel is 64 -> 64 channels, stride 1")
     torch.manual_seed(cfg * 7 + cin)
     x = (torch.randn(batch, cin, h, h, device="cuda") + 0.2).to(torch.bfloat16).to(memory_format=torch.channels_last)
     w = (torch.randn(cout, cin, 3, 3, device="cuda") * 0.05).to(torch.bfloat16).to(memory_format=torch.channels_last)
@@ -169,3 +172,50 @@ def test_gpu_conv_wgrad_every_variant(variant, cin, cout, stride, h, batch):
         C._conv_ext().force_wgrad_variant(-1)
     _close(dw, wr.grad, 5e-3)
     _close(dwb, wr.grad, 2e-2)
+
+
+SP_SHAPES = [
+    # n, h, w: ragged in both tile dimensions (8 rows x 32 columns), one tile, the ResNet shape
+    (2, 56, 56),
+    (3, 9, 33),
+    (1, 8, 32),
+    (2, 17, 70),
+    (5, 3, 5),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,w", SP_SHAPES)
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_gpu_conv_spatial_tile_kernel(n, h, w, dtype):
+    """The spatial-tile 3x3 kernel (csrc/conv/conv3x3_sp.hip, the default for 64 -> 64 channels
+    stride 1): forward with and without the BN statistics epilogue and the flipped-weight data
+    gradient, against fp32 torch, on shapes ragged in both tile dimensions; the statistics rows
+    are one per persistent workgroup."""
+    from apex import _native
+    from apex.ops import conv as C
+
+    ext = _native.require("conv").conv
+    torch.manual_seed(h * 131 + w)
+    x = (torch.randn(n, 64, h, w, device="cuda") + 0.1).to(dtype).contiguous(memory_format=torch.channels_last)
+    wt = (torch.randn(64, 64, 3, 3, device="cuda") * 0.05).to(dtype).contiguous(memory_format=torch.channels_last)
+    shift = torch.randn(64, device="cuda") * 0.1
+    C._conv_ext().force_fprop_cfg(21)
+    try:
+        y = C.conv_tap_forward(x, wt, 1, 1)
+        yr = F.conv2d(x.float(), wt.float(), None, 1, 1)
+        assert y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
+        _close(y, yr, 1e-2)
+        y2, part = C.conv_tap_forward(x, wt, 1, 1, stats_shift=shift)
+        assert torch.equal(y2, y)
+        yf = y.float().permute(0, 2, 3, 1).reshape(-1, 64)
+        sm, si, _ = ext.bn_finalize(part, float(yf.size(0)), shift, None, None, None, None, 1e-5, 0.1)
+        torch.testing.assert_close(sm, yf.mean(0), atol=1e-4 * max(1.0, float(yf.std())), rtol=1e-4)
+        torch.testing.assert_close(si, torch.rsqrt(yf.var(0, unbiased=False) + 1e-5), atol=0, rtol=1e-3)
+        gy = torch.randn_like(yr).to(dtype).contiguous(memory_format=torch.channels_last)
+        xr = x.float().requires_grad_(True)
+        torch.autograd.backward(F.conv2d(xr, wt.float(), None, 1, 1), gy.float())
+        dx = C.conv_tap_dgrad(gy, wt, x.shape, 1, 1)
+        _close(dx, xr.grad, 2e-2)
+    finally:
+        C._conv_ext().force_fprop_cfg(-1)
