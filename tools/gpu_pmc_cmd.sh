@@ -17,6 +17,6 @@ timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python3 $S "$@" > $O/fetch.log 2>&1 || stop fetch $?
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python3 $S "$@" > $O/write.log 2>&1 || stop write $?
 cd $R
-python tools/pmc_summary.py $O --by-grid --md $O/pmc.md > /dev/null
+python tools/pmc_summary.py $O --by-grid --filter "${PMC_FILTER:-apex_amd::}" --md $O/pmc.md > /dev/null
 rm -rf $O/trace $O/sq $O/sq2 $O/fetch $O/write
 echo PMC_DONE
