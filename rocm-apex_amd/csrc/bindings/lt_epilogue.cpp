@@ -126,6 +126,12 @@ std::mutex g_plan_mu;
 // the fastest — the single-answer heuristic picked a 32 x 32-tile BGRADB kernel ~10x slower than
 // the plain GEMM at the GPT-2 shapes
 constexpr int kTop = 8;
+// Timing the top answers is limited to problems with every dimension <= 16384 (the transformer
+// dense shapes it was validated on): at 32768 tokens (and at m = 200704) one of the extra
+// candidates makes hipBLASLt fail to initialise its kernel ("Could not initialize Tensile host")
+// and then fault inside the library (tools/gpu_r04ab.sh), while the heuristic's first answer
+// runs fine — larger problems take that first answer, as torch.matmul does.
+constexpr int64_t kTuneMaxDim = 16384;
 bool tune_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("APEX_AMD_LT_TUNE");
@@ -160,9 +166,10 @@ bool lt_run(const Problem& p, const void* a, const void* b, void* d, const void*
              "workspace pref");
     hipblasLtMatmulHeuristicResult_t res[kTop];
     int found = 0;
+    const bool tune = tune_enabled() && p.m <= kTuneMaxDim && p.n <= kTuneMaxDim && p.k <= kTuneMaxDim;
     const hipblasStatus_t st =
         hipblasLtMatmulAlgoGetHeuristic(h, plan->ds.op, plan->ds.a, plan->ds.b, plan->ds.d, plan->ds.d, pref,
-                                        tune_enabled() ? kTop : 1, res, &found);
+                                        tune ? kTop : 1, res, &found);
     hipblasLtMatmulPreferenceDestroy(pref);
     int valid[kTop], nv = 0;
     if (st == HIPBLAS_STATUS_SUCCESS)

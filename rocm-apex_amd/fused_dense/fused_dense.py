@@ -162,11 +162,15 @@ def wgrad_gemm(g2, x2):
     """dW[N, K] = g2[M, N]^T x2[M, K] for the dense layers: the native split-K kernel for small
     outputs (``native_wgrad_ok``), else hipBLASLt through the wrapper's per-shape top-8 timing
     (``lt_gemm.mm``: 149 vs 176 us for torch.matmul's first-heuristic kernel at the GPT-2 QKV
-    shape 16384 x 3072 x 1024, ties elsewhere; profiles/gemm_routes_r04t.jsonl), else torch."""
+    shape 16384 x 3072 x 1024, ties elsewhere; profiles/gemm_routes_r04t.jsonl) up to 16384 tokens,
+    else torch.matmul."""
     if native_wgrad_ok(g2, x2):
         return _g().linear_wgrad(g2, x2)
     lt = _lt(g2, x2)
-    if lt is not None and hasattr(lt, "mm") and g2.dim() == 2 and x2.dim() == 2:
+    # only where the timed plans were validated (<= 16384 tokens, every dim <= 16384): at 65536
+    # tokens hipBLASLt's own first answer for this layout faults (tools/gpu_r04ab.sh probes)
+    if (lt is not None and hasattr(lt, "mm") and g2.dim() == 2 and x2.dim() == 2
+            and max(g2.size(0), g2.size(1), x2.size(1)) <= 16384):
         r = lt.mm(g2.contiguous(), x2.contiguous(), True, False)
         if r:
             return r[0]
