@@ -12,6 +12,8 @@ the sequence; the all-reduces become reduce-scatter / all-gather pairs of the sa
 and the GEMM + bias epilogue goes through :mod:`apex.fused_dense` (gfx950 MFMA kernel) when it
 supports the dtype, else ``torch.matmul`` (hipBLASLt).
 """
+import os
+
 import torch
 import torch.nn.functional as F
 from torch.nn import init
@@ -87,13 +89,21 @@ def _initialize_affine_weight_cpu(weight, output_size, input_size, per_partition
 
 
 def _linear(x, weight, bias):
-    """y = x W^T + b through the fused GEMM+bias kernel when available."""
+    """y = x W^T + b on fused_dense's route: the hipBLASLt bias-epilogue GEMM with per-shape timed
+    plans by default (APEX_AMD_DENSE_ROUTE=lt: 87-97 vs 124 us for the native kernel at the GPT-2
+    QKV shape 16384 x 3072 x 1024, 31 vs 41 us at 1024 x 1024; profiles/gemm_routes_r04t.jsonl),
+    the native GEMM + bias kernel with APEX_AMD_DENSE_ROUTE=native, torch elsewhere."""
     try:
-        from ...fused_dense.fused_dense import fused_linear_available, linear_bias_forward
+        from ...fused_dense import fused_dense as fd
     except Exception:  # pragma: no cover - module not importable
-        fused_linear_available = None
-    if fused_linear_available is not None and fused_linear_available(x, weight, bias):
-        return linear_bias_forward(x, weight, bias)
+        fd = None
+    route = os.environ.get("APEX_AMD_TP_LINEAR", "")  # lt | torch | native (A/B override)
+    if fd is not None and fd.fused_linear_available(x, weight, bias) and route != "torch":
+        if route == "native" or (not route and fd.route_mode() == "native"):
+            return fd.linear_bias_forward(x, weight, bias)
+        return fd._lib_dense_fwd(x, weight, bias)
+    if bias is not None and x.dim() >= 2:
+        return torch.addmm(bias, x.reshape(-1, x.shape[-1]), weight.t()).view(x.shape[:-1] + (weight.shape[0],))
     out = torch.matmul(x, weight.t())
     return out + bias if bias is not None else out
 
