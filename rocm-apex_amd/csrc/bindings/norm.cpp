@@ -73,7 +73,8 @@ std::vector<at::Tensor> fwd_impl(const at::Tensor& input, at::IntArrayRef shape,
 
 std::vector<at::Tensor> bwd_impl(const at::Tensor& dout, const c10::optional<at::Tensor>& mean, const at::Tensor& invvar,
                                  const at::Tensor& input, at::IntArrayRef shape, const c10::optional<at::Tensor>& gamma,
-                                 bool has_beta, double /*eps*/, bool rms) {
+                                 bool has_beta, double /*eps*/, bool rms,
+                                 const c10::optional<at::Tensor>& dres = c10::nullopt) {
   TORCH_CHECK(input.is_cuda(), "layer_norm: input must be a GPU tensor");
   const c10::hip::HIPGuard g(input.get_device());
   at::Tensor x = input.contiguous();
@@ -113,6 +114,13 @@ std::vector<at::Tensor> bwd_impl(const at::Tensor& dout, const c10::optional<at:
   a.w_t = dtype_code(wt);
   a.out_t = dtype_code(dy.scalar_type());
   a.rms = rms;
+  at::Tensor dr;
+  if (dres.has_value() && dres->defined()) {
+    dr = dres->contiguous();
+    TORCH_CHECK(dr.is_cuda() && dr.numel() == x.numel() && dr.scalar_type() == dy.scalar_type(),
+                "layer_norm backward: residual gradient must match the output gradient");
+    a.dres = dr.data_ptr();
+  }
   TORCH_CHECK(a.out_t == a.in_t || a.out_t == a.w_t, "layer_norm backward: grad dtype must be input or weight dtype");
   norm_bwd(a, cus, cur_stream());
   return {dx, dgamma, dbeta};
@@ -136,9 +144,12 @@ void bind_norm(pybind11::module_& root) {
   });
   m.def("backward_affine",
         [](at::Tensor dout, at::Tensor mean, at::Tensor invvar, at::Tensor x, std::vector<int64_t> shape,
-           at::Tensor gamma, c10::optional<at::Tensor> beta, double eps) {
-          return bwd_impl(dout, mean, invvar, x, shape, gamma, beta.has_value() && beta->defined(), eps, false);
-        });
+           at::Tensor gamma, c10::optional<at::Tensor> beta, double eps, c10::optional<at::Tensor> dres) {
+          return bwd_impl(dout, mean, invvar, x, shape, gamma, beta.has_value() && beta->defined(), eps, false, dres);
+        },
+        pybind11::arg("dout"), pybind11::arg("mean"), pybind11::arg("invvar"), pybind11::arg("input"),
+        pybind11::arg("normalized_shape"), pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("epsilon"),
+        pybind11::arg("dres") = c10::nullopt);
   m.def("backward", [](at::Tensor dout, at::Tensor mean, at::Tensor invvar, at::Tensor x, std::vector<int64_t> shape,
                        double eps) {
     return bwd_impl(dout, mean, invvar, x, shape, c10::nullopt, false, eps, false)[0];

@@ -37,6 +37,10 @@ struct NormBwdArgs {
   int n2;
   int in_t, w_t, out_t;
   bool rms;
+  // nullable [n1, n2] (out_t): a gradient added to dx in the same pass — the residual branch's
+  // gradient of a pre-LN transformer block (x feeds both the norm and the residual add), so the
+  // autograd sum of the two is not a separate elementwise kernel
+  const void* dres = nullptr;
 };
 
 // fp32 scratch needed by norm_bwd for (n1, n2) on a device with `cus` compute units.

@@ -24,7 +24,7 @@ __global__ void __launch_bounds__(block_threads<W>())
 ln_bwd_kernel(const TO* __restrict__ dy, const TI* __restrict__ x, const float* __restrict__ mean,
               const float* __restrict__ invvar, const TW* __restrict__ gamma, TI* __restrict__ dx,
               float* __restrict__ part_g, float* __restrict__ part_b, int64_t n1, int n2, bool rms,
-              bool want_dgamma, bool want_dbeta) {
+              bool want_dgamma, bool want_dbeta, const TO* __restrict__ dres) {
   constexpr int NT = block_threads<W>();
   constexpr int RPB = NT / 64 / W;
   __shared__ float red[2 * RPB * W];
@@ -60,6 +60,7 @@ ln_bwd_kernel(const TO* __restrict__ dy, const TI* __restrict__ x, const float* 
   // current one is reduced and written, so every lane keeps two rows' bytes in flight
   Raw8<TI> px[VPT];
   Raw8<TO> pd[VPT];
+  Raw8<TO> pr[VPT];  // dres (a residual branch's gradient summed into dx), when given
   float pmu = 0.f, piv = 0.f;
   auto prefetch = [&](int64_t grp) {
     const int64_t row = grp * RPB + row_in_block;
@@ -73,9 +74,11 @@ ln_bwd_kernel(const TO* __restrict__ dy, const TI* __restrict__ x, const float* 
       if (ok && v < nv) {
         px[j].load(x + rr * n2 + v * 8);
         pd[j].load(dy + rr * n2 + v * 8);
+        if (dres != nullptr) pr[j].load(dres + rr * n2 + v * 8);
       } else {
         px[j].zero();
         pd[j].zero();
+        pr[j].zero();
       }
     }
   };
@@ -85,11 +88,12 @@ ln_bwd_kernel(const TO* __restrict__ dy, const TI* __restrict__ x, const float* 
     const bool valid = row < n1;
     const int64_t rr = valid ? row : 0;
     const float mu = pmu, iv = piv;
-    float xh[VPT][8], d[VPT][8];
+    float xh[VPT][8], d[VPT][8], rsd[VPT][8];
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
       px[j].unpack(xh[j]);
       pd[j].unpack(d[j]);
+      if (dres != nullptr) pr[j].unpack(rsd[j]);
     }
     prefetch(grp + gridDim.x);
     float s1 = 0.f, s2 = 0.f;
@@ -119,6 +123,10 @@ ln_bwd_kernel(const TO* __restrict__ dy, const TI* __restrict__ x, const float* 
           float o[8];
 #pragma unroll
           for (int k = 0; k < 8; ++k) o[k] = iv * (d[j][k] * g[j][k] - m1 - xh[j][k] * m2);
+          if (dres != nullptr) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) o[k] += rsd[j][k];
+          }
           Vec8<TI>::store(dx + rr * n2 + v * 8, o);
         }
       }
@@ -176,7 +184,7 @@ template <typename TI, typename TW, typename TO>
 __global__ void __launch_bounds__(256)
 ln_bwd_dx_generic_kernel(const TO* __restrict__ dy, const TI* __restrict__ x, const float* __restrict__ mean,
                          const float* __restrict__ invvar, const TW* __restrict__ gamma, TI* __restrict__ dx,
-                         int64_t n1, int n2, bool rms) {
+                         int64_t n1, int n2, bool rms, const TO* __restrict__ dres) {
   __shared__ float red[8];
   const int64_t row = blockIdx.x;
   const float mu = rms ? 0.f : mean[row];
@@ -195,7 +203,7 @@ ln_bwd_dx_generic_kernel(const TO* __restrict__ dy, const TI* __restrict__ x, co
   for (int i = threadIdx.x; i < n2; i += 256) {
     const float gd = to_f(dr[i]) * (gamma ? to_f(gamma[i]) : 1.f);
     const float xh = (to_f(xr[i]) - mu) * iv;
-    dx[row * n2 + i] = from_f<TI>(iv * (gd - m1 - xh * m2));
+    dx[row * n2 + i] = from_f<TI>(iv * (gd - m1 - xh * m2) + (dres ? to_f(dres[row * n2 + i]) : 0.f));
   }
 }
 
@@ -230,7 +238,7 @@ static int launch_bwd(const NormBwdArgs& a, int cus, hipStream_t s) {
   float* pb = a.workspace + (int64_t)grid * a.n2;
   hipLaunchKernelGGL((ln_bwd_kernel<TI, TW, TO, W, VPT>), dim3(grid), dim3(NT), lds, s, (const TO*)a.dy,
                      (const TI*)a.x, a.mean, a.invvar, (const TW*)a.gamma, (TI*)a.dx, pg, pb, a.n1, a.n2, a.rms,
-                     wg, wb);
+                     wg, wb, (const TO*)a.dres);
   return grid;
 }
 
@@ -247,7 +255,7 @@ static int generic_parts(int64_t n1, int n2, int cus) {
 void norm_bwd_impl(const NormBwdArgs& a, int cus, hipStream_t s) {
   if (a.n1 <= 0 || a.n2 <= 0) return;
   const Cfg c = pick_cfg(a.n2);
-  const bool fast = c.W > 0 && (a.n2 % 8 == 0) && aligned16(a.x) && aligned16(a.dy) && aligned16(a.dx) &&
+  const bool fast = c.W > 0 && (a.n2 % 8 == 0) && aligned16(a.x) && aligned16(a.dy) && aligned16(a.dx) && aligned16(a.dres) &&
                     aligned16(a.gamma);
   const bool want = a.dgamma != nullptr || a.dbeta != nullptr;
   dispatch_norm_types(a.in_t, a.w_t, a.out_t, [&](auto ti, auto tw, auto to) {
@@ -265,7 +273,7 @@ void norm_bwd_impl(const NormBwdArgs& a, int cus, hipStream_t s) {
     } else {
       hipLaunchKernelGGL((ln_bwd_dx_generic_kernel<TI, TW, TO>), dim3((unsigned)a.n1), dim3(256), 0, s,
                          (const TO*)a.dy, (const TI*)a.x, a.mean, a.invvar, (const TW*)a.gamma, (TI*)a.dx, a.n1,
-                         a.n2, a.rms);
+                         a.n2, a.rms, (const TO*)a.dres);
       if (want) {
         nparts = generic_parts(a.n1, a.n2, cus);
         hipLaunchKernelGGL((ln_bwd_gb_generic_kernel<TI, TO>), dim3((a.n2 + 255) / 256, nparts), dim3(256), 0, s,

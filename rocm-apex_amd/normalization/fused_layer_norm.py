@@ -40,6 +40,41 @@ class FusedLayerNormAffineFunction(torch.autograd.Function):
         return dx, dw, db, None, None, None
 
 
+class FusedLayerNormResidualFunction(torch.autograd.Function):
+    """(LN(x), x) as ONE autograd node for a pre-LN residual block, where x feeds both the norm and
+    the residual add: backward gets both gradients and the LayerNorm backward kernel returns
+    dx = LN'(dy) + d(residual) in the same pass — the autograd sum of the two branches is not a
+    separate elementwise kernel (two per transformer layer)."""
+
+    @staticmethod
+    def forward(ctx, input, weight, bias, normalized_shape, eps):
+        ctx.normalized_shape = _shape(normalized_shape)
+        ctx.eps = eps
+        x = input.contiguous()
+        w = weight.contiguous()
+        b = bias.contiguous() if bias is not None else None
+        y, mean, invvar = lnops.ln_fwd(x, ctx.normalized_shape, w, b, eps)
+        ctx.save_for_backward(x, w, b, mean, invvar)
+        return y, input.view_as(input)
+
+    @staticmethod
+    def backward(ctx, grad_output, grad_residual):
+        x, w, b, mean, invvar = ctx.saved_tensors
+        dres = grad_residual.contiguous() if grad_residual is not None else None
+        dx, dw, db = lnops.ln_bwd(grad_output.contiguous(), x, mean, invvar, ctx.normalized_shape, w, b, ctx.eps,
+                                  dres=dres)
+        return dx, dw, db, None, None
+
+
+def layer_norm_with_residual(ln, input):
+    """``(ln(input), input)`` with the two branches' gradients summed inside the LayerNorm backward
+    when ``ln`` is an affine FusedLayerNorm (else the plain pair: autograd adds them)."""
+    if (isinstance(ln, FusedLayerNorm) and ln.elementwise_affine and input.is_cuda
+            and not torch.is_autocast_enabled("cuda") and input.dtype == ln.weight.dtype):
+        return FusedLayerNormResidualFunction.apply(input, ln.weight, ln.bias, ln.normalized_shape, ln.eps)
+    return ln(input), input
+
+
 class FusedLayerNormAffineMixedDtypesFunction(FusedLayerNormAffineFunction):
     @staticmethod
     def forward(ctx, input, weight, bias, normalized_shape, eps):

@@ -51,8 +51,13 @@ def ln_fwd(x, normalized_shape, weight, bias, eps, rms=False, out_dtype=None):
     return y.reshape(x.shape).to(od), mean, invvar
 
 
-def ln_bwd(dy, x, mean, invvar, normalized_shape, weight, bias, eps, rms=False):
-    """Returns (dx, dgamma, dbeta) (dgamma/dbeta None when weight is None)."""
+def ln_bwd(dy, x, mean, invvar, normalized_shape, weight, bias, eps, rms=False, dres=None):
+    """Returns (dx, dgamma, dbeta) (dgamma/dbeta None when weight is None).  ``dres``: a gradient
+    added to dx (the residual branch's, summed inside the affine LayerNorm kernel on the GPU)."""
+    if dres is not None and not (_native.use_native(x) and not rms and weight is not None
+                                 and dres.dtype == dy.dtype):
+        dx, dgamma, dbeta = ln_bwd(dy, x, mean, invvar, normalized_shape, weight, bias, eps, rms)
+        return dx + dres.to(dx.dtype).reshape(dx.shape), dgamma, dbeta
     if _native.use_native(x):
         m = _norm()
         if rms:
@@ -61,7 +66,8 @@ def ln_bwd(dy, x, mean, invvar, normalized_shape, weight, bias, eps, rms=False):
                 return dx, dgamma, None
             return m.rms_backward(dy, invvar, x, list(normalized_shape), eps), None, None
         if weight is not None:
-            dx, dgamma, dbeta = m.backward_affine(dy, mean, invvar, x, list(normalized_shape), weight, bias, eps)
+            dx, dgamma, dbeta = m.backward_affine(dy, mean, invvar, x, list(normalized_shape), weight, bias, eps,
+                                                  dres=dres)
             return dx, dgamma, (dbeta if bias is not None else None)
         return m.backward(dy, mean, invvar, x, list(normalized_shape), eps), None, None
     n1, n2 = compute_n1_n2(x, normalized_shape)

@@ -17,6 +17,7 @@ import torch
 import torch.nn.functional as F
 
 from ...normalization import FusedLayerNorm as LayerNorm
+from ...normalization.fused_layer_norm import layer_norm_with_residual
 from ...ops.attention import flash_attn_func, packed_qkv_self_attention
 from ..functional.fused_bias_dropout_add import fused_bias_dropout_add
 from .. import parallel_state, tensor_parallel
@@ -253,19 +254,31 @@ class ParallelTransformerLayer(MegatronModule):
 
     def forward(self, hidden_states, attention_mask, encoder_output=None, enc_dec_attn_mask=None,
                 inference_params=None):
-        ln_out = self.input_layernorm(hidden_states)
+        post = self.apply_residual_connection_post_layernorm
+        # pre-LN: the block input feeds the norm AND the residual add; one autograd node for both
+        # sums their gradients inside the LayerNorm backward kernel
+        if post:
+            ln_out, res_in = self.input_layernorm(hidden_states), None
+        else:
+            ln_out, res_in = layer_norm_with_residual(self.input_layernorm, hidden_states)
         attn_out, attn_bias = self.self_attention(ln_out, attention_mask)
-        residual = ln_out if self.apply_residual_connection_post_layernorm else hidden_states
+        residual = ln_out if post else res_in
         bda = get_bias_dropout_add(self.training)
         ln_in = bda(attn_out, attn_bias, residual, self.hidden_dropout)
-        ln_out = self.post_attention_layernorm(ln_in)
+        if post or self.layer_type == LayerType.decoder:
+            ln_out, ln_in_res = self.post_attention_layernorm(ln_in), ln_in
+        else:
+            ln_out, ln_in_res = layer_norm_with_residual(self.post_attention_layernorm, ln_in)
         if self.layer_type == LayerType.decoder:
             attn_out, attn_bias = self.inter_attention(ln_out, enc_dec_attn_mask, encoder_output=encoder_output)
             residual = ln_out if self.apply_residual_connection_post_layernorm else ln_in
             ln_in = bda(attn_out, attn_bias, residual, self.hidden_dropout)
             ln_out = self.post_inter_attention_layernorm(ln_in)
         mlp_out, mlp_bias = self.mlp(ln_out)
-        residual = ln_out if self.apply_residual_connection_post_layernorm else ln_in
+        if self.layer_type == LayerType.decoder:
+            residual = ln_out if post else ln_in
+        else:
+            residual = ln_out if post else ln_in_res
         return bda(mlp_out, mlp_bias, residual, self.hidden_dropout)
 
 

@@ -200,3 +200,48 @@ def test_gpu_fast_layer_norm(hidden, itype, wtype):
     torch.testing.assert_close(m.weight.grad.float() / s, wr.grad / s, atol=tol, rtol=tol)
     s = float(br.grad.abs().max())
     torch.testing.assert_close(m.bias.grad.float() / s, br.grad / s, atol=tol, rtol=tol)
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hidden", [1024, 768, 4096])
+def test_gpu_layer_norm_with_residual_matches_autograd_sum(hidden):
+    """(LN(x), x) as one node (the LayerNorm backward kernel adds the residual branch's gradient
+    into dx) against the plain module + autograd's sum of the two branches."""
+    from apex.normalization import FusedLayerNorm
+    from apex.normalization.fused_layer_norm import layer_norm_with_residual
+
+    torch.manual_seed(hidden)
+    dt = torch.bfloat16
+    ln = FusedLayerNorm(hidden).cuda().to(dt)
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.2, 0.2)
+    x = torch.randn(3, 257, hidden, device="cuda").to(dt)
+    gy = torch.randn_like(x)
+    gr = torch.randn_like(x)
+    xa = x.clone().requires_grad_(True)
+    y, r = layer_norm_with_residual(ln, xa)
+    torch.autograd.backward([y, r * 1.0], [gy, gr])
+    ga, gwa, gba = xa.grad, ln.weight.grad.clone(), ln.bias.grad.clone()
+    ln.weight.grad = ln.bias.grad = None
+    xb = x.clone().requires_grad_(True)
+    yb = ln(xb)
+    torch.autograd.backward([yb, xb * 1.0], [gy, gr])
+    assert torch.equal(y, yb)
+    torch.testing.assert_close(ga.float(), xb.grad.float(), atol=2e-2, rtol=1e-2)
+    torch.testing.assert_close(gwa.float(), ln.weight.grad.float(), atol=0, rtol=0)
+    torch.testing.assert_close(gba.float(), ln.bias.grad.float(), atol=0, rtol=0)
+
+
+def test_layer_norm_with_residual_cpu_fallback():
+    """Off the GPU the pair is the plain module output and the input itself; gradients sum."""
+    from apex.normalization.fused_layer_norm import layer_norm_with_residual
+
+    torch.manual_seed(0)
+    ln = FusedLayerNorm(16)
+    x = torch.randn(4, 16, requires_grad=True)
+    y, r = layer_norm_with_residual(ln, x)
+    assert r is x
+    (y.sum() + (2 * r).sum()).backward()
+    x2 = x.detach().clone().requires_grad_(True)
+    (ln(x2).sum() + (2 * x2).sum()).backward()
+    torch.testing.assert_close(x.grad, x2.grad)

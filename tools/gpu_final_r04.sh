@@ -11,4 +11,10 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 rc=$?; tail -3 $O/smoke.log; [ $rc -ne 0 ] && stop smoke $rc
 timeout -k 10 400 python bench.py > $O/bench.log 2>&1
 rc=$?; tail -1 $O/bench.log | cut -c1-300; [ $rc -ne 0 ] && stop bench $rc
+if [ -n "$TRANSFORMERS" ]; then
+  timeout -k 10 500 python bench.py --model gpt2-medium > $O/gpt2.log 2>&1
+  rc=$?; tail -1 $O/gpt2.log | cut -c1-200; [ $rc -ne 0 ] && stop gpt2 $rc
+  timeout -k 10 500 python bench.py --model bert-large > $O/bert.log 2>&1
+  rc=$?; tail -1 $O/bert.log | cut -c1-200; [ $rc -ne 0 ] && stop bert $rc
+fi
 echo ALL_DONE
