@@ -5,6 +5,7 @@ Autograd functions over :mod:`apex.ops.layer_norm` (gfx950 kernels on GPU).  The
 variant returns the output in the dtype of ``weight`` (e.g. bf16 activations with fp32 gamma in
 Megatron-style models).  Under ``torch.autocast`` the inputs are cast like ``F.layer_norm``."""
 import numbers
+import os
 
 import torch
 from torch.nn import functional as F
@@ -12,6 +13,9 @@ from torch.nn import init
 from torch.nn.parameter import Parameter
 
 from .._autocast_utils import _autocast_disabled, _cast_if_autocast_enabled
+
+# APEX_AMD_LN_RESIDUAL=0: layer_norm_with_residual returns the plain pair (A/B switch)
+_LN_RESIDUAL = os.environ.get("APEX_AMD_LN_RESIDUAL", "1") != "0"
 from ..ops import layer_norm as lnops
 
 
@@ -69,7 +73,7 @@ class FusedLayerNormResidualFunction(torch.autograd.Function):
 def layer_norm_with_residual(ln, input):
     """``(ln(input), input)`` with the two branches' gradients summed inside the LayerNorm backward
     when ``ln`` is an affine FusedLayerNorm (else the plain pair: autograd adds them)."""
-    if (isinstance(ln, FusedLayerNorm) and ln.elementwise_affine and input.is_cuda
+    if (_LN_RESIDUAL and isinstance(ln, FusedLayerNorm) and ln.elementwise_affine and input.is_cuda
             and not torch.is_autocast_enabled("cuda") and input.dtype == ln.weight.dtype):
         return FusedLayerNormResidualFunction.apply(input, ln.weight, ln.bias, ln.normalized_shape, ln.eps)
     return ln(input), input
