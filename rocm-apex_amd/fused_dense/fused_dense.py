@@ -158,6 +158,18 @@ def native_wgrad_ok(g2, x2):
             and x2.is_contiguous())
 
 
+def _native_wide_wgrad(g2, x2):
+    if os.environ.get("APEX_AMD_WIDE_WGRAD", "1") == "0":
+        return False
+    if not (g2.is_cuda and _native.use_native(g2) and _native.submodule("gemm") is not None):
+        return False
+    if g2.dtype not in (torch.float16, torch.bfloat16) or x2.dtype != g2.dtype or g2.dim() != 2 or x2.dim() != 2:
+        return False
+    m, n = g2.shape
+    k = x2.shape[1]
+    return n <= 1024 and k >= 4096 and m >= 8192 and n % 256 == 0 and k % 256 == 0 and m % 64 == 0
+
+
 def wgrad_gemm(g2, x2):
     """dW[N, K] = g2[M, N]^T x2[M, K] for the dense layers: the native split-K kernel for small
     outputs (``native_wgrad_ok``), else hipBLASLt through the wrapper's per-shape top-8 timing
@@ -166,6 +178,12 @@ def wgrad_gemm(g2, x2):
     else torch.matmul."""
     if native_wgrad_ok(g2, x2):
         return _g().linear_wgrad(g2, x2)
+    if _native_wide_wgrad(g2, x2):
+        # short-wide weight (<= 1024 rows, >= 4096 columns, e.g. the MLP's 4h -> h projection):
+        # the native split-K GEMM leads hipBLASLt (153 vs 164 us at 16384 tokens,
+        # profiles/gemm_routes_r04t.jsonl)
+        m, n = g2.shape
+        return _g().matmul(g2, False, x2, False, n, x2.shape[1], m, 0, None, None, False)[0]
     lt = _lt(g2, x2)
     # only where the timed plans were validated (<= 16384 tokens, every dim <= 16384): at 65536
     # tokens hipBLASLt's own first answer for this layout faults (tools/gpu_r04ab.sh probes)
