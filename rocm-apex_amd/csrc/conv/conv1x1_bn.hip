@@ -117,8 +117,13 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
           *reinterpret_cast<const uint4*>(p.w + (int64_t)(col0 + n) * KR + k8);
     }
   } else {
+    // transposed image: consecutive threads take consecutive k, so the 2-byte LDS stores of a
+    // wave land on consecutive addresses (the n-major order put all 64 lanes on two banks:
+    // 32-way conflicts, the 29-55 % conflict cycles of the dgrad forms in
+    // profiles/pmc_resnet_kernels_r04.md); the 16-byte global reads stride by rows instead (a
+    // one-time read of a small, L2-resident weight)
     for (int i = tid; i < NC * KR / 8; i += NT) {
-      const int k = i / (NC / 8), n8 = (i % (NC / 8)) * 8;
+      const int k = i % KR, n8 = (i / KR) * 8;
       const uint4 v = *reinterpret_cast<const uint4*>(p.w + (int64_t)k * p.ncols + col0 + n8);
       const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
