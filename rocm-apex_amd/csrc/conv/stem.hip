@@ -471,6 +471,7 @@ __global__ void __launch_bounds__(512, 1) wgrad_kernel(const BwdArgs a) {
   const int steps = p_begin < p_end ? (int)((p_end - p_begin + WPX - 1) / WPX) : 0;
   for (int i = tid; i < 5 * CO; i += 512) cf[i] = i < 2 * CO ? a.coef[i] : a.cb[i - 2 * CO];
   const int c8 = tid & 7;
+  const int rot = (tid >> 1) & 3;  // = ((tid + 512 * i) >> 1) & 3 for every im2col item i
   const size_t rowstep = (size_t)g.wp * 4;
 
   Gather G[WG_NI];
@@ -498,8 +499,9 @@ __global__ void __launch_bounds__(512, 1) wgrad_kernel(const BwdArgs a) {
       const uint32_t oh = fdiv(rem, a.div_ow), ow = rem - oh * a.div_ow.d;
       const uint4* src = reinterpret_cast<const uint4*>(a.xp + ((size_t)(nn * g.hp + 2 * oh) * g.wp + 2 * ow) * 4 +
                                                          r * rowstep);
+      // im[i][q] holds chunk (q + rot) & 3 of the pair (bank-conflict-free commit, see there)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) im[i][q] = (MODE & 4) ? make_uint4(0, 0, 0, 0) : src[q];
+      for (int q = 0; q < 4; ++q) im[i][q] = (MODE & 4) ? make_uint4(0, 0, 0, 0) : src[(q + rot) & 3];
     }
   };
   auto commit = [&](int st) {
@@ -530,8 +532,12 @@ __global__ void __launch_bounds__(512, 1) wgrad_kernel(const BwdArgs a) {
       const int pr = tid + 512 * i;
       if (pr >= WPX * 7) continue;
       uint4* dst = reinterpret_cast<uint4*>(il + (pr / 7) * ISTR + (pr % 7) * KROW);
+      // ds_write_b128 banks over 8-lane groups on a 128-B window: a pair's 64 B start on the
+      // 64-B half (pr / 7 + pr % 7) & 1 = pr & 1 (ISTR is 576 B), so lanes of one parity would
+      // all hit the same 16-B slot (4-way); rotating the chunk order by (pr >> 1) & 3 gives the 8
+      // lanes of a group 8 distinct slots
 #pragma unroll
-      for (int q = 0; q < 4; ++q) dst[q] = im[i][q];
+      for (int q = 0; q < 4; ++q) dst[(q + rot) & 3] = im[i][q];
     }
   };
 
