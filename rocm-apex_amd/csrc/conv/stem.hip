@@ -129,8 +129,11 @@ __device__ __forceinline__ int chan_of_row(int m) { return 16 * ((m >> 2) & 1) +
 
 template <typename T>
 __global__ void __launch_bounds__(256, 1) fprop_kernel(const FpArgs a) {
-  __shared__ float red[4 * 64 * 33];
+  __shared__ __attribute__((aligned(16))) float red[4 * 64 * 33];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, pl = lane & 31;
+  // per-wave 4 KB output slab (32 pixels x 8 chunks of 16 B, chunk c of pixel x at c ^ (x & 7)) in
+  // the statistics array, which is only used after the tile loop
+  uint4* slab = reinterpret_cast<uint4*>(red) + wave * 256;
   const Geo& g = a.g;
   s16x8 wa[2][NKS];
   const int chm = chan_of_row(pl);
@@ -171,7 +174,7 @@ __global__ void __launch_bounds__(256, 1) fprop_kernel(const FpArgs a) {
       acc[0] = mma<T>(wa[0][ks], b[ks], acc[0]);
       acc[1] = mma<T>(wa[1][ks], b[ks], acc[1]);
     }
-    if (p >= g.m) return;
+    const bool live = p < g.m;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       uint32_t wv[8];
@@ -179,16 +182,30 @@ __global__ void __launch_bounds__(256, 1) fprop_kernel(const FpArgs a) {
       for (int i = 0; i < 8; ++i) {
         const T lo = from_f<T>(acc[t][2 * i]), hi = from_f<T>(acc[t][2 * i + 1]);
         wv[i] = (uint32_t)lo.x | ((uint32_t)hi.x << 16);
-        const float vl = to_f(lo) - sft[t][2 * i], vh = to_f(hi) - sft[t][2 * i + 1];
-        s1[t][2 * i] += vl;
-        s2[t][2 * i] = fmaf(vl, vl, s2[t][2 * i]);
-        s1[t][2 * i + 1] += vh;
-        s2[t][2 * i + 1] = fmaf(vh, vh, s2[t][2 * i + 1]);
+        if (live) {
+          const float vl = to_f(lo) - sft[t][2 * i], vh = to_f(hi) - sft[t][2 * i + 1];
+          s1[t][2 * i] += vl;
+          s2[t][2 * i] = fmaf(vl, vl, s2[t][2 * i]);
+          s1[t][2 * i + 1] += vh;
+          s2[t][2 * i + 1] = fmaf(vh, vh, s2[t][2 * i + 1]);
+        }
       }
-      uint4* dst = reinterpret_cast<uint4*>(a.y + (size_t)p * CO + 32 * t + 16 * h);
-      dst[0] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-      dst[1] = make_uint4(wv[4], wv[5], wv[6], wv[7]);
+      // a lane holds 2 x 16 B of its pixel's 128-B row: through the slab, so that each global
+      // store below writes 8 whole rows (1 KB contiguous) instead of 16 B of 64 rows; the XOR
+      // keeps the 8-lane ds_write_b128 groups (8 pixels, one chunk) on 8 distinct 16-B slots
+      const int c0 = 4 * t + 2 * h, x7 = pl & 7;
+      slab[pl * 8 + (c0 ^ x7)] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+      slab[pl * 8 + ((c0 + 1) ^ x7)] = make_uint4(wv[4], wv[5], wv[6], wv[7]);
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own slab: no workgroup barrier
+    const uint32_t pbase = p - (uint32_t)pl;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int L = lane + 64 * j, x = L >> 3, c = L & 7;
+      const uint4 v = slab[x * 8 + (c ^ (x & 7))];
+      if (pbase + (uint32_t)x < g.m) *reinterpret_cast<uint4*>(a.y + (size_t)(pbase + x) * CO + 8 * c) = v;
+    }
+    asm volatile("" ::: "memory");
   };
 
   // double-buffered: the next tile's 14 loads are in flight under this tile's 28 MFMAs
@@ -207,6 +224,7 @@ __global__ void __launch_bounds__(256, 1) fprop_kernel(const FpArgs a) {
 
   // fold the statistics: per-lane sums -> LDS -> one row per workgroup (fixed order)
   const int ch = threadIdx.x & 63, which = threadIdx.x >> 6;  // which: 0 = s1, 1 = s2 (threads < 128)
+  __syncthreads();  // every wave is done with its output slab
   for (int pass = 0; pass < 2; ++pass) {
     float* row = red + (wave * 64 + lane) * 33;
 #pragma unroll
