@@ -417,28 +417,57 @@ __global__ void __launch_bounds__(256) bwd_reduce_kernel(const BwdArgs a) {
   Vec8<float>::load(mu, a.mean + c8 * 8);
 #pragma unroll
   for (int e = 0; e < 8; ++e) a1[e] = a2[e] = 0.f;
-  const uint32_t total = a.g.m * 8u, stride = gridDim.x * 256u;
-  // two items per trip, every load of both issued before either is consumed
-  for (uint32_t i0 = blockIdx.x * 256u + tid; i0 < total; i0 += 2 * stride) {
-    Gather G[2];
-    uint4 yv[2];
-    bool live[2];
+  // one item = a 2 x 2 quad of conv-output pixels (rows 2 qh, 2 qh + 1; columns 2 qw, 2 qw + 1) x 8
+  // channels: every pool window containing one of them is among (qh | qh + 1) x (qw | qw + 1), so
+  // the quad loads those 4 windows once instead of 4 per pixel.  A pixel at padded row
+  // hh = 2 qh + 1 + dy sits at window row hh - 2 ph = 1 + dy - 2 sh of slot row sh (in the window only
+  // for sh = 0 or dy = 1); columns alike.  Per pixel the matching windows are summed in the same
+  // (ph, pw) order as gather_sum, so its pooled gradient is bitwise the per-pixel gather's.
+  const uint32_t qh_n = (uint32_t)(a.g.oh + 1) >> 1, qw_n = (uint32_t)(a.g.ow + 1) >> 1;
+  const uint32_t total = (uint32_t)a.g.n * qh_n * qw_n * 8u, stride = gridDim.x * 256u;
+  for (uint32_t i = blockIdx.x * 256u + tid; i < total; i += stride) {
+    const uint32_t q = i >> 3, nn = q / (qh_n * qw_n), rem = q - nn * (qh_n * qw_n);
+    const int qh = (int)(rem / qw_n), qw = (int)(rem - (uint32_t)qh * qw_n);
+    uint2 ix[4];
+    uint4 gv[4], yv[4];
+    bool wok[4], pok[4];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const uint32_t i = i0 + u * stride;
-      live[u] = i < total;
-      const uint32_t pix = (live[u] ? i : i0) >> 3;
-      const uint32_t nn = fdiv(pix, a.div_ohw), rem = pix - nn * a.div_ohw.d;
-      const uint32_t yh = fdiv(rem, a.div_ow), yw = rem - yh * a.div_ow.d;
-      gather_issue(a, nn, (int)yh, (int)yw, c8, G[u]);
-      yv[u] = *reinterpret_cast<const uint4*>(a.y + (size_t)pix * CO + c8 * 8);
+    for (int s = 0; s < 4; ++s) {
+      const int ph = qh + (s >> 1), pw = qw + (s & 1);
+      wok[s] = ph < a.g.ph && pw < a.g.pw;
+      const size_t o = ((size_t)(nn * a.g.ph + min(ph, a.g.ph - 1)) * a.g.pw + min(pw, a.g.pw - 1)) * CO + c8 * 8;
+      ix[s] = *reinterpret_cast<const uint2*>(a.idx + o);
+      gv[s] = *reinterpret_cast<const uint4*>(a.dp + o);
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (!live[u]) continue;
+    for (int d = 0; d < 4; ++d) {
+      const int yh = 2 * qh + (d >> 1), yw = 2 * qw + (d & 1);
+      pok[d] = yh < a.g.oh && yw < a.g.ow;
+      const size_t pix = ((size_t)nn * a.g.oh + min(yh, a.g.oh - 1)) * a.g.ow + min(yw, a.g.ow - 1);
+      yv[d] = *reinterpret_cast<const uint4*>(a.y + pix * CO + c8 * 8);
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      if (!pok[d]) continue;
+      const int dy = d >> 1, dx = d & 1;
       float v[8], gs[8];
-      Vec8<T>::load(v, reinterpret_cast<const T*>(&yv[u]));
-      gather_sum<T>(G[u], gs);
+      Vec8<T>::load(v, reinterpret_cast<const T*>(&yv[d]));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) gs[e] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int sr = s >> 1, sc2 = s & 1;
+        if ((sr && !dy) || (sc2 && !dx)) continue;  // compile-time: the window misses the pixel
+        const uint32_t kk = wok[s] ? (uint32_t)((1 + dy - 2 * sr) * 3 + (1 + dx - 2 * sc2)) : 255u;
+        const uint32_t w[2] = {ix[s].x, ix[s].y};
+        const uint32_t gw[4] = {gv[s].x, gv[s].y, gv[s].z, gv[s].w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t k = (w[e >> 2] >> (8 * (e & 3))) & 0xffu;
+          const float g = to_f(T{(uint16_t)((gw[e >> 1] >> (16 * (e & 1))) & 0xffffu)});
+          gs[e] += k == kk ? g : 0.f;
+        }
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float gm = fmaf(v[e], sc[e], sh[e]) > 0.f ? gs[e] : 0.f;
