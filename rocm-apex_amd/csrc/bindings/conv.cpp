@@ -125,6 +125,29 @@ void wgrad(const at::Tensor& in, const at::Tensor& dy, at::Tensor& dw_out, int64
              cur_stream());
 }
 
+// True when conv_wgrad takes the halo-tile kernel (csrc/conv/conv3x3_wgrad.hip) for a 3x3 pad-1
+// stride-1 conv of an [n, h, w, c] input to kout channels (ops/conv.py tap_route)
+bool halo_wgrad_supported(int64_t n, int64_t h, int64_t w, int64_t c, int64_t kout) {
+  ConvTapArgs a{};
+  void* aligned = reinterpret_cast<void*>(static_cast<uintptr_t>(256));  // alignment checks only
+  a.in = a.wt = aligned;
+  a.out = aligned;
+  a.n = (int)n;
+  a.ih = a.oh = a.oht = (int)h;
+  a.iw = a.ow = a.owt = (int)w;
+  a.c = (int)c;
+  a.kout = (int)kout;
+  a.ish = a.isw = a.osh = a.osw = 1;
+  a.oph = a.opw = 0;
+  a.ntaps = 9;
+  for (int t = 0; t < 9; ++t) {
+    a.dh[t] = t / 3 - 1;
+    a.dw[t] = t % 3 - 1;
+  }
+  a.dtype = kBF16;
+  return conv_hwgrad_supported(a);
+}
+
 // y = pro(a) . W^T (+ BN statistics partials); see conv_api.h.  Returns (y, part or empty).
 std::vector<at::Tensor> bn1x1(const at::Tensor& a, const at::Tensor& w, bool w_kmajor_out,
                               const c10::optional<at::Tensor>& pcoef, const c10::optional<at::Tensor>& shift,
@@ -530,6 +553,8 @@ void bind_conv(pybind11::module_& root) {
   m.def("wgrad", &wgrad);
   m.def("force_fprop_cfg", &conv_force_fprop_cfg);
   m.def("force_wgrad_variant", &conv_force_wgrad_variant);
+  m.def("halo_wgrad_supported", &halo_wgrad_supported);
+  m.attr("WGRAD_HALO") = kWgradHalo;
   m.def("bn1x1", &bn1x1, pybind11::arg("a"), pybind11::arg("w"), pybind11::arg("w_kmajor_out") = false,
         pybind11::arg("pcoef") = pybind11::none(), pybind11::arg("shift") = pybind11::none(),
         pybind11::arg("stats") = false, pybind11::arg("res") = pybind11::none(),

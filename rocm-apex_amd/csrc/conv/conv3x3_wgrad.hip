@@ -1,0 +1,433 @@
+// Halo-tile 3x3 (pad 1, stride 1) weight gradient for gfx950: dW[k][tap][c] = sum over output
+// pixels p of dY[p][k] * X[p shifted by tap][c], NHWC bf16 / fp16, fp32 accumulation.
+//
+// Why not the per-tap split-M kernel (conv_igemm.hip wgrad2_kernel) or MIOpen's igemm_wrw: both
+// stage the shifted input ONCE PER TAP (9 gathers of the same rows per pixel tile) and re-stage
+// dY for every tap's column block, so at ResNet-50 shapes they run at 15-20 % of the MFMA peak
+// (profiles/resnet50_node_r04z.md: igemm_wrw 117-154 us per 59-GFLOP conv).  Here:
+//   * a workgroup owns an output block of KB (64 / 128) output channels x ALL 9 taps x 64 input
+//     channels, and walks a contiguous range of pixel TILES: R output rows of one image (or G
+//     whole small images), at most 112 pixels (7 reduction slices of 16);
+//   * per tile the dY rows [112][KB] and the input HALO [(R + 2) x HC slots][64] (zero outside the
+//     image, HC >= w + 2 columns) are staged into LDS ONCE by buffer_load ... lds (out-of-range
+//     offsets fill zeros: padding, ragged tails, images past the batch), through a 3-stage ring
+//     with counted vmcnt and a raw barrier (cdna_hip_programming.md "Pipelining across barriers");
+//   * every tap reads its shifted window straight out of the halo: for a 16-pixel slice each lane
+//     holds the halo slot of its two pixel rows (tile-invariant, computed once), the tap's column
+//     shift is one of three precomputed addresses and its row shift an instruction-immediate
+//     offset (HC % 4 == 0 keeps the bank swizzle invariant under row shifts);
+//   * one dY fragment feeds 9 MFMAs (one per tap), so per 32x32x16 MFMA a wave reads ~1.1 (TK 1)
+//     or ~0.6 (TK 2) fragments from LDS, both operands through ds_read_b64_tr_b16 (pixel-major
+//     images, the reduction dim is their row).
+// Each workgroup writes its fp32 partial block ([split][k][9][c]); a fixed-order pass sums the
+// splits (deterministic, no float atomics).
+// Reference capability: the weight-gradient graphs of apex/contrib/bottleneck
+// (apex/contrib/csrc/bottleneck/bottleneck.cpp:2236 bottleneck_backward_wgrad2), which run on
+// cuDNN there and not at all on ROCm.
+#include "apex_amd/conv_api.h"
+#include "apex_amd/dispatch.h"
+#include "apex_amd/mfma.h"
+
+#include <algorithm>
+#include <stdexcept>
+
+namespace apex_amd {
+namespace hwg {
+using namespace mfma;
+
+constexpr int NT = 256;         // 4 waves
+constexpr int NS = 7;           // 16-pixel reduction slices per tile
+constexpr int NPP = NS * 16;    // tile pixel capacity
+constexpr int S = 3;            // LDS ring stages
+
+struct Args {
+  const uint16_t* x;   // [n][h][w][c]
+  const uint16_t* dy;  // [n][h][w][k]
+  float* ws;           // [splits][k][9][c]
+  const float* xcoef;  // nullable [2][c]: x' = relu(x * xcoef[c] + xcoef[c + C]) (the producing BN + ReLU)
+  int h, w, c, k;
+  int R, HR, HC, hs;   // tile rows, halo rows / columns per image block, halo slots (G * HR * HC)
+  int np;              // real pixels per tile (G * R * w)
+  int tpi;             // tiles per image (h / R); 1 for whole-image tiles
+  int ntiles, splits, nblk_c;
+  int xbytes, dybytes;
+};
+
+template <int TK, int HSL, int HC_>
+struct Cfg {
+  static constexpr int HC = HC_;                       // halo columns (slots per halo row)
+  static constexpr int KB = 64 * TK;                   // output channels per workgroup
+  static constexpr int DYR = TK == 1 ? 128 : 112;      // dY image rows (DMA count a multiple of 4)
+  static constexpr int DYI = DYR * KB * 2 / 1024;      // dY DMA instructions per tile
+  static constexpr int HI = HSL / 8;                   // halo DMA instructions per tile (8 slots each)
+  static constexpr int DYW = DYI / 4, HW = HI / 4;     // per wave
+  static constexpr int PER = DYW + HW;
+  static constexpr int DY_EL = DYR * KB;               // dY image (elements)
+  static constexpr int STAGE_EL = DY_EL + HSL * 64;    // one ring stage (elements)
+  static constexpr size_t LDS = (size_t)S * STAGE_EL * 2;
+  static_assert(DYI % 4 == 0 && HI % 4 == 0, "DMA instructions must split evenly over the 4 waves");
+  static_assert(DYR >= NPP, "dY image holds the tile");
+  static_assert(LDS <= 160 * 1024, "ring exceeds the 160 KiB LDS");
+};
+
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int xcd = orig % 8, q = nwg / 8, r = nwg % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+__device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint16_t* lds_dst) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_dst, 16, (int)voff, 0, 0,
+                                           0);
+}
+
+// 16-byte chunk swizzle of a pixel-major image row r (W elements per row) read by
+// ds_read_b64_tr_b16: the 4 consecutive rows a 16-lane group reads land in 4 different 64-byte
+// quarters of the bank row
+template <int W>
+__device__ __forceinline__ int swz(int r) {
+  return W == 64 ? ((r >> 1) & 1) : (r & 3);
+}
+
+template <int W>
+__device__ __forceinline__ int img_addr(int row, int col) {
+  const int ck = col >> 3, off = col & 7;
+  return row * W + ((ck ^ (swz<W>(row) << 2)) << 3) + off;
+}
+
+__device__ __forceinline__ s16x8 frag2(const uint16_t* lo, const uint16_t* hi) {
+  const s16x4 a = tr_read(lo), b = tr_read(hi);
+  return s16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+template <typename T, int TK, int HSL, int HC>
+__global__ void __launch_bounds__(NT, 1) wgrad_kernel(const Args p) {
+  using C = Cfg<TK, HSL, HC>;
+  constexpr int KB = C::KB;
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 31, lh = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kg = wave >> 1, ct = wave & 1;  // kout tiles kg*TK .. +TK-1, c tile ct (32 channels)
+  const int nblk = (p.k / KB) * p.nblk_c;
+  const int wg = xcd_remap(blockIdx.x, nblk * p.splits);
+  // consecutive workgroups (one XCD) share a pixel range: dY / halo re-reads hit that XCD's L2
+  const int split = wg / nblk, blk = wg - split * nblk;
+  const int k0 = (blk / p.nblk_c) * KB, c0 = (blk % p.nblk_c) * 64;
+  const int t_begin = (int)((int64_t)split * p.ntiles / p.splits);
+  const int t_end = (int)((int64_t)(split + 1) * p.ntiles / p.splits);
+  const int nt = t_end - t_begin;
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, __builtin_amdgcn_readfirstlane(p.xbytes), 0x00020000);
+  const __amdgpu_buffer_rsrc_t dr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.dy, 0, __builtin_amdgcn_readfirstlane(p.dybytes), 0x00020000);
+
+  // ---- DMA constants of this lane (tile-invariant) ----
+  int dyrow[C::DYW];
+  uint32_t dyrel[C::DYW];
+#pragma unroll
+  for (int i = 0; i < C::DYW; ++i) {
+    const int j = i * 4 + wave;
+    int row, sc;
+    if constexpr (TK == 1) {
+      row = 8 * j + (lane >> 3);
+      sc = (lane & 7) ^ (swz<64>(row) << 2);
+    } else {
+      row = 4 * j + (lane >> 4);
+      sc = (lane & 15) ^ (swz<128>(row) << 2);
+    }
+    dyrow[i] = row;
+    dyrel[i] = (uint32_t)((row * p.k + k0 + 8 * sc) * 2);
+  }
+  int hrel[C::HW];
+  uint32_t hfl[C::HW];  // bit 0: column in range, bit 1: top halo row, bit 2: bottom halo row
+  const int hblk = p.HR * HC;
+#pragma unroll
+  for (int i = 0; i < C::HW; ++i) {
+    const int j = i * 4 + wave;
+    const int slot = 8 * j + (lane >> 3);
+    const int sc = (lane & 7) ^ (swz<64>(slot) << 2);
+    const int gi = slot / hblk, rem = slot - gi * hblk;
+    const int hy = rem / HC, hx = rem - hy * HC;
+    const bool ok = slot < p.hs && hx >= 1 && hx <= p.w;
+    hrel[i] = (((gi * p.h + hy - 1) * p.w) + hx - 1) * p.c * 2 + (c0 + 8 * sc) * 2;
+    hfl[i] = (ok ? 1u : 0u) | (hy == 0 ? 2u : 0u) | (hy == p.HR - 1 ? 4u : 0u);
+  }
+
+  auto issue = [&](int t, int stage) {
+    const int px0 = t * p.np;
+    const int y0 = (t % p.tpi) * p.R;
+    const uint32_t kill = (y0 == 0 ? 2u : 0u) | (y0 + p.R == p.h ? 4u : 0u);
+    uint16_t* base = lds + stage * C::STAGE_EL;
+    const uint32_t dyo = (uint32_t)px0 * (uint32_t)p.k * 2u;
+#pragma unroll
+    for (int i = 0; i < C::DYW; ++i) {
+      const uint32_t voff = dyrow[i] < p.np ? dyo + dyrel[i] : 0x80000000u;
+      bdma16(dr, voff, base + (i * 4 + wave) * 512);
+    }
+    const int xo = px0 * p.c * 2;
+#pragma unroll
+    for (int i = 0; i < C::HW; ++i) {
+      const bool valid = (hfl[i] & 1u) && !(hfl[i] & kill);
+      const uint32_t voff = valid ? (uint32_t)(xo + hrel[i]) : 0x80000000u;
+      bdma16(xr, voff, base + C::DY_EL + (i * 4 + wave) * 512);
+    }
+  };
+
+  // ---- fragment addresses (elements from a stage base; tile-invariant) ----
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+  int aaddr[TK][2];
+#pragma unroll
+  for (int i = 0; i < TK; ++i) {
+    const int col = 32 * (kg * TK + i) + 16 * (g & 1) + 4 * pp;
+    const int r0 = 8 * (g >> 1) + q;
+    aaddr[i][0] = img_addr<KB>(r0, col);
+    aaddr[i][1] = img_addr<KB>(r0 + 4, col);
+  }
+  // halo: per slice, lo / hi pixel row, tap column shift dw = -1, 0, 1 at tap row dh = -1 (dh = 0
+  // and 1 add HC and 2 HC slots: an instruction-immediate offset, HC being a compile-time size)
+  int baddr[NS][2][3];
+  {
+    const int col = 32 * ct + 16 * (g & 1) + 4 * pp;
+    const int rw = p.R * p.w;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) {
+        const int px = 16 * s + 8 * (g >> 1) + q + 4 * hl;
+        int slot = HC + 1;  // pixel rows past the tile: any real slot (their dY rows are zero)
+        if (px < p.np) {
+          const int gi = px / rw, rem = px - gi * rw;
+          const int y = rem / p.w, x = rem - y * p.w;
+          slot = (gi * p.HR + y + 1) * HC + x + 1;
+        }
+#pragma unroll
+        for (int d = 0; d < 3; ++d) baddr[s][hl][d] = C::DY_EL + img_addr<64>(slot - HC + d - 1, col);
+      }
+  }
+
+  f32x16 acc[TK][9];
+#pragma unroll
+  for (int i = 0; i < TK; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = zero16();
+
+#pragma unroll
+  for (int st = 0; st < S - 1; ++st)
+    if (st < nt) issue(t_begin + st, st);
+
+  for (int it = 0; it < nt; ++it) {
+    // this wave's DMA of tile it has landed (younger tiles may still be in flight); the barrier
+    // publishes every wave's pieces and retires every wave's reads of the stage refilled next
+    const int ahead = min(nt - 1 - it, S - 2);
+    if (ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::PER) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (it + S - 1 < nt) issue(t_begin + it + S - 1, (it + S - 1) % S);
+    const uint16_t* sb = lds + (it % S) * C::STAGE_EL;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      s16x8 af[TK], bf[9];
+#pragma unroll
+      for (int i = 0; i < TK; ++i)
+        af[i] = frag2(sb + aaddr[i][0] + s * 16 * KB, sb + aaddr[i][1] + s * 16 * KB);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int dh = t / 3, dw = t % 3;
+        bf[t] = frag2(sb + baddr[s][0][dw] + dh * HC * 64, sb + baddr[s][1][dw] + dh * HC * 64);
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < TK; ++i) acc[i][t] = mma<T>(af[i], bf[t], acc[i][t]);
+    }
+  }
+
+  // ---- fp32 partial block: lane holds c = c0 + 32 ct + lr, k rows crow(r, lh) ----
+  float* dst = p.ws + (int64_t)split * p.k * 9 * p.c;
+#pragma unroll
+  for (int i = 0; i < TK; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kr = k0 + 32 * (kg * TK + i) + crow(r, lh);
+        dst[((int64_t)kr * 9 + t) * p.c + c0 + 32 * ct + lr] = acc[i][t][r];
+      }
+}
+
+// fixed-order sum of the split partials (16 thread groups per block each take every 16th split,
+// then one LDS fold in group order)
+template <typename TO>
+__global__ void __launch_bounds__(256) reduce_kernel(const float* __restrict__ part, int splits, int64_t n,
+                                                     TO* __restrict__ out) {
+  __shared__ float red[16][16 * 8 + 4];
+  const int v = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int64_t i = ((int64_t)blockIdx.x * 16 + v) * 8;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (i < n)
+    for (int q = grp; q < splits; q += 16) {
+      float t8[8];
+      Vec8<float>::load(t8, part + (int64_t)q * n + i);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += t8[e];
+    }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[grp][v * 8 + e] = a[e];
+  __syncthreads();
+  if (grp != 0 || i >= n) return;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = 0.f;
+  for (int g2 = 0; g2 < 16; ++g2)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] += red[g2][v * 8 + e];
+  Vec8<TO>::store(out + i, a);
+}
+
+// ---- launch plan ----
+// Instantiated (TK, halo slots, halo columns) tuples, in order of preference: 128-channel blocks
+// where the ring still holds 3 stages (28 x 28 / 14 x 14 at ResNet-50 widths), else 64.
+struct Inst {
+  int tk, hsl, hc;
+};
+// (TK 2 — 18 accumulator tiles, 288 registers per lane — does not fit beside the operands without
+// spilling on hipcc 7.2, so every block is 64 output channels for now)
+constexpr Inst kInst[] = {{1, 224, 12}, {1, 256, 16}, {1, 256, 32}, {1, 256, 60}};
+
+struct Plan {
+  bool ok;
+  int tk, hsl, R, G, HR, HC, hs, np, tpi, ntiles, splits, nblk_c;
+};
+
+// tile geometry for halo width hc and slot budget hsl: rows of one image (the largest divisor of
+// h whose pixels and halo fit) or, for small images, as many whole images as fit
+inline bool tile_geo(int h, int w, int hc, int hsl, int& R, int& G) {
+  if (w + 2 > hc) return false;
+  R = 0;
+  G = 1;
+  if (h * w <= NPP / 2) {
+    if ((h + 2) * hc > hsl) return false;
+    R = h;
+    G = std::max(1, std::min(NPP / (h * w), hsl / ((h + 2) * hc)));
+    return true;
+  }
+  for (int r = h; r >= 1; --r)
+    if (h % r == 0 && r * w <= NPP && (r + 2) * hc <= hsl) {
+      R = r;
+      return true;
+    }
+  return false;
+}
+
+inline Plan make_plan(const ConvTapArgs& a, int cus) {
+  Plan pl{};
+  pl.ok = false;
+  const int h = a.oh, w = a.ow;
+  if (w < 1 || h < 1) return pl;
+  double best = -1.0;
+  for (const Inst& in : kInst) {
+    if (in.tk == 2 && a.kout % 128) continue;
+    int R, G;
+    if (!tile_geo(h, w, in.hc, in.hsl, R, G)) continue;
+    // pixel-slot efficiency, with a 10 % bonus for the 128-channel block (half the halo re-reads)
+    const double eff = (double)(G * R * w) / NPP * (in.tk == 2 ? 1.1 : 1.0);
+    if (eff > best + 1e-9) {
+      best = eff;
+      pl.tk = in.tk;
+      pl.hsl = in.hsl;
+      pl.HC = in.hc;
+      pl.R = R;
+      pl.G = G;
+    }
+  }
+  if (best < 0) return pl;
+  pl.HR = pl.R + 2;
+  pl.hs = pl.G * pl.HR * pl.HC;
+  pl.np = pl.G * pl.R * w;
+  pl.tpi = pl.G > 1 ? 1 : h / pl.R;
+  pl.ntiles = pl.G > 1 ? (a.n + pl.G - 1) / pl.G : a.n * pl.tpi;
+  pl.nblk_c = a.c / 64;
+  const int nblk = (a.kout / (64 * pl.tk)) * pl.nblk_c;
+  int sp = std::max(1, cus / nblk);
+  sp = std::min(sp, pl.ntiles);
+  pl.splits = sp;
+  pl.ok = true;
+  return pl;
+}
+
+}  // namespace hwg
+
+bool conv_hwgrad_supported(const ConvTapArgs& a) {
+  if (a.dtype != kBF16 && a.dtype != kF16) return false;
+  if (a.ntaps != 9 || a.c % 64 || a.kout % 64 || a.c <= 0 || a.kout <= 0 || a.n <= 0) return false;
+  if (a.ish != 1 || a.isw != 1 || a.osh != 1 || a.osw != 1 || a.oph != 0 || a.opw != 0) return false;
+  if (a.oh != a.ih || a.ow != a.iw || a.oht != a.oh || a.owt != a.ow) return false;
+  for (int t = 0; t < 9; ++t)
+    if (a.dh[t] != t / 3 - 1 || a.dw[t] != t % 3 - 1) return false;
+  const int64_t xb = (int64_t)a.n * a.ih * a.iw * a.c * 2, db = (int64_t)a.n * a.oh * a.ow * a.kout * 2;
+  // buffer ranges, and the per-tile byte origins in 32 bits with a tile of headroom
+  if (xb + (int64_t)hwg::NPP * 8 * a.c * 2 >= (1ll << 31) || db + (int64_t)hwg::NPP * a.kout * 2 >= (1ll << 31))
+    return false;
+  if (((uintptr_t)a.in & 15) || ((uintptr_t)a.out & 15)) return false;
+  return hwg::make_plan(a, 256).ok;
+}
+
+int64_t conv_hwgrad_workspace_floats(const ConvTapArgs& a, int cus) {
+  const hwg::Plan pl = hwg::make_plan(a, cus);
+  return (int64_t)pl.splits * a.kout * 9 * a.c;
+}
+
+void conv_hwgrad(const ConvTapArgs& a, const void* dy, void* dw_out, int out_dtype, float* ws, int cus,
+                 hipStream_t s) {
+  if (!conv_hwgrad_supported(a) || ((uintptr_t)dy & 15) || ((uintptr_t)dw_out & 15) || ((uintptr_t)ws & 15))
+    throw std::runtime_error("conv_hwgrad: unsupported shape / dtype / alignment");
+  const hwg::Plan pl = hwg::make_plan(a, cus);
+  hwg::Args p;
+  p.x = static_cast<const uint16_t*>(a.in);
+  p.dy = static_cast<const uint16_t*>(dy);
+  p.ws = ws;
+  p.xcoef = nullptr;
+  p.h = a.ih;
+  p.w = a.iw;
+  p.c = a.c;
+  p.k = a.kout;
+  p.R = pl.R;
+  p.HR = pl.HR;
+  p.HC = pl.HC;
+  p.hs = pl.hs;
+  p.np = pl.np;
+  p.tpi = pl.tpi;
+  p.ntiles = pl.ntiles;
+  p.splits = pl.splits;
+  p.nblk_c = pl.nblk_c;
+  p.xbytes = (int)((int64_t)a.n * a.ih * a.iw * a.c * 2);
+  p.dybytes = (int)((int64_t)a.n * a.oh * a.ow * a.kout * 2);
+  const int nblk = (a.kout / (64 * pl.tk)) * pl.nblk_c;
+  const unsigned grid = (unsigned)(nblk * pl.splits);
+  dispatch_16(a.dtype, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    auto go = [&](auto kern, size_t lds) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(hwg::NT), lds, s, p);
+    };
+#define HWG_CASE(TK_, HSL_, HC_)                                                   \
+  if (pl.tk == TK_ && pl.hsl == HSL_ && pl.HC == HC_) {                            \
+    go(hwg::wgrad_kernel<T, TK_, HSL_, HC_>, hwg::Cfg<TK_, HSL_, HC_>::LDS);       \
+    return;                                                                        \
+  }
+    HWG_CASE(1, 224, 12) HWG_CASE(1, 256, 16) HWG_CASE(1, 256, 32) HWG_CASE(1, 256, 60)
+#undef HWG_CASE
+    throw std::runtime_error("conv_hwgrad: no kernel for the plan");
+  }, "conv_hwgrad");
+  const int64_t n = (int64_t)a.kout * 9 * a.c;
+  const int64_t blocks = (n / 8 + 15) / 16;
+  dispatch_float(out_dtype, [&](auto tag) {
+    using TO = typename decltype(tag)::type;
+    hipLaunchKernelGGL((hwg::reduce_kernel<TO>), dim3((unsigned)blocks), dim3(256), 0, s, (const float*)ws, pl.splits,
+                       n, (TO*)dw_out);
+  }, "conv_hwgrad out");
+  check_launch("conv_hwgrad");
+}
+
+}  // namespace apex_amd

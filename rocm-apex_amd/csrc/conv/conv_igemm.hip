@@ -1266,7 +1266,14 @@ static int wgrad_variant(const ConvTapArgs& a) {
   return plan::conv_wgrad_variant_ok(a, 3) ? 3 : 0;
 }
 
+// the halo-tile kernel (conv3x3_wgrad.hip) wherever it applies, unless a tap-kernel variant is forced
+static bool use_halo_wgrad(const ConvTapArgs& a) {
+  if (g_wgrad_variant >= 0 && g_wgrad_variant != kWgradHalo) return false;
+  return conv_hwgrad_supported(a);
+}
+
 int64_t conv_wgrad_workspace_floats(const ConvTapArgs& a, int cus) {
+  if (use_halo_wgrad(a)) return conv_hwgrad_workspace_floats(a, cus);
   const conv::WgPlan p = plan::conv_wgrad(a, cus, wgrad_variant(a));
   return (int64_t)p.splits * a.kout * a.ntaps * a.c;
 }
@@ -1275,6 +1282,10 @@ void conv_wgrad(const ConvTapArgs& a, const void* dy, void* dw_out, int out_dtyp
                 hipStream_t s) {
   if (!conv_wgrad_supported(a) || !aligned16(dy) || !aligned16(dw_out) || !aligned16(ws))
     throw std::runtime_error("conv_wgrad: unsupported shape / dtype / alignment");
+  if (use_halo_wgrad(a)) {
+    conv_hwgrad(a, dy, dw_out, out_dtype, ws, cus, s);
+    return;
+  }
   const conv::Geo g = conv::make_geo(a);
   const int v = wgrad_variant(a);
   const conv::WgPlan p = plan::conv_wgrad(a, cus, v);

@@ -70,8 +70,17 @@ void conv_sp_fprop(const ConvTapArgs& a, int cus, hipStream_t s);
 // (dy = `out` geometry with osh = osw = 1, oph = opw = 0; x = `in`).  fp32 result [kout][ntaps][c]
 // through split-K partials in `ws` (conv_wgrad_workspace_floats), summed in a fixed order.
 bool conv_wgrad_supported(const ConvTapArgs& a);
-// A/B hook: force one weight-gradient variant (launch_plan.h conv_wgrad; -1 = per-shape default)
+// A/B hook: force one weight-gradient variant (launch_plan.h conv_wgrad; -1 = per-shape default;
+// kWgradHalo = the halo-tile kernel below)
 void conv_force_wgrad_variant(int v);
+constexpr int kWgradHalo = 5;
+// halo-tile 3x3 stride-1 weight gradient (csrc/conv/conv3x3_wgrad.hip): one workgroup per
+// (output-channel block x all 9 taps x 64 input channels) over a range of pixel tiles, the input
+// halo staged once per tile; the default engine of conv_wgrad wherever it applies
+bool conv_hwgrad_supported(const ConvTapArgs& a);
+int64_t conv_hwgrad_workspace_floats(const ConvTapArgs& a, int cus);
+void conv_hwgrad(const ConvTapArgs& a, const void* dy, void* dw_out, int out_dtype, float* ws, int cus,
+                 hipStream_t s);
 int64_t conv_wgrad_workspace_floats(const ConvTapArgs& a, int cus);
 void conv_wgrad(const ConvTapArgs& a, const void* dy, void* dw_out, int out_dtype, float* ws, int cus,
                 hipStream_t s);

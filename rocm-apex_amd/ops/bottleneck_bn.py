@@ -254,7 +254,7 @@ def _conv_fwd(x, w, stride, pad):
 
 
 def _conv_bwd(gy, x, w, stride, pad, need_x=True):
-    _, dg, wg = convops.tap_route(x.size(1), w.size(0), w.size(2), stride, x.size(2))
+    _, dg, wg = convops.tap_route(x.size(1), w.size(0), w.size(2), stride, x.size(2), x.size(3))
     dx = dw = None
     if need_x and dg:
         dx = convops.conv_tap_dgrad(gy, w, x.shape, stride, pad)

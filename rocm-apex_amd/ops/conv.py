@@ -127,6 +127,8 @@ class Conv1x1NHWC(nn.Conv2d):
 # Implicit-GEMM convolutions (csrc/conv/conv_igemm.hip): 3x3 stride 1/2 and strided 1x1, NHWC.
 # ------------------------------------------------------------------------------------------------
 _TAP_ENABLED = os.environ.get("APEX_AMD_CONV_IGEMM", "1") != "0"
+# the halo-tile 3x3 weight gradient (csrc/conv/conv3x3_wgrad.hip); 0 = the r04 routes (A/B)
+_HALO_WGRAD = os.environ.get("APEX_AMD_HALO_WGRAD", "1") != "0"
 
 
 def _conv_ext():
@@ -289,7 +291,16 @@ def conv_tap_wgrad(gy, x, w_shape, stride, pad, out_dtype):
     return dw.permute(0, 3, 1, 2)  # [K, C, R, S] in channels_last memory
 
 
-def tap_route(cin, cout, k, stride, h):
+def _halo_wgrad(cin, cout, h, w):
+    if not _HALO_WGRAD:
+        return False
+    ext = _native.submodule("conv")
+    if ext is None or not hasattr(ext, "halo_wgrad_supported"):
+        return False
+    return bool(ext.halo_wgrad_supported(1, h, w, cin, cout))
+
+
+def tap_route(cin, cout, k, stride, h, w=None):
     """(fwd, dgrad, wgrad) through the native kernels for this shape, from the per-shape A/B
     against MIOpen on MI355X (ResNet-50 bs 256 bf16; r04: profiles/conv_cfg_sweep_r04.jsonl,
     profiles/wgrad3x3_variants_r04.jsonl — r02: conv_cfg_sweep_r02.jsonl):
@@ -298,12 +309,15 @@ def tap_route(cin, cout, k, stride, h):
       * 3x3 data gradient: native except the stride-2 one at <= 128 channels (per-phase launches,
         173.9 vs 171.0 us);
       * 1x1 stride 2 (downsample): data gradient native (0.70-0.91x MIOpen);
-      * 3x3 weight gradient: native (wgrad2 128 x 64) only at 28x28x128 stride 1 (136 vs 149 us);
-        MIOpen's is 5-12 % ahead at the other shapes."""
+      * 3x3 weight gradient, stride 1: the halo-tile kernel (conv3x3_wgrad.hip) wherever it takes
+        the shape; r04 routes otherwise (wgrad2 128 x 64 only at 28x28x128: 136 vs 149 us, MIOpen
+        5-12 % ahead at the other shapes)."""
     if not _TAP_ENABLED:
         return False, False, False
     if k == 3:
-        return True, not (stride == 2 and cout <= 128), (stride == 1 and cin == 128 and cout == 128 and h == 28)
+        wg = stride == 1 and (_halo_wgrad(cin, cout, h, h if w is None else w)
+                              or (cin == 128 and cout == 128 and h == 28))
+        return True, not (stride == 2 and cout <= 128), wg
     if k == 1 and stride == 2:
         return False, True, False
     return False, False, False
@@ -358,7 +372,8 @@ class Conv2dNHWC(nn.Conv2d):
 
     def forward(self, x):
         if self._native_ok(x):
-            route = tap_route(self.in_channels, self.out_channels, self.kernel_size[0], self.stride[0], x.shape[2])
+            route = tap_route(self.in_channels, self.out_channels, self.kernel_size[0], self.stride[0], x.shape[2],
+                              x.shape[3])
             if any(route):
                 return _ConvTapFn.apply(x, self.weight, self.stride[0], self.padding[0], route)
         return super().forward(x)
