@@ -49,6 +49,11 @@ def parse():
     ap.add_argument("--materialize-master-grads", action="store_true",
                     help="reference-style unscale into fp32 master grads (slower path)")
     ap.add_argument("--sync-bn", action="store_true")
+    ap.add_argument("--message-size", type=float, default=1e7,
+                    help="DDP gradient bucket size in elements (apex.parallel.DistributedDataParallel message_size)")
+    ap.add_argument("--comm-steps", type=int, default=3,
+                    help="N > 1: untimed steps after the timed ones with collective timing on (allreduce_exposed_ms, "
+                         "bn_exchange_ms_per_step in the JSON config)")
     ap.add_argument("--bn", default="fused", choices=["fused", "torch"],
                     help="fused: apex.contrib.groupbn NHWC BN with fused ReLU / add+ReLU (gfx950 kernels); "
                          "torch: nn.BatchNorm2d + ReLU (MIOpen)")
@@ -138,7 +143,7 @@ def main():
     model, optimizer = amp.initialize(model, optimizer, opt_level=args.opt_level, cast_model_type=low,
                                       keep_batchnorm_fp32=True, verbosity=0)
     if distributed:
-        model = apex.parallel.DistributedDataParallel(model)
+        model = apex.parallel.DistributedDataParallel(model, message_size=int(args.message_size))
     criterion = torch.nn.CrossEntropyLoss().to(dev)
     args.bn_exchange = None
     if sync_bn:
@@ -265,11 +270,30 @@ def timed(args, step, dev, world, rank, distributed, B, impl, desc=None):
     # fused bottleneck nodes run per timed step (16 on ResNet-50's fused path; graph replays do
     # not re-enter Python, so the count is taken from the eager / capture steps)
     nodes = (bottleneck_bn.NODE_CALLS[0] - nodes0) / args.steps
+    # collective accounting (N > 1): a few more steps, NOT timed, with events around the DDP
+    # tail all-reduce and every batch-norm statistics exchange (apex.parallel.comm_timing)
+    comm = {}
+    if distributed and args.comm_steps > 0 and not getattr(args, "graph", False):
+        from apex.parallel import comm_timing
+
+        comm_timing.reset()
+        comm_timing.enable(True)
+        for _ in range(args.comm_steps):
+            step()
+        comm_timing.enable(False)
+        per = comm_timing.summary(args.comm_steps)
+        comm = {"allreduce_exposed_ms": per.get("allreduce_exposed", 0.0),
+                "bn_exchange_ms_per_step": per.get("bn_exchange", 0.0),
+                "comm_timing_steps": args.comm_steps}
+        t2 = torch.tensor([comm["allreduce_exposed_ms"], comm["bn_exchange_ms_per_step"]], device=dev,
+                          dtype=torch.float64)
+        dist.all_reduce(t2, op=dist.ReduceOp.MAX)
+        comm["allreduce_exposed_ms"], comm["bn_exchange_ms_per_step"] = (round(float(v), 4) for v in t2.tolist())
     value = world * B * args.steps / elapsed
     if rank == 0 and desc is not None:
         value = world * desc["items_per_gpu_step"] * args.steps / elapsed
         cfg = dict(desc["config"], final_loss=round(float(loss.item()), 4),
-                   timing="hipgraph-replay" if getattr(args, "graph", False) else "eager")
+                   timing="hipgraph-replay" if getattr(args, "graph", False) else "eager", **comm)
         res = {"metric": desc["metric"], "value": round(value, 2), "unit": desc["unit"], "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
@@ -309,6 +333,9 @@ def timed(args, step, dev, world, rank, distributed, B, impl, desc=None):
                 "parallelism": f"dp{world}",
                 "timing": "hipgraph-replay" if getattr(args, "graph", False) else "eager",
                 "bn_exchange": getattr(args, "bn_exchange", None),
+                "ddp_message_size": int(args.message_size) if distributed else None,
+                "allreduce_exposed_ms": comm.get("allreduce_exposed_ms"),
+                "bn_exchange_ms_per_step": comm.get("bn_exchange_ms_per_step"),
                 "block_nodes_per_step": None if getattr(args, "graph", False) else nodes,
                 "block_node": bool(nodes > 0) if not getattr(args, "graph", False) else None,
                 "final_loss": round(float(loss.item()), 4),

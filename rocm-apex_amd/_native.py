@@ -86,4 +86,7 @@ def column_sum(x, out_dtype):
     if (use_native(x) and submodule("gemm") is not None and x.dim() >= 2 and x.is_contiguous()
             and x.shape[-1] % 8 == 0 and x.dtype in (torch.float16, torch.bfloat16, torch.float32)):
         return _C.gemm.column_sum(x.reshape(-1, x.shape[-1]), out_dtype)
-    return x.reshape(-1, x.shape[-1]).sum(0, dtype=torch.float32).to(out_dtype)
+    # torch fallback: accumulate in at least fp32 (fp64 stays fp64: a double-precision gradcheck
+    # of a FusedDense backward must not lose bits here)
+    acc = torch.promote_types(x.dtype, torch.float32)
+    return x.reshape(-1, x.shape[-1]).sum(0, dtype=acc).to(out_dtype)

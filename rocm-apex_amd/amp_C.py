@@ -15,7 +15,7 @@ __all__ = [
     "multi_tensor_norm_out", "multi_tensor_adam", "multi_tensor_adam_capturable", "multi_tensor_adam_undo", "multi_tensor_sgd",
     "multi_tensor_sgd_capturable", "multi_tensor_adagrad", "multi_tensor_novograd", "multi_tensor_lamb",
     "multi_tensor_lamb_mp", "multi_tensor_lamb_stage1_cuda", "multi_tensor_lamb_stage2_cuda",
-    "multi_tensor_cast", "amp_update_scale_", "mta_cache_clear", "mta_cache_size",
+    "multi_tensor_lamb_stage1_capturable", "multi_tensor_lamb_stage2_capturable", "multi_tensor_cast", "amp_update_scale_", "mta_cache_clear", "mta_cache_size",
 ]
 
 

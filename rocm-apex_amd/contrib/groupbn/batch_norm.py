@@ -219,6 +219,13 @@ def bn_relu_maxpool(x, bn, pool):
 
 def _exchange_gather(payload, group):
     """[world, n] fp32: every group member's ``payload`` (peer memory, else RCCL / gloo)."""
+    from ...parallel import comm_timing
+
+    with comm_timing.span("bn_exchange", payload.device):
+        return _exchange_gather_impl(payload, group)
+
+
+def _exchange_gather_impl(payload, group):
     import torch.distributed as dist
 
     from ...parallel.peer_memory import get_peer_exchange
@@ -241,6 +248,13 @@ def _exchange_sum(payload, group):
     """Group sums as [rows, n] rows to be added in order by the consumer kernel: the peer path
     hands back every member's row (summed in rank order in-kernel, identical on all members),
     the collective path one all-reduced row."""
+    from ...parallel import comm_timing
+
+    with comm_timing.span("bn_exchange", payload.device):
+        return _exchange_sum_impl(payload, group)
+
+
+def _exchange_sum_impl(payload, group):
     import torch.distributed as dist
 
     from ...parallel.peer_memory import get_peer_exchange

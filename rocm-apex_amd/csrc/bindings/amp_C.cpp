@@ -362,6 +362,40 @@ void multi_tensor_lamb_stage2_cuda(int chunk_size, at::Tensor noop, TL tl, at::T
                         (float)weight_decay, use_nvlamb.value_or(false), make_launch(tl[0][0]));
 }
 
+// capturable legacy pair (DistributedFusedLAMB): `skip` int32 device flag gates both launches,
+// step / lr are fp32 device scalars — no host value per step, no sync
+void multi_tensor_lamb_stage1_capturable(int chunk_size, at::Tensor skip, TL tl, at::Tensor per_tensor_decay,
+                                         at::Tensor step, bool bias_correction, double beta1, double beta2,
+                                         double eps, at::Tensor global_grad_norm, double max_global_grad_norm,
+                                         double beta3) {
+  if (!prepare(tl)) return;
+  TORCH_CHECK(tl.size() == 5, "multi_tensor_lamb_stage1_capturable expects 5 lists (g, p, m, v, update)");
+  TORCH_CHECK(step.is_cuda() && step.scalar_type() == at::kFloat && step.numel() == 1, "step: fp32 [1] device tensor");
+  TORCH_CHECK(skip.is_cuda() && skip.scalar_type() == at::kInt && skip.numel() >= 1, "skip: int32 device flag");
+  const c10::hip::HIPGuard g(tl[0][0].get_device());
+  auto m = mta_meta(tl, chunk_size);
+  mt_lamb_legacy_stage1(m, dtype_code(tl[0][0].scalar_type()), dtype_code(tl[1][0].scalar_type()), noop_ptr(skip),
+                        per_tensor_decay.data_ptr<float>(), (float)beta1, (float)beta2, (float)beta3, 1.f, 1.f,
+                        (float)eps, global_grad_norm.data_ptr<float>(), (float)max_global_grad_norm,
+                        make_launch(tl[0][0]), step.data_ptr<float>(), bias_correction ? 1 : 0);
+}
+
+void multi_tensor_lamb_stage2_capturable(int chunk_size, at::Tensor skip, TL tl, at::Tensor per_tensor_param_norm,
+                                         at::Tensor per_tensor_update_norm, at::Tensor lr, double weight_decay,
+                                         bool use_nvlamb) {
+  if (!prepare(tl)) return;
+  TORCH_CHECK(tl.size() == 2 || tl.size() == 3, "multi_tensor_lamb_stage2_capturable expects 2 or 3 lists");
+  TORCH_CHECK(lr.is_cuda() && lr.scalar_type() == at::kFloat && lr.numel() == 1, "lr: fp32 [1] device tensor");
+  TORCH_CHECK(skip.is_cuda() && skip.scalar_type() == at::kInt && skip.numel() >= 1, "skip: int32 device flag");
+  const c10::hip::HIPGuard g(tl[0][0].get_device());
+  auto m = mta_meta(tl, chunk_size);
+  const int out_t = tl.size() == 3 ? dtype_code(tl[2][0].scalar_type()) : -1;
+  mt_lamb_legacy_stage2(m, dtype_code(tl[0][0].scalar_type()), dtype_code(tl[1][0].scalar_type()), out_t,
+                        noop_ptr(skip), per_tensor_param_norm.data_ptr<float>(),
+                        per_tensor_update_norm.data_ptr<float>(), 0.f, (float)weight_decay, use_nvlamb,
+                        make_launch(tl[0][0]), lr.data_ptr<float>());
+}
+
 void multi_tensor_cast(int chunk_size, at::Tensor noop, TL tl) {
   if (!prepare(tl)) return;
   TORCH_CHECK(tl.size() == 2, "multi_tensor_cast expects 2 lists");
@@ -422,6 +456,10 @@ void bind_amp_C(pybind11::module_& root) {
         pybind11::arg("epsilon"), pybind11::arg("global_grad_norm"), pybind11::arg("max_global_grad_norm"),
         pybind11::arg("beta3") = c10::nullopt);
   m.def("multi_tensor_lamb_stage2_cuda", &multi_tensor_lamb_stage2_cuda, "legacy LAMB stage 2");
+  m.def("multi_tensor_lamb_stage1_capturable", &multi_tensor_lamb_stage1_capturable,
+        "legacy LAMB stage 1, skip-gated, device step");
+  m.def("multi_tensor_lamb_stage2_capturable", &multi_tensor_lamb_stage2_capturable,
+        "legacy LAMB stage 2, skip-gated, device lr");
   m.def("multi_tensor_cast", &multi_tensor_cast, "out = in (dtype conversion)");
   m.def("amp_update_scale_", &amp_update_scale_, "device-side dynamic loss scale update");
   m.def("mta_cache_clear", &mta_cache_clear, "drop cached multi-tensor work tables");

@@ -15,8 +15,11 @@
 #include "common.h"
 
 #include <hipblaslt/hipblaslt.h>
+#include <hipblaslt/hipblaslt-ext.hpp>
 
+#include <algorithm>
 #include <cstdlib>
+#include <vector>
 #include <memory>
 #include <mutex>
 #include <tuple>
@@ -87,8 +90,11 @@ struct Plan {
   bool ok = false;
   hipblasLtMatmulAlgo_t algo;
   Descs ds;
-  int candidates = 0;   // heuristic results considered
+  int candidates = 0;   // heuristic results that passed the support screen
   float best_us = 0.f;  // measured time of the pick (0: not timed)
+  int choice = 0;       // index of the pick among the screened candidates (rank-consistent when synced)
+  std::vector<hipblasLtMatmulAlgo_t> cand;
+  std::vector<float> cand_us;  // measured per-candidate time (-1: not timed / failed to launch)
 };
 
 void make_descs(const Problem& p, Descs& ds, hipDataType bias_t, bool has_aux, int64_t aux_ld) {
@@ -124,14 +130,24 @@ std::mutex g_plan_mu;
 // APEX_AMD_LT_TUNE=0: take the heuristic's first answer (deterministic across ranks / runs);
 // default: time the top kTop answers once per problem on its first (non-captured) call and keep
 // the fastest — the single-answer heuristic picked a 32 x 32-tile BGRADB kernel ~10x slower than
-// the plain GEMM at the GPT-2 shapes
+// the plain GEMM at the GPT-2 shapes.  Every candidate is screened with
+// hipblaslt_ext::matmulIsAlgoSupported (and its workspace need against ours) before it is
+// launched at all.  The pick is recorded as an index into the screened list: plan_choices() /
+// set_plan_choice() let the Python side make it identical on every rank of a tensor-parallel
+// group (apex.fused_dense.sync_lt_plans broadcasts rank 0's picks), so partial sums never come
+// from different kernels on different ranks.
 constexpr int kTop = 8;
-// Timing the top answers is limited to problems with every dimension <= 16384 (the transformer
-// dense shapes it was validated on): at 32768 tokens (and at m = 200704) one of the extra
-// candidates makes hipBLASLt fail to initialise its kernel ("Could not initialize Tensile host")
-// and then fault inside the library (tools/gpu_r04ab.sh), while the heuristic's first answer
-// runs fine — larger problems take that first answer, as torch.matmul does.
-constexpr int64_t kTuneMaxDim = 16384;
+// Timing is limited to problems with every dimension <= APEX_AMD_LT_TUNE_MAX_DIM (default 16384,
+// the transformer dense shapes it was validated on): before the support screen existed, one
+// unscreened candidate at 32768 tokens (and at m = 200704) made hipBLASLt fail to initialise its
+// kernel ("Could not initialize Tensile host") and crash the process (tools/gpu_r04ab.sh).
+int64_t tune_max_dim() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("APEX_AMD_LT_TUNE_MAX_DIM");
+    return e ? (int64_t)std::atoll(e) : (int64_t)16384;
+  }();
+  return v;
+}
 bool tune_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("APEX_AMD_LT_TUNE");
@@ -166,18 +182,27 @@ bool lt_run(const Problem& p, const void* a, const void* b, void* d, const void*
              "workspace pref");
     hipblasLtMatmulHeuristicResult_t res[kTop];
     int found = 0;
-    const bool tune = tune_enabled() && p.m <= kTuneMaxDim && p.n <= kTuneMaxDim && p.k <= kTuneMaxDim;
+    const int64_t cap = tune_max_dim();
+    const bool tune = tune_enabled() && p.m <= cap && p.n <= cap && p.k <= cap;
     const hipblasStatus_t st =
         hipblasLtMatmulAlgoGetHeuristic(h, plan->ds.op, plan->ds.a, plan->ds.b, plan->ds.d, plan->ds.d, pref,
                                         tune ? kTop : 1, res, &found);
     hipblasLtMatmulPreferenceDestroy(pref);
-    int valid[kTop], nv = 0;
     if (st == HIPBLAS_STATUS_SUCCESS)
-      for (int i = 0; i < found; ++i)
-        if (res[i].state == HIPBLAS_STATUS_SUCCESS) valid[nv++] = i;
+      for (int i = 0; i < found; ++i) {
+        if (res[i].state != HIPBLAS_STATUS_SUCCESS) continue;
+        size_t need = 0;
+        if (hipblaslt_ext::matmulIsAlgoSupported(h, plan->ds.op, &alpha, plan->ds.a, plan->ds.b, &beta, plan->ds.d,
+                                                 plan->ds.d, res[i].algo, need) != HIPBLAS_STATUS_SUCCESS ||
+            need > kWorkspace)
+          continue;  // screened out: never launched
+        plan->cand.push_back(res[i].algo);
+      }
+    const int nv = (int)plan->cand.size();
     plan->ok = nv > 0;
     plan->candidates = nv;
-    if (plan->ok) plan->algo = res[valid[0]].algo;
+    plan->cand_us.assign(nv, -1.f);
+    if (plan->ok) plan->algo = plan->cand[0];
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(stream, &cs);
     if (nv > 1 && cs == hipStreamCaptureStatusNone) {
@@ -187,7 +212,7 @@ bool lt_run(const Problem& p, const void* a, const void* b, void* d, const void*
       (void)hipEventCreate(&e1);
       float best = 1e30f;
       for (int j = 0; j < nv; ++j) {
-        const hipblasLtMatmulAlgo_t* al = &res[valid[j]].algo;
+        const hipblasLtMatmulAlgo_t* al = &plan->cand[j];
         if (hipblasLtMatmul(h, plan->ds.op, &alpha, a, plan->ds.a, b, plan->ds.b, &beta, d, plan->ds.d, d, plan->ds.d,
                             al, wsp, kWorkspace, stream) != HIPBLAS_STATUS_SUCCESS)
           continue;  // warm-up; a candidate that fails to launch is skipped
@@ -199,9 +224,11 @@ bool lt_run(const Problem& p, const void* a, const void* b, void* d, const void*
         (void)hipEventSynchronize(e1);
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, e0, e1);
+        plan->cand_us[j] = ms * 1000.f / 3.f;
         if (ms < best) {
           best = ms;
           plan->algo = *al;
+          plan->choice = j;
         }
       }
       plan->best_us = best * 1000.f / 3.f;
@@ -332,6 +359,44 @@ std::vector<std::tuple<int64_t, int64_t, int64_t, int, int, double>> lt_plan_tab
   return out;
 }
 
+int64_t lt_plan_count() {
+  std::lock_guard<std::mutex> lock(g_plan_mu);
+  return (int64_t)plans().size();
+}
+
+// Rank-consistent picks: every planned problem as its full key
+// [m, n, k, lda, ldb, ldd, ta, tb, type, epilogue, candidates, choice], sorted (so the list is the
+// same on every rank that planned the same problems) ...
+std::vector<std::vector<int64_t>> lt_plan_choices() {
+  std::lock_guard<std::mutex> lock(g_plan_mu);
+  std::vector<std::vector<int64_t>> out;
+  for (const auto& kv : plans()) {
+    const Problem& p = kv.first;
+    out.push_back({p.m, p.n, p.k, p.lda, p.ldb, p.ldd, (int64_t)p.ta, (int64_t)p.tb, (int64_t)p.type,
+                   (int64_t)p.epi, (int64_t)kv.second->candidates, (int64_t)kv.second->choice});
+  }
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
+// ... and the setter: take candidate `choice` for the problem with this key on `device` (the list
+// of screened candidates is the same on every rank: same library, same problem, same heuristic).
+// Returns false when the problem is not planned here or the candidate count differs.
+bool lt_set_plan_choice(std::vector<int64_t> key, int64_t device) {
+  TORCH_CHECK(key.size() == 12, "set_plan_choice: key must be one plan_choices() row");
+  std::lock_guard<std::mutex> lock(g_plan_mu);
+  Problem p{key[0], key[1], key[2], key[3], key[4], key[5], key[6] != 0, key[7] != 0, (hipDataType)key[8],
+            (hipblasLtEpilogue_t)key[9], (int)device};
+  auto it = plans().find(p);
+  if (it == plans().end()) return false;
+  Plan& pl = *it->second;
+  if ((int64_t)pl.cand.size() != key[10] || key[11] < 0 || key[11] >= (int64_t)pl.cand.size()) return false;
+  pl.choice = (int)key[11];
+  pl.algo = pl.cand[pl.choice];
+  pl.best_us = pl.cand_us[pl.choice];
+  return true;
+}
+
 }  // namespace
 
 void bind_lt(pybind11::module_& root) {
@@ -345,6 +410,9 @@ void bind_lt(pybind11::module_& root) {
         pybind11::arg("trans_b") = false);
   m.def("clear_cache", &lt_clear_cache);
   m.def("plan_table", &lt_plan_table);
+  m.def("plan_choices", &lt_plan_choices);
+  m.def("plan_count", &lt_plan_count);
+  m.def("set_plan_choice", &lt_set_plan_choice, pybind11::arg("key"), pybind11::arg("device"));
   m.attr("EPI_NONE") = 0;
   m.attr("EPI_BIAS") = 1;
   m.attr("EPI_GELU_AUX_BIAS") = 2;

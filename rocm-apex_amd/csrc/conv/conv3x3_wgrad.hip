@@ -407,8 +407,24 @@ void conv_hwgrad(const ConvTapArgs& a, const void* dy, void* dw_out, int out_dty
   dispatch_16(a.dtype, [&](auto tag) {
     using T = typename decltype(tag)::type;
     auto go = [&](auto kern, size_t lds) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds);
+      // the LDS opt-in once per kernel instance (a per-launch attribute call is host time on
+      // every step of an eager training loop)
+      static thread_local const void* done[16] = {};
+      const void* fp = reinterpret_cast<const void*>(kern);
+      bool seen = false;
+      for (const void*& d : done) {
+        if (d == fp) {
+          seen = true;
+          break;
+        }
+        if (!d) {
+          (void)hipFuncSetAttribute(fp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+          d = fp;
+          seen = true;
+          break;
+        }
+      }
+      if (!seen) (void)hipFuncSetAttribute(fp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(kern, dim3(grid), dim3(hwg::NT), lds, s, p);
     };
 #define HWG_CASE(TK_, HSL_, HC_)                                                   \

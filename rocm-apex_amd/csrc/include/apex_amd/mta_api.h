@@ -88,11 +88,14 @@ void mt_lamb_stage2(const MtaMeta& m, int u_t, int p_t, int out_t, int* noop, co
 // Legacy two-kernel LAMB (reference csrc/multi_tensor_lamb_stage_1.cu / _2.cu)
 void mt_lamb_legacy_stage1(const MtaMeta& m, int g_t, int p_t, int* noop, const float* per_tensor_decay,
                            float beta1, float beta2, float beta3, float bc1, float bc2, float eps,
-                           const float* global_grad_norm, float max_global_grad_norm, const Launch& L);
+                           const float* global_grad_norm, float max_global_grad_norm, const Launch& L,
+                           const float* step_dev = nullptr, int bias_correction = 1);
 // lists p, update [, model out (16-bit or fp8 copy of the updated p)]
+// step_dev / lr_dev non-null: capturable form — skipped entirely while *noop != 0, bias
+// corrections from the device step count, learning rate read on the device
 void mt_lamb_legacy_stage2(const MtaMeta& m, int p_t, int u_t, int out_t, int* noop,
                            const float* per_tensor_param_norm, const float* per_tensor_update_norm, float lr,
-                           float weight_decay, bool use_nvlamb, const Launch& L);
+                           float weight_decay, bool use_nvlamb, const Launch& L, const float* lr_dev = nullptr);
 
 // Dynamic loss-scale update, fully on device (sync-free amp).  state = {scale, inv_scale_used,
 // unskipped, skipped_total}; skip_flag <- dynamic && overflow.

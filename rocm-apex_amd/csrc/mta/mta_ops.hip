@@ -6,6 +6,8 @@
 #include <cstring>
 
 #include "apex_amd/mta_api.h"
+
+#include <type_traits>
 #include "apex_amd/dispatch.h"
 
 namespace apex_amd {
@@ -652,16 +654,29 @@ void mt_lamb_stage2(const MtaMeta& m, int u_t, int p_t, int out_t, int* noop, co
 // Legacy LAMB pair (per-tensor decay, reference csrc/multi_tensor_lamb_stage_1.cu:17-151 and
 // csrc/multi_tensor_lamb_stage_2.cu:20-125).  Lists stage1: g, p, m, v, update.  stage2: p, update.
 // ---------------------------------------------------------------------------------------------
+// DEV: the capturable form (DistributedFusedLAMB's sync-free step) — the whole launch is a no-op
+// when *noop (the device skip flag) is set, and the bias corrections come from the device step
+// counter (reference apex/contrib/optimizers/distributed_fused_lamb.py:702-712 keeps is_finite
+// and _step on the device the same way)
+template <bool DEV>
 struct LambLegacy1Op : MtaOpBase {
   static constexpr unsigned kRead = 0b01111, kWrite = 0b11100;
-  static constexpr bool kSkipOnNoop = false;
+  static constexpr bool kSkipOnNoop = DEV;
   const float* decay;
   float beta1, beta2, beta3, bc1, bc2, eps, max_norm;
   const float* gnorm;
-  struct TS { float clip, decay; };
+  const float* step;  // DEV: device step count (after this step's increment)
+  int bias_correction;
+  struct TS { float clip, decay, bc1, bc2; };
   __device__ __forceinline__ TS tensor_state(int t) const {
     const float gn = *gnorm;
-    return {(gn > max_norm) ? gn / max_norm : 1.f, decay[t]};
+    float b1 = bc1, b2 = bc2;
+    if constexpr (DEV) {
+      const float st = *step;
+      b1 = bias_correction ? 1.f - powf(beta1, st) : 1.f;
+      b2 = bias_correction ? 1.f - powf(beta2, st) : 1.f;
+    }
+    return {(gn > max_norm) ? gn / max_norm : 1.f, decay[t], b1, b2};
   }
   template <int N>
   __device__ __forceinline__ void apply(float (&r)[5][N], const TS& s, bool&, float*) const {
@@ -670,7 +685,7 @@ struct LambLegacy1Op : MtaOpBase {
       const float sg = r[0][k] / s.clip;
       const float mm = r[2][k] * beta1 + beta3 * sg;
       const float vv = r[3][k] * beta2 + (1.f - beta2) * sg * sg;
-      r[4][k] = (mm / bc1) / (sqrtf(vv / bc2) + eps) + s.decay * r[1][k];
+      r[4][k] = (mm / s.bc1) / (sqrtf(vv / s.bc2) + eps) + s.decay * r[1][k];
       r[2][k] = mm;
       r[3][k] = vv;
     }
@@ -679,43 +694,58 @@ struct LambLegacy1Op : MtaOpBase {
 
 void mt_lamb_legacy_stage1(const MtaMeta& m, int g_t, int p_t, int* noop, const float* per_tensor_decay,
                            float beta1, float beta2, float beta3, float bc1, float bc2, float eps,
-                           const float* global_grad_norm, float max_global_grad_norm, const Launch& L) {
-  LambLegacy1Op op;
-  op.decay = per_tensor_decay;
-  op.beta1 = beta1;
-  op.beta2 = beta2;
-  op.beta3 = beta3;
-  op.bc1 = bc1;
-  op.bc2 = bc2;
-  op.eps = eps;
-  op.gnorm = global_grad_norm;
-  op.max_norm = max_global_grad_norm;
+                           const float* global_grad_norm, float max_global_grad_norm, const Launch& L,
+                           const float* step_dev, int bias_correction) {
+  auto fill = [&](auto& op) {
+    op.decay = per_tensor_decay;
+    op.beta1 = beta1;
+    op.beta2 = beta2;
+    op.beta3 = beta3;
+    op.bc1 = bc1;
+    op.bc2 = bc2;
+    op.eps = eps;
+    op.gnorm = global_grad_norm;
+    op.max_norm = max_global_grad_norm;
+    op.step = step_dev;
+    op.bias_correction = bias_correction;
+  };
   const int grid = mta_grid(m.nchunks, L.max_blocks);
   dispatch_float(g_t, [&](auto tg) {
     dispatch_float(p_t, [&](auto tp) {
       using TG = typename decltype(tg)::type;
       using TP = typename decltype(tp)::type;
-      mta_elementwise_kernel<LambLegacy1Op, TG, TP, TP, TP, TP><<<grid, kMtaBlock, 0, L.stream>>>(m, noop, op);
+      if (step_dev) {
+        LambLegacy1Op<true> op;
+        fill(op);
+        mta_elementwise_kernel<LambLegacy1Op<true>, TG, TP, TP, TP, TP><<<grid, kMtaBlock, 0, L.stream>>>(m, noop, op);
+      } else {
+        LambLegacy1Op<false> op;
+        fill(op);
+        mta_elementwise_kernel<LambLegacy1Op<false>, TG, TP, TP, TP, TP><<<grid, kMtaBlock, 0, L.stream>>>(m, noop, op);
+      }
     }, "multi_tensor_lamb_stage1(param)");
   }, "multi_tensor_lamb_stage1(grad)");
   check_launch("multi_tensor_lamb_stage1_cuda");
 }
 
-// D == 3: the updated master is also written to a model-dtype (16-bit or fp8) copy
-template <int D>
+// D == 3: the updated master is also written to a model-dtype (16-bit or fp8) copy.  DEV: skip-
+// gated launch (kSkipOnNoop) with the learning rate read from the device
+template <int D, bool DEV>
 struct LambLegacy2Op : MtaOpBase {
   static constexpr unsigned kRead = 0b011, kWrite = (D == 3) ? 0b101 : 0b001;
-  static constexpr bool kSkipOnNoop = false;
+  static constexpr bool kSkipOnNoop = DEV;
   const float* pn;
   const float* un;
+  const float* lr_dev;
   float lr, wd;
   bool nv;
   struct TS { float ratio; };
   __device__ __forceinline__ TS tensor_state(int t) const {
-    float ratio = lr;
+    const float l = DEV ? *lr_dev : lr;
+    float ratio = l;
     if (nv || wd != 0.f) {
       const float a = pn[t], b = un[t];
-      ratio = (a != 0.f && b != 0.f) ? lr * (a / b) : lr;
+      ratio = (a != 0.f && b != 0.f) ? l * (a / b) : l;
     }
     return {ratio};
   }
@@ -731,33 +761,39 @@ struct LambLegacy2Op : MtaOpBase {
 
 void mt_lamb_legacy_stage2(const MtaMeta& m, int p_t, int u_t, int out_t, int* noop,
                            const float* per_tensor_param_norm, const float* per_tensor_update_norm, float lr,
-                           float weight_decay, bool use_nvlamb, const Launch& L) {
+                           float weight_decay, bool use_nvlamb, const Launch& L, const float* lr_dev) {
   auto fill = [&](auto& op) {
     op.pn = per_tensor_param_norm;
     op.un = per_tensor_update_norm;
     op.lr = lr;
+    op.lr_dev = lr_dev;
     op.wd = weight_decay;
     op.nv = use_nvlamb;
   };
   const int grid = mta_grid(m.nchunks, L.max_blocks);
-  dispatch_float(p_t, [&](auto tp) {
-    dispatch_float(u_t, [&](auto tu) {
-      using TP = typename decltype(tp)::type;
-      using TU = typename decltype(tu)::type;
-      if (out_t < 0) {
-        LambLegacy2Op<2> op;
-        fill(op);
-        mta_elementwise_kernel<LambLegacy2Op<2>, TP, TU><<<grid, kMtaBlock, 0, L.stream>>>(m, noop, op);
-      } else {
-        dispatch_model_out(out_t, [&](auto to) {
-          using TO = typename decltype(to)::type;
-          LambLegacy2Op<3> op;
+  auto run = [&](auto dev_tag) {
+    constexpr bool DEV = decltype(dev_tag)::value;
+    dispatch_float(p_t, [&](auto tp) {
+      dispatch_float(u_t, [&](auto tu) {
+        using TP = typename decltype(tp)::type;
+        using TU = typename decltype(tu)::type;
+        if (out_t < 0) {
+          LambLegacy2Op<2, DEV> op;
           fill(op);
-          mta_elementwise_kernel<LambLegacy2Op<3>, TP, TU, TO><<<grid, kMtaBlock, 0, L.stream>>>(m, noop, op);
-        }, "multi_tensor_lamb_stage2(model out)");
-      }
-    }, "multi_tensor_lamb_stage2(update)");
-  }, "multi_tensor_lamb_stage2(param)");
+          mta_elementwise_kernel<LambLegacy2Op<2, DEV>, TP, TU><<<grid, kMtaBlock, 0, L.stream>>>(m, noop, op);
+        } else {
+          dispatch_model_out(out_t, [&](auto to) {
+            using TO = typename decltype(to)::type;
+            LambLegacy2Op<3, DEV> op;
+            fill(op);
+            mta_elementwise_kernel<LambLegacy2Op<3, DEV>, TP, TU, TO><<<grid, kMtaBlock, 0, L.stream>>>(m, noop, op);
+          }, "multi_tensor_lamb_stage2(model out)");
+        }
+      }, "multi_tensor_lamb_stage2(update)");
+    }, "multi_tensor_lamb_stage2(param)");
+  };
+  if (lr_dev) run(std::true_type{});
+  else run(std::false_type{});
   check_launch("multi_tensor_lamb_stage2_cuda");
 }
 

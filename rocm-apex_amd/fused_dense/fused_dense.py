@@ -98,6 +98,48 @@ def _lt(*tensors):
     return _native.submodule("lt_gemm")
 
 
+_LT_SYNCED = {}
+
+
+def sync_lt_plans(group=None, src=0):
+    """Make every rank of ``group`` use group-rank ``src``'s hipBLASLt algorithm picks.
+
+    The library route times its top candidates per problem in each process (lt_epilogue.cpp
+    lt_run), so two tensor-parallel ranks could run different kernels for the same GEMM and
+    produce bitwise-different partial sums.  This broadcasts ``src``'s (problem, pick) table and
+    applies it (the screened candidate lists are identical on every rank: same library, same
+    problem).  Returns the number of picks applied here.  Reference counterpart: cuBLASLt's
+    single heuristic answer (csrc/fused_dense_cuda.cu:298-299, requestedAlgoCount = 1)."""
+    import torch.distributed as dist
+
+    lt = _native.submodule("lt_gemm")
+    if lt is None or not hasattr(lt, "plan_choices") or not (dist.is_available() and dist.is_initialized()):
+        return 0
+    if dist.get_world_size(group) <= 1:
+        return 0
+    obj = [lt.plan_choices() if dist.get_rank(group) == src else None]
+    dist.broadcast_object_list(obj, src=dist.get_global_rank(group, src) if group is not None else src, group=group)
+    dev = torch.cuda.current_device() if torch.cuda.is_available() else 0
+    return sum(1 for key in obj[0] if lt.set_plan_choice(list(key), dev))
+
+
+def maybe_sync_lt_plans(group):
+    """sync_lt_plans(group) whenever this process planned new hipBLASLt problems since the last
+    sync for ``group`` (every rank of a tensor-parallel group plans the same problems at the same
+    calls, so all of them enter the collective together)."""
+    import torch.distributed as dist
+
+    lt = _native.submodule("lt_gemm")
+    if lt is None or not hasattr(lt, "plan_count") or not (dist.is_available() and dist.is_initialized()):
+        return
+    if dist.get_world_size(group) <= 1:
+        return
+    n = lt.plan_count()
+    if _LT_SYNCED.get(id(group)) != n:
+        sync_lt_plans(group)
+        _LT_SYNCED[id(group)] = n
+
+
 def route_table():
     """{(op, M, N, K, dtype): 'native' | 'library'} decided so far in this process."""
     return {k: ("native" if v else "library") for k, v in _ROUTES.items()}

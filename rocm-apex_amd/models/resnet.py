@@ -112,7 +112,11 @@ class Bottleneck(nn.Module):
     def forward_linked(self, x, link_in, nxt=None):
         """Fused-node forward that chains with its neighbours (``ops.bottleneck_bn.BlockLink``):
         returns ``(out, link_out)``; falls back to ``forward`` (and no link) off the node path.
-        ``nxt``: the block that consumes the output (it may take over the output pass)."""
+        ``nxt``: the block that consumes the output (it may take over the output pass).
+
+        Only ``run_linked`` may call this: with a deferring ``link_out`` the returned tensor is
+        EMPTY until ``nxt``'s conv1 (or ``BlockLink.materialize``) writes it, and ``run_linked``
+        is what guarantees one of the two runs before anything else reads it."""
         from ..ops import bottleneck_bn
 
         if self.fused_bn and not isinstance(x, tuple) and self.training and bottleneck_bn.block_supported(self, x):
@@ -167,6 +171,8 @@ def run_linked(blocks, x):
             x, link = blk(x), None
     if link is not None:
         link.materialize()
+    # the hand-off contract: no block output is left deferred (uninitialised) once the walk ends
+    assert link is None or link.pend is None, "run_linked: a deferred block output was never computed"
     return x
 
 

@@ -22,6 +22,7 @@ Everything else (CPU, autocast, other layouts / dtypes, odd channel counts) is p
 Reference capability: the fused 1x1 convolutions of apex/contrib/bottleneck (cudnn-frontend
 graphs, ``apex/contrib/csrc/bottleneck/bottleneck.cpp``) — here the GEMM is our own MFMA kernel.
 """
+import functools
 import os
 
 import torch
@@ -291,6 +292,7 @@ def conv_tap_wgrad(gy, x, w_shape, stride, pad, out_dtype):
     return dw.permute(0, 3, 1, 2)  # [K, C, R, S] in channels_last memory
 
 
+@functools.lru_cache(maxsize=None)
 def _halo_wgrad(cin, cout, h, w):
     if not _HALO_WGRAD:
         return False
@@ -300,6 +302,7 @@ def _halo_wgrad(cin, cout, h, w):
     return bool(ext.halo_wgrad_supported(1, h, w, cin, cout))
 
 
+@functools.lru_cache(maxsize=None)
 def tap_route(cin, cout, k, stride, h, w=None):
     """(fwd, dgrad, wgrad) through the native kernels for this shape, from the per-shape A/B
     against MIOpen on MI355X (ResNet-50 bs 256 bf16; r04: profiles/conv_cfg_sweep_r04.jsonl,

@@ -353,6 +353,35 @@ def multi_tensor_lamb_stage2_cuda(chunk_size, noop, tl, per_tensor_param_norm, p
             o.copy_(p)
 
 
+def multi_tensor_lamb_stage1_capturable(chunk_size, skip, tl, per_tensor_decay, step, bias_correction, beta1, beta2,
+                                        epsilon, global_grad_norm, max_global_grad_norm, beta3):
+    """Skip-gated stage 1 with the bias corrections from the device step count (no-op while
+    ``skip`` is set)."""
+    if int(skip.reshape(-1)[0]) != 0:
+        return
+    st = float(step.reshape(-1)[0])
+    bc1 = (1 - beta1 ** st) if bias_correction else 1.0
+    bc2 = (1 - beta2 ** st) if bias_correction else 1.0
+    gn = float(global_grad_norm.reshape(-1)[0])
+    clip = gn / max_global_grad_norm if gn > max_global_grad_norm else 1.0
+    for i, (g, p, m, v, u) in enumerate(zip(*tl)):
+        sg = _f(g) / clip
+        mf = _f(m) * beta1 + beta3 * sg
+        vf = _f(v) * beta2 + (1 - beta2) * sg * sg
+        u.copy_((mf / bc1) / ((vf / bc2).sqrt() + epsilon) + float(per_tensor_decay[i]) * _f(p))
+        m.copy_(mf)
+        v.copy_(vf)
+
+
+def multi_tensor_lamb_stage2_capturable(chunk_size, skip, tl, per_tensor_param_norm, per_tensor_update_norm, lr,
+                                        weight_decay, use_nvlamb):
+    """Skip-gated stage 2 with a device learning rate."""
+    if int(skip.reshape(-1)[0]) != 0:
+        return
+    multi_tensor_lamb_stage2_cuda(chunk_size, skip, tl, per_tensor_param_norm, per_tensor_update_norm,
+                                  float(lr.reshape(-1)[0]), weight_decay, use_nvlamb)
+
+
 def multi_tensor_cast(chunk_size, noop, tl):
     for x, y in zip(tl[0], tl[1]):
         y.copy_(x)

@@ -73,8 +73,10 @@ def stem_supported(conv, bn, pool, x):
             and _pair(pool.padding) == (1, 1) and _pair(getattr(pool, "dilation", 1)) == (1, 1)
             and not getattr(pool, "ceil_mode", False) and not getattr(pool, "return_indices", False)):
         return False
-    return not any(getattr(mod, attr) for mod in (conv, bn, pool)
-                   for attr in ("_forward_hooks", "_forward_pre_hooks", "_backward_hooks"))
+    if x.dtype != w.dtype:  # the module path would raise on the mismatch; do not cast silently
+        return False
+    return not any(getattr(mod, attr, None) for mod in (conv, bn, pool)
+                   for attr in ("_forward_hooks", "_forward_pre_hooks", "_backward_hooks", "_backward_pre_hooks"))
 
 
 def stem_forward(conv, bn, pool, x):

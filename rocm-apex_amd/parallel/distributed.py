@@ -33,6 +33,8 @@ import torch
 import torch.distributed as dist
 from torch.nn.modules import Module
 
+from . import comm_timing
+
 
 def _world(group=None):
     return dist.get_world_size(group) if dist.is_initialized() else 1
@@ -386,12 +388,15 @@ class DistributedDataParallel(Module):
                             v.copy_(p.grad)
                             p.grad = v
                     b.ready = len(b.params)
-            for b in self._buckets:
-                if not b.fired:
-                    self._allreduce_bucket(b)
-            for b in self._buckets:
-                if b.work is not None:
-                    self._finish_bucket(b)
+            # exposed communication: from here (every backward kernel is enqueued) to the last
+            # bucket's completion on the compute stream (parallel.comm_timing, bench JSON)
+            with comm_timing.span("allreduce_exposed", self._buckets[0].buffer.device if self._buckets else None):
+                for b in self._buckets:
+                    if not b.fired:
+                        self._allreduce_bucket(b)
+                for b in self._buckets:
+                    if b.work is not None:
+                        self._finish_bucket(b)
         finally:
             for b in self._buckets:
                 b.ready = 0

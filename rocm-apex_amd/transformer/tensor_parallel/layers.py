@@ -88,6 +88,18 @@ def _initialize_affine_weight_cpu(weight, output_size, input_size, per_partition
     return None
 
 
+def _sync_lt_picks():
+    """Rank 0's hipBLASLt picks for the tensor-parallel group (fused_dense.maybe_sync_lt_plans),
+    when a group exists."""
+    from .. import parallel_state as ps
+
+    if ps._TENSOR_MODEL_PARALLEL_GROUP is None:
+        return
+    from ...fused_dense.fused_dense import maybe_sync_lt_plans
+
+    maybe_sync_lt_plans(ps._TENSOR_MODEL_PARALLEL_GROUP)
+
+
 def _linear(x, weight, bias):
     """y = x W^T + b on fused_dense's route: the hipBLASLt bias-epilogue GEMM with per-shape timed
     plans by default (APEX_AMD_DENSE_ROUTE=lt: 87-97 vs 124 us for the native kernel at the GPT-2
@@ -101,7 +113,9 @@ def _linear(x, weight, bias):
     if fd is not None and fd.fused_linear_available(x, weight, bias) and route != "torch":
         if route == "native" or (not route and fd.route_mode() == "native"):
             return fd.linear_bias_forward(x, weight, bias)
-        return fd._lib_dense_fwd(x, weight, bias)
+        y = fd._lib_dense_fwd(x, weight, bias)
+        _sync_lt_picks()  # one algorithm per GEMM across the tensor-parallel group
+        return y
     if bias is not None and x.dim() >= 2:
         return torch.addmm(bias, x.reshape(-1, x.shape[-1]), weight.t()).view(x.shape[:-1] + (weight.shape[0],))
     out = torch.matmul(x, weight.t())
@@ -119,7 +133,9 @@ def _wgrad(go2, ti2):
     if go2.is_cuda:
         from ...fused_dense.fused_dense import wgrad_gemm
 
-        return wgrad_gemm(go2, ti2)
+        dw = wgrad_gemm(go2, ti2)
+        _sync_lt_picks()
+        return dw
     return go2.t().matmul(ti2)
 
 

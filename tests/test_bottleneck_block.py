@@ -3,6 +3,7 @@ epilogues, bn2 apply+ReLU as conv3's operand prologue, one gradient out) against
 PyTorch bottleneck with the same weights: forward output, input gradient, every weight / BN
 parameter gradient and the running statistics."""
 import copy
+import statistics
 
 import pytest
 import torch
@@ -207,8 +208,8 @@ def test_gpu_fused_bottleneck_resnet50_step_matches_module_path(force_native, mo
     assert fc1 <= 1.5 * fc2 + 0.02, (fc1, fc2)
 
 
-def _chain(bn_group=1, peer=True):
-    """A 3-block stage-1 chain (downsampling block + 2 identity blocks), fused BN, bf16 convs."""
+def _chain(bn_group=1, peer=True, dtype=torch.bfloat16):
+    """A 3-block stage-1 chain (downsampling block + 2 identity blocks), fused BN, 16-bit convs."""
     import torch.nn as nn
 
     from apex.contrib.groupbn import BatchNorm2d_NHWC
@@ -223,7 +224,7 @@ def _chain(bn_group=1, peer=True):
     chain = nn.ModuleList(blocks)
     for m in chain.modules():
         if isinstance(m, nn.Conv2d):
-            m.to(torch.bfloat16)
+            m.to(dtype)
         if isinstance(m, BatchNorm2d_NHWC):
             with torch.no_grad():
                 m.weight.uniform_(0.5, 1.5)
@@ -386,3 +387,81 @@ def test_gpu_resnet50_syncbn_keeps_the_16_nodes():
     from tests._dist_utils import run_multiprocess
 
     run_multiprocess(_sync_resnet_worker, 2, (), timeout=180)
+
+
+def _chain_f64_reference(chain, x, gy):
+    """The chain's module path in float64 on the CPU (the groupbn modules run their torch
+    reference there): output, input gradient and parameter gradients."""
+    ref = copy.deepcopy(chain).cpu().double().train()
+    xi = x.detach().cpu().double().requires_grad_(True)
+    y = xi
+    for blk in ref:
+        y = blk(y)
+    if isinstance(y, tuple):
+        y = y[0]
+    y.backward(gy.detach().cpu().double())
+    return y.detach(), xi.grad, {n: p.grad for n, p in ref.named_parameters()}
+
+
+def _arm_distances(dtype, seed=3):
+    torch.manual_seed(seed)
+    base = _chain(dtype=dtype).cuda().to(memory_format=torch.channels_last).train()
+    x = torch.randn(4, 64, 14, 14, device="cuda").to(dtype).to(memory_format=torch.channels_last)
+    gy = torch.randn(4, 256, 14, 14, device="cuda").to(dtype).to(memory_format=torch.channels_last)
+    y64, g64, p64 = _chain_f64_reference(base, x, gy)
+    out = {}
+    for arm, node, linked in (("linked", True, True), ("unlinked", True, False), ("module", False, True)):
+        c = copy.deepcopy(base)
+        y, g, pg, _ = _run_chain(c, x, gy, node, linked=linked)
+        out[arm] = dict(y=y, g=g, p=pg,
+                        dy=_rel(y.cpu().double(), y64), dg=_rel(g.cpu().double(), g64),
+                        dp=statistics.median(_rel(pg[n].cpu().double(), p64[n]) for n in p64))
+    return out
+
+
+@pytest.mark.gpu
+def test_gpu_bottleneck_chain_fp16_arm_pins_the_tolerances():
+    """the chain tolerances above (0.3 dx / 0.35 params vs the per-module
+    path) are set by bf16 rounding noise; an O(0.1) bug in a hand-off would hide under them.  With
+    fp16 operands (3 more mantissa bits) every arm's distance to a float64 reference must shrink
+    by >= 4x — a real bug does not shrink with precision — and the node arms (linked, unlinked) must
+    stay as close to float64 as the per-module path."""
+    bf, hf = _arm_distances(torch.bfloat16), _arm_distances(torch.float16)
+    for arm in ("linked", "unlinked", "module"):
+        for k in ("dy", "dg", "dp"):
+            assert hf[arm][k] * 4 <= bf[arm][k] + 1e-4, (arm, k, bf[arm][k], hf[arm][k])
+    for k in ("dg", "dp"):
+        assert hf["linked"][k] <= 2 * hf["module"][k] + 1e-3, (k, hf["linked"][k], hf["module"][k])
+        assert hf["unlinked"][k] <= 2 * hf["module"][k] + 1e-3, (k, hf["unlinked"][k], hf["module"][k])
+    # the fp16 node arms against each other: only one reduction's summation order differs
+    assert _rel(hf["linked"]["g"], hf["unlinked"]["g"]) < 5e-3
+    for prec, d in (("bf16", bf), ("fp16", hf)):
+        print(prec, {a: {k: round(d[a][k], 5) for k in ("dy", "dg", "dp")} for a in d})
+
+
+def _sync_chain_fp16_worker(rank, world):
+    """The 2-rank SyncBN chain with fp16 convs: its distance to the 1-rank full-batch node chain
+    shrinks with precision like every other arm (an exchange bug would not)."""
+    torch.cuda.set_device(0)
+    res = {}
+    for dt in (torch.bfloat16, torch.float16):
+        torch.manual_seed(3)
+        full = _chain(dtype=dt).cuda().to(memory_format=torch.channels_last).train()
+        mine = copy.deepcopy(full)
+        x = torch.randn(8, 64, 14, 14, device="cuda").to(dt).to(memory_format=torch.channels_last)
+        gy = torch.randn(8, 256, 14, 14, device="cuda").to(dt).to(memory_format=torch.channels_last)
+        yf, gf, _, _ = _run_chain(full, x, gy, True)
+        sl = slice(rank * 4, rank * 4 + 4)
+        ys, gs, _, _ = _run_chain(mine, x[sl].contiguous(memory_format=torch.channels_last),
+                                  gy[sl].contiguous(memory_format=torch.channels_last), True, world, None, True)
+        res[dt] = (_rel(ys, yf[sl]), _rel(gs, gf[sl]))
+    print(rank, res)
+    assert res[torch.float16][1] * 4 <= res[torch.bfloat16][1] + 1e-4, res
+    assert res[torch.float16][1] < 0.03, res
+
+
+@pytest.mark.gpu
+def test_gpu_bottleneck_chain_syncbn_fp16_arm():
+    from tests._dist_utils import run_multiprocess
+
+    run_multiprocess(_sync_chain_fp16_worker, 2, (), timeout=240)

@@ -321,3 +321,71 @@ def test_contrib_legacy_optimizers_with_fp16_optimizer():
                            0.01, step)
     for p, q in zip(model.parameters(), ref.parameters()):
         torch.testing.assert_close(p, q, atol=1e-5, rtol=1e-4)
+
+
+def _lamb_overflow_worker(rank, world):
+    """DistributedFusedLAMB's step is gated on the device skip flag (no host read of it): an
+    overflow on one rank leaves every rank's weights and moments untouched and does not advance
+    the device step count; the sharded checkpoint carries that count."""
+    from apex.contrib.optimizers import DistributedFusedLAMB
+
+    model = _model(2)
+    opt = DistributedFusedLAMB(model.parameters(), lr=1e-2, weight_decay=0.01, min_block_elems=128)
+    before = [p.detach().clone() for p in model.parameters()]
+    x, y = _batches(rank, 1)[0]
+    xb = x.clone()
+    if rank == 1:
+        xb[0, 0] = float("inf")
+    torch.nn.functional.mse_loss(model(xb), y).backward()
+    opt.step()
+    assert opt.has_overflow
+    for p, b in zip(model.parameters(), before):
+        assert torch.equal(p, b)
+    assert float(opt._m.abs().sum()) == 0 and float(opt._step_t) == 0.0
+    torch.nn.functional.mse_loss(model(x), y).backward()
+    opt.step()
+    assert not opt.has_overflow and float(opt._step_t) == 1.0
+    assert any(not torch.equal(p, b) for p, b in zip(model.parameters(), before))
+    sd = opt.state_dict()
+    opt2 = DistributedFusedLAMB(_model(2).parameters(), lr=1e-2, weight_decay=0.01, min_block_elems=128)
+    opt2.load_state_dict(sd)
+    assert float(opt2._step_t) == 1.0
+    torch.testing.assert_close(opt2._v, opt._v)
+
+
+def test_distributed_lamb_overflow_skip_on_device():
+    run_multiprocess(_lamb_overflow_worker, world=2)
+
+
+def _lamb_sync_free_worker(rank, world):
+    from apex.contrib.optimizers import DistributedFusedLAMB
+
+    dev = torch.device("cuda", 0)
+    model = _model(4).to(dev)
+    opt = DistributedFusedLAMB(model.parameters(), lr=1e-2, weight_decay=0.01, max_grad_norm=1.0,
+                               min_block_elems=128)
+    x, y = (t.to(dev) for t in _batches(rank, 1)[0])
+
+    def one():
+        torch.nn.functional.mse_loss(model(x), y).backward()
+        opt.step()
+
+    one()
+    one()  # work tables / buffers built
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        one()
+        one()
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    torch.cuda.synchronize()
+    assert float(opt._step_t) == 4.0
+
+
+@pytest.mark.gpu
+def test_gpu_distributed_lamb_step_makes_no_host_sync():
+    """The whole LAMB step (unscale / overflow check / grad-norm clip, stage 1, the fused
+    [2, num_params] norm all-reduce, stage 2, all-gather) runs under torch's sync debug mode set
+    to raise on any device -> host synchronization."""
+    run_multiprocess(_lamb_sync_free_worker, world=1, backend="nccl")

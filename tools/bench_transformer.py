@@ -59,7 +59,7 @@ def build(args, dev, distributed):
         opt = FusedLAMB(model.parameters(), lr=1e-4, weight_decay=0.01, max_grad_norm=1.0, materialize_master_grads=mm)
     model, opt = amp.initialize(model, opt, opt_level=args.opt_level, cast_model_type=low, verbosity=0)
     if distributed:
-        model = apex.parallel.DistributedDataParallel(model)
+        model = apex.parallel.DistributedDataParallel(model, message_size=int(getattr(args, "message_size", 1e7)))
     V = cfg["vocab"]
     tokens = torch.randint(0, V, (B, S), device=dev)
     labels = torch.randint(0, V, (B, S), device=dev)

@@ -117,6 +117,37 @@ def newest_header() -> float:
     return t
 
 
+_INCLUDE_RX = None
+
+
+def header_deps(path: str, seen=None) -> set:
+    """Transitive set of this package's headers a source includes (``#include "apex_amd/..."``
+    or a relative quote include), so a header edit rebuilds only the units that use it."""
+    global _INCLUDE_RX
+    import re
+
+    if _INCLUDE_RX is None:
+        _INCLUDE_RX = re.compile(r'^\s*#\s*include\s*"([^"]+)"', re.M)
+    seen = set() if seen is None else seen
+    try:
+        text = open(path, encoding="utf-8", errors="replace").read()
+    except OSError:
+        return seen
+    for inc in _INCLUDE_RX.findall(text):
+        for base in (os.path.join(CSRC, "include"), os.path.dirname(path)):
+            cand = os.path.normpath(os.path.join(base, inc))
+            if os.path.isfile(cand):
+                if cand not in seen:
+                    seen.add(cand)
+                    header_deps(cand, seen)
+                break
+    return seen
+
+
+def newest_dep(src: str) -> float:
+    return max([os.path.getmtime(src)] + [os.path.getmtime(h) for h in header_deps(src)])
+
+
 def obj_for(src: str, build_dir: str = BUILD) -> str:
     rel = os.path.relpath(src, CSRC).replace(os.sep, "__")
     return os.path.join(build_dir, rel + ".o")
@@ -168,7 +199,6 @@ def build(jobs_n: int | None = None, clean: bool = False, verbose: bool = False,
         shutil.rmtree(build_dir)
     os.makedirs(build_dir, exist_ok=True)
     jobs, link = compile_cmds(verbose, extensions, out, build_dir, tuple(defines))
-    hdr = newest_header()
     # module.cpp's registrations depend on which subsystem bindings exist (-D macros): rebuild it
     # whenever that set changes
     _, cpp = sources(extensions)
@@ -179,7 +209,7 @@ def build(jobs_n: int | None = None, clean: bool = False, verbose: bool = False,
     todo = []
     for src, cmd in jobs:
         o = obj_for(src, build_dir)
-        stale = not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(src), hdr)
+        stale = not os.path.exists(o) or os.path.getmtime(o) < newest_dep(src)
         if stale or (subsystems_changed and src.endswith("module.cpp")):
             todo.append((src, cmd))
     n = jobs_n or min(len(todo) or 1, max(1, (os.cpu_count() or 4)))
