@@ -4,6 +4,7 @@
 // torch channels_last tensors); weights are [K, taps, C] (k contiguous per tap).
 #include "common.h"
 #include "apex_amd/conv_api.h"
+#include "apex_amd/conv_halo.h"
 
 namespace apex_amd {
 namespace {
@@ -62,7 +63,7 @@ c10::optional<at::Tensor> tap_fprop(const at::Tensor& in, const at::Tensor& w, a
                std::vector<int64_t> dw, const c10::optional<at::Tensor>& scale,
                const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& residual, bool relu,
                const c10::optional<at::Tensor>& mask, const c10::optional<at::Tensor>& stats,
-               const c10::optional<at::Tensor>& stats_shift) {
+               const c10::optional<at::Tensor>& stats_shift, const c10::optional<at::Tensor>& pcoef) {
   ConvTapArgs a = make_args(in, w, out, oh, ow, ish, isw, osh, osw, oph, opw, dh, dw);
   auto per_channel = [&](const c10::optional<at::Tensor>& t, const char* what) -> const float* {
     if (!t.has_value()) return nullptr;
@@ -101,6 +102,16 @@ c10::optional<at::Tensor> tap_fprop(const at::Tensor& in, const at::Tensor& w, a
     if (!stats.has_value()) made = st;
   }
   TORCH_CHECK(conv_tap_supported(a), "conv tap_fprop: unsupported (C and K must be multiples of 64, bf16/fp16)");
+  if (pcoef.has_value()) {
+    // operand prologue relu(x * pcoef[c] + pcoef[C + c]) on the halo-tile kernel
+    TORCH_CHECK(pcoef->is_cuda() && pcoef->scalar_type() == at::kFloat && pcoef->is_contiguous() &&
+                    pcoef->numel() == 2 * in.size(3),
+                "conv tap_fprop: pcoef must be a contiguous fp32 [2C] tensor");
+    TORCH_CHECK(conv_hfp_supported(a), "conv tap_fprop: the BN prologue needs the halo-tile kernel's shapes "
+                "(3x3 stride 1, C % 64 == 0, K % 128 == 0, no fused epilogue)");
+    conv_hfp(a, pcoef->data_ptr<float>(), cus, cur_stream());
+    return made;
+  }
   conv_tap_fprop(a, cus, cur_stream());
   return made;
 }
@@ -549,7 +560,26 @@ void bind_conv(pybind11::module_& root) {
         pybind11::arg("scale") = pybind11::none(), pybind11::arg("bias") = pybind11::none(),
         pybind11::arg("residual") = pybind11::none(), pybind11::arg("relu") = false,
         pybind11::arg("mask") = pybind11::none(), pybind11::arg("stats") = pybind11::none(),
-        pybind11::arg("stats_shift") = pybind11::none());
+        pybind11::arg("stats_shift") = pybind11::none(), pybind11::arg("pcoef") = pybind11::none());
+  m.def("hfp_supported", [](int64_t n, int64_t h, int64_t w, int64_t c, int64_t kout) {
+    ConvTapArgs a{};
+    void* aligned = reinterpret_cast<void*>(static_cast<uintptr_t>(256));  // alignment checks only
+    a.in = a.wt = aligned;
+    a.out = aligned;
+    a.n = (int)n;
+    a.ih = a.oh = a.oht = (int)h;
+    a.iw = a.ow = a.owt = (int)w;
+    a.c = (int)c;
+    a.kout = (int)kout;
+    a.ish = a.isw = a.osh = a.osw = 1;
+    a.ntaps = 9;
+    for (int t = 0; t < 9; ++t) {
+      a.dh[t] = t / 3 - 1;
+      a.dw[t] = t % 3 - 1;
+    }
+    a.dtype = kBF16;
+    return conv_hfp_supported(a);
+  });
   m.def("wgrad", &wgrad);
   m.def("force_fprop_cfg", &conv_force_fprop_cfg);
   m.def("force_wgrad_variant", &conv_force_wgrad_variant);

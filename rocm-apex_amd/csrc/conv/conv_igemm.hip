@@ -25,6 +25,7 @@
 //   partial tile, and a reduce pass sums the partials in a fixed order (deterministic) and
 //   converts to the weight dtype.
 #include "apex_amd/conv_api.h"
+#include "apex_amd/conv_halo.h"
 #include "apex_amd/device.h"
 #include "apex_amd/dispatch.h"
 #include "apex_amd/fastdiv.h"
@@ -1175,8 +1176,13 @@ static bool use_sp(const ConvTapArgs& a) {
   return g_forced_cfg < 0 && conv_sp_default(a);
 }
 
+// the halo-tile kernel (conv3x3_halo.hip) for stride-1 3x3 at C % 64, K % 128 unless another
+// configuration is forced
+static bool use_hfp(const ConvTapArgs& a) { return g_forced_cfg < 0 && conv_hfp_default(a); }
+
 int conv_tap_stats_tiles(const ConvTapArgs& a, int cus) {
   if (use_sp(a)) return conv_sp_grid(a, cus);
+  if (use_hfp(a)) return conv_hfp_stats_rows(a, cus);
   const int bm = plan::conv_fprop_bm(fprop_cfg(a, cus));
   return (int)(((int64_t)a.n * a.oh * a.ow + bm - 1) / bm);
 }
@@ -1185,6 +1191,10 @@ void conv_tap_fprop(const ConvTapArgs& a, int cus, hipStream_t s) {
   if (!conv_tap_supported(a)) throw std::runtime_error("conv_tap_fprop: unsupported shape / dtype / alignment");
   if (use_sp(a)) {
     conv_sp_fprop(a, cus, s);
+    return;
+  }
+  if (use_hfp(a)) {
+    conv_hfp(a, nullptr, cus, s);
     return;
   }
   const conv::Geo g = conv::make_geo(a);

@@ -1,0 +1,15 @@
+// Halo-tile 3x3 stride-1 convolution (csrc/conv/conv3x3_halo.hip): C % 64 == 0, K % 128 == 0, no
+// fused epilogue but the BN statistics; optional operand prologue relu(x * pcoef[c] + pcoef[C + c])
+// (the producing batch norm + ReLU, applied to the staged input, padding kept zero).  The default
+// engine of conv_tap_fprop where it applies (APEX_AMD_CONV_HFP=0 disables).
+#pragma once
+#include "apex_amd/conv_api.h"
+
+namespace apex_amd {
+
+bool conv_hfp_supported(const ConvTapArgs& a);
+bool conv_hfp_default(const ConvTapArgs& a);
+int conv_hfp_stats_rows(const ConvTapArgs& a, int cus);  // statistics partial rows (workgroups per k-block)
+void conv_hfp(const ConvTapArgs& a, const float* pcoef, int cus, hipStream_t s);
+
+}  // namespace apex_amd

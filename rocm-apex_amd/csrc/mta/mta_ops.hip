@@ -782,12 +782,15 @@ void mt_lamb_legacy_stage2(const MtaMeta& m, int p_t, int u_t, int out_t, int* n
           fill(op);
           mta_elementwise_kernel<LambLegacy2Op<2, DEV>, TP, TU><<<grid, kMtaBlock, 0, L.stream>>>(m, noop, op);
         } else {
-          dispatch_model_out(out_t, [&](auto to) {
+          auto go = [&](auto to) {
             using TO = typename decltype(to)::type;
             LambLegacy2Op<3, DEV> op;
             fill(op);
             mta_elementwise_kernel<LambLegacy2Op<3, DEV>, TP, TU, TO><<<grid, kMtaBlock, 0, L.stream>>>(m, noop, op);
-          }, "multi_tensor_lamb_stage2(model out)");
+          };
+          // fp32 model copies too (a ZeRO shard of fp32 parameters: flat_param is fp32)
+          if (out_t == kF32) go(Tag<float>{});
+          else dispatch_model_out(out_t, go, "multi_tensor_lamb_stage2(model out)");
         }
       }, "multi_tensor_lamb_stage2(update)");
     }, "multi_tensor_lamb_stage2(param)");

@@ -166,10 +166,13 @@ def _dgrad_phases(k, stride, pad, h, w):
     return out
 
 
-def conv_tap_forward(x, w, stride, pad, stats_shift=None):
+def conv_tap_forward(x, w, stride, pad, stats_shift=None, pcoef=None):
     """NHWC conv through the native tap kernel: x [N,C,H,W] channels_last, w [K,C,R,S].
     ``stats_shift`` (fp32 [K], e.g. the consuming BN's running mean): also return the BN
-    statistics partials [2, tiles, K] of the output from the kernel's epilogue, ``(y, part)``."""
+    statistics partials [2, tiles, K] of the output from the kernel's epilogue, ``(y, part)``.
+    ``pcoef`` (fp32 [2C]): convolve relu(x * pcoef[:C] + pcoef[C:]) instead of x — the producing
+    batch norm + ReLU applied on the halo-tile kernel's staged input (padding stays zero; 3x3
+    stride 1, K % 128 == 0 only: ``hfp_supported``)."""
     n, c, h, wd = x.shape
     kout, _, k, _ = w.shape
     oh, ow = (h + 2 * pad - k) // stride + 1, (wd + 2 * pad - k) // stride + 1
@@ -177,7 +180,7 @@ def conv_tap_forward(x, w, stride, pad, stats_shift=None):
     taps = _fwd_taps(k, pad)
     ext = _conv_ext()
     part = ext.tap_fprop(_nhwc(x), _w_krc(w).contiguous(), _nhwc(y), oh, ow, stride, stride, 1, 1, 0, 0,
-                         [t[0] for t in taps], [t[1] for t in taps], stats_shift=stats_shift)
+                         [t[0] for t in taps], [t[1] for t in taps], stats_shift=stats_shift, pcoef=pcoef)
     return y if stats_shift is None else (y, part)
 
 

@@ -424,19 +424,22 @@ def test_gpu_bottleneck_chain_fp16_arm_pins_the_tolerances():
     """the chain tolerances above (0.3 dx / 0.35 params vs the per-module
     path) are set by bf16 rounding noise; an O(0.1) bug in a hand-off would hide under them.  With
     fp16 operands (3 more mantissa bits) every arm's distance to a float64 reference must shrink
-    by >= 4x — a real bug does not shrink with precision — and the node arms (linked, unlinked) must
-    stay as close to float64 as the per-module path."""
+    by >= 2.5x — a real bug does not shrink with precision — and the node arms (linked, unlinked) must
+    stay as close to float64 as the per-module path (within 2x)."""
     bf, hf = _arm_distances(torch.bfloat16), _arm_distances(torch.float16)
+    for prec, d in (("bf16", bf), ("fp16", hf)):
+        print(prec, {a: {k: round(d[a][k], 5) for k in ("dy", "dg", "dp")} for a in d})
+    # measured (r05, 1 x MI355X): every arm shrinks 3-4x from bf16 to fp16 (BN backward's mean
+    # subtraction amplifies the activations' rounding, so not the full 8x of 3 mantissa bits); a
+    # wrong hand-off or coefficient would leave an O(0.1) distance that does not shrink at all
     for arm in ("linked", "unlinked", "module"):
         for k in ("dy", "dg", "dp"):
-            assert hf[arm][k] * 4 <= bf[arm][k] + 1e-4, (arm, k, bf[arm][k], hf[arm][k])
+            assert hf[arm][k] * 2.5 <= bf[arm][k] + 1e-4, (arm, k, bf[arm][k], hf[arm][k])
     for k in ("dg", "dp"):
         assert hf["linked"][k] <= 2 * hf["module"][k] + 1e-3, (k, hf["linked"][k], hf["module"][k])
         assert hf["unlinked"][k] <= 2 * hf["module"][k] + 1e-3, (k, hf["unlinked"][k], hf["module"][k])
     # the fp16 node arms against each other: only one reduction's summation order differs
     assert _rel(hf["linked"]["g"], hf["unlinked"]["g"]) < 5e-3
-    for prec, d in (("bf16", bf), ("fp16", hf)):
-        print(prec, {a: {k: round(d[a][k], 5) for k in ("dy", "dg", "dp")} for a in d})
 
 
 def _sync_chain_fp16_worker(rank, world):
@@ -456,7 +459,9 @@ def _sync_chain_fp16_worker(rank, world):
                                   gy[sl].contiguous(memory_format=torch.channels_last), True, world, None, True)
         res[dt] = (_rel(ys, yf[sl]), _rel(gs, gf[sl]))
     print(rank, res)
-    assert res[torch.float16][1] * 4 <= res[torch.bfloat16][1] + 1e-4, res
+    # measured: 0.074-0.076 (bf16) -> 0.019-0.020 (fp16), 3.7-3.9x; an exchange bug (local count,
+    # missing sums) would not shrink
+    assert res[torch.float16][1] * 2.5 <= res[torch.bfloat16][1] + 1e-4, res
     assert res[torch.float16][1] < 0.03, res
 
 
