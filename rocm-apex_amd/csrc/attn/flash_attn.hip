@@ -75,6 +75,12 @@ __device__ __forceinline__ uint32_t drop_pair(uint32_t row, uint32_t k) {
 }
 __device__ __forceinline__ uint32_t drop_bits(uint32_t h, uint32_t k) { return (k & 1u) ? (h >> 16) : (h & 0xFFFFu); }
 __device__ __forceinline__ uint32_t drop_t16(float p) { return (uint32_t)fminf(p * 65536.f, 65536.f); }
+// 1 / keep rate of the quantised test: exactly (65536 - t16) / 65536 of the 16-bit values survive,
+// so scaling by 1 / (1 - p) would bias the expected activation by (1 - p) 65536 / (65536 - t16)
+__device__ __forceinline__ float drop_inv_keep(float p) {
+  const uint32_t t = drop_t16(p);
+  return t < 65536u ? 65536.f / (float)(65536u - t) : 0.f;
+}
 // neighbour lane's value (lanes l, l ^ 1: DPP quad_perm [1, 0, 3, 2])
 __device__ __forceinline__ uint32_t swap_pair_lane(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
@@ -265,7 +271,7 @@ __global__ void __launch_bounds__(256, (fwd_occupancy<D, MODE, QF, LO>())) fwd_k
     const float inv_scale = 1.f / a.scale;
     const bool dropout = MODE >= 1 && a.p_drop > 0.f;  // MODE 0: no dropout (compiled out)
     const uint32_t thresh = drop_t16(a.p_drop);
-    const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
+    const float inv_keep = dropout ? drop_inv_keep(a.p_drop) : 1.f;
     const uint32_t smix = seed_mix_of(a.seed, drop_offset(a));
     const uint32_t bh = (uint32_t)(b * a.h + hq);
     uint32_t drow[QF];
@@ -494,7 +500,7 @@ __global__ void __launch_bounds__(256, 1) bwd_kernel(const AttnBwdArgs ba) {
   const float c = a.scale * kLog2e;
   const bool dropout = !PLAIN && a.p_drop > 0.f;  // PLAIN: no bias, no dropout (compiled out)
   const uint32_t thresh = drop_t16(a.p_drop);
-  const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
+  const float inv_keep = dropout ? drop_inv_keep(a.p_drop) : 1.f;
   const uint32_t smix = seed_mix_of(a.seed, drop_offset(a));
   const int group = a.h / a.h_k;
   // dQ tile ownership: d-tile dtq, key part kpart of kparts (NDT * kparts == 4 waves)
@@ -756,7 +762,7 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
     const float c = a.scale * kLog2e;
     const bool dropout = MODE >= 1 && a.p_drop > 0.f;  // MODE 0: no dropout (compiled out)
     const uint32_t thresh = drop_t16(a.p_drop);
-    const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
+    const float inv_keep = dropout ? drop_inv_keep(a.p_drop) : 1.f;
     const uint32_t smix = seed_mix_of(a.seed, drop_offset(a));
     const int group = a.h / a.h_k;
     constexpr int QCH = QB * CPR, QCPT = (QCH + 255) / 256;
@@ -1005,7 +1011,7 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dq_kernel(const A
     const float c = a.scale * kLog2e;
     const bool dropout = MODE >= 1 && a.p_drop > 0.f;  // MODE 0: no dropout (compiled out)
     const uint32_t thresh = drop_t16(a.p_drop);
-    const float inv_keep = dropout ? 1.f / (1.f - a.p_drop) : 1.f;
+    const float inv_keep = dropout ? drop_inv_keep(a.p_drop) : 1.f;
     const uint32_t smix = seed_mix_of(a.seed, drop_offset(a));
     const uint32_t bh = (uint32_t)(b * a.h + hq);
     const uint32_t drow = dropout ? drop_row(smix, bh, (uint32_t)myq) : 0u;

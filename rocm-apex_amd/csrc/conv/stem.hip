@@ -360,52 +360,11 @@ struct BwdArgs {
   float* ws;              // wgrad: [G][64][224]
   Geo g;
   FastDiv div_ohw, div_ow;
-  uint32_t chunk;         // wgrad: pixels per workgroup (multiple of 64)
+  FastDiv div_q, div_qw;  // wgrad: quads per image, quads per row
+  uint32_t nq;            // wgrad: quads in the batch
+  uint32_t chunk;         // wgrad: quads per workgroup (multiple of WQ)
+  uint32_t xbytes;        // wgrad: halo'd image bytes (im2col buffer-load bound)
 };
-
-// raw loads of one (pixel, 8-channel) item's pooled-gradient windows: <= 2 x 2 windows contain a
-// stride-2 / size-3 / pad-1 pool input pixel
-struct Gather {
-  uint2 ix[4];
-  uint4 gv[4];
-  uint32_t kk;  // byte s: the window index the pixel has in window s (255: no window)
-};
-
-__device__ __forceinline__ void gather_issue(const BwdArgs& a, uint32_t nn, int yh, int yw, int c8, Gather& G) {
-  const int hh = yh + 1, ww = yw + 1;
-  const int ph_lo = hh >= 3 ? ((hh - 3) >> 1) + 1 : 0, ph_hi = min(a.g.ph - 1, hh >> 1);
-  const int pw_lo = ww >= 3 ? ((ww - 3) >> 1) + 1 : 0, pw_hi = min(a.g.pw - 1, ww >> 1);
-  G.kk = 0;
-  // every slot loads (a missing window re-reads a valid one and can never match): no branch
-  // around a load, so the compiler's vmcnt waits stay counted
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int ph = ph_lo + (s >> 1), pw = pw_lo + (s & 1);
-    const bool valid = ph <= ph_hi && pw <= pw_hi;
-    const int phc = min(ph, ph_hi), pwc = min(pw, pw_hi);
-    G.kk |= (valid ? (uint32_t)((hh - 2 * ph) * 3 + (ww - 2 * pw)) : 255u) << (8 * s);
-    const size_t o = ((size_t)(nn * a.g.ph + phc) * a.g.pw + pwc) * CO + c8 * 8;
-    G.ix[s] = *reinterpret_cast<const uint2*>(a.idx + o);
-    G.gv[s] = *reinterpret_cast<const uint4*>(a.dp + o);
-  }
-}
-
-template <typename T>
-__device__ __forceinline__ void gather_sum(const Gather& G, float (&gs)[8]) {
-#pragma unroll
-  for (int e = 0; e < 8; ++e) gs[e] = 0.f;
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const uint32_t w[2] = {G.ix[s].x, G.ix[s].y};
-    const uint32_t gw[4] = {G.gv[s].x, G.gv[s].y, G.gv[s].z, G.gv[s].w};
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const uint32_t k = (w[e >> 2] >> (8 * (e & 3))) & 0xffu;
-      const float v = to_f(T{(uint16_t)((gw[e >> 1] >> (16 * (e & 1))) & 0xffffu)});
-      gs[e] += k == ((G.kk >> (8 * s)) & 0xffu) ? v : 0.f;
-    }
-  }
-}
 
 template <typename T>
 __global__ void __launch_bounds__(256) bwd_reduce_kernel(const BwdArgs a) {
@@ -422,7 +381,7 @@ __global__ void __launch_bounds__(256) bwd_reduce_kernel(const BwdArgs a) {
   // the quad loads those 4 windows once instead of 4 per pixel.  A pixel at padded row
   // hh = 2 qh + 1 + dy sits at window row hh - 2 ph = 1 + dy - 2 sh of slot row sh (in the window only
   // for sh = 0 or dy = 1); columns alike.  Per pixel the matching windows are summed in the same
-  // (ph, pw) order as gather_sum, so its pooled gradient is bitwise the per-pixel gather's.
+  // (ph, pw) order a per-pixel gather would use.
   const uint32_t qh_n = (uint32_t)(a.g.oh + 1) >> 1, qw_n = (uint32_t)(a.g.ow + 1) >> 1;
   const uint32_t total = (uint32_t)a.g.n * qh_n * qw_n * 8u, stride = gridDim.x * 256u;
   for (uint32_t i = blockIdx.x * 256u + tid; i < total; i += stride) {
@@ -491,123 +450,199 @@ __global__ void __launch_bounds__(256) bwd_reduce_kernel(const BwdArgs a) {
 }
 
 // ---- backward: weight gradient with the BN-backward prologue ---------------------------------
-constexpr int WPX = 128;          // pixels per step
-constexpr int DSTR = CO + 32;     // dX image row stride (elements): rows 192 B apart in bank space
-constexpr int ISTR = KT + 64;     // im2col image row stride: rows 64 B apart in bank space
-constexpr int WG_LDS = WPX * (DSTR + ISTR) * 2;
-constexpr int WG_NI = WPX * 8 / 512;          // dX items (pixel, 8 channels) per thread per step
-constexpr int WG_NP = (WPX * 7 + 511) / 512;  // im2col (pixel, kernel row) pairs per thread per step
+constexpr int WPX = 128;            // pixels per step (the GEMM k dimension)
+constexpr int WQ = WPX / 4;         // 2 x 2 pixel quads per step
+constexpr int DSTR = CO + 32;       // dX image row stride (elements): rows 192 B apart in bank space
+constexpr int IL_EL = 7 * WPX * KROW;  // im2col image [kernel row][pixel][32] (elements)
+static_assert((WPX * DSTR + 2 * IL_EL) * 2 + 5 * CO * 4 <= 160 * 1024, "stem wgrad LDS");
 
-// All 8 waves stage and all run MFMAs.  A step is 128 pixels: its loads are issued BEFORE the
-// previous step's MFMAs (they land under them), committed to the single LDS stage after an
-// LDS-only barrier, and consumed after a second one.  One memory latency per 128 pixels instead of
-// one per 32: the prefetch that a register double-buffer is meant to provide does not survive the
-// compiler's loop rotation here (it copies in-flight load destinations and waits on them).
+__device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint16_t* lds_dst) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_dst, 16, (int)voff,
+                                           (int)soff, 0, 0);
+}
+
+// A step is 32 quads of conv-output pixels (2 x 2, as in bwd_reduce_kernel) = 128 pixels: pixel row
+// 4 q + d of the step is pixel d (row-major in the quad) of quad q, in the dX image and in the
+// im2col image alike (the GEMM k order is free).
+//  * dX: one (quad, 4 channels) item per lane loads the quad's 4 pool windows and 4 BN inputs once
+//    (2 loads per pixel instead of 5 for a per-pixel gather) into registers, two steps ahead (two
+//    register sets); the item is committed (pool gather, ReLU mask, dX = A g + B y + K) to the
+//    single dX stage after the previous step's MFMAs.
+//  * im2col: kernel row r of a pixel is 64 contiguous bytes of the halo'd NHWC4 image, so it goes
+//    global -> LDS by buffer_load ... lds (lane-linear 16 B: wave w stages pixels 16 w .. 16 w + 15,
+//    4 lanes each, all 7 rows; [r][pixel][32] rows are 64 B apart, conflict-free for the
+//    transposed fragment reads) into a 2-stage ring, with no registers in flight.
+// The im2col DMA of step s + 1 is issued after step s's commit barrier and lands under its MFMAs.
+// Waves 0-6 run the MFMAs (k-tile u = wave = kernel row u, both 32-channel tiles).
 // MODE (diagnostics, APEX_AMD_STEM_WG_MODE; 0 in production): bit 0 skips the pooled-gradient
-// gather, bit 1 the MFMAs, bit 2 the im2col loads
+// gather loads, bit 1 the MFMAs, bit 2 the im2col loads
 template <typename T, int MODE>
 __global__ void __launch_bounds__(512, 1) wgrad_kernel(const BwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  // three distinct LDS objects: the compiler's alias analysis then sees that the MFMA reads of one
+  // im2col stage do not depend on the DMA in flight into the other, and does not wait for it
+  __shared__ __attribute__((aligned(16))) uint16_t dl[WPX * DSTR];
+  __shared__ __attribute__((aligned(16))) uint16_t il0[IL_EL];
+  __shared__ __attribute__((aligned(16))) uint16_t il1[IL_EL];
   __shared__ __attribute__((aligned(16))) float cf[5 * CO];  // forward scale | shift, backward A | B | K
-  uint16_t* dl = lds;
-  uint16_t* il = lds + WPX * DSTR;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, pl = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, pl = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const Geo& g = a.g;
-  const uint32_t p_begin = blockIdx.x * a.chunk;
-  const uint32_t p_end = min(p_begin + a.chunk, g.m);
-  const int steps = p_begin < p_end ? (int)((p_end - p_begin + WPX - 1) / WPX) : 0;
+  const uint32_t q_begin = blockIdx.x * a.chunk;
+  const uint32_t q_end = min(q_begin + a.chunk, a.nq);
+  const int steps = q_begin < q_end ? (int)((q_end - q_begin + WQ - 1) / WQ) : 0;
   for (int i = tid; i < 5 * CO; i += 512) cf[i] = i < 2 * CO ? a.coef[i] : a.cb[i - 2 * CO];
-  const int c8 = tid & 7;
-  const int rot = (tid >> 1) & 3;  // = ((tid + 512 * i) >> 1) & 3 for every im2col item i
-  const size_t rowstep = (size_t)g.wp * 4;
+  const int c4 = tid & 15, ql = tid >> 4;  // dX item: quad ql of the step, channels 4 c4 ..
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.xp, 0, __builtin_amdgcn_readfirstlane(a.xbytes), 0x00020000);
+  const uint32_t rowbytes = __builtin_amdgcn_readfirstlane((uint32_t)g.wp * 8);
 
-  Gather G[WG_NI];
-  uint4 yv[WG_NI], im[WG_NP][4];
-  auto issue = [&](int st) {
-    const uint32_t base = p_begin + (uint32_t)st * WPX;
+  auto quad_of = [&](uint32_t q, uint32_t& nn, int& qh, int& qw) {
+    nn = fdiv(q, a.div_q);
+    const uint32_t rem = q - nn * a.div_q.d;
+    const uint32_t t = fdiv(rem, a.div_qw);
+    qh = (int)t;
+    qw = (int)(rem - t * a.div_qw.d);
+  };
+
+  // the pooled-gradient gather of a step, raw, in registers (two sets: issued two steps ahead)
+  struct GRegs {
+    uint32_t ix[4];
+    uint2 gv[4], yv[4];
+    uint32_t okm;  // bits 0-3: window s exists; bits 4-7: pixel d exists; bit 8: quad live
+  };
+  constexpr int NG = (MODE & 1) ? 4 : 12;  // gather loads per lane per step
+  auto issue_dma = [&](int st, uint16_t* ilst) {
+    if constexpr (!(MODE & 4)) {
+      const uint32_t base = q_begin + (uint32_t)st * WQ;
+      // im2col: pixel 16 wave + (lane >> 2) of the step, 16-B chunk lane & 3, kernel rows 0..6
+      const int px = 16 * wave + (lane >> 2);
+      uint32_t nn;
+      int qh, qw;
+      quad_of(min(base + (uint32_t)(px >> 2), q_end - 1), nn, qh, qw);
+      const int oh = min(2 * qh + ((px >> 1) & 1), g.oh - 1), ow = min(2 * qw + (px & 1), g.ow - 1);
+      const uint32_t voff = ((nn * (uint32_t)g.hp + 2u * (uint32_t)oh) * (uint32_t)g.wp + 2u * (uint32_t)ow) * 8u +
+                            16u * (uint32_t)(lane & 3);
+      uint16_t* dst = ilst + 16 * wave * KROW;
 #pragma unroll
-    for (int i = 0; i < WG_NI; ++i) {
-      const uint32_t pix = base + (uint32_t)((tid + 512 * i) >> 3);
-      const uint32_t pc = pix < p_end ? pix : p_end - 1;
-      const uint32_t nn = fdiv(pc, a.div_ohw), rem = pc - nn * a.div_ohw.d;
-      const uint32_t yh = fdiv(rem, a.div_ow), yw = rem - yh * a.div_ow.d;
-      if constexpr (MODE & 1) G[i] = Gather{};
-      else gather_issue(a, nn, (int)yh, (int)yw, c8, G[i]);
-      yv[i] = *reinterpret_cast<const uint4*>(a.y + (size_t)pc * CO + c8 * 8);
-    }
-#pragma unroll
-    for (int i = 0; i < WG_NP; ++i) {
-      // every lane loads (lanes past the last pair re-read pair 0; commit skips their store)
-      const int pr = (tid + 512 * i) < WPX * 7 ? tid + 512 * i : 0;
-      const uint32_t pix = base + (uint32_t)(pr / 7);
-      const int r = pr % 7;
-      const uint32_t pc = pix < p_end ? pix : p_end - 1;
-      const uint32_t nn = fdiv(pc, a.div_ohw), rem = pc - nn * a.div_ohw.d;
-      const uint32_t oh = fdiv(rem, a.div_ow), ow = rem - oh * a.div_ow.d;
-      const uint4* src = reinterpret_cast<const uint4*>(a.xp + ((size_t)(nn * g.hp + 2 * oh) * g.wp + 2 * ow) * 4 +
-                                                         r * rowstep);
-      // im[i][q] holds chunk (q + rot) & 3 of the pair (bank-conflict-free commit, see there)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) im[i][q] = (MODE & 4) ? make_uint4(0, 0, 0, 0) : src[(q + rot) & 3];
+      for (int r = 0; r < 7; ++r) bdma16(xr, voff, (uint32_t)r * rowbytes, dst + r * WPX * KROW);
     }
   };
-  auto commit = [&](int st) {
-    const uint32_t base = p_begin + (uint32_t)st * WPX;
-    float sc[8], sh[8], A[8], B[8], K[8];
-    Vec8<float>::load(sc, cf + c8 * 8);
-    Vec8<float>::load(sh, cf + CO + c8 * 8);
-    Vec8<float>::load(A, cf + 2 * CO + c8 * 8);
-    Vec8<float>::load(B, cf + 3 * CO + c8 * 8);
-    Vec8<float>::load(K, cf + 4 * CO + c8 * 8);
+  auto issue_gather = [&](int st, GRegs& G) {
+    const uint32_t base = q_begin + (uint32_t)st * WQ;
+    const uint32_t q = min(base + (uint32_t)ql, q_end - 1);
+    uint32_t nn;
+    int qh, qw;
+    quad_of(q, nn, qh, qw);
+    uint32_t okm = base + (uint32_t)ql < q_end ? 256u : 0u;
+    // every slot loads (clamped addresses): no branch around a load, counted vmcnt waits
 #pragma unroll
-    for (int i = 0; i < WG_NI; ++i) {
-      const bool live = base + (uint32_t)((tid + 512 * i) >> 3) < p_end;
-      float gs[8], v[8], dx[8];
-      gather_sum<T>(G[i], gs);
-      const uint32_t yw4[4] = {yv[i].x, yv[i].y, yv[i].z, yv[i].w};
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        v[e] = to_f(T{(uint16_t)((yw4[e >> 1] >> (16 * (e & 1))) & 0xffffu)});
-        const float gm = fmaf(v[e], sc[e], sh[e]) > 0.f ? gs[e] : 0.f;
-        // dX rounded to the storage type, as the unfused path's dx tensor
-        dx[e] = live ? fmaf(A[e], gm, fmaf(B[e], v[e], K[e])) : 0.f;
+    for (int s = 0; s < 4; ++s) {
+      const int ph = qh + (s >> 1), pw = qw + (s & 1);
+      okm |= (ph < g.ph && pw < g.pw) ? 1u << s : 0u;
+      const size_t o = ((size_t)(nn * g.ph + min(ph, g.ph - 1)) * g.pw + min(pw, g.pw - 1)) * CO + c4 * 4;
+      if constexpr (MODE & 1) {
+        G.ix[s] = 0;
+        G.gv[s] = make_uint2(0, 0);
+      } else {
+        G.ix[s] = *reinterpret_cast<const uint32_t*>(a.idx + o);
+        G.gv[s] = *reinterpret_cast<const uint2*>(a.dp + o);
       }
-      Vec8<T>::store(reinterpret_cast<T*>(dl + ((tid + 512 * i) >> 3) * DSTR + c8 * 8), dx);
     }
 #pragma unroll
-    for (int i = 0; i < WG_NP; ++i) {
-      const int pr = tid + 512 * i;
-      if (pr >= WPX * 7) continue;
-      uint4* dst = reinterpret_cast<uint4*>(il + (pr / 7) * ISTR + (pr % 7) * KROW);
-      // ds_write_b128 banks over 8-lane groups on a 128-B window: a pair's 64 B start on the
-      // 64-B half (pr / 7 + pr % 7) & 1 = pr & 1 (ISTR is 576 B), so lanes of one parity would
-      // all hit the same 16-B slot (4-way); rotating the chunk order by (pr >> 1) & 3 gives the 8
-      // lanes of a group 8 distinct slots
+    for (int d = 0; d < 4; ++d) {
+      const int yh = 2 * qh + (d >> 1), yw = 2 * qw + (d & 1);
+      okm |= (yh < g.oh && yw < g.ow) ? 16u << d : 0u;
+      const size_t pix = ((size_t)nn * g.oh + min(yh, g.oh - 1)) * g.ow + min(yw, g.ow - 1);
+      G.yv[d] = *reinterpret_cast<const uint2*>(a.y + pix * CO + c4 * 4);
+    }
+    G.okm = okm;
+  };
+  auto commit = [&](const GRegs& G) {
+    float sc[4], sh[4], A[4], B[4], K[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) dst[(q + rot) & 3] = im[i][q];
+    for (int e = 0; e < 4; ++e) {
+      sc[e] = cf[c4 * 4 + e];
+      sh[e] = cf[CO + c4 * 4 + e];
+      A[e] = cf[2 * CO + c4 * 4 + e];
+      B[e] = cf[3 * CO + c4 * 4 + e];
+      K[e] = cf[4 * CO + c4 * 4 + e];
+    }
+    const uint32_t okm = G.okm;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int dy = d >> 1, dxc = d & 1;
+      const float lv = (okm & 256u) && (okm & (16u << d)) ? 1.f : 0.f;
+      const uint32_t yw2[2] = {G.yv[d].x, G.yv[d].y};
+      float gs[4] = {0.f, 0.f, 0.f, 0.f}, dx[4];
+      // the windows holding pixel d, summed in the (ph, pw) order a per-pixel gather uses
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int sr = s >> 1, sc2 = s & 1;
+        if ((sr && !dy) || (sc2 && !dxc)) continue;  // compile-time: the window misses the pixel
+        const uint32_t kk = (okm >> s) & 1u ? (uint32_t)((1 + dy - 2 * sr) * 3 + (1 + dxc - 2 * sc2)) : 255u;
+        const uint32_t gw[2] = {G.gv[s].x, G.gv[s].y};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t k = (G.ix[s] >> (8 * e)) & 0xffu;
+          const float gg = to_f(T{(uint16_t)((gw[e >> 1] >> (16 * (e & 1))) & 0xffffu)});
+          gs[e] += k == kk ? gg : 0.f;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v = to_f(T{(uint16_t)((yw2[e >> 1] >> (16 * (e & 1))) & 0xffffu)});
+        const float gm = fmaf(v, sc[e], sh[e]) > 0.f ? gs[e] : 0.f;
+        // dX rounded to the storage type, as the unfused path's dx tensor; a dead pixel's operands
+        // are a clamped live pixel's (finite), so the mask multiply zeroes it without the
+        // per-element branch a select turns into
+        dx[e] = fmaf(A[e], gm, fmaf(B[e], v, K[e])) * lv;
+      }
+      *reinterpret_cast<uint2*>(dl + (4 * ql + d) * DSTR + c4 * 4) =
+          make_uint2((uint32_t)from_f<T>(dx[0]).x | ((uint32_t)from_f<T>(dx[1]).x << 16),
+                     (uint32_t)from_f<T>(dx[2]).x | ((uint32_t)from_f<T>(dx[3]).x << 16));
     }
   };
 
-  // waves 0-6 own k-tile u = wave (both 32-channel tiles); wave 7 only stages
   f32x16 acc[2] = {zero16(), zero16()};
-  __syncthreads();  // cf
-  if (steps > 0) issue(0);
-  for (int st = 0; st < steps; ++st) {
-    commit(st);
+  GRegs g0, g1;
+  // Issue order: gather(0), DMA(0), gather(1); then in step s: DMA(s + 1), gather(s + 2), issued
+  // unconditionally (past the last step: the last step's again, discarded), so on every path the
+  // loads younger than DMA(s) when step s commits are gather(s + 1)'s NG: vmcnt(NG) retires DMA(s)
+  // (and gather(s), which the commit used), and the compiler's own counted waits stay exact.
+  auto step = [&](int st, uint16_t* cur, uint16_t* nxt, GRegs& G) {
+    commit(G);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NG) : "memory");
     lds_barrier();
-    if (st + 1 < steps) issue(st + 1);  // lands under this step's MFMAs
+    issue_dma(min(st + 1, steps - 1), nxt);      // lands under this step's MFMAs
+    issue_gather(min(st + 2, steps - 1), G);     // two steps ahead (G was just committed)
     if (wave < 7 && !(MODE & 2)) {
+      const uint16_t* ib = cur + wave * WPX * KROW;
 #pragma unroll
       for (int ks = 0; ks < WPX / 16; ++ks) {
         const int klo = 16 * ks + 8 * h;
         const s16x8 a0 = frag_tr<DSTR>(dl, 0, klo, klo + 4, lane);
         const s16x8 a1 = frag_tr<DSTR>(dl, 32, klo, klo + 4, lane);
-        const s16x8 bf = frag_tr<ISTR>(il, 32 * wave, klo, klo + 4, lane);
+        const s16x8 bf = frag_tr<KROW>(ib, 0, klo, klo + 4, lane);
         acc[0] = mma<T>(a0, bf, acc[0]);
         acc[1] = mma<T>(a1, bf, acc[1]);
       }
     }
     lds_barrier();
+  };
+  __syncthreads();  // cf
+  if (steps > 0) {
+    issue_gather(0, g0);
+    issue_dma(0, il0);
+    issue_gather(min(1, steps - 1), g1);
+    // pairs (the im2col stage and the gather register set of every access are compile-time; no
+    // branch around a step inside the loop, so the back edge always carries the same loads)
+    int st = 0;
+    for (; st + 1 < steps; st += 2) {
+      step(st, il0, il1, g0);
+      step(st + 1, il1, il0, g1);
+    }
+    if (st < steps) step(st, il0, il1, g0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the discarded tail loads
   }
   if (wave < 7) {
     float* ws = a.ws + (size_t)blockIdx.x * CO * KT;
@@ -762,10 +797,15 @@ void stem_wgrad(const void* dp, const uint8_t* idx, const void* y, const float* 
   stem::BwdArgs a = bwd_args(dp, idx, y, coef, n, h, w);
   a.cb = cb;
   a.xp = (const uint16_t*)xp;
+  a.xbytes = (uint32_t)((int64_t)n * a.g.hp * a.g.wp * 8);
   a.ws = ws;
   const int G = stem_wgrad_parts(cus);
-  a.chunk = (uint32_t)(((int64_t)a.g.m + G - 1) / G);
-  a.chunk = (a.chunk + stem::WPX - 1) / stem::WPX * stem::WPX;
+  const uint32_t qh_n = (uint32_t)(a.g.oh + 1) / 2, qw_n = (uint32_t)(a.g.ow + 1) / 2;
+  a.nq = (uint32_t)a.g.n * qh_n * qw_n;
+  a.div_q = make_fastdiv(qh_n * qw_n);
+  a.div_qw = make_fastdiv(qw_n);
+  a.chunk = (uint32_t)(((int64_t)a.nq + G - 1) / G);
+  a.chunk = (a.chunk + stem::WQ - 1) / stem::WQ * stem::WQ;
 
   if (cin < 1 || cin > 4) throw std::runtime_error("stem wgrad: 1-4 input channels");
   dispatch_16(t, [&](auto tag) {
@@ -774,11 +814,7 @@ void stem_wgrad(const void* dp, const uint8_t* idx, const void* y, const float* 
       const char* e = std::getenv("APEX_AMD_STEM_WG_MODE");
       return e ? std::atoi(e) : 0;
     }();
-    auto go = [&](auto kern) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                stem::WG_LDS);
-      hipLaunchKernelGGL(kern, dim3(G), dim3(512), stem::WG_LDS, s, a);
-    };
+    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(G), dim3(512), 0, s, a); };
     switch (mode) {
       case 1: go(stem::wgrad_kernel<T, 1>); break;
       case 2: go(stem::wgrad_kernel<T, 2>); break;

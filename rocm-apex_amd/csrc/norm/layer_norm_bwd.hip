@@ -165,6 +165,144 @@ ln_bwd_kernel(const TO* __restrict__ dy, const TI* __restrict__ x, const float* 
   }
 }
 
+// Wide rows (16384 < n2 <= 65536): one 1024-thread workgroup (16 waves, <= 128 VGPRs) per row,
+// persistent over rows.  x and dy stay raw (16-bit: 4 words per 8 elements) in registers and are
+// unpacked in each of the two passes; gamma is re-read per row (L1 / L2 hits).  With GB (VPT 2,
+// n2 <= 16384) the lane also accumulates dy * xhat and dy of its 16 columns (32 registers) and the
+// workgroup leaves one partial row, as the narrow kernels do; at VPT 4 / 8 those accumulators do
+// not fit beside the row at 16 waves (VPT 4 spills), so ln_bwd_gb_wide_kernel makes the partials
+// in a column-tiled pass (x and dy read once more).  The narrow 8-wave kernel holds gamma and the
+// accumulators of 4 vectors per lane and spills: rows past 8192 take this kernel.
+template <typename TI, typename TW, typename TO, int VPT, bool GB>
+__global__ void __launch_bounds__(1024)
+ln_bwd_wide_kernel(const TO* __restrict__ dy, const TI* __restrict__ x, const float* __restrict__ mean,
+                   const float* __restrict__ invvar, const TW* __restrict__ gamma, TI* __restrict__ dx,
+                   float* __restrict__ part_g, float* __restrict__ part_b, int64_t n1, int n2, bool rms,
+                   const TO* __restrict__ dres) {
+  constexpr int W = 16;
+  constexpr int GV = GB ? VPT : 1;
+  __shared__ float red[2 * W];
+  const int li = threadIdx.x;
+  const int wave = li >> 6;
+  const int nv = n2 >> 3;
+  const float inv_n = 1.f / (float)n2;
+  float ag[GV][8], ab[GV][8];
+#pragma unroll
+  for (int j = 0; j < GV; ++j)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ag[j][k] = ab[j][k] = 0.f;
+  auto gload = [&](int v, float (&gj)[8]) {
+    if (gamma != nullptr) {
+      Vec8<TW>::load(gj, gamma + v * 8);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) gj[k] = 1.f;
+    }
+  };
+  for (int64_t row = blockIdx.x; row < n1; row += gridDim.x) {
+    const float mu = rms ? 0.f : mean[row], iv = invvar[row];
+    Raw8<TI> px[VPT];
+    Raw8<TO> pd[VPT];
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int v = j * W * 64 + li;
+      if (v < nv) {
+        px[j].load(x + row * n2 + v * 8);
+        pd[j].load(dy + row * n2 + v * 8);
+      } else {
+        px[j].zero();
+        pd[j].zero();
+      }
+    }
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int v = j * W * 64 + li;
+      if (v < nv) {
+        float xh[8], d[8], gj[8];
+        px[j].unpack(xh);
+        pd[j].unpack(d);
+        gload(v, gj);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          xh[k] = (xh[k] - mu) * iv;
+          const float gd = d[k] * gj[k];
+          s1 += gd;
+          s2 += gd * xh[k];
+          if constexpr (GB) {
+            ag[j < GV ? j : 0][k] += d[k] * xh[k];
+            ab[j < GV ? j : 0][k] += d[k];
+          }
+        }
+      }
+      // one vector's gamma / unpacked values live at a time (the scheduler would otherwise hoist
+      // every vector's gamma load and spill at 16 waves)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    row_sum2<W>(s1, s2, red, 0, wave);
+    const float m1 = rms ? 0.f : s1 * inv_n;
+    const float m2 = s2 * inv_n;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int v = j * W * 64 + li;
+      if (v < nv) {
+        float xh[8], d[8], gj[8], o[8];
+        px[j].unpack(xh);
+        pd[j].unpack(d);
+        gload(v, gj);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = iv * (d[k] * gj[k] - m1 - (xh[k] - mu) * iv * m2);
+        if (dres != nullptr) {
+          float rs[8];
+          Vec8<TO>::load(rs, dres + row * n2 + v * 8);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] += rs[k];
+        }
+        Vec8<TI>::store(dx + row * n2 + v * 8, o);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if constexpr (GB) {
+    if (part_g == nullptr) return;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int v = j * W * 64 + li;
+      if (v < nv) {
+        Vec8<float>::store(part_g + (int64_t)blockIdx.x * n2 + v * 8, ag[j]);
+        Vec8<float>::store(part_b + (int64_t)blockIdx.x * n2 + v * 8, ab[j]);
+      }
+    }
+  }
+}
+
+// dgamma / dbeta partials of wide rows: grid (n2 / 2048 column blocks, P row parts); a thread owns
+// 8 columns (16-byte loads) over rows p, p + P, ...; partial row p of each quantity out.
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256)
+ln_bwd_gb_wide_kernel(const TO* __restrict__ dy, const TI* __restrict__ x, const float* __restrict__ mean,
+                      const float* __restrict__ invvar, float* __restrict__ part_g, float* __restrict__ part_b,
+                      int64_t n1, int n2, bool rms) {
+  const int v = blockIdx.x * 256 + threadIdx.x;
+  if (v >= (n2 >> 3)) return;
+  float sg[8], sb[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sg[k] = sb[k] = 0.f;
+  for (int64_t r = blockIdx.y; r < n1; r += gridDim.y) {
+    const float mu = rms ? 0.f : mean[r], iv = invvar[r];
+    float xv[8], d[8];
+    Vec8<TI>::load(xv, x + r * n2 + v * 8);
+    Vec8<TO>::load(d, dy + r * n2 + v * 8);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sg[k] += d[k] * ((xv[k] - mu) * iv);
+      sb[k] += d[k];
+    }
+  }
+  Vec8<float>::store(part_g + (int64_t)blockIdx.y * n2 + v * 8, sg);
+  Vec8<float>::store(part_b + (int64_t)blockIdx.y * n2 + v * 8, sb);
+}
+
 // dgamma[c] = sum_b part[b][c] in fixed b order.  Block = 64 columns x 4 row-groups.
 template <typename TW>
 __global__ void __launch_bounds__(256)
@@ -242,6 +380,34 @@ static int launch_bwd(const NormBwdArgs& a, int cus, hipStream_t s) {
   return grid;
 }
 
+// the raw x / dy words a lane of the wide kernel keeps per row must stay <= 64 of its 128 VGPRs
+// (fp32 rows at 8 vectors per lane take the generic kernels)
+template <typename TI, typename TO, int VPT>
+constexpr bool wide_ok() { return VPT * 2 * (int)(sizeof(TI) + sizeof(TO)) <= 64; }
+
+template <typename TI, typename TW, typename TO, int VPT>
+static int launch_bwd_wide(const NormBwdArgs& a, int cus, hipStream_t s) {
+  const bool want = a.dgamma != nullptr || a.dbeta != nullptr;
+  const int grid = (int)(a.n1 < cus ? a.n1 : cus);
+  constexpr bool GB = VPT <= 2;
+  float* pg = want && GB ? a.workspace : nullptr;
+  float* pb = want && GB ? a.workspace + (int64_t)grid * a.n2 : nullptr;
+  hipLaunchKernelGGL((ln_bwd_wide_kernel<TI, TW, TO, VPT, GB>), dim3(grid), dim3(1024), 0, s, (const TO*)a.dy,
+                     (const TI*)a.x, a.mean, a.invvar, (const TW*)a.gamma, (TI*)a.dx, pg, pb, a.n1, a.n2, a.rms,
+                     (const TO*)a.dres);
+  if (!want) return 0;
+  if (GB) return grid;
+  const int cb = (a.n2 / 8 + 255) / 256;
+  int64_t p = ((int64_t)cus * 4 + cb - 1) / cb;
+  if (p > a.n1) p = a.n1;
+  if (p > 1024) p = 1024;
+  const int parts = (int)(p < 1 ? 1 : p);
+  hipLaunchKernelGGL((ln_bwd_gb_wide_kernel<TI, TO>), dim3(cb, parts), dim3(256), 0, s, (const TO*)a.dy,
+                     (const TI*)a.x, a.mean, a.invvar, a.workspace, a.workspace + (int64_t)parts * a.n2, a.n1, a.n2,
+                     a.rms);
+  return parts;
+}
+
 static bool aligned16(const void* p) { return p == nullptr || ((uintptr_t)p & 15u) == 0; }
 
 static int generic_parts(int64_t n1, int n2, int cus) {
@@ -263,13 +429,19 @@ void norm_bwd_impl(const NormBwdArgs& a, int cus, hipStream_t s) {
     using TW = typename decltype(tw)::type;
     using TO = typename decltype(to)::type;
     int nparts = 0;
-    if (fast) {
+    const bool wide_fits = c.W < 16 || (c.VPT == 4 ? wide_ok<TI, TO, 4>() : wide_ok<TI, TO, 8>());
+    // rows of 8193 .. 16384 (the forward's 8-wave geometry): the 16-wave kernel at 2 vectors per
+    // lane (see ln_bwd_wide_kernel)
+    const bool wide2 = c.W == 8;
+    if (fast && wide_fits) {
       if (c.W == 1 && c.VPT == 1) nparts = launch_bwd<TI, TW, TO, 1, 1>(a, cus, s);
       else if (c.W == 1 && c.VPT == 2) nparts = launch_bwd<TI, TW, TO, 1, 2>(a, cus, s);
       else if (c.W == 1 && c.VPT == 4) nparts = launch_bwd<TI, TW, TO, 1, 4>(a, cus, s);
       else if (c.W == 4 && c.VPT == 2) nparts = launch_bwd<TI, TW, TO, 4, 2>(a, cus, s);
       else if (c.W == 4 && c.VPT == 4) nparts = launch_bwd<TI, TW, TO, 4, 4>(a, cus, s);
-      else nparts = launch_bwd<TI, TW, TO, 8, 4>(a, cus, s);
+      else if (wide2) nparts = launch_bwd_wide<TI, TW, TO, 2>(a, cus, s);
+      else if (c.VPT == 4) nparts = launch_bwd_wide<TI, TW, TO, 4>(a, cus, s);
+      else if constexpr (wide_ok<TI, TO, 8>()) nparts = launch_bwd_wide<TI, TW, TO, 8>(a, cus, s);
     } else {
       hipLaunchKernelGGL((ln_bwd_dx_generic_kernel<TI, TW, TO>), dim3((unsigned)a.n1), dim3(256), 0, s,
                          (const TO*)a.dy, (const TI*)a.x, a.mean, a.invvar, (const TW*)a.gamma, (TI*)a.dx, a.n1,

@@ -18,6 +18,12 @@ ln_fwd_kernel(const TI* __restrict__ x, const TW* __restrict__ gamma, const TW* 
               int n2, float eps, bool rms) {
   constexpr int NT = block_threads<W>();
   constexpr int RPB = NT / 64 / W;  // rows per block
+  // wide rows (16 waves, 1024 threads => <= 128 VGPRs): gamma / beta are re-read per row (L2 /
+  // L1 hits) instead of held in registers, and an fp32 row at 8 vectors per lane is not
+  // double-buffered (64 raw words per row)
+  constexpr bool GREG = W * VPT <= 32;
+  constexpr bool PF = !(sizeof(TI) == 4 && VPT > 4);
+  constexpr int GV = GREG ? VPT : 1;
   __shared__ float red[2 * RPB * W];
   const int wave = threadIdx.x >> 6;
   const int row_in_block = wave / W;
@@ -27,20 +33,23 @@ ln_fwd_kernel(const TI* __restrict__ x, const TW* __restrict__ gamma, const TW* 
   const int64_t ngroups = (n1 + RPB - 1) / RPB;
   const float inv_n = 1.f / (float)n2;
 
-  // gamma / beta are the same for every row this lane visits: loaded once
-  float g[VPT][8], b[VPT][8];
-#pragma unroll
-  for (int j = 0; j < VPT; ++j) {
+  // gamma / beta are the same for every row this lane visits: loaded once (GREG)
+  float g[GV][8], b[GV][8];
+  auto load_gb = [&](int j, float (&gj)[8], float (&bj)[8]) {
     const int v = j * W * 64 + li;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      g[j][k] = 1.f;
-      b[j][k] = 0.f;
+      gj[k] = 1.f;
+      bj[k] = 0.f;
     }
     if (v < nv) {
-      if (gamma != nullptr) Vec8<TW>::load(g[j], gamma + v * 8);
-      if (beta != nullptr) Vec8<TW>::load(b[j], beta + v * 8);
+      if (gamma != nullptr) Vec8<TW>::load(gj, gamma + v * 8);
+      if (beta != nullptr) Vec8<TW>::load(bj, beta + v * 8);
     }
+  };
+  if constexpr (GREG) {
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) load_gb(j, g[j], b[j]);
   }
   // persistent, software-pipelined: the next row-group's input is loaded raw while the current
   // row is reduced and stored (two rows' bytes in flight per lane)
@@ -55,14 +64,15 @@ ln_fwd_kernel(const TI* __restrict__ x, const TW* __restrict__ gamma, const TW* 
       else px[j].zero();
     }
   };
-  prefetch(blockIdx.x);
+  if constexpr (PF) prefetch(blockIdx.x);
   for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int64_t row = grp * RPB + row_in_block;
     const bool valid = row < n1;
+    if constexpr (!PF) prefetch(grp);
     float r[VPT][8];
 #pragma unroll
     for (int j = 0; j < VPT; ++j) px[j].unpack(r[j]);
-    prefetch(grp + gridDim.x);
+    if constexpr (PF) prefetch(grp + gridDim.x);
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < VPT; ++j)
@@ -94,9 +104,13 @@ ln_fwd_kernel(const TI* __restrict__ x, const TW* __restrict__ gamma, const TW* 
     for (int j = 0; j < VPT; ++j) {
       const int v = j * W * 64 + li;
       if (v < nv) {
+        float gl[8], bl[8];
+        if constexpr (!GREG) load_gb(j, gl, bl);
+        const float* gj = GREG ? g[j < GV ? j : 0] : gl;
+        const float* bj = GREG ? b[j < GV ? j : 0] : bl;
         float o[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] = (r[j][k] - mu) * iv * g[j][k] + b[j][k];
+        for (int k = 0; k < 8; ++k) o[k] = (r[j][k] - mu) * iv * gj[k] + bj[k];
         Vec8<TO>::store(yr + v * 8, o);
       }
     }
@@ -141,7 +155,7 @@ static void launch_fwd(const NormFwdArgs& a, int cus, hipStream_t s) {
   constexpr int NT = block_threads<W>();
   constexpr int RPB = NT / 64 / W;
   const int64_t ngroups = (a.n1 + RPB - 1) / RPB;
-  const int64_t cap = (int64_t)cus * (W == 8 ? 2 : 4);  // resident blocks per CU of the persistent grid
+  const int64_t cap = (int64_t)cus * (W == 16 ? 1 : W == 8 ? 2 : 4);  // resident blocks per CU (persistent grid)
   const int64_t grid = ngroups < cap ? ngroups : cap;
   hipLaunchKernelGGL((ln_fwd_kernel<TI, TW, TO, W, VPT>), dim3((unsigned)grid), dim3(NT), 0, s,
                      (const TI*)a.x, (const TW*)a.gamma, (const TW*)a.beta, (TO*)a.y, a.mean, a.invvar, a.n1,
@@ -170,7 +184,9 @@ void norm_fwd_impl(const NormFwdArgs& a, int cus, hipStream_t s) {
     else if (c.W == 1 && c.VPT == 4) launch_fwd<TI, TW, TO, 1, 4>(a, cus, s);
     else if (c.W == 4 && c.VPT == 2) launch_fwd<TI, TW, TO, 4, 2>(a, cus, s);
     else if (c.W == 4 && c.VPT == 4) launch_fwd<TI, TW, TO, 4, 4>(a, cus, s);
-    else launch_fwd<TI, TW, TO, 8, 4>(a, cus, s);
+    else if (c.W == 8) launch_fwd<TI, TW, TO, 8, 4>(a, cus, s);
+    else if (c.VPT == 4) launch_fwd<TI, TW, TO, 16, 4>(a, cus, s);
+    else launch_fwd<TI, TW, TO, 16, 8>(a, cus, s);
   });
   check_launch("layer_norm forward");
 }

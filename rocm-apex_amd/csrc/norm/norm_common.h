@@ -5,8 +5,10 @@
 // lane holds VPT vectors of 8 elements in registers (one 16-byte load per vector for 16-bit
 // types), so a row is read from HBM exactly once per pass and all statistics are two-pass
 // (mean, then sum of squared deviations) on register-resident data — no Welford merge chain,
-// no re-read.  Vector j of lane li covers columns [(j*W*64 + li)*8, +8).  Supported fast-path
-// widths: n2 % 8 == 0 and n2 <= 16384; anything else takes the generic block-per-row kernels.
+// no re-read.  Vector j of lane li covers columns [(j*W*64 + li)*8, +8).  Fast-path widths:
+// n2 % 8 == 0 and n2 <= 65536 (above 16384: one 1024-thread workgroup of 16 waves per row with
+// gamma / beta read per row from L2 instead of held in registers, the "wide" kernels); anything
+// else takes the generic block-per-row kernels.
 #pragma once
 #include "apex_amd/colreduce.h"
 #include "apex_amd/device.h"
@@ -29,11 +31,13 @@ inline Cfg pick_cfg(int n2) {
   if (n2 <= 4096) return {4, 2};
   if (n2 <= 8192) return {4, 4};
   if (n2 <= 16384) return {8, 4};
+  if (n2 <= 32768) return {16, 4};
+  if (n2 <= 65536) return {16, 8};
   return {0, 0};
 }
 
 template <int W>
-constexpr int block_threads() { return W == 8 ? 512 : 256; }
+constexpr int block_threads() { return W == 16 ? 1024 : W == 8 ? 512 : 256; }
 
 // Sum over the W waves of one row; `red` is LDS of [rows_per_block * W] floats.  Every thread
 // of the block must call it (it contains barriers).

@@ -55,6 +55,13 @@ def dropout_keep_mask(seed, offset, bh, sq, sk, p, device="cpu"):
     return bits >= min(int(p * 65536.0), 65536)
 
 
+def dropout_keep_scale(p):
+    """1 / the kernels' exact keep rate: (65536 - t16) / 65536 of the 16-bit tests survive
+    (t16 = floor(p * 65536)), so the unbiased scale is 65536 / (65536 - t16), not 1 / (1 - p)."""
+    t16 = min(int(p * 65536.0), 65536)
+    return 65536.0 / (65536 - t16) if t16 < 65536 else 0.0
+
+
 def _native_ok(q, k, v, bias):
     if not (q.is_cuda and _native.use_native(q)):
         return False
@@ -105,7 +112,7 @@ def _ref_padded(q, k, v, scale, causal, bias, p, seed, offset, batch_index):
         b0 = 0 if batch_index is None else batch_index
         bh = (torch.arange(B).view(B, 1) + b0) * H + torch.arange(H).view(1, H)
         keep = dropout_keep_mask(seed, offset, bh.view(-1), Sq, Sk, p, q.device).view(B, H, Sq, Sk)
-        probs = probs * keep / (1.0 - p)
+        probs = probs * keep * dropout_keep_scale(p)
     out = torch.matmul(probs, vf).transpose(1, 2).to(q.dtype)
     return out, lse.permute(1, 0, 2).reshape(H, B * Sq)
 

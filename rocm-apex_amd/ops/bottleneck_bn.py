@@ -50,6 +50,21 @@ _NATIVE_K = (64, 128, 256, 512)
 _C3B = os.environ.get("APEX_AMD_CONV3_BWD", "1") != "0"
 # block output pass deferred into the next block's conv1 (BlockLink.defer); 0 = A/B off
 _DEFER = os.environ.get("APEX_AMD_DEFER_OUTPUT", "1") != "0"
+# library 1x1 GEMMs (stage-3/4 shapes) through the hipBLASLt wrapper's timed plans
+# (csrc/bindings/lt_epilogue.cpp lt_run: screened top candidates timed once per shape) instead of
+# torch.matmul's single heuristic answer (+0.3 % img/s in a same-box A/B: profiles/r05/ab_rn_lt_r05f.txt)
+_LT_1X1 = os.environ.get("APEX_AMD_RN_LT", "1") == "1"
+
+
+def _lib_mm(a, b, trans_b):
+    """a . op(b) for the library 1x1 routes."""
+    if _LT_1X1 and a.is_cuda and a.dtype in (torch.float16, torch.bfloat16) and a.dtype == b.dtype:
+        lt = _native.submodule("lt_gemm")
+        if lt is not None:
+            r = lt.mm(a, b, False, trans_b)
+            if r:
+                return r[0]
+    return torch.matmul(a, b.t() if trans_b else b)
 
 
 def _conv():
@@ -224,7 +239,7 @@ def conv1x1_bn_fwd(a2, w2d, pcoef, bn):
         return (y2,) + finalize_part(part, float(m), bn)
     if pcoef is not None:
         a2 = _bn().apply(a2, None, pcoef, True)[0]
-    y2 = torch.matmul(a2, w2d.t())
+    y2 = _lib_mm(a2, w2d, True)
     return (y2,) + stats_pass(y2, bn)
 
 
@@ -237,7 +252,7 @@ def conv1x1_dgrad(g2, w2d, add2=None, add_inplace=False):
         return _conv().bn1x1(g2, w2d, True, None, None, False, add2)[0]
     if add2 is not None:
         return add2.addmm_(g2, w2d) if add_inplace else torch.addmm(add2, g2, w2d)
-    return torch.matmul(g2, w2d)
+    return _lib_mm(g2, w2d, False)
 
 
 def conv1x1_wgrad(g2, x2, xcoef, w):

@@ -26,7 +26,8 @@ def naive(q, k, v, scale, causal=False, bias=None, keep=None, p=0.0):
         s = s.masked_fill(torch.ones(s.shape[-2:], dtype=torch.bool, device=s.device).triu(1), float("-inf"))
     pr = torch.softmax(s, -1)
     if keep is not None:
-        pr = pr * keep / (1 - p)
+        # the kernels' exact keep rate (16-bit threshold): 65536 / (65536 - floor(p * 65536))
+        pr = pr * keep * (65536.0 / (65536 - int(p * 65536.0)))
     return (pr @ vf).transpose(1, 2)
 
 
@@ -425,3 +426,13 @@ def test_cpu_reference_functional_api_matches_modules():
     got = fast_encdec_attn_func(False, False, 8, q, kv, e.in_proj_weight_q, e.in_proj_weight_kv, e.out_proj_weight,
                                 None, 0.0)
     torch.testing.assert_close(got, ref, atol=1e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1, 0.25, 0.3333, 0.9])
+def test_dropout_keep_scale_is_unbiased_for_the_16bit_threshold(p):
+    from apex.ops.attention import dropout_keep_scale, dropout_keep_mask
+    t16 = min(int(p * 65536.0), 65536)
+    # exactly (65536 - t16) of the 65536 16-bit test values survive: scale x keep rate == 1
+    assert dropout_keep_scale(p) * (65536 - t16) / 65536 == pytest.approx(1.0, rel=1e-12)
+    keep = dropout_keep_mask(7, 0, [0, 1], 64, 256, p)
+    assert abs(keep.float().mean().item() * dropout_keep_scale(p) - 1.0) < 0.05

@@ -3,7 +3,8 @@
 Model: reference tests/L0/run_fused_layer_norm/test_fused_layer_norm.py:10-111 (fused module vs
 ``F.layer_norm`` in fp32 / half / bf16).  GPU tests compare the gfx950 kernels against a plain
 fp32 PyTorch reference of the same op, over widths that exercise every register-resident
-geometry (norm_common.h pick_cfg) and the generic path (n2 % 8 != 0, n2 > 16384)."""
+geometry (norm_common.h pick_cfg; 16-wave wide rows up to 65536) and the generic path (n2 % 8 != 0,
+n2 > 65536, fp32 rows past 32768 in the backward)."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -55,7 +56,9 @@ def test_cpu_rms_norm():
     y.sum().backward()
 
 
-WIDTHS = [64, 768, 1000, 1024, 2048, 3072, 4096, 5120, 8192, 12288, 16384, 20008]
+# 20008: generic (n2 % 8 != 0); 24576 .. 65536: the 16-wave wide kernels (40000: a partial last
+# vector column block; fp32 at 65536 takes the generic backward)
+WIDTHS = [64, 768, 1000, 1024, 2048, 3072, 4096, 5120, 8192, 12288, 16384, 20008, 24576, 32768, 40000, 65536]
 TOL = {torch.float32: (1e-4, 1e-4), torch.float16: (2e-2, 1e-2), torch.bfloat16: (5e-2, 2e-2)}
 
 
@@ -114,7 +117,7 @@ def test_gpu_mixed_dtypes(n2, dtype):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(FusedRMSNorm is None, reason="no RMSNorm")
-@pytest.mark.parametrize("n2", [512, 2048, 8192, 1000])
+@pytest.mark.parametrize("n2", [512, 2048, 8192, 1000, 49152])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_gpu_rms_norm(n2, dtype):
     torch.manual_seed(2)
@@ -172,7 +175,7 @@ def test_cpu_fast_layer_norm_module():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("hidden", [768, 1024, 4096, 12288, 25600])
+@pytest.mark.parametrize("hidden", [768, 1024, 4096, 12288, 25600, 32768, 65536])
 @pytest.mark.parametrize("itype,wtype", [(torch.bfloat16, torch.bfloat16), (torch.float16, torch.float32),
                                          (torch.float32, torch.float32)])
 def test_gpu_fast_layer_norm(hidden, itype, wtype):
