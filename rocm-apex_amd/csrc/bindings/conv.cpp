@@ -160,10 +160,17 @@ bool halo_wgrad_supported(int64_t n, int64_t h, int64_t w, int64_t c, int64_t ko
 }
 
 // y = pro(a) . W^T (+ BN statistics partials); see conv_api.h.  Returns (y, part or empty).
+// rows of the residual: M, or those of its stride-2 subsample when res_h, res_w > 0 (M = N res_h res_w)
+static int64_t res_rows(int64_t m, int64_t res_h, int64_t res_w) {
+  if (res_h <= 0 || res_w <= 0) return m;
+  TORCH_CHECK(m % (res_h * res_w) == 0, "subsampled residual: M is not a multiple of res_h * res_w");
+  return m / (res_h * res_w) * ((res_h + 1) / 2) * ((res_w + 1) / 2);
+}
+
 std::vector<at::Tensor> bn1x1(const at::Tensor& a, const at::Tensor& w, bool w_kmajor_out,
                               const c10::optional<at::Tensor>& pcoef, const c10::optional<at::Tensor>& shift,
                               bool stats, const c10::optional<at::Tensor>& res,
-                              const c10::optional<at::Tensor>& py, bool want_aout) {
+                              const c10::optional<at::Tensor>& py, bool want_aout, int64_t res_h, int64_t res_w) {
   TORCH_CHECK(a.is_cuda() && a.dim() == 2 && a.is_contiguous(), "bn1x1: a must be a contiguous [M, K] GPU tensor");
   TORCH_CHECK(w.is_cuda() && w.dim() == 2 && w.is_contiguous() && w.scalar_type() == a.scalar_type(),
               "bn1x1: w must be a contiguous 2-D tensor of a's dtype");
@@ -194,11 +201,13 @@ std::vector<at::Tensor> bn1x1(const at::Tensor& a, const at::Tensor& w, bool w_k
     part = at::empty({2, conv1x1_bn_partials(m, k, ncols, pc != nullptr, cus), ncols}, a.options().dtype(at::kFloat));
   if (res.has_value())
     TORCH_CHECK(res->is_cuda() && res->is_contiguous() && res->scalar_type() == a.scalar_type() &&
-                    res->numel() == m * ncols,
-                "bn1x1: res must be a contiguous [M, ncols] tensor of a's dtype");
+                    res->numel() == res_rows(m, res_h, res_w) * ncols,
+                "bn1x1: res must be a contiguous [M, ncols] tensor of a's dtype (subsampled rows with res_hw)");
+  TORCH_CHECK(res_h <= 0 || w_kmajor_out, "bn1x1: a subsampled residual is a dgrad-form option");
   conv1x1_bn(a.data_ptr(), w.data_ptr(), y.data_ptr(), m, k, ncols, w_kmajor_out, dtype_code(a.scalar_type()), pc, sh,
              stats ? part.data_ptr<float>() : nullptr, cus, cur_stream(), res.has_value() ? res->data_ptr() : nullptr,
-             bnbwd ? py->data_ptr() : nullptr, want_aout ? aout.data_ptr() : nullptr);
+             bnbwd ? py->data_ptr() : nullptr, want_aout ? aout.data_ptr() : nullptr, false, nullptr, (int)res_h,
+             (int)res_w);
   return {y, part, aout};
 }
 
@@ -318,7 +327,8 @@ at::Tensor wgrad1x1(const at::Tensor& g, const at::Tensor& x, const c10::optiona
 std::vector<at::Tensor> dgrad_bnred(const at::Tensor& g, const at::Tensor& w, const c10::optional<at::Tensor>& res,
                                     const c10::optional<at::Tensor>& bits, const at::Tensor& x, const at::Tensor& mean,
                                     const c10::optional<at::Tensor>& coef, const c10::optional<at::Tensor>& py,
-                                    const c10::optional<at::Tensor>& pcoef, bool want_aout) {
+                                    const c10::optional<at::Tensor>& pcoef, bool want_aout, int64_t res_h,
+                                    int64_t res_w) {
   TORCH_CHECK(g.is_cuda() && g.dim() == 2 && g.is_contiguous() && w.dim() == 2 && w.is_contiguous() &&
                   w.scalar_type() == g.scalar_type() && w.size(0) == g.size(1),
               "dgrad_bnred: g [M, k] and w [k, ncols] expected");
@@ -336,8 +346,9 @@ std::vector<at::Tensor> dgrad_bnred(const at::Tensor& g, const at::Tensor& w, co
   TORCH_CHECK(mean.is_contiguous() && mean.scalar_type() == at::kFloat && mean.numel() == ncols,
               "dgrad_bnred: mean must be fp32 [ncols]");
   if (res.has_value())
-    TORCH_CHECK(res->is_contiguous() && res->scalar_type() == g.scalar_type() && res->numel() == m * ncols,
-                "dgrad_bnred: res must be a contiguous [M, ncols] tensor");
+    TORCH_CHECK(res->is_contiguous() && res->scalar_type() == g.scalar_type() &&
+                    res->numel() == res_rows(m, res_h, res_w) * ncols,
+                "dgrad_bnred: res must be a contiguous [M, ncols] tensor (subsampled rows with res_hw)");
   const bool pro = py.has_value();
   TORCH_CHECK(pro == pcoef.has_value(), "dgrad_bnred: py and pcoef go together");
   if (pro)
@@ -356,7 +367,8 @@ std::vector<at::Tensor> dgrad_bnred(const at::Tensor& g, const at::Tensor& w, co
                       res.has_value() ? res->data_ptr() : nullptr, bits.has_value() ? bits->data_ptr<uint8_t>() : nullptr,
                       x.data_ptr(), mean.data_ptr<float>(), part.data_ptr<float>(), cus, cur_stream(),
                       coef.has_value() ? coef->data_ptr<float>() : nullptr, pro ? py->data_ptr() : nullptr,
-                      pro ? pcoef->data_ptr<float>() : nullptr, want_aout ? aout.data_ptr() : nullptr);
+                      pro ? pcoef->data_ptr<float>() : nullptr, want_aout ? aout.data_ptr() : nullptr, (int)res_h,
+                      (int)res_w);
   return {out, part, aout};
 }
 
@@ -588,7 +600,8 @@ void bind_conv(pybind11::module_& root) {
   m.def("bn1x1", &bn1x1, pybind11::arg("a"), pybind11::arg("w"), pybind11::arg("w_kmajor_out") = false,
         pybind11::arg("pcoef") = pybind11::none(), pybind11::arg("shift") = pybind11::none(),
         pybind11::arg("stats") = false, pybind11::arg("res") = pybind11::none(),
-        pybind11::arg("py") = pybind11::none(), pybind11::arg("want_aout") = false);
+        pybind11::arg("py") = pybind11::none(), pybind11::arg("want_aout") = false, pybind11::arg("res_h") = 0,
+        pybind11::arg("res_w") = 0);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn1x1_addrelu", &bn1x1_addrelu, pybind11::arg("a"), pybind11::arg("res"), pybind11::arg("pcoef"),
         pybind11::arg("w"), pybind11::arg("shift") = pybind11::none(), pybind11::arg("out") = pybind11::none());
@@ -597,7 +610,7 @@ void bind_conv(pybind11::module_& root) {
   m.def("dgrad_bnred", &dgrad_bnred, pybind11::arg("g"), pybind11::arg("w"), pybind11::arg("res"),
         pybind11::arg("bits"), pybind11::arg("x"), pybind11::arg("mean"), pybind11::arg("coef") = pybind11::none(),
         pybind11::arg("py") = pybind11::none(), pybind11::arg("pcoef") = pybind11::none(),
-        pybind11::arg("want_aout") = false);
+        pybind11::arg("want_aout") = false, pybind11::arg("res_h") = 0, pybind11::arg("res_w") = 0);
   m.def("bnbwd_finalize", &bnbwd_finalize);
   m.def("part_payload", &part_payload, pybind11::arg("part"), pybind11::arg("count"),
         pybind11::arg("shift") = pybind11::none());

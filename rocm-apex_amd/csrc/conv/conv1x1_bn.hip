@@ -25,6 +25,7 @@
 // dgrad (dX = dY . W) is the same kernel with the weight read transposed into the LDS image.
 #include "apex_amd/conv_api.h"
 #include "apex_amd/dispatch.h"
+#include "apex_amd/fastdiv.h"
 #include "apex_amd/mfma.h"
 
 #include <cstdlib>
@@ -45,6 +46,11 @@ struct Args {
   const float* shift;   // STATS: per-output-channel shift [ncols] (nullable = 0)
   float* part;          // STATS: [2][gridDim.x][ncols] partial sums (S1 slab, then S2 slab)
   const uint16_t* res;  // nullable [M][ncols]: y += res before the store (a residual gradient)
+  // rs_w2 > 0: res is the gradient of a stride-2 subsample of this output instead, [N][rs_h2][rs_w2]
+  // [ncols] over output rows (n, y, x) of an [N][H][W] image (rs_hw = H W, rs_w = W): only the
+  // rows with even y and x get res[n][y / 2][x / 2] (the strided 1x1 downsample's data gradient)
+  FastDiv rs_hw, rs_w;
+  int rs_h2, rs_w2;
   const uint16_t* py;   // PRO == kProBnBwd: second operand tensor [M][K] (the BN's input)
   uint16_t* aout;       // PRO == kProBnBwd / kProBnAddRelu, nullable: the transformed operand written out [M][K]
   uint8_t* bout;        // PRO == kProBnAddRelu, nullable: its ReLU bits [M * K / 8] (bit j of byte i = element 8 i + j)
@@ -281,7 +287,18 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
         const int64_t off = (row0 + rr) * p.ncols + col0 + 64 * g + c8;
         const bool ok = row0 + rr < p.m;
         rv[i] = make_uint4(0, 0, 0, 0);
-        if (has_res && ok) rv[i] = *reinterpret_cast<const uint4*>(p.res + off);
+        if (has_res && ok) {
+          int64_t roff = off;
+          bool rok = true;
+          if (p.rs_w2 > 0) {  // kernel-argument-uniform branch
+            const uint32_t R = (uint32_t)(row0 + rr);
+            const uint32_t img = fdiv(R, p.rs_hw), rem = R - img * p.rs_hw.d;
+            const uint32_t yy = fdiv(rem, p.rs_w), xx = rem - yy * p.rs_w.d;
+            rok = ((yy | xx) & 1u) == 0;
+            roff = (((int64_t)img * p.rs_h2 + (yy >> 1)) * p.rs_w2 + (xx >> 1)) * p.ncols + col0 + 64 * g + c8;
+          }
+          if (rok) rv[i] = *reinterpret_cast<const uint4*>(p.res + roff);
+        }
         if constexpr (RED) {
           xq[i] = ok ? *reinterpret_cast<const uint4*>(p.rx + off) : make_uint4(0, 0, 0, 0);
           mbv[i] = (ok && p.rbits) ? p.rbits[off >> 3] : 0u;
@@ -660,6 +677,19 @@ bool conv1x1_bn_supported(int64_t m, int k, int ncols) {
   return true;
 }
 
+namespace c1bn {
+// res_h, res_w > 0: the residual is the stride-2 subsample gradient of an [N][res_h][res_w] output
+inline void set_res_geometry(Args& a, int64_t m, int res_h, int res_w) {
+  if (res_h <= 0 || res_w <= 0) return;
+  if (m % ((int64_t)res_h * res_w) != 0 || m >= (1ll << 31))
+    throw std::runtime_error("conv1x1_bn: subsampled residual needs M = N * res_h * res_w < 2^31");
+  a.rs_hw = make_fastdiv((uint32_t)(res_h * res_w));
+  a.rs_w = make_fastdiv((uint32_t)res_w);
+  a.rs_h2 = (res_h + 1) / 2;
+  a.rs_w2 = (res_w + 1) / 2;
+}
+}  // namespace c1bn
+
 int conv1x1_bn_partials(int64_t m, int k, int ncols, bool pro, int cus, bool pro_addrelu) {
   return c1bn::grid_x(m, c1bn::col_tile(ncols, k), k,
                       pro_addrelu ? c1bn::kProBnAddRelu : pro ? c1bn::kProBnRelu : c1bn::kProNone, cus, ncols);
@@ -667,9 +697,10 @@ int conv1x1_bn_partials(int64_t m, int k, int ncols, bool pro, int cus, bool pro
 
 void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int ncols, bool w_kmajor_out, int dtype,
                 const float* pcoef, const float* shift, float* part, int cus, hipStream_t s, const void* res,
-                const void* py, void* aout, bool pro_relu, uint8_t* bout) {
+                const void* py, void* aout, bool pro_relu, uint8_t* bout, int res_h, int res_w) {
   if (!conv1x1_bn_supported(m, k, ncols)) throw std::runtime_error("conv1x1_bn: unsupported shape");
-  c1bn::Args args;
+  c1bn::Args args{};
+  c1bn::set_res_geometry(args, m, res_h, res_w);
   args.a = static_cast<const uint16_t*>(a);
   args.w = static_cast<const uint16_t*>(w);
   args.y = static_cast<uint16_t*>(y);
@@ -727,7 +758,8 @@ int conv1x1_dgrad_bnred_partials(int64_t m, int k, int ncols, int cus, bool pro)
 
 void conv1x1_dgrad_bnred(const void* g, const void* w, void* out, int64_t m, int k, int ncols, int dtype,
                          const void* res, const uint8_t* bits, const void* x, const float* mean, float* part, int cus,
-                         hipStream_t s, const float* rcoef, const void* py, const float* pcoef, void* aout) {
+                         hipStream_t s, const float* rcoef, const void* py, const float* pcoef, void* aout, int res_h,
+                         int res_w) {
   if (!conv1x1_bn_supported(m, k, ncols)) throw std::runtime_error("conv1x1_dgrad_bnred: unsupported shape");
   if ((!bits && !rcoef) || !x || !mean || !part)
     throw std::runtime_error("conv1x1_dgrad_bnred: a mask source (bits or coef), x, mean and part are required");
@@ -740,6 +772,7 @@ void conv1x1_dgrad_bnred(const void* g, const void* w, void* out, int64_t m, int
   args.ncols = ncols;
   args.part = part;
   args.res = static_cast<const uint16_t*>(res);
+  c1bn::set_res_geometry(args, m, res_h, res_w);
   args.rbits = bits;
   args.rcoef = rcoef;
   args.rx = static_cast<const uint16_t*>(x);

@@ -100,7 +100,9 @@ void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int nco
                 const void* py = nullptr,     // dgrad form: BN-backward prologue a' = c0 a + c1 py + c2,
                 void* aout = nullptr,         //   pcoef [3][k]; aout (nullable) receives a' [M][k]
                 bool pro_relu = false,        // forward form with py: a' = relu(c0 a + c1 py + c2) (the
-                uint8_t* bout = nullptr);     //   block output: BN + residual + ReLU), bits to bout
+                uint8_t* bout = nullptr,      //   block output: BN + residual + ReLU), bits to bout
+                int res_h = 0, int res_w = 0);  // > 0: res is [N][ceil(res_h/2)][ceil(res_w/2)][ncols], the
+                                                //   stride-2 subsample's gradient, added at even (y, x) only
 // batch statistics from the partials: save_mean / save_invstd, running-stat EMA (nullable),
 // coef = [scale | shift] of the apply (w, b nullable = affine-free)
 void conv1x1_bn_finalize(const float* part, int g, int c, float n, const float* shift, const float* w, const float* b,
@@ -130,7 +132,7 @@ int conv1x1_dgrad_bnred_partials(int64_t m, int k, int ncols, int cus, bool pro 
 void conv1x1_dgrad_bnred(const void* g, const void* w, void* out, int64_t m, int k, int ncols, int dtype,
                          const void* res, const uint8_t* bits, const void* x, const float* mean, float* part, int cus,
                          hipStream_t s, const float* rcoef = nullptr, const void* py = nullptr,
-                         const float* pcoef = nullptr, void* aout = nullptr);
+                         const float* pcoef = nullptr, void* aout = nullptr, int res_h = 0, int res_w = 0);
 void conv1x1_bnbwd_finalize(const float* part, int g, int c, float inv_n, const float* mean, const float* istd,
                             const float* w, float* gw, float* gb, float* coef, hipStream_t s);
 

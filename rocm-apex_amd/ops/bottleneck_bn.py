@@ -54,6 +54,11 @@ _DEFER = os.environ.get("APEX_AMD_DEFER_OUTPUT", "1") != "0"
 # (csrc/bindings/lt_epilogue.cpp lt_run: screened top candidates timed once per shape) instead of
 # torch.matmul's single heuristic answer (+0.3 % img/s in a same-box A/B: profiles/r05/ab_rn_lt_r05f.txt)
 _LT_1X1 = os.environ.get("APEX_AMD_RN_LT", "1") == "1"
+# the strided 1x1 downsample as a 1x1 over the stride-2 subsample of its input (one strided copy):
+# native GEMMs with the BN statistics epilogue / split-M weight gradient instead of the library's
+# strided convolution, and its data gradient added at the even pixels inside conv1's dgrad
+# epilogue (conv1x1_bn.hip rs_*) instead of a zero-filled dense tensor
+_DS_SUB = os.environ.get("APEX_AMD_DS_SUBSAMPLE", "1") != "0"
 
 
 def _lib_mm(a, b, trans_b):
@@ -243,13 +248,21 @@ def conv1x1_bn_fwd(a2, w2d, pcoef, bn):
     return (y2,) + stats_pass(y2, bn)
 
 
-def conv1x1_dgrad(g2, w2d, add2=None, add_inplace=False):
+def conv1x1_dgrad(g2, w2d, add2=None, add_inplace=False, sub_hw=None):
     """dX = g . W (+ add2): W [Cout, Cin], g [M, Cout].  ``add_inplace``: add2 is a temporary
     the caller no longer needs, so the library GEMM accumulates into it (beta = 1) instead of
-    first copying it to a fresh output (a full D2D copy per call)."""
+    first copying it to a fresh output (a full D2D copy per call).  ``sub_hw = (h, w)``: add2 is
+    the gradient of the stride-2 subsample of the [N, h, w] output, added at even (y, x) only."""
     m, kout = g2.shape
     if _dgrad_native(m, kout, w2d.size(1)):
-        return _conv().bn1x1(g2, w2d, True, None, None, False, add2)[0]
+        h, w = sub_hw if sub_hw is not None else (0, 0)
+        return _conv().bn1x1(g2, w2d, True, None, None, False, add2, res_h=h, res_w=w)[0]
+    if sub_hw is not None:
+        h, w = sub_hw
+        dx = _lib_mm(g2, w2d, False)
+        c = dx.size(1)
+        dx.view(-1, h, w, c)[:, ::2, ::2].add_(add2.view(-1, (h + 1) // 2, (w + 1) // 2, c))
+        return dx
     if add2 is not None:
         return add2.addmm_(g2, w2d) if add_inplace else torch.addmm(add2, g2, w2d)
     return _lib_mm(g2, w2d, False)
@@ -316,10 +329,13 @@ class _BottleneckFn(torch.autograd.Function):
             sm2, si2, c2, in2 = stats_pass(y2m, bn2)
         # conv3 with bn2's apply + ReLU on its operand load (+ bn3 statistics)
         y3, sm3, si3, c3, in3 = conv1x1_bn_fwd(y2m, w3.view(cout, width), c2, bn3)
-        yd = smd = sid = cd = ind = None
+        yd = smd = sid = cd = ind = xs2 = None
         if wds is not None:
             if stride == 1:
                 yd, smd, sid, cd, ind = conv1x1_bn_fwd(x2, wds.view(cout, cin), None, bnd)
+            elif _DS_SUB and stride == 2 and wds.size(2) == 1:
+                xs2 = _m2(x[:, :, ::2, ::2].contiguous(memory_format=torch.channels_last))
+                yd, smd, sid, cd, ind = conv1x1_bn_fwd(xs2, wds.view(cout, cin), None, bnd)
             else:
                 yd = _m2(_conv_fwd(x, wds, stride, 0))
                 smd, sid, cd, ind = stats_pass(yd, bnd)
@@ -337,7 +353,7 @@ class _BottleneckFn(torch.autograd.Function):
         else:
             out2, bits = _bn().apply(y3, yd, c3, True, True, cd)
         ctx.save_for_backward(x, w1, w2, w3, wds, g1, g2, g3, gds, y1, z1, y2m, y3, yd, bits,
-                              sm1, si1, c1, sm2, si2, c2, sm3, si3, c3, smd, sid, cd, in1, in2, in3, ind)
+                              sm1, si1, c1, sm2, si2, c2, sm3, si3, c3, smd, sid, cd, in1, in2, in3, ind, xs2)
         ctx.geo = (n, h, wd, oh, ow, stride)
         ctx.links = (link_in, link_out)
         ctx.groups = (bn1.group, bn2.group, bn3.group, bnd.group if bnd is not None else None)
@@ -348,7 +364,7 @@ class _BottleneckFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         (x, w1, w2, w3, wds, g1, g2, g3, gds, y1, z1, y2m, y3, yd, bits,
-         sm1, si1, c1, sm2, si2, c2, sm3, si3, c3, smd, sid, cd, in1, in2, in3, ind) = ctx.saved_tensors
+         sm1, si1, c1, sm2, si2, c2, sm3, si3, c3, smd, sid, cd, in1, in2, in3, ind, xs2) = ctx.saved_tensors
         n, h, wd, oh, ow, stride = ctx.geo
         gr1, gr2, gr3, grd = ctx.groups
         bn = _bn()
@@ -406,6 +422,7 @@ class _BottleneckFn(torch.autograd.Function):
         dy1, gg1, gb1 = bwd_full(dz1, y1, g1, sm1, si1, c1, True, gr1, in1)
         # shortcut gradient, then conv1's data gradient summed onto it
         dwd = ggd = gbd = None
+        sub_hw = None  # (h, w): ``short`` is the subsampled downsample gradient (see _DS_SUB)
         if wds is None:
             # dm is this node's own temporary unless the block above handed it in (then it is
             # autograd's incoming gradient, which must not be written)
@@ -417,15 +434,20 @@ class _BottleneckFn(torch.autograd.Function):
             if stride == 1:
                 short = conv1x1_dgrad(dyd, wds.view(cout, cin))
                 dwd = conv1x1_wgrad(dyd, x2, None, wds)
+            elif xs2 is not None:
+                short = conv1x1_dgrad(dyd, wds.view(cout, cin))
+                dwd = conv1x1_wgrad(dyd, xs2, None, wds)
+                sub_hw = (h, wd)
             else:
                 dxd, dwd = _conv_bwd(_nchw(dyd, n, oh, ow), x, wds, stride, 0)
                 short = _m2(dxd.contiguous(memory_format=torch.channels_last))
         if link_in is not None and link_in.bits is not None and _red_native(dz1.size(0), width, cin):
             # mask with the block below's ReLU bits + its bn3 backward reduction, in this kernel
+            rh, rw = sub_hw if sub_hw is not None else (0, 0)
             dx, link_in.part, _ = _conv().dgrad_bnred(dy1, w1.view(width, cin), short, link_in.bits, link_in.y3,
-                                                      link_in.mean)
+                                                      link_in.mean, res_h=rh, res_w=rw)
         else:
-            dx = conv1x1_dgrad(dy1, w1.view(width, cin), short, short_tmp)
+            dx = conv1x1_dgrad(dy1, w1.view(width, cin), short, short_tmp, sub_hw)
         dw1 = conv1x1_wgrad(dy1, x2, None, w1)
         return (_nchw(dx, n, h, wd), dw1, dw2, dw3, dwd, gg1, gb1, gg2, gb2, gg3, gb3, ggd, gbd, None)
 

@@ -273,3 +273,46 @@ def test_gpu_bn1x1_addrelu_matches_apply_pass(m, k, ncols, dual):
     _close(y, ref, 1e-2)
     d = y.float() - shift
     torch.testing.assert_close(part[0].sum(0), d.sum(0), atol=0.05 + 1e-3 * float(d.abs().sum(0).max()), rtol=1e-3)
+
+
+def _scatter_sub(sub, n, h, w):
+    """[N * ceil(h/2) * ceil(w/2), C] stride-2 subsample gradient -> dense [N * h * w, C] (zeros at odd y / x)."""
+    c = sub.size(1)
+    dense = torch.zeros(n, h, w, c, device=sub.device, dtype=torch.float32)
+    dense[:, ::2, ::2] = sub.float().view(n, (h + 1) // 2, (w + 1) // 2, c)
+    return dense.view(-1, c)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,w,k,nc", [(2, 56, 56, 64, 256), (3, 28, 28, 128, 512), (2, 7, 9, 256, 128)])
+@pytest.mark.parametrize("red", [False, True])
+def test_gpu_dgrad_subsampled_residual(n, h, w, k, nc, red):
+    """The strided 1x1 downsample's data gradient [N, ceil(h/2), ceil(w/2), C] added at even (y, x)
+    in the dgrad epilogue (conv1x1_bn.hip rs_*): plain dgrad form and the BN-reduction form."""
+    ext = _ext()
+    torch.manual_seed(11)
+    dt = torch.bfloat16
+    m = n * h * w
+    g = torch.randn(m, k, device="cuda").to(dt)
+    wt = (torch.randn(k, nc, device="cuda") * 0.1).to(dt)
+    sub = torch.randn(n * ((h + 1) // 2) * ((w + 1) // 2), nc, device="cuda").to(dt)
+    dense = _scatter_sub(sub, n, h, w)
+    if not red:
+        out = ext.bn1x1(g, wt, True, None, None, False, sub, res_h=h, res_w=w)[0]
+        ref = (g.float() @ wt.float() + dense).to(dt)
+        _close(out, ref, 2e-2)
+        # the dense-residual path agrees with it
+        out_d = ext.bn1x1(g, wt, True, None, None, False, dense.to(dt))[0]
+        _close(out, out_d, 1e-2)
+        return
+    x = torch.randn(m, nc, device="cuda").to(dt)
+    mean = torch.randn(nc, device="cuda") * 0.1
+    maskb = torch.rand(m, nc, device="cuda") > 0.4
+    wts = (2 ** torch.arange(8, device="cuda")).view(1, 8)
+    bits = (maskb.view(-1, 8).long() * wts).sum(1).to(torch.uint8)
+    out, part, _ = ext.dgrad_bnred(g, wt, sub, bits, x, mean, res_h=h, res_w=w)
+    out_d, part_d, _ = ext.dgrad_bnred(g, wt, dense.to(dt), bits, x, mean)
+    ref = torch.where(maskb, (g.float() @ wt.float() + dense).to(dt).float(), torch.zeros(()).cuda())
+    _close(out, ref, 2e-2)
+    torch.testing.assert_close(out, out_d)
+    torch.testing.assert_close(part, part_d)

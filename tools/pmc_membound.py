@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Memory-bound kernels for a rocprofv3 counter pass WITH their own roof in the same run: a plain
 elementwise copy (torch.mul by 1, the fp32 Adam step's byte count) is profiled beside FusedAdam (fp32, 24 x 4M params),
-the multi-tensor L2 norm and scale, and LayerNorm forward / backward at hidden 1024 and 4096, so
+the multi-tensor L2 norm and scale, and LayerNorm forward / backward at hidden 1024, 4096, 32768 and
+65536 (16M elements each), so
 every kernel's FETCH+WRITE rate can be read against the copy rate under the same profiler clock
 (profiled passes run at ~1.9 GHz vs ~2.0 un-profiled).  3 calls each."""
 import os
@@ -49,8 +50,8 @@ def main():
 
     from apex.normalization import FusedLayerNorm
 
-    for hid in (1024, 4096):
-        x = torch.randn(16384, hid, device="cuda", dtype=dt, requires_grad=True)
+    for hid in (1024, 4096, 32768, 65536):
+        x = torch.randn(16384 * 1024 // hid, hid, device="cuda", dtype=dt, requires_grad=True)
         ln = FusedLayerNorm(hid).cuda().to(dt)
         y = ln(x)
         gy = torch.randn_like(y)
