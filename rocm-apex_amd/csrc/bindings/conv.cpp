@@ -217,9 +217,24 @@ std::vector<at::Tensor> bn1x1(const at::Tensor& a, const at::Tensor& w, bool w_k
 // downsample BN's input with that BN's scale / shift) — the same arithmetic as the standalone
 // apply / dual-apply passes, so the deferred output is bitwise the one they would write.
 // Returns (y = out . W^T, statistics partials about shift, out [M, K], ReLU bits [M K / 8]).
+// [N * h * w, C] (NHWC rows) -> its stride-2 subsample [N * ceil(h/2) * ceil(w/2), C]
+at::Tensor subsample2x(const at::Tensor& x, int64_t n, int64_t h, int64_t w) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.is_contiguous() && x.size(0) == n * h * w &&
+                  (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf),
+              "subsample2x: x must be a contiguous 16-bit [N * h * w, C] GPU tensor");
+  const c10::hip::HIPGuard g(x.get_device());
+  auto y = at::empty({n * ((h + 1) / 2) * ((w + 1) / 2), x.size(1)}, x.options());
+  conv_subsample2x(x.data_ptr(), y.data_ptr(), (int)n, (int)h, (int)w, (int)x.size(1), dtype_code(x.scalar_type()),
+                   device_cus(x.get_device()), cur_stream());
+  return y;
+}
+
+// pcoef: [4K] (a scale | res scale | a shift | res shift), or with split the output BN's [2K]
+// scale | shift and res_coef the residual BN's [2K] (none: the identity shortcut)
 std::vector<at::Tensor> bn1x1_addrelu(const at::Tensor& a, const at::Tensor& res, const at::Tensor& pcoef,
                                       const at::Tensor& w, const c10::optional<at::Tensor>& shift,
-                                      const c10::optional<at::Tensor>& out_opt) {
+                                      const c10::optional<at::Tensor>& out_opt, bool split,
+                                      const c10::optional<at::Tensor>& res_coef) {
   TORCH_CHECK(a.is_cuda() && a.dim() == 2 && a.is_contiguous(), "bn1x1_addrelu: a must be a contiguous [M, K] GPU tensor");
   TORCH_CHECK(res.is_cuda() && res.is_contiguous() && res.sizes() == a.sizes() && res.scalar_type() == a.scalar_type(),
               "bn1x1_addrelu: res must be shaped like a");
@@ -229,8 +244,12 @@ std::vector<at::Tensor> bn1x1_addrelu(const at::Tensor& a, const at::Tensor& res
   const int64_t m = a.size(0);
   const int k = (int)a.size(1), ncols = (int)w.size(0);
   TORCH_CHECK(conv1x1_bn_supported(m, k, ncols) && (m * k) % 8 == 0, "bn1x1_addrelu: unsupported shape");
-  TORCH_CHECK(pcoef.is_cuda() && pcoef.scalar_type() == at::kFloat && pcoef.is_contiguous() && pcoef.numel() == 4 * (int64_t)k,
-              "bn1x1_addrelu: pcoef must be contiguous fp32 [4K]");
+  TORCH_CHECK(pcoef.is_cuda() && pcoef.scalar_type() == at::kFloat && pcoef.is_contiguous() &&
+                  pcoef.numel() == (split ? 2 : 4) * (int64_t)k,
+              "bn1x1_addrelu: pcoef must be contiguous fp32 [4K] ([2K] with split)");
+  TORCH_CHECK(!res_coef.has_value() || (split && res_coef->is_cuda() && res_coef->scalar_type() == at::kFloat &&
+                                        res_coef->is_contiguous() && res_coef->numel() == 2 * (int64_t)k),
+              "bn1x1_addrelu: res_coef (split form only) must be contiguous fp32 [2K]");
   if (shift.has_value())
     TORCH_CHECK(shift->is_cuda() && shift->scalar_type() == at::kFloat && shift->is_contiguous() && shift->numel() == ncols,
                 "bn1x1_addrelu: shift must be contiguous fp32 [ncols]");
@@ -250,7 +269,8 @@ std::vector<at::Tensor> bn1x1_addrelu(const at::Tensor& a, const at::Tensor& res
   auto part = at::empty({2, conv1x1_bn_partials(m, k, ncols, true, cus, true), ncols}, a.options().dtype(at::kFloat));
   conv1x1_bn(a.data_ptr(), w.data_ptr(), y.data_ptr(), m, k, ncols, false, dtype_code(a.scalar_type()),
              pcoef.data_ptr<float>(), shift.has_value() ? shift->data_ptr<float>() : nullptr, part.data_ptr<float>(), cus,
-             cur_stream(), nullptr, res.data_ptr(), out.data_ptr(), true, bits.data_ptr<uint8_t>());
+             cur_stream(), nullptr, res.data_ptr(), out.data_ptr(), true, bits.data_ptr<uint8_t>(), 0, 0, split,
+             res_coef.has_value() ? res_coef->data_ptr<float>() : nullptr);
   return {y, part, out, bits};
 }
 
@@ -603,8 +623,10 @@ void bind_conv(pybind11::module_& root) {
         pybind11::arg("py") = pybind11::none(), pybind11::arg("want_aout") = false, pybind11::arg("res_h") = 0,
         pybind11::arg("res_w") = 0);
   m.def("bn_finalize", &bn_finalize);
+  m.def("subsample2x", &subsample2x, pybind11::arg("x"), pybind11::arg("n"), pybind11::arg("h"), pybind11::arg("w"));
   m.def("bn1x1_addrelu", &bn1x1_addrelu, pybind11::arg("a"), pybind11::arg("res"), pybind11::arg("pcoef"),
-        pybind11::arg("w"), pybind11::arg("shift") = pybind11::none(), pybind11::arg("out") = pybind11::none());
+        pybind11::arg("w"), pybind11::arg("shift") = pybind11::none(), pybind11::arg("out") = pybind11::none(),
+        pybind11::arg("split") = false, pybind11::arg("res_coef") = pybind11::none());
   m.def("wgrad3x3", &wgrad3x3, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("stride"),
         pybind11::arg("xcoef") = pybind11::none(), pybind11::arg("out_dtype") = pybind11::none());
   m.def("dgrad_bnred", &dgrad_bnred, pybind11::arg("g"), pybind11::arg("w"), pybind11::arg("res"),

@@ -10,8 +10,13 @@
 // An optimizer steps the same parameter/state tensors every iteration, so after the first step
 // every multi-tensor launch finds its table resident on the device: no per-step H2D traffic and
 // no kernel-argument packing (the reference repacks <=110 addresses per launch on the host,
-// csrc/multi_tensor_apply.cuh:84-146).
+// csrc/multi_tensor_apply.cuh:84-146).  Gradients set to None between steps come back at new
+// addresses: a list whose STRUCTURE (device, stream, depth, chunk size, sizes) matches a cached
+// table gets that table's changed address rows patched in place (one small upload, ordered on
+// the stream after the launches that read the old rows) instead of a full rebuild — unless the
+// table may be replayed by a captured graph.
 #include "common.h"
+#include <algorithm>
 #include <list>
 #include <mutex>
 #include <unordered_map>
@@ -25,6 +30,8 @@ struct Entry {
   MtaMeta meta;
   bool pinned_forever = false;
   std::list<uint64_t>::iterator lru_it;
+  uint64_t shash = 0;    // hash of the structural part of the key
+  size_t off_ptrs = 0;   // byte offset of the [depth][nt] address rows in the table
 };
 
 std::mutex g_mu;
@@ -85,12 +92,73 @@ MtaMeta mta_meta(const std::vector<std::vector<at::Tensor>>& lists, int chunk_si
   }
   uint64_t h = 0x1234567ull;
   for (auto v : key) h = mix(h, v);
+  // structural hash: every key word but the addresses
+  uint64_t sh = 0x7654321ull;
+  for (int i = 0; i < 5; ++i) sh = mix(sh, key[i]);
+  for (int t = 0; t < nt; ++t) sh = mix(sh, key[5 + (size_t)t * (depth + 1)]);
 
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_cache.find(h);
   if (it != g_cache.end() && it->second.key == key) {
     g_lru.splice(g_lru.begin(), g_lru, it->second.lru_it);
     return it->second.meta;
+  }
+  hipStreamCaptureStatus cap0 = hipStreamCaptureStatusNone;
+  hipStreamIsCapturing(cur_stream(), &cap0);
+  if (cap0 == hipStreamCaptureStatusNone && (it == g_cache.end() || !it->second.pinned_forever)) {
+    // the structurally identical table with the most matching addresses (recently used first)
+    auto best = g_cache.end();
+    size_t best_match = 0;
+    for (uint64_t lh : g_lru) {
+      auto c = g_cache.find(lh);
+      if (c == g_cache.end() || c->second.pinned_forever || c->second.shash != sh || c->second.key.size() != key.size())
+        continue;
+      bool same = true;
+      size_t match = 0;
+      for (size_t i = 0; i < key.size() && same; ++i) {
+        const bool is_ptr = i >= 5 && (i - 5) % (size_t)(depth + 1) != 0;
+        if (is_ptr) match += c->second.key[i] == key[i];
+        else same = c->second.key[i] == key[i];
+      }
+      if (same && (best == g_cache.end() || match > best_match)) {
+        best = c;
+        best_match = match;
+      }
+    }
+    if (best != g_cache.end()) {
+      Entry e = std::move(best->second);
+      g_lru.erase(e.lru_it);
+      g_cache.erase(best);
+      auto clash = g_cache.find(h);  // the new hash held by a different (unpinned) key: drop it
+      if (clash != g_cache.end()) {
+        g_lru.erase(clash->second.lru_it);
+        g_cache.erase(clash);
+      }
+      // patch the span of address rows that changed ([depth][nt] layout in the table)
+      std::vector<uint64_t> rows((size_t)depth * nt);
+      for (int t = 0; t < nt; ++t)
+        for (int d = 0; d < depth; ++d) rows[(size_t)d * nt + t] = key[5 + (size_t)t * (depth + 1) + 1 + d];
+      size_t lo = rows.size(), hi = 0;
+      for (int t = 0; t < nt; ++t)
+        for (int d = 0; d < depth; ++d) {
+          const size_t r = (size_t)d * nt + t;
+          if (e.key[5 + (size_t)t * (depth + 1) + 1 + d] != rows[r]) {
+            lo = std::min(lo, r);
+            hi = std::max(hi, r + 1);
+          }
+        }
+      const c10::hip::HIPGuard guard(dev.index());
+      if (lo < hi)
+        mta_upload_bytes(e.dev.data_ptr<uint8_t>() + e.off_ptrs + lo * sizeof(uint64_t), rows.data() + lo,
+                         (hi - lo) * sizeof(uint64_t), cur_stream());
+      e.meta.aligned = aligned ? 1 : 0;
+      e.key = std::move(key);
+      g_lru.push_front(h);
+      e.lru_it = g_lru.begin();
+      MtaMeta m = e.meta;
+      g_cache[h] = std::move(e);
+      return m;
+    }
   }
   if (it != g_cache.end()) {  // hash collision with a different key: drop the old one
     if (!it->second.pinned_forever) {
@@ -182,6 +250,8 @@ MtaMeta mta_meta(const std::vector<std::vector<at::Tensor>>& lists, int chunk_si
   e.key = std::move(key);
   e.dev = devbuf;
   e.meta = m;
+  e.shash = sh;
+  e.off_ptrs = off_ptrs;
   e.lru_it = g_lru.begin();
   if (cap != hipStreamCaptureStatusNone) e.pinned_forever = true;
   g_cache[h] = std::move(e);

@@ -51,6 +51,11 @@ struct Args {
   // rows with even y and x get res[n][y / 2][x / 2] (the strided 1x1 downsample's data gradient)
   FastDiv rs_hw, rs_w;
   int rs_h2, rs_w2;
+  // PRO == kProBnAddRelu with pc_split: pcoef is the output BN's [scale | shift] [2][K] and pc_res
+  // the residual (downsample) BN's [2][K], null = identity; the [4][K] rows are assembled on the
+  // LDS load (no separate concatenation launch on the host side)
+  const float* pc_res;
+  int pc_split;
   const uint16_t* py;   // PRO == kProBnBwd: second operand tensor [M][K] (the BN's input)
   uint16_t* aout;       // PRO == kProBnBwd / kProBnAddRelu, nullable: the transformed operand written out [M][K]
   uint8_t* bout;        // PRO == kProBnAddRelu, nullable: its ReLU bits [M * K / 8] (bit j of byte i = element 8 i + j)
@@ -139,8 +144,22 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
       }
     }
   }
-  if constexpr (PRO != kProNone)
+  if constexpr (PRO == kProBnAddRelu) {
+    if (p.pc_split) {
+      for (int i = tid; i < 4 * KR; i += NT) {
+        const int row = i / KR, kk = i - row * KR;
+        float v;
+        if (row == 0 || row == 2) v = p.pcoef[(row >> 1) * KR + kk];
+        else if (p.pc_res) v = p.pc_res[(row >> 1) * KR + kk];
+        else v = row == 1 ? 1.f : 0.f;
+        pc[i] = v;
+      }
+    } else {
+      for (int i = tid; i < 4 * KR; i += NT) pc[i] = p.pcoef[i];
+    }
+  } else if constexpr (PRO != kProNone) {
     for (int i = tid; i < pro_rows(PRO) * KR; i += NT) pc[i] = p.pcoef[i];
+  }
   float sh[CN], s1[CN], s2[CN];
 #pragma unroll
   for (int cb = 0; cb < CN; ++cb) {
@@ -697,9 +716,13 @@ int conv1x1_bn_partials(int64_t m, int k, int ncols, bool pro, int cus, bool pro
 
 void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int ncols, bool w_kmajor_out, int dtype,
                 const float* pcoef, const float* shift, float* part, int cus, hipStream_t s, const void* res,
-                const void* py, void* aout, bool pro_relu, uint8_t* bout, int res_h, int res_w) {
+                const void* py, void* aout, bool pro_relu, uint8_t* bout, int res_h, int res_w, bool pc_split,
+                const float* pc_res) {
   if (!conv1x1_bn_supported(m, k, ncols)) throw std::runtime_error("conv1x1_bn: unsupported shape");
   c1bn::Args args{};
+  args.pc_split = pc_split ? 1 : 0;
+  args.pc_res = pc_res;
+  if (pc_split && !(py && pro_relu)) throw std::runtime_error("conv1x1_bn: split coefficients are an add + ReLU option");
   c1bn::set_res_geometry(args, m, res_h, res_w);
   args.a = static_cast<const uint16_t*>(a);
   args.w = static_cast<const uint16_t*>(w);

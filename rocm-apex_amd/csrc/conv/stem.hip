@@ -654,21 +654,27 @@ __global__ void __launch_bounds__(512, 1) wgrad_kernel(const BwdArgs a) {
   }
 }
 
-// dW[co][c][r][s] (strided, weight dtype) = sum over the G partials of k = r * 32 + s * 4 + c
+// dW[co][c][r][s] (strided, weight dtype) = sum over the G partials of k = r * 32 + s * 4 + c.
+// A block owns 64 consecutive elements of the flat [64][224] partial; its 4 thread groups take
+// every 4th partial (coalesced 256-byte rows, 64 loads per thread in flight instead of one thread
+// walking all G partials), then one LDS fold in group order (fixed order: deterministic).
 template <typename TW>
 __global__ void __launch_bounds__(256) wgrad_reduce(const float* __restrict__ ws, int G, int cin, int64_t s0,
                                                     int64_t s1, int64_t s2, int64_t s3, TW* __restrict__ dw) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= CO * cin * 49) return;
-  const int s = i % 7, r = (i / 7) % 7, c = (i / 49) % cin, co = i / (49 * cin);
-  const size_t off = (size_t)co * KT + r * KROW + s * 4 + c;
+  __shared__ float red[4][64];
+  const int e = blockIdx.x * 64 + (threadIdx.x & 63), grp = threadIdx.x >> 6;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  int j = 0;
-  for (; j + 3 < G; j += 4)
+  int j = grp;
+  for (; j + 12 < G; j += 16)
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc[u] += ws[(size_t)(j + u) * CO * KT + off];
-  for (; j < G; ++j) acc[0] += ws[(size_t)j * CO * KT + off];
-  dw[co * s0 + c * s1 + r * s2 + s * s3] = from_f<TW>((acc[0] + acc[1]) + (acc[2] + acc[3]));
+    for (int u = 0; u < 4; ++u) acc[u] += ws[(size_t)(j + 4 * u) * CO * KT + e];
+  for (; j < G; j += 4) acc[0] += ws[(size_t)j * CO * KT + e];
+  red[grp][threadIdx.x & 63] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  __syncthreads();
+  if (grp != 0) return;
+  const float v = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+  const int co = e / KT, k = e % KT, r = k / KROW, sx = (k % KROW) / 4, c = k % 4;
+  if (sx < 7 && c < cin) dw[co * s0 + c * s1 + r * s2 + sx * s3] = from_f<TW>(v);
 }
 
 inline void check_geo(const Geo& g) {
@@ -825,7 +831,7 @@ void stem_wgrad(const void* dp, const uint8_t* idx, const void* y, const float* 
   }, "stem wgrad");
   dispatch_float(dw_t, [&](auto tag) {
     using TW = typename decltype(tag)::type;
-    hipLaunchKernelGGL((stem::wgrad_reduce<TW>), dim3((stem::CO * cin * 49 + 255) / 256), dim3(256), 0, s, ws, G, cin,
+    hipLaunchKernelGGL((stem::wgrad_reduce<TW>), dim3(stem::CO * stem::KT / 64), dim3(256), 0, s, ws, G, cin,
                        dw_strides[0], dw_strides[1], dw_strides[2], dw_strides[3], (TW*)dw);
   }, "stem wgrad reduce");
   check_launch("stem_wgrad");

@@ -93,6 +93,9 @@ void conv_wgrad(const ConvTapArgs& a, const void* dy, void* dw_out, int out_dtyp
 // (y - shift) and (y - shift)^2 for the consuming batch norm, finalized by conv1x1_bn_finalize.
 // Shapes: k in {64, 128, 256, 512}, ncols % 64 == 0, bf16 / fp16, 16-byte aligned rows.
 bool conv1x1_bn_supported(int64_t m, int k, int ncols);
+// y [N][ceil(h/2)][ceil(w/2)][c] = x [N][h][w][c] at even (y, x): a stride-2 1x1 conv's operand
+// (csrc/conv/layout.hip; 16-bit, c % 8 == 0, 16-byte aligned)
+void conv_subsample2x(const void* x, void* y, int n, int h, int w, int c, int dtype, int cus, hipStream_t s);
 int conv1x1_bn_partials(int64_t m, int k, int ncols, bool pro, int cus, bool pro_addrelu = false);
 void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int ncols, bool w_kmajor_out, int dtype,
                 const float* pcoef, const float* shift, float* part, int cus, hipStream_t s,
@@ -101,8 +104,10 @@ void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int nco
                 void* aout = nullptr,         //   pcoef [3][k]; aout (nullable) receives a' [M][k]
                 bool pro_relu = false,        // forward form with py: a' = relu(c0 a + c1 py + c2) (the
                 uint8_t* bout = nullptr,      //   block output: BN + residual + ReLU), bits to bout
-                int res_h = 0, int res_w = 0);  // > 0: res is [N][ceil(res_h/2)][ceil(res_w/2)][ncols], the
-                                                //   stride-2 subsample's gradient, added at even (y, x) only
+                int res_h = 0, int res_w = 0,  // > 0: res is [N][ceil(res_h/2)][ceil(res_w/2)][ncols], the
+                                               //   stride-2 subsample's gradient, added at even (y, x) only
+                bool pc_split = false,         // add + ReLU form: pcoef = the output BN's [2][k] and pc_res
+                const float* pc_res = nullptr);  //   the residual BN's [2][k] (null: identity) instead of [4][k]
 // batch statistics from the partials: save_mean / save_invstd, running-stat EMA (nullable),
 // coef = [scale | shift] of the apply (w, b nullable = affine-free)
 void conv1x1_bn_finalize(const float* part, int g, int c, float n, const float* shift, const float* w, const float* b,

@@ -76,8 +76,43 @@ def _conv():
     return _native.require("conv").conv
 
 
+class _Census:
+    """APEX_AMD_BN_CENSUS=1 (diagnostics): count the node's batch-norm pass calls by (function,
+    tensor shapes) and print the table at exit — maps the standalone bnh::* kernels of a trace to
+    the BN they serve."""
+
+    def __init__(self, mod):
+        import atexit
+        import collections
+
+        self._mod, self._n = mod, collections.Counter()
+        atexit.register(self._dump)
+
+    def __getattr__(self, name):
+        fn = getattr(self._mod, name)
+
+        def wrap(*a, **k):
+            shapes = tuple(tuple(t.shape) for t in a if isinstance(t, torch.Tensor) and t.dim() == 2)
+            self._n[(name, shapes)] += 1
+            return fn(*a, **k)
+
+        return wrap
+
+    def _dump(self):
+        for (name, shapes), n in sorted(self._n.items(), key=lambda kv: -kv[1]):
+            print(f"[bn census] {n:5d} {name} {shapes}", flush=True)
+
+
+_CENSUS = [None]
+
+
 def _bn():
-    return _native.require("bn_nhwc").bn_nhwc
+    mod = _native.require("bn_nhwc").bn_nhwc
+    if os.environ.get("APEX_AMD_BN_CENSUS") == "1":
+        if _CENSUS[0] is None:
+            _CENSUS[0] = _Census(mod)
+        return _CENSUS[0]
+    return mod
 
 
 def _m2(t):
@@ -307,10 +342,11 @@ class _BottleneckFn(torch.autograd.Function):
         # conv1 (+ bn1 statistics) -> bn1 apply + ReLU; with a deferred block below, conv1 computes
         # that block's output (BN + shortcut + ReLU) on its operand load and writes it into x
         if link_in is not None and link_in.pend is not None:
-            y3p, resp, pc3, outp, _, _ = link_in.pend
+            y3p, resp, pc3, outp, _, _pcd = link_in.pend
             link_in.pend = None
             DEFERRED_TAKEN[0] += 1
-            y1, part1, _, link_in.bits = _conv().bn1x1_addrelu(y3p, resp, pc3, w1.view(width, cin), bn1.rm, out=outp)
+            y1, part1, _, link_in.bits = _conv().bn1x1_addrelu(y3p, resp, pc3, w1.view(width, cin), bn1.rm, out=outp,
+                                                               split=True, res_coef=_pcd)
             sm1, si1, c1, in1 = finalize_part(part1, float(x2.size(0)), bn1)
         else:
             y1, sm1, si1, c1, in1 = conv1x1_bn_fwd(x2, w1.view(width, cin), None, bn1)
@@ -334,7 +370,7 @@ class _BottleneckFn(torch.autograd.Function):
             if stride == 1:
                 yd, smd, sid, cd, ind = conv1x1_bn_fwd(x2, wds.view(cout, cin), None, bnd)
             elif _DS_SUB and stride == 2 and wds.size(2) == 1:
-                xs2 = _m2(x[:, :, ::2, ::2].contiguous(memory_format=torch.channels_last))
+                xs2 = _conv().subsample2x(x2, n, h, wd)
                 yd, smd, sid, cd, ind = conv1x1_bn_fwd(xs2, wds.view(cout, cin), None, bnd)
             else:
                 yd = _m2(_conv_fwd(x, wds, stride, 0))
@@ -342,12 +378,11 @@ class _BottleneckFn(torch.autograd.Function):
         if link_out is not None and link_out.defer:
             # the block above computes this output in its conv1 (BlockLink docstring)
             res = x2 if wds is None else yd
-            sc, sh = c3[:cout], c3[cout:]
-            # [a scale | res scale | a shift | res shift]: the apply passes' arithmetic exactly
-            pc3 = (torch.cat([sc, torch.ones_like(sc), sh, torch.zeros_like(sh)]) if wds is None
-                   else torch.cat([sc, cd[:cout], sh, cd[cout:]]))
+            # the consumer's prologue takes bn3's [scale | shift] and the downsample BN's (None: the
+            # identity shortcut, scale 1 / shift 0) and assembles [a scale | res scale | a shift |
+            # res shift] on its LDS load: the apply passes' arithmetic exactly, no concatenation
             out2, bits = torch.empty_like(y3), None
-            link_out.pend = (y3, res, pc3, out2, c3, cd)
+            link_out.pend = (y3, res, c3, out2, c3, cd)
         elif wds is None:
             out2, bits = _bn().apply(y3, x2, c3, True, True)
         else:

@@ -269,6 +269,11 @@ def test_gpu_bn1x1_addrelu_matches_apply_pass(m, k, ncols, dual):
     y, part, out, bits = ext.bn1x1_addrelu(y3, res, pc, w, shift)
     assert torch.equal(out, want.view_as(out))
     assert torch.equal(bits.view(-1), want_bits.view(-1))
+    # the split-coefficient form (bn3's [2K] and the downsample BN's [2K] or None, assembled on the
+    # kernel's LDS load) is bitwise the concatenated one
+    y_s, part_s, out_s, bits_s = ext.bn1x1_addrelu(y3, res, c3, w, shift, split=True, res_coef=cd if dual else None)
+    assert torch.equal(out_s, out) and torch.equal(bits_s, bits) and torch.equal(y_s, y)
+    assert torch.equal(part_s, part)
     ref = out.float() @ w.float().t()
     _close(y, ref, 1e-2)
     d = y.float() - shift
@@ -316,3 +321,13 @@ def test_gpu_dgrad_subsampled_residual(n, h, w, k, nc, red):
     _close(out, ref, 2e-2)
     torch.testing.assert_close(out, out_d)
     torch.testing.assert_close(part, part_d)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,w,c", [(2, 56, 56, 256), (3, 7, 9, 64), (1, 28, 28, 1024)])
+def test_gpu_subsample2x(n, h, w, c):
+    """The stride-2 1x1 operand: y[n][i][j] = x[n][2i][2j], dense NHWC rows (csrc/conv/layout.hip)."""
+    ext = _ext()
+    x = torch.randn(n * h * w, c, device="cuda").to(torch.bfloat16)
+    y = ext.subsample2x(x, n, h, w)
+    assert torch.equal(y, x.view(n, h, w, c)[:, ::2, ::2].reshape(-1, c))

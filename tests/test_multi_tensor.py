@@ -224,3 +224,29 @@ def test_l2norm_mp_inf_in_early_chunk_many_chunks(device):
         torch.testing.assert_close(total, exp.reshape(1), rtol=1e-4, atol=1e-4)
         torch.testing.assert_close(per, torch.stack([x.norm() for x in xs]), rtol=1e-4, atol=1e-4)
         assert int(noop.item()) == 0
+
+
+@pytest.mark.gpu
+def test_new_addresses_patch_the_cached_table_gpu():
+    """Gradients set to None between steps come back at new addresses: a structurally identical
+    list patches the cached table's address rows (mta_host.cpp) instead of adding a table, and the
+    op reads the NEW tensors (not the old addresses)."""
+    amp_C.mta_cache_clear()
+    noop = _noop("cuda")
+    keep = []
+    for step in range(4):
+        xs = _lists("cuda", torch.float32, SIZES)
+        keep.append(xs)  # hold the old lists so the allocator cannot hand the same addresses back
+        ys = [torch.empty_like(x) for x in xs]
+        amp_C.multi_tensor_scale(CHUNK, noop, [xs, ys], 2.0)
+        for x, y in zip(xs, ys):
+            torch.testing.assert_close(y, x * 2.0)
+        if step == 0:
+            n1 = amp_C.mta_cache_size()
+    assert amp_C.mta_cache_size() == n1
+    # an exact repeat of an older list is still correct (it patches back)
+    ys = [torch.empty_like(x) for x in keep[0]]
+    amp_C.multi_tensor_scale(CHUNK, noop, [keep[0], ys], 3.0)
+    for x, y in zip(keep[0], ys):
+        torch.testing.assert_close(y, x * 3.0)
+    assert noop.item() == 0

@@ -1,0 +1,9 @@
+#!/bin/bash
+# A/B: every bottleneck 1x1 on the native fused kernels (stage 3/4 included) vs the per-shape routes;
+# fresh 3x3 fprop tile-configuration sweep
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r05j
+mkdir -p $O
+bash tools/ab_bench.sh r05j_native "APEX_AMD_FUSED_BLOCK_FORCE_NATIVE=0" "APEX_AMD_FUSED_BLOCK_FORCE_NATIVE=1" 2 || exit 1
+timeout -k 10 600 python -u tools/conv_cfg_sweep.py > $O/cfg_sweep.jsonl 2>&1; tail -3 $O/cfg_sweep.jsonl | cut -c1-300

@@ -64,7 +64,7 @@ def main():
     counters, durations = load(a.dir, a.by_grid)
     rows = []
     for k in sorted(set(counters) | set(durations)):
-        if a.filter not in k:
+        if not any(f in k for f in a.filter.split("|")):
             continue
         c = {n: sum(v) / len(v) for n, v in counters[k].items()}
         dur = sorted(durations.get(k, [0.0]))[len(durations.get(k, [0.0])) // 2]
