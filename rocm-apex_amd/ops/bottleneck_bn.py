@@ -42,9 +42,13 @@ from .. import _native
 from . import conv as convops
 
 _ENABLED = os.environ.get("APEX_AMD_FUSED_BLOCK", "1") != "0"
-# tests: take every native 1x1 route the kernels support, whatever the size (small test shapes
-# would otherwise route to the library)
-FORCE_NATIVE = os.environ.get("APEX_AMD_FUSED_BLOCK_FORCE_NATIVE", "0") == "1"
+# take every native 1x1 route the kernels support, whatever the size.  The per-op routes below
+# were chosen op by op in round 3 (hipBLASLt ahead on the plain stage-3/4 GEMMs); with the fused
+# kernels of round 4-5 the whole-step A/B favours native everywhere: the statistics epilogue, the
+# deferred output and the masked-dgrad reduction remove more standalone BN passes than the GEMM
+# loses (12,404-12,410 vs 12,339-12,350 img/s same box, profiles/r05/ab_force_native_r05j.txt).
+# APEX_AMD_FUSED_BLOCK_FORCE_NATIVE=0 restores the per-op routes.
+FORCE_NATIVE = os.environ.get("APEX_AMD_FUSED_BLOCK_FORCE_NATIVE", "1") == "1"
 _NATIVE_K = (64, 128, 256, 512)
 # conv3's fused data + weight gradient (csrc/conv/conv3_bwd.hip); 0 = the two-kernel path (A/B)
 _C3B = os.environ.get("APEX_AMD_CONV3_BWD", "1") != "0"
