@@ -623,6 +623,7 @@ void bind_conv(pybind11::module_& root) {
         pybind11::arg("py") = pybind11::none(), pybind11::arg("want_aout") = false, pybind11::arg("res_h") = 0,
         pybind11::arg("res_w") = 0);
   m.def("bn_finalize", &bn_finalize);
+  m.def("hfp_set_mode", &conv_hfp_set_mode, pybind11::arg("mode"));
   m.def("subsample2x", &subsample2x, pybind11::arg("x"), pybind11::arg("n"), pybind11::arg("h"), pybind11::arg("w"));
   m.def("bn1x1_addrelu", &bn1x1_addrelu, pybind11::arg("a"), pybind11::arg("res"), pybind11::arg("pcoef"),
         pybind11::arg("w"), pybind11::arg("shift") = pybind11::none(), pybind11::arg("out") = pybind11::none(),

@@ -439,13 +439,17 @@ bool conv_hfp_supported(const ConvTapArgs& a) {
 // M tiles are mostly ragged: fwd 98 vs 109 us, dgrad 87 vs 123 us at 7x7x512 bs 256); at 14 x 14 /
 // 28 x 28 the tap GEMM is as fast or faster (76 vs 73 / 102 vs 97 us dgrad; profiles/r05/
 // halo_fprop_ab_r05d.jsonl).  APEX_AMD_CONV_HFP=0: never, =all: wherever supported.
+static int g_hfp_mode = -1;  // conv_hfp_set_mode: -1 = the environment's choice
+void conv_hfp_set_mode(int mode) { g_hfp_mode = mode; }
+
 bool conv_hfp_default(const ConvTapArgs& a) {
-  static const int mode = [] {
+  static const int env_mode = [] {
     const char* e = std::getenv("APEX_AMD_CONV_HFP");
     if (e && e[0] == '0') return 0;
     if (e && e[0] == 'a') return 2;
     return 1;
   }();
+  const int mode = g_hfp_mode >= 0 ? g_hfp_mode : env_mode;
   if (mode == 0 || !conv_hfp_supported(a)) return false;
   return mode == 2 || (int64_t)a.oh * a.ow <= 64;
 }

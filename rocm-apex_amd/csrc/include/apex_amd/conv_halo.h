@@ -8,6 +8,8 @@
 namespace apex_amd {
 
 bool conv_hfp_supported(const ConvTapArgs& a);
+// 0: never, 1: small images (the default), 2: wherever supported; -1: back to APEX_AMD_CONV_HFP
+void conv_hfp_set_mode(int mode);
 bool conv_hfp_default(const ConvTapArgs& a);
 int conv_hfp_stats_rows(const ConvTapArgs& a, int cus);  // statistics partial rows (workgroups per k-block)
 void conv_hfp(const ConvTapArgs& a, const float* pcoef, int cus, hipStream_t s);

@@ -280,7 +280,10 @@ def conv_tap_dgrad(gy, w, x_shape, stride, pad, mask=None):
     for ph, pw, oh, ow, taps in phases:
         if not taps or oh <= 0 or ow <= 0:
             continue
-        wt = torch.stack([wk[:, r, s_, :] for r, s_, _, _ in taps], 1).contiguous()  # [C, taps, K]
+        if len(taps) == k * k:  # every tap in (r, s) row-major order: one permute-copy, no stack
+            wt = wk.reshape(c, k * k, kout).contiguous()  # [C, taps, K]
+        else:
+            wt = torch.stack([wk[:, r, s_, :] for r, s_, _, _ in taps], 1).contiguous()
         ext.tap_fprop(_nhwc(gy), wt, _nhwc(dx), oh, ow, 1, 1, stride, stride, ph, pw,
                       [t[2] for t in taps], [t[3] for t in taps], mask=None if mask is None else _nhwc(mask))
     return dx
