@@ -107,8 +107,13 @@ c10::optional<at::Tensor> tap_fprop(const at::Tensor& in, const at::Tensor& w, a
     TORCH_CHECK(pcoef->is_cuda() && pcoef->scalar_type() == at::kFloat && pcoef->is_contiguous() &&
                     pcoef->numel() == 2 * in.size(3),
                 "conv tap_fprop: pcoef must be a contiguous fp32 [2C] tensor");
-    TORCH_CHECK(conv_hfp_supported(a), "conv tap_fprop: the BN prologue needs the halo-tile kernel's shapes "
-                "(3x3 stride 1, C % 64 == 0, K % 128 == 0, no fused epilogue)");
+    // the spatial-tile 64 -> 64 kernel where it is the route, else the halo-tile kernel
+    if (conv_sp_default(a)) {
+      conv_sp_fprop_pro(a, pcoef->data_ptr<float>(), cus, cur_stream());
+      return made;
+    }
+    TORCH_CHECK(conv_hfp_supported(a), "conv tap_fprop: the BN prologue needs the spatial-tile (64 -> 64) or "
+                "halo-tile kernel's shapes (3x3 stride 1, C % 64 == 0, K % 128 == 0, no fused epilogue)");
     conv_hfp(a, pcoef->data_ptr<float>(), cus, cur_stream());
     return made;
   }
@@ -118,7 +123,7 @@ c10::optional<at::Tensor> tap_fprop(const at::Tensor& in, const at::Tensor& w, a
 
 // dw[k, t, c] (fp32-accumulated, written in dw's dtype) for the forward `in` -> dy geometry
 void wgrad(const at::Tensor& in, const at::Tensor& dy, at::Tensor& dw_out, int64_t ish, int64_t isw,
-           std::vector<int64_t> dh, std::vector<int64_t> dw) {
+           std::vector<int64_t> dh, std::vector<int64_t> dw, const c10::optional<at::Tensor>& xcoef) {
   check_nhwc(dy, "grad");
   TORCH_CHECK(dw_out.is_cuda() && dw_out.dim() == 3 && dw_out.is_contiguous(), "conv wgrad: dw must be [K, taps, C]");
   TORCH_CHECK(dw_out.size(0) == dy.size(3) && dw_out.size(1) == (int64_t)dh.size() && dw_out.size(2) == in.size(3),
@@ -131,6 +136,17 @@ void wgrad(const at::Tensor& in, const at::Tensor& dy, at::Tensor& dw_out, int64
   const c10::hip::HIPGuard g(in.get_device());
   TORCH_CHECK(conv_wgrad_supported(a), "conv wgrad: unsupported shape");
   const int cus = device_cus(in.get_device());
+  if (xcoef.has_value()) {
+    // input through the producing BN + ReLU: the halo-tile kernel only
+    TORCH_CHECK(xcoef->is_cuda() && xcoef->scalar_type() == at::kFloat && xcoef->is_contiguous() &&
+                    xcoef->numel() == 2 * in.size(3),
+                "conv wgrad: xcoef must be a contiguous fp32 [2C] tensor");
+    TORCH_CHECK(conv_hwgrad_supported(a), "conv wgrad: the BN prologue needs the halo-tile kernel's shapes");
+    auto ws = at::empty({conv_hwgrad_workspace_floats(a, cus)}, in.options().dtype(at::kFloat));
+    conv_hwgrad_pro(a, dy.data_ptr(), dw_out.data_ptr(), dtype_code(dw_out.scalar_type()), ws.data_ptr<float>(), cus,
+                    cur_stream(), xcoef->data_ptr<float>());
+    return;
+  }
   auto ws = at::empty({conv_wgrad_workspace_floats(a, cus)}, in.options().dtype(at::kFloat));
   conv_wgrad(a, dy.data_ptr(), dw_out.data_ptr(), dtype_code(dw_out.scalar_type()), ws.data_ptr<float>(), cus,
              cur_stream());
@@ -612,7 +628,9 @@ void bind_conv(pybind11::module_& root) {
     a.dtype = kBF16;
     return conv_hfp_supported(a);
   });
-  m.def("wgrad", &wgrad);
+  m.def("wgrad", &wgrad, pybind11::arg("x"), pybind11::arg("dy"), pybind11::arg("dw"), pybind11::arg("ish"),
+        pybind11::arg("isw"), pybind11::arg("dh"), pybind11::arg("dw_taps"),
+        pybind11::arg("xcoef") = pybind11::none());
   m.def("force_fprop_cfg", &conv_force_fprop_cfg);
   m.def("force_wgrad_variant", &conv_force_wgrad_variant);
   m.def("halo_wgrad_supported", &halo_wgrad_supported);

@@ -669,9 +669,20 @@ inline int grid_x(int64_t m, int nc, int kr, int pro, int cus, int ncols, bool r
 // column tile: the widest of 256 / 128 / 64 that divides ncols (256 needs the 128 accumulator
 // registers of 8 blocks; the register file holds it at 2 waves / SIMD; at k = 512 its weight
 // image would not fit the LDS)
+// The deepest reduction that still takes the 256- / 128-column tile (APEX_AMD_C1BN_NC256_MAXK,
+// APEX_AMD_C1BN_NC128_MAXK: A/B knobs).  At k = 256 the 256-column weight image (135 KB) leaves
+// one 4-wave workgroup per CU, which streams at about half the rate of 8 waves: 128 columns there
+// re-read the operand from L2 twice as often but run 2 workgroups per CU — +1.6 % on the whole
+// ResNet-50 step (12,109-12,168 -> 12,323-12,336 img/s same box, profiles/r05/ab_c1bn_nc_r05o.txt).
+inline int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
 inline int col_tile(int ncols, int kr) {
-  if (ncols % 256 == 0 && kr <= 256) return 256;
-  return ncols % 128 == 0 ? 128 : 64;
+  static const int max256 = env_int("APEX_AMD_C1BN_NC256_MAXK", 128);
+  static const int max128 = env_int("APEX_AMD_C1BN_NC128_MAXK", 512);
+  if (ncols % 256 == 0 && kr <= 256 && kr <= max256) return 256;
+  return ncols % 128 == 0 && kr <= max128 ? 128 : 64;
 }
 
 template <typename T, bool WT, int PRO, bool STATS, bool RED = false>

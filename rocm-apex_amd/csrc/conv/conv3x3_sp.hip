@@ -21,6 +21,7 @@
 // Optional epilogue: BN statistics partials (sum / sum of squares of y - shift) per workgroup,
 // rows = the persistent grid size (conv_sp_grid), for the consuming batch norm's finalize.
 #include "apex_amd/conv_api.h"
+#include "apex_amd/conv_halo.h"
 #include "apex_amd/dispatch.h"
 #include "apex_amd/mfma.h"
 
@@ -51,6 +52,7 @@ struct Args {
   int toff[9];        // per tap: (dh * HW + dw) * PS, the halo offset of the tap's window
   float* stats;       // nullable: [2][gridDim.x][64]
   const float* shift; // nullable
+  const float* pcoef; // PRO: [2][64] x' = relu(x * pcoef[c] + pcoef[64 + c]) (the producing BN + ReLU)
 };
 
 // LDS-only barrier: this wave's LDS accesses complete, then a raw s_barrier (__syncthreads()
@@ -65,7 +67,10 @@ __device__ __forceinline__ void lds_barrier() {
 // holds channels 16 lh .. 16 lh + 15 in register order (crow(r, lh) -> 16 lh + r)
 __device__ __forceinline__ int chan_of_row(int j) { return 16 * ((j >> 2) & 1) + (j & 3) + 4 * (j >> 3); }
 
-template <typename T, bool STATS>
+// PRO: the next tile's halo is transformed in registers (one 16-byte chunk per k-step in the
+// second half of the current tile's MFMA loop, when its loads have landed); the padding taps and
+// out-of-image slots stay exact zeros (the mask is the fetch's)
+template <typename T, bool STATS, bool PRO>
 __global__ void __launch_bounds__(NT, 1) fprop_kernel(const Args p) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   uint16_t* halo = lds;
@@ -81,6 +86,29 @@ __global__ void __launch_bounds__(NT, 1) fprop_kernel(const Args p) {
 
   const int tiles_img = p.tiles_x * p.tiles_y;
   uint4 hr[HPT];
+  uint32_t hok = 0;  // bit i: chunk i of the fetched halo lies inside the image
+  // a thread's halo chunks all hold channels 8 (tid & 7) .. + 7 (NT % 8 == 0)
+  float ps[PRO ? 8 : 1], pb[PRO ? 8 : 1];
+  if constexpr (PRO) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      ps[e] = p.pcoef[(tid & 7) * 8 + e];
+      pb[e] = p.pcoef[C + (tid & 7) * 8 + e];
+    }
+  }
+  auto xform = [&](int i) {
+    if constexpr (PRO) {
+      if ((hok >> i) & 1u) {
+        float v[8];
+        Vec8<T>::load(v, reinterpret_cast<const T*>(&hr[i]));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(v[e], ps[e], pb[e]), 0.f);
+        Vec8<T>::store(reinterpret_cast<T*>(&hr[i]), v);
+      } else {
+        hr[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
   // halo of tile `tile` -> registers (zero outside the image; every load unconditional on a
   // clamped address, the zero chosen after)
   auto fetch = [&](int tile) {
@@ -88,6 +116,7 @@ __global__ void __launch_bounds__(NT, 1) fprop_kernel(const Args p) {
     const int ty = rem / p.tiles_x, tx = rem - ty * p.tiles_x;
     const int y0 = ty * TH - 1, x0 = tx * TW - 1;
     const uint16_t* xb = p.x + (int64_t)img * p.h * p.wd * C;
+    hok = 0;
 #pragma unroll
     for (int i = 0; i < HPT; ++i) {
       const int q = tid + NT * i;
@@ -97,7 +126,9 @@ __global__ void __launch_bounds__(NT, 1) fprop_kernel(const Args p) {
       const bool ok = q < HCH && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.wd;
       const int cy = min(max(iy, 0), p.h - 1), cx = min(max(ix, 0), p.wd - 1);
       const uint4 v = *reinterpret_cast<const uint4*>(xb + ((int64_t)cy * p.wd + cx) * C + c8);
-      hr[i] = ok ? v : make_uint4(0, 0, 0, 0);
+      hok |= ok ? 1u << i : 0u;
+      if constexpr (PRO) hr[i] = v;  // the mask is applied with the transform (xform)
+      else hr[i] = ok ? v : make_uint4(0, 0, 0, 0);
     }
   };
   auto commit = [&]() {
@@ -120,6 +151,8 @@ __global__ void __launch_bounds__(NT, 1) fprop_kernel(const Args p) {
   int tile = blockIdx.x;
   const int tlast = p.ntiles - 1;
   fetch(min(tile, tlast));
+#pragma unroll
+  for (int i = 0; i < HPT; ++i) xform(i);
   commit();
   __syncthreads();
   // this lane's B-fragment base: output row 2 wid + b of the tile, column lr, halo (+1, +1)
@@ -160,8 +193,14 @@ __global__ void __launch_bounds__(NT, 1) fprop_kernel(const Args p) {
       acc[0][1] = mma<T>(fw[sl][1], fx[sl][0], acc[0][1]);
       acc[1][0] = mma<T>(fw[sl][0], fx[sl][1], acc[1][0]);
       acc[1][1] = mma<T>(fw[sl][1], fx[sl][1], acc[1][1]);
+      // PRO: one chunk of the next tile's halo per k-step from step 20 on (its loads have had 20
+      // steps of MFMAs to land), VALU under the MFMA pipe
+      if constexpr (PRO) {
+        if (st >= 20 && st - 20 < HPT) xform(st - 20);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
+    static_assert(!PRO || 20 + HPT <= NS, "halo transform steps");
 
     // every wave is done reading this tile's halo: commit the next one (the compiler waits for
     // the prefetch loads only), then the epilogue — its stores stay in flight under the next
@@ -266,7 +305,9 @@ int conv_sp_grid(const ConvTapArgs& a, int cus) {
   return (int)std::min<int64_t>(tiles, cus);
 }
 
-void conv_sp_fprop(const ConvTapArgs& a, int cus, hipStream_t s) {
+void conv_sp_fprop(const ConvTapArgs& a, int cus, hipStream_t s) { conv_sp_fprop_pro(a, nullptr, cus, s); }
+
+void conv_sp_fprop_pro(const ConvTapArgs& a, const float* pcoef, int cus, hipStream_t s) {
   if (!conv_sp_supported(a)) throw std::runtime_error("conv_sp_fprop: unsupported shape / epilogue");
   csp::Args p;
   p.x = static_cast<const uint16_t*>(a.in);
@@ -283,6 +324,7 @@ void conv_sp_fprop(const ConvTapArgs& a, int cus, hipStream_t s) {
   for (int t = 0; t < 9; ++t) p.toff[t] = (a.dh[t] * csp::HW + a.dw[t]) * csp::PS;
   p.stats = a.stats;
   p.shift = a.stats_shift;
+  p.pcoef = pcoef;
   const int grid = conv_sp_grid(a, cus);
   dispatch_16(a.dtype, [&](auto tag) {
     using T = typename decltype(tag)::type;
@@ -293,8 +335,13 @@ void conv_sp_fprop(const ConvTapArgs& a, int cus, hipStream_t s) {
                                 (int)csp::LDS);
       hipLaunchKernelGGL(kern, dim3(grid), dim3(csp::NT), csp::LDS, s, p);
     };
-    if (a.stats) go(csp::fprop_kernel<T, true>);
-    else go(csp::fprop_kernel<T, false>);
+    if (pcoef) {
+      if (a.stats) go(csp::fprop_kernel<T, true, true>);
+      else go(csp::fprop_kernel<T, false, true>);
+    } else {
+      if (a.stats) go(csp::fprop_kernel<T, true, false>);
+      else go(csp::fprop_kernel<T, false, false>);
+    }
   }, "conv_sp_fprop");
   check_launch("conv_sp_fprop");
 }

@@ -25,6 +25,7 @@
 // (apex/contrib/csrc/bottleneck/bottleneck.cpp:2236 bottleneck_backward_wgrad2), which run on
 // cuDNN there and not at all on ROCm.
 #include "apex_amd/conv_api.h"
+#include "apex_amd/conv_halo.h"
 #include "apex_amd/dispatch.h"
 #include "apex_amd/mfma.h"
 
@@ -99,7 +100,7 @@ __device__ __forceinline__ s16x8 frag2(const uint16_t* lo, const uint16_t* hi) {
   return s16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
-template <typename T, int TK, int HSL, int HC>
+template <typename T, int TK, int HSL, int HC, bool PRO>
 __global__ void __launch_bounds__(NT, 1) wgrad_kernel(const Args p) {
   using C = Cfg<TK, HSL, HC>;
   constexpr int KB = C::KB;
@@ -151,8 +152,29 @@ __global__ void __launch_bounds__(NT, 1) wgrad_kernel(const Args p) {
     hrel[i] = (((gi * p.h + hy - 1) * p.w) + hx - 1) * p.c * 2 + (c0 + 8 * sc) * 2;
     hfl[i] = (ok ? 1u : 0u) | (hy == 0 ? 2u : 0u) | (hy == p.HR - 1 ? 4u : 0u);
   }
+  // PRO (the producing BN + ReLU, x' = relu(x * xcoef[c] + xcoef[C + c])): every lane rewrites the
+  // 16-byte halo chunks IT loaded once their DMA has landed (no barrier needed before that; the
+  // stage's publishing barrier follows), interleaved with the previous tile's MFMA slices.
+  // Chunks the DMA zero-filled (padding, ragged tails, images past the batch) stay zero.  A
+  // lane's chunks hold channel group (lane & 7) or (lane & 7) ^ 4 (the slot's swizzle bit).
+  float xs[PRO ? 2 : 1][8], xb[PRO ? 2 : 1][8];
+  uint32_t hsw = 0;
+  if constexpr (PRO) {
+#pragma unroll
+    for (int gsel = 0; gsel < 2; ++gsel) {
+      const int ch = c0 + 8 * ((lane & 7) ^ (4 * gsel));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        xs[gsel][e] = p.xcoef[ch + e];
+        xb[gsel][e] = p.xcoef[p.c + ch + e];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < C::HW; ++i)
+      if (swz<64>(8 * (i * 4 + wave) + (lane >> 3))) hsw |= 1u << i;
+  }
 
-  auto issue = [&](int t, int stage) {
+  auto issue = [&](int t, int stage) -> uint32_t {
     const int px0 = t * p.np;
     const int y0 = (t % p.tpi) * p.R;
     const uint32_t kill = (y0 == 0 ? 2u : 0u) | (y0 + p.R == p.h ? 4u : 0u);
@@ -164,11 +186,26 @@ __global__ void __launch_bounds__(NT, 1) wgrad_kernel(const Args p) {
       bdma16(dr, voff, base + (i * 4 + wave) * 512);
     }
     const int xo = px0 * p.c * 2;
+    uint32_t vm = 0;  // bit i: halo chunk i of this lane holds image data (PRO rewrites it)
 #pragma unroll
     for (int i = 0; i < C::HW; ++i) {
       const bool valid = (hfl[i] & 1u) && !(hfl[i] & kill);
+      vm |= valid ? 1u << i : 0u;
       const uint32_t voff = valid ? (uint32_t)(xo + hrel[i]) : 0x80000000u;
       bdma16(xr, voff, base + C::DY_EL + (i * 4 + wave) * 512);
+    }
+    return vm;
+  };
+  auto xform = [&](int stage, uint32_t vm, int i) {
+    if constexpr (PRO) {
+      if (!((vm >> i) & 1u)) return;
+      uint16_t* q = lds + stage * C::STAGE_EL + C::DY_EL + (i * 4 + wave) * 512 + lane * 8;
+      const int gsel = (hsw >> i) & 1u;
+      float v[8];
+      Vec8<T>::load(v, reinterpret_cast<const T*>(q));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(v[e], gsel ? xs[1][e] : xs[0][e], gsel ? xb[1][e] : xb[0][e]), 0.f);
+      Vec8<T>::store(reinterpret_cast<T*>(q), v);
     }
   };
 
@@ -210,9 +247,22 @@ __global__ void __launch_bounds__(NT, 1) wgrad_kernel(const Args p) {
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[i][t] = zero16();
 
+  uint32_t vq0 = 0, vq1 = 0, vq2 = 0;  // halo valid masks of tiles it, it + 1, it + 2
 #pragma unroll
   for (int st = 0; st < S - 1; ++st)
-    if (st < nt) issue(t_begin + st, st);
+    if (st < nt) {
+      const uint32_t m = issue(t_begin + st, st);
+      if (st == 0) vq0 = m;
+      else vq1 = m;
+    }
+  if constexpr (PRO) {
+    if (nt > 0) {  // tile 0's own chunks (tile 1's DMA may stay in flight)
+      if (nt > 1 && S > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::PER) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < C::HW; ++i) xform(0, vq0, i);
+    }
+  }
 
   for (int it = 0; it < nt; ++it) {
     // this wave's DMA of tile it has landed (younger tiles may still be in flight); the barrier
@@ -223,8 +273,9 @@ __global__ void __launch_bounds__(NT, 1) wgrad_kernel(const Args p) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (it + S - 1 < nt) issue(t_begin + it + S - 1, (it + S - 1) % S);
+    if (it + S - 1 < nt) vq2 = issue(t_begin + it + S - 1, (it + S - 1) % S);
     const uint16_t* sb = lds + (it % S) * C::STAGE_EL;
+    const bool xnext = PRO && it + 1 < nt;  // PRO: rewrite tile it + 1's chunks under these MFMAs
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       s16x8 af[TK], bf[9];
@@ -240,7 +291,20 @@ __global__ void __launch_bounds__(NT, 1) wgrad_kernel(const Args p) {
       for (int t = 0; t < 9; ++t)
 #pragma unroll
         for (int i = 0; i < TK; ++i) acc[i][t] = mma<T>(af[i], bf[t], acc[i][t]);
+      if constexpr (PRO) {
+        if (xnext) {
+          if (s == 0) {  // tile it + 1's DMA landed (tile it + 2's may stay in flight)
+            if (S > 2 && it + 2 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::PER) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+#pragma unroll
+          for (int i = s * C::HW / NS; i < (s + 1) * C::HW / NS; ++i) xform((it + 1) % S, vq1, i);
+        }
+      }
     }
+    vq0 = vq1;
+    vq1 = vq2;
+    vq2 = 0;
   }
 
   // ---- fp32 partial block: lane holds c = c0 + 32 ct + lr, k rows crow(r, lh) ----
@@ -379,6 +443,11 @@ int64_t conv_hwgrad_workspace_floats(const ConvTapArgs& a, int cus) {
 
 void conv_hwgrad(const ConvTapArgs& a, const void* dy, void* dw_out, int out_dtype, float* ws, int cus,
                  hipStream_t s) {
+  conv_hwgrad_pro(a, dy, dw_out, out_dtype, ws, cus, s, nullptr);
+}
+
+void conv_hwgrad_pro(const ConvTapArgs& a, const void* dy, void* dw_out, int out_dtype, float* ws, int cus,
+                     hipStream_t s, const float* xcoef) {
   if (!conv_hwgrad_supported(a) || ((uintptr_t)dy & 15) || ((uintptr_t)dw_out & 15) || ((uintptr_t)ws & 15))
     throw std::runtime_error("conv_hwgrad: unsupported shape / dtype / alignment");
   const hwg::Plan pl = hwg::make_plan(a, cus);
@@ -386,7 +455,7 @@ void conv_hwgrad(const ConvTapArgs& a, const void* dy, void* dw_out, int out_dty
   p.x = static_cast<const uint16_t*>(a.in);
   p.dy = static_cast<const uint16_t*>(dy);
   p.ws = ws;
-  p.xcoef = nullptr;
+  p.xcoef = xcoef;
   p.h = a.ih;
   p.w = a.iw;
   p.c = a.c;
@@ -427,10 +496,11 @@ void conv_hwgrad(const ConvTapArgs& a, const void* dy, void* dw_out, int out_dty
       if (!seen) (void)hipFuncSetAttribute(fp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(kern, dim3(grid), dim3(hwg::NT), lds, s, p);
     };
-#define HWG_CASE(TK_, HSL_, HC_)                                                   \
-  if (pl.tk == TK_ && pl.hsl == HSL_ && pl.HC == HC_) {                            \
-    go(hwg::wgrad_kernel<T, TK_, HSL_, HC_>, hwg::Cfg<TK_, HSL_, HC_>::LDS);       \
-    return;                                                                        \
+#define HWG_CASE(TK_, HSL_, HC_)                                                          \
+  if (pl.tk == TK_ && pl.hsl == HSL_ && pl.HC == HC_) {                                   \
+    if (xcoef) go(hwg::wgrad_kernel<T, TK_, HSL_, HC_, true>, hwg::Cfg<TK_, HSL_, HC_>::LDS); \
+    else go(hwg::wgrad_kernel<T, TK_, HSL_, HC_, false>, hwg::Cfg<TK_, HSL_, HC_>::LDS);      \
+    return;                                                                               \
   }
     HWG_CASE(1, 224, 12) HWG_CASE(1, 256, 16) HWG_CASE(1, 256, 32) HWG_CASE(1, 256, 60)
 #undef HWG_CASE

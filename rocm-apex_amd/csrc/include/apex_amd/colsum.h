@@ -20,7 +20,11 @@ namespace apex_amd {
 
 template <int VEC>
 struct ColSum {
-  static __host__ __device__ __forceinline__ int ks(int tx, int ty) { return tx * ty + 8; }
+  // row pitch TX*TY + 4 words: the reduction's 32-lane groups read components k = 0..7 of lane
+  // columns txo = 0..3 at banks 4k + txo (TX*TY is a multiple of 32), all distinct; with + 8 the
+  // components k and k + 4 shared a bank (2-way: the 33 % conflict cycles of the BN partial
+  // kernels in profiles/pmc_resnet_kernels_r04al.md)
+  static __host__ __device__ __forceinline__ int ks(int tx, int ty) { return tx * ty + 4; }
   static __host__ __device__ __forceinline__ size_t lds_floats(int tx, int ty, int nq) {
     return (size_t)nq * VEC * ks(tx, ty);
   }

@@ -14,4 +14,14 @@ bool conv_hfp_default(const ConvTapArgs& a);
 int conv_hfp_stats_rows(const ConvTapArgs& a, int cus);  // statistics partial rows (workgroups per k-block)
 void conv_hfp(const ConvTapArgs& a, const float* pcoef, int cus, hipStream_t s);
 
+// the halo-tile 3x3 weight gradient (conv3x3_wgrad.hip) with its input through the producing BN
+// + ReLU, x' = relu(x * xcoef[c] + xcoef[C + c]) (xcoef fp32 [2][C], null = plain); same support
+// and workspace as conv_hwgrad
+void conv_hwgrad_pro(const ConvTapArgs& a, const void* dy, void* dw_out, int out_dtype, float* ws, int cus,
+                     hipStream_t s, const float* xcoef);
+
+// the spatial-tile 64 -> 64 3x3 forward (conv3x3_sp.hip) with the same input prologue (pcoef fp32
+// [2][64], null = plain; padding stays zero)
+void conv_sp_fprop_pro(const ConvTapArgs& a, const float* pcoef, int cus, hipStream_t s);
+
 }  // namespace apex_amd

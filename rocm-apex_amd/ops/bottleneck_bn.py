@@ -4,7 +4,9 @@ convolutions (``models.resnet.Bottleneck`` with ``fused_bn=True`` runs this on t
 Per block (M = N*H*W pixels, width w, output 4w) the forward is
 
     y1 = X . W1^T                + BN1 statistics in the conv epilogue   (csrc/conv/conv1x1_bn.hip)
-    z1 = relu(bn1(y1))                                                   (one apply pass)
+    z1 = relu(bn1(y1))                                                   (one apply pass; at the
+                                   stride-1 64 -> 64 and <= 64-pixel 3x3s it is the 3x3 conv's
+                                   staged-input prologue instead, recomputed by its wgrad)
     y2 = conv3x3(z1, W2)                                                 (native implicit GEMM / MIOpen)
     BN2 statistics                                                        (one read of y2)
     y3 = relu(bn2(y2)) . W3^T    + BN3 statistics: bn2's apply+ReLU is the conv's operand
@@ -33,6 +35,7 @@ memory or RCCL (``finalize_part`` / ``stats_pass`` / ``bwd_*``), so the fusions 
 
 ``APEX_AMD_FUSED_BLOCK=0`` disables the block node (the per-module fused path runs instead).
 """
+import functools
 import os
 
 import torch
@@ -78,6 +81,32 @@ def _lib_mm(a, b, trans_b):
 
 def _conv():
     return _native.require("conv").conv
+
+
+# opt-in: the folded kernels are slower than the apply pass they replace on this tree — 56x56x64:
+# forward 103.7 vs 111.4 us but weight gradient 137.3 vs 87.9 us, apply pass 31.5 us; 7x7x512:
+# +26 / +39 us vs 8 us (tools/bn1_fold_bench.py, profiles/r05/bn1_fold_r05o.jsonl; the halo
+# wgrad's in-LDS rewrite does not hide under its MFMAs yet); whole step 0 / -0.6 %
+_BN1_FOLD = os.environ.get("APEX_AMD_BN1_FOLD", "0") == "1"
+
+
+@functools.lru_cache(maxsize=None)
+def _bn1_fold(cin, cout, h, w):
+    """bn1's apply + ReLU folded into the stride-1 3x3 conv: its forward must run on a halo-staged
+    kernel with the prologue (the 64 -> 64 spatial tile, or the halo tile where it is the default
+    route: <= 64-pixel images) and its weight gradient on the halo-tile kernel (xcoef)."""
+    if not _BN1_FOLD:
+        return False
+    fwd, dg, wg = convops.tap_route(cin, cout, 3, 1, h, w)
+    if not (fwd and dg and wg and convops._halo_wgrad(cin, cout, h, w)):
+        return False
+    ext = _native.submodule("conv")
+    if ext is None:
+        return False
+    sp = cin == 64 and cout == 64 and os.environ.get("APEX_AMD_CONV_SP", "1") != "0"
+    hfp = (hasattr(ext, "hfp_supported") and h * w <= 64 and os.environ.get("APEX_AMD_CONV_HFP", "1")[:1] != "0"
+           and bool(ext.hfp_supported(1, h, w, cin, cout)))
+    return sp or hfp
 
 
 class _Census:
@@ -354,10 +383,18 @@ class _BottleneckFn(torch.autograd.Function):
             sm1, si1, c1, in1 = finalize_part(part1, float(x2.size(0)), bn1)
         else:
             y1, sm1, si1, c1, in1 = conv1x1_bn_fwd(x2, w1.view(width, cin), None, bn1)
-        z1 = _bn().apply(y1, None, c1, True)[0]
+        pro1 = stride == 1 and _bn1_fold(width, w2.size(0), h, wd)
+        # bn1's apply + ReLU on the 3x3 conv's staged input (and recomputed by its weight
+        # gradient) instead of a pass writing z1, where both halo-staged kernels take the shape
+        z1 = None if pro1 else _bn().apply(y1, None, c1, True)[0]
         # conv2 (3x3, stride) -> bn2 statistics (in the native conv's epilogue where it runs)
-        z1v = _nchw(z1, n, h, wd)
-        if convops.tap_route(z1v.size(1), w2.size(0), 3, stride, h)[0]:
+        z1v = _nchw(y1 if pro1 else z1, n, h, wd)
+        if pro1:
+            y2, part2 = convops.conv_tap_forward(z1v, w2, 1, 1, stats_shift=bn2.rm, pcoef=c1)
+            oh, ow = y2.shape[2], y2.shape[3]
+            y2m = _m2(y2)
+            sm2, si2, c2, in2 = finalize_part(part2, float(y2m.size(0)), bn2)
+        elif convops.tap_route(z1v.size(1), w2.size(0), 3, stride, h)[0]:
             y2, part2 = convops.conv_tap_forward(z1v, w2, stride, 1, stats_shift=bn2.rm)
             oh, ow = y2.shape[2], y2.shape[3]
             y2m = _m2(y2)
@@ -454,7 +491,12 @@ class _BottleneckFn(torch.autograd.Function):
         if dw3 is None:
             dw3 = conv1x1_wgrad(dx3, y2m, c2, w3)
         # conv2
-        dz1, dw2 = _conv_bwd(_nchw(dy2, n, oh, ow), _nchw(z1, n, h, wd), w2, stride, 1)
+        if z1 is None:  # bn1 folded into the 3x3 conv: its weight gradient recomputes z1 from y1
+            gy2 = _nchw(dy2, n, oh, ow)
+            dz1 = convops.conv_tap_dgrad(gy2, w2, (n, width, h, wd), 1, 1)
+            dw2 = convops.conv_tap_wgrad(gy2, _nchw(y1, n, h, wd), w2.shape, 1, 1, w2.dtype, xcoef=c1)
+        else:
+            dz1, dw2 = _conv_bwd(_nchw(dy2, n, oh, ow), _nchw(z1, n, h, wd), w2, stride, 1)
         dz1 = _m2(dz1.contiguous(memory_format=torch.channels_last))
         # bn1: reduction + dx pass (as conv1's dgrad operand prologue it moved the same bytes —
         # the reduction then has to write the masked gradient — and measured slower)

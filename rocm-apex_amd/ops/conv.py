@@ -289,12 +289,15 @@ def conv_tap_dgrad(gy, w, x_shape, stride, pad, mask=None):
     return dx
 
 
-def conv_tap_wgrad(gy, x, w_shape, stride, pad, out_dtype):
+def conv_tap_wgrad(gy, x, w_shape, stride, pad, out_dtype, xcoef=None):
+    """``xcoef`` (fp32 [2C]): the weight gradient of a conv whose input was relu(x * xcoef[:C] +
+    xcoef[C:]) — the producing BN + ReLU recomputed on the halo-tile kernel's staged input (3x3
+    stride 1 where ``halo_wgrad_supported``)."""
     kout, c, k, _ = w_shape
     dw = torch.empty((kout, k, k, c), dtype=out_dtype, device=gy.device)
     taps = _fwd_taps(k, pad)
     _conv_ext().wgrad(_nhwc(x), _nhwc(gy), dw.view(kout, k * k, c), stride, stride, [t[0] for t in taps],
-                      [t[1] for t in taps])
+                      [t[1] for t in taps], xcoef)
     return dw.permute(0, 3, 1, 2)  # [K, C, R, S] in channels_last memory
 
 

@@ -94,3 +94,29 @@ def test_gpu_halo_fprop_bn_relu_prologue(n, h, w, cin, cout):
     z = torch.relu(x.float() * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1)).to(torch.bfloat16)
     ref = F.conv2d(z.double().cpu(), wt.double().cpu(), None, 1, 1)
     _close(y, ref, 1e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,w", [(2, 56, 56), (3, 17, 40)])
+def test_gpu_spatial_fprop_bn_relu_prologue_is_bitwise_the_apply_pass(n, h, w):
+    """The 64 -> 64 spatial-tile forward (conv3x3_sp.hip) with the producing BN + ReLU applied to its
+    register-staged halo (padding taps stay zero) is BITWISE the forward of the materialised
+    apply-pass output, statistics epilogue included."""
+    import apex
+    from apex.ops import conv as C
+
+    apex._native.require("conv").conv.hfp_set_mode(0)  # the spatial kernel's route, not the halo-tile one
+    bn = apex._native.require("bn_nhwc").bn_nhwc
+    torch.manual_seed(h)
+    dt = torch.bfloat16
+    y = torch.randn(n, 64, h, w, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
+    wt = (torch.randn(64, 64, 3, 3, device="cuda") * 0.05).to(dt).contiguous(memory_format=torch.channels_last)
+    coef = torch.cat([torch.rand(64, device="cuda") + 0.5, torch.randn(64, device="cuda") * 0.5])
+    z = bn.apply(y.permute(0, 2, 3, 1).reshape(-1, 64), None, coef, True)[0]
+    zv = z.view(n, h, w, 64).permute(0, 3, 1, 2)
+    shift = torch.randn(64, device="cuda") * 0.1
+    want, wpart = C.conv_tap_forward(zv, wt, 1, 1, stats_shift=shift)
+    got, gpart = C.conv_tap_forward(y, wt, 1, 1, stats_shift=shift, pcoef=coef)
+    assert torch.equal(got, want) and torch.equal(gpart, wpart)
+    ref = F.conv2d(zv.double().cpu(), wt.double().cpu(), None, 1, 1)
+    _close(got, ref, 1e-2)

@@ -83,3 +83,27 @@ def test_gpu_halo_wgrad_is_the_default_route():
     finally:
         ext.force_wgrad_variant(-1)
     assert torch.equal(dflt, forced)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,w,cin,cout", [(2, 56, 56, 64, 64), (2, 28, 28, 128, 128), (3, 7, 7, 512, 64),
+                                            (2, 10, 13, 64, 64)])
+def test_gpu_halo_wgrad_bn_relu_prologue_is_bitwise_the_apply_pass(n, h, w, cin, cout):
+    """x' = relu(x * xcoef[c] + xcoef[C + c]) recomputed on the halo kernel's staged input (each lane
+    rewrites the chunks it loaded; padding stays zero) gives BITWISE the weight gradient of the
+    materialised apply-pass output (the same fma / max / rounding)."""
+    import apex
+    from apex.ops import conv as C
+
+    bn = apex._native.require("bn_nhwc").bn_nhwc
+    torch.manual_seed(h + cin)
+    dt = torch.bfloat16
+    y = torch.randn(n, cin, h, w, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(n, cout, h, w, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
+    coef = torch.cat([torch.rand(cin, device="cuda") + 0.5, torch.randn(cin, device="cuda") * 0.5])
+    z = bn.apply(y.permute(0, 2, 3, 1).reshape(-1, cin), None, coef, True)[0]
+    zv = z.view(n, h, w, cin).permute(0, 3, 1, 2)
+    want = C.conv_tap_wgrad(gy, zv, (cout, cin, 3, 3), 1, 1, torch.float32)
+    got = C.conv_tap_wgrad(gy, y, (cout, cin, 3, 3), 1, 1, torch.float32, xcoef=coef)
+    assert torch.equal(got, want)
+    _close(got, _ref(zv, gy, cout), 1e-2)
