@@ -180,6 +180,12 @@ MtaMeta mta_meta(const std::vector<std::vector<at::Tensor>>& lists, int chunk_si
     nchunks += (int)c;
   }
   first[nt] = nchunks;
+  static const int item = [] {
+    const char* e = std::getenv("APEX_AMD_MTA_ITEM");  // A/B knob: elements per work item
+    return e ? std::atoi(e) : 16384;
+  }();
+  const int split = mta_split(chunk_size, item);
+  TORCH_CHECK((int64_t)nchunks * split < (1ll << 31), "multi_tensor_apply: too many work items");
 
   const size_t off_sizes = 0;
   const size_t off_ptrs = align8(off_sizes + sizeof(int64_t) * nt);
@@ -227,6 +233,7 @@ MtaMeta mta_meta(const std::vector<std::vector<at::Tensor>>& lists, int chunk_si
   m.chunk_size = chunk_size;
   m.depth = depth;
   m.aligned = aligned ? 1 : 0;
+  m.split = split;
 
   // LRU eviction (never evict tables a captured graph may replay)
   while (g_cache.size() >= kMaxEntries && !g_lru.empty()) {

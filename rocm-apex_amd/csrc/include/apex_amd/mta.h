@@ -21,7 +21,7 @@ struct MtaMeta {
   const int2* chunks;     // [nchunks] {tensor index, chunk index within tensor}
   const int* first_chunk; // [ntensors + 1] prefix of chunk counts (chunks of a tensor are contiguous)
   uint64_t* partials;     // [2 * nchunks] tagged per-chunk partials: (launch tag << 32) | float bits
-  float* stage;           // [2 * nchunks] the finalizing block's verified copy of the partials
+  float* stage;           // [2 * nchunks] the finalizing block's validated per-chunk sums of the partials
   unsigned* ticket;       // arrival counter for single-pass grid reductions (reset by last block)
   unsigned* epoch;        // tag of the previous launch over this table (bumped by the last block)
   int ntensors;
@@ -29,7 +29,18 @@ struct MtaMeta {
   int chunk_size;
   int depth;
   int aligned;            // every base pointer 32-byte aligned -> vector path legal
+  int split;              // elementwise (no-reduction) launches: work items per chunk (mta_split)
 };
+
+// Elementwise launches split each chunk into `split` work items of chunk_size / split elements.
+// The API's chunk (the reference's 2048 * 32 = 64k elements) gives a 100M-parameter step only 6
+// blocks per CU, too few loads in flight for HBM3E; 16k-element items raise that to the 8-block cap
+// with a grid-strided tail: +4-5 % on Adam / SGD (tools/mta_bench.py, profiles/r05/mta_split_r05.jsonl).
+// Reductions stay one item per chunk: split items cost each block a drain + block reduction per
+// item, which measured 85 -> 117 us on a 100M-element L2 norm.
+inline int mta_split(int chunk_size, int item) {
+  return (item > 0 && chunk_size > item && chunk_size % item == 0 && item % kVec == 0) ? chunk_size / item : 1;
+}
 
 template <typename T>
 __device__ __forceinline__ T* mta_ptr(const MtaMeta& m, int d, int t, int64_t start) {
@@ -156,6 +167,14 @@ __device__ __forceinline__ void mta_finish(const MtaMeta& meta, const Op& op, un
   }
 }
 
+// bytes each lane loads per kVec-element step (the lists the op reads)
+template <unsigned Mask, typename... Ts>
+constexpr int mta_read_bytes() {
+  int b = 0, i = 0;
+  ((b += ((Mask >> i++) & 1u) ? (int)sizeof(Ts) * kVec : 0), ...);
+  return b;
+}
+
 // Ops with kNumAcc > 0 accumulate per-element sums (or maxima when Op::kAccMax) which are
 // reduced per chunk into meta.partials; the last block then calls op.finalize(meta, smem).
 template <typename Op, typename... Ts>
@@ -163,6 +182,9 @@ __global__ void __launch_bounds__(kMtaBlock) mta_elementwise_kernel(MtaMeta meta
   constexpr int D = sizeof...(Ts);
   constexpr int NA = Op::kNumAcc;
   __shared__ float smem[kMtaBlock / 64 * 2 + 2];
+  const int split = NA == 0 ? meta.split : 1;
+  const int item = meta.chunk_size / split;
+  const int nwork = meta.nchunks * split;
   if constexpr (Op::kSkipOnNoop) {
     // uniform early exit; a reduction op still has to take part in the ticket protocol.  The
     // flag can also be raised DURING this launch (kCheckPartial ops set it on a non-finite
@@ -172,8 +194,8 @@ __global__ void __launch_bounds__(kMtaBlock) mta_elementwise_kernel(MtaMeta meta
       if constexpr (NA == 0) return;
       else {
         const unsigned tag = __hip_atomic_load(meta.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-        for (int w = blockIdx.x; w < meta.nchunks; w += gridDim.x)
-          if (threadIdx.x < NA) mta_put_partial(meta.partials + (size_t)threadIdx.x * meta.nchunks + w, 0.f, tag);
+        for (int w = blockIdx.x; w < nwork; w += gridDim.x)
+          if (threadIdx.x < NA) mta_put_partial(meta.partials + (size_t)threadIdx.x * nwork + w, 0.f, tag);
         if (mta_last_block(meta.ticket, reinterpret_cast<int*>(&smem[kMtaBlock / 64 * 2])))
           mta_finish(meta, op, tag, true);
         return;
@@ -183,11 +205,13 @@ __global__ void __launch_bounds__(kMtaBlock) mta_elementwise_kernel(MtaMeta meta
   bool bad = false;
   unsigned tag = 0;
   if constexpr (NA > 0) tag = __hip_atomic_load(meta.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-  for (int w = blockIdx.x; w < meta.nchunks; w += gridDim.x) {
-    const int2 tc = meta.chunks[w];
-    const int64_t start = (int64_t)tc.y * meta.chunk_size;
+  for (int w = blockIdx.x; w < nwork; w += gridDim.x) {
+    const int c = split == 1 ? w : w / split;
+    const int2 tc = meta.chunks[c];
+    const int64_t start = (int64_t)tc.y * meta.chunk_size + (int64_t)(w - c * split) * item;
     const int64_t rem = meta.sizes[tc.x] - start;
-    const int len = rem < meta.chunk_size ? (int)rem : meta.chunk_size;
+    if (rem <= 0) continue;  // a split item past the end of its tensor's last chunk
+    const int len = rem < item ? (int)rem : item;
     void* base[D];
     ListIO<Op, D, 0, Ts...>::set_base(base, meta, tc.x, start);
     const auto ts = op.tensor_state(tc.x);
@@ -196,7 +220,9 @@ __global__ void __launch_bounds__(kMtaBlock) mta_elementwise_kernel(MtaMeta meta
     for (int a = 0; a < (NA > 0 ? NA : 1); ++a) acc[a] = 0.f;
     const int nvec = meta.aligned ? (len / kVec) : 0;
     int v = threadIdx.x;
-    if constexpr (APEX_MTA_ILP > 1) {
+    // light streams (<= 32 B loaded per lane per step, e.g. a bf16 -> fp32 scale) keep two steps
+    // loads in flight per lane; heavier ones (Adam: 128 B) have enough with one
+    if constexpr (Op::kWrite != 0 && (APEX_MTA_ILP > 1 || mta_read_bytes<Op::kRead, Ts...>() <= 32)) {
       // two vectors per thread per trip: both loads are in flight before either is stored
       for (; v + kMtaBlock < nvec; v += 2 * kMtaBlock) {
         float r0[D][kVec], r1[D][kVec];
@@ -237,7 +263,7 @@ __global__ void __launch_bounds__(kMtaBlock) mta_elementwise_kernel(MtaMeta meta
         float s = op.acc_is_max() ? block_max(acc[a], smem + a * (kMtaBlock / 64))
                                   : block_sum(acc[a], smem + a * (kMtaBlock / 64));
         if (threadIdx.x == 0) {
-          mta_put_partial(meta.partials + (size_t)a * meta.nchunks + w, s, tag);
+          mta_put_partial(meta.partials + (size_t)a * nwork + w, s, tag);
           if (Op::kCheckPartial && !is_finite(s)) bad = true;
         }
       }
@@ -257,6 +283,12 @@ __global__ void __launch_bounds__(kMtaBlock) mta_elementwise_kernel(MtaMeta meta
 }
 
 inline int mta_grid(int nchunks, int max_blocks) { return nchunks < max_blocks ? (nchunks > 0 ? nchunks : 1) : max_blocks; }
+// one block per work item, up to the resident-block cap (grid-strided beyond it); reductions
+// (kNumAcc > 0) pass split = false
+inline int mta_grid_work(const MtaMeta& m, int max_blocks, bool split = true) {
+  const int64_t n = (int64_t)m.nchunks * (split ? m.split : 1);
+  return mta_grid(n < max_blocks ? (int)n : max_blocks, max_blocks);
+}
 
 // Base class for ops without reductions / per-tensor state.
 struct MtaOpBase {
@@ -292,11 +324,28 @@ __device__ __forceinline__ float mta_get_partial(const uint64_t* p, unsigned tag
   return __uint_as_float((unsigned)(w & 0xffffffffu));
 }
 
-// Finalizing block, all threads: validate every tagged partial in parallel and stage the
-// values for the per-tensor sums (read back by this same block after the barrier).
+// Finalizing block, all threads: validate every tagged partial and stage the values for the
+// per-tensor sums (read back by this same block after the barrier).  Each thread issues its
+// partials in batches of 8 independent atomic loads (one round trip per batch instead of one per
+// partial), then checks the tags and re-reads only a word that is not yet this launch's.
 __device__ __forceinline__ void mta_collect_partials(const MtaMeta& m, int num_acc, unsigned tag) {
+  constexpr int B = 8;
   const int n = num_acc * m.nchunks;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) m.stage[i] = mta_get_partial(m.partials + i, tag);
+  for (int i0 = threadIdx.x; i0 < n; i0 += B * blockDim.x) {
+    uint64_t w[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const int i = i0 + b * blockDim.x;
+      w[b] = i < n ? __hip_atomic_load(m.partials + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    }
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const int i = i0 + b * blockDim.x;
+      if (i < n)
+        m.stage[i] = (unsigned)(w[b] >> 32) == tag ? __uint_as_float((unsigned)(w[b] & 0xffffffffu))
+                                                   : mta_get_partial(m.partials + i, tag);
+    }
+  }
   __syncthreads();
 }
 

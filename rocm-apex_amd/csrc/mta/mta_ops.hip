@@ -61,7 +61,7 @@ struct ScaleOp : MtaOpBase {
 void mt_scale(const MtaMeta& m, int in_t, int out_t, int* noop, DevScalar scale, const Launch& L) {
   ScaleOp op;
   op.scale = scale;
-  const int grid = mta_grid(m.nchunks, L.max_blocks);
+  const int grid = mta_grid_work(m, L.max_blocks);
   dispatch_float(in_t, [&](auto ti) {
     dispatch_float(out_t, [&](auto to) {
       using TI = typename decltype(ti)::type;
@@ -96,7 +96,7 @@ void mt_axpby(const MtaMeta& m, int x_t, int y_t, int out_t, int* noop, float a,
   op.a = a;
   op.b = b;
   op.check = arg_to_check;
-  const int grid = mta_grid(m.nchunks, L.max_blocks);
+  const int grid = mta_grid_work(m, L.max_blocks);
   dispatch_float(x_t, [&](auto tx) {
     dispatch_float(y_t, [&](auto ty) {
       dispatch_float(out_t, [&](auto to) {
@@ -123,7 +123,7 @@ struct CheckFiniteOp : MtaOpBase {
 };
 
 void mt_check_finite(const MtaMeta& m, int t, int* noop, const Launch& L) {
-  const int grid = mta_grid(m.nchunks, L.max_blocks);
+  const int grid = mta_grid_work(m, L.max_blocks);
   dispatch_float(t, [&](auto tt) {
     using T = typename decltype(tt)::type;
     mta_elementwise_kernel<CheckFiniteOp, T><<<grid, kMtaBlock, 0, L.stream>>>(m, noop, CheckFiniteOp{});
@@ -206,7 +206,7 @@ static void launch_norm(const MtaMeta& m, int in_t, int out_t, int* noop, const 
 
 void mt_norm(const MtaMeta& m, int in_t, int out_t, int* noop, float* total, float* per_tensor, int mode,
              bool skip_on_noop, DevScalar scale, bool blend, float alpha, float beta, const Launch& L) {
-  const int grid = mta_grid(m.nchunks, L.max_blocks);
+  const int grid = mta_grid_work(m, L.max_blocks, false);
   auto fill = [&](auto& op) {
     op.mode = mode;
     op.scale = scale;
@@ -226,6 +226,20 @@ void mt_norm(const MtaMeta& m, int in_t, int out_t, int* noop, float* total, flo
   check_launch("multi_tensor_norm");
 }
 
+// Optimizer math at the reference's precision: its multi-tensor and optimizer kernels are built
+// with --use_fast_math (reference setup.py:167,210,352,375), i.e. approximate divide and sqrt.  Here
+// that is one v_rcp_f32 / v_sqrt_f32 (1 ulp) instead of the ~10-instruction IEEE sequences, and a
+// per-tensor divisor (bias correction) becomes a multiply by its reciprocal, computed once per chunk:
+// Adam drops from ~60 to ~15 VALU ops per element, so its waves spend their time on memory.
+// (APEX_MTA_IEEE=1: variant build with IEEE sqrt / divide, for the A/B in tools/mta_bench.py)
+#if APEX_MTA_IEEE
+__device__ __forceinline__ float fm_sqrt(float x) { return sqrtf(x); }
+__device__ __forceinline__ float fm_rcp(float x) { return 1.f / x; }
+#else
+__device__ __forceinline__ float fm_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float fm_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+#endif
+
 // =============================================================================================
 // Adam / AdamW (reference csrc/multi_tensor_adam.cu:24-127 for the math; op order kept so the
 // python fallback and this kernel agree to rounding)
@@ -235,20 +249,24 @@ struct AdamOp : MtaOpBase {
   static constexpr unsigned kRead = 0b1111, kWrite = (D == 5) ? 0b11110 : 0b1110;
   static constexpr bool kSkipOnNoop = SKIP;
   AdamArgs a;
-  struct TS { float lr, inv, bc1, bc2; };
+  struct TS { float lr, inv, rbc1, rbc2; };  // reciprocal bias corrections
   __device__ __forceinline__ TS tensor_state(int) const {
     TS s;
     s.lr = a.lr.get();
     s.inv = a.inv_scale.get();
+    float bc1 = a.bc1, bc2 = a.bc2;
     if (a.step_dev && a.bias_correction) {
       const float st = *a.step_dev;
-      s.bc1 = 1.f - powf(a.beta1, st);
-      s.bc2 = 1.f - powf(a.beta2, st);
-    } else {
-      s.bc1 = a.bc1;
-      s.bc2 = a.bc2;
+      bc1 = 1.f - powf(a.beta1, st);
+      bc2 = 1.f - powf(a.beta2, st);
     }
+    s.rbc1 = 1.f / bc1;
+    s.rbc2 = 1.f / bc2;
     return s;
+  }
+  // the step's update m^/(sqrt(v^)+eps), shared with AdamUndoOp so the undo inverts it exactly
+  static __device__ __forceinline__ float update(float mm, float vv, const TS& s, float eps) {
+    return (mm * s.rbc1) * fm_rcp(fm_sqrt(vv * s.rbc2) + eps);
   }
   template <int N>
   __device__ __forceinline__ void apply(float (&r)[D][N], const TS& s, bool&, float*) const {
@@ -260,13 +278,11 @@ struct AdamOp : MtaOpBase {
         g = g + a.weight_decay * p;
         mm = a.beta1 * mm + (1.f - a.beta1) * g;
         vv = a.beta2 * vv + (1.f - a.beta2) * g * g;
-        const float denom = sqrtf(vv / s.bc2) + a.eps;
-        p = p - s.lr * ((mm / s.bc1) / denom);
+        p = p - s.lr * update(mm, vv, s, a.eps);
       } else {
         mm = a.beta1 * mm + (1.f - a.beta1) * g;
         vv = a.beta2 * vv + (1.f - a.beta2) * g * g;
-        const float denom = sqrtf(vv / s.bc2) + a.eps;
-        p = p - s.lr * (((mm / s.bc1) / denom) + a.weight_decay * p);
+        p = p - s.lr * (update(mm, vv, s, a.eps) + a.weight_decay * p);
       }
       r[1][k] = p;
       r[2][k] = mm;
@@ -298,7 +314,7 @@ static void launch_adam(const MtaMeta& m, int g_t, int p_t, int out_t, int* noop
 }
 
 void mt_adam(const MtaMeta& m, int g_t, int p_t, int out_t, int* noop, const AdamArgs& a, const Launch& L) {
-  const int grid = mta_grid(m.nchunks, L.max_blocks);
+  const int grid = mta_grid_work(m, L.max_blocks);
   if (m.depth == 5) {
     if (p_t != kF32) throw std::runtime_error("multi_tensor_adam: master params must be fp32 with a model copy");
     if (a.skip_on_noop) launch_adam<5, true>(m, g_t, p_t, out_t, noop, a, grid, L.stream);
@@ -335,8 +351,7 @@ struct AdamUndoOp : MtaOpBase {
     for (int k = 0; k < N; ++k) {
       float g = r[0][k] * s.inv;
       const float p = r[1][k], mm = r[2][k], vv = r[3][k];
-      const float denom = sqrtf(vv / s.bc2) + a.eps;
-      const float upd = (mm / s.bc1) / denom;
+      const float upd = AdamOp<D, true>::update(mm, vv, s, a.eps);
       float p0;
       if (a.mode == 0) {
         p0 = p + s.lr * upd;
@@ -353,7 +368,7 @@ struct AdamUndoOp : MtaOpBase {
 };
 
 void mt_adam_undo(const MtaMeta& m, int g_t, int out_t, int* noop, const AdamArgs& a, const Launch& L) {
-  const int grid = mta_grid(m.nchunks, L.max_blocks);
+  const int grid = mta_grid_work(m, L.max_blocks);
   dispatch_float(g_t, [&](auto tg) {
     using TG = typename decltype(tg)::type;
     if (m.depth == 5) {
@@ -407,7 +422,7 @@ struct SgdOp : MtaOpBase {
 };
 
 void mt_sgd(const MtaMeta& m, int g_t, int w_t, int out_t, int* noop, const SgdArgs& a, const Launch& L) {
-  const int grid = mta_grid(m.nchunks, L.max_blocks);
+  const int grid = mta_grid_work(m, L.max_blocks);
   dispatch_float(g_t, [&](auto tg) {
     using TG = typename decltype(tg)::type;
     dispatch_float(w_t, [&](auto tw) {
@@ -445,10 +460,10 @@ struct AdagradOp : MtaOpBase {
       if (mode == 0) {
         g = g + wd * p;
         h = h + g * g;
-        p = p - lr * (g / (sqrtf(h) + eps));
+        p = p - lr * (g * fm_rcp(fm_sqrt(h) + eps));
       } else {
         h = h + g * g;
-        p = p - lr * (g / (sqrtf(h) + eps) + wd * p);
+        p = p - lr * (g * fm_rcp(fm_sqrt(h) + eps) + wd * p);
       }
       r[1][k] = p;
       r[2][k] = h;
@@ -462,7 +477,7 @@ void mt_adagrad(const MtaMeta& m, int t, int* noop, float lr, float eps, int mod
   op.eps = eps;
   op.wd = wd;
   op.mode = mode;
-  const int grid = mta_grid(m.nchunks, L.max_blocks);
+  const int grid = mta_grid_work(m, L.max_blocks);
   dispatch_float(t, [&](auto tt) {
     using T = typename decltype(tt)::type;
     mta_elementwise_kernel<AdagradOp, T, T, T><<<grid, kMtaBlock, 0, L.stream>>>(m, noop, op);
@@ -503,7 +518,7 @@ struct NovoOp : MtaOpBase {
 void mt_novograd(const MtaMeta& m, int t, int* noop, const NovoArgs& a, const Launch& L) {
   NovoOp op;
   op.a = a;
-  const int grid = mta_grid(m.nchunks, L.max_blocks);
+  const int grid = mta_grid_work(m, L.max_blocks);
   dispatch_float(t, [&](auto tt) {
     using T = typename decltype(tt)::type;
     mta_elementwise_kernel<NovoOp, T, T, T><<<grid, kMtaBlock, 0, L.stream>>>(m, noop, op);
@@ -524,21 +539,21 @@ struct LambStage1Op {
   static constexpr unsigned kRead = 0b1111, kWrite = 0b1101;
   static constexpr bool kSkipOnNoop = SKIP;
   LambArgs a;
-  struct TS { float clip, bc1, bc2, inv; };
+  struct TS { float gscale, rbc1, rbc2; };  // inv_scale / clip and reciprocal bias corrections
   __device__ __forceinline__ TS tensor_state(int) const {
     TS s;
     const float gn = *a.global_grad_norm;
     const float mx = a.max_grad_norm.get();
-    s.clip = (mx > 0.f && gn > mx) ? gn / mx : 1.f;
-    s.inv = a.inv_scale.get();
+    const float clip = (mx > 0.f && gn > mx) ? gn / mx : 1.f;
+    s.gscale = a.inv_scale.get() / clip;
+    float bc1 = a.bc1, bc2 = a.bc2;
     if (a.step_dev && a.bias_correction) {
       const float st = *a.step_dev;
-      s.bc1 = 1.f - powf(a.beta1, st);
-      s.bc2 = 1.f - powf(a.beta2, st);
-    } else {
-      s.bc1 = a.bc1;
-      s.bc2 = a.bc2;
+      bc1 = 1.f - powf(a.beta1, st);
+      bc2 = 1.f - powf(a.beta2, st);
     }
+    s.rbc1 = 1.f / bc1;
+    s.rbc2 = 1.f / bc2;
     return s;
   }
   template <int N>
@@ -547,18 +562,18 @@ struct LambStage1Op {
     for (int k = 0; k < N; ++k) {
       const float p = r[1][k];
       float mm = r[2][k], vv = r[3][k];
-      float sg = (r[0][k] * s.inv) / s.clip;
+      float sg = r[0][k] * s.gscale;
       const float pd = a.weight_decay != 0.f ? p : 0.f;
       float upd;
       if (a.mode == 0) {
         sg = sg + a.weight_decay * pd;
         mm = mm * a.beta1 + a.beta3 * sg;
         vv = vv * a.beta2 + (1.f - a.beta2) * sg * sg;
-        upd = (mm / s.bc1) / (sqrtf(vv / s.bc2) + a.eps);
+        upd = (mm * s.rbc1) * fm_rcp(fm_sqrt(vv * s.rbc2) + a.eps);
       } else {
         mm = mm * a.beta1 + a.beta3 * sg;
         vv = vv * a.beta2 + (1.f - a.beta2) * sg * sg;
-        upd = ((mm / s.bc1) / (sqrtf(vv / s.bc2) + a.eps)) + a.weight_decay * pd;
+        upd = (mm * s.rbc1) * fm_rcp(fm_sqrt(vv * s.rbc2) + a.eps) + a.weight_decay * pd;
       }
       acc[0] += p * p;
       acc[1] += upd * upd;
@@ -603,7 +618,7 @@ struct LambStage2Op : MtaOpBase {
 };
 
 void mt_lamb_stage1(const MtaMeta& m, int g_t, int p_t, int* noop, const LambArgs& a, const Launch& L) {
-  const int grid = mta_grid(m.nchunks, L.max_blocks);
+  const int grid = mta_grid_work(m, L.max_blocks, false);
   auto go = [&](auto skip_tag) {
     constexpr bool S = decltype(skip_tag)::value;
     LambStage1Op<S> op;
@@ -623,7 +638,7 @@ void mt_lamb_stage1(const MtaMeta& m, int g_t, int p_t, int* noop, const LambArg
 
 void mt_lamb_stage2(const MtaMeta& m, int u_t, int p_t, int out_t, int* noop, const LambArgs& a,
                     const Launch& L) {
-  const int grid = mta_grid(m.nchunks, L.max_blocks);
+  const int grid = mta_grid_work(m, L.max_blocks);
   auto go = [&](auto skip_tag) {
     constexpr bool S = decltype(skip_tag)::value;
     dispatch_float(u_t, [&](auto tu) {
@@ -667,7 +682,7 @@ struct LambLegacy1Op : MtaOpBase {
   const float* gnorm;
   const float* step;  // DEV: device step count (after this step's increment)
   int bias_correction;
-  struct TS { float clip, decay, bc1, bc2; };
+  struct TS { float rclip, decay, rbc1, rbc2; };  // reciprocals of the clip and bias corrections
   __device__ __forceinline__ TS tensor_state(int t) const {
     const float gn = *gnorm;
     float b1 = bc1, b2 = bc2;
@@ -676,16 +691,16 @@ struct LambLegacy1Op : MtaOpBase {
       b1 = bias_correction ? 1.f - powf(beta1, st) : 1.f;
       b2 = bias_correction ? 1.f - powf(beta2, st) : 1.f;
     }
-    return {(gn > max_norm) ? gn / max_norm : 1.f, decay[t], b1, b2};
+    return {(gn > max_norm) ? max_norm / gn : 1.f, decay[t], 1.f / b1, 1.f / b2};
   }
   template <int N>
   __device__ __forceinline__ void apply(float (&r)[5][N], const TS& s, bool&, float*) const {
 #pragma unroll
     for (int k = 0; k < N; ++k) {
-      const float sg = r[0][k] / s.clip;
+      const float sg = r[0][k] * s.rclip;
       const float mm = r[2][k] * beta1 + beta3 * sg;
       const float vv = r[3][k] * beta2 + (1.f - beta2) * sg * sg;
-      r[4][k] = (mm / s.bc1) / (sqrtf(vv / s.bc2) + eps) + s.decay * r[1][k];
+      r[4][k] = (mm * s.rbc1) * fm_rcp(fm_sqrt(vv * s.rbc2) + eps) + s.decay * r[1][k];
       r[2][k] = mm;
       r[3][k] = vv;
     }
@@ -709,7 +724,7 @@ void mt_lamb_legacy_stage1(const MtaMeta& m, int g_t, int p_t, int* noop, const 
     op.step = step_dev;
     op.bias_correction = bias_correction;
   };
-  const int grid = mta_grid(m.nchunks, L.max_blocks);
+  const int grid = mta_grid_work(m, L.max_blocks);
   dispatch_float(g_t, [&](auto tg) {
     dispatch_float(p_t, [&](auto tp) {
       using TG = typename decltype(tg)::type;
@@ -770,7 +785,7 @@ void mt_lamb_legacy_stage2(const MtaMeta& m, int p_t, int u_t, int out_t, int* n
     op.wd = weight_decay;
     op.nv = use_nvlamb;
   };
-  const int grid = mta_grid(m.nchunks, L.max_blocks);
+  const int grid = mta_grid_work(m, L.max_blocks);
   auto run = [&](auto dev_tag) {
     constexpr bool DEV = decltype(dev_tag)::value;
     dispatch_float(p_t, [&](auto tp) {
@@ -814,7 +829,7 @@ struct CastOp : MtaOpBase {
 };
 
 void mt_cast(const MtaMeta& m, int in_t, int out_t, int* noop, const Launch& L) {
-  const int grid = mta_grid(m.nchunks, L.max_blocks);
+  const int grid = mta_grid_work(m, L.max_blocks);
   dispatch_any(in_t, [&](auto ti) {
     dispatch_any(out_t, [&](auto to) {
       using TI = typename decltype(ti)::type;

@@ -219,15 +219,15 @@ def build(jobs_n: int | None = None, clean: bool = False, verbose: bool = False,
         with cf.ThreadPoolExecutor(max_workers=n) as ex:
             futs = {ex.submit(run, cmd, verbose): src for src, cmd in todo}
             for f in cf.as_completed(futs):
-                rc, out, dt = f.result()
+                rc, log, dt = f.result()
                 src = os.path.relpath(futs[f], ROOT)
                 if rc != 0:
                     failed.append(src)
-                    print(f"[build_native] FAILED {src}\n{out}", flush=True)
+                    print(f"[build_native] FAILED {src}\n{log}", flush=True)
                 else:
                     print(f"[build_native] {src} ({dt:.1f}s)", flush=True)
-                    if out.strip() and verbose:
-                        print(out)
+                    if log.strip() and verbose:
+                        print(log)
     if failed:
         raise RuntimeError(f"native build failed: {failed}")
     with open(stamp, "w") as f:

@@ -49,15 +49,29 @@ def main():
             65536, noop, [G16, P, M, V, O16], lr, 0.9, 0.999, 1e-8, step, 1, 1, 0.0, inv), 28),
         "adam_fp32": (lambda: amp_C.multi_tensor_adam(65536, noop, [G32, P, M, V], 1e-4, 0.9, 0.999, 1e-8, 1, 1, 1,
                                                       0.0), 28),
+        "adam_fp32_chunk16k": (lambda: amp_C.multi_tensor_adam(16384, noop, [G32, P, M, V], 1e-4, 0.9, 0.999, 1e-8, 1, 1,
+                                                                1, 0.0), 28),
+        "adam_fp32_chunk256k": (lambda: amp_C.multi_tensor_adam(262144, noop, [G32, P, M, V], 1e-4, 0.9, 0.999, 1e-8, 1,
+                                                                 1, 1, 0.0), 28),
         "sgd_fp32_mom": (lambda: amp_C.multi_tensor_sgd(65536, noop, [G32, P, M], 0.0, 0.9, 0.0, 1e-4, False, False,
                                                         False, 1.0), 20),
+        "sgd_fp32_mom_chunk16k": (lambda: amp_C.multi_tensor_sgd(16384, noop, [G32, P, M], 0.0, 0.9, 0.0, 1e-4, False,
+                                                                 False, False, 1.0), 20),
         "scale_bf16_to_fp32": (lambda: amp_C.multi_tensor_scale(65536, noop, [G16, V], 0.5), 6),
         "l2norm_fp32": (lambda: amp_C.multi_tensor_l2norm(65536, noop, [G32], False), 4),
     }
+    # the in-run roof: an elementwise kernel (torch.mul by 1) moving the fp32 Adam step's bytes
+    # (half read, half written), timed the same way in the same process
+    src = torch.empty(elems * 28 // 8, device=dev).uniform_()
+    dst = torch.empty_like(src)
+    roof = elems * 28 / timeit(lambda: torch.mul(src, 1.0, out=dst)) / 1e9
+    del src, dst
+    print(json.dumps({"variant": variant, "case": "copy_roof_28B", "GBps": round(roof, 1)}), flush=True)
     for name, (fn, bpe) in cases.items():
         sec = timeit(fn)
-        print(json.dumps({"variant": variant, "case": name, "us": round(sec * 1e6, 1),
-                          "GBps": round(elems * bpe / sec / 1e9, 1), "bytes_per_elem": bpe}), flush=True)
+        gbps = elems * bpe / sec / 1e9
+        print(json.dumps({"variant": variant, "case": name, "us": round(sec * 1e6, 1), "GBps": round(gbps, 1),
+                          "bytes_per_elem": bpe, "pct_of_copy": round(100 * gbps / roof, 1)}), flush=True)
 
 
 if __name__ == "__main__":
