@@ -98,8 +98,13 @@ constexpr int pick_nw(int nc, int kr, int pro, bool red) {
          : lds_bytes_nw(nc, kr, pro, red, 8) <= 160 * 1024 ? 8 : 4;
 }
 
+// the weight image leaves ONE 4-wave workgroup per CU: the register file of a whole SIMD per wave
+constexpr bool one_wg_per_cu(int nc, int kr, int pro, bool red) {
+  return pick_nw(nc, kr, pro, red) == 4 && lds_bytes_nw(nc, kr, pro, red, 4) > 80 * 1024;
+}
+
 template <typename T, int NC, int KR, bool WT, int PRO, bool STATS, bool RED, int NW, int DEPTH>
-__global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
+__global__ void __launch_bounds__(NW * 64, (NW == 8 || one_wg_per_cu(NC, KR, PRO, RED)) ? 1 : 2) fused1x1(Args p) {
   constexpr int kWaves = NW, kRowsB = NW * 32, NT = NW * 64;
   constexpr int BS = KR + 8;                 // B image row stride (elements)
   constexpr int CN = NC / 32;                // accumulator blocks per wave
@@ -445,6 +450,31 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) fused1x1(Args p) {
         ch = nch;
       }
     }
+  } else if constexpr (DEPTH >= 4) {
+    // deeper ring for the one-workgroup-per-CU shapes (a 4-wave CU needs more bytes in flight
+    // per wave): f[j] is consumed at step j of the unrolled rotation and refilled with the
+    // position DEPTH - 1 ahead; every index is a compile-time constant after the unroll
+    Frags f[DEPTH];
+    int tn = t, cn = ch;
+#pragma unroll
+    for (int j = 0; j < DEPTH - 1; ++j) {
+      load(f[j], min(tn, tlast), cn);
+      adv(tn, cn);
+    }
+    bool done = false;
+    while (!done) {
+#pragma unroll
+      for (int j = 0; j < DEPTH; ++j) {
+        if (!done) {
+          load(f[(j + DEPTH - 1) % DEPTH], min(tn, tlast), cn);
+          adv(tn, cn);
+          compute(f[j], t, ch);
+          if (ch == NCH - 1) epilogue(t);
+          adv(t, ch);
+          done = t >= p.ntiles;
+        }
+      }
+    }
   } else {
     Frags f0, f1, f2;
     int t1 = t, c1 = ch;
@@ -619,13 +649,20 @@ __global__ void __launch_bounds__(8 * kFinG) bwd_finalize(const float* __restric
   coef[2 * c + ch] = -A * (sdy * inv_n) - B * mean[ch];
 }
 
-// prefetch ring depth (APEX_AMD_C1BN_DEPTH=2|3 overrides, for A/B): 3 where the third register
-// set fits beside the accumulators without spills (<= 128 columns but 128 x 128), else 2
+// prefetch ring depth (APEX_AMD_C1BN_DEPTH=2..5 overrides, for A/B): 3 where the third register
+// set fits beside the accumulators without spills (<= 128 columns but 128 x 128), else 2; the
+// shapes whose weight image leaves ONE 4-wave workgroup per CU (128 columns x k 512) take a
+// deeper ring (APEX_AMD_C1BN_DEPTH1, default 4): 4 waves carry the CU's whole HBM stream
 static int g_c1bn_depth = [] {
   const char* e = std::getenv("APEX_AMD_C1BN_DEPTH");
   return e ? std::atoi(e) : 0;
 }();
+static int g_c1bn_depth1 = [] {
+  const char* e = std::getenv("APEX_AMD_C1BN_DEPTH1");
+  return e ? std::atoi(e) : 4;
+}();
 constexpr int default_depth(int nc, int kr) { return nc <= 128 && !(nc == 128 && kr == 128) ? 3 : 2; }
+
 
 template <typename T, int NC, int KR, bool WT, int PRO, bool STATS, bool RED, int DEPTH>
 void launch_d(const Args& a0, int cus, hipStream_t s) {
@@ -651,6 +688,15 @@ void launch_d(const Args& a0, int cus, hipStream_t s) {
 
 template <typename T, int NC, int KR, bool WT, int PRO, bool STATS, bool RED = false>
 void launch_t(const Args& a, int cus, hipStream_t s) {
+  if constexpr (one_wg_per_cu(NC, KR, PRO, RED)) {
+    int d = g_c1bn_depth >= 2 && g_c1bn_depth <= 5 ? g_c1bn_depth : g_c1bn_depth1;
+    // the BN-backward prologue + reduction form keeps a ring index dynamic at depth 4 (scratch)
+    if (PRO == kProBnBwd && RED && d == 4) d = 5;
+    if (d == 5) return launch_d<T, NC, KR, WT, PRO, STATS, RED, 5>(a, cus, s);
+    if (d == 4) return launch_d<T, NC, KR, WT, PRO, STATS, RED, 4>(a, cus, s);
+    if (d == 2) return launch_d<T, NC, KR, WT, PRO, STATS, RED, 2>(a, cus, s);
+    return launch_d<T, NC, KR, WT, PRO, STATS, RED, 3>(a, cus, s);
+  }
   const int d = g_c1bn_depth == 2 || g_c1bn_depth == 3 ? g_c1bn_depth : default_depth(NC, KR);
   if (d == 3) launch_d<T, NC, KR, WT, PRO, STATS, RED, 3>(a, cus, s);
   else launch_d<T, NC, KR, WT, PRO, STATS, RED, 2>(a, cus, s);

@@ -252,35 +252,69 @@ __global__ void coef_from_stats(const float* __restrict__ mean, const float* __r
 // MASKOUT: also write the ReLU mask as one bit per element (bit k of byte i = element 8i+k), so
 // the backward of a residual add+ReLU needs neither z nor a recompute (1/16 of a bf16 tensor)
 template <typename T, bool HAS_Z, bool RELU, bool MASKOUT>
+__device__ __forceinline__ void apply_vec(const T* __restrict__ x, const T* __restrict__ z, T* __restrict__ y,
+                                          uint8_t* __restrict__ mask, int64_t i, float (&v)[8], const float (&zz)[8],
+                                          const float (&sc)[8], const float (&sh)[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float o = fmaf(v[k], sc[k], sh[k]);
+    if constexpr (HAS_Z) o += zz[k];
+    if constexpr (RELU) o = fmaxf(o, 0.f);
+    v[k] = o;
+  }
+  Vec8<T>::store(y + i * 8, v);
+  if constexpr (MASKOUT) {
+    unsigned b = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) b |= (v[k] > 0.f ? 1u : 0u) << k;
+    mask[i] = (uint8_t)b;
+  }
+}
+
+// Elementwise passes: when the grid stride is a multiple of C (every power-of-two C up to the
+// stride: all ResNet widths), a lane keeps ONE 8-channel group for the whole pass, so its
+// per-channel coefficients are loaded once into registers instead of once per vector (they were
+// 2-5 extra 32-byte loads per 16-byte data load), and kEwU vectors are in flight per lane.
+constexpr int kEwU = 4;
+
+template <typename T, bool HAS_Z, bool RELU, bool MASKOUT>
 __global__ void __launch_bounds__(256) apply_kernel(const T* __restrict__ x, const T* __restrict__ z,
                                                     const float* __restrict__ coef, T* __restrict__ y, int64_t nvec,
                                                     int c, uint8_t* __restrict__ mask) {
   const int64_t stride = (int64_t)gridDim.x * 256;
   const int cstep = (int)((stride * 8) % c);
   int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  // the channel offset advances by a fixed step per grid stride: no 64-bit modulo in the loop
-  for (int c0 = (int)((i * 8) % c); i < nvec; i += stride, c0 = c0 + cstep >= c ? c0 + cstep - c : c0 + cstep) {
-    const int64_t e = i * 8;
-    float v[8], sc[8], sh[8];
-    Vec8<T>::load(v, x + e);
+  if (cstep == 0) {
+    const int c0 = (int)((i * 8) % c);
+    float sc[8], sh[8];
     load8f(sc, coef + c0);
     load8f(sh, coef + c + c0);
-    float zz[8];
-    if constexpr (HAS_Z) Vec8<T>::load(zz, z + e);
+    for (; i + (kEwU - 1) * stride < nvec; i += kEwU * stride) {
+      float v[kEwU][8], zz[kEwU][8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float o = fmaf(v[k], sc[k], sh[k]);
-      if constexpr (HAS_Z) o += zz[k];
-      if constexpr (RELU) o = fmaxf(o, 0.f);
-      v[k] = o;
-    }
-    Vec8<T>::store(y + e, v);
-    if constexpr (MASKOUT) {
-      unsigned b = 0;
+      for (int u = 0; u < kEwU; ++u) {
+        Vec8<T>::load(v[u], x + (i + u * stride) * 8);
+        if constexpr (HAS_Z) Vec8<T>::load(zz[u], z + (i + u * stride) * 8);
+      }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) b |= (v[k] > 0.f ? 1u : 0u) << k;
-      mask[i] = (uint8_t)b;
+      for (int u = 0; u < kEwU; ++u) apply_vec<T, HAS_Z, RELU, MASKOUT>(x, z, y, mask, i + u * stride, v[u], zz[u], sc, sh);
     }
+    for (; i < nvec; i += stride) {
+      float v[8], zz[8];
+      Vec8<T>::load(v, x + i * 8);
+      if constexpr (HAS_Z) Vec8<T>::load(zz, z + i * 8);
+      apply_vec<T, HAS_Z, RELU, MASKOUT>(x, z, y, mask, i, v, zz, sc, sh);
+    }
+    return;
+  }
+  // general C: the channel offset advances by a fixed step per grid stride (no 64-bit modulo)
+  for (int c0 = (int)((i * 8) % c); i < nvec; i += stride, c0 = c0 + cstep >= c ? c0 + cstep - c : c0 + cstep) {
+    float v[8], sc[8], sh[8], zz[8];
+    Vec8<T>::load(v, x + i * 8);
+    load8f(sc, coef + c0);
+    load8f(sh, coef + c + c0);
+    if constexpr (HAS_Z) Vec8<T>::load(zz, z + i * 8);
+    apply_vec<T, HAS_Z, RELU, MASKOUT>(x, z, y, mask, i, v, zz, sc, sh);
   }
 }
 
@@ -289,6 +323,21 @@ __global__ void __launch_bounds__(256) apply_kernel(const T* __restrict__ x, con
 // y = relu(bn_main(x) + bn_short(z))): both normalizations in the single output pass, so the
 // shortcut branch's normalized tensor is never written or re-read.
 template <typename T, bool MASKOUT>
+__device__ __forceinline__ void apply_dual_vec(T* __restrict__ y, uint8_t* __restrict__ mask, int64_t i,
+                                               float (&v)[8], const float (&w)[8], const float (&sx)[8],
+                                               const float (&hx)[8], const float (&sz)[8], const float (&hz)[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = fmaxf(fmaf(v[k], sx[k], hx[k]) + fmaf(w[k], sz[k], hz[k]), 0.f);
+  Vec8<T>::store(y + i * 8, v);
+  if constexpr (MASKOUT) {
+    unsigned b = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) b |= (v[k] > 0.f ? 1u : 0u) << k;
+    mask[i] = (uint8_t)b;
+  }
+}
+
+template <typename T, bool MASKOUT>
 __global__ void __launch_bounds__(256) apply_dual_kernel(const T* __restrict__ x, const T* __restrict__ z,
                                                          const float* __restrict__ cx, const float* __restrict__ cz,
                                                          T* __restrict__ y, int64_t nvec, int c,
@@ -296,24 +345,40 @@ __global__ void __launch_bounds__(256) apply_dual_kernel(const T* __restrict__ x
   const int64_t stride = (int64_t)gridDim.x * 256;
   const int cstep = (int)((stride * 8) % c);
   int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  for (int c0 = (int)((i * 8) % c); i < nvec; i += stride, c0 = c0 + cstep >= c ? c0 + cstep - c : c0 + cstep) {
-    const int64_t e = i * 8;
-    float v[8], w[8], sx[8], hx[8], sz[8], hz[8];
-    Vec8<T>::load(v, x + e);
-    Vec8<T>::load(w, z + e);
+  if (cstep == 0) {  // fixed channel group per lane (see apply_kernel)
+    const int c0 = (int)((i * 8) % c);
+    float sx[8], hx[8], sz[8], hz[8];
     load8f(sx, cx + c0);
     load8f(hx, cx + c + c0);
     load8f(sz, cz + c0);
     load8f(hz, cz + c + c0);
+    for (; i + (kEwU - 1) * stride < nvec; i += kEwU * stride) {
+      float v[kEwU][8], w[kEwU][8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = fmaxf(fmaf(v[k], sx[k], hx[k]) + fmaf(w[k], sz[k], hz[k]), 0.f);
-    Vec8<T>::store(y + e, v);
-    if constexpr (MASKOUT) {
-      unsigned b = 0;
+      for (int u = 0; u < kEwU; ++u) {
+        Vec8<T>::load(v[u], x + (i + u * stride) * 8);
+        Vec8<T>::load(w[u], z + (i + u * stride) * 8);
+      }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) b |= (v[k] > 0.f ? 1u : 0u) << k;
-      mask[i] = (uint8_t)b;
+      for (int u = 0; u < kEwU; ++u) apply_dual_vec<T, MASKOUT>(y, mask, i + u * stride, v[u], w[u], sx, hx, sz, hz);
     }
+    for (; i < nvec; i += stride) {
+      float v[8], w[8];
+      Vec8<T>::load(v, x + i * 8);
+      Vec8<T>::load(w, z + i * 8);
+      apply_dual_vec<T, MASKOUT>(y, mask, i, v, w, sx, hx, sz, hz);
+    }
+    return;
+  }
+  for (int c0 = (int)((i * 8) % c); i < nvec; i += stride, c0 = c0 + cstep >= c ? c0 + cstep - c : c0 + cstep) {
+    float v[8], w[8], sx[8], hx[8], sz[8], hz[8];
+    Vec8<T>::load(v, x + i * 8);
+    Vec8<T>::load(w, z + i * 8);
+    load8f(sx, cx + c0);
+    load8f(hx, cx + c + c0);
+    load8f(sz, cz + c0);
+    load8f(hz, cz + c + c0);
+    apply_dual_vec<T, MASKOUT>(y, mask, i, v, w, sx, hx, sz, hz);
   }
 }
 
@@ -516,6 +581,23 @@ __global__ void __launch_bounds__(256) bwd_coef_group(const float* __restrict__ 
 }
 
 template <typename T, bool HAS_Z, bool MASK>
+__device__ __forceinline__ void bwd_apply_vec(T* __restrict__ dx, int64_t i, float (&g)[8], float (&v)[8],
+                                              const float (&zz)[8], const float (&A)[8], const float (&B)[8],
+                                              const float (&K)[8], const float (&sc)[8], const float (&sh)[8]) {
+  if constexpr (MASK) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float o = fmaf(v[k], sc[k], sh[k]);
+      if constexpr (HAS_Z) o += zz[k];
+      if (!(o > 0.f)) g[k] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = fmaf(A[k], g[k], fmaf(B[k], v[k], K[k]));
+  Vec8<T>::store(dx + i * 8, v);
+}
+
+template <typename T, bool HAS_Z, bool MASK>
 __global__ void __launch_bounds__(256) bwd_apply(const T* __restrict__ dy, const T* __restrict__ x,
                                                  const T* __restrict__ z, const float* __restrict__ cf,
                                                  const float* __restrict__ cb, T* __restrict__ dx, int64_t nvec,
@@ -523,29 +605,51 @@ __global__ void __launch_bounds__(256) bwd_apply(const T* __restrict__ dy, const
   const int64_t stride = (int64_t)gridDim.x * 256;
   const int cstep = (int)((stride * 8) % c);
   int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  for (int c0 = (int)((i * 8) % c); i < nvec; i += stride, c0 = c0 + cstep >= c ? c0 + cstep - c : c0 + cstep) {
-    const int64_t e = i * 8;
-    float g[8], v[8], A[8], B[8], K[8];
-    Vec8<T>::load(g, dy + e);
-    Vec8<T>::load(v, x + e);
+  float sc[8], sh[8], zz[8];
+  if (cstep == 0) {  // fixed channel group per lane (see apply_kernel)
+    const int c0 = (int)((i * 8) % c);
+    float A[8], B[8], K[8];
     load8f(A, cb + c0);
     load8f(B, cb + c + c0);
     load8f(K, cb + 2 * c + c0);
     if constexpr (MASK) {
-      float sc[8], sh[8], zz[8];
       load8f(sc, cf + c0);
       load8f(sh, cf + c + c0);
-      if constexpr (HAS_Z) Vec8<T>::load(zz, z + e);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        float o = fmaf(v[k], sc[k], sh[k]);
-        if constexpr (HAS_Z) o += zz[k];
-        if (!(o > 0.f)) g[k] = 0.f;
-      }
     }
+    for (; i + (kEwU - 1) * stride < nvec; i += kEwU * stride) {
+      float g[kEwU][8], v[kEwU][8], zu[kEwU][8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = fmaf(A[k], g[k], fmaf(B[k], v[k], K[k]));
-    Vec8<T>::store(dx + e, v);
+      for (int u = 0; u < kEwU; ++u) {
+        Vec8<T>::load(g[u], dy + (i + u * stride) * 8);
+        Vec8<T>::load(v[u], x + (i + u * stride) * 8);
+        if constexpr (MASK && HAS_Z) Vec8<T>::load(zu[u], z + (i + u * stride) * 8);
+      }
+#pragma unroll
+      for (int u = 0; u < kEwU; ++u)
+        bwd_apply_vec<T, HAS_Z, MASK>(dx, i + u * stride, g[u], v[u], zu[u], A, B, K, sc, sh);
+    }
+    for (; i < nvec; i += stride) {
+      float g[8], v[8];
+      Vec8<T>::load(g, dy + i * 8);
+      Vec8<T>::load(v, x + i * 8);
+      if constexpr (MASK && HAS_Z) Vec8<T>::load(zz, z + i * 8);
+      bwd_apply_vec<T, HAS_Z, MASK>(dx, i, g, v, zz, A, B, K, sc, sh);
+    }
+    return;
+  }
+  for (int c0 = (int)((i * 8) % c); i < nvec; i += stride, c0 = c0 + cstep >= c ? c0 + cstep - c : c0 + cstep) {
+    float g[8], v[8], A[8], B[8], K[8];
+    Vec8<T>::load(g, dy + i * 8);
+    Vec8<T>::load(v, x + i * 8);
+    load8f(A, cb + c0);
+    load8f(B, cb + c + c0);
+    load8f(K, cb + 2 * c + c0);
+    if constexpr (MASK) {
+      load8f(sc, cf + c0);
+      load8f(sh, cf + c + c0);
+      if constexpr (HAS_Z) Vec8<T>::load(zz, z + i * 8);
+    }
+    bwd_apply_vec<T, HAS_Z, MASK>(dx, i, g, v, zz, A, B, K, sc, sh);
   }
 }
 
