@@ -245,6 +245,20 @@ at::Tensor subsample2x(const at::Tensor& x, int64_t n, int64_t h, int64_t w) {
   return y;
 }
 
+// [K, C, R, S] channels_last 16-bit weight -> its data-gradient image [C, len(taps), K] (taps: r * S + s)
+at::Tensor tap_weights(const at::Tensor& w, const std::vector<int64_t>& taps) {
+  TORCH_CHECK(w.is_cuda() && w.dim() == 4 && w.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  (w.scalar_type() == at::kBFloat16 || w.scalar_type() == at::kHalf),
+              "tap_weights: w must be a channels_last 16-bit [K, C, R, S] GPU tensor");
+  const int k = (int)w.size(0), c = (int)w.size(1), rs = (int)(w.size(2) * w.size(3));
+  TORCH_CHECK(!taps.empty() && taps.size() <= 9 && k % 8 == 0 && c % 8 == 0, "tap_weights: 1-9 taps, K, C % 8 == 0");
+  std::vector<int> t(taps.begin(), taps.end());
+  const c10::hip::HIPGuard g(w.get_device());
+  auto dst = at::empty({c, (int64_t)t.size(), k}, w.options().memory_format(at::MemoryFormat::Contiguous));
+  conv_tap_weights(w.data_ptr(), dst.data_ptr(), k, c, rs, t.data(), (int)t.size(), cur_stream());
+  return dst;
+}
+
 // pcoef: [4K] (a scale | res scale | a shift | res shift), or with split the output BN's [2K]
 // scale | shift and res_coef the residual BN's [2K] (none: the identity shortcut)
 std::vector<at::Tensor> bn1x1_addrelu(const at::Tensor& a, const at::Tensor& res, const at::Tensor& pcoef,
@@ -643,6 +657,7 @@ void bind_conv(pybind11::module_& root) {
   m.def("bn_finalize", &bn_finalize);
   m.def("hfp_set_mode", &conv_hfp_set_mode, pybind11::arg("mode"));
   m.def("subsample2x", &subsample2x, pybind11::arg("x"), pybind11::arg("n"), pybind11::arg("h"), pybind11::arg("w"));
+  m.def("tap_weights", &tap_weights, pybind11::arg("w"), pybind11::arg("taps"));
   m.def("bn1x1_addrelu", &bn1x1_addrelu, pybind11::arg("a"), pybind11::arg("res"), pybind11::arg("pcoef"),
         pybind11::arg("w"), pybind11::arg("shift") = pybind11::none(), pybind11::arg("out") = pybind11::none(),
         pybind11::arg("split") = false, pybind11::arg("res_coef") = pybind11::none());

@@ -5,6 +5,7 @@
 // (conv1x1_bn.hip, its BN-statistics epilogue and split-M weight gradient) run it.  One 16-byte
 // vector per lane, grid-stride; a pixel's C channels are contiguous in both tensors, so each wave
 // reads and writes whole 128-byte runs (torch's generic strided copy took 36 us per ResNet call).
+// conv_tap_weights: the data-gradient weight image (below).
 #include "apex_amd/conv_api.h"
 #include "apex_amd/dispatch.h"
 #include "apex_amd/fastdiv.h"
@@ -26,7 +27,65 @@ __global__ void __launch_bounds__(256) subsample2x_kernel(const uint4* __restric
   }
 }
 
+// tap_weights: dst[c][j][k] = w[k][tap[j]][c] — the [C][taps][K] operand image the tap kernels
+// take for a data gradient (conv_tap_dgrad), from the channels_last [K][R S][C] weight, with an
+// optional tap subset (the stride-2 phases).  A 64 (k) x 64 (c) tile per workgroup through LDS:
+// 16-byte reads along c, 16-byte writes along k (torch's permute-copy ran a 2-byte strided
+// kernel: ~13 us per ResNet-50 3x3 layer and step).
+struct TapList {
+  int n;
+  int t[9];
+};
+
+template <int PAD>
+__global__ void __launch_bounds__(256) tap_weights_kernel(const uint16_t* __restrict__ w, uint16_t* __restrict__ dst,
+                                                          int k, int c, int rs, TapList taps) {
+  __shared__ uint16_t tile[64][64 + PAD];
+  const int c0 = blockIdx.x * 64, k0 = blockIdx.y * 64, j = blockIdx.z;
+  const int tap = taps.t[j];
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = tid / 8 + 32 * h, c8 = (tid % 8) * 8;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (k0 + r < k && c0 + c8 < c)
+      v = *reinterpret_cast<const uint4*>(w + ((size_t)(k0 + r) * rs + tap) * c + c0 + c8);
+    const uint32_t q[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      tile[r][c8 + 2 * e] = (uint16_t)(q[e] & 0xffffu);
+      tile[r][c8 + 2 * e + 1] = (uint16_t)(q[e] >> 16);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int cc = tid / 8 + 32 * h, k8 = (tid % 8) * 8;
+    if (c0 + cc >= c || k0 + k8 >= k) continue;
+    uint32_t q[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      q[e] = (uint32_t)tile[k8 + 2 * e][cc] | ((uint32_t)tile[k8 + 2 * e + 1][cc] << 16);
+    *reinterpret_cast<uint4*>(dst + ((size_t)(c0 + cc) * taps.n + j) * k + k0 + k8) = make_uint4(q[0], q[1], q[2], q[3]);
+  }
+}
+
 }  // namespace layout
+
+void conv_tap_weights(const void* w, void* dst, int k, int c, int rs, const int* taps, int ntaps, hipStream_t s) {
+  if (k % 8 || c % 8 || k <= 0 || c <= 0 || ntaps < 1 || ntaps > 9 || rs < 1 || rs > 9)
+    throw std::runtime_error("conv_tap_weights: K, C multiples of 8, 1-9 taps");
+  if (((uintptr_t)w & 15) || ((uintptr_t)dst & 15)) throw std::runtime_error("conv_tap_weights: 16-byte alignment");
+  layout::TapList tl{};
+  tl.n = ntaps;
+  for (int j = 0; j < ntaps; ++j) {
+    if (taps[j] < 0 || taps[j] >= rs) throw std::runtime_error("conv_tap_weights: tap index out of range");
+    tl.t[j] = taps[j];
+  }
+  hipLaunchKernelGGL(layout::tap_weights_kernel<2>, dim3((unsigned)((c + 63) / 64), (unsigned)((k + 63) / 64), ntaps),
+                     dim3(256), 0, s, (const uint16_t*)w, (uint16_t*)dst, k, c, rs, tl);
+  check_launch("conv_tap_weights");
+}
 
 void conv_subsample2x(const void* x, void* y, int n, int h, int w, int c, int dtype, int cus, hipStream_t s) {
   if ((dtype != kBF16 && dtype != kF16) || c % 8 || n <= 0 || h <= 0 || w <= 0)

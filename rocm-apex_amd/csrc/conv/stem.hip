@@ -263,7 +263,9 @@ __global__ void __launch_bounds__(256, 1) fprop_kernel(const FpArgs a) {
 }
 
 // ---- BN apply + ReLU + 3x3/2 max pool (pad 1) -------------------------------------------------
-constexpr int PR = 2;  // pooled rows per lane: 5 input rows x 3 columns, all loads issued first
+// pooled rows per lane (2 PR + 1 input rows x 3 columns, all loads issued first; adjacent pooled
+// rows share an input row): APEX_AMD_STEM_PR = 2 (default) | 4 — 4 measured 144.7 vs 128 us in the
+// step (profiles/r05/ab_stem_pr_r05x.txt): the taller strip holds 27 loads per lane in flight
 
 struct PoolArgs {
   const uint16_t* y;   // [N][OH][OW][64]
@@ -300,7 +302,7 @@ __device__ __forceinline__ void hbest(const uint4 (&raw)[3], const bool (&ok)[3]
   }
 }
 
-template <typename T>
+template <typename T, int PR>
 __global__ void __launch_bounds__(256) pool_fwd_kernel(const PoolArgs a) {
   const Geo& g = a.g;
   const uint32_t total = (uint32_t)g.n * a.strips * g.pw * 8;
@@ -779,13 +781,18 @@ void stem_pool_fwd(const void* y, const float* coef, void* p, uint8_t* idx, int 
   a.coef = coef;
   a.p = (uint16_t*)p;
   a.idx = idx;
-  a.strips = (a.g.ph + stem::PR - 1) / stem::PR;
+  static const int pr = [] {
+    const char* e = std::getenv("APEX_AMD_STEM_PR");
+    return e && std::atoi(e) == 4 ? 4 : 2;
+  }();
+  a.strips = (a.g.ph + pr - 1) / pr;
   const int64_t total = (int64_t)n * a.strips * a.g.pw * 8;
   int64_t grid = (total + 255) / 256;
   if (grid > (int64_t)cus * 16) grid = (int64_t)cus * 16;
   dispatch_16(t, [&](auto tag) {
     using T = typename decltype(tag)::type;
-    hipLaunchKernelGGL((stem::pool_fwd_kernel<T>), dim3((unsigned)grid), dim3(256), 0, s, a);
+    if (pr == 2) hipLaunchKernelGGL((stem::pool_fwd_kernel<T, 2>), dim3((unsigned)grid), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((stem::pool_fwd_kernel<T, 4>), dim3((unsigned)grid), dim3(256), 0, s, a);
   }, "stem pool fwd");
   check_launch("stem_pool_fwd");
 }

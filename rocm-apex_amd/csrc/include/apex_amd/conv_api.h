@@ -96,6 +96,9 @@ bool conv1x1_bn_supported(int64_t m, int k, int ncols);
 // y [N][ceil(h/2)][ceil(w/2)][c] = x [N][h][w][c] at even (y, x): a stride-2 1x1 conv's operand
 // (csrc/conv/layout.hip; 16-bit, c % 8 == 0, 16-byte aligned)
 void conv_subsample2x(const void* x, void* y, int n, int h, int w, int c, int dtype, int cus, hipStream_t s);
+// dst[c][j][k] = w[k][taps[j]][c]: the data-gradient weight image [C][ntaps][K] of a channels_last
+// [K][rs][C] 16-bit weight (rs = R * S), for an ordered tap subset (1..9 taps)
+void conv_tap_weights(const void* w, void* dst, int k, int c, int rs, const int* taps, int ntaps, hipStream_t s);
 int conv1x1_bn_partials(int64_t m, int k, int ncols, bool pro, int cus, bool pro_addrelu = false);
 void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int ncols, bool w_kmajor_out, int dtype,
                 const float* pcoef, const float* shift, float* part, int cus, hipStream_t s,

@@ -277,10 +277,14 @@ def conv_tap_dgrad(gy, w, x_shape, stride, pad, mask=None):
     alloc = torch.empty if covered else torch.zeros  # phases no tap reaches get zero gradient
     dx = alloc((n, h, wd, c), dtype=gy.dtype, device=gy.device).permute(0, 3, 1, 2)
     wk = w.permute(1, 2, 3, 0)  # [C, R, S, K] view
+    native_w = (hasattr(ext, "tap_weights") and w.is_contiguous(memory_format=torch.channels_last)
+                and kout % 8 == 0 and c % 8 == 0)
     for ph, pw, oh, ow, taps in phases:
         if not taps or oh <= 0 or ow <= 0:
             continue
-        if len(taps) == k * k:  # every tap in (r, s) row-major order: one permute-copy, no stack
+        if native_w:  # [C, taps, K] in one tiled transpose launch (layout.hip conv_tap_weights)
+            wt = ext.tap_weights(w, [r * w.shape[3] + s_ for r, s_, _, _ in taps])
+        elif len(taps) == k * k:  # every tap in (r, s) row-major order: one permute-copy, no stack
             wt = wk.reshape(c, k * k, kout).contiguous()  # [C, taps, K]
         else:
             wt = torch.stack([wk[:, r, s_, :] for r, s_, _, _ in taps], 1).contiguous()

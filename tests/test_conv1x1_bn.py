@@ -331,3 +331,19 @@ def test_gpu_subsample2x(n, h, w, c):
     x = torch.randn(n * h * w, c, device="cuda").to(torch.bfloat16)
     y = ext.subsample2x(x, n, h, w)
     assert torch.equal(y, x.view(n, h, w, c)[:, ::2, ::2].reshape(-1, c))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,c,ks,taps", [(64, 64, 3, list(range(9))), (128, 256, 3, list(range(9))),
+                                         (72, 40, 3, [0, 2, 6, 8]), (512, 512, 3, [4]), (256, 1024, 1, [0]),
+                                         (200, 136, 3, [1, 7])])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_gpu_tap_weights(k, c, ks, taps, dt):
+    """The data-gradient weight image dst[c][j][k] = w[k][taps[j]][c] (csrc/conv/layout.hip): bitwise
+    the permute + stack copy it replaces in ops/conv.py conv_tap_dgrad, ragged tiles included."""
+    ext = _ext()
+    w = torch.randn(k, c, ks, ks, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
+    out = ext.tap_weights(w, taps)
+    wk = w.permute(1, 2, 3, 0)
+    ref = torch.stack([wk[:, t // ks, t % ks, :] for t in taps], 1).contiguous()
+    assert out.shape == (c, len(taps), k) and torch.equal(out, ref)
