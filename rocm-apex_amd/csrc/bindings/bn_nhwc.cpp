@@ -417,6 +417,33 @@ std::vector<at::Tensor> apply(at::Tensor x, OT z, at::Tensor coef, bool relu, bo
   return {y, mask};
 }
 
+// reduction only (the ReLU mask recomputed from x, nothing written): (coef [5, C] = coef_bwd [3, C]
+// followed by coef_fwd [2, C], grad_w, grad_b) — the operand of a consumer that applies
+// dx = A (mask ? dy : 0) + B x + K itself (the 1x1 dgrad's recomputed-mask prologue)
+std::vector<at::Tensor> bwd_coef(at::Tensor dy_, at::Tensor x, OT w, at::Tensor save_mean, at::Tensor save_invstd,
+                                 at::Tensor coef_fwd) {
+  check2d(x, "input");
+  const c10::hip::HIPGuard g(x.get_device());
+  at::Tensor dy = dy_.contiguous();
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "bn_nhwc: grad must match input");
+  const int64_t m = x.size(0);
+  const int c = (int)x.size(1);
+  TORCH_CHECK(coef_fwd.is_contiguous() && coef_fwd.scalar_type() == at::kFloat && coef_fwd.numel() == 2 * (int64_t)c,
+              "bn_nhwc bwd_coef: coef_fwd must be fp32 [2C]");
+  const int cus = device_cus(x.get_device());
+  int64_t wsf = 0;
+  const int gy = bn_nhwc_plan(m, c, cus, &wsf);
+  auto fo = x.options().dtype(at::kFloat);
+  auto ws = at::empty({wsf}, fo);
+  auto gw = at::empty({c}, fo), gb = at::empty({c}, fo), coef = at::empty({5, c}, fo);
+  bn_nhwc_bwd_reduce(dy.data_ptr(), x.data_ptr(), dtype_code(x.scalar_type()), nullptr, coef_fwd.data_ptr<float>(), true,
+                     save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(), fptr(w), gw.data_ptr<float>(),
+                     gb.data_ptr<float>(), coef.data_ptr<float>(), nullptr, m, c, ws.data_ptr<float>(), gy, cus,
+                     cur_stream(), nullptr, nullptr);
+  coef.narrow(0, 3, 2).view({-1}).copy_(coef_fwd.view({-1}));
+  return {coef, gw, gb};
+}
+
 // backward reduction only: (dy_masked, coef_bwd[3, C], grad_w, grad_b).  The dx pass is left to
 // the consumer (bwd_apply below, or a convolution whose operand prologue computes
 // dx = coef_bwd[0] * dy_masked + coef_bwd[1] * x + coef_bwd[2] on load).
@@ -469,6 +496,7 @@ void bind_bn_nhwc(pybind11::module_& root) {
   m.def("stats", &stats);
   m.def("bwd_reduce", &bwd_reduce);
   m.def("bwd_apply", &bwd_apply);
+  m.def("bwd_coef", &bwd_coef);
   m.def("apply", &apply, pybind11::arg("x"), pybind11::arg("z"), pybind11::arg("coef"), pybind11::arg("relu"),
         pybind11::arg("want_mask") = false, pybind11::arg("coef_z") = c10::nullopt);
   m.def("fwd_train_dual", &fwd_train_dual);

@@ -202,10 +202,13 @@ std::vector<at::Tensor> bn1x1(const at::Tensor& a, const at::Tensor& w, bool w_k
     return t->data_ptr<float>();
   };
   const bool bnbwd = py.has_value();
-  const float* pc = f32(pcoef, (bnbwd ? 3 : 2) * (int64_t)k, "pcoef");
+  // BN-backward prologue: pcoef [3K] (a = the masked gradient) or [5K] (+ the forward scale | shift:
+  // the ReLU mask recomputed from py, a = the unmasked gradient)
+  const bool pmask = bnbwd && pcoef.has_value() && pcoef->numel() == 5 * (int64_t)k;
+  const float* pc = f32(pcoef, (bnbwd ? (pmask ? 5 : 3) : 2) * (int64_t)k, "pcoef");
   TORCH_CHECK(!bnbwd || (pc && w_kmajor_out && py->is_cuda() && py->is_contiguous() &&
                          py->scalar_type() == a.scalar_type() && py->sizes() == a.sizes()),
-              "bn1x1: py (BN-backward prologue) needs the dgrad form, pcoef [3K] and a tensor shaped like a");
+              "bn1x1: py (BN-backward prologue) needs the dgrad form, pcoef [3K] / [5K] and a tensor shaped like a");
   TORCH_CHECK(!want_aout || bnbwd, "bn1x1: want_aout needs the BN-backward prologue");
   const float* sh = f32(shift, ncols, "shift");
   const c10::hip::HIPGuard g(a.get_device());
@@ -223,7 +226,7 @@ std::vector<at::Tensor> bn1x1(const at::Tensor& a, const at::Tensor& w, bool w_k
   conv1x1_bn(a.data_ptr(), w.data_ptr(), y.data_ptr(), m, k, ncols, w_kmajor_out, dtype_code(a.scalar_type()), pc, sh,
              stats ? part.data_ptr<float>() : nullptr, cus, cur_stream(), res.has_value() ? res->data_ptr() : nullptr,
              bnbwd ? py->data_ptr() : nullptr, want_aout ? aout.data_ptr() : nullptr, false, nullptr, (int)res_h,
-             (int)res_w);
+             (int)res_w, false, nullptr, pmask);
   return {y, part, aout};
 }
 
@@ -401,16 +404,19 @@ std::vector<at::Tensor> dgrad_bnred(const at::Tensor& g, const at::Tensor& w, co
                 "dgrad_bnred: res must be a contiguous [M, ncols] tensor (subsampled rows with res_hw)");
   const bool pro = py.has_value();
   TORCH_CHECK(pro == pcoef.has_value(), "dgrad_bnred: py and pcoef go together");
+  const bool pmask = pro && pcoef->numel() == 5 * (int64_t)k;  // [5k]: the ReLU mask recomputed from py
   if (pro)
     TORCH_CHECK(py->is_contiguous() && py->sizes() == g.sizes() && py->scalar_type() == g.scalar_type() &&
-                    pcoef->scalar_type() == at::kFloat && pcoef->is_contiguous() && pcoef->numel() == 3 * (int64_t)k,
-                "dgrad_bnred: py must match g, pcoef fp32 [3k]");
+                    pcoef->scalar_type() == at::kFloat && pcoef->is_contiguous() &&
+                    (pcoef->numel() == 3 * (int64_t)k || pmask),
+                "dgrad_bnred: py must match g, pcoef fp32 [3k] or [5k]");
   TORCH_CHECK(!want_aout || pro, "dgrad_bnred: want_aout needs the prologue");
   TORCH_CHECK(conv1x1_bn_supported(m, k, ncols), "dgrad_bnred: unsupported shape");
   const c10::hip::HIPGuard guard(g.get_device());
   const int cus = device_cus(g.get_device());
   auto out = at::empty({m, ncols}, g.options());
-  auto part = at::empty({2, conv1x1_dgrad_bnred_partials(m, k, ncols, cus, pro), ncols}, g.options().dtype(at::kFloat));
+  auto part =
+      at::empty({2, conv1x1_dgrad_bnred_partials(m, k, ncols, cus, pro, pmask), ncols}, g.options().dtype(at::kFloat));
   at::Tensor aout;
   if (want_aout) aout = at::empty_like(g);
   conv1x1_dgrad_bnred(g.data_ptr(), w.data_ptr(), out.data_ptr(), m, k, ncols, dtype_code(g.scalar_type()),
@@ -418,7 +424,7 @@ std::vector<at::Tensor> dgrad_bnred(const at::Tensor& g, const at::Tensor& w, co
                       x.data_ptr(), mean.data_ptr<float>(), part.data_ptr<float>(), cus, cur_stream(),
                       coef.has_value() ? coef->data_ptr<float>() : nullptr, pro ? py->data_ptr() : nullptr,
                       pro ? pcoef->data_ptr<float>() : nullptr, want_aout ? aout.data_ptr() : nullptr, (int)res_h,
-                      (int)res_w);
+                      (int)res_w, pmask);
   return {out, part, aout};
 }
 

@@ -77,11 +77,17 @@ constexpr int kProBnAddRelu = 3;  // a' = relu(fma(a, c[k], c[2K + k]) + fma(y, 
                                   //   block below's output BN + residual / downsample BN (y) + ReLU with
                                   //   the apply passes' exact arithmetic, so its apply pass is gone; a'
                                   //   and its ReLU bits are written out for the block's other uses
+constexpr int kProBnBwdMask = 4;  // a' = c[k] * (y * c[3K + k] + c[4K + k] > 0 ? a : 0) + c[K + k] * y + c[2K + k]:
+                                  //   kProBnBwd with the BN's forward ReLU mask recomputed from y (the
+                                  //   unmasked gradient in: the reduction pass writes nothing), the
+                                  //   standalone bwd_apply's exact arithmetic
 // per-k coefficient rows of a prologue
 constexpr int pro_rows(int pro) {
-  return pro == kProBnRelu ? 2 : pro == kProBnBwd ? 3 : pro == kProBnAddRelu ? 4 : 0;
+  return pro == kProBnRelu ? 2 : pro == kProBnBwd ? 3 : pro == kProBnAddRelu ? 4 : pro == kProBnBwdMask ? 5 : 0;
 }
-constexpr bool pro_two(int pro) { return pro == kProBnBwd || pro == kProBnAddRelu; }  // a second operand
+constexpr bool pro_two(int pro) {  // a second operand
+  return pro == kProBnBwd || pro == kProBnAddRelu || pro == kProBnBwdMask;
+}
 
 constexpr int kSS = 64 + 8;  // staging row stride (elements): rows h and h+4 land 16 banks apart
 
@@ -219,6 +225,10 @@ __global__ void __launch_bounds__(NW * 64, (NW == 8 || one_wg_per_cu(NC, KR, PRO
             v = fmaf(to_f(T{(uint16_t)a[j]}), c[0][j], c[2][j]) + fmaf(to_f(T{(uint16_t)f.y[s][j]}), c[1][j], c[3][j]);
             v = fmaxf(v, 0.f);
             mb |= (v > 0.f ? 1u : 0u) << j;
+          } else if constexpr (PRO == kProBnBwdMask) {
+            const float yv = to_f(T{(uint16_t)f.y[s][j]});
+            const float g = fmaf(yv, c[3][j], c[4][j]) > 0.f ? to_f(T{(uint16_t)a[j]}) : 0.f;
+            v = fmaf(c[0][j], g, fmaf(c[1][j], yv, c[2][j]));
           } else {
             v = fmaf(c[0][j], to_f(T{(uint16_t)a[j]}), fmaf(c[1][j], to_f(T{(uint16_t)f.y[s][j]}), c[2][j]));
           }
@@ -691,7 +701,7 @@ void launch_t(const Args& a, int cus, hipStream_t s) {
   if constexpr (one_wg_per_cu(NC, KR, PRO, RED)) {
     int d = g_c1bn_depth >= 2 && g_c1bn_depth <= 5 ? g_c1bn_depth : g_c1bn_depth1;
     // the BN-backward prologue + reduction form keeps a ring index dynamic at depth 4 (scratch)
-    if (PRO == kProBnBwd && RED && d == 4) d = 5;
+    if ((PRO == kProBnBwd || PRO == kProBnBwdMask) && RED && d == 4) d = 5;
     if (d == 5) return launch_d<T, NC, KR, WT, PRO, STATS, RED, 5>(a, cus, s);
     if (d == 4) return launch_d<T, NC, KR, WT, PRO, STATS, RED, 4>(a, cus, s);
     if (d == 2) return launch_d<T, NC, KR, WT, PRO, STATS, RED, 2>(a, cus, s);
@@ -731,6 +741,16 @@ inline int col_tile(int ncols, int kr) {
   return ncols % 128 == 0 && kr <= max128 ? 128 : 64;
 }
 
+// the column tile, narrowed while the workgroup's LDS (weight image + staging + prologue rows +
+// reduction sums) would not fit: the recomputed-mask BN-backward prologue's 5 rows at k 512
+inline int col_tile_fit(int ncols, int kr, int pro, bool red) {
+  int nc = col_tile(ncols, kr);
+  while (nc > 64 && lds_bytes_nw(nc, kr, pro, red, pick_nw(nc, kr, pro, red)) > 160 * 1024) nc /= 2;
+  if (lds_bytes_nw(nc, kr, pro, red, pick_nw(nc, kr, pro, red)) > 160 * 1024)
+    throw std::runtime_error("conv1x1_bn: no column tile fits the LDS for this reduction depth / prologue");
+  return nc;
+}
+
 template <typename T, bool WT, int PRO, bool STATS, bool RED = false>
 void dispatch_shape(const Args& a, int nc, int kr, int cus, hipStream_t s) {
 #define C1BN_CASE(NC_, KR_)                                 \
@@ -767,14 +787,14 @@ inline void set_res_geometry(Args& a, int64_t m, int res_h, int res_w) {
 }  // namespace c1bn
 
 int conv1x1_bn_partials(int64_t m, int k, int ncols, bool pro, int cus, bool pro_addrelu) {
-  return c1bn::grid_x(m, c1bn::col_tile(ncols, k), k,
-                      pro_addrelu ? c1bn::kProBnAddRelu : pro ? c1bn::kProBnRelu : c1bn::kProNone, cus, ncols);
+  const int pk = pro_addrelu ? c1bn::kProBnAddRelu : pro ? c1bn::kProBnRelu : c1bn::kProNone;
+  return c1bn::grid_x(m, c1bn::col_tile_fit(ncols, k, pk, false), k, pk, cus, ncols);
 }
 
 void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int ncols, bool w_kmajor_out, int dtype,
                 const float* pcoef, const float* shift, float* part, int cus, hipStream_t s, const void* res,
                 const void* py, void* aout, bool pro_relu, uint8_t* bout, int res_h, int res_w, bool pc_split,
-                const float* pc_res) {
+                const float* pc_res, bool pro_mask) {
   if (!conv1x1_bn_supported(m, k, ncols)) throw std::runtime_error("conv1x1_bn: unsupported shape");
   c1bn::Args args{};
   args.pc_split = pc_split ? 1 : 0;
@@ -794,14 +814,15 @@ void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int nco
   args.py = static_cast<const uint16_t*>(py);
   args.aout = static_cast<uint16_t*>(aout);
   args.bout = bout;
-  const int nc = c1bn::col_tile(ncols, k);
   const bool wt = w_kmajor_out;
   const bool stats = part != nullptr;
   // py given: the two-operand prologue (pcoef = [3][k]) — BN backward, or with pro_relu the block
   // below's output BN + residual + ReLU; else pcoef = the BN apply + ReLU [2][k]
   const int pro = pcoef == nullptr ? c1bn::kProNone
-                  : py            ? (pro_relu ? c1bn::kProBnAddRelu : c1bn::kProBnBwd)
+                  : py            ? (pro_relu ? c1bn::kProBnAddRelu : pro_mask ? c1bn::kProBnBwdMask : c1bn::kProBnBwd)
                                   : c1bn::kProBnRelu;
+  if (pro_mask && pro != c1bn::kProBnBwdMask) throw std::runtime_error("conv1x1_bn: pro_mask needs py and pcoef");
+  const int nc = c1bn::col_tile_fit(ncols, k, pro, false);
   if (aout && !c1bn::pro_two(pro)) throw std::runtime_error("conv1x1_bn: aout needs a two-operand prologue");
   if (bout && pro != c1bn::kProBnAddRelu) throw std::runtime_error("conv1x1_bn: bout needs the add + ReLU prologue");
   auto go = [&](auto tag) {
@@ -811,9 +832,11 @@ void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int nco
         throw std::runtime_error("conv1x1_bn: the transposed-weight (dgrad) form takes the BN-backward prologue only");
       if (pro == c1bn::kProBnAddRelu) throw std::runtime_error("conv1x1_bn: the add + ReLU prologue is a forward option");
       if (pro == c1bn::kProBnBwd) c1bn::dispatch_shape<T, true, c1bn::kProBnBwd, false>(args, nc, k, cus, s);
+      else if (pro == c1bn::kProBnBwdMask) c1bn::dispatch_shape<T, true, c1bn::kProBnBwdMask, false>(args, nc, k, cus, s);
       else c1bn::dispatch_shape<T, true, c1bn::kProNone, false>(args, nc, k, cus, s);
     } else {
-      if (pro == c1bn::kProBnBwd) throw std::runtime_error("conv1x1_bn: BN-backward prologue is a dgrad-form option");
+      if (pro == c1bn::kProBnBwd || pro == c1bn::kProBnBwdMask)
+        throw std::runtime_error("conv1x1_bn: BN-backward prologue is a dgrad-form option");
       if (pro == c1bn::kProBnAddRelu) {
         if (stats) c1bn::dispatch_shape<T, false, c1bn::kProBnAddRelu, true>(args, nc, k, cus, s);
         else c1bn::dispatch_shape<T, false, c1bn::kProBnAddRelu, false>(args, nc, k, cus, s);
@@ -832,14 +855,15 @@ void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int nco
   check_launch("conv1x1_bn");
 }
 
-int conv1x1_dgrad_bnred_partials(int64_t m, int k, int ncols, int cus, bool pro) {
-  return c1bn::grid_x(m, c1bn::col_tile(ncols, k), k, pro ? c1bn::kProBnBwd : c1bn::kProNone, cus, ncols, true);
+int conv1x1_dgrad_bnred_partials(int64_t m, int k, int ncols, int cus, bool pro, bool pro_mask) {
+  const int pk = pro ? (pro_mask ? c1bn::kProBnBwdMask : c1bn::kProBnBwd) : c1bn::kProNone;
+  return c1bn::grid_x(m, c1bn::col_tile_fit(ncols, k, pk, true), k, pk, cus, ncols, true);
 }
 
 void conv1x1_dgrad_bnred(const void* g, const void* w, void* out, int64_t m, int k, int ncols, int dtype,
                          const void* res, const uint8_t* bits, const void* x, const float* mean, float* part, int cus,
                          hipStream_t s, const float* rcoef, const void* py, const float* pcoef, void* aout, int res_h,
-                         int res_w) {
+                         int res_w, bool pro_mask) {
   if (!conv1x1_bn_supported(m, k, ncols)) throw std::runtime_error("conv1x1_dgrad_bnred: unsupported shape");
   if ((!bits && !rcoef) || !x || !mean || !part)
     throw std::runtime_error("conv1x1_dgrad_bnred: a mask source (bits or coef), x, mean and part are required");
@@ -860,10 +884,12 @@ void conv1x1_dgrad_bnred(const void* g, const void* w, void* out, int64_t m, int
   args.pcoef = pcoef;
   args.py = static_cast<const uint16_t*>(py);
   args.aout = static_cast<uint16_t*>(aout);
-  const int nc = c1bn::col_tile(ncols, k);
+  const int nc = c1bn::col_tile_fit(ncols, k, py ? (pro_mask ? c1bn::kProBnBwdMask : c1bn::kProBnBwd) : c1bn::kProNone,
+                                    true);
   dispatch_16(dtype, [&](auto tag) {
     using T = typename decltype(tag)::type;
-    if (py) c1bn::dispatch_shape<T, true, c1bn::kProBnBwd, false, true>(args, nc, k, cus, s);
+    if (py && pro_mask) c1bn::dispatch_shape<T, true, c1bn::kProBnBwdMask, false, true>(args, nc, k, cus, s);
+    else if (py) c1bn::dispatch_shape<T, true, c1bn::kProBnBwd, false, true>(args, nc, k, cus, s);
     else c1bn::dispatch_shape<T, true, c1bn::kProNone, false, true>(args, nc, k, cus, s);
   }, "conv1x1_dgrad_bnred");
   check_launch("conv1x1_dgrad_bnred");

@@ -110,7 +110,10 @@ void conv1x1_bn(const void* a, const void* w, void* y, int64_t m, int k, int nco
                 int res_h = 0, int res_w = 0,  // > 0: res is [N][ceil(res_h/2)][ceil(res_w/2)][ncols], the
                                                //   stride-2 subsample's gradient, added at even (y, x) only
                 bool pc_split = false,         // add + ReLU form: pcoef = the output BN's [2][k] and pc_res
-                const float* pc_res = nullptr);  //   the residual BN's [2][k] (null: identity) instead of [4][k]
+                const float* pc_res = nullptr,   //   the residual BN's [2][k] (null: identity) instead of [4][k]
+                bool pro_mask = false);          // BN-backward prologue with the ReLU mask recomputed from py:
+                                                 //   pcoef [5][k] = A | B | K | fwd scale | fwd shift,
+                                                 //   a' = A (py * scale + shift > 0 ? a : 0) + B py + K
 // batch statistics from the partials: save_mean / save_invstd, running-stat EMA (nullable),
 // coef = [scale | shift] of the apply (w, b nullable = affine-free)
 void conv1x1_bn_finalize(const float* part, int g, int c, float n, const float* shift, const float* w, const float* b,
@@ -133,14 +136,15 @@ void conv1x1_wgrad(const void* g, const void* x, void* dw, int out_dtype, int64_
 // out = mask(g . W + res) (mask = bits, that BN's forward ReLU bit mask) and per-column partial
 // sums [2][G][ncols] of out and out * (x - mean); G = conv1x1_dgrad_bnred_partials(...).
 // conv1x1_bnbwd_finalize turns them into grad_w, grad_b and coef_bwd [3][C].
-int conv1x1_dgrad_bnred_partials(int64_t m, int k, int ncols, int cus, bool pro = false);
+int conv1x1_dgrad_bnred_partials(int64_t m, int k, int ncols, int cus, bool pro = false, bool pro_mask = false);
 // bits null: mask = x * rcoef[c] + rcoef[ncols + c] > 0 (a plain BN + ReLU, recomputed);
 // py / pcoef (optional): the BN-backward operand prologue a' = pcoef0 g + pcoef1 py + pcoef2 of
 // the BN below this conv, with a' written to aout (nullable) for the weight gradient
 void conv1x1_dgrad_bnred(const void* g, const void* w, void* out, int64_t m, int k, int ncols, int dtype,
                          const void* res, const uint8_t* bits, const void* x, const float* mean, float* part, int cus,
                          hipStream_t s, const float* rcoef = nullptr, const void* py = nullptr,
-                         const float* pcoef = nullptr, void* aout = nullptr, int res_h = 0, int res_w = 0);
+                         const float* pcoef = nullptr, void* aout = nullptr, int res_h = 0, int res_w = 0,
+                         bool pro_mask = false);  // pcoef [5][k] with the recomputed ReLU mask (see conv1x1_bn)
 void conv1x1_bnbwd_finalize(const float* part, int g, int c, float inv_n, const float* mean, const float* istd,
                             const float* w, float* gw, float* gb, float* coef, hipStream_t s);
 

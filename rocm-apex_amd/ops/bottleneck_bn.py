@@ -88,6 +88,10 @@ def _conv():
 # +26 / +39 us vs 8 us (tools/bn1_fold_bench.py, profiles/r05/bn1_fold_r05o.jsonl; the halo
 # wgrad's in-LDS rewrite does not hide under its MFMAs yet); whole step 0 / -0.6 %
 _BN1_FOLD = os.environ.get("APEX_AMD_BN1_FOLD", "0") == "1"
+# bn1's dx as conv1's dgrad operand prologue with the ReLU mask recomputed from y1 (see backward)
+# opt-in: same-box A/B 12,414-12,423 vs 12,508-12,532 img/s without it (profiles/r05/ab_bn1_dx_pro_r05z.txt):
+# the two-operand prologue slows conv1's dgrad by more than the [M, width] pass it saves
+_BN1_DX_PRO = os.environ.get("APEX_AMD_BN1_DX_PRO", "0") == "1"
 
 
 @functools.lru_cache(maxsize=None)
@@ -498,9 +502,17 @@ class _BottleneckFn(torch.autograd.Function):
         else:
             dz1, dw2 = _conv_bwd(_nchw(dy2, n, oh, ow), _nchw(z1, n, h, wd), w2, stride, 1)
         dz1 = _m2(dz1.contiguous(memory_format=torch.channels_last))
-        # bn1: reduction + dx pass (as conv1's dgrad operand prologue it moved the same bytes —
-        # the reduction then has to write the masked gradient — and measured slower)
-        dy1, gg1, gb1 = bwd_full(dz1, y1, g1, sm1, si1, c1, True, gr1, in1)
+        # bn1: the reduction pass only, its dx as conv1's dgrad operand prologue with the ReLU mask
+        # recomputed from y1 (kProBnBwdMask: the reduction writes nothing, the prologue writes dy1
+        # for the weight gradient — one [M, width] pass fewer than reduction + dx + dgrad reading
+        # dy1); bwd_full where conv1's dgrad is not native or the BN is synchronized, and at width
+        # 512 (stage 4: the 5 coefficient rows next to the 128 x 512 weight image exceed the LDS)
+        bn1_pro = _BN1_DX_PRO and gr1 is None and width <= 256 and _dgrad_native(dz1.size(0), width, cin)
+        if bn1_pro:
+            pc1, gg1, gb1 = bn.bwd_coef(dz1, y1, g1, sm1, si1, c1)
+            pc1 = pc1.view(-1)
+        else:
+            dy1, gg1, gb1 = bwd_full(dz1, y1, g1, sm1, si1, c1, True, gr1, in1)
         # shortcut gradient, then conv1's data gradient summed onto it
         dwd = ggd = gbd = None
         sub_hw = None  # (h, w): ``short`` is the subsampled downsample gradient (see _DS_SUB)
@@ -522,11 +534,19 @@ class _BottleneckFn(torch.autograd.Function):
             else:
                 dxd, dwd = _conv_bwd(_nchw(dyd, n, oh, ow), x, wds, stride, 0)
                 short = _m2(dxd.contiguous(memory_format=torch.channels_last))
+        rh, rw = sub_hw if sub_hw is not None else (0, 0)
         if link_in is not None and link_in.bits is not None and _red_native(dz1.size(0), width, cin):
             # mask with the block below's ReLU bits + its bn3 backward reduction, in this kernel
-            rh, rw = sub_hw if sub_hw is not None else (0, 0)
-            dx, link_in.part, _ = _conv().dgrad_bnred(dy1, w1.view(width, cin), short, link_in.bits, link_in.y3,
-                                                      link_in.mean, res_h=rh, res_w=rw)
+            if bn1_pro:
+                dx, link_in.part, dy1 = _conv().dgrad_bnred(dz1, w1.view(width, cin), short, link_in.bits, link_in.y3,
+                                                            link_in.mean, py=y1, pcoef=pc1, want_aout=True, res_h=rh,
+                                                            res_w=rw)
+            else:
+                dx, link_in.part, _ = _conv().dgrad_bnred(dy1, w1.view(width, cin), short, link_in.bits, link_in.y3,
+                                                          link_in.mean, res_h=rh, res_w=rw)
+        elif bn1_pro:
+            dx, _, dy1 = _conv().bn1x1(dz1, w1.view(width, cin), True, pc1, None, False, short, y1, True, res_h=rh,
+                                       res_w=rw)
         else:
             dx = conv1x1_dgrad(dy1, w1.view(width, cin), short, short_tmp, sub_hw)
         dw1 = conv1x1_wgrad(dy1, x2, None, w1)

@@ -347,3 +347,46 @@ def test_gpu_tap_weights(k, c, ks, taps, dt):
     wk = w.permute(1, 2, 3, 0)
     ref = torch.stack([wk[:, t // ks, t % ks, :] for t in taps], 1).contiguous()
     assert out.shape == (c, len(taps), k) and torch.equal(out, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,k,nc,linked", [(4096, 64, 256, False), (4096, 64, 256, True), (2048, 128, 512, True),
+                                           (1024, 512, 1024, False), (1024, 512, 1024, True),
+                                           (1000, 256, 1024, True)])
+def test_gpu_bn_dx_prologue_with_recomputed_mask(m, k, nc, linked):
+    """bn1's dx as the conv1 dgrad operand prologue with the ReLU mask recomputed from y1
+    (kProBnBwdMask, pcoef [5k] from bn_nhwc.bwd_coef): the written a' is bitwise the standalone
+    reduction + dx passes' dx, and the dgrad (plain and with the block-below reduction) bitwise the
+    dgrad of that dx."""
+    from apex import _native
+
+    ext = _ext()
+    bn = _native.require("bn_nhwc").bn_nhwc
+    torch.manual_seed(5)
+    dt = torch.bfloat16
+    y1 = torch.randn(m, k, device="cuda").to(dt)
+    dz = torch.randn(m, k, device="cuda").to(dt)
+    wt = (torch.randn(k, nc, device="cuda") * 0.1).to(dt)
+    g1 = torch.rand(k, device="cuda") + 0.5
+    b1 = torch.randn(k, device="cuda") * 0.1
+    rm, rv = torch.zeros(k, device="cuda"), torch.ones(k, device="cuda")
+    sm, si, c1 = bn.stats(y1, g1, b1, rm, rv, 0.1, 1e-5)
+    c1 = c1.view(-1)
+    ref_dx, _, ref_gw, ref_gb = bn.bwd(dz, y1, None, g1, sm, si, c1, True, False)
+    pc5, gw, gb = bn.bwd_coef(dz, y1, g1, sm, si, c1)
+    assert torch.equal(gw, ref_gw) and torch.equal(gb, ref_gb)
+    short = torch.randn(m, nc, device="cuda").to(dt)
+    if not linked:
+        out, _, aout = ext.bn1x1(dz, wt, True, pc5.view(-1), None, False, short, y1, True)
+        ref_out = ext.bn1x1(ref_dx, wt, True, None, None, False, short)[0]
+        assert torch.equal(aout, ref_dx)
+        assert torch.equal(out, ref_out)
+        return
+    x = torch.randn(m, nc, device="cuda").to(dt)
+    mean = torch.randn(nc, device="cuda") * 0.1
+    bits = torch.randint(0, 256, (m * nc // 8,), device="cuda", dtype=torch.uint8)
+    out, part, aout = ext.dgrad_bnred(dz, wt, short, bits, x, mean, py=y1, pcoef=pc5.view(-1), want_aout=True)
+    ref_out, ref_part, _ = ext.dgrad_bnred(ref_dx, wt, short, bits, x, mean)
+    assert torch.equal(aout, ref_dx)
+    assert torch.equal(out, ref_out)
+    torch.testing.assert_close(part.sum(1), ref_part.sum(1), rtol=1e-5, atol=1e-3)

@@ -69,3 +69,21 @@ def test_arguments_derivations():
                          "32", "--vocab-size", "1000", "--bf16", "--micro-batch-size", "4"])
     assert a.ffn_hidden_size == 1024 and a.kv_channels == 32 and a.params_dtype == torch.bfloat16
     assert a.padded_vocab_size == 1024 and a.global_batch_size == 4 and a.encoder_seq_length == 32
+
+
+def test_resnet_channels_last_global_pool_matches_adaptive_avgpool():
+    """The fused-BN ResNet's global pool (models/resnet.py _SpatialMeanNHWC): same value and input
+    gradient as flatten(AdaptiveAvgPool2d(1)), the gradient already in channels_last memory."""
+    from apex.models.resnet import _SpatialMeanNHWC
+
+    torch.manual_seed(0)
+    x = torch.randn(3, 16, 7, 5, dtype=torch.float64).contiguous(memory_format=torch.channels_last).requires_grad_()
+    y = _SpatialMeanNHWC.apply(x)
+    g = torch.randn_like(y)
+    y.backward(g)
+    x2 = x.detach().clone().requires_grad_()
+    y2 = torch.flatten(torch.nn.AdaptiveAvgPool2d(1)(x2), 1)
+    y2.backward(g)
+    torch.testing.assert_close(y, y2)
+    torch.testing.assert_close(x.grad, x2.grad)
+    assert x.grad.is_contiguous(memory_format=torch.channels_last)
