@@ -21,7 +21,7 @@ def main():
         return None
 
     bench.timed = fake_timed
-    sys.argv = ["bench.py"]
+    sys.argv = ["bench.py"] + sys.argv[1:]
     bench.main()
     step = captured["step"]
     for _ in range(4):
@@ -37,11 +37,20 @@ def main():
         if ev.name not in ("aten::copy_", "aten::contiguous", "aten::to", "aten::_to_copy", "aten::clone"):
             continue
         dt = getattr(ev, "device_time_total", None) or getattr(ev, "cuda_time_total", 0)
-        if dt < 5:
+        if dt < 3:
             continue
         frames = [f for f in (ev.stack or []) if "rocm-apex_amd" in f or "bench.py" in f][:4]
         rows.append((dt, ev.name, ev.input_shapes, frames))
     rows.sort(key=lambda r: -r[0])
+    agg = {}
+    for dt, name, shapes, frames in rows:
+        key = (name, str(shapes))
+        n, t, fr = agg.get(key, (0, 0.0, frames))
+        agg[key] = (n + 1, t + dt, fr or frames)
+    for (name, shapes), (n, t, fr) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:15]:
+        print(f"[agg] {n:4d} x {name} {shapes}: {t:9.1f} us", flush=True)
+        for f in fr:
+            print(f"             {f}", flush=True)
     for dt, name, shapes, frames in rows[:25]:
         print(f"{dt:9.1f} us {name} {shapes}", flush=True)
         for f in frames:
