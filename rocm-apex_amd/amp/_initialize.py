@@ -141,11 +141,22 @@ class O2StateDictHook(object):
 
 def _wrap_forward(model, in_caster, out_caster):
     fwd = model.forward
+    # a model that declares ``_amp_casts_input = True`` takes its first positional tensor uncast
+    # and casts it itself (to ``model._amp_input_dtype``) where it is first consumed: the fused
+    # ResNet stem reads the fp32 batch and rounds it to the model dtype in its padding pass (the
+    # same round-to-nearest-even as ``.to()``), saving the standalone cast pass
+    own_cast = in_caster is not None and getattr(model, "_amp_casts_input", False)
+    if own_cast:
+        model._amp_input_dtype = in_caster.dtype
 
     @functools.wraps(fwd)
     def forward(*args, **kwargs):
         if in_caster is not None:
-            args, kwargs = in_caster(args), in_caster(kwargs)
+            if own_cast and args and isinstance(args[0], torch.Tensor) and args[0].is_cuda:
+                args = (args[0],) + tuple(in_caster(args[1:]))
+            else:
+                args = in_caster(args)
+            kwargs = in_caster(kwargs)
         return out_caster(fwd(*args, **kwargs))
 
     model.forward = forward

@@ -12,12 +12,27 @@
 #include "norm_common.h"
 #include "apex_amd/launch_plan.h"
 
+#include <cstdlib>
+
 namespace apex_amd {
 namespace norm {
 
 // Persistent grid: enough resident blocks to saturate HBM, few enough that the partial slab
 // stays small relative to the activations.
-inline int bwd_grid(int64_t ngroups, int cus) { return plan::ln_bwd_grid(ngroups, cus); }
+// APEX_AMD_LN_BWD_BPC = 3 | 4: that many resident blocks per CU instead of the plan's 2 (A/B knob;
+// the workspace holds max(2 * cus, 1024) partial rows, so the grid stays within it)
+inline int bwd_grid(int64_t ngroups, int cus) {
+  static const int bpc = [] {
+    const char* e = std::getenv("APEX_AMD_LN_BWD_BPC");
+    const int v = e ? std::atoi(e) : 2;
+    return v >= 2 && v <= 4 ? v : 2;
+  }();
+  if (bpc == 2) return plan::ln_bwd_grid(ngroups, cus);
+  int64_t cap = (int64_t)cus * bpc;
+  const int64_t ws_rows = (int64_t)cus * 2 > 1024 ? (int64_t)cus * 2 : 1024;
+  if (cap > ws_rows) cap = ws_rows;
+  return (int)(ngroups < cap ? (ngroups > 0 ? ngroups : 1) : cap);
+}
 
 template <typename TI, typename TW, typename TO, int W, int VPT>
 __global__ void __launch_bounds__(block_threads<W>())

@@ -20,6 +20,8 @@ In the fused model every block but the last hands its output on as a ``(main, sh
 aliases (``BatchNorm2d_NHWC(..., fork=True)``): the next block's conv1 reads one and its shortcut
 the other, so the two gradients of the block output reach the producing batch norm separately
 and are summed inside its backward reduction instead of by an autograd add over the activation."""
+import os
+
 import torch
 import torch.nn as nn
 
@@ -269,12 +271,23 @@ class ResNet(nn.Module):
                                 bn_group=self.bn_group))
         return nn.Sequential(*layers)
 
+    @property
+    def _amp_casts_input(self):
+        # amp O2 hands the fused-BN model its fp32 batch: the native stem casts it in its padding
+        # pass (forward below), every other path casts it first
+        return self.fused_bn and os.environ.get("APEX_AMD_STEM_INPUT_CAST", "1") != "0"
+
     def forward(self, x):
+        amp_dt = getattr(self, "_amp_input_dtype", None)
         if self.fused_bn:
             # stem: BN statistics, then normalize + ReLU + 3x3/2 max pool in one pass
             from ..contrib.groupbn import bn_relu_maxpool
             from ..ops import stem
 
+            self.conv1._amp_input_fp32_ok = amp_dt is not None and amp_dt == self.conv1.weight.dtype
+            if not (stem.stem_supported(self.conv1, self.bn1, self.maxpool, x) and not _has_hooks(())):
+                if amp_dt is not None and torch.is_tensor(x) and x.is_floating_point() and x.dtype != amp_dt:
+                    x = x.to(amp_dt)
             if stem.stem_supported(self.conv1, self.bn1, self.maxpool, x) and not _has_hooks(()):
                 # conv + BN statistics, BN + ReLU + pool, and the fused backward (ops/stem.py)
                 x = stem.stem_forward(self.conv1, self.bn1, self.maxpool, x)

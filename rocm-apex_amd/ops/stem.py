@@ -73,7 +73,9 @@ def stem_supported(conv, bn, pool, x):
             and _pair(pool.padding) == (1, 1) and _pair(getattr(pool, "dilation", 1)) == (1, 1)
             and not getattr(pool, "ceil_mode", False) and not getattr(pool, "return_indices", False)):
         return False
-    if x.dtype != w.dtype:  # the module path would raise on the mismatch; do not cast silently
+    # the module path would raise on a mismatch; an fp32 batch is taken only when amp O2 left its
+    # cast to the model (models/resnet.py): the padding pass rounds it to w's dtype
+    if x.dtype != w.dtype and not (x.dtype == torch.float32 and getattr(conv, "_amp_input_fp32_ok", False)):
         return False
     return not any(getattr(mod, attr, None) for mod in (conv, bn, pool)
                    for attr in ("_forward_hooks", "_forward_pre_hooks", "_backward_hooks", "_backward_pre_hooks"))

@@ -142,3 +142,36 @@ def test_stem_unsupported_on_cpu():
     model = resnet50(fused_bn=True)
     x = torch.randn(1, 3, 32, 32)
     assert not stem.stem_supported(model.conv1, model.bn1, model.maxpool, x)
+
+
+@pytest.mark.gpu
+def test_gpu_o2_fp32_batch_cast_in_the_stem_pad_is_bitwise_the_amp_cast():
+    """amp O2 leaves the fused-BN ResNet's input cast to its stem (models/resnet.py
+    _amp_casts_input): the padding pass rounds the fp32 batch to bf16 exactly as ``.to()`` does,
+    so the forward (the loss) equals that of a batch cast before the call bitwise; the gradients
+    agree to run-to-run noise (the library stride-2 data gradient is not bitwise reproducible)."""
+    import copy
+
+    from apex import amp
+    from apex.models.resnet import resnet50
+    from apex.optimizers import FusedAdam
+
+    torch.manual_seed(3)
+    base = resnet50(fused_bn=True).cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(8, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
+    t = torch.randint(0, 1000, (8,), device="cuda")
+    results = []
+    for pre_cast in (False, True):
+        model = copy.deepcopy(base)
+        opt = FusedAdam(model.parameters(), lr=1e-3)
+        model, opt = amp.initialize(model, opt, opt_level="O2", cast_model_type=torch.bfloat16,
+                                    keep_batchnorm_fp32=True, verbosity=0)
+        inp = x.to(torch.bfloat16) if pre_cast else x
+        loss = torch.nn.functional.cross_entropy(model(inp), t)
+        loss.backward()
+        results.append((loss.detach(), [p.grad.clone() for p in model.parameters() if p.grad is not None]))
+    (l0, g0), (l1, g1) = results
+    assert torch.equal(l0, l1)
+    assert len(g0) == len(g1)
+    for a, b in zip(g0, g1):
+        assert _rel(a, b) < 5e-2
