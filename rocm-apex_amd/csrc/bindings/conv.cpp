@@ -4,6 +4,7 @@
 // torch channels_last tensors); weights are [K, taps, C] (k contiguous per tap).
 #include "common.h"
 #include "apex_amd/conv_api.h"
+#include "apex_amd/layout_extra.h"
 #include "apex_amd/conv_halo.h"
 
 namespace apex_amd {
@@ -245,6 +246,18 @@ at::Tensor subsample2x(const at::Tensor& x, int64_t n, int64_t h, int64_t w) {
   auto y = at::empty({n * ((h + 1) / 2) * ((w + 1) / 2), x.size(1)}, x.options());
   conv_subsample2x(x.data_ptr(), y.data_ptr(), (int)n, (int)h, (int)w, (int)x.size(1), dtype_code(x.scalar_type()),
                    device_cus(x.get_device()), cur_stream());
+  return y;
+}
+
+// g [N, C] -> [N, C, h, w] channels_last with every pixel g * scale (global average pool backward)
+at::Tensor spatial_broadcast_b(const at::Tensor& g, int64_t h, int64_t w, double scale) {
+  TORCH_CHECK(g.is_cuda() && g.dim() == 2 && g.is_contiguous() &&
+                  (g.scalar_type() == at::kBFloat16 || g.scalar_type() == at::kHalf) && g.size(1) % 8 == 0,
+              "spatial_broadcast: g must be a contiguous 16-bit [N, C] GPU tensor, C % 8 == 0");
+  const c10::hip::HIPGuard guard(g.get_device());
+  auto y = at::empty({g.size(0), g.size(1), h, w}, g.options().memory_format(at::MemoryFormat::ChannelsLast));
+  spatial_broadcast(g.data_ptr(), y.data_ptr(), (int)g.size(0), (int)(h * w), (int)g.size(1), (float)scale,
+                    dtype_code(g.scalar_type()), device_cus(g.get_device()), cur_stream());
   return y;
 }
 
@@ -664,6 +677,8 @@ void bind_conv(pybind11::module_& root) {
   m.def("hfp_set_mode", &conv_hfp_set_mode, pybind11::arg("mode"));
   m.def("subsample2x", &subsample2x, pybind11::arg("x"), pybind11::arg("n"), pybind11::arg("h"), pybind11::arg("w"));
   m.def("tap_weights", &tap_weights, pybind11::arg("w"), pybind11::arg("taps"));
+  m.def("spatial_broadcast", &spatial_broadcast_b, pybind11::arg("g"), pybind11::arg("h"), pybind11::arg("w"),
+        pybind11::arg("scale"));
   m.def("bn1x1_addrelu", &bn1x1_addrelu, pybind11::arg("a"), pybind11::arg("res"), pybind11::arg("pcoef"),
         pybind11::arg("w"), pybind11::arg("shift") = pybind11::none(), pybind11::arg("out") = pybind11::none(),
         pybind11::arg("split") = false, pybind11::arg("res_coef") = pybind11::none());

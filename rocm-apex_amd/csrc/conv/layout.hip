@@ -7,6 +7,8 @@
 // reads and writes whole 128-byte runs (torch's generic strided copy took 36 us per ResNet call).
 // conv_tap_weights: the data-gradient weight image (below).
 #include "apex_amd/conv_api.h"
+#include "apex_amd/device.h"
+#include "apex_amd/layout_extra.h"
 #include "apex_amd/dispatch.h"
 #include "apex_amd/fastdiv.h"
 
@@ -70,7 +72,39 @@ __global__ void __launch_bounds__(256) tap_weights_kernel(const uint16_t* __rest
   }
 }
 
+// spatial_broadcast: y[n][p][c] = g[n][c] * scale for p < hw — the input gradient of a global
+// average pool written straight into channels_last memory (16-byte stores, grid-stride)
+template <typename T>
+__global__ void __launch_bounds__(256) spatial_broadcast_kernel(const T* __restrict__ g, T* __restrict__ y,
+                                                                uint32_t total, FastDiv cv, FastDiv hwd, float scale) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const uint32_t pix = fdiv(i, cv), v = i - pix * cv.d;
+    const uint32_t nn = fdiv(pix, hwd);
+    float a[8];
+    Vec8<T>::load(a, g + ((size_t)nn * cv.d + v) * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] *= scale;
+    Vec8<T>::store(y + (size_t)i * 8, a);
+  }
+}
+
 }  // namespace layout
+
+void spatial_broadcast(const void* g, void* y, int n, int hw, int c, float scale, int dtype, int cus, hipStream_t s) {
+  if ((dtype != kBF16 && dtype != kF16) || c % 8 || n <= 0 || hw <= 0)
+    throw std::runtime_error("spatial_broadcast: 16-bit, C % 8 == 0");
+  if (((uintptr_t)g & 15) || ((uintptr_t)y & 15)) throw std::runtime_error("spatial_broadcast: 16-byte alignment");
+  const int64_t total = (int64_t)n * hw * (c / 8);
+  if (total >= (1ll << 32)) throw std::runtime_error("spatial_broadcast: output past 2^32 vectors");
+  int64_t grid = (total + 255) / 256;
+  if (grid > (int64_t)cus * 8) grid = (int64_t)cus * 8;
+  dispatch_16(dtype, [&](auto tag) {
+    using T = typename decltype(tag)::type;
+    hipLaunchKernelGGL((layout::spatial_broadcast_kernel<T>), dim3((unsigned)grid), dim3(256), 0, s, (const T*)g, (T*)y,
+                       (uint32_t)total, make_fastdiv((uint32_t)(c / 8)), make_fastdiv((uint32_t)hw), scale);
+  }, "spatial_broadcast");
+  check_launch("spatial_broadcast");
+}
 
 void conv_tap_weights(const void* w, void* dst, int k, int c, int rs, const int* taps, int ntaps, hipStream_t s) {
   if (k % 8 || c % 8 || k <= 0 || c <= 0 || ntaps < 1 || ntaps > 9 || rs < 1 || rs > 9)

@@ -2,6 +2,7 @@
 tests/L0/run_transformer/run_gpt_minimal_test.py and run_bert_minimal_test.py: build the model
 with the TP/PP helpers, run forward/backward steps).  CPU tier: gloo world 2 — the TP=2 loss
 must equal the TP=1 loss of the same (CPU-initialised) weights."""
+import pytest
 import torch
 
 from tests._dist_utils import run_multiprocess
@@ -87,3 +88,16 @@ def test_resnet_channels_last_global_pool_matches_adaptive_avgpool():
     torch.testing.assert_close(y, y2)
     torch.testing.assert_close(x.grad, x2.grad)
     assert x.grad.is_contiguous(memory_format=torch.channels_last)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,c,h,w", [(4, 2048, 7, 7), (3, 64, 5, 9)])
+def test_gpu_global_pool_gradient_broadcast_is_bitwise_the_expand(n, c, h, w):
+    """layout.hip spatial_broadcast (the pool's backward on the GPU) == the torch expand path."""
+    from apex import _native
+
+    ext = _native.require("conv").conv
+    g = torch.randn(n, c, device="cuda").to(torch.bfloat16)
+    got = ext.spatial_broadcast(g, h, w, 1.0 / (h * w))
+    want = (g * (1.0 / (h * w))).view(n, 1, 1, c).expand(n, h, w, c).contiguous().permute(0, 3, 1, 2)
+    assert got.is_contiguous(memory_format=torch.channels_last) and torch.equal(got, want)
