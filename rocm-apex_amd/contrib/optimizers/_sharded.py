@@ -150,12 +150,33 @@ class FlatShardedBuffers:
 
     # ---- compressed all-gather payload ----
     def payload(self, dtype):
-        """fp8 gather buffer laid out like ``flat_param`` (allocated on first use)."""
+        """fp8 gather buffer laid out like ``flat_param`` (allocated on first use, with this rank's
+        shards already holding its current master weights: see ``refresh_payload``)."""
         buf = getattr(self, "_payload", None)
         if buf is None or buf.dtype != dtype:
             buf = torch.zeros(self.total, dtype=dtype, device=self.device)
             self._payload = buf
+            self._fill_payload(buf)
         return buf
+
+    def refresh_payload(self, dtype):
+        """Write this rank's master shards into its slice of the fp8 gather payload.  The step's
+        epilogue normally writes that slice, but a skipped (overflow) step leaves it untouched and
+        the all-gather still runs (the skip flag stays on the device), so the slice must always
+        hold the current weights: at allocation (not zeros) and after a checkpoint load (not the
+        pre-load weights)."""
+        if dtype is None or self.world == 1:
+            return
+        buf = getattr(self, "_payload", None)
+        if buf is None or buf.dtype != dtype:
+            self.payload(dtype)  # allocates and fills
+        else:
+            self._fill_payload(buf)
+
+    def _fill_payload(self, buf):
+        for b in range(self.num_blocks):
+            s = b * self.block + self.rank * self.shard
+            buf[s:s + self.shard].copy_(self.master[b].to(buf.dtype))
 
     def out_shards(self, gather_dtype=None):
         """Where the optimizer epilogue writes this rank's updated weights: the model-dtype

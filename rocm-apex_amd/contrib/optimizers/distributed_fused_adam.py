@@ -229,6 +229,9 @@ class DistributedFusedAdam(torch.optim.Optimizer):
             for b in range(self._flat.num_blocks):
                 self._flat.param_shard(b).copy_(self._flat.master[b].to(self._flat.dtype))
             self._flat.all_gather_params()
+            # a skipped first step after the load gathers the fp8 payload: it must hold the loaded
+            # weights, not the ones this optimizer held before
+            self._flat.refresh_payload(self._ag_dtype)
 
 
 def _record_found_inf(grad_scaler, optimizer, skip):

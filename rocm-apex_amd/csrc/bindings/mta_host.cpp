@@ -99,12 +99,15 @@ MtaMeta mta_meta(const std::vector<std::vector<at::Tensor>>& lists, int chunk_si
 
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_cache.find(h);
-  if (it != g_cache.end() && it->second.key == key) {
-    g_lru.splice(g_lru.begin(), g_lru, it->second.lru_it);
-    return it->second.meta;
-  }
   hipStreamCaptureStatus cap0 = hipStreamCaptureStatusNone;
   hipStreamIsCapturing(cur_stream(), &cap0);
+  if (it != g_cache.end() && it->second.key == key) {
+    g_lru.splice(g_lru.begin(), g_lru, it->second.lru_it);
+    // a table first built eagerly (e.g. by warm-up steps on the capture stream) and now recorded
+    // into a graph: the graph replays it, so it must never be address-patched or evicted again
+    if (cap0 != hipStreamCaptureStatusNone) it->second.pinned_forever = true;
+    return it->second.meta;
+  }
   if (cap0 == hipStreamCaptureStatusNone && (it == g_cache.end() || !it->second.pinned_forever)) {
     // the structurally identical table with the most matching addresses (recently used first)
     auto best = g_cache.end();

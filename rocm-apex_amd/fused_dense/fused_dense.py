@@ -123,21 +123,29 @@ def sync_lt_plans(group=None, src=0):
     return sum(1 for key in obj[0] if lt.set_plan_choice(list(key), dev))
 
 
-def maybe_sync_lt_plans(group):
-    """sync_lt_plans(group) whenever this process planned new hipBLASLt problems since the last
-    sync for ``group`` (every rank of a tensor-parallel group plans the same problems at the same
-    calls, so all of them enter the collective together)."""
+def maybe_sync_lt_plans(group, problem):
+    """sync_lt_plans(group) the first time this process runs ``problem`` (a hashable key of the
+    GEMM: op, shape, dtype) for ``group``; returns True when it synced, so the caller re-runs the
+    GEMM on the agreed pick.
+
+    The decision depends only on the tensor-parallel call sequence, which every rank of the group
+    runs identically (same problems, same order), so all ranks enter the collective together.  A
+    process-wide counter of planned problems would not do: library GEMMs outside the TP layers
+    (the ResNet 1x1s, non-TP fused_dense) plan problems on some ranks only and would leave the
+    other ranks outside the broadcast."""
     import torch.distributed as dist
 
     lt = _native.submodule("lt_gemm")
-    if lt is None or not hasattr(lt, "plan_count") or not (dist.is_available() and dist.is_initialized()):
-        return
+    if lt is None or not hasattr(lt, "plan_choices") or not (dist.is_available() and dist.is_initialized()):
+        return False
     if dist.get_world_size(group) <= 1:
-        return
-    n = lt.plan_count()
-    if _LT_SYNCED.get(id(group)) != n:
-        sync_lt_plans(group)
-        _LT_SYNCED[id(group)] = n
+        return False
+    seen = _LT_SYNCED.setdefault(id(group), set())
+    if problem in seen:
+        return False
+    seen.add(problem)
+    sync_lt_plans(group)
+    return True
 
 
 def route_table():

@@ -62,11 +62,15 @@ def snapshot(device):
         return None
     if not _SHARE:
         return t.clone()
-    snap = _SNAPS.get(t.device.index)
-    if snap is None:
-        snap = t.clone()
-        _SNAPS[t.device.index] = snap
-    return snap
+    # a snapshot is only shared within one capture state: one taken eagerly (e.g. warm-up with no
+    # trailing advance()) must not be reused inside a graph capture, whose replays would then all
+    # read that frozen copy instead of a clone made by the graph itself — and vice versa
+    capturing = torch.cuda.is_current_stream_capturing()
+    hit = _SNAPS.get(t.device.index)
+    if hit is None or hit[0] != capturing:
+        hit = (capturing, t.clone())
+        _SNAPS[t.device.index] = hit
+    return hit[1]
 
 
 def advance(device=None):

@@ -88,16 +88,16 @@ def _initialize_affine_weight_cpu(weight, output_size, input_size, per_partition
     return None
 
 
-def _sync_lt_picks():
-    """Rank 0's hipBLASLt picks for the tensor-parallel group (fused_dense.maybe_sync_lt_plans),
-    when a group exists."""
+def _sync_lt_picks(problem):
+    """Rank 0's hipBLASLt picks for the tensor-parallel group (fused_dense.maybe_sync_lt_plans) the
+    first time this TP problem runs; True when the caller must re-run the GEMM on the agreed pick."""
     from .. import parallel_state as ps
 
     if ps._TENSOR_MODEL_PARALLEL_GROUP is None:
-        return
+        return False
     from ...fused_dense.fused_dense import maybe_sync_lt_plans
 
-    maybe_sync_lt_plans(ps._TENSOR_MODEL_PARALLEL_GROUP)
+    return maybe_sync_lt_plans(ps._TENSOR_MODEL_PARALLEL_GROUP, problem)
 
 
 def _linear(x, weight, bias):
@@ -114,7 +114,11 @@ def _linear(x, weight, bias):
         if route == "native" or (not route and fd.route_mode() == "native"):
             return fd.linear_bias_forward(x, weight, bias)
         y = fd._lib_dense_fwd(x, weight, bias)
-        _sync_lt_picks()  # one algorithm per GEMM across the tensor-parallel group
+        # one algorithm per GEMM across the tensor-parallel group: the first call of a problem
+        # syncs rank 0's pick and recomputes, so even that call's output is rank-consistent
+        if _sync_lt_picks(("fwd", x.numel() // x.shape[-1], weight.shape[0], weight.shape[1], str(x.dtype),
+                           bias is not None)):
+            y = fd._lib_dense_fwd(x, weight, bias)
         return y
     if bias is not None and x.dim() >= 2:
         return torch.addmm(bias, x.reshape(-1, x.shape[-1]), weight.t()).view(x.shape[:-1] + (weight.shape[0],))
@@ -134,7 +138,8 @@ def _wgrad(go2, ti2):
         from ...fused_dense.fused_dense import wgrad_gemm
 
         dw = wgrad_gemm(go2, ti2)
-        _sync_lt_picks()
+        if _sync_lt_picks(("wgrad", go2.shape[0], go2.shape[1], ti2.shape[1], str(go2.dtype))):
+            dw = wgrad_gemm(go2, ti2)
         return dw
     return go2.t().matmul(ti2)
 

@@ -5,6 +5,7 @@ rank vs torch.optim.AdamW on the full model with all-reduced gradients, params c
 several steps) and test_distributed_fused_lamb.py (LAMB vs reference LAMB math).  CPU tiers run
 world_size 2 over gloo (fp32 params, so the comparison is tight)."""
 import copy
+import sys
 
 import pytest
 import torch
@@ -389,3 +390,114 @@ def test_gpu_distributed_lamb_step_makes_no_host_sync():
     [2, num_params] norm all-reduce, stage 2, all-gather) runs under torch's sync debug mode set
     to raise on any device -> host synchronization."""
     run_multiprocess(_lamb_sync_free_worker, world=1, backend="nccl")
+
+
+def _fp8_overflow_worker(rank, world, kind):
+    """fp8 all-gather + an overflow on the very first step: the skipped step still gathers the
+    payload (the skip flag stays on the device), which must hold the current master weights —
+    not the zeros it was allocated with — and, after a checkpoint load, the loaded weights."""
+    from apex.contrib.optimizers import DistributedFusedAdam, DistributedFusedLAMB
+
+    cls = DistributedFusedAdam if kind == "adam" else DistributedFusedLAMB
+    kw = dict(lr=1e-2, weight_decay=0.01, dwu_num_blocks=2, min_block_elems=256, e5m2_allgather=True)
+    dt = torch.float8_e5m2
+    model = _model(6)
+    before = [p.detach().clone() for p in model.parameters()]
+    opt = cls(model.parameters(), **kw)
+    x, y = _batches(rank, 1)[0]
+    xb = x.clone()
+    if rank == 1:
+        xb[0, 0] = float("inf")
+    torch.nn.functional.mse_loss(model(xb), y).backward()
+    opt.step()
+    assert opt.has_overflow
+    for p, b in zip(model.parameters(), before):
+        # the weights went through the fp8 gather unchanged (rounded), not zeroed
+        assert torch.equal(p.detach(), b.to(dt).to(b.dtype))
+        assert float(p.detach().abs().sum()) > 0
+    torch.nn.functional.mse_loss(model(x), y).backward()
+    opt.step()
+    assert not opt.has_overflow
+    sd = opt.state_dict()
+    trained = [p.detach().clone() for p in model.parameters()]
+    # a fresh optimizer over different weights: load, then overflow on its first step
+    model2 = _model(7)
+    opt2 = cls(model2.parameters(), **kw)
+    opt2.load_state_dict(sd)
+    torch.nn.functional.mse_loss(model2(xb), y).backward()
+    opt2.step()
+    assert opt2.has_overflow
+    master = _gathered_master(opt2)
+    for p, q, off in zip(model2.parameters(), trained, opt2._flat.offsets):
+        n = p.numel()
+        assert torch.equal(p.detach().reshape(-1), master[off:off + n].to(dt).to(p.dtype))
+        torch.testing.assert_close(p.detach(), q, rtol=0.13, atol=0.03)
+
+
+@pytest.mark.parametrize("kind", ["adam", "lamb"])
+def test_distributed_fp8_allgather_overflow_on_first_step(kind):
+    run_multiprocess(_fp8_overflow_worker, world=2, args=(kind,))
+
+
+class _NoHostRead:
+    """Raise on any host read of a tensor's value (``item`` / ``bool`` / ``float`` / ``int`` /
+    ``tolist`` / ``numpy``) inside the block: the CPU stand-in for torch's CUDA sync debug mode,
+    which only sees device syncs."""
+
+    _NAMES = ("item", "__bool__", "__float__", "__int__", "__index__", "tolist", "numpy")
+
+    def __enter__(self):
+        self._saved = {n: getattr(torch.Tensor, n) for n in self._NAMES}
+
+        saved = self._saved
+
+        def boom(name):
+            def f(*a, **k):
+                # the CPU stand-ins of the device kernels (ops/multi_tensor_ref.py) compute on the
+                # host by construction; only the optimizer's own Python path is checked
+                fr = sys._getframe(1)
+                while fr is not None:
+                    if fr.f_code.co_filename.endswith("multi_tensor_ref.py"):
+                        return saved[name](*a, **k)
+                    fr = fr.f_back
+                raise AssertionError(f"host read of a tensor value ({name}) inside the step")
+            return f
+
+        for n in self._NAMES:
+            setattr(torch.Tensor, n, boom(n))
+        return self
+
+    def __exit__(self, *exc):
+        for n, f in self._saved.items():
+            setattr(torch.Tensor, n, f)
+        return False
+
+
+def _sync_free_cpu_worker(rank, world, kind, ag):
+    from apex.contrib.optimizers import DistributedFusedAdam, DistributedFusedLAMB
+
+    cls = DistributedFusedAdam if kind == "adam" else DistributedFusedLAMB
+    model = _model(4)
+    opt = cls(model.parameters(), lr=1e-2, weight_decay=0.01, max_grad_norm=1.0, min_block_elems=128,
+              dwu_num_blocks=2, e5m2_allgather=ag)
+    batches = _batches(rank, 4)
+    for i, (x, y) in enumerate(batches):
+        xb = x.clone()
+        if i == 2 and rank == 0:
+            xb[0, 0] = float("nan")  # one overflow step, gated on the device flag
+        torch.nn.functional.mse_loss(model(xb), y).backward()
+        if i == 0:
+            opt.step()  # first step builds the buffers
+            continue
+        with _NoHostRead():
+            opt.step()
+    assert float(opt._step_t) == 3.0
+
+
+@pytest.mark.parametrize("kind", ["adam", "lamb"])
+@pytest.mark.parametrize("ag", [False, True])
+def test_distributed_step_reads_no_host_value_world2(kind, ag):
+    """world 2 (gloo): the whole sharded step — overflow flag all-reduce, grad-norm clip, the LAMB
+    [2, num_params] norm all-reduce, stages 1/2, the (fp8) all-gather — never reads a tensor value
+    on the host, overflow step included (the GPU tier checks the same under sync debug mode)."""
+    run_multiprocess(_sync_free_cpu_worker, world=2, args=(kind, ag))

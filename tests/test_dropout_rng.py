@@ -130,3 +130,36 @@ def test_gpu_advance_between_forward_and_backward(device_rng):
     for a, b in zip(got, ref):
         # (dQ is summed with float atomics: equal up to summation order, far below a mask change)
         torch.testing.assert_close(a.float(), b.float(), atol=2e-3, rtol=1e-2)
+
+
+@pytest.mark.gpu
+def test_gpu_eager_snapshot_not_reused_in_capture(device_rng):
+    """a snapshot taken eagerly (warm-up that ends without advance()) must not be
+    shared into a graph capture whose body advances only AFTER its dropout calls: every replay
+    must still draw a fresh mask."""
+    from apex.transformer.functional.fused_bias_dropout_add import fused_bias_dropout_add
+
+    torch.manual_seed(5)
+    x = torch.randn(128, 512, device="cuda", dtype=torch.bfloat16)
+    r = torch.zeros_like(x)
+
+    def step():
+        y = fused_bias_dropout_add(x, None, r, 0.25, True, 3, 9)
+        dropout_rng.advance()
+        return y
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step()
+        fused_bias_dropout_add(x, None, r, 0.25, True, 3, 9)  # eager snapshot left behind
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        y_s = step()
+    masks = []
+    for _ in range(3):
+        graph.replay()
+        torch.cuda.synchronize()
+        masks.append((y_s != 0).clone())
+    assert not torch.equal(masks[0], masks[1]) and not torch.equal(masks[1], masks[2])

@@ -52,3 +52,48 @@ def test_sync_lt_plans_noop_without_group():
     from apex.fused_dense import sync_lt_plans
 
     assert sync_lt_plans(None) == 0
+
+
+class _FakeLt:
+    """Stand-in for the hipBLASLt wrapper's plan table (CPU tier)."""
+
+    def __init__(self, rank):
+        self.rank, self.picks = rank, {}
+
+    def plan_choices(self):
+        return [k + (v,) for k, v in sorted(self.picks.items())]
+
+    def set_plan_choice(self, key, dev):
+        self.picks[tuple(key[:-1])] = key[-1]
+        return True
+
+
+def _decision_worker(rank, world):
+    """The sync decision follows the TP problem sequence (identical on every rank), not the
+    process-wide plan table: rank 1 planning extra library GEMMs of its own (a non-TP layer) must
+    neither make it enter a broadcast alone nor skip one the other rank enters."""
+    import torch.distributed as dist
+
+    from apex import _native
+    from apex.fused_dense import fused_dense as fd
+
+    fake = _FakeLt(rank)
+    orig = _native.submodule
+    _native.submodule = lambda name: fake if name == "lt_gemm" else orig(name)
+    try:
+        fake.picks[("fwd", 64, 32, 16)] = rank  # rank-local timed picks differ
+        if rank == 1:
+            fake.picks[("other", 1, 2, 3)] = 7  # a non-TP problem planned on rank 1 only
+        assert fd.maybe_sync_lt_plans(None, ("fwd", 64, 32, 16))
+        assert fake.picks[("fwd", 64, 32, 16)] == 0  # rank 0's pick everywhere
+        if rank == 1:
+            fake.picks[("other2", 4, 5, 6)] = 3
+        assert not fd.maybe_sync_lt_plans(None, ("fwd", 64, 32, 16))  # same problem: no collective
+        assert fd.maybe_sync_lt_plans(None, ("wgrad", 64, 32, 16))
+        dist.barrier()
+    finally:
+        _native.submodule = orig
+
+
+def test_lt_sync_decision_is_rank_consistent():
+    run_multiprocess(_decision_worker, world=2)

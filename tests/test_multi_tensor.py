@@ -250,3 +250,38 @@ def test_new_addresses_patch_the_cached_table_gpu():
     for x, y in zip(keep[0], ys):
         torch.testing.assert_close(y, x * 3.0)
     assert noop.item() == 0
+
+
+@pytest.mark.gpu
+def test_table_hit_during_capture_is_pinned_gpu():
+    """A table first built EAGERLY on the capture stream (warm-up) and then hit while a graph is
+    captured must be pinned: a later eager call with the same structure but new tensors may not
+    patch its address rows, or the next replay would read the new tensors (mta_host.cpp)."""
+    amp_C.mta_cache_clear()
+    s = torch.cuda.Stream()
+    noop = _noop("cuda")
+    xs = _lists("cuda", torch.float32, SIZES)
+    ys = [torch.empty_like(x) for x in xs]
+    with torch.cuda.stream(s):
+        amp_C.multi_tensor_scale(CHUNK, noop, [xs, ys], 2.0)  # eager warm-up builds the table
+    s.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        amp_C.multi_tensor_scale(CHUNK, noop, [xs, ys], 2.0)  # cache hit while capturing
+    # eager call on the same stream, same structure, new tensors
+    xs2 = _lists("cuda", torch.float32, SIZES)
+    ys2 = [torch.empty_like(x) for x in xs2]
+    with torch.cuda.stream(s):
+        amp_C.multi_tensor_scale(CHUNK, noop, [xs2, ys2], 2.0)
+    s.synchronize()
+    for x, y in zip(xs2, ys2):
+        torch.testing.assert_close(y, x * 2.0)
+    for x in xs:
+        x.mul_(-1.0)
+    for y in ys:
+        y.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    for x, y in zip(xs, ys):
+        torch.testing.assert_close(y, x * 2.0)
+    assert noop.item() == 0
