@@ -394,7 +394,8 @@ std::vector<at::Tensor> dgrad_bnred(const at::Tensor& g, const at::Tensor& w, co
                                     const c10::optional<at::Tensor>& bits, const at::Tensor& x, const at::Tensor& mean,
                                     const c10::optional<at::Tensor>& coef, const c10::optional<at::Tensor>& py,
                                     const c10::optional<at::Tensor>& pcoef, bool want_aout, int64_t res_h,
-                                    int64_t res_w) {
+                                    int64_t res_w, const c10::optional<at::Tensor>& x2,
+                                    const c10::optional<at::Tensor>& mean2) {
   TORCH_CHECK(g.is_cuda() && g.dim() == 2 && g.is_contiguous() && w.dim() == 2 && w.is_contiguous() &&
                   w.scalar_type() == g.scalar_type() && w.size(0) == g.size(1),
               "dgrad_bnred: g [M, k] and w [k, ncols] expected");
@@ -425,11 +426,17 @@ std::vector<at::Tensor> dgrad_bnred(const at::Tensor& g, const at::Tensor& w, co
                 "dgrad_bnred: py must match g, pcoef fp32 [3k] or [5k]");
   TORCH_CHECK(!want_aout || pro, "dgrad_bnred: want_aout needs the prologue");
   TORCH_CHECK(conv1x1_bn_supported(m, k, ncols), "dgrad_bnred: unsupported shape");
+  TORCH_CHECK(x2.has_value() == mean2.has_value(), "dgrad_bnred: x2 and mean2 go together");
+  if (x2.has_value())
+    TORCH_CHECK(x2->is_contiguous() && x2->scalar_type() == g.scalar_type() && x2->numel() == m * ncols &&
+                    mean2->is_contiguous() && mean2->scalar_type() == at::kFloat && mean2->numel() == ncols,
+                "dgrad_bnred: x2 must be the contiguous [M, ncols] input of the second BN, mean2 fp32 [ncols]");
   const c10::hip::HIPGuard guard(g.get_device());
   const int cus = device_cus(g.get_device());
   auto out = at::empty({m, ncols}, g.options());
-  auto part =
-      at::empty({2, conv1x1_dgrad_bnred_partials(m, k, ncols, cus, pro, pmask), ncols}, g.options().dtype(at::kFloat));
+  // [2][G][C], or [4][G][C] with the second BN: [sum g | sum g (x - mean) | sum g | sum g (x2 - mean2)]
+  auto part = at::empty({x2.has_value() ? 4 : 2, conv1x1_dgrad_bnred_partials(m, k, ncols, cus, pro, pmask), ncols},
+                        g.options().dtype(at::kFloat));
   at::Tensor aout;
   if (want_aout) aout = at::empty_like(g);
   conv1x1_dgrad_bnred(g.data_ptr(), w.data_ptr(), out.data_ptr(), m, k, ncols, dtype_code(g.scalar_type()),
@@ -437,7 +444,8 @@ std::vector<at::Tensor> dgrad_bnred(const at::Tensor& g, const at::Tensor& w, co
                       x.data_ptr(), mean.data_ptr<float>(), part.data_ptr<float>(), cus, cur_stream(),
                       coef.has_value() ? coef->data_ptr<float>() : nullptr, pro ? py->data_ptr() : nullptr,
                       pro ? pcoef->data_ptr<float>() : nullptr, want_aout ? aout.data_ptr() : nullptr, (int)res_h,
-                      (int)res_w, pmask);
+                      (int)res_w, pmask, x2.has_value() ? x2->data_ptr() : nullptr,
+                      mean2.has_value() ? mean2->data_ptr<float>() : nullptr);
   return {out, part, aout};
 }
 
@@ -687,7 +695,8 @@ void bind_conv(pybind11::module_& root) {
   m.def("dgrad_bnred", &dgrad_bnred, pybind11::arg("g"), pybind11::arg("w"), pybind11::arg("res"),
         pybind11::arg("bits"), pybind11::arg("x"), pybind11::arg("mean"), pybind11::arg("coef") = pybind11::none(),
         pybind11::arg("py") = pybind11::none(), pybind11::arg("pcoef") = pybind11::none(),
-        pybind11::arg("want_aout") = false, pybind11::arg("res_h") = 0, pybind11::arg("res_w") = 0);
+        pybind11::arg("want_aout") = false, pybind11::arg("res_h") = 0, pybind11::arg("res_w") = 0,
+        pybind11::arg("x2") = pybind11::none(), pybind11::arg("mean2") = pybind11::none());
   m.def("bnbwd_finalize", &bnbwd_finalize);
   m.def("part_payload", &part_payload, pybind11::arg("part"), pybind11::arg("count"),
         pybind11::arg("shift") = pybind11::none());

@@ -66,6 +66,12 @@ struct Args {
   const float* rcoef;    // the BN's forward apply coefficients [2][ncols] (recomputed-mask mode)
   const uint16_t* rx;    // the BN's input [M][ncols]
   const float* rmean;    // the BN's batch mean [ncols]
+  // RED, nullable: a SECOND batch norm fed by the same (masked) gradient — the downsample BN of
+  // the block below, whose output is summed with bn3's before the shared ReLU.  Its reduction
+  // sum(g * (x2 - mean2)) is accumulated too and part becomes [4][G][ncols]:
+  // [sum g | sum g (x - mean) | sum g | sum g (x2 - mean2)] (two contiguous [2][G] slabs)
+  const uint16_t* rx2;
+  const float* rmean2;
 };
 
 // operand prologues
@@ -93,7 +99,7 @@ constexpr int kSS = 64 + 8;  // staging row stride (elements): rows h and h+4 la
 
 constexpr int lds_bytes_nw(int nc, int kr, int pro, bool red, int nw) {
   return nc * (kr + 8) * 2 + nw * 32 * kSS * 2 + pro_rows(pro) * kr * 4 +
-         (red ? nw * 2 * nc * 4 : 0);
+         (red ? nw * 3 * nc * 4 : 0);
 }
 
 // waves per workgroup: 4 (two workgroups per CU) while the weight image is small; 8 sharing one
@@ -126,7 +132,7 @@ __global__ void __launch_bounds__(NW * 64, (NW == 8 || one_wg_per_cu(NC, KR, PRO
   uint16_t* bimg = lds;                       // [NC][BS]
   uint16_t* stg = lds + NC * BS;              // [kWaves][32][kSS]
   float* pc = reinterpret_cast<float*>(stg + kWaves * 32 * kSS);  // [2 or 3][KR]
-  float* rsum = pc + pro_rows(PRO) * KR;  // RED: [kWaves][2][NC]
+  float* rsum = pc + pro_rows(PRO) * KR;  // RED: [kWaves][3][NC]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, lr = lane & 31, lh = lane >> 5;
   const int col0 = blockIdx.y * NC;
@@ -178,7 +184,7 @@ __global__ void __launch_bounds__(NW * 64, (NW == 8 || one_wg_per_cu(NC, KR, PRO
     s1[cb] = s2[cb] = 0.f;
   }
   if constexpr (RED)
-    for (int i = tid; i < kWaves * 2 * NC; i += NT) rsum[i] = 0.f;
+    for (int i = tid; i < kWaves * 3 * NC; i += NT) rsum[i] = 0.f;
   __syncthreads();
 
   f32x16 acc[CN];
@@ -313,8 +319,9 @@ __global__ void __launch_bounds__(NW * 64, (NW == 8 || one_wg_per_cu(NC, KR, PRO
       // LDS staging below instead of after it (the compiler barrier keeps loads from being
       // hoisted across the staging otherwise)
       const bool has_res = WT && p.res != nullptr;  // residual add: a dgrad-form option
-      uint4 rv[4], xq[4];
+      uint4 rv[4], xq[4], xq2[4];
       unsigned mbv[4];
+      const bool red2 = RED && p.rx2 != nullptr;  // kernel-argument-uniform
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int qid = lane + 64 * i, rr = qid >> 3, c8 = (qid & 7) * 8;
@@ -335,6 +342,7 @@ __global__ void __launch_bounds__(NW * 64, (NW == 8 || one_wg_per_cu(NC, KR, PRO
         }
         if constexpr (RED) {
           xq[i] = ok ? *reinterpret_cast<const uint4*>(p.rx + off) : make_uint4(0, 0, 0, 0);
+          xq2[i] = (ok && red2) ? *reinterpret_cast<const uint4*>(p.rx2 + off) : make_uint4(0, 0, 0, 0);
           mbv[i] = (ok && p.rbits) ? p.rbits[off >> 3] : 0u;
         }
       }
@@ -343,12 +351,13 @@ __global__ void __launch_bounds__(NW * 64, (NW == 8 || one_wg_per_cu(NC, KR, PRO
 #pragma unroll
         for (int r = 0; r < 16; ++r) st[crow(r, lh) * kSS + 32 * q + lr] = from_f<T>(acc[2 * g + q][r]).x;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      float rs[8], rq[8], mu[8], rsc[8], rsh[8];
+      float rs[8], rq[8], rq2[8], mu[8], mu2[8], rsc[8], rsh[8];
       if constexpr (RED) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) rs[j] = rq[j] = 0.f;
+        for (int j = 0; j < 8; ++j) rs[j] = rq[j] = rq2[j] = 0.f;
         const int cc = col0 + 64 * g + (lane & 7) * 8;
         Vec8<float>::load(mu, p.rmean + cc);
+        if (red2) Vec8<float>::load(mu2, p.rmean2 + cc);
         if (!p.rbits) {  // wave-uniform: the mask of a plain BN + ReLU, recomputed from its input
           Vec8<float>::load(rsc, p.rcoef + cc);
           Vec8<float>::load(rsh, p.rcoef + p.ncols + cc);
@@ -386,6 +395,12 @@ __global__ void __launch_bounds__(NW * 64, (NW == 8 || one_wg_per_cu(NC, KR, PRO
                 rs[j] += gq;
                 rq[j] = fmaf(gq, xv[j] - mu[j], rq[j]);
               }
+              if (red2) {
+                float xv2[8];
+                Vec8<T>::load(xv2, reinterpret_cast<const T*>(&xq2[i]));
+#pragma unroll
+                for (int j = 0; j < 8; ++j) rq2[j] = fmaf(a[j], xv2[j] - mu2[j], rq2[j]);
+              }
             }
             Vec8<T>::store(reinterpret_cast<T*>(&v), a);
           }
@@ -409,12 +424,18 @@ __global__ void __launch_bounds__(NW * 64, (NW == 8 || one_wg_per_cu(NC, KR, PRO
             const float gq = __shfl_xor(sq, msk, 64);
             rs[j] = (up ? rs[j + half] : rs[j]) + gs;
             rq[j] = (up ? rq[j + half] : rq[j]) + gq;
+            if (red2) {
+              const float sq2 = up ? rq2[j] : rq2[j + half];
+              const float gq2 = __shfl_xor(sq2, msk, 64);
+              rq2[j] = (up ? rq2[j + half] : rq2[j]) + gq2;
+            }
           }
         }
         const int jc = ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1);
-        float* r0p = rsum + (wid * 2) * NC + 64 * g + (lane & 7) * 8 + jc;
+        float* r0p = rsum + (wid * 3) * NC + 64 * g + (lane & 7) * 8 + jc;
         r0p[0] += rs[0];
         r0p[NC] += rq[0];
+        if (red2) r0p[2 * NC] += rq2[0];
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
@@ -515,11 +536,14 @@ __global__ void __launch_bounds__(NW * 64, (NW == 8 || one_wg_per_cu(NC, KR, PRO
 
   if constexpr (RED) {
     __syncthreads();
-    for (int i = tid; i < 2 * NC; i += NT) {
+    // rows 0, 1 (and with the second BN: 2 = a copy of row 0, 3 = its g (x2 - mean2) sums)
+    const int nrows = p.rx2 ? 4 : 2;
+    for (int i = tid; i < nrows * NC; i += NT) {
       const int which = i / NC, n = i % NC;
+      const int src = which == 2 ? 0 : which == 3 ? 2 : which;
       float v = 0.f;
 #pragma unroll
-      for (int w = 0; w < kWaves; ++w) v += rsum[(w * 2 + which) * NC + n];
+      for (int w = 0; w < kWaves; ++w) v += rsum[(w * 3 + src) * NC + n];
       p.part[((int64_t)which * gridDim.x + blockIdx.x) * p.ncols + col0 + n] = v;
     }
   }
@@ -863,7 +887,7 @@ int conv1x1_dgrad_bnred_partials(int64_t m, int k, int ncols, int cus, bool pro,
 void conv1x1_dgrad_bnred(const void* g, const void* w, void* out, int64_t m, int k, int ncols, int dtype,
                          const void* res, const uint8_t* bits, const void* x, const float* mean, float* part, int cus,
                          hipStream_t s, const float* rcoef, const void* py, const float* pcoef, void* aout, int res_h,
-                         int res_w, bool pro_mask) {
+                         int res_w, bool pro_mask, const void* x2, const float* mean2) {
   if (!conv1x1_bn_supported(m, k, ncols)) throw std::runtime_error("conv1x1_dgrad_bnred: unsupported shape");
   if ((!bits && !rcoef) || !x || !mean || !part)
     throw std::runtime_error("conv1x1_dgrad_bnred: a mask source (bits or coef), x, mean and part are required");
@@ -881,6 +905,9 @@ void conv1x1_dgrad_bnred(const void* g, const void* w, void* out, int64_t m, int
   args.rcoef = rcoef;
   args.rx = static_cast<const uint16_t*>(x);
   args.rmean = mean;
+  if ((x2 == nullptr) != (mean2 == nullptr)) throw std::runtime_error("conv1x1_dgrad_bnred: x2 and mean2 go together");
+  args.rx2 = static_cast<const uint16_t*>(x2);
+  args.rmean2 = mean2;
   args.pcoef = pcoef;
   args.py = static_cast<const uint16_t*>(py);
   args.aout = static_cast<uint16_t*>(aout);

@@ -438,16 +438,20 @@ bool conv_hfp_supported(const ConvTapArgs& a) {
 // Default route only for small images (h * w <= 64: 7 x 7 at ResNet-50 stage 4, where the tap GEMM's
 // M tiles are mostly ragged: fwd 98 vs 109 us, dgrad 87 vs 123 us at 7x7x512 bs 256); at 14 x 14 /
 // 28 x 28 the tap GEMM is as fast or faster (76 vs 73 / 102 vs 97 us dgrad; profiles/r05/
-// halo_fprop_ab_r05d.jsonl).  APEX_AMD_CONV_HFP=0: never, =all: wherever supported.
+// halo_fprop_ab_r05d.jsonl).  APEX_AMD_CONV_HFP=1: that small-image route (off by default, see
+// below), =all: wherever supported, unset / 0: never.
 static int g_hfp_mode = -1;  // conv_hfp_set_mode: -1 = the environment's choice
 void conv_hfp_set_mode(int mode) { g_hfp_mode = mode; }
 
 bool conv_hfp_default(const ConvTapArgs& a) {
   static const int env_mode = [] {
     const char* e = std::getenv("APEX_AMD_CONV_HFP");
-    if (e && e[0] == '0') return 0;
+    if (e && e[0] == '1') return 1;
     if (e && e[0] == 'a') return 2;
-    return 1;
+    // off by default since round 6: the tap kernel (fprop2 128 x 128) now runs the 7x7x512
+    // forward faster than this kernel in the whole step (same-box A/B 12,477-12,487 vs
+    // 12,457-12,460 img/s, profiles/r06/ab_ds_hfp_r06c.txt; its dgrad twin runs 71 us vs 102)
+    return 0;
   }();
   const int mode = g_hfp_mode >= 0 ? g_hfp_mode : env_mode;
   if (mode == 0 || !conv_hfp_supported(a)) return false;

@@ -144,7 +144,10 @@ void conv1x1_dgrad_bnred(const void* g, const void* w, void* out, int64_t m, int
                          const void* res, const uint8_t* bits, const void* x, const float* mean, float* part, int cus,
                          hipStream_t s, const float* rcoef = nullptr, const void* py = nullptr,
                          const float* pcoef = nullptr, void* aout = nullptr, int res_h = 0, int res_w = 0,
-                         bool pro_mask = false);  // pcoef [5][k] with the recomputed ReLU mask (see conv1x1_bn)
+                         bool pro_mask = false,  // pcoef [5][k] with the recomputed ReLU mask (see conv1x1_bn)
+                         // a second BN fed by the same masked gradient (the downsample BN): part is
+                         // then [4][G][ncols] = [sum g | sum g (x - mean) | sum g | sum g (x2 - mean2)]
+                         const void* x2 = nullptr, const float* mean2 = nullptr);
 void conv1x1_bnbwd_finalize(const float* part, int g, int c, float inv_n, const float* mean, const float* istd,
                             const float* w, float* gw, float* gb, float* coef, hipStream_t s);
 

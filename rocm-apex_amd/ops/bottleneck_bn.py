@@ -92,6 +92,12 @@ _BN1_FOLD = os.environ.get("APEX_AMD_BN1_FOLD", "0") == "1"
 # opt-in: same-box A/B 12,414-12,423 vs 12,508-12,532 img/s without it (profiles/r05/ab_bn1_dx_pro_r05z.txt):
 # the two-operand prologue slows conv1's dgrad by more than the [M, width] pass it saves
 _BN1_DX_PRO = os.environ.get("APEX_AMD_BN1_DX_PRO", "0") == "1"
+# the downsample BN's dx as the downsample dgrad's operand prologue (stages 1-2, where that dgrad
+# is native); 0 = reduction + dx pass + plain dgrad (A/B)
+_DS_DX_PRO = os.environ.get("APEX_AMD_DS_DX_PRO", "1") != "0"
+# the downsample BN's backward reduction accumulated by the block above's dgrad_bnred epilogue
+# (BlockLink.yd: one more operand read there instead of a reduction pass over dm and yd)
+_DS_RED = os.environ.get("APEX_AMD_DS_RED", "1") != "0"
 
 
 @functools.lru_cache(maxsize=None)
@@ -108,7 +114,7 @@ def _bn1_fold(cin, cout, h, w):
     if ext is None:
         return False
     sp = cin == 64 and cout == 64 and os.environ.get("APEX_AMD_CONV_SP", "1") != "0"
-    hfp = (hasattr(ext, "hfp_supported") and h * w <= 64 and os.environ.get("APEX_AMD_CONV_HFP", "1")[:1] != "0"
+    hfp = (hasattr(ext, "hfp_supported") and h * w <= 64 and os.environ.get("APEX_AMD_CONV_HFP", "0")[:1] in ("1", "a")
            and bool(ext.hfp_supported(1, h, w, cin, cout)))
     return sp or hfp
 
@@ -178,10 +184,14 @@ class BlockLink:
     of the block output saved per boundary.  ``materialize`` runs the plain output pass instead
     for a consumer that does not take it."""
 
-    __slots__ = ("y3", "bits", "mean", "invstd", "part", "defer", "pend")
+    __slots__ = ("y3", "bits", "mean", "invstd", "part", "defer", "pend", "yd", "meand")
 
     def __init__(self, defer=False):
         self.y3 = self.bits = self.mean = self.invstd = self.part = self.pend = None
+        # downsampling block below: its downsample BN's input and batch mean — the same masked
+        # gradient feeds that BN, so block i+1's dgrad_bnred accumulates its reduction too
+        # (``part`` is then [4, G, C]: bn3's [2, G, C] slab, then the downsample BN's)
+        self.yd = self.meand = None
         self.defer = defer
 
     def materialize(self):
@@ -439,6 +449,8 @@ class _BottleneckFn(torch.autograd.Function):
         ctx.groups = (bn1.group, bn2.group, bn3.group, bnd.group if bnd is not None else None)
         if link_out is not None:
             link_out.y3, link_out.bits, link_out.mean, link_out.invstd = y3, bits, sm3, si3
+            if wds is not None and _DS_RED:
+                link_out.yd, link_out.meand = yd, smd
         return _nchw(out2, n, oh, ow)
 
     @staticmethod
@@ -457,9 +469,13 @@ class _BottleneckFn(torch.autograd.Function):
         # (the block above already masked the gradient and reduced it when linked); bn3's dx
         # pass runs as conv3's dgrad operand prologue (dx3 written as a by-product for the
         # weight gradient) where that kernel takes the shape
+        ds_part = None
         if link_out is not None and link_out.part is not None:
             dm = go2
-            cb3, gg3, gb3 = bwd_from_part(link_out.part, float(go2.size(0)), sm3, si3, g3, gr3, in3)
+            part = link_out.part
+            if part.size(0) == 4:  # the downsample BN's reduction came along (BlockLink.yd)
+                part, ds_part = part[0:2], part[2:4]
+            cb3, gg3, gb3 = bwd_from_part(part, float(go2.size(0)), sm3, si3, g3, gr3, in3)
             link_out.part = None
         else:
             if bits is None:  # deferred output: its ReLU bits came from the block above's conv1
@@ -523,12 +539,28 @@ class _BottleneckFn(torch.autograd.Function):
             short_tmp = dm is not go2
         else:
             short_tmp = True
-            dyd, ggd, gbd = bwd_full(dm, yd, gds, smd, sid, cd, False, grd, ind)
+            # the downsample BN's dx as the downsample dgrad's operand prologue (kProBnBwd: the
+            # reduction pass writes nothing, the prologue writes dyd for the weight gradient) —
+            # one [M, cout] pass and a launch fewer than reduction + dx pass + dgrad reading dyd
+            ds_pro = (_DS_DX_PRO and (grd is None or ds_part is not None) and (stride == 1 or xs2 is not None)
+                      and _dgrad_native(dm.size(0), cout, cin))
+            if ds_part is not None:  # reduced by the block above's dgrad_bnred epilogue
+                cbd, ggd, gbd = bwd_from_part(ds_part, float(dm.size(0)), smd, sid, gds, grd, ind)
+            elif ds_pro:
+                _, cbd, ggd, gbd = bn.bwd_reduce(dm, yd, gds, smd, sid, cd, False, None)
+            if ds_pro:
+                short, _, dyd = _conv().bn1x1(dm, wds.view(cout, cin), True, cbd.view(-1), None, False, None, yd, True)
+            elif ds_part is not None:
+                dyd = bn.bwd_apply(dm, yd, cd, cbd)
+            else:
+                dyd, ggd, gbd = bwd_full(dm, yd, gds, smd, sid, cd, False, grd, ind)
             if stride == 1:
-                short = conv1x1_dgrad(dyd, wds.view(cout, cin))
+                if not ds_pro:
+                    short = conv1x1_dgrad(dyd, wds.view(cout, cin))
                 dwd = conv1x1_wgrad(dyd, x2, None, wds)
             elif xs2 is not None:
-                short = conv1x1_dgrad(dyd, wds.view(cout, cin))
+                if not ds_pro:
+                    short = conv1x1_dgrad(dyd, wds.view(cout, cin))
                 dwd = conv1x1_wgrad(dyd, xs2, None, wds)
                 sub_hw = (h, wd)
             else:
@@ -537,13 +569,15 @@ class _BottleneckFn(torch.autograd.Function):
         rh, rw = sub_hw if sub_hw is not None else (0, 0)
         if link_in is not None and link_in.bits is not None and _red_native(dz1.size(0), width, cin):
             # mask with the block below's ReLU bits + its bn3 backward reduction, in this kernel
+            ds2 = dict(x2=link_in.yd, mean2=link_in.meand) if link_in.yd is not None else {}
             if bn1_pro:
                 dx, link_in.part, dy1 = _conv().dgrad_bnred(dz1, w1.view(width, cin), short, link_in.bits, link_in.y3,
                                                             link_in.mean, py=y1, pcoef=pc1, want_aout=True, res_h=rh,
-                                                            res_w=rw)
+                                                            res_w=rw, **ds2)
             else:
                 dx, link_in.part, _ = _conv().dgrad_bnred(dy1, w1.view(width, cin), short, link_in.bits, link_in.y3,
-                                                          link_in.mean, res_h=rh, res_w=rw)
+                                                          link_in.mean, res_h=rh, res_w=rw, **ds2)
+            link_in.yd = link_in.meand = None
         elif bn1_pro:
             dx, _, dy1 = _conv().bn1x1(dz1, w1.view(width, cin), True, pc1, None, False, short, y1, True, res_h=rh,
                                        res_w=rw)

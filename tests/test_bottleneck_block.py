@@ -470,3 +470,86 @@ def test_gpu_bottleneck_chain_syncbn_fp16_arm():
     from tests._dist_utils import run_multiprocess
 
     run_multiprocess(_sync_chain_fp16_worker, 2, (), timeout=240)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inplanes,planes,stride,h,batch", [(64, 64, 1, 14, 2), (256, 128, 2, 16, 2)])
+def test_gpu_downsample_dx_prologue_matches_apply_pass(inplanes, planes, stride, h, batch, monkeypatch):
+    """The downsample BN's dx computed as the downsample dgrad's operand prologue (kProBnBwd,
+    ``_DS_DX_PRO``) against the reduction + dx pass + plain dgrad: the prologue runs the dx pass's
+    arithmetic, so the dx it writes for the weight gradient — and with it every gradient of the
+    block — is bitwise the same."""
+    import apex  # noqa: F401
+    from apex.ops import bottleneck_bn
+
+    torch.manual_seed(3)
+    a = _make(inplanes, planes, stride, True, fused=True).cuda()
+    for mod in a.modules():
+        if isinstance(mod, torch.nn.Conv2d):
+            mod.to(torch.bfloat16)
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.weight.data.uniform_(0.5, 1.5)
+            mod.bias.data.uniform_(-0.2, 0.2)
+    a = a.to(memory_format=torch.channels_last).train()
+    b = copy.deepcopy(a)
+    x = torch.randn(batch, inplanes, h, h, device="cuda").to(torch.bfloat16).to(memory_format=torch.channels_last)
+    gy = None
+    outs = []
+    for mod, pro in ((a, True), (b, False)):
+        monkeypatch.setattr(bottleneck_bn, "_DS_DX_PRO", pro)
+        xi = x.clone().requires_grad_(True)
+        y = mod(xi)
+        if gy is None:
+            gy = torch.randn_like(y)
+        y.backward(gy)
+        outs.append((y.detach(), xi.grad, {n: p.grad for n, p in mod.named_parameters()}))
+    (ya, ga, pa), (yb, gb, pb) = outs
+    assert torch.equal(ya, yb)
+    # the downsample branch is bitwise (its dx, written by the prologue, is the dx pass's value);
+    # elsewhere the stride-2 block runs library 3x3 gradients whose summation order may vary from
+    # call to call (MIOpen weight gradient), so those compare at rounding level
+    for n in pa:
+        if n.startswith("downsample"):
+            assert torch.equal(pa[n], pb[n]), (n, _rel(pa[n], pb[n]))
+        else:
+            assert _rel(pa[n], pb[n]) < 1e-3, (n, _rel(pa[n], pb[n]))
+    if stride == 1:
+        assert torch.equal(ga, gb), _rel(ga, gb)
+    else:
+        assert _rel(ga, gb) < 1e-3, _rel(ga, gb)
+
+
+@pytest.mark.gpu
+def test_gpu_chain_downsample_reduction_in_block_above(monkeypatch):
+    """The downsampling block's downsample-BN backward reduction accumulated by the block above's
+    conv1 dgrad epilogue (BlockLink.yd, ``_DS_RED``: part [4, G, C]) against the reduction pass
+    over dm and yd: the same sums in another order, so the arms agree to rounding and a wrong
+    operand / mean / slab shows as an O(1) difference."""
+    from apex.ops import bottleneck_bn
+
+    torch.manual_seed(5)
+    a = _chain().cuda().to(memory_format=torch.channels_last).train()
+    b = copy.deepcopy(a)
+    x = torch.randn(4, 64, 14, 14, device="cuda").to(torch.bfloat16).to(memory_format=torch.channels_last)
+    gy = torch.randn(4, 256, 14, 14, device="cuda").to(torch.bfloat16).to(memory_format=torch.channels_last)
+    seen = []
+    conv = bottleneck_bn._conv()
+    orig = conv.dgrad_bnred
+
+    def spy(*args, **kw):
+        r = orig(*args, **kw)
+        seen.append(int(r[1].size(0)))
+        return r
+
+    monkeypatch.setattr(conv, "dgrad_bnred", spy, raising=False)
+    monkeypatch.setattr(bottleneck_bn, "_DS_RED", True)
+    ya, ga, pa, _ = _run_chain(a, x, gy, True)
+    with_ds = list(seen)
+    seen.clear()
+    monkeypatch.setattr(bottleneck_bn, "_DS_RED", False)
+    yb, gb, pb, _ = _run_chain(b, x, gy, True)
+    assert sorted(with_ds) == [2, 4] and sorted(seen) == [2, 2], (with_ds, seen)
+    assert torch.equal(ya, yb)
+    assert _rel(ga, gb) < 1e-2, _rel(ga, gb)
+    for n in pa:
+        assert _rel(pa[n], pb[n]) < 1e-2, (n, _rel(pa[n], pb[n]))
