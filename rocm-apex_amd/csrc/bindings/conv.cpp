@@ -2,6 +2,7 @@
 // submodule ``_C.conv`` used by apex.ops.conv (ResNet 3x3 / strided convolutions, NHWC).
 // Activations are dense NHWC [N, H, W, C] tensors (the python layer passes zero-copy views of
 // torch channels_last tensors); weights are [K, taps, C] (k contiguous per tap).
+#include "apex_amd/conv_ks.h"
 #include "common.h"
 #include "apex_amd/conv_api.h"
 #include "apex_amd/layout_extra.h"
@@ -195,7 +196,9 @@ std::vector<at::Tensor> bn1x1(const at::Tensor& a, const at::Tensor& w, bool w_k
   const int k = (int)a.size(1);
   const int ncols = (int)(w_kmajor_out ? w.size(1) : w.size(0));
   TORCH_CHECK((w_kmajor_out ? w.size(0) : w.size(1)) == k, "bn1x1: weight does not match the reduction dim");
-  TORCH_CHECK(conv1x1_bn_supported(m, k, ncols), "bn1x1: unsupported shape (k in 64/128/256/512, ncols % 64)");
+  // the deep reductions (k 1024 / 2048, ResNet stages 3-4) run on the K-streamed kernel
+  const bool ks = !conv1x1_bn_supported(m, k, ncols) && conv1x1_ks_supported(m, k, ncols);
+  TORCH_CHECK(ks || conv1x1_bn_supported(m, k, ncols), "bn1x1: unsupported shape (k % 64, ncols % 64)");
   auto f32 = [&](const c10::optional<at::Tensor>& t, int64_t n, const char* what) -> const float* {
     if (!t.has_value()) return nullptr;
     TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == n, "bn1x1: ",
@@ -217,6 +220,16 @@ std::vector<at::Tensor> bn1x1(const at::Tensor& a, const at::Tensor& w, bool w_k
   auto y = at::empty({m, ncols}, a.options());
   at::Tensor part, aout;
   if (want_aout) aout = at::empty_like(a);
+  if (ks) {
+    TORCH_CHECK(!res.has_value() && res_h <= 0 && !pmask && (bnbwd || pc == nullptr),
+                "bn1x1: the deep-reduction kernel takes no residual, recomputed-mask or BN-apply prologue");
+    if (stats) part = at::empty({2, conv1x1_ks_partials(m, k, ncols, cus, bnbwd ? 2 : 0), ncols}, a.options().dtype(at::kFloat));
+    conv1x1_ks(a.data_ptr(), w.data_ptr(), y.data_ptr(), m, k, ncols, w_kmajor_out, dtype_code(a.scalar_type()), pc,
+               bnbwd ? 2 : 0, false, nullptr, sh, stats ? part.data_ptr<float>() : nullptr,
+               bnbwd ? py->data_ptr() : nullptr, want_aout ? aout.data_ptr() : nullptr, nullptr, nullptr, nullptr,
+               nullptr, cus, cur_stream());
+    return {y, part, aout};
+  }
   if (stats)
     part = at::empty({2, conv1x1_bn_partials(m, k, ncols, pc != nullptr, cus), ncols}, a.options().dtype(at::kFloat));
   if (res.has_value())
@@ -289,7 +302,8 @@ std::vector<at::Tensor> bn1x1_addrelu(const at::Tensor& a, const at::Tensor& res
               "bn1x1_addrelu: w must be [ncols, K] of a's dtype");
   const int64_t m = a.size(0);
   const int k = (int)a.size(1), ncols = (int)w.size(0);
-  TORCH_CHECK(conv1x1_bn_supported(m, k, ncols) && (m * k) % 8 == 0, "bn1x1_addrelu: unsupported shape");
+  const bool ks = !conv1x1_bn_supported(m, k, ncols) && conv1x1_ks_supported(m, k, ncols);
+  TORCH_CHECK((ks || conv1x1_bn_supported(m, k, ncols)) && (m * k) % 8 == 0, "bn1x1_addrelu: unsupported shape");
   TORCH_CHECK(pcoef.is_cuda() && pcoef.scalar_type() == at::kFloat && pcoef.is_contiguous() &&
                   pcoef.numel() == (split ? 2 : 4) * (int64_t)k,
               "bn1x1_addrelu: pcoef must be contiguous fp32 [4K] ([2K] with split)");
@@ -312,6 +326,14 @@ std::vector<at::Tensor> bn1x1_addrelu(const at::Tensor& a, const at::Tensor& res
     out = at::empty_like(a);
   }
   auto bits = at::empty({m * k / 8}, a.options().dtype(at::kByte));
+  if (ks) {
+    auto part = at::empty({2, conv1x1_ks_partials(m, k, ncols, cus, 3), ncols}, a.options().dtype(at::kFloat));
+    conv1x1_ks(a.data_ptr(), w.data_ptr(), y.data_ptr(), m, k, ncols, false, dtype_code(a.scalar_type()),
+               pcoef.data_ptr<float>(), 3, split, res_coef.has_value() ? res_coef->data_ptr<float>() : nullptr,
+               shift.has_value() ? shift->data_ptr<float>() : nullptr, part.data_ptr<float>(), res.data_ptr(),
+               out.data_ptr(), bits.data_ptr<uint8_t>(), nullptr, nullptr, nullptr, cus, cur_stream());
+    return {y, part, out, bits};
+  }
   auto part = at::empty({2, conv1x1_bn_partials(m, k, ncols, true, cus, true), ncols}, a.options().dtype(at::kFloat));
   conv1x1_bn(a.data_ptr(), w.data_ptr(), y.data_ptr(), m, k, ncols, false, dtype_code(a.scalar_type()),
              pcoef.data_ptr<float>(), shift.has_value() ? shift->data_ptr<float>() : nullptr, part.data_ptr<float>(), cus,
@@ -425,7 +447,8 @@ std::vector<at::Tensor> dgrad_bnred(const at::Tensor& g, const at::Tensor& w, co
                     (pcoef->numel() == 3 * (int64_t)k || pmask),
                 "dgrad_bnred: py must match g, pcoef fp32 [3k] or [5k]");
   TORCH_CHECK(!want_aout || pro, "dgrad_bnred: want_aout needs the prologue");
-  TORCH_CHECK(conv1x1_bn_supported(m, k, ncols), "dgrad_bnred: unsupported shape");
+  const bool ks = !conv1x1_bn_supported(m, k, ncols) && conv1x1_ks_supported(m, k, ncols);
+  TORCH_CHECK(ks || conv1x1_bn_supported(m, k, ncols), "dgrad_bnred: unsupported shape");
   TORCH_CHECK(x2.has_value() == mean2.has_value(), "dgrad_bnred: x2 and mean2 go together");
   if (x2.has_value())
     TORCH_CHECK(x2->is_contiguous() && x2->scalar_type() == g.scalar_type() && x2->numel() == m * ncols &&
@@ -434,6 +457,19 @@ std::vector<at::Tensor> dgrad_bnred(const at::Tensor& g, const at::Tensor& w, co
   const c10::hip::HIPGuard guard(g.get_device());
   const int cus = device_cus(g.get_device());
   auto out = at::empty({m, ncols}, g.options());
+  if (ks) {
+    TORCH_CHECK(coef.has_value() && !res.has_value() && res_h <= 0 && !x2.has_value() && !pmask,
+                "dgrad_bnred: the deep-reduction kernel takes the recomputed mask (coef) only: no bits, residual, "
+                "second BN or masked prologue");
+    auto part = at::empty({2, conv1x1_ks_partials(m, k, ncols, cus, pro ? 2 : 0), ncols}, g.options().dtype(at::kFloat));
+    at::Tensor aout;
+    if (want_aout) aout = at::empty_like(g);
+    conv1x1_ks(g.data_ptr(), w.data_ptr(), out.data_ptr(), m, k, ncols, true, dtype_code(g.scalar_type()),
+               pro ? pcoef->data_ptr<float>() : nullptr, pro ? 2 : 0, false, nullptr, nullptr, part.data_ptr<float>(),
+               pro ? py->data_ptr() : nullptr, want_aout ? aout.data_ptr() : nullptr, nullptr,
+               coef->data_ptr<float>(), x.data_ptr(), mean.data_ptr<float>(), cus, cur_stream());
+    return {out, part, aout};
+  }
   // [2][G][C], or [4][G][C] with the second BN: [sum g | sum g (x - mean) | sum g | sum g (x2 - mean2)]
   auto part = at::empty({x2.has_value() ? 4 : 2, conv1x1_dgrad_bnred_partials(m, k, ncols, cus, pro, pmask), ncols},
                         g.options().dtype(at::kFloat));
@@ -698,6 +734,7 @@ void bind_conv(pybind11::module_& root) {
         pybind11::arg("want_aout") = false, pybind11::arg("res_h") = 0, pybind11::arg("res_w") = 0,
         pybind11::arg("x2") = pybind11::none(), pybind11::arg("mean2") = pybind11::none());
   m.def("bnbwd_finalize", &bnbwd_finalize);
+  m.def("ks1x1_supported", [](int64_t m, int64_t k, int64_t ncols) { return conv1x1_ks_supported(m, (int)k, (int)ncols); });
   m.def("part_payload", &part_payload, pybind11::arg("part"), pybind11::arg("count"),
         pybind11::arg("shift") = pybind11::none());
   m.def("conv3_bwd", &conv3_bwd_b);

@@ -53,6 +53,28 @@ _ENABLED = os.environ.get("APEX_AMD_FUSED_BLOCK", "1") != "0"
 # APEX_AMD_FUSED_BLOCK_FORCE_NATIVE=0 restores the per-op routes.
 FORCE_NATIVE = os.environ.get("APEX_AMD_FUSED_BLOCK_FORCE_NATIVE", "1") == "1"
 _NATIVE_K = (64, 128, 256, 512)
+# the deep reductions of stages 3-4 (k 1024 / 2048) on the K-streamed fused kernel
+# (csrc/conv/conv1x1_ks.hip: weights through an LDS-DMA ring): conv1's / the downsample's forward
+# with the statistics epilogue and conv3's data gradient with bn2's backward reduction in the
+# epilogue, instead of hipBLASLt + a statistics / reduction pass.  OPT-IN (APEX_AMD_C1KS=1): the
+# kernel is latency-bound at 8 waves x two 64-deep chunks of operands in flight (the 256-column
+# accumulators leave no registers for a deeper ring), so the fused forms run at or behind
+# hipBLASLt + the pass: stage-3 conv1 48.8 vs 36.6 + 10.6 us, conv3 dgrad + bn2 sums 57 vs
+# 37 + 14.5 us (profiles/r06/resnet50_step_timeline_r06h.md), whole step -0.4 %
+# (profiles/r06/ab_c1ks_r06g.txt).  The two-operand prologues (deferred output, bn3 dx:
+# APEX_AMD_C1KS_PRO=1) re-read both operands per 128-column block: 128 / 109 us vs 111 / 105 us
+# for the passes + hipBLASLt (profiles/r06/resnet50_step_timeline_r06f.md), -2.8 %.
+_KS = os.environ.get("APEX_AMD_C1KS", "0") == "1"
+_KS_PRO = os.environ.get("APEX_AMD_C1KS_PRO", "0") == "1"
+
+
+def _k_native(k):
+    return k in _NATIVE_K or (_KS and k % 64 == 0 and 1024 <= k <= 2048)
+
+
+def _ks_only(k):
+    """A deep reduction only the K-streamed kernel takes."""
+    return k not in _NATIVE_K and _k_native(k)
 # conv3's fused data + weight gradient (csrc/conv/conv3_bwd.hip); 0 = the two-kernel path (A/B)
 _C3B = os.environ.get("APEX_AMD_CONV3_BWD", "1") != "0"
 # block output pass deferred into the next block's conv1 (BlockLink.defer); 0 = A/B off
@@ -298,13 +320,13 @@ def bwd_full(dy, x, w, sm, si, coef, relu, group, inv_n):
 # with the separate statistics / apply passes.
 def _fwd_native(m, k, n):
     if FORCE_NATIVE:
-        return k in _NATIVE_K and n % 64 == 0
+        return _k_native(k) and n % 64 == 0
     return k in _NATIVE_K and n % 64 == 0 and n <= 512 and not (k == 512 and n >= 256)
 
 
 def _dgrad_native(m, kout, cin):
     if FORCE_NATIVE:
-        return kout in _NATIVE_K and cin % 64 == 0
+        return _k_native(kout) and cin % 64 == 0
     return kout in _NATIVE_K and cin % 64 == 0 and cin <= 256 and m >= 100000
 
 
@@ -336,7 +358,8 @@ def conv1x1_dgrad(g2, w2d, add2=None, add_inplace=False, sub_hw=None):
     first copying it to a fresh output (a full D2D copy per call).  ``sub_hw = (h, w)``: add2 is
     the gradient of the stride-2 subsample of the [N, h, w] output, added at even (y, x) only."""
     m, kout = g2.shape
-    if _dgrad_native(m, kout, w2d.size(1)):
+    # (a residual / subsampled residual is an option of the resident-weight kernel only)
+    if _dgrad_native(m, kout, w2d.size(1)) and (kout in _NATIVE_K or (add2 is None and sub_hw is None)):
         h, w = sub_hw if sub_hw is not None else (0, 0)
         return _conv().bn1x1(g2, w2d, True, None, None, False, add2, res_h=h, res_w=w)[0]
     if sub_hw is not None:
@@ -491,11 +514,19 @@ class _BottleneckFn(torch.autograd.Function):
             dw3 = dw3.view_as(w3)
             cb2, gg2, gb2 = bwd_from_part(part2, float(dm.size(0)), sm2, si2, g2, gr2, in2)
             dy2 = bn.bwd_apply(dz2, y2m, c2, cb2)
-        elif _dgrad_native(dm.size(0), cout, width) and width == 64:
+        elif _dgrad_native(dm.size(0), cout, width) and _ks_only(cout) and not _KS_PRO:
+            # stages 3-4 (K-streamed kernel): bn3's dx pass, then conv3's dgrad with bn2's ReLU mask
+            # recomputed and its backward sums in the epilogue (no bn2 reduction pass)
+            dx3 = bn.bwd_apply(dm, y3, c3, cb3)
+            dz2, part2, _ = _conv().dgrad_bnred(dx3, w3m, None, None, y2m, sm2, coef=c2)
+            cb2, gg2, gb2 = bwd_from_part(part2, float(dm.size(0)), sm2, si2, g2, gr2, in2)
+            dy2 = bn.bwd_apply(dz2, y2m, c2, cb2)
+        elif _dgrad_native(dm.size(0), cout, width) and (width == 64 or _ks_only(cout)):
             # conv3 dgrad with bn3's dx as the operand prologue (dx3 written for the wgrad) AND
             # bn2's ReLU mask + backward reduction in the epilogue: bn2's reduction pass is gone
             # (stage 1 only: at 128+ channels the longer epilogue costs more than the pass,
-            # profiles/resnet50_node_r03e.md)
+            # profiles/resnet50_node_r03e.md; and stages 3-4 on the K-streamed kernel, whose
+            # epilogue runs under the deep reduction's MFMAs)
             dz2, part2, dx3 = _conv().dgrad_bnred(dm, w3m, None, None, y2m, sm2, coef=c2, py=y3,
                                                   pcoef=cb3.view(-1), want_aout=True)
             cb2, gg2, gb2 = bwd_from_part(part2, float(dm.size(0)), sm2, si2, g2, gr2, in2)
@@ -543,7 +574,7 @@ class _BottleneckFn(torch.autograd.Function):
             # reduction pass writes nothing, the prologue writes dyd for the weight gradient) —
             # one [M, cout] pass and a launch fewer than reduction + dx pass + dgrad reading dyd
             ds_pro = (_DS_DX_PRO and (grd is None or ds_part is not None) and (stride == 1 or xs2 is not None)
-                      and _dgrad_native(dm.size(0), cout, cin))
+                      and _dgrad_native(dm.size(0), cout, cin) and (cout in _NATIVE_K or _KS_PRO))
             if ds_part is not None:  # reduced by the block above's dgrad_bnred epilogue
                 cbd, ggd, gbd = bwd_from_part(ds_part, float(dm.size(0)), smd, sid, gds, grd, ind)
             elif ds_pro:
@@ -627,7 +658,10 @@ def takes_deferred_input(block, x_shape, dtype):
         return False
     n, c, h, w = x_shape
     width = block.conv1.out_channels
-    return block.conv1.in_channels == c and _fwd_native(n * h * w, c, width) and _bn_ok(block.bn1)
+    # (the deep stage-3 / 4 reductions take the deferred output only with the K-streamed kernel's
+    # two-operand prologue, _KS_PRO)
+    return (block.conv1.in_channels == c and _fwd_native(n * h * w, c, width) and (c in _NATIVE_K or _KS_PRO)
+            and _bn_ok(block.bn1))
 
 
 # block outputs computed by the next block's conv1 (BlockLink.defer) since import
