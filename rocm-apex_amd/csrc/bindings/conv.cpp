@@ -65,7 +65,9 @@ c10::optional<at::Tensor> tap_fprop(const at::Tensor& in, const at::Tensor& w, a
                std::vector<int64_t> dw, const c10::optional<at::Tensor>& scale,
                const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& residual, bool relu,
                const c10::optional<at::Tensor>& mask, const c10::optional<at::Tensor>& stats,
-               const c10::optional<at::Tensor>& stats_shift, const c10::optional<at::Tensor>& pcoef) {
+               const c10::optional<at::Tensor>& stats_shift, const c10::optional<at::Tensor>& pcoef,
+               const c10::optional<at::Tensor>& red_x, const c10::optional<at::Tensor>& red_coef,
+               const c10::optional<at::Tensor>& red_mean) {
   ConvTapArgs a = make_args(in, w, out, oh, ow, ish, isw, osh, osw, oph, opw, dh, dw);
   auto per_channel = [&](const c10::optional<at::Tensor>& t, const char* what) -> const float* {
     if (!t.has_value()) return nullptr;
@@ -90,10 +92,24 @@ c10::optional<at::Tensor> tap_fprop(const at::Tensor& in, const at::Tensor& w, a
                 "conv tap_fprop: mask must match the output's shape, layout and dtype");
     a.mask = mask->data_ptr();
   }
+  if (red_x.has_value()) {
+    // BN backward reduction of the stored gradient (returned as the [2, tiles, K] partials)
+    check_nhwc(*red_x, "red_x");
+    TORCH_CHECK(red_x->sizes() == out.sizes() && red_x->strides() == out.strides() &&
+                    red_x->scalar_type() == out.scalar_type() && red_coef.has_value() && red_mean.has_value() &&
+                    !stats_shift.has_value() && !mask.has_value() && !pcoef.has_value(),
+                "conv tap_fprop: red_x must match the output (layout, dtype) and comes with red_coef / red_mean only");
+    TORCH_CHECK(red_coef->is_cuda() && red_coef->scalar_type() == at::kFloat && red_coef->is_contiguous() &&
+                    red_coef->numel() == 2 * out.size(3),
+                "conv tap_fprop: red_coef must be a contiguous fp32 [2K] tensor");
+    a.red_x = red_x->data_ptr();
+    a.red_coef = red_coef->data_ptr<float>();
+    a.red_mean = per_channel(red_mean, "red_mean");
+  }
   const c10::hip::HIPGuard g(in.get_device());
   const int cus = device_cus(in.get_device());
   c10::optional<at::Tensor> made;
-  if (stats.has_value() || stats_shift.has_value()) {
+  if (stats.has_value() || stats_shift.has_value() || red_x.has_value()) {
     const int64_t rows = conv_tap_stats_tiles(a, cus);
     at::Tensor st = stats.has_value() ? *stats : at::empty({2, rows, out.size(3)}, out.options().dtype(at::kFloat));
     TORCH_CHECK(st.is_cuda() && st.scalar_type() == at::kFloat && st.is_contiguous() &&
@@ -685,7 +701,9 @@ void bind_conv(pybind11::module_& root) {
         pybind11::arg("scale") = pybind11::none(), pybind11::arg("bias") = pybind11::none(),
         pybind11::arg("residual") = pybind11::none(), pybind11::arg("relu") = false,
         pybind11::arg("mask") = pybind11::none(), pybind11::arg("stats") = pybind11::none(),
-        pybind11::arg("stats_shift") = pybind11::none(), pybind11::arg("pcoef") = pybind11::none());
+        pybind11::arg("stats_shift") = pybind11::none(), pybind11::arg("pcoef") = pybind11::none(),
+        pybind11::arg("red_x") = pybind11::none(), pybind11::arg("red_coef") = pybind11::none(),
+        pybind11::arg("red_mean") = pybind11::none());
   m.def("hfp_supported", [](int64_t n, int64_t h, int64_t w, int64_t c, int64_t kout) {
     ConvTapArgs a{};
     void* aligned = reinterpret_cast<void*>(static_cast<uintptr_t>(256));  // alignment checks only

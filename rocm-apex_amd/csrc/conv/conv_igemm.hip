@@ -61,6 +61,9 @@ struct Geo {
   int relu;
   float* stats;         // nullable: BN statistics partials [2][tiles_m][kout] of the stored output
   const float* shift;   //   about this per-channel shift (nullable = 0)
+  const uint16_t* rx;   // nullable: BN backward reduction mode (ConvTapArgs::red_x) — stats then
+  const float* rcoef;   //   holds sum(g) / sum(g (x - mean)) of the masked gradient g
+  const float* rmean;
 };
 
 inline Geo make_geo(const ConvTapArgs& a) {
@@ -76,6 +79,9 @@ inline Geo make_geo(const ConvTapArgs& a) {
   g.shift = a.stats_shift;
   g.mask = reinterpret_cast<const uint16_t*>(a.mask);
   g.relu = a.relu;
+  g.rx = reinterpret_cast<const uint16_t*>(a.red_x);
+  g.rcoef = a.red_coef;
+  g.rmean = a.red_mean;
   for (int t = 0; t < kConvMaxTaps; ++t) {
     g.dh[t] = t < a.ntaps ? a.dh[t] : 0;
     g.dw[t] = t < a.ntaps ? a.dw[t] : 0;
@@ -156,10 +162,15 @@ __device__ __forceinline__ void epi_chunk(const Geo& g, uint16_t* __restrict__ Y
   if (g.scale) Vec8<float>::load(sc, g.scale + gc);
   if (g.bias) Vec8<float>::load(bi, g.bias + gc);
   const bool affine = g.scale || g.bias;
-  float sft[8];
+  float sft[8], rsc[8], rsh[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) sft[e] = 0.f;
+  for (int e = 0; e < 8; ++e) sft[e] = rsc[e] = rsh[e] = 0.f;
   if (g.stats && g.shift) Vec8<float>::load(sft, g.shift + gc);
+  if (g.rx) {  // BN backward reduction: sft = the BN's mean, rsc / rsh its forward apply coefficients
+    Vec8<float>::load(sft, g.rmean + gc);
+    Vec8<float>::load(rsc, g.rcoef + gc);
+    Vec8<float>::load(rsh, g.rcoef + g.kout + gc);
+  }
   const int ohw = g.oh * g.ow;
 #pragma unroll
   for (int it = 0; it < (EH + RP - 1) / RP; ++it) {
@@ -197,8 +208,21 @@ __device__ __forceinline__ void epi_chunk(const Geo& g, uint16_t* __restrict__ Y
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = mk[e] > 0.f ? v[e] : 0.f;
       }
+      if (g.rx) {
+        // the stored (rounded) gradient, masked by the BN's forward ReLU recomputed from its
+        // input: what the standalone reduction pass would read back and sum
+        float xv[8];
+        Vec8<T>::load(xv, reinterpret_cast<const T*>(g.rx) + pix * g.kout + gc);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float gq = fmaf(xv[e], rsc[e], rsh[e]) > 0.f ? to_f(from_f<T>(v[e])) : 0.f;
+          v[e] = gq;
+          st1[e] += gq;
+          st2[e] = fmaf(gq, xv[e] - sft[e], st2[e]);
+        }
+      }
       Vec8<T>::store(reinterpret_cast<T*>(Y) + pix * g.kout + gc, v);
-      if (g.stats) {
+      if (g.stats && !g.rx) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float d = v[e] - sft[e];
@@ -1172,13 +1196,14 @@ static int fprop_cfg(const ConvTapArgs& a, int cus) { return plan::conv_fprop_cf
 // wherever it applies unless another configuration is forced
 constexpr int kSpCfg = 21;
 static bool use_sp(const ConvTapArgs& a) {
+  if (a.red_x) return false;  // the BN backward reduction epilogue is the tap kernels' (epi_chunk)
   if (g_forced_cfg == kSpCfg) return conv_sp_supported(a);
   return g_forced_cfg < 0 && conv_sp_default(a);
 }
 
 // the halo-tile kernel (conv3x3_halo.hip) for stride-1 3x3 at C % 64, K % 128 unless another
 // configuration is forced
-static bool use_hfp(const ConvTapArgs& a) { return g_forced_cfg < 0 && conv_hfp_default(a); }
+static bool use_hfp(const ConvTapArgs& a) { return !a.red_x && g_forced_cfg < 0 && conv_hfp_default(a); }
 
 int conv_tap_stats_tiles(const ConvTapArgs& a, int cus) {
   if (use_sp(a)) return conv_sp_grid(a, cus);
@@ -1198,7 +1223,12 @@ void conv_tap_fprop(const ConvTapArgs& a, int cus, hipStream_t s) {
     return;
   }
   const conv::Geo g = conv::make_geo(a);
-  const int cfg = fprop_cfg(a, cus);
+  int cfg = fprop_cfg(a, cus);
+  // the reduction epilogue lives in epi_chunk (fprop / fprop2); the persistent fprop3 writes from
+  // registers: take the fprop2 choice of the shape instead
+  if (a.red_x && cfg >= 14) cfg = plan::conv_fprop_cfg(a, cus, -1);
+  if (a.red_x && (!a.stats || a.stats_shift || a.mask || a.residual || a.relu || a.scale || a.bias))
+    throw std::runtime_error("conv_tap_fprop: the BN backward reduction takes stats only (no other epilogue)");
   dispatch_16(a.dtype, [&](auto tag) {
     using T = typename decltype(tag)::type;
     auto go = [&](auto cfg_tag) {

@@ -49,6 +49,14 @@ struct ConvTapArgs {
   // fp32, finalized by conv1x1_bn_finalize (no separate statistics pass over y)
   float* stats = nullptr;
   const float* stats_shift = nullptr;
+  // optional BN backward reduction instead (data-gradient launches whose output is the gradient of
+  // a BN + ReLU's output; red_x = that BN's input in the output's layout and dtype): the stored
+  // value is masked by red_x * red_coef[k] + red_coef[K + k] > 0 (the forward ReLU recomputed) and
+  // `stats` gets the per-M-tile sums of it and of it * (red_x - red_mean[k]) — the BN's backward
+  // reduction, finalized by conv1x1_bnbwd_finalize (no reduction pass over the gradient)
+  const void* red_x = nullptr;
+  const float* red_coef = nullptr;
+  const float* red_mean = nullptr;
 };
 
 // shape constraints: c % 64 == 0, kout % 64 == 0, 16-byte aligned pointers

@@ -117,6 +117,12 @@ _BN1_DX_PRO = os.environ.get("APEX_AMD_BN1_DX_PRO", "0") == "1"
 # the downsample BN's dx as the downsample dgrad's operand prologue (stages 1-2, where that dgrad
 # is native); 0 = reduction + dx pass + plain dgrad (A/B)
 _DS_DX_PRO = os.environ.get("APEX_AMD_DS_DX_PRO", "1") != "0"
+# bn1's backward reduction in the stride-1 3x3 data gradient's epilogue (conv_igemm.hip epi_chunk,
+# ReLU mask recomputed from y1) instead of a reduction pass over dz1.  Opt-in: the y1 read lands in
+# the per-tile epilogue of the non-persistent tap kernel, where it is exposed, and costs what the
+# pass saves (same-box A/B 12,151-12,185 vs 12,160-12,205 img/s without it,
+# profiles/r06/ab_bn1_red_r06k.txt)
+_BN1_RED = os.environ.get("APEX_AMD_BN1_RED", "0") == "1"
 # the downsample BN's backward reduction accumulated by the block above's dgrad_bnred epilogue
 # (BlockLink.yd: one more operand read there instead of a reduction pass over dm and yd)
 _DS_RED = os.environ.get("APEX_AMD_DS_RED", "1") != "0"
@@ -542,10 +548,20 @@ class _BottleneckFn(torch.autograd.Function):
         if dw3 is None:
             dw3 = conv1x1_wgrad(dx3, y2m, c2, w3)
         # conv2
+        # stride-1 3x3 dgrad on the tap kernels (width > 64: stage 1's 64 -> 64 runs the spatial
+        # kernel, which has no reduction epilogue), a local BN (the group exchange takes the pass)
+        red1 = (_BN1_RED and z1 is not None and stride == 1 and width > 64 and gr1 is None
+                and convops.tap_route(width, w2.size(0), 3, 1, h, wd)[1])
         if z1 is None:  # bn1 folded into the 3x3 conv: its weight gradient recomputes z1 from y1
             gy2 = _nchw(dy2, n, oh, ow)
             dz1 = convops.conv_tap_dgrad(gy2, w2, (n, width, h, wd), 1, 1)
             dw2 = convops.conv_tap_wgrad(gy2, _nchw(y1, n, h, wd), w2.shape, 1, 1, w2.dtype, xcoef=c1)
+        elif red1:
+            # bn1's backward reduction in the 3x3 dgrad's epilogue (ReLU mask recomputed from y1):
+            # dz1 comes out masked with its [2, tiles, width] sums, no reduction pass over it
+            gy2 = _nchw(dy2, n, oh, ow)
+            dz1, part1 = convops.conv_tap_dgrad(gy2, w2, (n, width, h, wd), 1, 1, red=(_nchw(y1, n, h, wd), c1, sm1))
+            dw2 = _conv_bwd(gy2, _nchw(z1, n, h, wd), w2, stride, 1, need_x=False)[1]
         else:
             dz1, dw2 = _conv_bwd(_nchw(dy2, n, oh, ow), _nchw(z1, n, h, wd), w2, stride, 1)
         dz1 = _m2(dz1.contiguous(memory_format=torch.channels_last))
@@ -554,8 +570,12 @@ class _BottleneckFn(torch.autograd.Function):
         # for the weight gradient — one [M, width] pass fewer than reduction + dx + dgrad reading
         # dy1); bwd_full where conv1's dgrad is not native or the BN is synchronized, and at width
         # 512 (stage 4: the 5 coefficient rows next to the 128 x 512 weight image exceed the LDS)
-        bn1_pro = _BN1_DX_PRO and gr1 is None and width <= 256 and _dgrad_native(dz1.size(0), width, cin)
-        if bn1_pro:
+        bn1_pro = (_BN1_DX_PRO and not red1 and gr1 is None and width <= 256
+                   and _dgrad_native(dz1.size(0), width, cin))
+        if red1:  # dz1 is already masked: bn1's coefficients from the epilogue partials, then its dx
+            cb1, gg1, gb1 = bwd_from_part(part1, float(dz1.size(0)), sm1, si1, g1, gr1, in1)
+            dy1 = bn.bwd_apply(dz1, y1, c1, cb1)
+        elif bn1_pro:
             pc1, gg1, gb1 = bn.bwd_coef(dz1, y1, g1, sm1, si1, c1)
             pc1 = pc1.view(-1)
         else:

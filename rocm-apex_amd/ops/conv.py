@@ -128,6 +128,9 @@ class Conv1x1NHWC(nn.Conv2d):
 # Implicit-GEMM convolutions (csrc/conv/conv_igemm.hip): 3x3 stride 1/2 and strided 1x1, NHWC.
 # ------------------------------------------------------------------------------------------------
 _TAP_ENABLED = os.environ.get("APEX_AMD_CONV_IGEMM", "1") != "0"
+# the stride-2 3x3 data gradient at <= 128 channels (ResNet-50 stage 2's first block) on the native
+# per-phase tap kernels instead of MIOpen (A/B knob)
+_S2_DGRAD_128 = os.environ.get("APEX_AMD_S2_DGRAD_128", "0") == "1"
 # the halo-tile 3x3 weight gradient (csrc/conv/conv3x3_wgrad.hip); 0 = the r04 routes (A/B)
 _HALO_WGRAD = os.environ.get("APEX_AMD_HALO_WGRAD", "1") != "0"
 
@@ -265,10 +268,13 @@ def conv_bn_act(x, w, scale, bias, residual=None, relu=True, stride=1, padding=0
         return _conv_bn_act_reference(x, w, scale.detach(), bias.detach(), residual, relu, stride, padding)
 
 
-def conv_tap_dgrad(gy, w, x_shape, stride, pad, mask=None):
+def conv_tap_dgrad(gy, w, x_shape, stride, pad, mask=None, red=None):
     """Data gradient through the native tap kernel.  ``mask`` (optional, the layer input's producer
     ReLU output, same shape as dx): dx *= (mask > 0) in the kernel's epilogue — the previous
-    stage's dReLU fused into this dconv."""
+    stage's dReLU fused into this dconv.  ``red = (x, coef, mean)`` (stride 1): dx is the gradient
+    of relu(bn(x)) with forward coefficients ``coef`` [2C] and batch mean ``mean``; the epilogue
+    masks it with that ReLU (recomputed) and returns ``(dx, part)``, part = [2, tiles, C] partials
+    of sum(dx) and sum(dx * (x - mean)) — the BN's backward reduction, no pass over dx."""
     n, c, h, wd = x_shape
     kout, _, k, _ = w.shape
     ext = _conv_ext()
@@ -279,6 +285,9 @@ def conv_tap_dgrad(gy, w, x_shape, stride, pad, mask=None):
     wk = w.permute(1, 2, 3, 0)  # [C, R, S, K] view
     native_w = (hasattr(ext, "tap_weights") and w.is_contiguous(memory_format=torch.channels_last)
                 and kout % 8 == 0 and c % 8 == 0)
+    if red is not None and len(phases) != 1:
+        raise ValueError("conv_tap_dgrad: the BN reduction epilogue takes a single-phase (stride 1) dgrad")
+    part = None
     for ph, pw, oh, ow, taps in phases:
         if not taps or oh <= 0 or ow <= 0:
             continue
@@ -288,9 +297,15 @@ def conv_tap_dgrad(gy, w, x_shape, stride, pad, mask=None):
             wt = wk.reshape(c, k * k, kout).contiguous()  # [C, taps, K]
         else:
             wt = torch.stack([wk[:, r, s_, :] for r, s_, _, _ in taps], 1).contiguous()
+        if red is not None:
+            rx, rcoef, rmean = red
+            part = ext.tap_fprop(_nhwc(gy), wt, _nhwc(dx), oh, ow, 1, 1, stride, stride, ph, pw,
+                                 [t[2] for t in taps], [t[3] for t in taps], red_x=_nhwc(rx), red_coef=rcoef,
+                                 red_mean=rmean)
+            continue
         ext.tap_fprop(_nhwc(gy), wt, _nhwc(dx), oh, ow, 1, 1, stride, stride, ph, pw,
                       [t[2] for t in taps], [t[3] for t in taps], mask=None if mask is None else _nhwc(mask))
-    return dx
+    return dx if red is None else (dx, part)
 
 
 def conv_tap_wgrad(gy, x, w_shape, stride, pad, out_dtype, xcoef=None):
@@ -333,7 +348,7 @@ def tap_route(cin, cout, k, stride, h, w=None):
     if k == 3:
         wg = stride == 1 and (_halo_wgrad(cin, cout, h, h if w is None else w)
                               or (cin == 128 and cout == 128 and h == 28))
-        return True, not (stride == 2 and cout <= 128), wg
+        return True, not (stride == 2 and cout <= 128) or _S2_DGRAD_128, wg
     if k == 1 and stride == 2:
         return False, True, False
     return False, False, False

@@ -219,3 +219,38 @@ def test_gpu_conv_spatial_tile_kernel(n, h, w, dtype):
         _close(dx, xr.grad, 2e-2)
     finally:
         C._conv_ext().force_fprop_cfg(-1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,c,h", [(4, 128, 28), (8, 256, 14), (16, 512, 7), (3, 128, 9)])
+def test_gpu_dgrad_bn_reduction_epilogue(n, c, h):
+    """The stride-1 3x3 data gradient with the producing BN's backward reduction in its epilogue
+    (ops/conv.conv_tap_dgrad ``red``): the stored gradient is bitwise the plain dgrad masked by the
+    BN's ReLU (recomputed from its input), and the partials sum to the float64 reduction of it."""
+    import apex
+    from apex.ops import conv as convops
+
+    torch.manual_seed(c + h)
+    dt = torch.bfloat16
+    gy = torch.randn(n, c, h, h, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(c, c, 3, 3, device="cuda") * 0.05).to(dt).contiguous(memory_format=torch.channels_last)
+    x = torch.randn(n, c, h, h, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
+    coef = torch.cat([torch.rand(c, device="cuda") + 0.5, torch.randn(c, device="cuda") * 0.3])
+    mean = torch.randn(c, device="cuda") * 0.1
+    plain = convops.conv_tap_dgrad(gy, w, x.shape, 1, 1)
+    dz, part = convops.conv_tap_dgrad(gy, w, x.shape, 1, 1, red=(x, coef, mean))
+    mask = (x.float() * coef[:c].view(1, -1, 1, 1) + coef[c:].view(1, -1, 1, 1)) > 0
+    want = torch.where(mask, plain, torch.zeros_like(plain))
+    assert torch.equal(dz, want)
+    g = dz.double().permute(0, 2, 3, 1).reshape(-1, c)
+    xm = x.double().permute(0, 2, 3, 1).reshape(-1, c) - mean.double()
+    assert part.dim() == 3 and part.size(0) == 2 and part.size(2) == c
+    scale = float(g.abs().sum(0).max()) + 1e-6
+    torch.testing.assert_close(part[0].double().sum(0), g.sum(0), atol=1e-5 * scale + 1e-4, rtol=1e-5)
+    torch.testing.assert_close(part[1].double().sum(0), (g * xm).sum(0), atol=1e-5 * float((g * xm).abs().sum(0).max()) + 1e-4,
+                               rtol=1e-5)
+    # the node's finalize consumes it like the standalone reduction's partials
+    ext = apex._native.require("conv").conv
+    istd = torch.rand(c, device="cuda") + 0.5
+    coef_b, gw, gb = ext.bnbwd_finalize(part, float(g.size(0)), mean, istd, None)
+    torch.testing.assert_close(gb.double(), g.sum(0), atol=1e-3 * scale, rtol=1e-4)
