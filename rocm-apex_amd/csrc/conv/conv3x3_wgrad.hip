@@ -30,16 +30,15 @@
 #include "apex_amd/mfma.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 
 namespace apex_amd {
 namespace hwg {
 using namespace mfma;
 
-constexpr int NT = 256;         // 4 waves
 constexpr int NS = 7;           // 16-pixel reduction slices per tile
 constexpr int NPP = NS * 16;    // tile pixel capacity
-constexpr int S = 3;            // LDS ring stages
 
 struct Args {
   const uint16_t* x;   // [n][h][w][c]
@@ -54,19 +53,24 @@ struct Args {
   int xbytes, dybytes;
 };
 
-template <int TK, int HSL, int HC_>
+// NW waves: 4 (one per SIMD: 64 output channels, a 3-stage ring) or 8 (two per SIMD sharing each
+// halo tile: 128 output channels, so a staged halo feeds twice the MFMAs; 2-stage ring to fit the
+// LDS; APEX_AMD_HWG_NW=8)
+template <int TK, int HSL, int HC_, int NW_ = 4>
 struct Cfg {
+  static constexpr int NW = NW_, NT = NW * 64;
+  static constexpr int S = NW == 8 ? 2 : 3;            // LDS ring stages
   static constexpr int HC = HC_;                       // halo columns (slots per halo row)
-  static constexpr int KB = 64 * TK;                   // output channels per workgroup
-  static constexpr int DYR = TK == 1 ? 128 : 112;      // dY image rows (DMA count a multiple of 4)
+  static constexpr int KB = 32 * (NW / 2) * TK;        // output channels per workgroup
+  static constexpr int DYR = (TK == 1 || NW == 8) ? 128 : 112;  // dY image rows (DMA count % NW == 0)
   static constexpr int DYI = DYR * KB * 2 / 1024;      // dY DMA instructions per tile
   static constexpr int HI = HSL / 8;                   // halo DMA instructions per tile (8 slots each)
-  static constexpr int DYW = DYI / 4, HW = HI / 4;     // per wave
+  static constexpr int DYW = DYI / NW, HW = HI / NW;   // per wave
   static constexpr int PER = DYW + HW;
   static constexpr int DY_EL = DYR * KB;               // dY image (elements)
   static constexpr int STAGE_EL = DY_EL + HSL * 64;    // one ring stage (elements)
   static constexpr size_t LDS = (size_t)S * STAGE_EL * 2;
-  static_assert(DYI % 4 == 0 && HI % 4 == 0, "DMA instructions must split evenly over the 4 waves");
+  static_assert(DYI % NW == 0 && HI % NW == 0, "DMA instructions must split evenly over the waves");
   static_assert(DYR >= NPP, "dY image holds the tile");
   static_assert(LDS <= 160 * 1024, "ring exceeds the 160 KiB LDS");
 };
@@ -100,10 +104,11 @@ __device__ __forceinline__ s16x8 frag2(const uint16_t* lo, const uint16_t* hi) {
   return s16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
-template <typename T, int TK, int HSL, int HC, bool PRO>
-__global__ void __launch_bounds__(NT, 1) wgrad_kernel(const Args p) {
-  using C = Cfg<TK, HSL, HC>;
-  constexpr int KB = C::KB;
+template <typename T, int TK, int HSL, int HC, bool PRO, int NW = 4>
+__global__ void __launch_bounds__(NW * 64, 1) wgrad_kernel(const Args p) {
+  using C = Cfg<TK, HSL, HC, NW>;
+  constexpr int KB = C::KB, S = C::S;
+  static_assert(!(PRO && S < 3), "the BN prologue rewrites the next tile's halo under the current MFMAs: 3 stages");
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, lr = lane & 31, lh = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -126,9 +131,9 @@ __global__ void __launch_bounds__(NT, 1) wgrad_kernel(const Args p) {
   uint32_t dyrel[C::DYW];
 #pragma unroll
   for (int i = 0; i < C::DYW; ++i) {
-    const int j = i * 4 + wave;
+    const int j = i * NW + wave;
     int row, sc;
-    if constexpr (TK == 1) {
+    if constexpr (KB == 64) {
       row = 8 * j + (lane >> 3);
       sc = (lane & 7) ^ (swz<64>(row) << 2);
     } else {
@@ -143,7 +148,7 @@ __global__ void __launch_bounds__(NT, 1) wgrad_kernel(const Args p) {
   const int hblk = p.HR * HC;
 #pragma unroll
   for (int i = 0; i < C::HW; ++i) {
-    const int j = i * 4 + wave;
+    const int j = i * NW + wave;
     const int slot = 8 * j + (lane >> 3);
     const int sc = (lane & 7) ^ (swz<64>(slot) << 2);
     const int gi = slot / hblk, rem = slot - gi * hblk;
@@ -171,7 +176,7 @@ __global__ void __launch_bounds__(NT, 1) wgrad_kernel(const Args p) {
     }
 #pragma unroll
     for (int i = 0; i < C::HW; ++i)
-      if (swz<64>(8 * (i * 4 + wave) + (lane >> 3))) hsw |= 1u << i;
+      if (swz<64>(8 * (i * NW + wave) + (lane >> 3))) hsw |= 1u << i;
   }
 
   auto issue = [&](int t, int stage) -> uint32_t {
@@ -183,7 +188,7 @@ __global__ void __launch_bounds__(NT, 1) wgrad_kernel(const Args p) {
 #pragma unroll
     for (int i = 0; i < C::DYW; ++i) {
       const uint32_t voff = dyrow[i] < p.np ? dyo + dyrel[i] : 0x80000000u;
-      bdma16(dr, voff, base + (i * 4 + wave) * 512);
+      bdma16(dr, voff, base + (i * NW + wave) * 512);
     }
     const int xo = px0 * p.c * 2;
     uint32_t vm = 0;  // bit i: halo chunk i of this lane holds image data (PRO rewrites it)
@@ -192,14 +197,14 @@ __global__ void __launch_bounds__(NT, 1) wgrad_kernel(const Args p) {
       const bool valid = (hfl[i] & 1u) && !(hfl[i] & kill);
       vm |= valid ? 1u << i : 0u;
       const uint32_t voff = valid ? (uint32_t)(xo + hrel[i]) : 0x80000000u;
-      bdma16(xr, voff, base + C::DY_EL + (i * 4 + wave) * 512);
+      bdma16(xr, voff, base + C::DY_EL + (i * NW + wave) * 512);
     }
     return vm;
   };
   auto xform = [&](int stage, uint32_t vm, int i) {
     if constexpr (PRO) {
       if (!((vm >> i) & 1u)) return;
-      uint16_t* q = lds + stage * C::STAGE_EL + C::DY_EL + (i * 4 + wave) * 512 + lane * 8;
+      uint16_t* q = lds + stage * C::STAGE_EL + C::DY_EL + (i * NW + wave) * 512 + lane * 8;
       const int gsel = (hsw >> i) & 1u;
       float v[8];
       Vec8<T>::load(v, reinterpret_cast<const T*>(q));
@@ -360,8 +365,20 @@ constexpr Inst kInst[] = {{1, 224, 12}, {1, 256, 16}, {1, 256, 32}, {1, 256, 60}
 
 struct Plan {
   bool ok;
-  int tk, hsl, R, G, HR, HC, hs, np, tpi, ntiles, splits, nblk_c;
+  int tk, hsl, R, G, HR, HC, hs, np, tpi, ntiles, splits, nblk_c, nw;
 };
+
+// 8-wave workgroups (128 output channels per staged halo: two waves per SIMD, half the halo
+// staging per MFMA) wherever kout % 128 == 0 and no prologue: 92 -> 80 us at 7x7 / 14x14, 82.5 ->
+// 74.5 us at 28x28 in the step (profiles/r06/resnet50_step_timeline_r06m.md), whole step +0.15 %
+// same box (profiles/r06/ab_hwg_nw8_r06l.txt).  APEX_AMD_HWG_NW=4 restores the 4-wave kernel.
+inline int env_nw() {
+  static const int v = [] {
+    const char* e = std::getenv("APEX_AMD_HWG_NW");
+    return e && std::atoi(e) == 4 ? 4 : 8;
+  }();
+  return v;
+}
 
 // tile geometry for halo width hc and slot budget hsl: rows of one image (the largest divisor of
 // h whose pixels and halo fit) or, for small images, as many whole images as fit
@@ -383,14 +400,16 @@ inline bool tile_geo(int h, int w, int hc, int hsl, int& R, int& G) {
   return false;
 }
 
-inline Plan make_plan(const ConvTapArgs& a, int cus) {
+inline Plan make_plan(const ConvTapArgs& a, int cus, bool pro = false) {
   Plan pl{};
   pl.ok = false;
   const int h = a.oh, w = a.ow;
   if (w < 1 || h < 1) return pl;
+  pl.nw = (!pro && a.kout % 128 == 0) ? env_nw() : 4;
   double best = -1.0;
-  for (const Inst& in : kInst) {
+  for (Inst in : kInst) {
     if (in.tk == 2 && a.kout % 128) continue;
+    if (pl.nw == 8) in.hsl = 256;  // (the 8-wave DMA split needs halo pieces % 8)
     int R, G;
     if (!tile_geo(h, w, in.hc, in.hsl, R, G)) continue;
     // pixel-slot efficiency, with a 10 % bonus for the 128-channel block (half the halo re-reads)
@@ -411,7 +430,7 @@ inline Plan make_plan(const ConvTapArgs& a, int cus) {
   pl.tpi = pl.G > 1 ? 1 : h / pl.R;
   pl.ntiles = pl.G > 1 ? (a.n + pl.G - 1) / pl.G : a.n * pl.tpi;
   pl.nblk_c = a.c / 64;
-  const int nblk = (a.kout / (64 * pl.tk)) * pl.nblk_c;
+  const int nblk = (a.kout / (32 * (pl.nw / 2) * pl.tk)) * pl.nblk_c;
   int sp = std::max(1, cus / nblk);
   sp = std::min(sp, pl.ntiles);
   pl.splits = sp;
@@ -437,7 +456,11 @@ bool conv_hwgrad_supported(const ConvTapArgs& a) {
 }
 
 int64_t conv_hwgrad_workspace_floats(const ConvTapArgs& a, int cus) {
+  // (the prologue form always plans 4 waves; the plain form may plan 8 with fewer splits: size for
+  // the larger of the two so one workspace serves either)
   const hwg::Plan pl = hwg::make_plan(a, cus);
+  const hwg::Plan p4 = hwg::make_plan(a, cus, true);
+  if (p4.splits > pl.splits) return (int64_t)p4.splits * a.kout * 9 * a.c;
   return (int64_t)pl.splits * a.kout * 9 * a.c;
 }
 
@@ -450,7 +473,7 @@ void conv_hwgrad_pro(const ConvTapArgs& a, const void* dy, void* dw_out, int out
                      hipStream_t s, const float* xcoef) {
   if (!conv_hwgrad_supported(a) || ((uintptr_t)dy & 15) || ((uintptr_t)dw_out & 15) || ((uintptr_t)ws & 15))
     throw std::runtime_error("conv_hwgrad: unsupported shape / dtype / alignment");
-  const hwg::Plan pl = hwg::make_plan(a, cus);
+  const hwg::Plan pl = hwg::make_plan(a, cus, xcoef != nullptr);
   hwg::Args p;
   p.x = static_cast<const uint16_t*>(a.in);
   p.dy = static_cast<const uint16_t*>(dy);
@@ -471,7 +494,7 @@ void conv_hwgrad_pro(const ConvTapArgs& a, const void* dy, void* dw_out, int out
   p.nblk_c = pl.nblk_c;
   p.xbytes = (int)((int64_t)a.n * a.ih * a.iw * a.c * 2);
   p.dybytes = (int)((int64_t)a.n * a.oh * a.ow * a.kout * 2);
-  const int nblk = (a.kout / (64 * pl.tk)) * pl.nblk_c;
+  const int nblk = (a.kout / (32 * (pl.nw / 2) * pl.tk)) * pl.nblk_c;
   const unsigned grid = (unsigned)(nblk * pl.splits);
   dispatch_16(a.dtype, [&](auto tag) {
     using T = typename decltype(tag)::type;
@@ -494,13 +517,17 @@ void conv_hwgrad_pro(const ConvTapArgs& a, const void* dy, void* dw_out, int out
         }
       }
       if (!seen) (void)hipFuncSetAttribute(fp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(hwg::NT), lds, s, p);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(pl.nw * 64), lds, s, p);
     };
-#define HWG_CASE(TK_, HSL_, HC_)                                                          \
-  if (pl.tk == TK_ && pl.hsl == HSL_ && pl.HC == HC_) {                                   \
-    if (xcoef) go(hwg::wgrad_kernel<T, TK_, HSL_, HC_, true>, hwg::Cfg<TK_, HSL_, HC_>::LDS); \
-    else go(hwg::wgrad_kernel<T, TK_, HSL_, HC_, false>, hwg::Cfg<TK_, HSL_, HC_>::LDS);      \
-    return;                                                                               \
+#define HWG_CASE(TK_, HSL_, HC_)                                                                    \
+  if (pl.nw == 4 && pl.tk == TK_ && pl.hsl == HSL_ && pl.HC == HC_) {                               \
+    if (xcoef) go(hwg::wgrad_kernel<T, TK_, HSL_, HC_, true>, hwg::Cfg<TK_, HSL_, HC_>::LDS);           \
+    else go(hwg::wgrad_kernel<T, TK_, HSL_, HC_, false>, hwg::Cfg<TK_, HSL_, HC_>::LDS);                \
+    return;                                                                                         \
+  }                                                                                                 \
+  if (pl.nw == 8 && !xcoef && pl.tk == TK_ && pl.hsl == 256 && pl.HC == HC_) {                        \
+    go(hwg::wgrad_kernel<T, TK_, 256, HC_, false, 8>, hwg::Cfg<TK_, 256, HC_, 8>::LDS);                \
+    return;                                                                                         \
   }
     HWG_CASE(1, 224, 12) HWG_CASE(1, 256, 16) HWG_CASE(1, 256, 32) HWG_CASE(1, 256, 60)
 #undef HWG_CASE

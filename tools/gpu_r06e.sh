@@ -13,4 +13,4 @@ db=$(find $R/gpurun_out/prof_tl_$TAG -name '*results.db' | head -1)
 python3 tools/prof_timeline.py "$db" --after spin_kernel --steps 10 --step 5 --md $O/timeline.md || exit 1
 python3 tools/prof_summary.py "$db" --after spin_kernel --steps 10 --top 100 --md $O/resnet_prof.md > /dev/null || exit 1
 rm -rf $R/gpurun_out/prof_tl_$TAG
-grep -n "ks<" $O/timeline.md | cut -c1-200 | head -40
+head -12 $O/resnet_prof.md
