@@ -161,21 +161,47 @@ __global__ void __launch_bounds__(NW * 64, (NW == 8 || one_wg_per_cu(NC, KR, PRO
       }
     }
   }
+  // coefficient rows: 16-byte loads (4 consecutive k of one row; KR % 4 == 0, rows start 16-byte
+  // aligned when the tensors are), all of a thread's loads issued before its LDS stores
+  const bool pc_vec = ((reinterpret_cast<uintptr_t>(p.pcoef) | reinterpret_cast<uintptr_t>(p.pc_res)) & 15) == 0;
   if constexpr (PRO == kProBnAddRelu) {
     if (p.pc_split) {
-      for (int i = tid; i < 4 * KR; i += NT) {
-        const int row = i / KR, kk = i - row * KR;
-        float v;
-        if (row == 0 || row == 2) v = p.pcoef[(row >> 1) * KR + kk];
-        else if (p.pc_res) v = p.pc_res[(row >> 1) * KR + kk];
-        else v = row == 1 ? 1.f : 0.f;
-        pc[i] = v;
+      if (pc_vec) {
+        constexpr int N4 = KR;  // 4 rows x KR / 4 vectors
+#pragma unroll 4
+        for (int i = tid; i < N4; i += NT) {
+          const int row = i / (KR / 4), kk = (i - row * (KR / 4)) * 4;
+          float4 v;
+          if (row == 0 || row == 2) v = *reinterpret_cast<const float4*>(p.pcoef + (row >> 1) * KR + kk);
+          else if (p.pc_res) v = *reinterpret_cast<const float4*>(p.pc_res + (row >> 1) * KR + kk);
+          else v = row == 1 ? make_float4(1.f, 1.f, 1.f, 1.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+          *reinterpret_cast<float4*>(pc + row * KR + kk) = v;
+        }
+      } else {
+        for (int i = tid; i < 4 * KR; i += NT) {
+          const int row = i / KR, kk = i - row * KR;
+          float v;
+          if (row == 0 || row == 2) v = p.pcoef[(row >> 1) * KR + kk];
+          else if (p.pc_res) v = p.pc_res[(row >> 1) * KR + kk];
+          else v = row == 1 ? 1.f : 0.f;
+          pc[i] = v;
+        }
       }
+    } else if (pc_vec) {
+#pragma unroll 4
+      for (int i = tid; i < KR; i += NT)
+        reinterpret_cast<float4*>(pc)[i] = reinterpret_cast<const float4*>(p.pcoef)[i];
     } else {
       for (int i = tid; i < 4 * KR; i += NT) pc[i] = p.pcoef[i];
     }
   } else if constexpr (PRO != kProNone) {
-    for (int i = tid; i < pro_rows(PRO) * KR; i += NT) pc[i] = p.pcoef[i];
+    if (pc_vec) {
+#pragma unroll 4
+      for (int i = tid; i < pro_rows(PRO) * KR / 4; i += NT)
+        reinterpret_cast<float4*>(pc)[i] = reinterpret_cast<const float4*>(p.pcoef)[i];
+    } else {
+      for (int i = tid; i < pro_rows(PRO) * KR; i += NT) pc[i] = p.pcoef[i];
+    }
   }
   float sh[CN], s1[CN], s2[CN];
 #pragma unroll
@@ -483,27 +509,41 @@ __global__ void __launch_bounds__(NW * 64, (NW == 8 || one_wg_per_cu(NC, KR, PRO
     }
   } else if constexpr (DEPTH >= 4) {
     // deeper ring for the one-workgroup-per-CU shapes (a 4-wave CU needs more bytes in flight
-    // per wave): f[j] is consumed at step j of the unrolled rotation and refilled with the
-    // position DEPTH - 1 ahead; every index is a compile-time constant after the unroll
-    Frags f[DEPTH];
+    // per wave).  Named register sets rotated by an explicit unrolled body: an array of them
+    // indexed by the rotation (even with constant indices after the unroll) was left in scratch
+    // at DEPTH 4 (592 B per lane, profiles/r06/scratch_census_r06s.md)
+    static_assert(DEPTH <= 5, "ring depth");
+    Frags f0, f1, f2, f3, f4;  // f4: DEPTH 5 only
     int tn = t, cn = ch;
-#pragma unroll
-    for (int j = 0; j < DEPTH - 1; ++j) {
-      load(f[j], min(tn, tlast), cn);
+    auto pre = [&](Frags& f) {
+      load(f, min(tn, tlast), cn);
       adv(tn, cn);
-    }
+    };
+    pre(f0);
+    pre(f1);
+    pre(f2);
+    if constexpr (DEPTH == 5) pre(f3);
     bool done = false;
+    auto step = [&](Frags& nxt, const Frags& cur) {
+      if (done) return;
+      pre(nxt);
+      compute(cur, t, ch);
+      if (ch == NCH - 1) epilogue(t);
+      adv(t, ch);
+      done = t >= p.ntiles;
+    };
     while (!done) {
-#pragma unroll
-      for (int j = 0; j < DEPTH; ++j) {
-        if (!done) {
-          load(f[(j + DEPTH - 1) % DEPTH], min(tn, tlast), cn);
-          adv(tn, cn);
-          compute(f[j], t, ch);
-          if (ch == NCH - 1) epilogue(t);
-          adv(t, ch);
-          done = t >= p.ntiles;
-        }
+      if constexpr (DEPTH == 4) {
+        step(f3, f0);
+        step(f0, f1);
+        step(f1, f2);
+        step(f2, f3);
+      } else {
+        step(f4, f0);
+        step(f0, f1);
+        step(f1, f2);
+        step(f2, f3);
+        step(f3, f4);
       }
     }
   } else {

@@ -72,9 +72,9 @@ constexpr int KCH = 64;        // reduction depth of one weight chunk
 constexpr int WS = 3;
 constexpr int slot_el(int nc) { return nc * KCH; }
 
-inline size_t lds_bytes(int nc, int pro, bool red, int k) {
-  return (size_t)WS * slot_el(nc) * 2 + (size_t)NW * 32 * kSS * 2 + (size_t)pro_rows(pro) * k * 4 +
-         (red ? (size_t)NW * 2 * nc * 4 : 0);
+// (RED: the per-wave backward sums stay in registers and meet in the weight ring after the loop)
+inline size_t lds_bytes(int nc, int pro, int k) {
+  return (size_t)WS * slot_el(nc) * 2 + (size_t)NW * 32 * kSS * 2 + (size_t)pro_rows(pro) * k * 4;
 }
 
 __device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint16_t* lds_dst) {
@@ -102,12 +102,13 @@ __global__ void __launch_bounds__(NT, 1) fused1x1_ks(Args p) {
   constexpr int PW = NC * KCH * 2 / 1024 / NW;  // 1-KB DMA pieces per wave per chunk
   constexpr int LA = pro_two(PRO) ? 2 * KC : KC;  // operand loads per wave per chunk
   static_assert(PW >= 1 && NC * KCH * 2 == PW * NW * 1024, "weight chunk must split into whole pieces per wave");
-  static_assert(DEPTH >= 3, "the counted DMA wait assumes two chunks of operand loads behind each piece");
+  // (the counted DMA wait below holds for any DEPTH: the DMA runs two chunks ahead of its use and
+  // every step issues PW pieces + LA operand loads)
+  static_assert(DEPTH >= 2, "operand fragments at least one step ahead");
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   uint16_t* bimg = lds;                                            // [WS][SLOT]
   uint16_t* stg = lds + WS * SLOT;                                 // [NW][32][kSS]
   float* pc = reinterpret_cast<float*>(stg + NW * 32 * kSS);       // [rows][K]
-  float* rsum = pc + pro_rows(PRO) * p.k;                          // RED: [NW][2][NC]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, lr = lane & 31, lh = lane >> 5;
   const int col0 = blockIdx.y * NC;
@@ -136,8 +137,21 @@ __global__ void __launch_bounds__(NT, 1) fused1x1_ks(Args p) {
 #pragma unroll
     for (int i = 0; i < PW; ++i) bdma16(wr, wrel[i] + cofs, bimg + slot * SLOT + (wave + NW * i) * 512);
   };
+  // coefficient rows by 16-byte loads (K % 64 == 0; the rows start 16-byte aligned when the
+  // tensors do), several in flight per thread
+  const bool pc_vec = ((reinterpret_cast<uintptr_t>(p.pcoef) | reinterpret_cast<uintptr_t>(p.pc_res)) & 15) == 0;
   if constexpr (PRO == kProBnAddRelu) {
-    if (p.pc_split) {
+    if (p.pc_split && pc_vec) {
+#pragma unroll 4
+      for (int i = tid; i < K; i += NT) {  // 4 rows x K / 4 vectors
+        const int row = i / (K / 4), kk = (i - row * (K / 4)) * 4;
+        float4 v;
+        if (row == 0 || row == 2) v = *reinterpret_cast<const float4*>(p.pcoef + (row >> 1) * K + kk);
+        else if (p.pc_res) v = *reinterpret_cast<const float4*>(p.pc_res + (row >> 1) * K + kk);
+        else v = row == 1 ? make_float4(1.f, 1.f, 1.f, 1.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(pc + row * K + kk) = v;
+      }
+    } else if (p.pc_split) {
       for (int i = tid; i < 4 * K; i += NT) {
         const int row = i / K, kk = i - row * K;
         float v;
@@ -146,15 +160,23 @@ __global__ void __launch_bounds__(NT, 1) fused1x1_ks(Args p) {
         else v = row == 1 ? 1.f : 0.f;
         pc[i] = v;
       }
+    } else if (pc_vec) {
+#pragma unroll 4
+      for (int i = tid; i < K; i += NT) reinterpret_cast<float4*>(pc)[i] = reinterpret_cast<const float4*>(p.pcoef)[i];
     } else {
       for (int i = tid; i < 4 * K; i += NT) pc[i] = p.pcoef[i];
     }
   } else if constexpr (PRO != kProNone) {
-    for (int i = tid; i < pro_rows(PRO) * K; i += NT) pc[i] = p.pcoef[i];
+    if (pc_vec) {
+#pragma unroll 4
+      for (int i = tid; i < pro_rows(PRO) * K / 4; i += NT)
+        reinterpret_cast<float4*>(pc)[i] = reinterpret_cast<const float4*>(p.pcoef)[i];
+    } else {
+      for (int i = tid; i < pro_rows(PRO) * K; i += NT) pc[i] = p.pcoef[i];
+    }
   }
-  if constexpr (RED)
-    for (int i = tid; i < NW * 2 * NC; i += NT) rsum[i] = 0.f;
   float sh[CN], s1[CN], s2[CN];
+  float racc[RED ? CN / 2 : 1][2] = {};  // RED: this lane's column of each 64-column group (see epilogue)
 #pragma unroll
   for (int cb = 0; cb < CN; ++cb) {
     sh[cb] = (STATS && p.shift) ? p.shift[col0 + 32 * cb + lr] : 0.f;
@@ -334,10 +356,8 @@ __global__ void __launch_bounds__(NT, 1) fused1x1_ks(Args p) {
             rq[j] = (up ? rq[j + half] : rq[j]) + gq;
           }
         }
-        const int jc = ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1);
-        float* r0p = rsum + (wid * 2) * NC + 64 * g + (lane & 7) * 8 + jc;
-        r0p[0] += rs[0];
-        r0p[NC] += rq[0];
+        racc[g][0] += rs[0];
+        racc[g][1] += rq[0];
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
@@ -393,6 +413,16 @@ __global__ void __launch_bounds__(NT, 1) fused1x1_ks(Args p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup's LDS is released
 
   if constexpr (RED) {
+    // per-wave sums [NW][2][NC] into the (now idle) weight ring, then a fixed-order wave reduction
+    float* rsum = reinterpret_cast<float*>(bimg);
+    __syncthreads();
+    const int jc = ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1);
+#pragma unroll
+    for (int g = 0; g < CN / 2; ++g) {
+      float* r0p = rsum + (wid * 2) * NC + 64 * g + (lane & 7) * 8 + jc;
+      r0p[0] = racc[g][0];
+      r0p[NC] = racc[g][1];
+    }
     __syncthreads();
     for (int i = tid; i < 2 * NC; i += NT) {
       const int which = i / NC, n = i % NC;
@@ -442,7 +472,7 @@ inline int env_nc() {
 inline int col_tile(int64_t m, int ncols, int cus, int pro) {
   const int f = env_nc();
   if (f == 64 || f == 128 || f == 256) {
-    if (ncols % f == 0 && !(f == 256 && pro_two(pro))) return f;
+    if (ncols % f == 0) return f;
   }
   const int64_t ntiles = (m + ROWS - 1) / ROWS;
   for (int nc : {256, 128, 64}) {
@@ -463,8 +493,10 @@ inline int grid_x(int64_t m, int nc, int ncols, int cus) {
 
 template <typename T, int NC, bool WT, int PRO, bool STATS, bool RED>
 void launch(const Args& a0, int cus, hipStream_t s) {
-  constexpr int DEPTH = 3;  // two chunks of operands in flight per wave
-  const size_t lds = lds_bytes(NC, PRO, RED, a0.k);
+  // operand fragments in flight per wave: two chunks ahead, one beside 256 columns with a two-operand
+  // prologue (the register file holds 8 accumulator blocks + one chunk of both operands)
+  constexpr int DEPTH = (NC == 256 && pro_two(PRO)) ? 2 : 3;
+  const size_t lds = lds_bytes(NC, PRO, a0.k);
   if (lds > 160 * 1024) throw std::runtime_error("conv1x1_ks: LDS budget exceeded (reduction too deep for the prologue)");
   auto kern = &fused1x1_ks<T, NC, WT, PRO, STATS, RED, DEPTH>;
   static size_t attr = 0;
@@ -481,9 +513,7 @@ void launch(const Args& a0, int cus, hipStream_t s) {
 
 template <typename T, bool WT, int PRO, bool STATS, bool RED>
 void dispatch_nc(const Args& a, int nc, int cus, hipStream_t s) {
-  if constexpr (!pro_two(PRO)) {  // (a two-operand prologue beside 256 columns would spill: col_tile)
-    if (nc == 256) return launch<T, 256, WT, PRO, STATS, RED>(a, cus, s);
-  }
+  if (nc == 256) return launch<T, 256, WT, PRO, STATS, RED>(a, cus, s);
   if (nc == 128) launch<T, 128, WT, PRO, STATS, RED>(a, cus, s);
   else launch<T, 64, WT, PRO, STATS, RED>(a, cus, s);
 }

@@ -139,7 +139,9 @@ __global__ void __launch_bounds__(512, 1) fused_kernel(const Args p) {
 #pragma unroll
       for (int i = 0; i < C::NY; ++i) {
         const int lr = yr + (256 / (W / 8)) * i;
-        *reinterpret_cast<uint4*>(y2b(b) + lr * C::YS + yc) = ry2[set][i];
+        // component-wise (the aggregate copy kept ry2 in a scratch alloca)
+        const uint32_t v0 = ry2[set][i].x, v1 = ry2[set][i].y, v2 = ry2[set][i].z, v3 = ry2[set][i].w;
+        *reinterpret_cast<uint4*>(y2b(b) + lr * C::YS + yc) = make_uint4(v0, v1, v2, v3);
       }
     };
     // loads are issued unconditionally (past the end: the last tile again, discarded) and the
@@ -220,20 +222,23 @@ __global__ void __launch_bounds__(512, 1) fused_kernel(const Args p) {
       const int lm = 32 * mh + pl;
       const int64_t row = (int64_t)t * TM + lm;
       if (row < p.m) {
-        float y[16];
-        Vec8<T>::load(*reinterpret_cast<float(*)[8]>(&y[0]), reinterpret_cast<const T*>(yy + lm * C::YS + c0));
-        Vec8<T>::load(*reinterpret_cast<float(*)[8]>(&y[8]), reinterpret_cast<const T*>(yy + lm * C::YS + c0 + 8));
-        float g[16];
+        // two separate 8-element arrays: pointer casts into one 16-element array kept it (and the
+        // gradient row) in scratch, 80 B per lane (profiles/r06/scratch_census_r06s.md)
+        float ylo[8], yhi[8], glo[8], ghi[8];
+        Vec8<T>::load(ylo, reinterpret_cast<const T*>(yy + lm * C::YS + c0));
+        Vec8<T>::load(yhi, reinterpret_cast<const T*>(yy + lm * C::YS + c0 + 8));
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float gq = fmaf(y[r], ec[c0 + r], ec[W + c0 + r]) > 0.f ? to_f(from_f<T>(acc[r])) : 0.f;
-          g[r] = gq;
+          const float yv = r < 8 ? ylo[r & 7] : yhi[r & 7];
+          const float gq = fmaf(yv, ec[c0 + r], ec[W + c0 + r]) > 0.f ? to_f(from_f<T>(acc[r])) : 0.f;
+          if (r < 8) glo[r & 7] = gq;
+          else ghi[r & 7] = gq;
           s1[r] += gq;
-          s2[r] = fmaf(gq, y[r] - ec[2 * W + c0 + r], s2[r]);
+          s2[r] = fmaf(gq, yv - ec[2 * W + c0 + r], s2[r]);
         }
         T* dst = reinterpret_cast<T*>(p.dz2 + row * W + c0);
-        Vec8<T>::store(dst, *reinterpret_cast<float(*)[8]>(&g[0]));
-        Vec8<T>::store(dst + 8, *reinterpret_cast<float(*)[8]>(&g[8]));
+        Vec8<T>::store(dst, glo);
+        Vec8<T>::store(dst + 8, ghi);
       }
     }
     lds_barrier();
