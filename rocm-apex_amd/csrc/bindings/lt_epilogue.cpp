@@ -18,6 +18,7 @@
 #include <hipblaslt/hipblaslt-ext.hpp>
 
 #include <algorithm>
+#include <cstdint>
 #include <cstdlib>
 #include <vector>
 #include <memory>
@@ -137,14 +138,15 @@ std::mutex g_plan_mu;
 // group (apex.fused_dense.sync_lt_plans broadcasts rank 0's picks), so partial sums never come
 // from different kernels on different ranks.
 constexpr int kTop = 8;
-// Timing is limited to problems with every dimension <= APEX_AMD_LT_TUNE_MAX_DIM (default 16384,
-// the transformer dense shapes it was validated on): before the support screen existed, one
-// unscreened candidate at 32768 tokens (and at m = 200704) made hipBLASLt fail to initialise its
-// kernel ("Could not initialize Tensile host") and crash the process (tools/gpu_r04ab.sh).
+// APEX_AMD_LT_TUNE_MAX_DIM=<n> limits timing to problems with every dimension <= n (default: no
+// limit).  Round 4 capped it at 16384: before the support screen existed, one unscreened candidate
+// at 32768 tokens (and at m = 200704) made hipBLASLt fail to initialise its kernel ("Could not
+// initialize Tensile host") and crash the process (tools/gpu_r04ab.sh).  With the screen, the
+// uncapped timing runs every one of those shapes (profiles/r06/lt_probe_uncapped_r06v.log).
 int64_t tune_max_dim() {
   static const int64_t v = [] {
     const char* e = std::getenv("APEX_AMD_LT_TUNE_MAX_DIM");
-    return e ? (int64_t)std::atoll(e) : (int64_t)16384;
+    return e ? (int64_t)std::atoll(e) : INT64_MAX;
   }();
   return v;
 }

@@ -798,8 +798,11 @@ inline int env_int(const char* name, int dflt) {
   const char* e = std::getenv(name);
   return e ? std::atoi(e) : dflt;
 }
+// 256-column tiles only on request (APEX_AMD_C1BN_NC256_MAXK=<max k>): their 128 accumulator
+// registers beside the backward-reduction epilogue spilled (80-120 B / lane); 128-column tiles at
+// k <= 128 measured +0.8 % on the step (profiles/r06/ab_c1bn_nc256_r06u.txt)
 inline int col_tile(int ncols, int kr) {
-  static const int max256 = env_int("APEX_AMD_C1BN_NC256_MAXK", 128);
+  static const int max256 = env_int("APEX_AMD_C1BN_NC256_MAXK", 0);
   static const int max128 = env_int("APEX_AMD_C1BN_NC128_MAXK", 512);
   if (ncols % 256 == 0 && kr <= 256 && kr <= max256) return 256;
   return ncols % 128 == 0 && kr <= max128 ? 128 : 64;
