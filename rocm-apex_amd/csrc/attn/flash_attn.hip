@@ -1127,10 +1127,13 @@ constexpr size_t bwd_lds() {
   return (size_t)(128 * Geo<D>::TSTR + 2 * 32 * Geo<D>::KSTR + 32 * (128 + 8)) * 2 + 2 * 32 * 4;
 }
 
-// query fragments per wave: APEX_ATTN_FWD_QF=1|2 (A/B; default 1)
-inline int fwd_qf() {
+// query fragments per wave: APEX_ATTN_FWD_QF=1|2 forces one; default 2 for the bias (+ dropout)
+// mode at d <= 64 (its 1-fragment form spills 46 VGPRs; BERT-large +1.8 % same box) and 1 otherwise
+// (GPT-2 medium's causal dropout mode: 2 fragments -2 %; profiles/r06/ab_attn_fwd_qf_r06x.txt)
+inline int fwd_qf(const AttnArgs& a, int d) {
   const char* e = std::getenv("APEX_ATTN_FWD_QF");
-  return (e != nullptr && e[0] == '2') ? 2 : 1;
+  if (e != nullptr && (e[0] == '1' || e[0] == '2')) return e[0] - '0';
+  return (a.bias != nullptr && d <= 64) ? 2 : 1;
 }
 
 // occupancy: APEX_ATTN_FWD_OCC=lo (A/B; default the per-shape rule in fwd_occupancy)
@@ -1151,7 +1154,7 @@ void launch_fwd_qf(const AttnArgs& a, hipStream_t s) {
 
 template <typename T, int D>
 void launch_fwd(const AttnArgs& a, hipStream_t s) {
-  if (fwd_qf() == 2) launch_fwd_qf<T, D, 2, false>(a, s);
+  if (fwd_qf(a, D) == 2) launch_fwd_qf<T, D, 2, false>(a, s);
   else if (fwd_lo()) launch_fwd_qf<T, D, 1, true>(a, s);
   else launch_fwd_qf<T, D, 1, false>(a, s);
 }

@@ -144,7 +144,10 @@ struct FCfg {
 // ([EH][BN + 4] floats): fused scale / bias / residual / ReLU / mask, 16-byte row stores.  The
 // consuming BN's statistics of the stored values accumulate in the caller's st1 / st2 (8
 // columns per thread) over all chunks of the tile; stats_fold writes the tile's row.
-template <typename T, int BN, int THREADS, int EH>
+// RED: the BN backward reduction mode (Geo::rx) — a compile-time variant: the runtime branch alone
+// cost the plain epilogue its occupancy (stage-2 F2Cfg<256,64,8,1,2> 97 -> 136 us in the step,
+// profiles/r06/resnet50_step_timeline_r06m.md vs _r06f.md)
+template <typename T, int BN, int THREADS, int EH, bool RED = false>
 __device__ __forceinline__ void epi_chunk(const Geo& g, uint16_t* __restrict__ Y, const float* cs, int row0c,
                                           int col0, int tid, float (&st1)[8], float (&st2)[8]) {
   constexpr int CST = BN + 4;
@@ -162,11 +165,11 @@ __device__ __forceinline__ void epi_chunk(const Geo& g, uint16_t* __restrict__ Y
   if (g.scale) Vec8<float>::load(sc, g.scale + gc);
   if (g.bias) Vec8<float>::load(bi, g.bias + gc);
   const bool affine = g.scale || g.bias;
-  float sft[8], rsc[8], rsh[8];
+  float sft[8], rsc[RED ? 8 : 1], rsh[RED ? 8 : 1];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) sft[e] = rsc[e] = rsh[e] = 0.f;
-  if (g.stats && g.shift) Vec8<float>::load(sft, g.shift + gc);
-  if (g.rx) {  // BN backward reduction: sft = the BN's mean, rsc / rsh its forward apply coefficients
+  for (int e = 0; e < 8; ++e) sft[e] = 0.f;
+  if (g.stats && g.shift && !RED) Vec8<float>::load(sft, g.shift + gc);
+  if constexpr (RED) {  // BN backward reduction: sft = the BN's mean, rsc / rsh its forward apply coefficients
     Vec8<float>::load(sft, g.rmean + gc);
     Vec8<float>::load(rsc, g.rcoef + gc);
     Vec8<float>::load(rsh, g.rcoef + g.kout + gc);
@@ -208,7 +211,7 @@ __device__ __forceinline__ void epi_chunk(const Geo& g, uint16_t* __restrict__ Y
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = mk[e] > 0.f ? v[e] : 0.f;
       }
-      if (g.rx) {
+      if constexpr (RED) {
         // the stored (rounded) gradient, masked by the BN's forward ReLU recomputed from its
         // input: what the standalone reduction pass would read back and sum
         float xv[8];
@@ -222,7 +225,7 @@ __device__ __forceinline__ void epi_chunk(const Geo& g, uint16_t* __restrict__ Y
         }
       }
       Vec8<T>::store(reinterpret_cast<T*>(Y) + pix * g.kout + gc, v);
-      if (g.stats && !g.rx) {
+      if (g.stats && !RED) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float d = v[e] - sft[e];
@@ -263,7 +266,7 @@ __device__ __forceinline__ s16x8 frag_k(const uint16_t* tile, int rowbase, int k
   return *reinterpret_cast<const s16x8*>(tile + row * BK + 8 * c);
 }
 
-template <typename T, typename C>
+template <typename T, typename C, bool RED = false>
 __global__ void __launch_bounds__(C::THREADS, 1)
 fprop_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y, Geo g) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
@@ -400,7 +403,7 @@ fprop_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, ui
         }
     }
     __syncthreads();
-    epi_chunk<T, BN, C::THREADS, 128>(g, Y, cs, row0 + 128 * half, col0, tid, st1, st2);
+    epi_chunk<T, BN, C::THREADS, 128, RED>(g, Y, cs, row0 + 128 * half, col0, tid, st1, st2);
     __syncthreads();
   }
   if (g.stats) stats_fold<BN, C::THREADS>(g, cs, bm, (g.m + BMT - 1) / BMT, col0, tid, st1, st2);
@@ -437,7 +440,7 @@ __device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, 
                                            0);
 }
 
-template <typename T, typename C>
+template <typename T, typename C, bool RED = false>
 __global__ void __launch_bounds__(C::THREADS, 1)
 fprop2_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y, Geo g) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
@@ -566,7 +569,7 @@ fprop2_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, u
         }
     }
     __syncthreads();
-    epi_chunk<T, BN, C::THREADS, 128>(g, Y, cs, row0 + 128 * half, col0, tid, st1, st2);
+    epi_chunk<T, BN, C::THREADS, 128, RED>(g, Y, cs, row0 + 128 * half, col0, tid, st1, st2);
     __syncthreads();
   }
   if (g.stats) stats_fold<BN, C::THREADS>(g, cs, bm, (g.m + BMT - 1) / BMT, col0, tid, st1, st2);
@@ -1235,15 +1238,23 @@ void conv_tap_fprop(const ConvTapArgs& a, int cus, hipStream_t s) {
       using C = decltype(cfg_tag);
       const int64_t tiles_m = (g.m + conv::BM - 1) / conv::BM;
       const unsigned grid = (unsigned)(tiles_m * (a.kout / C::BN));
-      hipLaunchKernelGGL((conv::fprop_kernel<T, C>), dim3(grid), dim3(C::THREADS), C::LDS, s, (const uint16_t*)a.in,
-                         (const uint16_t*)a.wt, (uint16_t*)a.out, g);
+      if (a.red_x)
+        hipLaunchKernelGGL((conv::fprop_kernel<T, C, true>), dim3(grid), dim3(C::THREADS), C::LDS, s,
+                           (const uint16_t*)a.in, (const uint16_t*)a.wt, (uint16_t*)a.out, g);
+      else
+        hipLaunchKernelGGL((conv::fprop_kernel<T, C>), dim3(grid), dim3(C::THREADS), C::LDS, s, (const uint16_t*)a.in,
+                           (const uint16_t*)a.wt, (uint16_t*)a.out, g);
     };
     auto go2 = [&](auto cfg_tag) {
       using C = decltype(cfg_tag);
       const int64_t tiles_m = (g.m + C::BM - 1) / C::BM;
       const unsigned grid = (unsigned)(tiles_m * (a.kout / C::BN));
-      hipLaunchKernelGGL((conv::fprop2_kernel<T, C>), dim3(grid), dim3(C::THREADS), C::LDS, s,
-                         (const uint16_t*)a.in, (const uint16_t*)a.wt, (uint16_t*)a.out, g);
+      if (a.red_x)
+        hipLaunchKernelGGL((conv::fprop2_kernel<T, C, true>), dim3(grid), dim3(C::THREADS), C::LDS, s,
+                           (const uint16_t*)a.in, (const uint16_t*)a.wt, (uint16_t*)a.out, g);
+      else
+        hipLaunchKernelGGL((conv::fprop2_kernel<T, C>), dim3(grid), dim3(C::THREADS), C::LDS, s,
+                           (const uint16_t*)a.in, (const uint16_t*)a.wt, (uint16_t*)a.out, g);
     };
     auto go3 = [&](auto cfg_tag) {
       using C = decltype(cfg_tag);
