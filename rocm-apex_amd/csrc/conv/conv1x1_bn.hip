@@ -115,7 +115,9 @@ constexpr bool one_wg_per_cu(int nc, int kr, int pro, bool red) {
   return pick_nw(nc, kr, pro, red) == 4 && lds_bytes_nw(nc, kr, pro, red, 4) > 80 * 1024;
 }
 
-template <typename T, int NC, int KR, bool WT, int PRO, bool STATS, bool RED, int NW, int DEPTH>
+// RED2: the second (downsample) BN's reduction in the RED epilogue — compile-time, since the
+// runtime form cost every single-BN dgrad ~6 % (stage 3: 110.6 -> 117.6 us, r06a vs r06z)
+template <typename T, int NC, int KR, bool WT, int PRO, bool STATS, bool RED, int NW, int DEPTH, bool RED2 = false>
 __global__ void __launch_bounds__(NW * 64, (NW == 8 || one_wg_per_cu(NC, KR, PRO, RED)) ? 1 : 2) fused1x1(Args p) {
   constexpr int kWaves = NW, kRowsB = NW * 32, NT = NW * 64;
   constexpr int BS = KR + 8;                 // B image row stride (elements)
@@ -347,7 +349,7 @@ __global__ void __launch_bounds__(NW * 64, (NW == 8 || one_wg_per_cu(NC, KR, PRO
       const bool has_res = WT && p.res != nullptr;  // residual add: a dgrad-form option
       uint4 rv[4], xq[4], xq2[4];
       unsigned mbv[4];
-      const bool red2 = RED && p.rx2 != nullptr;  // kernel-argument-uniform
+      constexpr bool red2 = RED && RED2;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int qid = lane + 64 * i, rr = qid >> 3, c8 = (qid & 7) * 8;
@@ -368,7 +370,7 @@ __global__ void __launch_bounds__(NW * 64, (NW == 8 || one_wg_per_cu(NC, KR, PRO
         }
         if constexpr (RED) {
           xq[i] = ok ? *reinterpret_cast<const uint4*>(p.rx + off) : make_uint4(0, 0, 0, 0);
-          xq2[i] = (ok && red2) ? *reinterpret_cast<const uint4*>(p.rx2 + off) : make_uint4(0, 0, 0, 0);
+          if constexpr (red2) xq2[i] = ok ? *reinterpret_cast<const uint4*>(p.rx2 + off) : make_uint4(0, 0, 0, 0);
           mbv[i] = (ok && p.rbits) ? p.rbits[off >> 3] : 0u;
         }
       }
@@ -383,7 +385,7 @@ __global__ void __launch_bounds__(NW * 64, (NW == 8 || one_wg_per_cu(NC, KR, PRO
         for (int j = 0; j < 8; ++j) rs[j] = rq[j] = rq2[j] = 0.f;
         const int cc = col0 + 64 * g + (lane & 7) * 8;
         Vec8<float>::load(mu, p.rmean + cc);
-        if (red2) Vec8<float>::load(mu2, p.rmean2 + cc);
+        if constexpr (red2) Vec8<float>::load(mu2, p.rmean2 + cc);
         if (!p.rbits) {  // wave-uniform: the mask of a plain BN + ReLU, recomputed from its input
           Vec8<float>::load(rsc, p.rcoef + cc);
           Vec8<float>::load(rsh, p.rcoef + p.ncols + cc);
@@ -421,7 +423,7 @@ __global__ void __launch_bounds__(NW * 64, (NW == 8 || one_wg_per_cu(NC, KR, PRO
                 rs[j] += gq;
                 rq[j] = fmaf(gq, xv[j] - mu[j], rq[j]);
               }
-              if (red2) {
+              if constexpr (red2) {
                 float xv2[8];
                 Vec8<T>::load(xv2, reinterpret_cast<const T*>(&xq2[i]));
 #pragma unroll
@@ -450,7 +452,7 @@ __global__ void __launch_bounds__(NW * 64, (NW == 8 || one_wg_per_cu(NC, KR, PRO
             const float gq = __shfl_xor(sq, msk, 64);
             rs[j] = (up ? rs[j + half] : rs[j]) + gs;
             rq[j] = (up ? rq[j + half] : rq[j]) + gq;
-            if (red2) {
+            if constexpr (red2) {
               const float sq2 = up ? rq2[j] : rq2[j + half];
               const float gq2 = __shfl_xor(sq2, msk, 64);
               rq2[j] = (up ? rq2[j + half] : rq2[j]) + gq2;
@@ -461,7 +463,7 @@ __global__ void __launch_bounds__(NW * 64, (NW == 8 || one_wg_per_cu(NC, KR, PRO
         float* r0p = rsum + (wid * 3) * NC + 64 * g + (lane & 7) * 8 + jc;
         r0p[0] += rs[0];
         r0p[NC] += rq[0];
-        if (red2) r0p[2 * NC] += rq2[0];
+        if constexpr (red2) r0p[2 * NC] += rq2[0];
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
@@ -738,13 +740,13 @@ static int g_c1bn_depth1 = [] {
 constexpr int default_depth(int nc, int kr) { return nc <= 128 && !(nc == 128 && kr == 128) ? 3 : 2; }
 
 
-template <typename T, int NC, int KR, bool WT, int PRO, bool STATS, bool RED, int DEPTH>
+template <typename T, int NC, int KR, bool WT, int PRO, bool STATS, bool RED, int DEPTH, bool RED2 = false>
 void launch_d(const Args& a0, int cus, hipStream_t s) {
   constexpr int NW = pick_nw(NC, KR, PRO, RED);
   constexpr int lds = lds_bytes_nw(NC, KR, PRO, RED, NW);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fused1x1<T, NC, KR, WT, PRO, STATS, RED, NW, DEPTH>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fused1x1<T, NC, KR, WT, PRO, STATS, RED, NW, DEPTH, RED2>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
@@ -756,24 +758,24 @@ void launch_d(const Args& a0, int cus, hipStream_t s) {
   const int gy = a.ncols / NC;
   int gx = (cus * per_cu + gy - 1) / gy;
   if (gx > a.ntiles) gx = a.ntiles;
-  hipLaunchKernelGGL((fused1x1<T, NC, KR, WT, PRO, STATS, RED, NW, DEPTH>), dim3(gx, a.ncols / NC), dim3(NW * 64),
+  hipLaunchKernelGGL((fused1x1<T, NC, KR, WT, PRO, STATS, RED, NW, DEPTH, RED2>), dim3(gx, a.ncols / NC), dim3(NW * 64),
                      lds, s, a);
 }
 
-template <typename T, int NC, int KR, bool WT, int PRO, bool STATS, bool RED = false>
+template <typename T, int NC, int KR, bool WT, int PRO, bool STATS, bool RED = false, bool RED2 = false>
 void launch_t(const Args& a, int cus, hipStream_t s) {
   if constexpr (one_wg_per_cu(NC, KR, PRO, RED)) {
     int d = g_c1bn_depth >= 2 && g_c1bn_depth <= 5 ? g_c1bn_depth : g_c1bn_depth1;
     // the BN-backward prologue + reduction form keeps a ring index dynamic at depth 4 (scratch)
     if ((PRO == kProBnBwd || PRO == kProBnBwdMask) && RED && d == 4) d = 5;
-    if (d == 5) return launch_d<T, NC, KR, WT, PRO, STATS, RED, 5>(a, cus, s);
-    if (d == 4) return launch_d<T, NC, KR, WT, PRO, STATS, RED, 4>(a, cus, s);
-    if (d == 2) return launch_d<T, NC, KR, WT, PRO, STATS, RED, 2>(a, cus, s);
-    return launch_d<T, NC, KR, WT, PRO, STATS, RED, 3>(a, cus, s);
+    if (d == 5) return launch_d<T, NC, KR, WT, PRO, STATS, RED, 5, RED2>(a, cus, s);
+    if (d == 4) return launch_d<T, NC, KR, WT, PRO, STATS, RED, 4, RED2>(a, cus, s);
+    if (d == 2) return launch_d<T, NC, KR, WT, PRO, STATS, RED, 2, RED2>(a, cus, s);
+    return launch_d<T, NC, KR, WT, PRO, STATS, RED, 3, RED2>(a, cus, s);
   }
   const int d = g_c1bn_depth == 2 || g_c1bn_depth == 3 ? g_c1bn_depth : default_depth(NC, KR);
-  if (d == 3) launch_d<T, NC, KR, WT, PRO, STATS, RED, 3>(a, cus, s);
-  else launch_d<T, NC, KR, WT, PRO, STATS, RED, 2>(a, cus, s);
+  if (d == 3) launch_d<T, NC, KR, WT, PRO, STATS, RED, 3, RED2>(a, cus, s);
+  else launch_d<T, NC, KR, WT, PRO, STATS, RED, 2, RED2>(a, cus, s);
 }
 
 inline int grid_x(int64_t m, int nc, int kr, int pro, int cus, int ncols, bool red = false) {
@@ -818,11 +820,11 @@ inline int col_tile_fit(int ncols, int kr, int pro, bool red) {
   return nc;
 }
 
-template <typename T, bool WT, int PRO, bool STATS, bool RED = false>
+template <typename T, bool WT, int PRO, bool STATS, bool RED = false, bool RED2 = false>
 void dispatch_shape(const Args& a, int nc, int kr, int cus, hipStream_t s) {
 #define C1BN_CASE(NC_, KR_)                                 \
   if (nc == NC_ && kr == KR_) {                             \
-    launch_t<T, NC_, KR_, WT, PRO, STATS, RED>(a, cus, s);  \
+    launch_t<T, NC_, KR_, WT, PRO, STATS, RED, RED2>(a, cus, s);  \
     return;                                                 \
   }
   C1BN_CASE(64, 64) C1BN_CASE(64, 128) C1BN_CASE(64, 256) C1BN_CASE(64, 512)
@@ -956,10 +958,12 @@ void conv1x1_dgrad_bnred(const void* g, const void* w, void* out, int64_t m, int
   args.aout = static_cast<uint16_t*>(aout);
   const int nc = c1bn::col_tile_fit(ncols, k, py ? (pro_mask ? c1bn::kProBnBwdMask : c1bn::kProBnBwd) : c1bn::kProNone,
                                     true);
+  if (x2 && py) throw std::runtime_error("conv1x1_dgrad_bnred: the second BN's reduction is a plain-dgrad option");
   dispatch_16(dtype, [&](auto tag) {
     using T = typename decltype(tag)::type;
     if (py && pro_mask) c1bn::dispatch_shape<T, true, c1bn::kProBnBwdMask, false, true>(args, nc, k, cus, s);
     else if (py) c1bn::dispatch_shape<T, true, c1bn::kProBnBwd, false, true>(args, nc, k, cus, s);
+    else if (x2) c1bn::dispatch_shape<T, true, c1bn::kProNone, false, true, true>(args, nc, k, cus, s);
     else c1bn::dispatch_shape<T, true, c1bn::kProNone, false, true>(args, nc, k, cus, s);
   }, "conv1x1_dgrad_bnred");
   check_launch("conv1x1_dgrad_bnred");
