@@ -800,20 +800,22 @@ inline int env_int(const char* name, int dflt) {
   const char* e = std::getenv(name);
   return e ? std::atoi(e) : dflt;
 }
-// 256-column tiles only on request (APEX_AMD_C1BN_NC256_MAXK=<max k>): their 128 accumulator
-// registers beside the backward-reduction epilogue spilled (80-120 B / lane); 128-column tiles at
-// k <= 128 measured +0.8 % on the step (profiles/r06/ab_c1bn_nc256_r06u.txt)
-inline int col_tile(int ncols, int kr) {
+// 256-column tiles only on request (APEX_AMD_C1BN_NC256_MAXK / _RED_MAXK = <max k>): beside the
+// backward-reduction epilogue their 128 accumulator registers spilled (80-120 B / lane) and
+// 128-column tiles measured +0.8 % on the step (profiles/r06/ab_c1bn_nc256_r06u.txt); keeping 256
+// for the other forms at k <= 64 measured -0.4 % (profiles/r06/ab_tap_prefetch_nc256_r06ab.txt)
+inline int col_tile(int ncols, int kr, bool red) {
   static const int max256 = env_int("APEX_AMD_C1BN_NC256_MAXK", 0);
+  static const int max256_red = env_int("APEX_AMD_C1BN_NC256_RED_MAXK", 0);
   static const int max128 = env_int("APEX_AMD_C1BN_NC128_MAXK", 512);
-  if (ncols % 256 == 0 && kr <= 256 && kr <= max256) return 256;
+  if (ncols % 256 == 0 && kr <= 256 && kr <= (red ? max256_red : max256)) return 256;
   return ncols % 128 == 0 && kr <= max128 ? 128 : 64;
 }
 
 // the column tile, narrowed while the workgroup's LDS (weight image + staging + prologue rows +
 // reduction sums) would not fit: the recomputed-mask BN-backward prologue's 5 rows at k 512
 inline int col_tile_fit(int ncols, int kr, int pro, bool red) {
-  int nc = col_tile(ncols, kr);
+  int nc = col_tile(ncols, kr, red);
   while (nc > 64 && lds_bytes_nw(nc, kr, pro, red, pick_nw(nc, kr, pro, red)) > 160 * 1024) nc /= 2;
   if (lds_bytes_nw(nc, kr, pro, red, pick_nw(nc, kr, pro, red)) > 160 * 1024)
     throw std::runtime_error("conv1x1_bn: no column tile fits the LDS for this reduction depth / prologue");

@@ -392,11 +392,11 @@ def _conv_fwd(x, w, stride, pad):
     return convops.conv_tap_forward(x, w, stride, pad) if fwd else F.conv2d(x, w, None, stride, pad)
 
 
-def _conv_bwd(gy, x, w, stride, pad, need_x=True):
+def _conv_bwd(gy, x, w, stride, pad, need_x=True, pre=None):
     _, dg, wg = convops.tap_route(x.size(1), w.size(0), w.size(2), stride, x.size(2), x.size(3))
     dx = dw = None
     if need_x and dg:
-        dx = convops.conv_tap_dgrad(gy, w, x.shape, stride, pad)
+        dx = convops.conv_tap_dgrad(gy, w, x.shape, stride, pad, pre=pre)
     if wg:
         dw = convops.conv_tap_wgrad(gy, x, w.shape, stride, pad, w.dtype)
     if (need_x and not dg) or not wg:
@@ -475,6 +475,9 @@ class _BottleneckFn(torch.autograd.Function):
                               sm1, si1, c1, sm2, si2, c2, sm3, si3, c3, smd, sid, cd, in1, in2, in3, ind, xs2)
         ctx.geo = (n, h, wd, oh, ow, stride)
         ctx.links = (link_in, link_out)
+        # the 3x3 data gradient's weight images, built on a side stream under this forward
+        ctx.pre2 = (convops.tap_images_async(w2, (n, width, h, wd), stride, 1)
+                    if pro1 or convops.tap_route(width, w2.size(0), 3, stride, h, wd)[1] else None)
         ctx.groups = (bn1.group, bn2.group, bn3.group, bnd.group if bnd is not None else None)
         if link_out is not None:
             link_out.y3, link_out.bits, link_out.mean, link_out.invstd = y3, bits, sm3, si3
@@ -554,16 +557,17 @@ class _BottleneckFn(torch.autograd.Function):
                 and convops.tap_route(width, w2.size(0), 3, 1, h, wd)[1])
         if z1 is None:  # bn1 folded into the 3x3 conv: its weight gradient recomputes z1 from y1
             gy2 = _nchw(dy2, n, oh, ow)
-            dz1 = convops.conv_tap_dgrad(gy2, w2, (n, width, h, wd), 1, 1)
+            dz1 = convops.conv_tap_dgrad(gy2, w2, (n, width, h, wd), 1, 1, pre=ctx.pre2)
             dw2 = convops.conv_tap_wgrad(gy2, _nchw(y1, n, h, wd), w2.shape, 1, 1, w2.dtype, xcoef=c1)
         elif red1:
             # bn1's backward reduction in the 3x3 dgrad's epilogue (ReLU mask recomputed from y1):
             # dz1 comes out masked with its [2, tiles, width] sums, no reduction pass over it
             gy2 = _nchw(dy2, n, oh, ow)
-            dz1, part1 = convops.conv_tap_dgrad(gy2, w2, (n, width, h, wd), 1, 1, red=(_nchw(y1, n, h, wd), c1, sm1))
+            dz1, part1 = convops.conv_tap_dgrad(gy2, w2, (n, width, h, wd), 1, 1, red=(_nchw(y1, n, h, wd), c1, sm1),
+                                                pre=ctx.pre2)
             dw2 = _conv_bwd(gy2, _nchw(z1, n, h, wd), w2, stride, 1, need_x=False)[1]
         else:
-            dz1, dw2 = _conv_bwd(_nchw(dy2, n, oh, ow), _nchw(z1, n, h, wd), w2, stride, 1)
+            dz1, dw2 = _conv_bwd(_nchw(dy2, n, oh, ow), _nchw(z1, n, h, wd), w2, stride, 1, pre=ctx.pre2)
         dz1 = _m2(dz1.contiguous(memory_format=torch.channels_last))
         # bn1: the reduction pass only, its dx as conv1's dgrad operand prologue with the ReLU mask
         # recomputed from y1 (kProBnBwdMask: the reduction writes nothing, the prologue writes dy1

@@ -268,7 +268,48 @@ def conv_bn_act(x, w, scale, bias, residual=None, relu=True, stride=1, padding=0
         return _conv_bn_act_reference(x, w, scale.detach(), bias.detach(), residual, relu, stride, padding)
 
 
-def conv_tap_dgrad(gy, w, x_shape, stride, pad, mask=None, red=None):
+# APEX_AMD_TAP_PREFETCH=1: build the data-gradient weight images on a side stream during the
+# forward (opt-in: the concurrent launches slowed the step 1.6 %, same box,
+# profiles/r06/ab_tap_prefetch_nc256_r06ab.txt; default: in line, in front of each dgrad)
+_TAP_PREFETCH = os.environ.get("APEX_AMD_TAP_PREFETCH", "0") == "1"
+_SIDE = {}
+
+
+def _side_stream(dev):
+    st = _SIDE.get(dev)
+    if st is None:
+        st = _SIDE[dev] = torch.cuda.Stream(device=dev)
+    return st
+
+
+def tap_images_async(w, x_shape, stride, pad):
+    """The data-gradient weight images of every phase of ``conv_tap_dgrad(.., w, x_shape, stride,
+    pad)``, built on a side stream during the forward (the weight is final for the step there):
+    the ~5 us transposition launches then overlap the forward's kernels instead of sitting in
+    front of each dgrad.  Returns an opaque handle for ``conv_tap_dgrad(pre=...)``, or None
+    (disabled, capturing, not CUDA, or a weight the native transposition does not take)."""
+    if not (_TAP_PREFETCH and w.is_cuda) or torch.cuda.is_current_stream_capturing():
+        return None
+    ext = _conv_ext()
+    n, c, h, wd = x_shape
+    kout, _, k, _ = w.shape
+    if not (hasattr(ext, "tap_weights") and w.is_contiguous(memory_format=torch.channels_last)
+            and kout % 8 == 0 and c % 8 == 0):
+        return None
+    cur = torch.cuda.current_stream(w.device)
+    side = _side_stream(w.device)
+    side.wait_stream(cur)
+    imgs = []
+    with torch.cuda.stream(side):
+        for _, _, oh, ow, taps in _dgrad_phases(k, stride, pad, h, wd):
+            if taps and oh > 0 and ow > 0:
+                imgs.append(ext.tap_weights(w, [r * w.shape[3] + s_ for r, s_, _, _ in taps]))
+    ev = torch.cuda.Event()
+    ev.record(side)
+    return imgs, ev, w._version
+
+
+def conv_tap_dgrad(gy, w, x_shape, stride, pad, mask=None, red=None, pre=None):
     """Data gradient through the native tap kernel.  ``mask`` (optional, the layer input's producer
     ReLU output, same shape as dx): dx *= (mask > 0) in the kernel's epilogue — the previous
     stage's dReLU fused into this dconv.  ``red = (x, coef, mean)`` (stride 1): dx is the gradient
@@ -288,10 +329,20 @@ def conv_tap_dgrad(gy, w, x_shape, stride, pad, mask=None, red=None):
     if red is not None and len(phases) != 1:
         raise ValueError("conv_tap_dgrad: the BN reduction epilogue takes a single-phase (stride 1) dgrad")
     part = None
+    imgs = None
+    if pre is not None and native_w and pre[2] == w._version:  # images from tap_images_async
+        imgs, ev, _ = pre
+        cur = torch.cuda.current_stream(gy.device)
+        cur.wait_event(ev)
+        for t in imgs:
+            t.record_stream(cur)
+        imgs = list(imgs)
     for ph, pw, oh, ow, taps in phases:
         if not taps or oh <= 0 or ow <= 0:
             continue
-        if native_w:  # [C, taps, K] in one tiled transpose launch (layout.hip conv_tap_weights)
+        if imgs:
+            wt = imgs.pop(0)
+        elif native_w:  # [C, taps, K] in one tiled transpose launch (layout.hip conv_tap_weights)
             wt = ext.tap_weights(w, [r * w.shape[3] + s_ for r, s_, _, _ in taps])
         elif len(taps) == k * k:  # every tap in (r, s) row-major order: one permute-copy, no stack
             wt = wk.reshape(c, k * k, kout).contiguous()  # [C, taps, K]

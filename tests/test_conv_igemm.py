@@ -254,3 +254,38 @@ def test_gpu_dgrad_bn_reduction_epilogue(n, c, h):
     istd = torch.rand(c, device="cuda") + 0.5
     coef_b, gw, gb = ext.bnbwd_finalize(part, float(g.size(0)), mean, istd, None)
     torch.testing.assert_close(gb.double(), g.sum(0), atol=1e-3 * scale, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stride", [1, 2])
+def test_gpu_tap_dgrad_prefetched_weight_images_bitwise(monkeypatch, stride):
+    """APEX_AMD_TAP_PREFETCH (opt-in): the data-gradient weight images built on a side stream
+    during the forward give the in-line dgrad bitwise, and a weight changed in place after the
+    prefetch falls back to in-line images."""
+    from apex.ops import conv as convops
+
+    monkeypatch.setattr(convops, "_TAP_PREFETCH", True)
+    torch.manual_seed(11 + stride)
+    dt = torch.bfloat16
+    n, c, k, h = 3, 128, 128, 14
+    w = (torch.randn(k, c, 3, 3, device="cuda") * 0.05).to(dt).contiguous(memory_format=torch.channels_last)
+    oh = (h + 2 - 3) // stride + 1
+    gy = torch.randn(n, k, oh, oh, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
+    shape = (n, c, h, h)
+    pre = convops.tap_images_async(w, shape, stride, 1)
+    assert pre is not None
+    want = convops.conv_tap_dgrad(gy, w, shape, stride, 1)
+    got = convops.conv_tap_dgrad(gy, w, shape, stride, 1, pre=pre)
+    assert torch.equal(got, want)
+    pre = convops.tap_images_async(w, shape, stride, 1)
+    with torch.no_grad():
+        w.mul_(2)
+    assert torch.equal(convops.conv_tap_dgrad(gy, w, shape, stride, 1, pre=pre),
+                       convops.conv_tap_dgrad(gy, w, shape, stride, 1))
+
+
+def test_tap_prefetch_is_off_on_cpu_tensors():
+    from apex.ops import conv as convops
+
+    w = torch.randn(64, 64, 3, 3).contiguous(memory_format=torch.channels_last)
+    assert convops.tap_images_async(w, (1, 64, 8, 8), 1, 1) is None
