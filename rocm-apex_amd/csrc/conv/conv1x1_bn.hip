@@ -766,7 +766,9 @@ template <typename T, int NC, int KR, bool WT, int PRO, bool STATS, bool RED = f
 void launch_t(const Args& a, int cus, hipStream_t s) {
   if constexpr (one_wg_per_cu(NC, KR, PRO, RED)) {
     int d = g_c1bn_depth >= 2 && g_c1bn_depth <= 5 ? g_c1bn_depth : g_c1bn_depth1;
-    // the BN-backward prologue + reduction form keeps a ring index dynamic at depth 4 (scratch)
+    // the BN-backward prologue + reduction form at depth 5 (its round-5 depth-4 ring sat in scratch;
+    // the named ring of round 6 removed that for every form, and depth 4 stays the measured best for
+    // the others: profiles/r06/ab_c1bn_depth_r06ae.txt)
     if ((PRO == kProBnBwd || PRO == kProBnBwdMask) && RED && d == 4) d = 5;
     if (d == 5) return launch_d<T, NC, KR, WT, PRO, STATS, RED, 5, RED2>(a, cus, s);
     if (d == 4) return launch_d<T, NC, KR, WT, PRO, STATS, RED, 4, RED2>(a, cus, s);
