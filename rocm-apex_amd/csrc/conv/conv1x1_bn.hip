@@ -962,10 +962,11 @@ void conv1x1_dgrad_bnred(const void* g, const void* w, void* out, int64_t m, int
   args.aout = static_cast<uint16_t*>(aout);
   const int nc = c1bn::col_tile_fit(ncols, k, py ? (pro_mask ? c1bn::kProBnBwdMask : c1bn::kProBnBwd) : c1bn::kProNone,
                                     true);
-  if (x2 && py) throw std::runtime_error("conv1x1_dgrad_bnred: the second BN's reduction is a plain-dgrad option");
   dispatch_16(dtype, [&](auto tag) {
     using T = typename decltype(tag)::type;
-    if (py && pro_mask) c1bn::dispatch_shape<T, true, c1bn::kProBnBwdMask, false, true>(args, nc, k, cus, s);
+    if (py && pro_mask && x2) c1bn::dispatch_shape<T, true, c1bn::kProBnBwdMask, false, true, true>(args, nc, k, cus, s);
+    else if (py && pro_mask) c1bn::dispatch_shape<T, true, c1bn::kProBnBwdMask, false, true>(args, nc, k, cus, s);
+    else if (py && x2) c1bn::dispatch_shape<T, true, c1bn::kProBnBwd, false, true, true>(args, nc, k, cus, s);
     else if (py) c1bn::dispatch_shape<T, true, c1bn::kProBnBwd, false, true>(args, nc, k, cus, s);
     else if (x2) c1bn::dispatch_shape<T, true, c1bn::kProNone, false, true, true>(args, nc, k, cus, s);
     else c1bn::dispatch_shape<T, true, c1bn::kProNone, false, true>(args, nc, k, cus, s);

@@ -553,3 +553,27 @@ def test_gpu_chain_downsample_reduction_in_block_above(monkeypatch):
     assert _rel(ga, gb) < 1e-2, _rel(ga, gb)
     for n in pa:
         assert _rel(pa[n], pb[n]) < 1e-2, (n, _rel(pa[n], pb[n]))
+
+
+@pytest.mark.gpu
+def test_gpu_chain_bn1_dx_prologue_with_downsample_reduction(monkeypatch):
+    """The opt-in bn1-dx prologue of conv1's dgrad (``_BN1_DX_PRO``, kProBnBwdMask) on the block
+    above a downsampling block also carries that block's downsample-BN reduction (the second BN
+    of the epilogue, a compile-time kernel variant since round 6): the chain runs and agrees with
+    the default path to rounding."""
+    from apex.ops import bottleneck_bn
+
+    torch.manual_seed(9)
+    a = _chain().cuda().to(memory_format=torch.channels_last).train()
+    b = copy.deepcopy(a)
+    x = torch.randn(4, 64, 14, 14, device="cuda").to(torch.bfloat16).to(memory_format=torch.channels_last)
+    gy = torch.randn(4, 256, 14, 14, device="cuda").to(torch.bfloat16).to(memory_format=torch.channels_last)
+    monkeypatch.setattr(bottleneck_bn, "_DS_RED", True)
+    monkeypatch.setattr(bottleneck_bn, "_BN1_DX_PRO", True)
+    ya, ga, pa, _ = _run_chain(a, x, gy, True)
+    monkeypatch.setattr(bottleneck_bn, "_BN1_DX_PRO", False)
+    yb, gb, pb, _ = _run_chain(b, x, gy, True)
+    assert torch.equal(ya, yb)
+    assert _rel(ga, gb) < 1e-2, _rel(ga, gb)
+    for n in pa:
+        assert _rel(pa[n], pb[n]) < 1e-2, (n, _rel(pa[n], pb[n]))
