@@ -258,9 +258,12 @@ def timed(args, step, dev, world, rank, distributed, B, impl, desc=None):
     start = time.perf_counter()
     for i in range(args.steps):
         loss = step()
+    enq = time.perf_counter() - start  # host enqueue time of the timed steps (no device sync)
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
+    if os.environ.get("APEX_BENCH_HOST") and rank == 0:
+        print(f"[bench] host enqueue {1e3 * enq / args.steps:.3f} ms/step", file=sys.stderr, flush=True)
     elapsed = time.perf_counter() - start
     t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
     if distributed:
