@@ -320,16 +320,31 @@ __global__ void __launch_bounds__(256, (fwd_occupancy<D, MODE, QF, LO>())) fwd_k
           #pragma unroll
           for (int r = 0; r < 16; ++r) x[0][t][r] = sacc[f][t][r];
         if (need_mask) {
+          // key-contiguous bias over a whole tile: the lane's 32 keys are 8 runs of 4 (crow), so 8
+          // 16-byte loads instead of 32 scalar ones (BERT's key-padding mask: the forward ran 2.4x
+          // the bias-free kernel, profiles/r06/pmc_attn_r06.md)
+          const bool bvec = biasb != nullptr && a.bias_sk == 1 && kb0 + BN <= sq.lk &&
+                            ((reinterpret_cast<uintptr_t>(biasb) | (uintptr_t)(a.bias_sq * 4)) & 15) == 0;
+          const float* brow = bvec ? biasb + (int64_t)(qvalid[f] ? myq[f] : 0) * a.bias_sq + kb0 + 4 * h2 : nullptr;
           #pragma unroll
           for (int t = 0; t < 2; ++t)
             #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int key = kb0 + 32 * t + crow(r, h2);
-              const bool ok = key < sq.lk && (!a.causal || key <= myq[f]);
-              float v = x[0][t][r];
-              if (biasb != nullptr && ok && qvalid[f])
-                v += biasb[(int64_t)myq[f] * a.bias_sq + (int64_t)key * a.bias_sk] * inv_scale;
-              x[0][t][r] = ok ? v : -INFINITY;
+            for (int i = 0; i < 4; ++i) {
+              // one 4-key run at a time: 4 live registers (all 32 values at once spilled)
+              float4 q4 = make_float4(0.f, 0.f, 0.f, 0.f);
+              if (bvec) q4 = *reinterpret_cast<const float4*>(brow + 32 * t + 8 * i);
+              #pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const int r = 4 * i + j;
+                const int key = kb0 + 32 * t + crow(r, h2);
+                const bool ok = key < sq.lk && (!a.causal || key <= myq[f]);
+                float v = x[0][t][r];
+                if (biasb != nullptr && ok && qvalid[f]) {
+                  const float bvv = j == 0 ? q4.x : j == 1 ? q4.y : j == 2 ? q4.z : q4.w;
+                  v += (bvec ? bvv : biasb[(int64_t)myq[f] * a.bias_sq + (int64_t)key * a.bias_sk]) * inv_scale;
+                }
+                x[0][t][r] = ok ? v : -INFINITY;
+              }
             }
         }
         float mx = -INFINITY;
@@ -775,6 +790,9 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
       const float* del_h = ba.delta + (int64_t)hq * a.rows_q + sq.qrow0;
       const uint32_t bh = (uint32_t)(b * a.h + hq);
       const float* biash = (MODE == 2 && a.bias) ? a.bias + (int64_t)b * a.bias_sb + (int64_t)hq * a.bias_sh : nullptr;
+      // a key-only bias (bias_sq 0: key padding) is one value per lane (its key) for the whole head
+      const bool bkey_ok = biash != nullptr && a.bias_sq == 0 && kvalid;
+      const float bkey = bkey_ok ? biash[(int64_t)mykey * a.bias_sk] * kLog2e : 0.f;
       const int q_begin = a.causal ? (k_start / QB) * QB : 0;
       uint4 pq[QCPT], pg[QCPT];
       float plse = INFINITY, pdel = 0.f;
@@ -857,7 +875,8 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dkdv_kernel(const
             const int q = q0s + crow(r, h2);
             const bool ok = kvalid && q < sq.lq && (!a.causal || mykey <= q);
             float xv = p[r];
-            if (biash != nullptr && ok) xv += biash[(int64_t)q * a.bias_sq + (int64_t)mykey * a.bias_sk] * kLog2e;
+            if (biash != nullptr && ok)
+              xv += bkey_ok ? bkey : biash[(int64_t)q * a.bias_sq + (int64_t)mykey * a.bias_sk] * kLog2e;
             p[r] = ok ? xv : -INFINITY;
           }
         }

@@ -436,3 +436,30 @@ def test_dropout_keep_scale_is_unbiased_for_the_16bit_threshold(p):
     assert dropout_keep_scale(p) * (65536 - t16) / 65536 == pytest.approx(1.0, rel=1e-12)
     keep = dropout_keep_mask(7, 0, [0, 1], 64, 256, p)
     assert abs(keep.float().mean().item() * dropout_keep_scale(p) - 1.0) < 0.05
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("per_query", [False, True])
+def test_gpu_flash_bias_vector_loads_bitwise(per_query):
+    """The additive bias read as 16-byte key runs (key-contiguous bias over whole 64-key tiles) and
+    as one value per key for a key-only bias in dK/dV: bitwise the per-element loads they replace,
+    forced here by handing the same values in through a stride-2 view."""
+    torch.manual_seed(21)
+    b, s, h, d = 2, 256, 4, 64
+    q = torch.randn(b, s, h, d, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn_like(q, requires_grad=True)
+    v = torch.randn_like(q, requires_grad=True)
+    shape = (b, h, s, s) if per_query else (b, 1, 1, s)
+    dense = torch.randn(*shape, device="cuda")
+    dense[..., -s // 8:] = -10000.0
+    wide = torch.zeros(*shape[:-1], 2 * s, device="cuda")
+    wide[..., ::2] = dense
+    strided = wide[..., ::2]
+    assert strided.stride(-1) == 2 and torch.equal(strided, dense)
+    g = torch.randn_like(q)
+    outs = []
+    for bias in (dense, strided):
+        o = flash_attn_func(q, k, v, dropout_p=0.1, bias=bias, seed=5, offset=3)
+        outs.append((o,) + torch.autograd.grad(o, (q, k, v), g))
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
