@@ -1066,15 +1066,27 @@ __global__ void __launch_bounds__(256, (D == 128 ? 1 : 2)) bwd_dq_kernel(const A
         #pragma unroll
         for (int r = 0; r < 16; ++r) ds[t][r] = s[t][r] * c - lse2;
       if (need_mask) {  // wave-uniform: the interior tiles run the element loop branch-free
+        // key-contiguous bias over a whole tile: one 16-byte run of 4 keys at a time (see the forward)
+        const bool bvec = biasp != nullptr && a.bias_sk == 1 && kb0 + BN <= sq.lk && qvalid &&
+                          (reinterpret_cast<uintptr_t>(biasp) & 15) == 0;
         #pragma unroll
         for (int t = 0; t < 2; ++t)
           #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = kb0 + 32 * t + crow(r, h2);
-            const bool ok = qvalid && key < sq.lk && (!a.causal || key <= myq);
-            float xv = ds[t][r];
-            if (biasp != nullptr && ok) xv += biasp[(int64_t)key * a.bias_sk] * kLog2e;
-            ds[t][r] = ok ? xv : -INFINITY;
+          for (int i = 0; i < 4; ++i) {
+            float4 q4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (bvec) q4 = *reinterpret_cast<const float4*>(biasp + kb0 + 4 * h2 + 32 * t + 8 * i);
+            #pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int r = 4 * i + j;
+              const int key = kb0 + 32 * t + crow(r, h2);
+              const bool ok = qvalid && key < sq.lk && (!a.causal || key <= myq);
+              float xv = ds[t][r];
+              if (biasp != nullptr && ok) {
+                const float bvv = j == 0 ? q4.x : j == 1 ? q4.y : j == 2 ? q4.z : q4.w;
+                xv += (bvec ? bvv : biasp[(int64_t)key * a.bias_sk]) * kLog2e;
+              }
+              ds[t][r] = ok ? xv : -INFINITY;
+            }
           }
       }
       #pragma unroll
