@@ -171,18 +171,21 @@ void wgrad(const at::Tensor& in, const at::Tensor& dy, at::Tensor& dw_out, int64
 }
 
 // True when conv_wgrad takes the halo-tile kernel (csrc/conv/conv3x3_wgrad.hip) for a 3x3 pad-1
-// stride-1 conv of an [n, h, w, c] input to kout channels (ops/conv.py tap_route)
-bool halo_wgrad_supported(int64_t n, int64_t h, int64_t w, int64_t c, int64_t kout) {
+// stride-1 / stride-2 conv of an [n, h, w, c] input to kout channels (ops/conv.py tap_route)
+bool halo_wgrad_supported(int64_t n, int64_t h, int64_t w, int64_t c, int64_t kout, int64_t stride) {
   ConvTapArgs a{};
   void* aligned = reinterpret_cast<void*>(static_cast<uintptr_t>(256));  // alignment checks only
   a.in = a.wt = aligned;
   a.out = aligned;
   a.n = (int)n;
-  a.ih = a.oh = a.oht = (int)h;
-  a.iw = a.ow = a.owt = (int)w;
+  a.ih = (int)h;
+  a.iw = (int)w;
+  a.oh = a.oht = (int)((h - 1) / stride + 1);
+  a.ow = a.owt = (int)((w - 1) / stride + 1);
   a.c = (int)c;
   a.kout = (int)kout;
-  a.ish = a.isw = a.osh = a.osw = 1;
+  a.ish = a.isw = (int)stride;
+  a.osh = a.osw = 1;
   a.oph = a.opw = 0;
   a.ntaps = 9;
   for (int t = 0; t < 9; ++t) {
@@ -728,7 +731,8 @@ void bind_conv(pybind11::module_& root) {
         pybind11::arg("xcoef") = pybind11::none());
   m.def("force_fprop_cfg", &conv_force_fprop_cfg);
   m.def("force_wgrad_variant", &conv_force_wgrad_variant);
-  m.def("halo_wgrad_supported", &halo_wgrad_supported);
+  m.def("halo_wgrad_supported", &halo_wgrad_supported, pybind11::arg("n"), pybind11::arg("h"), pybind11::arg("w"),
+        pybind11::arg("c"), pybind11::arg("kout"), pybind11::arg("stride") = 1);
   m.attr("WGRAD_HALO") = kWgradHalo;
   m.def("bn1x1", &bn1x1, pybind11::arg("a"), pybind11::arg("w"), pybind11::arg("w_kmajor_out") = false,
         pybind11::arg("pcoef") = pybind11::none(), pybind11::arg("shift") = pybind11::none(),

@@ -41,11 +41,13 @@ constexpr int NS = 7;           // 16-pixel reduction slices per tile
 constexpr int NPP = NS * 16;    // tile pixel capacity
 
 struct Args {
-  const uint16_t* x;   // [n][h][w][c]
+  const uint16_t* x;   // [n][ih][iw][c]
   const uint16_t* dy;  // [n][h][w][k]
   float* ws;           // [splits][k][9][c]
   const float* xcoef;  // nullable [2][c]: x' = relu(x * xcoef[c] + xcoef[c + C]) (the producing BN + ReLU)
-  int h, w, c, k;
+  int h, w, c, k;      // output grid, channels
+  int ih, iw;          // input grid (= h, w at stride 1; 2h, 2w at stride 2)
+  int he;              // stride 2: halo slots of the even-column plane (w + 1; odd plane follows)
   int R, HR, HC, hs;   // tile rows, halo rows / columns per image block, halo slots (G * HR * HC)
   int np;              // real pixels per tile (G * R * w)
   int tpi;             // tiles per image (h / R); 1 for whole-image tiles
@@ -56,13 +58,18 @@ struct Args {
 // NW waves: 4 (one per SIMD: 64 output channels, a 3-stage ring) or 8 (two per SIMD sharing each
 // halo tile: 128 output channels, so a staged halo feeds twice the MFMAs; 2-stage ring to fit the
 // LDS; APEX_AMD_HWG_NW=8)
-template <int TK, int HSL, int HC_, int NW_ = 4>
+// ST 2 (stride-2 convs): the halo of R output rows is 2R + 1 input rows, its columns split into an
+// even plane (input columns -1, 1, 3, ...) and an odd plane (0, 2, ...), so the three column taps of
+// consecutive output pixels read consecutive slots as at stride 1; ~4x the halo per pixel, so a
+// 2-stage ring (no prologue form)
+template <int TK, int HSL, int HC_, int NW_ = 4, int ST = 1, int NS_ = NS>
 struct Cfg {
   static constexpr int NW = NW_, NT = NW * 64;
-  static constexpr int S = NW == 8 ? 2 : 3;            // LDS ring stages
+  static constexpr int S = (NW == 8 || ST == 2) ? 2 : 3;  // LDS ring stages
   static constexpr int HC = HC_;                       // halo columns (slots per halo row)
   static constexpr int KB = 32 * (NW / 2) * TK;        // output channels per workgroup
-  static constexpr int DYR = (TK == 1 || NW == 8) ? 128 : 112;  // dY image rows (DMA count % NW == 0)
+  // dY image rows (DMA count % NW == 0); the stride-2 8-wave form stages just its slices' rows
+  static constexpr int DYR = (ST == 2 && NW == 8) ? NS_ * 16 : ((TK == 1 || NW == 8) ? 128 : 112);
   static constexpr int DYI = DYR * KB * 2 / 1024;      // dY DMA instructions per tile
   static constexpr int HI = HSL / 8;                   // halo DMA instructions per tile (8 slots each)
   static constexpr int DYW = DYI / NW, HW = HI / NW;   // per wave
@@ -71,7 +78,7 @@ struct Cfg {
   static constexpr int STAGE_EL = DY_EL + HSL * 64;    // one ring stage (elements)
   static constexpr size_t LDS = (size_t)S * STAGE_EL * 2;
   static_assert(DYI % NW == 0 && HI % NW == 0, "DMA instructions must split evenly over the waves");
-  static_assert(DYR >= NPP, "dY image holds the tile");
+  static_assert(DYR >= NS_ * 16, "dY image holds the tile");
   static_assert(LDS <= 160 * 1024, "ring exceeds the 160 KiB LDS");
 };
 
@@ -104,9 +111,10 @@ __device__ __forceinline__ s16x8 frag2(const uint16_t* lo, const uint16_t* hi) {
   return s16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
-template <typename T, int TK, int HSL, int HC, bool PRO, int NW = 4>
+template <typename T, int TK, int HSL, int HC, bool PRO, int NW = 4, int ST = 1, int NSL = NS>
 __global__ void __launch_bounds__(NW * 64, 1) wgrad_kernel(const Args p) {
-  using C = Cfg<TK, HSL, HC, NW>;
+  using C = Cfg<TK, HSL, HC, NW, ST, NSL>;
+  static_assert(ST == 1 || !PRO, "stride 2: no prologue form");
   constexpr int KB = C::KB, S = C::S;
   static_assert(!(PRO && S < 3), "the BN prologue rewrites the next tile's halo under the current MFMAs: 3 stages");
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
@@ -152,10 +160,12 @@ __global__ void __launch_bounds__(NW * 64, 1) wgrad_kernel(const Args p) {
     const int slot = 8 * j + (lane >> 3);
     const int sc = (lane & 7) ^ (swz<64>(slot) << 2);
     const int gi = slot / hblk, rem = slot - gi * hblk;
-    const int hy = rem / HC, hx = rem - hy * HC;
-    const bool ok = slot < p.hs && hx >= 1 && hx <= p.w;
-    hrel[i] = (((gi * p.h + hy - 1) * p.w) + hx - 1) * p.c * 2 + (c0 + 8 * sc) * 2;
-    hfl[i] = (ok ? 1u : 0u) | (hy == 0 ? 2u : 0u) | (hy == p.HR - 1 ? 4u : 0u);
+    const int hy = rem / HC, hj = rem - hy * HC;
+    const int hx = ST == 1 ? hj : (hj < p.he ? 2 * hj : 2 * (hj - p.he) + 1);
+    const bool ok = slot < p.hs && hx >= 1 && hx <= p.iw;
+    hrel[i] = (((gi * p.ih + hy - 1) * p.iw) + hx - 1) * p.c * 2 + (c0 + 8 * sc) * 2;
+    // (stride 2: the last halo row, input row 2 (y0 + R) - 1, is inside the image)
+    hfl[i] = (ok ? 1u : 0u) | (hy == 0 ? 2u : 0u) | (ST == 1 && hy == p.HR - 1 ? 4u : 0u);
   }
   // PRO (the producing BN + ReLU, x' = relu(x * xcoef[c] + xcoef[C + c])): every lane rewrites the
   // 16-byte halo chunks IT loaded once their DMA has landed (no barrier needed before that; the
@@ -190,7 +200,7 @@ __global__ void __launch_bounds__(NW * 64, 1) wgrad_kernel(const Args p) {
       const uint32_t voff = dyrow[i] < p.np ? dyo + dyrel[i] : 0x80000000u;
       bdma16(dr, voff, base + (i * NW + wave) * 512);
     }
-    const int xo = px0 * p.c * 2;
+    const int xo = px0 * (ST * ST) * p.c * 2;  // the tile's input origin (ih = ST h, iw = ST w)
     uint32_t vm = 0;  // bit i: halo chunk i of this lane holds image data (PRO rewrites it)
 #pragma unroll
     for (int i = 0; i < C::HW; ++i) {
@@ -226,23 +236,29 @@ __global__ void __launch_bounds__(NW * 64, 1) wgrad_kernel(const Args p) {
   }
   // halo: per slice, lo / hi pixel row, tap column shift dw = -1, 0, 1 at tap row dh = -1 (dh = 0
   // and 1 add HC and 2 HC slots: an instruction-immediate offset, HC being a compile-time size)
-  int baddr[NS][2][3];
+  int baddr[NSL][2][3];
   {
     const int col = 32 * ct + 16 * (g & 1) + 4 * pp;
     const int rw = p.R * p.w;
 #pragma unroll
-    for (int s = 0; s < NS; ++s)
+    for (int s = 0; s < NSL; ++s)
 #pragma unroll
       for (int hl = 0; hl < 2; ++hl) {
         const int px = 16 * s + 8 * (g >> 1) + q + 4 * hl;
-        int slot = HC + 1;  // pixel rows past the tile: any real slot (their dY rows are zero)
+        // slots of tap row 0, column taps 0 / 1 / 2 (pixel rows past the tile: any real slots,
+        // their dY rows are zero)
+        int sl0 = 0, sl1 = 1, sl2 = 2;
         if (px < p.np) {
           const int gi = px / rw, rem = px - gi * rw;
           const int y = rem / p.w, x = rem - y * p.w;
-          slot = (gi * p.HR + y + 1) * HC + x + 1;
+          const int rb = (gi * p.HR + ST * y) * HC;
+          sl0 = rb + x;
+          sl1 = ST == 1 ? rb + x + 1 : rb + p.he + x;
+          sl2 = rb + x + (ST == 1 ? 2 : 1);
         }
-#pragma unroll
-        for (int d = 0; d < 3; ++d) baddr[s][hl][d] = C::DY_EL + img_addr<64>(slot - HC + d - 1, col);
+        baddr[s][hl][0] = C::DY_EL + img_addr<64>(sl0, col);
+        baddr[s][hl][1] = C::DY_EL + img_addr<64>(sl1, col);
+        baddr[s][hl][2] = C::DY_EL + img_addr<64>(sl2, col);
       }
   }
 
@@ -282,7 +298,7 @@ __global__ void __launch_bounds__(NW * 64, 1) wgrad_kernel(const Args p) {
     const uint16_t* sb = lds + (it % S) * C::STAGE_EL;
     const bool xnext = PRO && it + 1 < nt;  // PRO: rewrite tile it + 1's chunks under these MFMAs
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
+    for (int s = 0; s < NSL; ++s) {
       s16x8 af[TK], bf[9];
 #pragma unroll
       for (int i = 0; i < TK; ++i)
@@ -303,7 +319,7 @@ __global__ void __launch_bounds__(NW * 64, 1) wgrad_kernel(const Args p) {
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           }
 #pragma unroll
-          for (int i = s * C::HW / NS; i < (s + 1) * C::HW / NS; ++i) xform((it + 1) % S, vq1, i);
+          for (int i = s * C::HW / NSL; i < (s + 1) * C::HW / NSL; ++i) xform((it + 1) % S, vq1, i);
         }
       }
     }
@@ -365,8 +381,18 @@ constexpr Inst kInst[] = {{1, 224, 12}, {1, 256, 16}, {1, 256, 32}, {1, 256, 60}
 
 struct Plan {
   bool ok;
-  int tk, hsl, R, G, HR, HC, hs, np, tpi, ntiles, splits, nblk_c, nw;
+  int tk, hsl, R, G, HR, HC, hs, np, tpi, ntiles, splits, nblk_c, nw, st, ns, he;
 };
+
+// stride-2 instances (4 waves, 64 output channels, 2-stage ring): (halo slots, halo columns,
+// 16-pixel slices) — 7 x 7 / 14 x 14 outputs (two whole images / 7 rows per tile, 98 pixels of
+// 112) and 28 x 28 (2 rows, 56 pixels of 64); halo slots % 32 == 0 (the DMA split over 4 waves)
+// 8-wave forms (128 output channels share each staged halo: half the halo bytes per MFMA, the
+// stride-2 kernel's limit) where the 2-stage ring fits: 28 x 28 (2 rows) and 7 x 7 (one image)
+struct Inst2 {
+  int hsl, hc, ns, nw;
+};
+constexpr Inst2 kInst2[] = {{480, 16, 7, 4}, {480, 32, 7, 4}, {320, 60, 4, 4}, {320, 60, 4, 8}, {256, 16, 4, 8}};
 
 // 8-wave workgroups (128 output channels per staged halo: two waves per SIMD, half the halo
 // staging per MFMA) wherever kout % 128 == 0 and no prologue: 92 -> 80 us at 7x7 / 14x14, 82.5 ->
@@ -400,31 +426,80 @@ inline bool tile_geo(int h, int w, int hc, int hsl, int& R, int& G) {
   return false;
 }
 
+// stride 2: R output rows (a divisor of h) or G whole images per tile, 2R + 1 halo rows, columns
+// w + 1 (even plane) + w (odd plane) <= hc
+inline bool tile_geo2(int h, int w, Inst2 in, int& R, int& G) {
+  if (2 * w + 1 > in.hc) return false;
+  const int npp = in.ns * 16;
+  R = 0;
+  G = 1;
+  if (h * w <= npp / 2) {
+    if ((2 * h + 1) * in.hc > in.hsl) return false;
+    R = h;
+    G = std::max(1, std::min(npp / (h * w), in.hsl / ((2 * h + 1) * in.hc)));
+    return true;
+  }
+  for (int r = h; r >= 1; --r)
+    if (h % r == 0 && r * w <= npp && (2 * r + 1) * in.hc <= in.hsl) {
+      R = r;
+      return true;
+    }
+  return false;
+}
+
 inline Plan make_plan(const ConvTapArgs& a, int cus, bool pro = false) {
   Plan pl{};
   pl.ok = false;
   const int h = a.oh, w = a.ow;
   if (w < 1 || h < 1) return pl;
-  pl.nw = (!pro && a.kout % 128 == 0) ? env_nw() : 4;
-  double best = -1.0;
-  for (Inst in : kInst) {
-    if (in.tk == 2 && a.kout % 128) continue;
-    if (pl.nw == 8) in.hsl = 256;  // (the 8-wave DMA split needs halo pieces % 8)
-    int R, G;
-    if (!tile_geo(h, w, in.hc, in.hsl, R, G)) continue;
-    // pixel-slot efficiency, with a 10 % bonus for the 128-channel block (half the halo re-reads)
-    const double eff = (double)(G * R * w) / NPP * (in.tk == 2 ? 1.1 : 1.0);
-    if (eff > best + 1e-9) {
-      best = eff;
-      pl.tk = in.tk;
-      pl.hsl = in.hsl;
-      pl.HC = in.hc;
-      pl.R = R;
-      pl.G = G;
+  pl.st = a.ish;
+  pl.ns = NS;
+  pl.he = 0;
+  if (pl.st == 2) {
+    if (pro) return pl;
+    pl.tk = 1;
+    const bool nw8 = a.kout % 128 == 0 && env_nw() == 8;
+    double best = -1.0;
+    for (Inst2 in : kInst2) {
+      int R, G;
+      if ((in.nw == 8 && !nw8) || !tile_geo2(h, w, in, R, G)) continue;
+      // pixel-slot efficiency, 8-wave forms weighted 1.3x (half the halo traffic per MFMA)
+      const double eff = (double)(G * R * w) / (in.ns * 16) * (in.nw == 8 ? 1.3 : 1.0);
+      if (eff > best + 1e-9) {
+        best = eff;
+        pl.nw = in.nw;
+        pl.hsl = in.hsl;
+        pl.HC = in.hc;
+        pl.ns = in.ns;
+        pl.R = R;
+        pl.G = G;
+      }
     }
+    if (best < 0) return pl;
+    pl.HR = 2 * pl.R + 1;
+    pl.he = w + 1;
+  } else {
+    pl.nw = (!pro && a.kout % 128 == 0) ? env_nw() : 4;
+    double best = -1.0;
+    for (Inst in : kInst) {
+      if (in.tk == 2 && a.kout % 128) continue;
+      if (pl.nw == 8) in.hsl = 256;  // (the 8-wave DMA split needs halo pieces % 8)
+      int R, G;
+      if (!tile_geo(h, w, in.hc, in.hsl, R, G)) continue;
+      // pixel-slot efficiency, with a 10 % bonus for the 128-channel block (half the halo re-reads)
+      const double eff = (double)(G * R * w) / NPP * (in.tk == 2 ? 1.1 : 1.0);
+      if (eff > best + 1e-9) {
+        best = eff;
+        pl.tk = in.tk;
+        pl.hsl = in.hsl;
+        pl.HC = in.hc;
+        pl.R = R;
+        pl.G = G;
+      }
+    }
+    if (best < 0) return pl;
+    pl.HR = pl.R + 2;
   }
-  if (best < 0) return pl;
-  pl.HR = pl.R + 2;
   pl.hs = pl.G * pl.HR * pl.HC;
   pl.np = pl.G * pl.R * w;
   pl.tpi = pl.G > 1 ? 1 : h / pl.R;
@@ -443,13 +518,15 @@ inline Plan make_plan(const ConvTapArgs& a, int cus, bool pro = false) {
 bool conv_hwgrad_supported(const ConvTapArgs& a) {
   if (a.dtype != kBF16 && a.dtype != kF16) return false;
   if (a.ntaps != 9 || a.c % 64 || a.kout % 64 || a.c <= 0 || a.kout <= 0 || a.n <= 0) return false;
-  if (a.ish != 1 || a.isw != 1 || a.osh != 1 || a.osw != 1 || a.oph != 0 || a.opw != 0) return false;
-  if (a.oh != a.ih || a.ow != a.iw || a.oht != a.oh || a.owt != a.ow) return false;
+  // stride 1 (same-size output) or stride 2 of an even-sized input (ih = 2 oh, iw = 2 ow)
+  if (a.ish != a.isw || (a.ish != 1 && a.ish != 2)) return false;
+  if (a.osh != 1 || a.osw != 1 || a.oph != 0 || a.opw != 0) return false;
+  if (a.ih != a.ish * a.oh || a.iw != a.isw * a.ow || a.oht != a.oh || a.owt != a.ow) return false;
   for (int t = 0; t < 9; ++t)
     if (a.dh[t] != t / 3 - 1 || a.dw[t] != t % 3 - 1) return false;
   const int64_t xb = (int64_t)a.n * a.ih * a.iw * a.c * 2, db = (int64_t)a.n * a.oh * a.ow * a.kout * 2;
   // buffer ranges, and the per-tile byte origins in 32 bits with a tile of headroom
-  if (xb + (int64_t)hwg::NPP * 8 * a.c * 2 >= (1ll << 31) || db + (int64_t)hwg::NPP * a.kout * 2 >= (1ll << 31))
+  if (xb + (int64_t)hwg::NPP * 8 * a.ish * a.isw * a.c * 2 >= (1ll << 31) || db + (int64_t)hwg::NPP * a.kout * 2 >= (1ll << 31))
     return false;
   if (((uintptr_t)a.in & 15) || ((uintptr_t)a.out & 15)) return false;
   return hwg::make_plan(a, 256).ok;
@@ -479,8 +556,11 @@ void conv_hwgrad_pro(const ConvTapArgs& a, const void* dy, void* dw_out, int out
   p.dy = static_cast<const uint16_t*>(dy);
   p.ws = ws;
   p.xcoef = xcoef;
-  p.h = a.ih;
-  p.w = a.iw;
+  p.h = a.oh;
+  p.w = a.ow;
+  p.ih = a.ih;
+  p.iw = a.iw;
+  p.he = pl.he;
   p.c = a.c;
   p.k = a.kout;
   p.R = pl.R;
@@ -519,13 +599,21 @@ void conv_hwgrad_pro(const ConvTapArgs& a, const void* dy, void* dw_out, int out
       if (!seen) (void)hipFuncSetAttribute(fp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(kern, dim3(grid), dim3(pl.nw * 64), lds, s, p);
     };
+#define HWG_CASE2(HSL_, HC_, NS_, NW_)                                                              \
+  if (pl.st == 2 && pl.nw == NW_ && pl.hsl == HSL_ && pl.HC == HC_ && pl.ns == NS_) {                  \
+    go(hwg::wgrad_kernel<T, 1, HSL_, HC_, false, NW_, 2, NS_>, hwg::Cfg<1, HSL_, HC_, NW_, 2, NS_>::LDS);  \
+    return;                                                                                         \
+  }
+    HWG_CASE2(480, 16, 7, 4) HWG_CASE2(480, 32, 7, 4) HWG_CASE2(320, 60, 4, 4) HWG_CASE2(320, 60, 4, 8)
+    HWG_CASE2(256, 16, 4, 8)
+#undef HWG_CASE2
 #define HWG_CASE(TK_, HSL_, HC_)                                                                    \
-  if (pl.nw == 4 && pl.tk == TK_ && pl.hsl == HSL_ && pl.HC == HC_) {                               \
+  if (pl.st == 1 && pl.nw == 4 && pl.tk == TK_ && pl.hsl == HSL_ && pl.HC == HC_) {                               \
     if (xcoef) go(hwg::wgrad_kernel<T, TK_, HSL_, HC_, true>, hwg::Cfg<TK_, HSL_, HC_>::LDS);           \
     else go(hwg::wgrad_kernel<T, TK_, HSL_, HC_, false>, hwg::Cfg<TK_, HSL_, HC_>::LDS);                \
     return;                                                                                         \
   }                                                                                                 \
-  if (pl.nw == 8 && !xcoef && pl.tk == TK_ && pl.hsl == 256 && pl.HC == HC_) {                        \
+  if (pl.st == 1 && pl.nw == 8 && !xcoef && pl.tk == TK_ && pl.hsl == 256 && pl.HC == HC_) {                        \
     go(hwg::wgrad_kernel<T, TK_, 256, HC_, false, 8>, hwg::Cfg<TK_, 256, HC_, 8>::LDS);                \
     return;                                                                                         \
   }

@@ -133,6 +133,9 @@ _TAP_ENABLED = os.environ.get("APEX_AMD_CONV_IGEMM", "1") != "0"
 _S2_DGRAD_128 = os.environ.get("APEX_AMD_S2_DGRAD_128", "0") == "1"
 # the halo-tile 3x3 weight gradient (csrc/conv/conv3x3_wgrad.hip); 0 = the r04 routes (A/B)
 _HALO_WGRAD = os.environ.get("APEX_AMD_HALO_WGRAD", "1") != "0"
+# its stride-2 form (even-sized inputs: ResNet-50's three downsampling 3x3s) instead of MIOpen's
+# igemm_wrw; 0 = MIOpen (A/B)
+_HALO_WGRAD_S2 = os.environ.get("APEX_AMD_HALO_WGRAD_S2", "1") != "0"
 
 
 def _conv_ext():
@@ -362,7 +365,8 @@ def conv_tap_dgrad(gy, w, x_shape, stride, pad, mask=None, red=None, pre=None):
 def conv_tap_wgrad(gy, x, w_shape, stride, pad, out_dtype, xcoef=None):
     """``xcoef`` (fp32 [2C]): the weight gradient of a conv whose input was relu(x * xcoef[:C] +
     xcoef[C:]) — the producing BN + ReLU recomputed on the halo-tile kernel's staged input (3x3
-    stride 1 where ``halo_wgrad_supported``)."""
+    stride 1 where ``halo_wgrad_supported``).  3x3 pad-1 weight gradients of stride 1, and of stride
+    2 over an even-sized input, run on the halo-tile kernel where it takes the shape."""
     kout, c, k, _ = w_shape
     dw = torch.empty((kout, k, k, c), dtype=out_dtype, device=gy.device)
     taps = _fwd_taps(k, pad)
@@ -372,13 +376,14 @@ def conv_tap_wgrad(gy, x, w_shape, stride, pad, out_dtype, xcoef=None):
 
 
 @functools.lru_cache(maxsize=None)
-def _halo_wgrad(cin, cout, h, w):
-    if not _HALO_WGRAD:
+def _halo_wgrad(cin, cout, h, w, stride=1):
+    """``h``, ``w``: the conv's INPUT size."""
+    if not _HALO_WGRAD or (stride == 2 and not _HALO_WGRAD_S2):
         return False
     ext = _native.submodule("conv")
     if ext is None or not hasattr(ext, "halo_wgrad_supported"):
         return False
-    return bool(ext.halo_wgrad_supported(1, h, w, cin, cout))
+    return bool(ext.halo_wgrad_supported(1, h, w, cin, cout, stride))
 
 
 @functools.lru_cache(maxsize=None)
@@ -393,12 +398,15 @@ def tap_route(cin, cout, k, stride, h, w=None):
       * 1x1 stride 2 (downsample): data gradient native (0.70-0.91x MIOpen);
       * 3x3 weight gradient, stride 1: the halo-tile kernel (conv3x3_wgrad.hip) wherever it takes
         the shape; r04 routes otherwise (wgrad2 128 x 64 only at 28x28x128: 136 vs 149 us, MIOpen
-        5-12 % ahead at the other shapes)."""
+        5-12 % ahead at the other shapes);
+      * 3x3 weight gradient, stride 2 (even-sized input): the halo-tile kernel's stride-2 form
+        (round 6), else MIOpen."""
     if not _TAP_ENABLED:
         return False, False, False
     if k == 3:
-        wg = stride == 1 and (_halo_wgrad(cin, cout, h, h if w is None else w)
-                              or (cin == 128 and cout == 128 and h == 28))
+        wg = ((stride == 1 and (_halo_wgrad(cin, cout, h, h if w is None else w)
+                                or (cin == 128 and cout == 128 and h == 28)))
+              or (stride == 2 and _halo_wgrad(cin, cout, h, h if w is None else w, 2)))
         return True, not (stride == 2 and cout <= 128) or _S2_DGRAD_128, wg
     if k == 1 and stride == 2:
         return False, True, False

@@ -22,12 +22,12 @@ SHAPES = [
 ]
 
 
-def _ref(x, gy, cout):
+def _ref(x, gy, cout, stride=1):
     """float64 weight gradient on the CPU (exact products of the 16-bit operands)."""
     xd = x.detach().double().cpu().requires_grad_(False)
     gd = gy.detach().double().cpu()
     w = torch.zeros(cout, x.size(1), 3, 3, dtype=torch.float64, requires_grad=True)
-    torch.autograd.backward(F.conv2d(xd, w, None, 1, 1), gd)
+    torch.autograd.backward(F.conv2d(xd, w, None, stride, 1), gd)
     return w.grad
 
 
@@ -107,3 +107,62 @@ def test_gpu_halo_wgrad_bn_relu_prologue_is_bitwise_the_apply_pass(n, h, w, cin,
     got = C.conv_tap_wgrad(gy, y, (cout, cin, 3, 3), 1, 1, torch.float32, xcoef=coef)
     assert torch.equal(got, want)
     _close(got, _ref(zv, gy, cout), 1e-2)
+
+
+# stride 2 over even-sized inputs (n, input h, input w, cin, cout): ResNet-50's three downsampling
+# 3x3s (56 -> 28 on 2-row tiles, 8 and 4 waves; 28 -> 14 on 7-row tiles; 14 -> 7 as two whole
+# images per tile with an odd batch, 4 waves, or one image per tile, 8 waves), a 5-row tile, one
+# whole non-square image per tile, a tiny image
+SHAPES_S2 = [
+    (2, 56, 56, 128, 128),
+    (2, 56, 56, 128, 64),
+    (3, 28, 28, 256, 128),
+    (3, 14, 14, 512, 64),
+    (3, 14, 14, 256, 128),
+    (2, 20, 20, 64, 64),
+    (2, 12, 16, 64, 128),
+    (3, 4, 4, 64, 64),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n,h,w,cin,cout", SHAPES_S2)
+def test_gpu_halo_wgrad_stride2_matches_float64(dtype, n, h, w, cin, cout):
+    """the stride-2 form (2R + 1 halo rows, even / odd column planes) against float64 torch"""
+    from apex import _native
+    from apex.ops import conv as C
+
+    ext = _native.require("conv").conv
+    assert ext.halo_wgrad_supported(n, h, w, cin, cout, 2), "shape expected on the halo kernel"
+    torch.manual_seed(h * 17 + w + cin)
+    x = (torch.randn(n, cin, h, w, device="cuda") + 0.1).to(dtype).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(n, cout, h // 2, w // 2, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    ref = _ref(x, gy, cout, 2)
+    ext.force_wgrad_variant(ext.WGRAD_HALO)
+    try:
+        dw32 = C.conv_tap_wgrad(gy, x, (cout, cin, 3, 3), 2, 1, torch.float32)
+        dw16 = C.conv_tap_wgrad(gy, x, (cout, cin, 3, 3), 2, 1, dtype)
+        again = C.conv_tap_wgrad(gy, x, (cout, cin, 3, 3), 2, 1, torch.float32)
+    finally:
+        ext.force_wgrad_variant(-1)
+    _close(dw32, ref, 2e-5)
+    _close(dw16, ref, 8e-3)
+    assert torch.equal(dw32, again), "split partials must be summed in a fixed order"
+    # the default dispatcher takes the same kernel
+    assert torch.equal(C.conv_tap_wgrad(gy, x, (cout, cin, 3, 3), 2, 1, torch.float32), dw32)
+
+
+def test_halo_wgrad_stride2_route():
+    """ResNet-50's downsampling 3x3 weight gradients route to the native kernel when the
+    extension takes their shapes (the stride-2 form), MIOpen otherwise."""
+    from apex import _native
+    from apex.ops import conv as C
+
+    ext = _native.submodule("conv")
+    for h, c in ((56, 128), (28, 256), (14, 512)):
+        want = bool(ext is not None and C._HALO_WGRAD and C._HALO_WGRAD_S2
+                    and ext.halo_wgrad_supported(1, h, h, c, c, 2))
+        assert C.tap_route(c, c, 3, 2, h, h)[2] == want
+    if ext is not None:
+        assert not ext.halo_wgrad_supported(1, 15, 15, 64, 64, 2), "odd inputs stay on the other engines"
