@@ -17,7 +17,8 @@ bool has(const OT& t) { return t.has_value() && t->defined(); }
 
 // C[M][N] = A(M x K) B(K x N); see gemm_api.h for the major-ness conventions.
 at::Tensor run_gemm(const at::Tensor& a, bool a_kmajor, const at::Tensor& b, bool b_kmajor, int64_t m, int64_t n,
-                    int64_t k, int epilogue, const OT& bias, const OT& aux_in, at::Tensor* aux_out) {
+                    int64_t k, int epilogue, const OT& bias, const OT& aux_in, at::Tensor* aux_out,
+                    at::Tensor* colsum_out = nullptr, at::ScalarType colsum_t = at::kFloat) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm: GPU tensors expected");
   TORCH_CHECK(a.is_contiguous() && b.is_contiguous(), "gemm: contiguous operands expected");
   TORCH_CHECK(a.scalar_type() == b.scalar_type(), "gemm: operand dtype mismatch");
@@ -61,7 +62,25 @@ at::Tensor run_gemm(const at::Tensor& a, bool a_kmajor, const at::Tensor& b, boo
     ws = at::empty({wsf}, a.options().dtype(at::kFloat));
     g.splitk_ws = ws.data_ptr<float>();
   }
+  at::Tensor cpart;
+  const bool fused_cs = colsum_out != nullptr && gemm_colsum_fusable(g, cus);
+  if (fused_cs) {
+    // column sums of C in the epilogue: one fp32 row per 256-row tile, then a fixed-order fold
+    cpart = at::empty({(m + 255) / 256, n}, a.options().dtype(at::kFloat));
+    g.colpart = cpart.data_ptr<float>();
+  }
   gemm_mfma(g, cus, cur_stream());
+  if (colsum_out != nullptr) {
+    *colsum_out = at::empty({n}, a.options().dtype(colsum_t));
+    if (fused_cs) {
+      column_sum_finalize(cpart.data_ptr<float>(), (int)cpart.size(0), (int)n, colsum_out->data_ptr(),
+                          dtype_code(colsum_t), cur_stream());
+    } else {
+      auto cws = at::empty({column_sum_workspace_floats(m, (int)n, cus)}, a.options().dtype(at::kFloat));
+      column_sum(c.data_ptr(), dtype_code(c.scalar_type()), m, (int)n, n, colsum_out->data_ptr(), dtype_code(colsum_t),
+                 cws.data_ptr<float>(), cus, cur_stream());
+    }
+  }
   return c;
 }
 
@@ -138,6 +157,16 @@ void bind_gemm(pybind11::module_& root) {
     const c10::hip::HIPGuard guard(dy.get_device());
     return linear_wgrad(as2d(dy), as2d(x));
   });
+  g.def("linear_dgrad_bgrad", [](at::Tensor dy, at::Tensor w, int epi, at::Tensor aux_in,
+                                 c10::optional<at::ScalarType> out_dtype) {
+    // (dz, db): dz = (dy W) * act'(aux_in) with db = column sums of the stored dz in the GEMM's
+    // epilogue (the reference's DGELU_BGRAD, csrc/fused_dense_cuda.cu:977) — no pass over dz
+    const c10::hip::HIPGuard guard(dy.get_device());
+    at::Tensor d = as2d(dy), db;
+    auto dz = run_gemm(d, true, w.contiguous(), false, d.size(0), w.size(1), d.size(1), epi, c10::nullopt, aux_in,
+                       nullptr, &db, out_dtype.value_or(d.scalar_type()));
+    return std::make_tuple(dz, db);
+  }, py::arg("dy"), py::arg("w"), py::arg("epilogue"), py::arg("aux_in"), py::arg("out_dtype") = c10::nullopt);
   g.def("dgelu_column_sum", [](at::Tensor dy, at::Tensor aux, c10::optional<at::ScalarType> out_dtype) {
     // (dz, db): dz = dy * gelu_tanh'(aux), db = column sums of dz — one pass
     const c10::hip::HIPGuard guard(dy.get_device());
@@ -193,9 +222,11 @@ void bind_gemm(pybind11::module_& root) {
     auto x2 = as2d(input), dy2 = as2d(grad_output);
     auto dw2 = linear_wgrad(dy2, output1);
     auto db2 = colsum(dy2, w2.scalar_type());
-    auto dh = linear_dgrad(dy2, w2, kEpiDGelu, gelu_in);  // (dy W2) * gelu'(pre-activation)
+    // (dy W2) * gelu'(pre-activation), its column sums (db1) in the same epilogue
+    at::Tensor db1;
+    auto dh = run_gemm(dy2, true, w2.contiguous(), false, dy2.size(0), w2.size(1), dy2.size(1), kEpiDGelu,
+                       c10::nullopt, gelu_in, nullptr, &db1, w1.scalar_type());
     auto dw1 = linear_wgrad(dh, x2);
-    auto db1 = colsum(dh, w1.scalar_type());
     auto dx = linear_dgrad(dh, w1, kEpiNone, c10::nullopt);
     return std::vector<at::Tensor>{dx, dw1, db1, dw2, db2};
   });

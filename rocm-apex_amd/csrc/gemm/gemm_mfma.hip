@@ -486,7 +486,7 @@ template <typename T, bool AK, bool BKM, int EPI, int NW>
 __global__ void __launch_bounds__(NW * 64, 1)
 gemm256_nt(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, T* __restrict__ C, int64_t lda,
            int64_t ldb, int64_t ldc, int M, int N, int K, const T* __restrict__ bias, const T* __restrict__ aux_in,
-           T* __restrict__ aux_out, float* __restrict__ part, int kchunk) {
+           T* __restrict__ aux_out, float* __restrict__ part, int kchunk, float* __restrict__ colpart) {
   constexpr int WN = NW / 2;           // waves along N
   constexpr int NJ = BN / WN / 32;     // 32-wide column fragments per wave (2 or 4)
   constexpr int NT = NW * 64;
@@ -542,9 +542,9 @@ gemm256_nt(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, T* __
   float* cs = reinterpret_cast<float*>(lds);
   const int ch = tid & 31, rsub = tid >> 5;  // rsub in [0, NT / 32)
   const int gc = col0 + ch * 8;
-  float bv[8];
+  float bv[8], csum[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) bv[e] = 0.f;
+  for (int e = 0; e < 8; ++e) bv[e] = csum[e] = 0.f;
   if (bias != nullptr && gc < N) Vec8<T>::load(bv, bias + gc);
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
@@ -617,9 +617,27 @@ gemm256_nt(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, T* __
           }
         }
         Vec8<T>::store(C + off, v);
+        if (colpart != nullptr) {
+          // column sums of the STORED (rounded) values: the bias gradient of this GEMM's output,
+          // as the reference's DGELU_BGRAD epilogue (csrc/fused_dense_cuda.cu:977)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) csum[e] += to_f(from_f<T>(v[e]));
+        }
       }
     }
     __syncthreads();
+  }
+  if (colpart != nullptr) {
+    // fold the NT / 32 row groups of each column (fixed order), one fp32 partial per (M tile, column)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs[rsub * BN + ch * 8 + e] = csum[e];
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      float t = 0.f;
+#pragma unroll
+      for (int r = 0; r < NT / 32; ++r) t += cs[r * BN + c];
+      if (col0 + c < N) colpart[(int64_t)bm * N + col0 + c] = t;
+    }
   }
 }
 
@@ -673,7 +691,7 @@ void launch_nw(const GemmArgs& g, hipStream_t s, int cus) {
   if (sp > 1) {
     hipLaunchKernelGGL((gemm256_nt<T, AK, BKM, kEpiNone, NW>), dim3(tiles, sp), dim3(THREADS), LDS_BYTES, s,
                        (const uint16_t*)g.a, (const uint16_t*)g.b, (T*)g.c, g.lda, g.ldb, g.ldc, g.m, g.n, g.k,
-                       (const T*)nullptr, (const T*)nullptr, (T*)nullptr, g.splitk_ws, kchunk);
+                       (const T*)nullptr, (const T*)nullptr, (T*)nullptr, g.splitk_ws, kchunk, (float*)nullptr);
     const int64_t nvec = (int64_t)g.m * g.n / 8;
     int64_t grid = (nvec + 255) / 256;
     if (grid > (int64_t)cus * 8) grid = (int64_t)cus * 8;
@@ -684,7 +702,7 @@ void launch_nw(const GemmArgs& g, hipStream_t s, int cus) {
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(tiles), dim3(THREADS), LDS_BYTES, s, (const uint16_t*)g.a, (const uint16_t*)g.b,
                        (T*)g.c, g.lda, g.ldb, g.ldc, g.m, g.n, g.k, (const T*)g.bias, (const T*)g.aux_in,
-                       (T*)g.aux_out, (float*)nullptr, g.k);
+                       (T*)g.aux_out, (float*)nullptr, g.k, g.colpart);
   };
   switch (g.epilogue) {
     case kEpiNone: go(gemm256_nt<T, AK, BKM, kEpiNone, NW>); break;
@@ -1030,8 +1048,17 @@ bool gemm_supported(const GemmArgs& g) {
   return true;
 }
 
+bool gemm_colsum_fusable(const GemmArgs& g, int cus) {
+  if (!gemm_supported(g) || !gemm::g256::usable(g, cus)) return false;
+  if (g.a_kmajor && g.b_kmajor && gemm::g8p::enabled()) return false;
+  int kc;
+  return g.splitk_ws == nullptr || gemm::g256::splitk_parts(g, cus, &kc) <= 1;
+}
+
 void gemm_mfma(const GemmArgs& g, int cus, hipStream_t s) {
   if (!gemm_supported(g)) throw std::runtime_error("gemm_mfma: unsupported shape/alignment/dtype");
+  if (g.colpart != nullptr && !gemm_colsum_fusable(g, cus))
+    throw std::runtime_error("gemm_mfma: the column-sum epilogue needs the 256-tile kernel (gemm_colsum_fusable)");
   dispatch_16(g.dtype, [&](auto tag) {
     using T = typename decltype(tag)::type;
     if (gemm::g256::usable(g, cus)) {
@@ -1053,6 +1080,14 @@ int64_t gemm_splitk_workspace_floats(const GemmArgs& g, int cus) {
   int kc;
   const int sp = gemm::g256::splitk_parts(g, cus, &kc);
   return sp > 1 ? (int64_t)sp * g.m * g.n : 0;
+}
+
+void column_sum_finalize(const float* part, int p, int n, void* out, int out_dtype, hipStream_t s) {
+  dispatch_float(out_dtype, [&](auto tag) {
+    using TO = typename decltype(tag)::type;
+    hipLaunchKernelGGL((gemm::colsum_finalize<TO>), dim3((n + 15) / 16), dim3(256), 0, s, part, p, n, (TO*)out);
+  }, "column_sum_finalize");
+  check_launch("column_sum_finalize");
 }
 
 int64_t column_sum_workspace_floats(int64_t m, int n, int cus) { return (int64_t)gemm::colsum_parts(m, n, cus) * n; }

@@ -38,10 +38,18 @@ struct GemmArgs {
   const void* aux_in;   // [M][ldc] or null
   void* aux_out;        // [M][ldc] or null
   float* splitk_ws;     // fp32 split-K partials (gemm_splitk_workspace_floats) or null = no split
+  // fp32 [ceil(m / 256)][n] column sums of the stored C per 256-row tile, or null (the bias
+  // gradient of an activation-gradient GEMM: DGELU_BGRAD; gemm_colsum_fusable shapes only),
+  // summed by column_sum_finalize
+  float* colpart = nullptr;
 };
 
 // true when the shape / alignment / dtype is supported by the MFMA kernel
 bool gemm_supported(const GemmArgs& g);
+// true when g runs on the 256-tile kernel unsplit, which takes GemmArgs::colpart
+bool gemm_colsum_fusable(const GemmArgs& g, int cus);
+// out[n] = sum over p rows of part[p][n] (fixed order), written in out_dtype
+void column_sum_finalize(const float* part, int p, int n, void* out, int out_dtype, hipStream_t s);
 void gemm_mfma(const GemmArgs& g, int cus, hipStream_t s);
 // fp32 workspace a split-K launch of g needs (0: the shape runs unsplit).  Split-K is used for
 // no-epilogue GEMMs whose output has too few 256x256 tiles to fill the chip but whose K is long

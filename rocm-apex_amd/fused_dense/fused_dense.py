@@ -78,6 +78,11 @@ def _gelu_pass(z):
 
 
 _ROUTES = {}
+# FusedDenseGeluDense backward where hipBLASLt has no usable DGELU kernel (bf16 on gfx950): the
+# native MFMA dgrad GEMM with dGeLU AND the bias-gradient column sums in its epilogue (the
+# reference's DGELU_BGRAD, csrc/fused_dense_cuda.cu:977) — "native" (default) — or the library
+# dgrad + one dGeLU / column-sum pass over its output ("pass", A/B)
+_DGELU_ROUTE = os.environ.get("APEX_AMD_DGELU_ROUTE", "native")
 
 
 def route_mode():
@@ -385,6 +390,11 @@ class FusedDenseGeluDenseFunc(torch.autograd.Function):
             else:
                 r = lt.dgelu_bgrad(*args, False)  # dGeLU epilogue; db1 from the wgrad's BGRADB
                 gz = r[0] if r else None
+        if gz is None and (_DGELU_ROUTE == "native" and route_mode() != "library" and _native.use_native(g2) and _native.submodule("gemm") is not None
+                           and g2.dtype in (torch.float16, torch.bfloat16) and weight2.dtype == g2.dtype
+                           and gelu_in.dtype == g2.dtype and g2.shape[1] % 8 == 0 and weight2.shape[1] % 8 == 0):
+            gz, db1 = _g().linear_dgrad_bgrad(g2.contiguous(), weight2.contiguous(), _g().EPI_DGELU,
+                                              gelu_in.reshape(h.shape).contiguous(), weight1.dtype)
         if gz is None:
             dh = g2.matmul(weight2)
             z = gelu_in.reshape(h.shape)

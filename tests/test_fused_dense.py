@@ -130,12 +130,17 @@ def test_gpu_fused_dense_reference_test(dtype, route, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("route", ["native", "lt", "lt_bgradb", "library", "auto"])
+@pytest.mark.parametrize("route", ["native", "lt", "lt_bgradb", "lt_dgelu_pass", "library", "auto"])
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 def test_gpu_fused_dense_gelu_dense(dtype, route, monkeypatch):
     if route == "lt_bgradb":
         route = "lt"
         monkeypatch.setenv("APEX_AMD_LT_BGRADB", "1")
+    if route == "lt_dgelu_pass":  # library dgrad + the one-pass dGeLU / column sum (A/B arm)
+        import importlib
+
+        route = "lt"
+        monkeypatch.setattr(importlib.import_module("apex.fused_dense.fused_dense"), "_DGELU_ROUTE", "pass")
     monkeypatch.setenv("APEX_AMD_DENSE_ROUTE", route)
     torch.manual_seed(2)
     x = (torch.randn(2, 256, 512, device="cuda") * 0.5).to(dtype).requires_grad_(True)
@@ -420,6 +425,33 @@ def test_gpu_dgelu_column_sum_vs_fp32(m, n, dtype):
     torch.testing.assert_close(db.float(), ref_db, atol=1e-2 * max(1.0, m ** 0.5), rtol=1e-2)
     _, db32 = g.dgelu_column_sum(dy, z, torch.float32)
     torch.testing.assert_close(db32, ref_db, atol=1e-3 * max(1.0, m ** 0.5), rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("m,k,n", [(16384, 1024, 4096), (1000, 256, 1024), (300, 64, 520)])
+def test_gpu_dgrad_dgelu_bgrad_epilogue(m, k, n, dtype):
+    """Native dgrad GEMM with dGeLU and the bias-gradient column sums in its epilogue
+    (linear_dgrad_bgrad, the reference's DGELU_BGRAD): dz vs float64 torch, db BITWISE-close to
+    the fp32 sum of the stored dz, the fused sums equal to the separate dGeLU epilogue's output,
+    and small shapes (no 256-tile kernel) on the column-sum pass fallback."""
+    from apex import _native
+
+    g = _native.require("gemm").gemm
+    torch.manual_seed(m + n)
+    dy = torch.randn(m, k, device="cuda").to(dtype)
+    w = (torch.randn(k, n, device="cuda") * 0.05).to(dtype)
+    z = (torch.randn(m, n, device="cuda") * 2).to(dtype)
+    dz, db = g.linear_dgrad_bgrad(dy, w, g.EPI_DGELU, z, torch.float32)
+    assert dz.dtype == dtype and db.dtype == torch.float32 and db.shape == (n,)
+    zr = z.double().requires_grad_(True)
+    ref = torch.autograd.grad(torch.nn.functional.gelu(zr, approximate="tanh"), zr, dy.double() @ w.double())[0]
+    torch.testing.assert_close(dz.double(), ref, atol=3e-2, rtol=2e-2)
+    assert torch.equal(dz, g.linear_dgrad(dy, w, g.EPI_DGELU, z)), "the column sums must not change dz"
+    torch.testing.assert_close(db.double(), dz.double().sum(0), atol=1e-4 * max(1.0, m ** 0.5), rtol=1e-5)
+    _, db16 = g.linear_dgrad_bgrad(dy, w, g.EPI_DGELU, z)
+    assert db16.dtype == dtype
+    torch.testing.assert_close(db16.float(), db.float(), atol=1e-2 * max(1.0, m ** 0.5), rtol=1e-2)
 
 
 @pytest.mark.gpu

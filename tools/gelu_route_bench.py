@@ -49,6 +49,7 @@ def main():
             "bwd_torch_dgrad+dgelu_colsum_pass": lambda: g.dgelu_column_sum(gy.matmul(w2), z),
             "bwd_native_dgelu_epilogue+colsum": lambda: _native.column_sum(g.linear_dgrad(gy, w2, g.EPI_DGELU, z), dt),
             "bwd_native_dgelu_epilogue_only": lambda: g.linear_dgrad(gy, w2, g.EPI_DGELU, z),
+            "bwd_native_dgelu_bgrad_epilogue": lambda: g.linear_dgrad_bgrad(gy, w2, g.EPI_DGELU, z),
             "fwd_lt_bias_only": lambda: lt.linear(x, w1, b1, lt.EPI_BIAS),
         }
         # numerics of the native epilogue forms against the unfused composition
