@@ -472,10 +472,12 @@ def test_gpu_gelu_pass(dtype):
 
     g = apex._native.require("gemm").gemm
     torch.manual_seed(4)
-    z = (torch.randn(4099, 1024, device="cuda") * 3).to(dtype)
-    y = g.gelu(z)
-    ref = torch.nn.functional.gelu(z.float(), approximate="tanh")
-    torch.testing.assert_close(y.float(), ref, atol=2e-2, rtol=2e-2)
+    # ragged grid-stride tail, a multi-trip size (4 vectors per lane per trip), a single vector
+    for shape in ((4099, 1024), (8192, 4096), (1, 8)):
+        z = (torch.randn(*shape, device="cuda") * 3).to(dtype)
+        y = g.gelu(z)
+        ref = torch.nn.functional.gelu(z.float(), approximate="tanh")
+        torch.testing.assert_close(y.float(), ref, atol=2e-2, rtol=2e-2)
 
 
 @pytest.mark.gpu
