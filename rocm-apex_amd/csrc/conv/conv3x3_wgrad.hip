@@ -388,11 +388,13 @@ struct Plan {
 // 16-pixel slices) — 7 x 7 / 14 x 14 outputs (two whole images / 7 rows per tile, 98 pixels of
 // 112) and 28 x 28 (2 rows, 56 pixels of 64); halo slots % 32 == 0 (the DMA split over 4 waves)
 // 8-wave forms (128 output channels share each staged halo: half the halo bytes per MFMA, the
-// stride-2 kernel's limit) where the 2-stage ring fits: 28 x 28 (2 rows) and 7 x 7 (one image)
+// stride-2 kernel's limit) where the 2-stage ring fits: 28 x 28 (2 rows), 14 x 14 (2 rows) and
+// 7 x 7 (one image)
 struct Inst2 {
   int hsl, hc, ns, nw;
 };
-constexpr Inst2 kInst2[] = {{480, 16, 7, 4}, {480, 32, 7, 4}, {320, 60, 4, 4}, {320, 60, 4, 8}, {256, 16, 4, 8}};
+constexpr Inst2 kInst2[] = {{480, 16, 7, 4}, {480, 32, 7, 4}, {320, 60, 4, 4}, {320, 60, 4, 8}, {256, 16, 4, 8},
+                            {192, 32, 2, 8}};
 
 // 8-wave workgroups (128 output channels per staged halo: two waves per SIMD, half the halo
 // staging per MFMA) wherever kout % 128 == 0 and no prologue: 92 -> 80 us at 7x7 / 14x14, 82.5 ->
@@ -605,7 +607,7 @@ void conv_hwgrad_pro(const ConvTapArgs& a, const void* dy, void* dw_out, int out
     return;                                                                                         \
   }
     HWG_CASE2(480, 16, 7, 4) HWG_CASE2(480, 32, 7, 4) HWG_CASE2(320, 60, 4, 4) HWG_CASE2(320, 60, 4, 8)
-    HWG_CASE2(256, 16, 4, 8)
+    HWG_CASE2(256, 16, 4, 8) HWG_CASE2(192, 32, 2, 8)
 #undef HWG_CASE2
 #define HWG_CASE(TK_, HSL_, HC_)                                                                    \
   if (pl.st == 1 && pl.nw == 4 && pl.tk == TK_ && pl.hsl == HSL_ && pl.HC == HC_) {                               \

@@ -110,13 +110,14 @@ def test_gpu_halo_wgrad_bn_relu_prologue_is_bitwise_the_apply_pass(n, h, w, cin,
 
 
 # stride 2 over even-sized inputs (n, input h, input w, cin, cout): ResNet-50's three downsampling
-# 3x3s (56 -> 28 on 2-row tiles, 8 and 4 waves; 28 -> 14 on 7-row tiles; 14 -> 7 as two whole
-# images per tile with an odd batch, 4 waves, or one image per tile, 8 waves), a 5-row tile, one
-# whole non-square image per tile, a tiny image
+# 3x3s (56 -> 28 on 2-row tiles, 8 and 4 waves; 28 -> 14 on 2-row tiles, 8 waves, or 7-row tiles,
+# 4 waves; 14 -> 7 as two whole images per tile with an odd batch, 4 waves, or one image per tile,
+# 8 waves), a 5-row tile, one whole non-square image per tile, a tiny image
 SHAPES_S2 = [
     (2, 56, 56, 128, 128),
     (2, 56, 56, 128, 64),
     (3, 28, 28, 256, 128),
+    (3, 28, 28, 256, 64),
     (3, 14, 14, 512, 64),
     (3, 14, 14, 256, 128),
     (2, 20, 20, 64, 64),

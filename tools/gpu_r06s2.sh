@@ -9,4 +9,4 @@ timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method threa
 tail -2 $O/test_hwg.txt
 timeout -k 10 200 python tools/wgrad_s2_bench.py > $O/wgrad_s2.jsonl 2>&1 || { tail -20 $O/wgrad_s2.jsonl; exit 1; }
 cat $O/wgrad_s2.jsonl
-tools/ab_bench.sh r06s2/ab2 "APEX_AB_NOP=1" "APEX_AMD_HALO_WGRAD_S2=0" 2
+tools/ab_bench.sh r06s2/ab3 "APEX_AB_NOP=1" "APEX_AMD_HALO_WGRAD_S2=0" 2
