@@ -23,7 +23,9 @@ Routing (static, identical on every rank and every run; ``APEX_AMD_DENSE_ROUTE``
   coverage differs by dtype (profiles/lt_probe_r03.jsonl, ROCm 7.2 on gfx950): fp16 has every
   epilogue; bf16 has BIAS and BGRADB but no GELU_AUX_BIAS, and its DGELU kernels give wrong
   results (disabled in lt_epilogue.cpp), so bf16 runs GEMM+bias then one GeLU pass forward, and
-  dgrad + GeLU-backward + wgrad + column sum backward.  BGRADB is opt-in (see ``_lt_bgradb``);  A shape the library has no kernel for at all falls back to the torch ops;
+  backward the native MFMA dgrad GEMM with dGeLU and the bias-gradient column sums in its
+  epilogue (``_DGELU_ROUTE``; 197 vs 201 us library dgrad + pass at the GPT-2 MLP shape,
+  profiles/r06/gelu_routes_r06ar.jsonl) + the library wgrad.  BGRADB is opt-in (see ``_lt_bgradb``);  A shape the library has no kernel for at all falls back to the torch ops;
 * ``native``: every GEMM on the gfx950 MFMA kernels (``csrc/gemm/gemm_mfma.hip``) with their
   own fused epilogues;
 * ``library``: plain torch ops (addmm + GeLU + sum) — the A/B baseline;
