@@ -124,6 +124,11 @@ def _host_scale(scaler):
     return None if scaler.sync_free else scaler.loss_scale()
 
 
+# accumulate fresh fp32 grads onto stashed ones with the device loss scale (sync-free); False =
+# read the scale on the host as the reference does (A/B, tests)
+_STASH_DEVICE_SCALE = True
+
+
 def post_backward_models_are_masters(scaler, params, stashed_grads, scale_override=None):
     host = _host_scale(scaler)
     grads_have_scale, stashed_have_scale, out_scale = host, 1.0, 1.0
@@ -143,7 +148,15 @@ def post_backward_models_are_masters(scaler, params, stashed_grads, scale_overri
             needing_with_stash.append(param.grad)
             stashed.append(stashed_grad)
     if needing_with_stash and grads_have_scale is None:
-        grads_have_scale = scaler.loss_scale()  # accumulation across losses needs the number
+        if _STASH_DEVICE_SCALE and scale_override is None and scaler.sync_free and needing_with_stash[0].is_cuda:
+            # sync-free accumulation onto the stash (e.g. zero_grad left zeroed fp32 grads): the
+            # fresh grads unscaled by the DEVICE scale (overflow-checked), then the stash added —
+            # the reference's axpby(1 / scale, 1) without reading the scale on the host
+            scaler.unscale(needing_with_stash, needing_with_stash, None, models_are_masters=True)
+            torch._foreach_add_(needing_with_stash, stashed)
+            needing_with_stash, stashed = [], []
+        else:
+            grads_have_scale = scaler.loss_scale()  # accumulation across losses needs the number
     if needing:
         scaler.unscale(needing, needing, None, models_are_masters=True,
                        scale_override=None if scale_override is None else grads_have_scale / out_scale)
